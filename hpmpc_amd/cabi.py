@@ -1,0 +1,212 @@
+"""ctypes bindings for the HPMPC hot-path C ABI.
+
+The same marshalling drives three libraries that export the reference's prototypes:
+
+* ``libhpmpc_mi355x.so`` (the product: C-ABI shim + HIP kernels, symbols exactly as named in
+  ``include/mpc_solvers.h`` / ``include/lqcp_solvers.h`` of the reference),
+* ``oracle/liboracle.so`` (the clean-room CPU restatement, ``orc_`` prefix; test infrastructure),
+* ``oracle/_ref/libhpmpc_ref.so`` (the real reference c99 build; dev container only).
+
+This is the ctypes stub a Python maintainer of the reference would write.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from .ocp import OCPQP, rup
+
+DP = C.POINTER(C.c_double)
+IP = C.POINTER(C.c_int)
+
+
+def load(path: str) -> C.CDLL:
+    if not os.path.exists(path):
+        raise FileNotFoundError(path)
+    return C.CDLL(path, mode=os.RTLD_LOCAL | getattr(os, "RTLD_NOW", 2))
+
+
+def _dptr(a: np.ndarray):
+    assert a.dtype == np.float64 and a.flags.c_contiguous, (a.dtype, a.flags)
+    return a.ctypes.data_as(DP)
+
+
+def dpp(arrs):
+    """list of float64 arrays -> double** (keeps no references: caller keeps arrs alive)."""
+    return (DP * max(len(arrs), 1))(*[_dptr(a) for a in arrs])
+
+
+def ipp(arrs):
+    return (IP * max(len(arrs), 1))(*[np.ascontiguousarray(a, dtype=np.int32).ctypes.data_as(IP) for a in arrs])
+
+
+def iv(a):
+    a = np.ascontiguousarray(a, dtype=np.int32)
+    return (C.c_int * len(a))(*a.tolist())
+
+
+class HpmpcAPI:
+    """Thin wrapper calling ``<prefix><reference symbol>`` of a loaded library on an OCPQP."""
+
+    def __init__(self, lib: C.CDLL, prefix: str = ""):
+        self.lib = lib
+        self.p = prefix
+
+    def fn(self, name: str):
+        f = getattr(self.lib, self.p + name)
+        return f
+
+    # ---------------------------------------------------------------------------------------------
+    def ric_sizes(self, qp: OCPQP):
+        N = qp.N
+        a = (C.c_int(N), iv(qp.nx), iv(qp.nu), iv(qp.nb), iv(qp.ng))
+        w = self.fn("d_back_ric_rec_sv_tv_work_space_size_bytes")(*a)
+        m = self.fn("d_back_ric_rec_sv_tv_memory_space_size_bytes")(*a)
+        return w, m
+
+    def ipm_ws_size(self, qp: OCPQP):
+        N = qp.N
+        return self.fn("d_ip2_res_mpc_hard_tv_work_space_size_bytes")(
+            C.c_int(N), iv(qp.nx), iv(qp.nu), iv(qp.nb), iv(qp.ng))
+
+    # ---------------------------------------------------------------------------------------------
+    def ric_sv(self, qp: OCPQP, *, update_b=0, b=None, update_q=0, q=None, bd=None, Qx=None, qx=None,
+               compute_pi=1, compute_Pb=0, memory=None, work=None):
+        """d_back_ric_rec_sv_tv_res (lqcp_solvers/d_back_ric_rec.c:112).  Returns ux, pi, Pb, memory."""
+        N = qp.N
+        wsz, msz = self.ric_sizes(qp)
+        memory = np.zeros(msz // 8 + 8) if memory is None else memory
+        work = np.zeros(wsz // 8 + 8) if work is None else work
+        ux = [np.zeros(rup(qp.nux(k) + 1, 4) + 4) for k in range(N + 1)]
+        pi = [np.zeros(rup(int(qp.nx[k + 1]), 4) + 4) for k in range(N)]
+        Pb = [np.zeros(rup(int(qp.nx[k + 1]), 4) + 4) for k in range(N)]
+        z = [np.zeros(8)]
+        b = b if b is not None else [np.zeros(rup(int(qp.nx[k + 1]), 4) + 4) for k in range(N)]
+        q = q if q is not None else [np.zeros(rup(qp.nux(k) + 1, 4) + 4) for k in range(N + 1)]
+        bd = bd if bd is not None else z * (N + 1)
+        Qx = Qx if Qx is not None else z * (N + 1)
+        qx = qx if qx is not None else z * (N + 1)
+        dct = qp.DCt if qp.DCt else z * (N + 1)
+        self.fn("d_back_ric_rec_sv_tv_res")(
+            C.c_int(N), iv(qp.nx), iv(qp.nu), iv(qp.nb), ipp(qp.idxb), iv(qp.ng), C.c_int(update_b),
+            dpp(qp.BAbt), dpp(b), C.c_int(update_q), dpp(qp.RSQrq), dpp(q), dpp(bd), dpp(dct), dpp(Qx), dpp(qx),
+            dpp(ux), C.c_int(compute_pi), dpp(pi), C.c_int(compute_Pb), dpp(Pb), _dptr(memory), _dptr(work))
+        return ux, pi, Pb, memory
+
+    def ric_trf(self, qp: OCPQP, *, bd=None, Qx=None, memory=None):
+        N = qp.N
+        wsz, msz = self.ric_sizes(qp)
+        memory = np.zeros(msz // 8 + 8) if memory is None else memory
+        work = np.zeros(wsz // 8 + 8)
+        z = [np.zeros(8)]
+        bd = bd if bd is not None else z * (N + 1)
+        Qx = Qx if Qx is not None else z * (N + 1)
+        dct = qp.DCt if qp.DCt else z * (N + 1)
+        self.fn("d_back_ric_rec_trf_tv_res")(
+            C.c_int(N), iv(qp.nx), iv(qp.nu), iv(qp.nb), ipp(qp.idxb), iv(qp.ng), dpp(qp.BAbt), dpp(qp.RSQrq),
+            dpp(dct), dpp(Qx), dpp(bd), _dptr(memory), _dptr(work))
+        return memory
+
+    def ric_trs(self, qp: OCPQP, memory, *, b, q, qx=None, compute_pi=1, compute_Pb=1, Pb=None):
+        N = qp.N
+        wsz, _ = self.ric_sizes(qp)
+        work = np.zeros(wsz // 8 + 8)
+        ux = [np.zeros(rup(qp.nux(k) + 1, 4) + 4) for k in range(N + 1)]
+        pi = [np.zeros(rup(int(qp.nx[k + 1]), 4) + 4) for k in range(N)]
+        Pb = Pb if Pb is not None else [np.zeros(rup(int(qp.nx[k + 1]), 4) + 4) for k in range(N)]
+        z = [np.zeros(8)]
+        qx = qx if qx is not None else z * (N + 1)
+        dct = qp.DCt if qp.DCt else z * (N + 1)
+        self.fn("d_back_ric_rec_trs_tv_res")(
+            C.c_int(N), iv(qp.nx), iv(qp.nu), iv(qp.nb), ipp(qp.idxb), iv(qp.ng), dpp(qp.BAbt), dpp(b), dpp(q),
+            dpp(dct), dpp(qx), dpp(ux), C.c_int(compute_pi), dpp(pi), C.c_int(compute_Pb), dpp(Pb),
+            _dptr(memory), _dptr(work))
+        return ux, pi, Pb
+
+    # ---------------------------------------------------------------------------------------------
+    def ipm(self, qp: OCPQP, *, k_max=50, mu0=2.0, mu_tol=1e-12, alpha_min=1e-8, warm_start=0, compute_mult=1,
+            ux=None, work=None):
+        """d_ip2_res_mpc_hard_tv (mpc_solvers/d_ip2_res_hard.c:116).  Returns dict."""
+        N = qp.N
+        nu_N = qp.nu.copy()
+        wsz = self.ipm_ws_size(qp)
+        work = np.zeros(wsz // 8 + 16) if work is None else work
+        ux_, pi, lam, t = qp.alloc_solution()
+        if ux is not None:
+            for k in range(N + 1):
+                ux_[k][: len(ux[k])] = ux[k]
+        stat = np.zeros(5 * k_max + 5)
+        kk = C.c_int(0)
+        dct = qp.DCt if qp.DCt else [np.zeros(8)] * (N + 1)
+        ret = self.fn("d_ip2_res_mpc_hard_tv")(
+            C.byref(kk), C.c_int(k_max), C.c_double(mu0), C.c_double(mu_tol), C.c_double(alpha_min),
+            C.c_int(warm_start), _dptr(stat), C.c_int(N), iv(qp.nx), iv(nu_N), iv(qp.nb), ipp(qp.idxb), iv(qp.ng),
+            dpp(qp.BAbt), dpp(qp.RSQrq), dpp(dct), dpp(qp.d), dpp(ux_), C.c_int(compute_mult), dpp(pi), dpp(lam),
+            dpp(t), _dptr(work))
+        return dict(ret=ret, kk=kk.value, stat=stat[: 5 * kk.value].copy(), ux=ux_, pi=pi, lam=lam, t=t,
+                    work=work)
+
+    def single_newton(self, qp: OCPQP, ux0, pi0, lam0, t0, *, k_max=1, mu0=0.0, mu_tol=1e-12, alpha_min=1e-8,
+                      compute_mult=1, work=None):
+        N = qp.N
+        wsz = self.ipm_ws_size(qp)
+        work = np.zeros(wsz // 8 + 16) if work is None else work
+        ux, pi, lam, t = qp.alloc_solution()
+        stat = np.zeros(5 * k_max + 5)
+        kk = C.c_int(0)
+        dct = qp.DCt if qp.DCt else [np.zeros(8)] * (N + 1)
+        ret = self.fn("d_ip2_res_mpc_hard_tv_single_newton_step")(
+            C.byref(kk), C.c_int(k_max), C.c_double(mu0), C.c_double(mu_tol), C.c_double(alpha_min), C.c_int(0),
+            _dptr(stat), C.c_int(N), iv(qp.nx), iv(qp.nu), iv(qp.nb), ipp(qp.idxb), iv(qp.ng), dpp(qp.BAbt),
+            dpp(qp.RSQrq), dpp(dct), dpp(qp.d), dpp(ux), C.c_int(compute_mult), dpp(pi), dpp(lam), dpp(t),
+            _dptr(work), dpp(ux0), dpp(pi0), dpp(lam0), dpp(t0))
+        return dict(ret=ret, kk=kk.value, stat=stat[: 5 * kk.value].copy(), ux=ux, pi=pi, lam=lam, t=t, work=work)
+
+    def kkt_new_rhs(self, qp: OCPQP, work, b, q, compute_mult=1):
+        """d_kkt_solve_new_rhs_res_mpc_hard_tv (d_ip2_res_hard.c:1922), re-using ``work`` from ipm()."""
+        N = qp.N
+        ux, pi, lam, t = qp.alloc_solution()
+        dct = qp.DCt if qp.DCt else [np.zeros(8)] * (N + 1)
+        self.fn("d_kkt_solve_new_rhs_res_mpc_hard_tv")(
+            C.c_int(N), iv(qp.nx), iv(qp.nu), iv(qp.nb), ipp(qp.idxb), iv(qp.ng), dpp(qp.BAbt), dpp(b),
+            dpp(qp.RSQrq), dpp(q), dpp(dct), dpp(qp.d), dpp(ux), C.c_int(compute_mult), dpp(pi), dpp(lam), dpp(t),
+            _dptr(work))
+        return dict(ux=ux, pi=pi, lam=lam, t=t)
+
+    def residuals(self, qp: OCPQP, b, q, ux, pi, lam, t):
+        """d_res_res_mpc_hard_tv (mpc_solvers/c99/d_res_ip_res_hard.c:39)."""
+        N = qp.N
+        rq = [np.zeros(rup(qp.nux(k) + 1, 4) + 4) for k in range(N + 1)]
+        rb = [np.zeros(rup(int(qp.nx[k + 1]), 4) + 4) for k in range(N)]
+        rd = [np.zeros(max(qp.nconstr(k), 1) + 4) for k in range(N + 1)]
+        rm = [np.zeros(max(qp.nconstr(k), 1) + 4) for k in range(N + 1)]
+        work = np.zeros(2 * max([qp.png(k) for k in range(N + 1)] + [1]) + 8)
+        mu = C.c_double(0.0)
+        dct = qp.DCt if qp.DCt else [np.zeros(8)] * (N + 1)
+        self.fn("d_res_res_mpc_hard_tv")(
+            C.c_int(N), iv(qp.nx), iv(qp.nu), iv(qp.nb), ipp(qp.idxb), iv(qp.ng), dpp(qp.BAbt), dpp(b),
+            dpp(qp.RSQrq), dpp(q), dpp(ux), dpp(dct), dpp(qp.d), dpp(pi), dpp(lam), dpp(t), _dptr(work), dpp(rq),
+            dpp(rb), dpp(rd), dpp(rm), C.byref(mu))
+        return dict(rq=rq, rb=rb, rd=rd, rm=rm, mu=mu.value)
+
+
+def bq_from_qp(qp: OCPQP):
+    """b[k] and q[k] vectors extracted from the augmented rows (as the IPM does, d_ip2_res_hard.c:202-220)."""
+    from .ocp import unpack_lib4
+
+    b, q = [], []
+    for k in range(qp.N):
+        nux = qp.nux(k)
+        M = unpack_lib4(qp.BAbt[k], nux + 1, int(qp.nx[k + 1]))
+        bb = np.zeros(rup(int(qp.nx[k + 1]), 4) + 4)
+        bb[: qp.nx[k + 1]] = M[nux]
+        b.append(bb)
+    for k in range(qp.N + 1):
+        nux = qp.nux(k)
+        M = unpack_lib4(qp.RSQrq[k], nux + 1, nux)
+        qq = np.zeros(rup(nux + 1, 4) + 4)
+        qq[:nux] = M[nux]
+        q.append(qq)
+    return b, q

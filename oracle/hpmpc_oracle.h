@@ -1,0 +1,62 @@
+/*
+ * hpmpc_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * Clean-room CPU restatement of the HPMPC hot path (backward Riccati recursion + residual-based
+ * Mehrotra IPM on lib4 panel-major data).  It is the parity checker for the MI355X build: only
+ * tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it.  The product
+ * (libhpmpc_mi355x.so) never links, calls or falls back to it.
+ *
+ * Every entry point has the SAME argument list and meaning as the reference routine it restates
+ * (file:line relative to the reference checkout), prefixed with orc_ so that it can live in one
+ * process next to the product's reference-named symbols.  Workspace/memory layouts are private to
+ * the oracle and sized by the oracle's own *_size_bytes functions.
+ */
+#ifndef HPMPC_ORACLE_H_
+#define HPMPC_ORACLE_H_
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* lqcp_solvers/d_back_ric_rec.c:43 */
+int orc_d_back_ric_rec_sv_tv_work_space_size_bytes(int N, int *nx, int *nu, int *nb, int *ng);
+/* lqcp_solvers/d_back_ric_rec.c:79 */
+int orc_d_back_ric_rec_sv_tv_memory_space_size_bytes(int N, int *nx, int *nu, int *nb, int *ng);
+/* lqcp_solvers/d_back_ric_rec.c:112 */
+void orc_d_back_ric_rec_sv_tv_res(int N, int *nx, int *nu, int *nb, int **idxb, int *ng, int update_b,
+    double **hpBAbt, double **b, int update_q, double **hpRSQrq, double **q, double **bd, double **hpDCt,
+    double **Qx, double **qx, double **hux, int compute_pi, double **hpi, int compute_Pb, double **hPb,
+    double *memory, double *work);
+/* lqcp_solvers/d_back_ric_rec.c:403 */
+void orc_d_back_ric_rec_trf_tv_res(int N, int *nx, int *nu, int *nb, int **idxb, int *ng, double **hpBAbt,
+    double **hpRSQrq, double **hpDCt, double **Qx, double **bd, double *memory, double *work);
+/* lqcp_solvers/d_back_ric_rec.c:564 */
+void orc_d_back_ric_rec_trs_tv_res(int N, int *nx, int *nu, int *nb, int **idxb, int *ng, double **hpBAbt,
+    double **hb, double **hq, double **hpDCt, double **qx, double **hux, int compute_pi, double **hpi,
+    int compute_Pb, double **hPb, double *memory, double *work);
+
+/* mpc_solvers/d_ip2_res_hard.c:57 */
+int orc_d_ip2_res_mpc_hard_tv_work_space_size_bytes(int N, int *nx, int *nu, int *nb, int *ng);
+/* mpc_solvers/d_ip2_res_hard.c:116 */
+int orc_d_ip2_res_mpc_hard_tv(int *kk, int k_max, double mu0, double mu_tol, double alpha_min, int warm_start,
+    double *stat, int N, int *nx, int *nu_N, int *nb, int **idxb, int *ng, double **pBAbt, double **pQ,
+    double **pDCt, double **d, double **ux, int compute_mult, double **pi, double **lam, double **t,
+    double *double_work_memory);
+/* mpc_solvers/d_ip2_res_hard.c:1348 */
+int orc_d_ip2_res_mpc_hard_tv_single_newton_step(int *kk, int k_max, double mu0, double mu_tol, double alpha_min,
+    int warm_start, double *stat, int N, int *nx, int *nu_N, int *nb, int **idxb, int *ng, double **pBAbt,
+    double **pQ, double **pDCt, double **d, double **ux, int compute_mult, double **pi, double **lam, double **t,
+    double *double_work_memory, double **ux0, double **pi0, double **lam0, double **t0);
+/* mpc_solvers/d_ip2_res_hard.c:1922 */
+void orc_d_kkt_solve_new_rhs_res_mpc_hard_tv(int N, int *nx, int *nu_N, int *nb, int **idxb, int *ng,
+    double **pBAbt, double **b, double **pQ, double **q, double **pDCt, double **d, double **ux, int compute_mult,
+    double **pi, double **lam, double **t, double *double_work_memory);
+/* mpc_solvers/c99/d_res_ip_res_hard.c:39 */
+void orc_d_res_res_mpc_hard_tv(int N, int *nx, int *nu, int *nb, int **idxb, int *ng, double **hpBAbt, double **hb,
+    double **hpQ, double **hq, double **hux, double **hpDCt, double **hd, double **hpi, double **hlam, double **ht,
+    double *work, double **hrq, double **hrb, double **hrd, double **hrm, double *mu);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
