@@ -1,0 +1,122 @@
+// hk_prims.h -- wave64 cross-lane primitives for the MI355X (gfx950) Riccati/IPM kernels.
+//
+// One problem is owned by one wavefront.  A stage's (nu+nx) x (nu+nx) block lives in the f64 MFMA
+// C/D register layout of v_mfma_f64_16x16x4_f64 ("tile layout"):
+//     lane l = 16*g + c  (g = l>>4 in 0..3 "row group", c = l&15 "column"),
+//     register r in 0..3 holds element (row g+4r, col c).
+// Vectors use one of two replicated layouts:
+//     col layout : one double per lane, value v[c]           (identical in the 4 row groups)
+//     row layout : double[4] per lane,  value v[g+4r] in r   (identical in the 16 columns)
+// Every primitive below keeps replicated values bitwise identical across their replicas.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace hk {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+__device__ __forceinline__ double mk(int hi, int lo) { return __hiloint2double(hi, lo); }
+
+// DPP move of a double (two v_mov_b32_dpp); CTRL is the DPP control word.
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov(double x) {
+    int lo = __double2loint(x), hi = __double2hiint(x);
+    lo = __builtin_amdgcn_update_dpp(0, lo, CTRL, 0xf, 0xf, false);
+    hi = __builtin_amdgcn_update_dpp(0, hi, CTRL, 0xf, 0xf, false);
+    return mk(hi, lo);
+}
+
+// broadcast lane P of every 16-lane row to the whole row (DPP row_newbcast, gfx90a+)
+template <int P>
+__device__ __forceinline__ double row_bcast(double x) { return dpp_mov<0x150 + P>(x); }
+
+// value of lane `src` (wave-uniform) as a scalar
+__device__ __forceinline__ double readlane(double x, int src) {
+    int lo = __builtin_amdgcn_readlane(__double2loint(x), src);
+    int hi = __builtin_amdgcn_readlane(__double2hiint(x), src);
+    return mk(hi, lo);
+}
+
+// Broadcast row group GS (lanes 16*GS..16*GS+15) to all four row groups, lane-column preserving:
+// result at lane (g,c) = x at lane (GS,c).  v_permlane32_swap + v_permlane16_swap (gfx950).
+template <int GS>
+__device__ __forceinline__ double rowgroup_bcast(double x) {
+    int lo = __double2loint(x), hi = __double2hiint(x);
+    // step 1: replicate the 32-lane half that holds GS
+    auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    int lo1 = (GS < 2) ? (int)a[0] : (int)a[1];
+    int hi1 = (GS < 2) ? (int)b[0] : (int)b[1];
+    // step 2: replicate the 16-lane row (even/odd) inside the half
+    auto c = __builtin_amdgcn_permlane16_swap(lo1, lo1, false, false);
+    auto d = __builtin_amdgcn_permlane16_swap(hi1, hi1, false, false);
+    int lo2 = (GS % 2 == 0) ? (int)c[0] : (int)c[1];
+    int hi2 = (GS % 2 == 0) ? (int)d[0] : (int)d[1];
+    return mk(hi2, lo2);
+}
+
+// Sum over the four row groups: result at (g,c) = sum_g' x(g',c); identical in all row groups.
+__device__ __forceinline__ double xrow_sum(double x) {
+    int lo = __double2loint(x), hi = __double2hiint(x);
+    auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    double s1 = mk((int)b[0], (int)a[0]) + mk((int)b[1], (int)a[1]);  // rows {0,1}+{2,3}
+    lo = __double2loint(s1);
+    hi = __double2hiint(s1);
+    auto c = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    auto d = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    return mk((int)d[0], (int)c[0]) + mk((int)d[1], (int)c[1]);
+}
+
+// Sum over the 16 lanes of each row (rotate-and-add butterfly); identical in all 16 lanes.
+__device__ __forceinline__ double row_sum16(double x) {
+    x += dpp_mov<0x128>(x);  // row_ror:8
+    x += dpp_mov<0x124>(x);  // row_ror:4
+    x += dpp_mov<0x122>(x);  // row_ror:2
+    x += dpp_mov<0x121>(x);  // row_ror:1
+    return x;
+}
+
+// wave-wide reductions (all lanes get the result)
+__device__ __forceinline__ double wave_sum(double x) {
+    x = row_sum16(x);
+    return xrow_sum(x);
+}
+__device__ __forceinline__ double wave_min(double x) {
+    x = fmin(x, dpp_mov<0x128>(x));
+    x = fmin(x, dpp_mov<0x124>(x));
+    x = fmin(x, dpp_mov<0x122>(x));
+    x = fmin(x, dpp_mov<0x121>(x));
+    int lo = __double2loint(x), hi = __double2hiint(x);
+    auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    x = fmin(mk((int)b[0], (int)a[0]), mk((int)b[1], (int)a[1]));
+    lo = __double2loint(x);
+    hi = __double2hiint(x);
+    auto c = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    auto d = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    return fmin(mk((int)d[0], (int)c[0]), mk((int)d[1], (int)c[1]));
+}
+
+// Cholesky pivot with the reference's clamp (kernel_dpotrf_c99_lib4.c:555-640): d > 1e-15 gives
+// s = sqrt(d), inv = 1/s; otherwise both 0.  v_rsq_f64 refined by two Newton steps (~1 ulp).
+__device__ __forceinline__ void chol_pivot(double d, double &s, double &inv) {
+    const bool ok = d > 1e-15;
+    const double dd = ok ? d : 1.0;
+    double y = __builtin_amdgcn_rsq(dd);
+    const double h = 0.5 * dd;
+    double e = fma(-h * y, y, 0.5);
+    y = fma(y, e, y);
+    e = fma(-h * y, y, 0.5);
+    y = fma(y, e, y);
+    s = ok ? dd * y : 0.0;
+    inv = ok ? y : 0.0;
+}
+
+__device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+}  // namespace hk

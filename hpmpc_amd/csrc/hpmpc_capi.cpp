@@ -1,0 +1,728 @@
+// hpmpc_capi.cpp -- host side of libhpmpc_mi355x.so: the reference-named C ABI (drop-in for
+// HPMPC's lqcp_solvers.h / mpc_solvers.h hot path) and the batched device API.  Every call runs on
+// the GPU through the kernels in hpmpc_kernels.hip; there is no CPU fallback.
+//
+// Host marshalling of the single-problem entry points:
+//   * the caller's per-stage lib4 blocks (pointers may alias across stages) are copied stage by stage
+//     into a pinned staging arena, uploaded with one hipMemcpyAsync and solved by a 1-problem launch;
+//   * the reference's documented in-place side effects on hpRSQrq / hpBAbt (update_q / update_b
+//     rows, box diagonal and gradient, d_back_ric_rec.c:197-209, :249-291) are applied to the caller's
+//     buffers in the reference's stage order, and each stage's device copy receives exactly the
+//     values the reference factorises for that stage;
+//   * "memory" / "double_work_memory" hold this library's private device image (factor + persistent
+//     IPM iterate) so that trs and d_kkt_solve_new_rhs_res_mpc_hard_tv can re-use it.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "../../include/hpmpc_mi355x.h"
+#include "hpmpc_kargs.h"
+
+extern "C" int hk_launch(int which, const KArgs* a, int count, hipStream_t stream);
+
+namespace {
+
+enum { K_SV = 0, K_TRF = 1, K_TRS = 2, K_RES = 3, K_IPM = 4, K_KKT = 5 };
+constexpr int FSTRIDE = 288, V16 = 16, V32 = 32, BS = 4, NCL = 2;
+
+struct StageInfoH {  // mirror of hk::StageInfo
+    int nu, nx, nb, ng, xo, nx1, nu1, xo1, sdB, sdR, oB, oR, oD, pnb, r0, r1;
+};
+
+inline int rup(int n, int m) { return (n + m - 1) / m * m; }
+inline double& P4(double* A, int sd, int i, int j) { return A[(i / BS) * BS * sd + i % BS + BS * j]; }
+
+thread_local int g_err = 0;
+
+void set_err(int code, const char* what) {
+    g_err = code;
+    if (code) fprintf(stderr, "[hpmpc_mi355x] %s (code %d)\n", what, code);
+}
+
+bool hip_ok(hipError_t e, const char* what) {
+    if (e == hipSuccess) return true;
+    char msg[256];
+    snprintf(msg, sizeof msg, "HIP error in %s: %s", what, hipGetErrorString(e));
+    set_err(HPMPC_MI355X_EHIP, msg);
+    return false;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------
+// Plan: stage tables shared by every problem of a batch.
+// ------------------------------------------------------------------------------------------------
+struct hpmpc_mi355x_plan {
+    int N = 0;
+    std::vector<int> nx, nu, nb, ng;
+    std::vector<std::vector<int>> idxb;
+    std::vector<StageInfoH> st;
+    std::vector<signed char> tileslot, slotvar;
+    std::vector<long long> offB, offR;  // packed default layout
+    long long packB = 0, packR = 0;
+    void* d_st = nullptr;
+    signed char *d_tileslot = nullptr, *d_slotvar = nullptr;
+    std::vector<long long> dev_offB, dev_offR;  // offsets currently uploaded into d_st
+};
+
+namespace {
+
+bool plan_supported(int N, const int* nx, const int* nu, const int* nb, const int* ng, const char** why) {
+    for (int k = 0; k <= N; k++) {
+        const int u = k < N ? nu[k] : 0;
+        if (ng[k] != 0) {
+            *why = "general constraints (ng > 0) are not supported on the GPU path";
+            return false;
+        }
+        if (u < 0 || nx[k] < 0 || u + nx[k] > 16 || rup(u, 4) + nx[k] > 16) {
+            *why = "stage size beyond the 16-wide tile (nu+nx <= 16, round_up(nu,4)+nx <= 16)";
+            return false;
+        }
+        if (nb[k] < 0 || nb[k] > u + nx[k]) {
+            *why = "nb[k] > nu[k]+nx[k]";
+            return false;
+        }
+    }
+    if (N < 1) {
+        *why = "N must be >= 1";
+        return false;
+    }
+    return true;
+}
+
+bool plan_upload_stages(hpmpc_mi355x_plan* P, const long long* offB, const long long* offR) {
+    const int N = P->N;
+    bool same = !P->dev_offB.empty();
+    for (int k = 0; same && k < N; k++) same = P->dev_offB[k] == offB[k];
+    for (int k = 0; same && k <= N; k++) same = P->dev_offR[k] == offR[k];
+    if (same) return true;
+    for (int k = 0; k <= N; k++) {
+        P->st[k].oB = k < N ? (int)offB[k] : 0;
+        P->st[k].oR = (int)offR[k];
+    }
+    P->dev_offB.assign(offB, offB + N);
+    P->dev_offR.assign(offR, offR + N + 1);
+    return hip_ok(hipMemcpy(P->d_st, P->st.data(), sizeof(StageInfoH) * (N + 1), hipMemcpyHostToDevice),
+                  "plan stage upload");
+}
+
+long long ws_doubles(int N) { return (long long)(N + 1) * (FSTRIDE + 9 * V16 + 8 * V32); }
+
+}  // namespace
+
+extern "C" hpmpc_mi355x_plan* hpmpc_mi355x_plan_create(int N, const int* nx, const int* nu, const int* nb,
+                                                       const int* const* idxb, const int* ng) {
+    const char* why = nullptr;
+    if (!plan_supported(N, nx, nu, nb, ng, &why)) {
+        set_err(HPMPC_MI355X_EUNSUPPORTED, why);
+        return nullptr;
+    }
+    auto* P = new hpmpc_mi355x_plan();
+    P->N = N;
+    P->nx.assign(nx, nx + N + 1);
+    P->nu.assign(nu, nu + N + 1);
+    P->nu[N] = 0;
+    P->nb.assign(nb, nb + N + 1);
+    P->ng.assign(ng, ng + N + 1);
+    P->idxb.resize(N + 1);
+    P->st.resize(N + 1);
+    P->tileslot.assign((N + 1) * 16, -1);
+    P->slotvar.assign((N + 1) * 16, 0);
+    P->offB.resize(N);
+    P->offR.resize(N + 1);
+    for (int k = 0; k <= N; k++) {
+        StageInfoH& s = P->st[k];
+        s.nu = P->nu[k];
+        s.nx = nx[k];
+        s.nb = nb[k];
+        s.ng = 0;
+        s.xo = rup(s.nu, 4);
+        s.nx1 = k < N ? nx[k + 1] : 0;
+        s.nu1 = k + 1 < N ? P->nu[k + 1] : 0;
+        s.xo1 = rup(s.nu1, 4);
+        s.sdB = rup(s.nx1, NCL);
+        s.sdR = rup(s.nu + s.nx, NCL);
+        s.pnb = rup(nb[k], BS);
+        s.oD = k * V32;
+        s.r0 = s.r1 = 0;
+        const int nux = s.nu + s.nx;
+        if (k < N) {
+            P->offB[k] = P->packB;
+            P->packB += (long long)rup(nux + 1, BS) * s.sdB;
+        }
+        P->offR[k] = P->packR;
+        P->packR += (long long)rup(nux + 1, BS) * s.sdR;
+        P->idxb[k].assign(idxb[k], idxb[k] + nb[k]);
+        for (int l = 0; l < nb[k]; l++) {
+            const int v = idxb[k][l];
+            const int t = v < s.nu ? v : s.xo + (v - s.nu);
+            P->tileslot[k * 16 + t] = (signed char)l;
+            P->slotvar[k * 16 + l] = (signed char)v;
+        }
+    }
+    bool ok = hip_ok(hipMalloc(&P->d_st, sizeof(StageInfoH) * (N + 1)), "plan alloc") &&
+              hip_ok(hipMalloc((void**)&P->d_tileslot, (N + 1) * 16), "plan alloc") &&
+              hip_ok(hipMalloc((void**)&P->d_slotvar, (N + 1) * 16), "plan alloc") &&
+              hip_ok(hipMemcpy(P->d_tileslot, P->tileslot.data(), (N + 1) * 16, hipMemcpyHostToDevice), "plan") &&
+              hip_ok(hipMemcpy(P->d_slotvar, P->slotvar.data(), (N + 1) * 16, hipMemcpyHostToDevice), "plan") &&
+              plan_upload_stages(P, P->offB.data(), P->offR.data());
+    if (!ok) {
+        hpmpc_mi355x_plan_destroy(P);
+        return nullptr;
+    }
+    g_err = 0;
+    return P;
+}
+
+extern "C" void hpmpc_mi355x_plan_destroy(hpmpc_mi355x_plan* P) {
+    if (!P) return;
+    if (P->d_st) (void)hipFree(P->d_st);
+    if (P->d_tileslot) (void)hipFree(P->d_tileslot);
+    if (P->d_slotvar) (void)hipFree(P->d_slotvar);
+    delete P;
+}
+
+extern "C" long long hpmpc_mi355x_ws_doubles(const hpmpc_mi355x_plan* P) { return P ? ws_doubles(P->N) : 0; }
+
+extern "C" int hpmpc_mi355x_last_error(void) { return g_err; }
+
+extern "C" const char* hpmpc_mi355x_version(void) {
+    return "hpmpc_mi355x 0.1 gfx950 (wave-per-problem, f64 MFMA 16x16x4 stage contractions)";
+}
+
+namespace {
+
+KArgs base_args(const hpmpc_mi355x_plan* P, int nprob, int p0) {
+    KArgs a;
+    memset(&a, 0, sizeof a);
+    a.N = P->N;
+    a.nprob = nprob;
+    a.p0 = p0;
+    a.st = P->d_st;
+    a.tileslot = P->d_tileslot;
+    a.slotvar = P->d_slotvar;
+    a.sV16 = (long long)(P->N + 1) * V16;
+    a.sV32 = (long long)(P->N + 1) * V32;
+    a.sW = ws_doubles(P->N);
+    return a;
+}
+
+bool layout_apply(hpmpc_mi355x_plan* P, const hpmpc_mi355x_layout* lay, KArgs& a) {
+    if (lay && lay->BAbt_off && lay->RSQrq_off) {
+        if (!plan_upload_stages(P, lay->BAbt_off, lay->RSQrq_off)) return false;
+    } else if (!plan_upload_stages(P, P->offB.data(), P->offR.data())) {
+        return false;
+    }
+    a.sB = lay ? lay->BAbt_stride : P->packB;
+    a.sR = lay ? lay->RSQrq_stride : P->packR;
+    return true;
+}
+
+}  // namespace
+
+extern "C" int hpmpc_mi355x_ipm_batch(const hpmpc_mi355x_plan* plan, const hpmpc_mi355x_layout* lay, int nprob,
+                                      int p0, int count, const double* BAbt, const double* RSQrq, const double* d,
+                                      double* ux, double* pi, double* lam, double* t, double* ws, int k_max,
+                                      double mu0, double mu_tol, double alpha_min, int warm_start, int compute_mult,
+                                      int* kk, int* ret, double* stat, void* stream) {
+    auto* P = const_cast<hpmpc_mi355x_plan*>(plan);
+    if (!P) return g_err = HPMPC_MI355X_EUNSUPPORTED;
+    KArgs a = base_args(P, nprob, p0);
+    if (!layout_apply(P, lay, a)) return g_err;
+    a.BAbt = BAbt;
+    a.RSQ = RSQrq;
+    a.d = d;
+    a.ux = ux;
+    a.pi = pi;
+    a.lam = lam;
+    a.t = t;
+    a.ws = ws;
+    a.k_max = k_max;
+    a.mu0 = mu0;
+    a.mu_tol = mu_tol;
+    a.alpha_min = alpha_min;
+    a.warm_start = warm_start;
+    a.compute_mult = compute_mult;
+    a.kk = kk;
+    a.ret = ret;
+    a.stat = stat;
+    int e = hk_launch(K_IPM, &a, count, (hipStream_t)stream);
+    if (e) {
+        set_err(HPMPC_MI355X_EHIP, "hk_ipm launch failed");
+        return HPMPC_MI355X_EHIP;
+    }
+    return g_err = 0;
+}
+
+extern "C" int hpmpc_mi355x_ric_sv_batch(const hpmpc_mi355x_plan* plan, const hpmpc_mi355x_layout* lay, int nprob,
+                                         int p0, int count, const double* BAbt, const double* RSQrq, double* ux,
+                                         double* pi, double* ws, int compute_pi, int compute_Pb, double* Pb,
+                                         void* stream) {
+    auto* P = const_cast<hpmpc_mi355x_plan*>(plan);
+    if (!P) return g_err = HPMPC_MI355X_EUNSUPPORTED;
+    KArgs a = base_args(P, nprob, p0);
+    if (!layout_apply(P, lay, a)) return g_err;
+    a.BAbt = BAbt;
+    a.RSQ = RSQrq;
+    a.ux = ux;
+    a.pi = pi;
+    a.ws = ws;
+    a.compute_pi = compute_pi;
+    a.compute_Pb = compute_Pb && Pb;
+    a.vPb = Pb;
+    int e = hk_launch(K_SV, &a, count, (hipStream_t)stream);
+    if (e) {
+        set_err(HPMPC_MI355X_EHIP, "hk_ric_sv launch failed");
+        return HPMPC_MI355X_EHIP;
+    }
+    return g_err = 0;
+}
+
+extern "C" int hpmpc_mi355x_ric_trs_batch(const hpmpc_mi355x_plan* plan, const hpmpc_mi355x_layout* lay, int nprob,
+                                          int p0, int count, const double* BAbt, const double* RSQrq, const double* b,
+                                          const double* q, double* ux, double* pi, double* ws, int compute_pi,
+                                          int compute_Pb, double* Pb, void* stream) {
+    auto* P = const_cast<hpmpc_mi355x_plan*>(plan);
+    if (!P) return g_err = HPMPC_MI355X_EUNSUPPORTED;
+    KArgs a = base_args(P, nprob, p0);
+    if (!layout_apply(P, lay, a)) return g_err;
+    a.BAbt = BAbt;
+    a.RSQ = RSQrq;
+    a.vb = b;
+    a.vq = q;
+    a.ux = ux;
+    a.pi = pi;
+    a.ws = ws;
+    a.compute_pi = compute_pi;
+    a.compute_Pb = compute_Pb;
+    a.vPb = Pb;
+    int e = hk_launch(K_TRS, &a, count, (hipStream_t)stream);
+    if (e) {
+        set_err(HPMPC_MI355X_EHIP, "hk_ric_trs launch failed");
+        return HPMPC_MI355X_EHIP;
+    }
+    return g_err = 0;
+}
+
+// ================================================================================================
+// Single-problem reference entry points
+// ================================================================================================
+namespace {
+
+// Thread-local device context: one stream, growable device arena, pinned staging arena, plan cache.
+struct Ctx {
+    hipStream_t stream = nullptr;
+    double* dev = nullptr;
+    size_t dev_cap = 0;
+    double* host = nullptr;
+    size_t host_cap = 0;
+    hpmpc_mi355x_plan* plan = nullptr;
+    std::vector<int> key;
+    ~Ctx() {
+        if (plan) hpmpc_mi355x_plan_destroy(plan);
+        if (dev) (void)hipFree(dev);
+        if (host) (void)hipHostFree(host);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+    bool ensure(size_t n) {
+        if (!stream && !hip_ok(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "stream create"))
+            return false;
+        if (n > dev_cap) {
+            if (dev) (void)hipFree(dev);
+            dev = nullptr;
+            dev_cap = 0;
+            if (!hip_ok(hipMalloc((void**)&dev, n * sizeof(double)), "device arena")) return false;
+            dev_cap = n;
+        }
+        if (n > host_cap) {
+            if (host) (void)hipHostFree(host);
+            host = nullptr;
+            host_cap = 0;
+            if (!hip_ok(hipHostMalloc((void**)&host, n * sizeof(double), 0), "pinned arena")) return false;
+            host_cap = n;
+        }
+        memset(host, 0, n * sizeof(double));
+        return true;
+    }
+    hpmpc_mi355x_plan* get_plan(int N, const int* nx, const int* nu, const int* nb, int** idxb, const int* ng) {
+        std::vector<int> k;
+        k.push_back(N);
+        for (int i = 0; i <= N; i++) {
+            k.push_back(nx[i]);
+            k.push_back(i < N ? nu[i] : 0);
+            k.push_back(nb[i]);
+            k.push_back(ng[i]);
+            for (int l = 0; l < nb[i]; l++) k.push_back(idxb[i][l]);
+        }
+        if (plan && k == key) return plan;
+        if (plan) hpmpc_mi355x_plan_destroy(plan);
+        plan = hpmpc_mi355x_plan_create(N, nx, nu, nb, idxb, ng);
+        key = plan ? k : std::vector<int>();
+        return plan;
+    }
+};
+
+thread_local Ctx g_ctx;
+
+// Arena carve (doubles) for one problem.
+struct Arena {
+    size_t BAbt, RSQ, d, ux, pi, lam, t, ws, vb, vq, vQx, vqx, vPb, stat, ints, total;
+};
+
+Arena arena(const hpmpc_mi355x_plan* P, int k_max) {
+    Arena A;
+    size_t o = 0;
+    auto take = [&](size_t n) {
+        size_t r = o;
+        o += (n + 7) / 8 * 8;
+        return r;
+    };
+    const size_t n1 = P->N + 1;
+    A.BAbt = take(P->packB);
+    A.RSQ = take(P->packR);
+    A.d = take(n1 * V32);
+    A.ux = take(n1 * V16);
+    A.pi = take(n1 * V16);
+    A.lam = take(n1 * V32);
+    A.t = take(n1 * V32);
+    A.ws = take(ws_doubles(P->N));
+    A.vb = take(n1 * V16);
+    A.vq = take(n1 * V16);
+    A.vQx = take(n1 * V16);
+    A.vqx = take(n1 * V16);
+    A.vPb = take(n1 * V16);
+    A.stat = take(5 * (size_t)(k_max > 0 ? k_max : 1) + 8);
+    A.ints = take(8);
+    A.total = o;
+    return A;
+}
+
+KArgs arena_args(const hpmpc_mi355x_plan* P, const Arena& A, double* dev) {
+    KArgs a = base_args(P, 1, 0);
+    a.sB = P->packB;
+    a.sR = P->packR;
+    a.BAbt = dev + A.BAbt;
+    a.RSQ = dev + A.RSQ;
+    a.d = dev + A.d;
+    a.ux = dev + A.ux;
+    a.pi = dev + A.pi;
+    a.lam = dev + A.lam;
+    a.t = dev + A.t;
+    a.ws = dev + A.ws;
+    a.vb = dev + A.vb;
+    a.vq = dev + A.vq;
+    a.vQx = dev + A.vQx;
+    a.vqx = dev + A.vqx;
+    a.vPb = dev + A.vPb;
+    a.stat = dev + A.stat;
+    a.kk = reinterpret_cast<int*>(dev + A.ints);
+    a.ret = a.kk + 1;
+    a.mu_out = dev + A.ints + 2;
+    return a;
+}
+
+// copy stage blocks (lib4, possibly aliased) into the packed arena layout
+void stage_BAbt(const hpmpc_mi355x_plan* P, double* H, const Arena& A, double** hpBAbt) {
+    for (int k = 0; k < P->N; k++) {
+        const auto& s = P->st[k];
+        const size_t n = (size_t)rup(s.nu + s.nx + 1, BS) * s.sdB;
+        memcpy(H + A.BAbt + P->offB[k], hpBAbt[k], n * sizeof(double));
+    }
+}
+void stage_RSQ(const hpmpc_mi355x_plan* P, double* H, const Arena& A, double** hpQ) {
+    for (int k = 0; k <= P->N; k++) {
+        const auto& s = P->st[k];
+        const size_t n = (size_t)rup(s.nu + s.nx + 1, BS) * s.sdR;
+        memcpy(H + A.RSQ + P->offR[k], hpQ[k], n * sizeof(double));
+    }
+}
+void stage_d(const hpmpc_mi355x_plan* P, double* H, const Arena& A, double** d) {
+    for (int k = 0; k <= P->N; k++) {
+        const int pnb = P->st[k].pnb;
+        if (P->nb[k] > 0) memcpy(H + A.d + k * V32, d[k], 2 * pnb * sizeof(double));
+    }
+}
+
+bool run(int which, const KArgs& a, const char* name) {
+    int e = hk_launch(which, &a, 1, g_ctx.stream);
+    if (e) {
+        char msg[128];
+        snprintf(msg, sizeof msg, "%s launch failed (%d)", name, e);
+        set_err(HPMPC_MI355X_EHIP, msg);
+        return false;
+    }
+    return true;
+}
+
+bool up(const Arena& A) {
+    return hip_ok(hipMemcpyAsync(g_ctx.dev, g_ctx.host, A.total * sizeof(double), hipMemcpyHostToDevice,
+                                 g_ctx.stream),
+                  "H2D");
+}
+bool down(const Arena& A) {
+    return hip_ok(hipMemcpyAsync(g_ctx.host, g_ctx.dev, A.total * sizeof(double), hipMemcpyDeviceToHost,
+                                 g_ctx.stream),
+                  "D2H") &&
+           hip_ok(hipStreamSynchronize(g_ctx.stream), "sync");
+}
+
+}  // namespace
+
+extern "C" int d_back_ric_rec_sv_tv_work_space_size_bytes(int N, int* nx, int* nu, int* nb, int* ng) {
+    (void)N;
+    (void)nx;
+    (void)nu;
+    (void)nb;
+    (void)ng;
+    return 64;  // all temporaries live on the device
+}
+
+extern "C" int d_back_ric_rec_sv_tv_memory_space_size_bytes(int N, int* nx, int* nu, int* nb, int* ng) {
+    (void)nx;
+    (void)nu;
+    (void)nb;
+    (void)ng;
+    return (int)(((long long)(N + 1) * FSTRIDE * 8 + 63) / 64 * 64);
+}
+
+extern "C" void d_back_ric_rec_sv_tv_res(int N, int* nx, int* nu, int* nb, int** idxb, int* ng, int update_b,
+                                         double** hpBAbt, double** b, int update_q, double** hpQ, double** q,
+                                         double** bd, double** hpDCt, double** Qx, double** qx, double** hux,
+                                         int compute_pi, double** hpi, int compute_Pb, double** hPb, double* memory,
+                                         double* work) {
+    (void)hpDCt;
+    (void)work;
+    g_err = 0;
+    hpmpc_mi355x_plan* P = g_ctx.get_plan(N, nx, nu, nb, idxb, ng);
+    if (!P) return;
+    Arena A = arena(P, 1);
+    if (!g_ctx.ensure(A.total)) return;
+    double* H = g_ctx.host;
+    // Stage copies receive exactly what the reference factorises for that stage; the caller's
+    // buffers get the reference's side effects, applied in its stage order (N .. 0).
+    for (int k = N; k >= 0; k--) {
+        const auto& s = P->st[k];
+        const int nux = s.nu + s.nx, cnux = s.sdR;
+        if (update_q)
+            for (int j = 0; j < nux; j++) P4(hpQ[k], cnux, nux, j) = q[k][j];
+        for (int l = 0; l < nb[k]; l++) {
+            const int ii = idxb[k][l];
+            P4(hpQ[k], cnux, ii, ii) = bd[k][l] + Qx[k][l];
+        }
+        for (int l = 0; l < nb[k]; l++) P4(hpQ[k], cnux, nux, idxb[k][l]) += qx[k][l];
+        memcpy(H + A.RSQ + P->offR[k], hpQ[k], (size_t)rup(nux + 1, BS) * cnux * sizeof(double));
+        if (k < N) {
+            if (update_b)
+                for (int j = 0; j < s.nx1; j++) P4(hpBAbt[k], s.sdB, nux, j) = b[k][j];
+            memcpy(H + A.BAbt + P->offB[k], hpBAbt[k], (size_t)rup(nux + 1, BS) * s.sdB * sizeof(double));
+        }
+    }
+    KArgs a = arena_args(P, A, g_ctx.dev);
+    a.compute_pi = compute_pi;
+    a.compute_Pb = compute_Pb;
+    if (!up(A) || !run(K_SV, a, "hk_ric_sv") || !down(A)) return;
+    for (int k = 0; k <= N; k++) {
+        const int nux = P->st[k].nu + P->st[k].nx;
+        memcpy(hux[k], H + A.ux + k * V16, nux * sizeof(double));
+        if (k < N && compute_pi) memcpy(hpi[k], H + A.pi + k * V16, nx[k + 1] * sizeof(double));
+        if (k < N && compute_Pb) memcpy(hPb[k], H + A.vPb + k * V16, nx[k + 1] * sizeof(double));
+    }
+    memcpy(memory, H + A.ws, (size_t)(N + 1) * FSTRIDE * sizeof(double));
+}
+
+extern "C" void d_back_ric_rec_trf_tv_res(int N, int* nx, int* nu, int* nb, int** idxb, int* ng, double** hpBAbt,
+                                          double** hpQ, double** hpDCt, double** Qx, double** bd, double* memory,
+                                          double* work) {
+    (void)hpDCt;
+    (void)work;
+    g_err = 0;
+    hpmpc_mi355x_plan* P = g_ctx.get_plan(N, nx, nu, nb, idxb, ng);
+    if (!P) return;
+    Arena A = arena(P, 1);
+    if (!g_ctx.ensure(A.total)) return;
+    double* H = g_ctx.host;
+    for (int k = N; k >= 0; k--) {
+        const auto& s = P->st[k];
+        const int nux = s.nu + s.nx, cnux = s.sdR;
+        for (int l = 0; l < nb[k]; l++) {
+            const int ii = idxb[k][l];
+            P4(hpQ[k], cnux, ii, ii) = bd[k][l] + Qx[k][l];
+        }
+        memcpy(H + A.RSQ + P->offR[k], hpQ[k], (size_t)rup(nux + 1, BS) * cnux * sizeof(double));
+        if (k < N) memcpy(H + A.BAbt + P->offB[k], hpBAbt[k], (size_t)rup(nux + 1, BS) * s.sdB * sizeof(double));
+    }
+    KArgs a = arena_args(P, A, g_ctx.dev);
+    if (!up(A) || !run(K_TRF, a, "hk_ric_trf") || !down(A)) return;
+    memcpy(memory, H + A.ws, (size_t)(N + 1) * FSTRIDE * sizeof(double));
+}
+
+extern "C" void d_back_ric_rec_trs_tv_res(int N, int* nx, int* nu, int* nb, int** idxb, int* ng, double** hpBAbt,
+                                          double** hb, double** hq, double** hpDCt, double** qx, double** hux,
+                                          int compute_pi, double** hpi, int compute_Pb, double** hPb, double* memory,
+                                          double* work) {
+    (void)hpDCt;
+    (void)work;
+    g_err = 0;
+    hpmpc_mi355x_plan* P = g_ctx.get_plan(N, nx, nu, nb, idxb, ng);
+    if (!P) return;
+    Arena A = arena(P, 1);
+    if (!g_ctx.ensure(A.total)) return;
+    double* H = g_ctx.host;
+    stage_BAbt(P, H, A, hpBAbt);
+    memcpy(H + A.ws, memory, (size_t)(N + 1) * FSTRIDE * sizeof(double));
+    for (int k = 0; k <= N; k++) {
+        const int nux = P->st[k].nu + P->st[k].nx;
+        memcpy(H + A.vq + k * V16, hq[k], nux * sizeof(double));
+        if (k < N) memcpy(H + A.vb + k * V16, hb[k], nx[k + 1] * sizeof(double));
+        if (k < N && !compute_Pb) memcpy(H + A.vPb + k * V16, hPb[k], nx[k + 1] * sizeof(double));
+        if (nb[k] > 0) memcpy(H + A.vqx + k * V16, qx[k], nb[k] * sizeof(double));
+    }
+    KArgs a = arena_args(P, A, g_ctx.dev);
+    a.use_box = 1;
+    a.compute_pi = compute_pi;
+    a.compute_Pb = compute_Pb;
+    if (!up(A) || !run(K_TRS, a, "hk_ric_trs") || !down(A)) return;
+    for (int k = 0; k <= N; k++) {
+        const int nux = P->st[k].nu + P->st[k].nx;
+        memcpy(hux[k], H + A.ux + k * V16, nux * sizeof(double));
+        if (k < N && compute_pi) memcpy(hpi[k], H + A.pi + k * V16, nx[k + 1] * sizeof(double));
+        if (k < N && compute_Pb) memcpy(hPb[k], H + A.vPb + k * V16, nx[k + 1] * sizeof(double));
+    }
+}
+
+extern "C" int d_ip2_res_mpc_hard_tv_work_space_size_bytes(int N, int* nx, int* nu, int* nb, int* ng) {
+    (void)nx;
+    (void)nu;
+    (void)nb;
+    (void)ng;
+    return (int)((ws_doubles(N) * 8 + 63) / 64 * 64);
+}
+
+extern "C" int d_ip2_res_mpc_hard_tv(int* kk, int k_max, double mu0, double mu_tol, double alpha_min, int warm_start,
+                                     double* stat, int N, int* nx, int* nu_N, int* nb, int** idxb, int* ng,
+                                     double** pBAbt, double** pQ, double** pDCt, double** d, double** ux,
+                                     int compute_mult, double** pi, double** lam, double** t,
+                                     double* double_work_memory) {
+    (void)pDCt;
+    g_err = 0;
+    hpmpc_mi355x_plan* P = g_ctx.get_plan(N, nx, nu_N, nb, idxb, ng);
+    if (!P) return g_err;
+    Arena A = arena(P, k_max);
+    if (!g_ctx.ensure(A.total)) return g_err;
+    double* H = g_ctx.host;
+    stage_BAbt(P, H, A, pBAbt);
+    stage_RSQ(P, H, A, pQ);
+    stage_d(P, H, A, d);
+    if (warm_start)
+        for (int k = 0; k <= N; k++) memcpy(H + A.ux + k * V16, ux[k], (P->st[k].nu + nx[k]) * sizeof(double));
+    KArgs a = arena_args(P, A, g_ctx.dev);
+    a.k_max = k_max;
+    a.mu0 = mu0;
+    a.mu_tol = mu_tol;
+    a.alpha_min = alpha_min;
+    a.warm_start = warm_start;
+    a.compute_mult = compute_mult;
+    if (!up(A) || !run(K_IPM, a, "hk_ipm") || !down(A)) return g_err;
+    const int* iv = reinterpret_cast<const int*>(H + A.ints);
+    *kk = iv[0];
+    for (int i = 0; i < 5 * iv[0]; i++) stat[i] = H[A.stat + i];
+    for (int k = 0; k <= N; k++) {
+        memcpy(ux[k], H + A.ux + k * V16, (P->st[k].nu + nx[k]) * sizeof(double));
+        if (k < N) memcpy(pi[k], H + A.pi + k * V16, nx[k + 1] * sizeof(double));
+        const int pnb = P->st[k].pnb;
+        if (nb[k] > 0) {
+            memcpy(lam[k], H + A.lam + k * V32, 2 * pnb * sizeof(double));
+            memcpy(t[k], H + A.t + k * V32, 2 * pnb * sizeof(double));
+        }
+    }
+    memcpy(double_work_memory, H + A.ws, ws_doubles(N) * sizeof(double));
+    return iv[1];
+}
+
+extern "C" void d_kkt_solve_new_rhs_res_mpc_hard_tv(int N, int* nx, int* nu_N, int* nb, int** idxb, int* ng,
+                                                    double** pBAbt, double** b, double** pQ, double** q,
+                                                    double** pDCt, double** d, double** ux, int compute_mult,
+                                                    double** pi, double** lam, double** t,
+                                                    double* double_work_memory) {
+    (void)pDCt;
+    g_err = 0;
+    hpmpc_mi355x_plan* P = g_ctx.get_plan(N, nx, nu_N, nb, idxb, ng);
+    if (!P) return;
+    Arena A = arena(P, 1);
+    if (!g_ctx.ensure(A.total)) return;
+    double* H = g_ctx.host;
+    stage_BAbt(P, H, A, pBAbt);
+    stage_RSQ(P, H, A, pQ);
+    stage_d(P, H, A, d);
+    memcpy(H + A.ws, double_work_memory, ws_doubles(N) * sizeof(double));
+    for (int k = 0; k <= N; k++) {
+        memcpy(H + A.vq + k * V16, q[k], (P->st[k].nu + nx[k]) * sizeof(double));
+        if (k < N) memcpy(H + A.vb + k * V16, b[k], nx[k + 1] * sizeof(double));
+    }
+    KArgs a = arena_args(P, A, g_ctx.dev);
+    a.compute_mult = compute_mult;
+    if (!up(A) || !run(K_KKT, a, "hk_kkt_new_rhs") || !down(A)) return;
+    for (int k = 0; k <= N; k++) {
+        memcpy(ux[k], H + A.ux + k * V16, (P->st[k].nu + nx[k]) * sizeof(double));
+        if (k < N) memcpy(pi[k], H + A.pi + k * V16, nx[k + 1] * sizeof(double));
+        const int pnb = P->st[k].pnb;
+        if (nb[k] > 0) {
+            memcpy(lam[k], H + A.lam + k * V32, 2 * pnb * sizeof(double));
+            memcpy(t[k], H + A.t + k * V32, 2 * pnb * sizeof(double));
+        }
+    }
+}
+
+extern "C" void d_res_res_mpc_hard_tv(int N, int* nx, int* nu, int* nb, int** idxb, int* ng, double** hpBAbt,
+                                      double** hb, double** hpQ, double** hq, double** hux, double** hpDCt,
+                                      double** hd, double** hpi, double** hlam, double** ht, double* work,
+                                      double** hrq, double** hrb, double** hrd, double** hrm, double* mu) {
+    (void)hpDCt;
+    (void)work;
+    g_err = 0;
+    hpmpc_mi355x_plan* P = g_ctx.get_plan(N, nx, nu, nb, idxb, ng);
+    if (!P) return;
+    Arena A = arena(P, 1);
+    if (!g_ctx.ensure(A.total)) return;
+    double* H = g_ctx.host;
+    stage_BAbt(P, H, A, hpBAbt);
+    stage_RSQ(P, H, A, hpQ);
+    stage_d(P, H, A, hd);
+    for (int k = 0; k <= N; k++) {
+        const int nux = P->st[k].nu + nx[k];
+        memcpy(H + A.vq + k * V16, hq[k], nux * sizeof(double));
+        memcpy(H + A.ux + k * V16, hux[k], nux * sizeof(double));
+        if (k < N) {
+            memcpy(H + A.vb + k * V16, hb[k], nx[k + 1] * sizeof(double));
+            memcpy(H + A.pi + k * V16, hpi[k], nx[k + 1] * sizeof(double));
+        }
+        const int pnb = P->st[k].pnb;
+        if (nb[k] > 0) {
+            memcpy(H + A.lam + k * V32, hlam[k], 2 * pnb * sizeof(double));
+            memcpy(H + A.t + k * V32, ht[k], 2 * pnb * sizeof(double));
+        }
+    }
+    KArgs a = arena_args(P, A, g_ctx.dev);
+    H[A.ints + 2] = *mu;  // mu is left untouched when there are no constraints (d_res_ip_res_hard.c:309-313)
+    if (!up(A) || !run(K_RES, a, "hk_res") || !down(A)) return;
+    const size_t n1 = N + 1;
+    const double* rq = H + A.ws;
+    const double* rb = rq + n1 * V16;
+    const double* rd = rb + n1 * V16;
+    const double* rm = rd + n1 * V32;
+    for (int k = 0; k <= N; k++) {
+        const int nux = P->st[k].nu + nx[k];
+        memcpy(hrq[k], rq + k * V16, nux * sizeof(double));
+        if (k < N) memcpy(hrb[k], rb + k * V16, nx[k + 1] * sizeof(double));
+        const int pnb = P->st[k].pnb;
+        if (nb[k] > 0) {
+            memcpy(hrd[k], rd + k * V32, 2 * pnb * sizeof(double));
+            memcpy(hrm[k], rm + k * V32, 2 * pnb * sizeof(double));
+        }
+    }
+    *mu = H[A.ints + 2];
+}

@@ -1,0 +1,31 @@
+// hpmpc_kargs.h -- kernel argument block shared by the host C-ABI and the HIP kernels.
+// Plain C layout; every pointer is a device pointer.  Per-problem arrays are problem-major with the
+// stride given next to them (0 = shared by all problems, i.e. time-invariant / aliased data).
+#pragma once
+
+struct KArgs {
+    int N, nprob, p0;             // horizon, problems in the batch, first problem of this launch
+    const void* st;               // hk::StageInfo[N+1]
+    const signed char* tileslot;  // (N+1)*16
+    const signed char* slotvar;   // (N+1)*16
+    const double* BAbt;           // lib4 stage blocks
+    long long sB;
+    const double* RSQ;
+    long long sR;
+    const double* d;  // bounds, V32 per stage: [lb (pnb) | ub (pnb)]
+    double* ws;       // per-problem workspace / factor memory
+    long long sW;
+    double *ux, *pi;  // V16 per stage (variable order / state order)
+    double *lam, *t;  // V32 per stage
+    long long sV16, sV32;
+    // Riccati entry points: optional inputs (V16 per stage, same strides as ux)
+    const double *vb, *vq, *vQx, *vqx;
+    double* vPb;
+    int update_b, update_q, use_box, compute_pi, compute_Pb;
+    // IPM
+    int k_max, warm_start, compute_mult;
+    double mu0, mu_tol, alpha_min;
+    int *kk, *ret;
+    double* stat;    // 5*k_max per problem
+    double* mu_out;  // per problem (residual kernel)
+};

@@ -1,0 +1,120 @@
+/*
+ * hpmpc_mi355x.h -- C ABI of libhpmpc_mi355x.so, the MI355X (gfx950) drop-in for HPMPC's
+ * Riccati / interior-point hot path.
+ *
+ * Part 1 re-exports the reference's own low-level entry points with byte-identical prototypes, so
+ * that the reference drivers (test_problems/test_d_ip_hard.c, test_d_ric_mpc.c) and the high-level
+ * wrappers (interfaces/c/fortran_order_interface.c) relink against this library unchanged.  Each
+ * prototype cites the reference declaration it replaces (paths relative to the reference checkout).
+ * All data are the reference's lib4 panel-major buffers (bs = 4, ncl = 2) on the HOST; every call
+ * runs on the GPU (no CPU fallback).  Workspace / memory contents are private to this library and
+ * are sized by this library's *_size_bytes functions.
+ *
+ * Part 2 is the additive batched API: many independent QPs that share stage sizes, with all data
+ * already resident in device memory (HBM).
+ *
+ * GPU-path limits (checked; a violation is reported through hpmpc_mi355x_last_error()):
+ *   nu[k] + nx[k] <= 16 and round_up(nu[k],4) + nx[k] <= 16 for every stage, ng[k] == 0.
+ * Error reporting: the reference's int entry points keep their codes 0/1/2/-1; this library adds
+ *   HPMPC_MI355X_EUNSUPPORTED (-10) and HPMPC_MI355X_EHIP (-11).  void entry points set the
+ *   thread-local code returned by hpmpc_mi355x_last_error() and print one line to stderr.
+ */
+#ifndef HPMPC_MI355X_H_
+#define HPMPC_MI355X_H_
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HPMPC_MI355X_EUNSUPPORTED (-10)
+#define HPMPC_MI355X_EHIP (-11)
+
+/* ================================ Part 1: reference entry points ================================ */
+
+/* include/lqcp_solvers.h:37 (lqcp_solvers/d_back_ric_rec.c:43) */
+int d_back_ric_rec_sv_tv_work_space_size_bytes(int N, int *nx, int *nu, int *nb, int *ng);
+/* include/lqcp_solvers.h:39 (d_back_ric_rec.c:79) */
+int d_back_ric_rec_sv_tv_memory_space_size_bytes(int N, int *nx, int *nu, int *nb, int *ng);
+/* include/lqcp_solvers.h:41 (d_back_ric_rec.c:112) -- factorise + solve */
+void d_back_ric_rec_sv_tv_res(int N, int *nx, int *nu, int *nb, int **idxb, int *ng, int update_b, double **hpBAbt,
+                              double **b, int update_q, double **hpQ, double **q, double **bd, double **hpDCt,
+                              double **Qx, double **qx, double **hux, int compute_pi, double **hpi, int compute_Pb,
+                              double **hPb, double *memory, double *work);
+/* include/lqcp_solvers.h:43 (d_back_ric_rec.c:403) -- factorise */
+void d_back_ric_rec_trf_tv_res(int N, int *nx, int *nu, int *nb, int **idxb, int *ng, double **hpBAbt, double **hpQ,
+                               double **hpDCt, double **Qx, double **bd, double *memory, double *work);
+/* include/lqcp_solvers.h:45 (d_back_ric_rec.c:564) -- solve with the factor left in memory */
+void d_back_ric_rec_trs_tv_res(int N, int *nx, int *nu, int *nb, int **idxb, int *ng, double **hpBAbt, double **hb,
+                               double **hq, double **hpDCt, double **qx, double **hux, int compute_pi, double **hpi,
+                               int compute_Pb, double **hPb, double *memory, double *work);
+
+/* include/mpc_solvers.h:41 (mpc_solvers/d_ip2_res_hard.c:57) */
+int d_ip2_res_mpc_hard_tv_work_space_size_bytes(int N, int *nx, int *nu, int *nb, int *ng);
+/* include/mpc_solvers.h:42 (d_ip2_res_hard.c:116) */
+int d_ip2_res_mpc_hard_tv(int *kk, int k_max, double mu0, double mu_tol, double alpha_min, int warm_start,
+                          double *stat, int N, int *nx, int *nu_N, int *nb, int **idxb, int *ng, double **pBAbt,
+                          double **pQ, double **pDCt, double **d, double **ux, int compute_mult, double **pi,
+                          double **lam, double **t, double *double_work_memory);
+/* include/mpc_solvers.h:46 (d_ip2_res_hard.c:1922) -- re-solve with the persisted factor/iterate */
+void d_kkt_solve_new_rhs_res_mpc_hard_tv(int N, int *nx, int *nu_N, int *nb, int **idxb, int *ng, double **pBAbt,
+                                         double **b, double **pQ, double **q, double **pDCt, double **d,
+                                         double **ux, int compute_mult, double **pi, double **lam, double **t,
+                                         double *double_work_memory);
+/* include/mpc_solvers.h:47 (mpc_solvers/c99/d_res_ip_res_hard.c:39) */
+void d_res_res_mpc_hard_tv(int N, int *nx, int *nu, int *nb, int **idxb, int *ng, double **hpBAbt, double **hb,
+                           double **hpQ, double **hq, double **hux, double **hpDCt, double **hd, double **hpi,
+                           double **hlam, double **ht, double *work, double **hrq, double **hrb, double **hrd,
+                           double **hrm, double *mu);
+
+/* ================================ Part 2: batched device API ==================================== */
+
+/* Opaque plan: stage sizes, box indices and device tables shared by every problem of a batch. */
+typedef struct hpmpc_mi355x_plan hpmpc_mi355x_plan;
+
+/* Create a plan for horizon N with per-stage sizes (nu[N] is ignored and treated as 0; idxb[k]
+ * lists the nb[k] boxed variables of stage k).  Returns NULL on unsupported sizes. */
+hpmpc_mi355x_plan *hpmpc_mi355x_plan_create(int N, const int *nx, const int *nu, const int *nb,
+                                            const int *const *idxb, const int *ng);
+void hpmpc_mi355x_plan_destroy(hpmpc_mi355x_plan *plan);
+
+/* Device-array geometry of a problem-major batch (all sizes in doubles). */
+typedef struct {
+    long long BAbt_stride;   /* doubles between problems (0: shared by all problems) */
+    long long RSQrq_stride;
+    const long long *BAbt_off;   /* host array [N]   : lib4 block of stage k inside one problem */
+    const long long *RSQrq_off;  /* host array [N+1] */
+} hpmpc_mi355x_layout;
+
+/* Doubles of per-problem device workspace the batched calls need (factor + IPM iterate). */
+long long hpmpc_mi355x_ws_doubles(const hpmpc_mi355x_plan *plan);
+
+/* Batched d_ip2_res_mpc_hard_tv on problems [p0, p0+count) of a batch of nprob problems.
+ * d, lam, t: 32 doubles per stage ([lb(pnb) | ub(pnb)], reference padded layout inside the stride);
+ * ux, pi: 16 doubles per stage (ux in the reference variable order, pi over x_{k+1}).
+ * kk, ret: per problem; stat: 5*k_max per problem.  Asynchronous on `stream` (hipStream_t). */
+int hpmpc_mi355x_ipm_batch(const hpmpc_mi355x_plan *plan, const hpmpc_mi355x_layout *lay, int nprob, int p0,
+                           int count, const double *BAbt, const double *RSQrq, const double *d, double *ux, double *pi,
+                           double *lam, double *t, double *ws, int k_max, double mu0, double mu_tol, double alpha_min,
+                           int warm_start, int compute_mult, int *kk, int *ret, double *stat, void *stream);
+
+/* Batched d_back_ric_rec_sv_tv_res (no box / no update rows): factor into ws, ux/pi as above. */
+int hpmpc_mi355x_ric_sv_batch(const hpmpc_mi355x_plan *plan, const hpmpc_mi355x_layout *lay, int nprob, int p0,
+                              int count, const double *BAbt, const double *RSQrq, double *ux, double *pi, double *ws,
+                              int compute_pi, int compute_Pb, double *Pb, void *stream);
+
+/* Batched d_back_ric_rec_trs_tv_res re-using the factor in ws; b (16/stage, state order), q (16/stage,
+ * variable order). */
+int hpmpc_mi355x_ric_trs_batch(const hpmpc_mi355x_plan *plan, const hpmpc_mi355x_layout *lay, int nprob, int p0,
+                               int count, const double *BAbt, const double *RSQrq, const double *b, const double *q,
+                               double *ux, double *pi, double *ws, int compute_pi, int compute_Pb, double *Pb,
+                               void *stream);
+
+/* Thread-local status of the last call (0 = success). */
+int hpmpc_mi355x_last_error(void);
+/* Library build string (architecture, kernel variant). */
+const char *hpmpc_mi355x_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HPMPC_MI355X_H_ */
