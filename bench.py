@@ -1,0 +1,224 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X Riccati / interior-point hot path (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1] shape at the metric's batch): 1024 box-constrained mass-spring
+MPC QPs per GPU, N=100, nx=12, nu=4 (nb = 4 / 10 / 6 on stage 0 / inner / N), fp64, time-variant
+stage data (no aliased buffers), solved by the residual-based Mehrotra IPM
+(d_ip2_res_mpc_hard_tv: mu0=2, mu_tol=1e-12, alpha_min=1e-8, k_max=50).
+
+A "step" is one batched IPM solve of the whole resident batch (one hk_ipm launch).  value = IP
+iterations per second over all ranks (sum of per-problem iteration counts / max-over-ranks time).
+The Riccati factorisation rate (d_back_ric_rec_sv_tv_res, nb = 0, compute_pi = 1) of the same
+batch is reported in the same JSON line.
+
+Multi-GPU: one process per GPU (torch.distributed.run); every rank generates its own shard of
+problems from the global problem seeds (no data-path collective: weak scaling); RCCL is used only
+for the barrier and the max-time / sum-of-iterations reductions.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
+PEAK_FP64_TFS = 78.6   # MI355X fp64 (vector = MFMA dense)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=1024, help="problems per GPU")
+    ap.add_argument("--N", type=int, default=100)
+    ap.add_argument("--nx", type=int, default=12)
+    ap.add_argument("--nu", type=int, default=4)
+    ap.add_argument("--k-max", type=int, default=50)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(qp, seconds, k_max):
+    """Time the reference c99 build (oracle/_ref, kind 'reference') -- or the clean-room oracle
+    (kind 'port') when the reference build is absent -- on one host core, problem after problem."""
+    from hpmpc_amd.cabi import HpmpcAPI, load
+
+    ref = os.path.join(ROOT, "oracle", "_ref", "libhpmpc_ref.so")
+    orc = os.path.join(ROOT, "oracle", "liboracle.so")
+    if os.path.exists(ref):
+        api, kind = HpmpcAPI(load(ref)), "reference"
+    elif os.path.exists(orc):
+        api, kind = HpmpcAPI(load(orc), "orc_"), "port"
+    else:
+        return None
+    iters = 0
+    nsolved = 0
+    t_solve = 0.0
+    t_end = time.perf_counter() + seconds
+    p = 0
+    while time.perf_counter() < t_end and p < qp.batch:
+        one = qp.problem(p)
+        t0 = time.perf_counter()
+        r = api.ipm(one, k_max=k_max)
+        t_solve += time.perf_counter() - t0
+        iters += r["kk"]
+        nsolved += 1
+        p += 1
+    return {"value": iters / t_solve, "unit": "IP-iter/s", "cores": 1, "kind": kind,
+            "sample": f"{nsolved} of the benchmark's problems solved sequentially on 1 core "
+                      f"({iters} IP iterations, {t_solve:.1f} s; ctypes marshalling included)"}
+
+
+def main():
+    args = parse()
+    import torch
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl")
+
+    from hpmpc_amd.batch import (BatchSolver, algorithmic_bytes_per_ip_iter, algorithmic_bytes_per_sv,
+                                 flops_ip_iter, flops_sv)
+    from hpmpc_amd.ocp import batch_x0, mass_spring_qp
+
+    B, N, nx, nu = args.batch, args.N, args.nx, args.nu
+    X0 = batch_x0(nx, B * world)[rank * B:(rank + 1) * B]
+    qp = mass_spring_qp(N, nx, nu, batch=B, x0=X0, time_variant=True, seed=1 + rank)
+    solver = BatchSolver(qp, k_max=args.k_max)
+    qp_ric = mass_spring_qp(N, nx, nu, boxes=False, batch=B, x0=X0, time_variant=True, seed=1 + rank)
+    ric = BatchSolver(qp_ric, k_max=1)
+    stream = torch.cuda.current_stream()
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    def max_over_ranks(x):
+        if dist is None:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum_over_ranks(x):
+        if dist is None:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return float(t.item())
+
+    # ---------------- IPM (headline) ----------------
+    for _ in range(args.warmup):
+        solver.ipm()
+    barrier()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        solver.ipm()
+        ev[i][1].record(stream)
+    barrier()
+    t1 = time.perf_counter()
+    dt = max_over_ranks(t1 - t0)
+    kk = solver.kk.cpu().numpy()
+    ret = solver.ret.cpu().numpy()
+    iters_step = float(kk.sum())
+    iters_total = sum_over_ranks(iters_step) * args.steps
+    value = iters_total / dt
+    launch_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    bytes_iter = algorithmic_bytes_per_ip_iter(qp)
+    achieved = iters_step * bytes_iter / (launch_ms * 1e-3) / 1e9  # GB/s of the hk_ipm launch
+    fl_iter = flops_ip_iter(N, nx, nu)
+
+    # ---------------- Riccati factorisation + solve ----------------
+    for _ in range(args.warmup):
+        ric.ric_sv()
+    barrier()
+    evr = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    barrier()
+    r0 = time.perf_counter()
+    for i in range(args.steps):
+        evr[i][0].record(stream)
+        ric.ric_sv()
+        evr[i][1].record(stream)
+    barrier()
+    r1 = time.perf_counter()
+    rdt = max_over_ranks(r1 - r0)
+    fact_total = B * world * args.steps
+    sv_ms = float(np.mean([a.elapsed_time(b) for a, b in evr]))
+    sv_bytes = algorithmic_bytes_per_sv(qp_ric)
+    sv_achieved = B * sv_bytes / (sv_ms * 1e-3) / 1e9
+
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_hk_ipm.json")
+    if os.path.exists(pmc):
+        try:
+            with open(pmc) as f:
+                pm = json.load(f)
+            if pm.get("workload") == f"ipm_N{N}_nx{nx}_nu{nu}_batch{B}":
+                traffic = pm.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(qp, args.cpu_seconds, args.k_max)
+
+    if rank == 0:
+        line = {
+            "metric": "IP iterations/sec (Riccati-based IPM, d_ip2_res_mpc_hard_tv), fp64, N=100 nx=12 nu=4 "
+                      "batch=1024 per GPU",
+            "value": value,
+            "unit": "IP-iter/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (mass-spring MPC, per-problem x0 ~ U(-2.5,2.5) from PCG64(20261015+p), time-variant "
+                    "A/B/Q perturbations; generated on each rank, no scatter)",
+            "config": {"workload": f"ipm_N{N}_nx{nx}_nu{nu}_batch{B}", "N": N, "nx": nx, "nu": nu,
+                       "batch_per_gpu": B, "global_batch": B * world, "k_max": args.k_max, "mu_tol": 1e-12,
+                       "parallelism": f"dp{world}" if world > 1 else "single",
+                       "sum_kk_per_step": iters_total / args.steps, "ret_counts": {
+                           str(int(r)): int((ret == r).sum()) for r in np.unique(ret)}},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": achieved / PEAK_HBM_GBS, "traffic": traffic, "kernel": "hk_ipm",
+                         "launch_ms": launch_ms, "algorithmic_bytes_per_ip_iter": bytes_iter,
+                         "fp64_tflops": iters_step * fl_iter / (launch_ms * 1e-3) / 1e12},
+            "riccati": {"value": fact_total / rdt, "unit": "fact/s", "kernel": "hk_ric_sv", "launch_ms": sv_ms,
+                        "roofline": {"bound": "hbm", "achieved": sv_achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                                     "frac": sv_achieved / PEAK_HBM_GBS,
+                                     "algorithmic_bytes_per_sv": sv_bytes,
+                                     "fp64_tflops": B * flops_sv(N, nx, nu) / (sv_ms * 1e-3) / 1e12}},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,222 @@
+"""Batched, device-resident front end of libhpmpc_mi355x.so (additive API).
+
+A batch is ``nprob`` independent QPs that share stage sizes and box indices.  All arrays live in
+HBM as problem-major torch tensors (torch is plumbing here: allocation, streams, events); the solve
+itself is one launch of the HIP kernels through the library's C ABI:
+
+    BAbt  (nprob, packB)   lib4 stage blocks, stage k at offB[k]      (d_ip2_res_hard.c pBAbt[k])
+    RSQrq (nprob, packR)   lib4 stage blocks, stage k at offR[k]      (pQ[k])
+    d     (nprob, N+1, 32) [lb (pnb) | ub (pnb)] per stage            (d[k])
+    ux    (nprob, N+1, 16) variable order u..x                        (ux[k])
+    pi    (nprob, N+1, 16) over x_{k+1}                               (pi[k])
+    lam/t (nprob, N+1, 32) reference padded layout                    (lam[k] / t[k])
+    ws    (nprob, ws_doubles) factor + persistent IPM iterate
+
+There is no CPU fallback: constructing a solver without a GPU or without the built library raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from .ocp import OCPQP
+
+_LIB = None
+LIBPATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libhpmpc_mi355x.so")
+
+
+def lib() -> C.CDLL:
+    """Load the in-tree HIP library (raises if it was not built)."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIBPATH):
+            raise RuntimeError(f"libhpmpc_mi355x.so not built ({LIBPATH}); run __graft_entry__.build()")
+        L = C.CDLL(LIBPATH, mode=os.RTLD_LOCAL | getattr(os, "RTLD_NOW", 2))
+        vp, i, d, ll = C.c_void_p, C.c_int, C.c_double, C.c_longlong
+        L.hpmpc_mi355x_plan_create.restype = vp
+        L.hpmpc_mi355x_plan_create.argtypes = [i, vp, vp, vp, vp, vp]
+        L.hpmpc_mi355x_plan_destroy.argtypes = [vp]
+        L.hpmpc_mi355x_ws_doubles.restype = ll
+        L.hpmpc_mi355x_ws_doubles.argtypes = [vp]
+        L.hpmpc_mi355x_ipm_batch.restype = i
+        L.hpmpc_mi355x_ipm_batch.argtypes = [vp, vp, i, i, i, vp, vp, vp, vp, vp, vp, vp, vp, i, d, d, d, i, i, vp,
+                                             vp, vp, vp]
+        L.hpmpc_mi355x_ric_sv_batch.restype = i
+        L.hpmpc_mi355x_ric_sv_batch.argtypes = [vp, vp, i, i, i, vp, vp, vp, vp, vp, i, i, vp, vp]
+        L.hpmpc_mi355x_ric_trf_batch.restype = i
+        L.hpmpc_mi355x_ric_trf_batch.argtypes = [vp, vp, i, i, i, vp, vp, vp, vp]
+        L.hpmpc_mi355x_ric_trs_batch.restype = i
+        L.hpmpc_mi355x_ric_trs_batch.argtypes = [vp, vp, i, i, i, vp, vp, vp, vp, vp, vp, vp, i, i, vp, vp]
+        L.hpmpc_mi355x_last_error.restype = i
+        L.hpmpc_mi355x_version.restype = C.c_char_p
+        _LIB = L
+    return _LIB
+
+
+class _Layout(C.Structure):
+    _fields_ = [("BAbt_stride", C.c_longlong), ("RSQrq_stride", C.c_longlong),
+                ("BAbt_off", C.POINTER(C.c_longlong)), ("RSQrq_off", C.POINTER(C.c_longlong))]
+
+
+class BatchSolver:
+    """Device-resident batch of OCP QPs + the batched HPMPC entry points."""
+
+    def __init__(self, qp: OCPQP, device="cuda", k_max: int = 50):
+        import torch
+
+        if not torch.cuda.is_available():
+            raise RuntimeError("BatchSolver needs a GPU (HIP device); there is no CPU fallback")
+        assert qp.batch is not None, "BatchSolver takes a batched OCPQP"
+        self.torch = torch
+        self.qp = qp
+        self.N = N = qp.N
+        self.nprob = qp.batch
+        self.k_max = k_max
+        self.dev = torch.device(device)
+        L = lib()
+        self._keep = []
+        idx_arrs = [np.ascontiguousarray(i, dtype=np.int32) for i in qp.idxb]
+        self._keep.append(idx_arrs)
+        idxp = (C.POINTER(C.c_int) * (N + 1))(*[a.ctypes.data_as(C.POINTER(C.c_int)) for a in idx_arrs])
+        self._keep.append(idxp)
+        ints = lambda a: np.ascontiguousarray(a, dtype=np.int32)
+        self._nx, self._nu, self._nb, self._ng = ints(qp.nx), ints(qp.nu), ints(qp.nb), ints(qp.ng)
+        self.plan = L.hpmpc_mi355x_plan_create(N, self._nx.ctypes.data, self._nu.ctypes.data, self._nb.ctypes.data,
+                                               C.cast(idxp, C.c_void_p), self._ng.ctypes.data)
+        if not self.plan:
+            raise ValueError(f"unsupported problem sizes for the GPU path (code {L.hpmpc_mi355x_last_error()})")
+        # problem-major packed inputs
+        offB = np.zeros(N, dtype=np.int64)
+        offR = np.zeros(N + 1, dtype=np.int64)
+        o = 0
+        for k in range(N):
+            offB[k] = o
+            o += qp.BAbt[k].shape[1]
+        packB = o
+        o = 0
+        for k in range(N + 1):
+            offR[k] = o
+            o += qp.RSQrq[k].shape[1]
+        packR = o
+        self.offB, self.offR = offB, offR
+        self.layout = _Layout(packB, packR, offB.ctypes.data_as(C.POINTER(C.c_longlong)),
+                              offR.ctypes.data_as(C.POINTER(C.c_longlong)))
+        hB = np.concatenate([a for a in qp.BAbt], axis=1)
+        hR = np.concatenate([a for a in qp.RSQrq], axis=1)
+        hd = np.zeros((self.nprob, N + 1, 32))
+        for k in range(N + 1):
+            n = qp.d[k].shape[1]
+            hd[:, k, :n] = qp.d[k]
+        f64 = torch.float64
+        self.BAbt = torch.from_numpy(hB).to(self.dev)
+        self.RSQrq = torch.from_numpy(hR).to(self.dev)
+        self.d = torch.from_numpy(hd).to(self.dev)
+        P = self.nprob
+        self.ux = torch.zeros((P, N + 1, 16), dtype=f64, device=self.dev)
+        self.pi = torch.zeros((P, N + 1, 16), dtype=f64, device=self.dev)
+        self.lam = torch.zeros((P, N + 1, 32), dtype=f64, device=self.dev)
+        self.t = torch.zeros((P, N + 1, 32), dtype=f64, device=self.dev)
+        self.Pb = torch.zeros((P, N + 1, 16), dtype=f64, device=self.dev)
+        self.wsd = int(L.hpmpc_mi355x_ws_doubles(self.plan))
+        self.ws = torch.zeros((P, self.wsd), dtype=f64, device=self.dev)
+        self.kk = torch.zeros(P, dtype=torch.int32, device=self.dev)
+        self.ret = torch.zeros(P, dtype=torch.int32, device=self.dev)
+        self.stat = torch.zeros((P, 5 * k_max), dtype=f64, device=self.dev)
+
+    def __del__(self):
+        try:
+            if getattr(self, "plan", None):
+                lib().hpmpc_mi355x_plan_destroy(self.plan)
+        except Exception:
+            pass
+
+    def _stream(self):
+        return self.torch.cuda.current_stream(self.dev).cuda_stream
+
+    def ipm(self, *, mu0=2.0, mu_tol=1e-12, alpha_min=1e-8, warm_start=0, compute_mult=1, p0=0, count=None):
+        """Batched d_ip2_res_mpc_hard_tv (asynchronous on torch's current stream)."""
+        count = self.nprob - p0 if count is None else count
+        rc = lib().hpmpc_mi355x_ipm_batch(
+            self.plan, C.byref(self.layout), self.nprob, p0, count, self.BAbt.data_ptr(), self.RSQrq.data_ptr(),
+            self.d.data_ptr(), self.ux.data_ptr(), self.pi.data_ptr(), self.lam.data_ptr(), self.t.data_ptr(),
+            self.ws.data_ptr(), self.k_max, mu0, mu_tol, alpha_min, warm_start, compute_mult, self.kk.data_ptr(),
+            self.ret.data_ptr(), self.stat.data_ptr(), self._stream())
+        if rc != 0:
+            raise RuntimeError(f"hpmpc_mi355x_ipm_batch failed ({rc})")
+
+    def ric_sv(self, *, compute_pi=1, compute_Pb=0, p0=0, count=None):
+        """Batched d_back_ric_rec_sv_tv_res (nb = ng = 0, no update rows): factor into ws."""
+        count = self.nprob - p0 if count is None else count
+        rc = lib().hpmpc_mi355x_ric_sv_batch(
+            self.plan, C.byref(self.layout), self.nprob, p0, count, self.BAbt.data_ptr(), self.RSQrq.data_ptr(),
+            self.ux.data_ptr(), self.pi.data_ptr(), self.ws.data_ptr(), compute_pi, compute_Pb,
+            self.Pb.data_ptr(), self._stream())
+        if rc != 0:
+            raise RuntimeError(f"hpmpc_mi355x_ric_sv_batch failed ({rc})")
+
+    def ric_trf(self, *, p0=0, count=None):
+        """Batched d_back_ric_rec_trf_tv_res (nb = ng = 0): factor into ws."""
+        count = self.nprob - p0 if count is None else count
+        rc = lib().hpmpc_mi355x_ric_trf_batch(self.plan, C.byref(self.layout), self.nprob, p0, count,
+                                              self.BAbt.data_ptr(), self.RSQrq.data_ptr(), self.ws.data_ptr(),
+                                              self._stream())
+        if rc != 0:
+            raise RuntimeError(f"hpmpc_mi355x_ric_trf_batch failed ({rc})")
+
+    def ric_trs(self, b, q, *, compute_pi=1, compute_Pb=1, p0=0, count=None):
+        """Batched d_back_ric_rec_trs_tv_res with the factor left in ws by ric_sv."""
+        count = self.nprob - p0 if count is None else count
+        rc = lib().hpmpc_mi355x_ric_trs_batch(
+            self.plan, C.byref(self.layout), self.nprob, p0, count, self.BAbt.data_ptr(), self.RSQrq.data_ptr(),
+            b.data_ptr(), q.data_ptr(), self.ux.data_ptr(), self.pi.data_ptr(), self.ws.data_ptr(), compute_pi,
+            compute_Pb, self.Pb.data_ptr(), self._stream())
+        if rc != 0:
+            raise RuntimeError(f"hpmpc_mi355x_ric_trs_batch failed ({rc})")
+
+
+def algorithmic_bytes_per_ip_iter(qp: OCPQP) -> float:
+    """Algorithmic HBM bytes of one residual-based IP iteration of one problem:
+    sv = BAbt + lower(RSQrq)+row read, L lower+row+inv_diag written, ux/pi written;
+    trs = L + BAbt re-read, rhs (q, b) in, (ux, pi) out; res = lower(RSQrq) + BAbt re-read, ux/pi in,
+    r_q/r_b out; IPM box vectors 24 doubles per box."""
+    tot = 0
+    N = qp.N
+    for k in range(N + 1):
+        nux = qp.nux(k)
+        nx1 = int(qp.nx[k + 1]) if k < N else 0
+        T = nux * (nux + 1) // 2
+        babt = (nux + 1) * nx1
+        rsq = T + nux
+        L = T + 2 * nux
+        sv = babt + rsq + L + nux + nx1
+        trs = L + babt + (nux + nx1) + (nux + nx1)
+        res = rsq + babt + (nux + nx1) + (nux + nx1)
+        tot += sv + trs + res + 24 * int(qp.nb[k])
+    return 8.0 * tot
+
+
+def algorithmic_bytes_per_sv(qp: OCPQP) -> float:
+    """8 N [(nux+1)nx' + (T+nux) + (T+2nux) + nux + nx'] (sum over stages)."""
+    tot = 0
+    N = qp.N
+    for k in range(N + 1):
+        nux = qp.nux(k)
+        nx1 = int(qp.nx[k + 1]) if k < N else 0
+        T = nux * (nux + 1) // 2
+        tot += (nux + 1) * nx1 + (T + nux) + (T + 2 * nux) + nux + nx1
+    return 8.0 * tot
+
+
+def flops_sv(N, nx, nu):
+    """Reference flop count of one sv (test_problems/test_d_ric_mpc.c:578-590), compute_pi included."""
+    return ((1 / 3) * nx ** 3 + 1.5 * nx ** 2) + N * ((7 / 3) * nx ** 3 + 4 * nx ** 2 * nu + 2 * nx * nu ** 2 +
+                                                    (1 / 3) * nu ** 3 + 6.5 * nx ** 2 + 9 * nx * nu + 2.5 * nu ** 2) \
+        - (nx * (nx + nu) + (1 / 3) * nx ** 3 + 1.5 * nx ** 2) + N * 2 * nx ** 2
+
+
+def flops_ip_iter(N, nx, nu):
+    trs = N * (6 * nx ** 2 + 8 * nx * nu + 2 * nu ** 2) + N * 2 * nx ** 2
+    res = N * (2 * (nx + nu) ** 2 + 4 * (nx + nu) * nx)
+    return flops_sv(N, nx, nu) + trs + res

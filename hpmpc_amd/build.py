@@ -1,0 +1,68 @@
+"""Build recipes for the in-tree native artefacts (no JIT cache: the .so files travel with the repo).
+
+* hpmpc_amd/lib/libhpmpc_mi355x.so -- HIP kernels for gfx950 + the reference-named C ABI (product)
+* oracle/liboracle.so              -- clean-room CPU restatement (test infrastructure)
+* oracle/_ref/libhpmpc_ref.so      -- the real reference c99 path (only when /root/reference exists)
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "hpmpc_amd", "csrc")
+LIBDIR = os.path.join(ROOT, "hpmpc_amd", "lib")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("HPMPC_ARCH", "gfx950")
+SOURCES = ["hpmpc_kernels.hip", "hpmpc_capi.cpp"]
+HEADERS = ["hk_prims.h", "hk_riccati.h", "hk_ipm.h", "hpmpc_kargs.h"]
+
+
+def _newer(out, deps):
+    if not os.path.exists(out):
+        return False
+    t = os.path.getmtime(out)
+    return all(os.path.getmtime(d) <= t for d in deps)
+
+
+def build_hip(force: bool = False, verbose: bool = False) -> str:
+    os.makedirs(LIBDIR, exist_ok=True)
+    out = os.path.join(LIBDIR, "libhpmpc_mi355x.so")
+    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [os.path.join(ROOT, "include", "hpmpc_mi355x.h")]
+    if not force and _newer(out, deps):
+        return out
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
+           "-Wno-unused-function"] + [os.path.join(CSRC, s) for s in SOURCES] + ["-o", out]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    return out
+
+
+def build_stamps(verbose: bool = False) -> str:
+    """Diagnostic variant with s_memtime stamps (tools/stamps.py); never loaded by the product."""
+    os.makedirs(LIBDIR, exist_ok=True)
+    out = os.path.join(LIBDIR, "libhpmpc_mi355x_stamps.so")
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-DHK_STAMPS",
+           "-Wno-unused-function"] + [os.path.join(CSRC, s) for s in SOURCES] + ["-o", out]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    return out
+
+
+def build_oracle(force: bool = False) -> None:
+    odir = os.path.join(ROOT, "oracle")
+    targets = ["oracle"]
+    if os.path.isdir(os.environ.get("HPMPC_REF", "/root/reference")):
+        targets.append("ref")
+    subprocess.run(["make", "-s", "-C", odir] + (["-B"] if force else []) + targets, check=True)
+
+
+def build_all(force: bool = False, verbose: bool = False) -> None:
+    build_hip(force=force, verbose=verbose)
+    build_oracle(force=force)
+
+
+if __name__ == "__main__":
+    build_all(force=True, verbose=True)

@@ -13,6 +13,25 @@
 
 namespace hk {
 
+// Diagnostic build only (-DHK_STAMPS): s_memtime stamps of one (problem, stage) into a debug buffer.
+#ifdef HK_STAMPS
+__device__ unsigned long long* g_dbg;
+__device__ int g_dbg_stage;
+#define HK_STAMP(slot, k)                                                                  \
+    do {                                                                                   \
+        unsigned long long t_;                                                             \
+        __builtin_amdgcn_sched_barrier(0);                                                 \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");         \
+        __builtin_amdgcn_sched_barrier(0);                                                 \
+        if (g_dbg && blockIdx.x == 0 && (k) == g_dbg_stage && (threadIdx.x & 63) == 0)     \
+            g_dbg[slot] = t_;                                                              \
+    } while (0)
+#else
+#define HK_STAMP(slot, k) \
+    do {                  \
+    } while (0)
+#endif
+
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
@@ -113,6 +132,23 @@ __device__ __forceinline__ void chol_pivot(double d, double &s, double &inv) {
     y = fma(y, e, y);
     s = ok ? dd * y : 0.0;
     inv = ok ? y : 0.0;
+}
+
+// Raw-buffer global access.  Masked lanes use an out-of-range offset: the hardware range check
+// returns 0 for the load and drops the store, so no exec-masked branch is emitted around the memory
+// op and the vector-memory counter stays exact (hipcc can then wait with a counted vmcnt instead of
+// draining every prefetch).  `base` must be wave-uniform; idx is per lane (doubles).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7FFFFFF0, 0x00020000);
+}
+__device__ __forceinline__ double gld(const double* base, int idx, bool ok = true) {
+    const int off = ok ? idx * 8 : (int)0xFFFFFFF0;
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rsrc(base), off, 0, 0));
+}
+__device__ __forceinline__ void gst(double* base, int idx, double v, bool ok = true) {
+    const int off = ok ? idx * 8 : (int)0xFFFFFFF0;
+    typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), rsrc(base), off, 0, 0);
 }
 
 __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {

@@ -33,6 +33,10 @@ constexpr int FSTRIDE = 288;  // factor doubles per stage: 4 regs x 64 lanes + l
 constexpr int V16 = 16;       // per-stage stride of tile/state vectors
 constexpr int V32 = 32;       // per-stage stride of constraint vectors ([lb | pad | ub | pad])
 
+__device__ __forceinline__ bool tile_active(int t, int nu, int nx, int xo) {
+    return t < nu || (t >= xo && t < xo + nx);
+}
+
 __device__ __forceinline__ int tile_var(int t, int nu, int nx, int xo) {
     return t < nu ? t : ((t >= xo && t < xo + nx) ? nu + (t - xo) : -1);
 }
@@ -40,6 +44,13 @@ __device__ __forceinline__ int tile_var(int t, int nu, int nx, int xo) {
 __device__ __forceinline__ double lib4_at(const double* A, int sd, int i, int j) {
     return A[(i >> 2) * 4 * sd + (i & 3) + 4 * j];
 }
+
+__device__ __forceinline__ int lib4_idx(int sd, int i, int j) { return (i >> 2) * 4 * sd + (i & 3) + 4 * j; }
+
+// Unconditional load + select: every lane issues the load (at a clamped, valid address), so the
+// number of outstanding vector-memory ops is the same on every path and hipcc can wait with a
+// counted s_waitcnt vmcnt(N) instead of draining the whole prefetch queue.
+__device__ __forceinline__ double ldsel(const double* p, int idx, bool ok) { return gld(p, idx, ok); }
 
 // LDS scratch for col->row layout conversion: 16 doubles per wave.
 struct Scratch {
@@ -59,81 +70,82 @@ __device__ __forceinline__ void col2row(Scratch* sm, double vc, double vr[4]) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// Stage Cholesky with the augmented row.  In: M (tile, full symmetric), ml (aug row, col layout).
-// Out: S = lower(L) + strict_upper(L') (symmetric storage: row p of S == column p of L),
-//      lc / lr : aug row l in col / row layout, invd : inverse diagonal (col layout).
-// Pivots outside [0,nu) U [xo, xo+nx) are skipped (zero padding, inv_diag = 0 as the clamp gives).
+// Stage Cholesky with the augmented row, blocked by 4 (one tile register per block row).
+// In : M (tile, full symmetric), ml (aug row, col layout).
+// Out: M = S = lower(L) + strict_upper(L') (symmetric storage: row p of S == column p of L),
+//      ml = aug row l (col layout), lr = l in row layout, invd = inverse diagonal (col layout).
+// Block b holds pivots 4b..4b+3 in register b (row group q = pivot 4b+q).  Inside a block the four
+// pivots only touch register b (row-group broadcast + readlane); the rank-4 trailing update of the
+// whole tile is ONE v_mfma_f64_16x16x4_f64 whose A and B fragments are register b itself (upper
+// storage of the panel), and the lower triangle is restored at the end by an identity-MFMA
+// transpose.  Pivots outside [0,nu) U [xo, xo+nx) are skipped (zero padding, inv_diag = 0).
+// Pivot clamp d > 1e-15 as in kernel_dpotrf_c99_lib4.c:555-640.
 // ------------------------------------------------------------------------------------------------
+template <int Q>
+__device__ __forceinline__ double rg_bcast(double x) { return rowgroup_bcast<Q>(x); }
+
 template <bool AUG>
-__device__ __forceinline__ void stage_chol(double M[4], double& ml, double lr[4], double& invd, int nu, int nx,
-                                           int xo) {
+__device__ __forceinline__ void stage_chol(d4& M, double& ml, double lr[4], double& invd, int nu, int nx, int xo,
+                                           int kdbg = -1) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
     invd = 0.0;
 #pragma unroll
     for (int r = 0; r < 4; r++) lr[r] = 0.0;
 #pragma unroll
-    for (int p = 0; p < 16; p++) {
-        const bool act = (p < nu) || (p >= xo && p < xo + nx);
-        if (!act) continue;  // wave-uniform
-        const int rp = p >> 2, gp = p & 3;
-        double d;
-        switch (rp) {  // p is a compile-time constant after unrolling
-            case 0: d = readlane(M[0], gp * 16 + p); break;
-            case 1: d = readlane(M[1], gp * 16 + p); break;
-            case 2: d = readlane(M[2], gp * 16 + p); break;
-            default: d = readlane(M[3], gp * 16 + p); break;
-        }
-        double s, inv;
-        chol_pivot(d, s, inv);
-        // column p in row layout: L[g+4r][p] = M[g+4r][p] * inv   (DPP row_newbcast:p)
-        double cr[4];
+    for (int b = 0; b < 4; b++) {
+        const bool any = (4 * b < nu) || (4 * b + 3 >= xo && 4 * b < xo + nx);
+        if (!any) continue;  // wave-uniform
+        double R = M[b];
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
-            double v;
-            switch (p) {
-#define HK_CASE(P) \
-    case P: v = row_bcast<P>(M[r]); break;
-                HK_CASE(0) HK_CASE(1) HK_CASE(2) HK_CASE(3) HK_CASE(4) HK_CASE(5) HK_CASE(6) HK_CASE(7)
-                HK_CASE(8) HK_CASE(9) HK_CASE(10) HK_CASE(11) HK_CASE(12) HK_CASE(13) HK_CASE(14)
-                default: v = row_bcast<15>(M[r]); break;
-#undef HK_CASE
+        for (int q = 0; q < 4; q++) {
+            const int p = 4 * b + q;
+            if (!tile_active(p, nu, nx, xo)) continue;  // wave-uniform
+            const double d = readlane(R, q * 16 + p);
+            double s, inv;
+            chol_pivot(d, s, inv);
+            // row q of the block (= column p of L) broadcast to every row group: colc = L[c][p], c > p
+            double rq;
+            switch (q) {
+                case 0: rq = rg_bcast<0>(R); break;
+                case 1: rq = rg_bcast<1>(R); break;
+                case 2: rq = rg_bcast<2>(R); break;
+                default: rq = rg_bcast<3>(R); break;
             }
-            cr[r] = (g + 4 * r > p) ? v * inv : 0.0;
-        }
-        // column p in col layout: L[c][p] = M[p][c] * inv   (row p broadcast from row group gp)
-        double mrow;
-        {
-            double src = (rp == 0) ? M[0] : (rp == 1) ? M[1] : (rp == 2) ? M[2] : M[3];
-            switch (gp) {
-                case 0: mrow = rowgroup_bcast<0>(src); break;
-                case 1: mrow = rowgroup_bcast<1>(src); break;
-                case 2: mrow = rowgroup_bcast<2>(src); break;
-                default: mrow = rowgroup_bcast<3>(src); break;
+            const double colc = (c > p) ? rq * inv : 0.0;
+            // remaining rows of the block: R[4b+g][c] -= L[4b+g][p] * L[c][p]   (g > q)
+            double lg = 0.0;
+            if (q < 3) {
+                const double l1 = readlane(colc, p + 1);
+                const double l2 = (q < 2) ? readlane(colc, p + 2) : 0.0;
+                const double l3 = (q < 1) ? readlane(colc, p + 3) : 0.0;
+                lg = (g == q + 1) ? l1 : (g == q + 2) ? l2 : (g == q + 3) ? l3 : 0.0;
             }
+            double Rn = R - lg * colc;
+            if (g == q) Rn = (c > p) ? colc : ((c == p) ? s : R);
+            R = Rn;
+            if (AUG) {
+                const double lp = readlane(ml, p) * inv;  // l_p = m_last[p] / L[p][p]
+                ml = (c == p) ? lp : ((c > p) ? ml - lp * colc : ml);
+                if (g == q) lr[b] = lp;
+            }
+            if (c == p) invd = inv;
         }
-        const double cc = (c > p) ? mrow * inv : 0.0;
-        // trailing update (both triangles) + write column p and row p (= column p, symmetric storage)
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const int row = g + 4 * r;
-            double m = M[r] - cr[r] * cc;
-            if (c == p) m = (row > p) ? cr[r] : (row == p ? s : M[r]);
-            if (row == p && c > p) m = cc;
-            M[r] = m;
+        HK_STAMP(16 + 2 * b, kdbg);
+        M[b] = R;
+        // rank-4 trailing update: M -= A A'  with A[i][kk] = L[i][4b+kk] for i > 4b+3 (panel rows)
+        if (4 * b + 4 < 16) {
+            const double a = (c > 4 * b + 3) ? R : 0.0;
+            M = mfma(-a, a, M);
         }
-        if (AUG) {
-            const double lp = readlane(ml, p) * inv;  // l_p = m_last[p] / L[p][p]
-            ml = (c == p) ? lp : ((c > p) ? ml - lp * cc : ml);
-#pragma unroll
-            for (int r = 0; r < 4; r++)
-                if (r == rp) lr[r] = (g == gp) ? lp : lr[r];
-        }
-        if (c == p) invd = inv;
+        HK_STAMP(17 + 2 * b, kdbg);
     }
-    // rows/cols that were never pivoted (padding) are zero already; strictly-upper part of inactive
-    // rows is zero too.
+    // lower triangle <- transpose of the upper storage:  T = S' via MFMA with an identity B operand
+    d4 T = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int r = 0; r < 4; r++) T = mfma(M[r], (c == 4 * r + g) ? 1.0 : 0.0, T);
+#pragma unroll
+    for (int r = 0; r < 4; r++) M[r] = (g + 4 * r > c) ? T[r] : M[r];
 }
-
 
 // ------------------------------------------------------------------------------------------------
 // Per-problem views used by the stage passes.
@@ -147,10 +159,28 @@ struct RicIO {
     double* F;                    // factor store (N+1)*FSTRIDE (private layout)
 };
 
-__device__ __forceinline__ StageInfo load_stage(const StageInfo* st, int k) { return st[k]; }
-
-__device__ __forceinline__ bool tile_active(int t, int nu, int nx, int xo) {
-    return t < nu || (t >= xo && t < xo + nx);
+// Stage record from the LDS table, forced into SGPRs (readfirstlane) so that every address derived
+// from it is provably wave-uniform (otherwise hipcc wraps each buffer op in a waterfall loop).
+__device__ __forceinline__ StageInfo load_stage(const StageInfo* st, int k) {
+    const StageInfo v = st[k];
+    StageInfo u;
+    u.nu = __builtin_amdgcn_readfirstlane(v.nu);
+    u.nx = __builtin_amdgcn_readfirstlane(v.nx);
+    u.nb = __builtin_amdgcn_readfirstlane(v.nb);
+    u.ng = __builtin_amdgcn_readfirstlane(v.ng);
+    u.xo = __builtin_amdgcn_readfirstlane(v.xo);
+    u.nx1 = __builtin_amdgcn_readfirstlane(v.nx1);
+    u.nu1 = __builtin_amdgcn_readfirstlane(v.nu1);
+    u.xo1 = __builtin_amdgcn_readfirstlane(v.xo1);
+    u.sdB = __builtin_amdgcn_readfirstlane(v.sdB);
+    u.sdR = __builtin_amdgcn_readfirstlane(v.sdR);
+    u.oB = __builtin_amdgcn_readfirstlane(v.oB);
+    u.oR = __builtin_amdgcn_readfirstlane(v.oR);
+    u.oD = __builtin_amdgcn_readfirstlane(v.oD);
+    u.pnb = __builtin_amdgcn_readfirstlane(v.pnb);
+    u.r0 = 0;
+    u.r1 = 0;
+    return u;
 }
 
 // lower / upper part of the symmetric factor storage S (lane (g,c), reg r = S[g+4r][c])
@@ -162,6 +192,55 @@ __device__ __forceinline__ void load_factor(const double* Fk, d4& S, double& lc,
     for (int r = 0; r < 4; r++) S[r] = Fk[r * 64 + l];
     lc = Fk[256 + c];
     invd = Fk[272 + c];
+}
+
+// ------------------------------------------------------------------------------------------------
+// Stage-data fragments.  Every pass over the stages issues the HBM loads of the NEXT stage (into
+// registers) before it computes the current one, so the dependent recursion never waits on memory.
+// ------------------------------------------------------------------------------------------------
+struct BwdFrag {
+    d4 Mi;         // RSQrq tile (mirrored lower part), tile coords of stage k
+    double mlq;    // augmented-row source: q (update_q) or the RSQrq last row
+    double dq;     // box Hessian term on this lane's diagonal slot (Qx), 0 if none
+    double qxv;    // box gradient term (qx), 0 if none
+    d4 bop;        // MFMA B operand per K-chunk: BAbt_k[var(c)][4kc+g-xo1]
+    d4 brow;       // b_k in row layout over the stage-(k+1) tile rows
+};
+
+template <bool AUG>
+__device__ __forceinline__ void bwd_fetch(const RicIO& io, const StageInfo& si, int k, int update_b,
+                                          const double* bsrc, int update_q, const double* qsrc, int use_box,
+                                          const double* Qx, const double* qx, BwdFrag& f) {
+    const int l = lane_id(), g = l >> 4, c = l & 15;
+    const int nu = si.nu, nx = si.nx, xo = si.xo, nux = nu + nx;
+    const double* R = io.RSQ + si.oR;
+    const int vc = tile_var(c, nu, nx, xo);
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int vi = tile_var(g + 4 * r, nu, nx, xo);
+        const int hi = vi > vc ? vi : vc, lo = vi > vc ? vc : vi;
+        f.Mi[r] = ldsel(R, lib4_idx(si.sdR, hi, lo), vi >= 0 && vc >= 0);
+    }
+    f.mlq = 0.0;
+    if (AUG) {
+        const double* qp = update_q ? qsrc + k * V16 : R;
+        const int qi = update_q ? vc : lib4_idx(si.sdR, nux, vc);
+        f.mlq = ldsel(qp, qi, vc >= 0);
+    }
+    const int slot = io.tileslot[k * 16 + c];
+    const bool bx = use_box && slot >= 0;
+    f.dq = ldsel(use_box ? Qx : R, k * V16 + slot, bx);
+    f.qxv = AUG ? ldsel(use_box ? qx : R, k * V16 + slot, bx) : 0.0;
+    const int nx1 = si.nx1, xo1 = si.xo1;
+    const double* Bk = io.BAbt + si.oB;
+    const double* bp = update_b ? bsrc + k * V16 : Bk;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int s = 4 * r + g - xo1;
+        const bool ok = (k < io.N) && s >= 0 && s < nx1;
+        f.bop[r] = ldsel(Bk, lib4_idx(si.sdB, vc, s), ok && vc >= 0);
+        f.brow[r] = AUG ? ldsel(bp, update_b ? s : lib4_idx(si.sdB, nux, s), ok) : 0.0;
+    }
 }
 
 // Backward Riccati recursion (sv when AUG, trf otherwise), d_back_ric_rec.c:186-335 / :447-558.
@@ -176,42 +255,31 @@ __device__ void ric_backward(const RicIO& io, Scratch* sm, int update_b, const d
     const int l = lane_id(), g = l >> 4, c = l & 15;
     d4 S = {0.0, 0.0, 0.0, 0.0};
     double lr_prev[4] = {0.0, 0.0, 0.0, 0.0};
+    StageInfo si = load_stage(io.st, io.N);
+    BwdFrag cur;
+    bwd_fetch<AUG>(io, si, io.N, update_b, bsrc, update_q, qsrc, use_box, Qx, qx, cur);
     for (int k = io.N; k >= 0; k--) {
-        const StageInfo si = load_stage(io.st, k);
-        const int nu = si.nu, nx = si.nx, xo = si.xo, nux = nu + nx;
-        const double* R = io.RSQ + si.oR;
-        const int vc = tile_var(c, nu, nx, xo);
-        // M = lower(RSQrq) mirrored to a full symmetric tile
-        d4 M;
+        HK_STAMP(0, k);
+        const int kn = k > 0 ? k - 1 : 0;  // unconditional prefetch (stage 0 re-read on the last pass)
+        const StageInfo sn = load_stage(io.st, kn);
+        BwdFrag nxt;
+        bwd_fetch<AUG>(io, sn, kn, update_b, bsrc, update_q, qsrc, use_box, Qx, qx, nxt);
+        HK_STAMP(1, k);
+        const int nu = si.nu, nx = si.nx, xo = si.xo;
+        d4 M = cur.Mi;
+        double ml = cur.mlq + cur.qxv;  // update_q row (or RSQrq row) + drowad qx
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const int vi = tile_var(g + 4 * r, nu, nx, xo);
-            M[r] = (vi >= 0 && vc >= 0) ? lib4_at(R, si.sdR, vi > vc ? vi : vc, vi > vc ? vc : vi) : 0.0;
-        }
-        double ml = 0.0;
-        if (AUG && vc >= 0) ml = update_q ? qsrc[k * V16 + vc] : lib4_at(R, si.sdR, nux, vc);
-        if (use_box && si.nb > 0) {
-            const int slot = io.tileslot[k * 16 + c];
-            if (slot >= 0) {
-                const double dq = Qx[k * V16 + slot];
-#pragma unroll
-                for (int r = 0; r < 4; r++)
-                    if (g + 4 * r == c) M[r] += dq;  // ddiaadin: diag = bd + Qx
-                if (AUG) ml += qx[k * V16 + slot];   // drowad: aug row += qx
-            }
-        }
+        for (int r = 0; r < 4; r++)
+            if (g + 4 * r == c) M[r] += cur.dq;  // ddiaadin: diag = bd + Qx
         if (k < io.N) {
             const int nx1 = si.nx1, xo1 = si.xo1;
-            const double* Bk = io.BAbt + si.oB;
             // W' = Lxx_{k+1}' BAbt_k'  (dtrmm_nt_u, d_back_ric_rec.c:262-264), rows in stage-(k+1) tile coords
             d4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
             for (int kc = 0; kc < 4; kc++) {
                 if (4 * kc + 3 < xo1 || 4 * kc >= xo1 + nx1) continue;  // uniform
-                const int qt = 4 * kc + g, s = qt - xo1;
-                const double bop = (vc >= 0 && s >= 0 && s < nx1) ? lib4_at(Bk, si.sdB, vc, s) : 0.0;
-                const double aop = (c >= xo1 && qt >= c) ? S[kc] : 0.0;
-                acc = mfma(aop, bop, acc);
+                const double aop = (c >= xo1 && 4 * kc + g >= c) ? S[kc] : 0.0;
+                acc = mfma(aop, cur.bop[kc], acc);
             }
             // M += W W'  (dsyrk part of dsyrk_dpotrf_lib, :325)
 #pragma unroll
@@ -220,15 +288,10 @@ __device__ void ric_backward(const RicIO& io, Scratch* sm, int update_b, const d
                 M = mfma(acc[r], acc[r], M);
             }
             if (AUG) {
-                // v = Lxx' b (col layout, stage k+1 tile), b from the BAbt augmented row or update_b
+                // v = Lxx' b (col layout, stage k+1 tile)
                 double part = 0.0;
 #pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    const int s = g + 4 * r - xo1;
-                    double bv = 0.0;
-                    if (s >= 0 && s < nx1) bv = update_b ? bsrc[k * V16 + s] : lib4_at(Bk, si.sdB, nux, s);
-                    part += (c >= xo1 ? lowS(S, r, g, c) : 0.0) * bv;
-                }
+                for (int r = 0; r < 4; r++) part += (c >= xo1 ? lowS(S, r, g, c) : 0.0) * cur.brow[r];
                 const double vcol = xrow_sum(part);
                 double vrow[4];
                 col2row(sm, vcol, vrow);
@@ -241,7 +304,7 @@ __device__ void ric_backward(const RicIO& io, Scratch* sm, int update_b, const d
                         pp += (j <= c && j >= xo1) ? S[r] * vrow[r] : 0.0;
                     }
                     const double pb = xrow_sum(pp);
-                    if (g == 0 && c >= xo1 && c < xo1 + nx1) Pb[k * V16 + (c - xo1)] = pb;
+                    gst(Pb, k * V16 + (c - xo1), pb, g == 0 && c >= xo1 && c < xo1 + nx1);
                 }
                 // w_last = b' Lxx + l_{k+1,x}   (dgead, :276)  -> m_last += W w_last
                 double mp = 0.0;
@@ -253,20 +316,22 @@ __device__ void ric_backward(const RicIO& io, Scratch* sm, int update_b, const d
                 ml += xrow_sum(mp);
             }
         }
-        double Ml[4] = {M[0], M[1], M[2], M[3]};
+        HK_STAMP(2, k);
         double lr[4], invd;
-        stage_chol<AUG>(Ml, ml, lr, invd, nu, nx, xo);
+        stage_chol<AUG>(M, ml, lr, invd, nu, nx, xo, k);
+        HK_STAMP(3, k);
         double* Fk = io.F + (long)k * FSTRIDE;
 #pragma unroll
         for (int r = 0; r < 4; r++) {
-            S[r] = Ml[r];
-            Fk[r * 64 + l] = Ml[r];
+            S[r] = M[r];
+            gst(Fk, r * 64 + l, M[r]);
             lr_prev[r] = lr[r];
         }
-        if (g == 0) {
-            Fk[256 + c] = AUG ? ml : 0.0;
-            Fk[272 + c] = invd;
-        }
+        gst(Fk, 256 + c, AUG ? ml : 0.0, g == 0);
+        gst(Fk, 272 + c, invd, g == 0);
+        HK_STAMP(4, k);
+        si = sn;
+        cur = nxt;
     }
 }
 
@@ -323,19 +388,6 @@ __device__ __forceinline__ double solve_ln(const d4& S, double invd, double h, i
     return h;
 }
 
-// x_{k+1} = b + BAbt_k' ux_k  (dgemv_t_lib alg 1, :347-351), col layout over stage-(k+1) tile.
-__device__ __forceinline__ double gemv_t_next(const double* Bk, const StageInfo& si, const double ur[4], double bval) {
-    const int l = lane_id(), g = l >> 4, c = l & 15;
-    const int s = c - si.xo1;
-    double part = 0.0;
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-        const int vi = tile_var(g + 4 * r, si.nu, si.nx, si.xo);
-        if (vi >= 0 && s >= 0 && s < si.nx1) part += lib4_at(Bk, si.sdB, vi, s) * ur[r];
-    }
-    return bval + xrow_sum(part);
-}
-
 // pi = Lxx (Lxx' x + p)  on the next-stage factor S1 (dtrmv_u_n + dtrmv_u_t, :355-365), col layout.
 __device__ __forceinline__ double pi_from_x(Scratch* sm, const d4& S1, int xo1, const double x1row[4], double pcol) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
@@ -354,110 +406,189 @@ __device__ __forceinline__ double pi_from_x(Scratch* sm, const d4& S1, int xo1, 
     return xrow_sum(p2);
 }
 
-// Forward substitution of the sv (d_back_ric_rec.c:339-397).  ux: variable order; pi: state order.
-__device__ void ric_forward_sv(const RicIO& io, Scratch* sm, int update_b, const double* bsrc, double* ux,
-                               int compute_pi, double* pi) {
-    const int l = lane_id(), g = l >> 4, c = l & 15;
-    double xcol = 0.0;  // x_k in col layout (stage-k tile coords)
+// Forward-pass fragment of stage k: its factor, the BAbt_k' gemv operand and b_k.
+struct FwdFrag {
     d4 S;
     double lc, invd;
-    load_factor(io.F, S, lc, invd);
+    d4 bt;       // bt[r] = BAbt_k[var(g+4r)][c - xo1]
+    double bval; // b_k[c - xo1]
+    double hc;   // trs: backward vector hux_k[var(c)]
+    double pk;   // trs: p_{k+1} = hux_{k+1}[x part] (col layout over stage-(k+1) tile)
+};
+
+// mode 0: sv (b from update_b source or the BAbt row); mode 1: trs (b from hb or the BAbt row, plus hc/pk)
+template <int MODE>
+__device__ __forceinline__ void fwd_fetch(const RicIO& io, int k, const double* bsrc, int use_bsrc,
+                                          const double* ux, int compute_pi, FwdFrag& f) {
+    const int l = lane_id(), g = l >> 4, c = l & 15;
+    const double* Fk = io.F + (long)k * FSTRIDE;
+#pragma unroll
+    for (int r = 0; r < 4; r++) f.S[r] = gld(Fk, r * 64 + l);
+    f.lc = gld(Fk, 256 + c);
+    f.invd = gld(Fk, 272 + c);
+    const int kk = k < io.N ? k : io.N - 1;  // stage N has no BAbt block: loads clamped, values masked
+    const bool live = k < io.N;
+    const StageInfo si = load_stage(io.st, kk);
+    const double* Bk = io.BAbt + si.oB;
+    const int s = c - si.xo1;
+    const bool ok = live && s >= 0 && s < si.nx1;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int vi = tile_var(g + 4 * r, si.nu, si.nx, si.xo);
+        f.bt[r] = ldsel(Bk, lib4_idx(si.sdB, vi, s), vi >= 0 && ok);
+    }
+    f.bval = use_bsrc ? ldsel(bsrc + kk * V16, s, ok) : ldsel(Bk, lib4_idx(si.sdB, si.nu + si.nx, s), ok);
+    f.hc = 0.0;
+    f.pk = 0.0;
+    if (MODE == 1) {
+        const int vc = tile_var(c, si.nu, si.nx, si.xo);
+        f.hc = ldsel(ux + kk * V16, vc, live && vc >= 0);
+        f.pk = ldsel(ux + (kk + 1) * V16, si.nu1 + s, compute_pi && ok);
+    }
+}
+
+// Shared forward substitution (sv: rhs = -l_k ; trs: rhs = -hux_k), d_back_ric_rec.c:339-397 / :704-790.
+// ux: variable order; pi: state order.
+template <int MODE>
+__device__ void ric_forward(const RicIO& io, Scratch* sm, const double* bsrc, int use_bsrc, double* ux,
+                            int compute_pi, double* pi) {
+    const int l = lane_id(), g = l >> 4, c = l & 15;
+    double xcol = 0.0;  // x_k in col layout (stage-k tile coords)
+    FwdFrag cur, nxt;
+    fwd_fetch<MODE>(io, 0, bsrc, use_bsrc, ux, compute_pi, cur);
+    fwd_fetch<MODE>(io, 1, bsrc, use_bsrc, ux, compute_pi, nxt);
     for (int k = 0; k < io.N; k++) {
+        HK_STAMP(8, k);
+        FwdFrag nn;
+        fwd_fetch<MODE>(io, k + 2 <= io.N ? k + 2 : io.N, bsrc, use_bsrc, ux, compute_pi, nn);
         const StageInfo si = load_stage(io.st, k);
-        const int nu = si.nu, nx = si.nx, xo = si.xo, nux = nu + nx;
+        const int nu = si.nu, nx = si.nx, xo = si.xo;
         const bool all = (k == 0);
         double xrow[4];
         col2row(sm, xcol, xrow);
         double part = 0.0;
         if (!all) {
 #pragma unroll
-            for (int r = 0; r < 4; r++) part += (g + 4 * r >= xo) ? lowS(S, r, g, c) * xrow[r] : 0.0;
+            for (int r = 0; r < 4; r++) part += (g + 4 * r >= xo) ? lowS(cur.S, r, g, c) * xrow[r] : 0.0;
         }
-        const double rc = -lc - xrow_sum(part);
+        const double rhs = (MODE == 0) ? cur.lc : cur.hc;
+        const double rc = -rhs - xrow_sum(part);
         double rrow[4], ur[4];
         col2row(sm, rc, rrow);
 #pragma unroll
         for (int r = 0; r < 4; r++) ur[r] = all ? 0.0 : xrow[r];
-        solve_lt(S, invd, rrow, ur, nu, nx, xo, all);
-        // store ux_k (variable order) from row layout (lanes c == 0)
-        if (c == 0) {
+        HK_STAMP(9, k);
+        solve_lt(cur.S, cur.invd, rrow, ur, nu, nx, xo, all);
+        HK_STAMP(10, k);
 #pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const int v = tile_var(g + 4 * r, nu, nx, xo);
-                if (v >= 0) ux[k * V16 + v] = ur[r];
-            }
+        for (int r = 0; r < 4; r++) {
+            const int v = tile_var(g + 4 * r, nu, nx, xo);
+            gst(ux, k * V16 + v, ur[r], c == 0 && v >= 0);
         }
-        const double* Bk = io.BAbt + si.oB;
+        // x_{k+1} = b + BAbt_k' ux_k  (dgemv_t_lib alg 1, :347-351), col layout over stage-(k+1) tile
+        double gp = 0.0;
+#pragma unroll
+        for (int r = 0; r < 4; r++) gp += cur.bt[r] * ur[r];
         const int s = c - si.xo1;
-        double bval = 0.0;
-        if (s >= 0 && s < si.nx1) bval = update_b ? bsrc[k * V16 + s] : lib4_at(Bk, si.sdB, nux, s);
-        const double x1 = gemv_t_next(Bk, si, ur, bval);
-        xcol = (s >= 0 && s < si.nx1) ? x1 : 0.0;
-        d4 S1;
-        double lc1, invd1;
-        load_factor(io.F + (long)(k + 1) * FSTRIDE, S1, lc1, invd1);
+        const bool ok = s >= 0 && s < si.nx1;
+        const double x1 = cur.bval + xrow_sum(gp);
+        xcol = ok ? x1 : 0.0;
+        HK_STAMP(11, k);
         if (compute_pi) {
             double x1row[4];
             col2row(sm, xcol, x1row);
-            const double pv = pi_from_x(sm, S1, si.xo1, x1row, lc1);
-            if (g == 0 && s >= 0 && s < si.nx1) pi[k * V16 + s] = pv;
+            double pv;
+            if (MODE == 0)
+                pv = pi_from_x(sm, nxt.S, si.xo1, x1row, nxt.lc);  // pi_k = Lxx (Lxx' x + l_x)
+            else
+                pv = pi_from_x(sm, nxt.S, si.xo1, x1row, 0.0) + cur.pk;  // pi_k = p_{k+1} + P x
+            gst(pi, k * V16 + s, pv, g == 0 && ok);
         }
-        S = S1;
-        lc = lc1;
-        invd = invd1;
+        HK_STAMP(12, k);
+        cur = nxt;
+        nxt = nn;
     }
-    // x_N
     const StageInfo sN = load_stage(io.st, io.N);
     const int v = tile_var(c, sN.nu, sN.nx, sN.xo);
-    if (g == 0 && v >= 0) ux[io.N * V16 + v] = xcol;
+    gst(ux, io.N * V16 + v, xcol, g == 0 && v >= 0);
 }
 
-// stage gradient g_k[c] = q_k + qx at the box slots (dvecad_libsp, :612-620), col layout
-__device__ __forceinline__ double stage_grad(const RicIO& io, int k, const StageInfo& si, const double* hq,
-                                             int use_box, const double* qx) {
-    const int c = lane_id() & 15;
-    const int v = tile_var(c, si.nu, si.nx, si.xo);
-    double h = 0.0;
-    if (v >= 0) h = hq ? hq[k * V16 + v] : lib4_at(io.RSQ + si.oR, si.sdR, si.nu + si.nx, v);
-    if (use_box && si.nb > 0) {
-        const int slot = io.tileslot[k * 16 + c];
-        if (slot >= 0) h += qx[k * V16 + slot];
+__device__ __forceinline__ void ric_forward_sv(const RicIO& io, Scratch* sm, int update_b, const double* bsrc,
+                                               double* ux, int compute_pi, double* pi) {
+    ric_forward<0>(io, sm, bsrc, update_b, ux, compute_pi, pi);
+}
+
+// Backward fragment of the trs at stage k.
+struct TrsFrag {
+    d4 S;
+    double invd;
+    d4 bop;      // BAbt_k[var(c)][g+4r-xo1]
+    d4 brow;     // hb_k in row layout over stage-(k+1) tile rows (compute_Pb)
+    double h0;   // gradient g_k[c] = q + qx (col layout)
+    double pbc;  // stored Pb_k (col layout over stage-(k+1) tile) when !compute_Pb
+};
+
+__device__ __forceinline__ void trs_fetch(const RicIO& io, int k, const double* hb, const double* hq, int use_box,
+                                          const double* qx, int compute_Pb, const double* Pb, TrsFrag& f) {
+    const int l = lane_id(), g = l >> 4, c = l & 15;
+    const double* Fk = io.F + (long)k * FSTRIDE;
+#pragma unroll
+    for (int r = 0; r < 4; r++) f.S[r] = gld(Fk, r * 64 + l);
+    f.invd = gld(Fk, 272 + c);
+    const StageInfo si = load_stage(io.st, k);
+    const int nu = si.nu, nx = si.nx, xo = si.xo, nux = nu + nx;
+    const int vc = tile_var(c, nu, nx, xo);
+    const double* R = io.RSQ + si.oR;
+    double h = hq ? ldsel(hq + k * V16, vc, vc >= 0) : ldsel(R, lib4_idx(si.sdR, nux, vc), vc >= 0);
+    const int slot = io.tileslot[k * 16 + c];
+    h += ldsel(use_box ? qx : R, k * V16 + slot, use_box && slot >= 0);  // dvecad_libsp (:612-620)
+    f.h0 = h;
+    const int kb = k < io.N ? k : io.N - 1;
+    const StageInfo sb = load_stage(io.st, kb);
+    const double* Bk = io.BAbt + sb.oB;
+    const int xo1 = si.xo1, nx1 = si.nx1;
+    const double* bp = hb ? hb + kb * V16 : Bk;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int sr = g + 4 * r - xo1;
+        const bool ok = k < io.N && sr >= 0 && sr < nx1;
+        f.bop[r] = ldsel(Bk, lib4_idx(sb.sdB, vc, sr), ok && vc >= 0);
+        f.brow[r] = ldsel(bp, hb ? sr : lib4_idx(sb.sdB, nux, sr), ok && compute_Pb);
     }
-    return h;
+    const int s = c - xo1;
+    f.pbc = ldsel(Pb + kb * V16, s, !compute_Pb && k < io.N && s >= 0 && s < nx1);
 }
 
 // Riccati solve with an existing factor (d_back_ric_rec.c:564-791).
-// hb: state order, hq: variable order, qx: slot order; ux (variable order) doubles as the backward
-// work vector exactly like hux in the reference.
+// hb: state order, hq: variable order (null: the BAbt / RSQrq augmented rows), qx: slot order;
+// ux (variable order) doubles as the backward work vector exactly like hux in the reference.
 __device__ void ric_trs(const RicIO& io, Scratch* sm, const double* hb, const double* hq, int use_box,
                         const double* qx, double* ux, int compute_pi, double* pi, int compute_Pb, double* Pb) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
     // ---- backward
-    StageInfo sn = load_stage(io.st, io.N);
-    double h = stage_grad(io, io.N, sn, hq, use_box, qx);
+    TrsFrag cur;
+    trs_fetch(io, io.N, hb, hq, use_box, qx, compute_Pb, Pb, cur);
     {
+        const StageInfo sn = load_stage(io.st, io.N);
         const int v = tile_var(c, sn.nu, sn.nx, sn.xo);
-        if (g == 0 && v >= 0) ux[io.N * V16 + v] = h;
+        gst(ux, io.N * V16 + v, cur.h0, g == 0 && v >= 0);
     }
-    double pcol = h;  // hux_{k+1} in col layout (stage-(k+1) tile coords)
-    d4 S1;
-    double lc1, invd1;
-    load_factor(io.F + (long)io.N * FSTRIDE, S1, lc1, invd1);
+    double pcol = cur.h0;  // hux_{k+1} in col layout (stage-(k+1) tile coords)
+    d4 S1 = cur.S;
+    TrsFrag nxt;
+    trs_fetch(io, io.N - 1, hb, hq, use_box, qx, compute_Pb, Pb, nxt);
     for (int k = io.N - 1; k >= 0; k--) {
+        cur = nxt;
+        trs_fetch(io, k > 0 ? k - 1 : 0, hb, hq, use_box, qx, compute_Pb, Pb, nxt);
         const StageInfo si = load_stage(io.st, k);
         const int nu = si.nu, nx = si.nx, xo = si.xo, xo1 = si.xo1, nx1 = si.nx1;
-        const double* Bk = io.BAbt + si.oB;
         const int vc = tile_var(c, nu, nx, xo);
-        double pbc;
         const int s = c - xo1;
+        double pbc = cur.pbc;
         if (compute_Pb) {
-            double brow[4], part = 0.0;
+            double part = 0.0;
 #pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const int sr = g + 4 * r - xo1;
-                brow[r] = (sr >= 0 && sr < nx1) ? (hb ? hb[k * V16 + sr] : lib4_at(Bk, si.sdB, nu + nx, sr)) : 0.0;
-                part += (c >= xo1 ? lowS(S1, r, g, c) : 0.0) * brow[r];
-            }
+            for (int r = 0; r < 4; r++) part += (c >= xo1 ? lowS(S1, r, g, c) : 0.0) * cur.brow[r];
             const double vcol = xrow_sum(part);
             double vrow[4];
             col2row(sm, vcol, vrow);
@@ -468,91 +599,23 @@ __device__ void ric_trs(const RicIO& io, Scratch* sm, const double* hb, const do
                 pp += (j <= c && j >= xo1) ? S1[r] * vrow[r] : 0.0;
             }
             pbc = xrow_sum(pp);
-            if (g == 0 && s >= 0 && s < nx1) Pb[k * V16 + s] = pbc;
-        } else {
-            pbc = (s >= 0 && s < nx1) ? Pb[k * V16 + s] : 0.0;
+            gst(Pb, k * V16 + s, pbc, g == 0 && s >= 0 && s < nx1);
         }
         const double wc = (s >= 0 && s < nx1) ? pbc + pcol : 0.0;
         double wrow[4];
         col2row(sm, wc, wrow);
-        h = stage_grad(io, k, si, hq, use_box, qx);
         double part = 0.0;
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const int sr = g + 4 * r - xo1;
-            if (vc >= 0 && sr >= 0 && sr < nx1) part += lib4_at(Bk, si.sdB, vc, sr) * wrow[r];
-        }
-        h += xrow_sum(part);
-        d4 S;
-        double lc, invd;
-        load_factor(io.F + (long)k * FSTRIDE, S, lc, invd);
-        h = solve_ln(S, invd, h, nu, nx, xo, k == 0);
-        if (g == 0 && vc >= 0) ux[k * V16 + vc] = h;
+        for (int r = 0; r < 4; r++) part += cur.bop[r] * wrow[r];
+        double h = cur.h0 + xrow_sum(part);
+        h = solve_ln(cur.S, cur.invd, h, nu, nx, xo, k == 0);
+        gst(ux, k * V16 + vc, h, g == 0 && vc >= 0);
         pcol = h;
-        S1 = S;
-        lc1 = lc;
-        invd1 = invd;
+        S1 = cur.S;
     }
+    __syncthreads();  // hux_k written by row group 0 is re-read by every lane below
     // ---- forward
-    double xcol = 0.0;
-    d4 S;
-    double lc, invd;
-    load_factor(io.F, S, lc, invd);
-    for (int k = 0; k < io.N; k++) {
-        const StageInfo si = load_stage(io.st, k);
-        const int nu = si.nu, nx = si.nx, xo = si.xo;
-        const bool all = (k == 0);
-        const int vc = tile_var(c, nu, nx, xo);
-        const int s = c - si.xo1;
-        const StageInfo s1 = load_stage(io.st, k + 1);
-        double pk = 0.0;
-        if (compute_pi) {
-            const int v1 = tile_var(c, s1.nu, s1.nx, s1.xo);
-            pk = (v1 >= 0 && c >= s1.xo) ? ux[(k + 1) * V16 + v1] : 0.0;  // p_{k+1} = hux_{k+1}[x]
-        }
-        const double hc = (vc >= 0) ? ux[k * V16 + vc] : 0.0;
-        double xrow[4];
-        col2row(sm, xcol, xrow);
-        double part = 0.0;
-        if (!all) {
-#pragma unroll
-            for (int r = 0; r < 4; r++) part += (g + 4 * r >= xo) ? lowS(S, r, g, c) * xrow[r] : 0.0;
-        }
-        const double rc = -hc - xrow_sum(part);
-        double rrow[4], ur[4];
-        col2row(sm, rc, rrow);
-#pragma unroll
-        for (int r = 0; r < 4; r++) ur[r] = all ? 0.0 : xrow[r];
-        solve_lt(S, invd, rrow, ur, nu, nx, xo, all);
-        if (c == 0) {
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const int v = tile_var(g + 4 * r, nu, nx, xo);
-                if (v >= 0) ux[k * V16 + v] = ur[r];
-            }
-        }
-        const double* Bk = io.BAbt + si.oB;
-        double bval = 0.0;
-        if (s >= 0 && s < si.nx1) bval = hb ? hb[k * V16 + s] : lib4_at(Bk, si.sdB, nu + nx, s);
-        const double x1 = gemv_t_next(Bk, si, ur, bval);
-        xcol = (s >= 0 && s < si.nx1) ? x1 : 0.0;
-        d4 Sn;
-        double lcn, invdn;
-        load_factor(io.F + (long)(k + 1) * FSTRIDE, Sn, lcn, invdn);
-        if (compute_pi) {
-            double x1row[4];
-            col2row(sm, xcol, x1row);
-            // pi_k = p_{k+1} + Lxx (Lxx' x_{k+1})   (:735-745)
-            const double pv = pi_from_x(sm, Sn, si.xo1, x1row, 0.0) + pk;
-            if (g == 0 && s >= 0 && s < si.nx1) pi[k * V16 + s] = pv;
-        }
-        S = Sn;
-        lc = lcn;
-        invd = invdn;
-    }
-    const StageInfo sN = load_stage(io.st, io.N);
-    const int v = tile_var(c, sN.nu, sN.nx, sN.xo);
-    if (g == 0 && v >= 0) ux[io.N * V16 + v] = xcol;
+    ric_forward<1>(io, sm, hb, hb != nullptr, ux, compute_pi, pi);
 }
 
 }  // namespace hk

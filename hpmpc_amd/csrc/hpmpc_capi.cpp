@@ -190,6 +190,10 @@ extern "C" long long hpmpc_mi355x_ws_doubles(const hpmpc_mi355x_plan* P) { retur
 
 extern "C" int hpmpc_mi355x_last_error(void) { return g_err; }
 
+// Diagnostic builds (-DHK_STAMPS) record s_memtime stamps of problem 0 into this device buffer.
+static unsigned long long* g_dbg_buf = nullptr;
+extern "C" void hpmpc_mi355x_debug_buffer(void* dev_ptr) { g_dbg_buf = (unsigned long long*)dev_ptr; }
+
 extern "C" const char* hpmpc_mi355x_version(void) {
     return "hpmpc_mi355x 0.1 gfx950 (wave-per-problem, f64 MFMA 16x16x4 stage contractions)";
 }
@@ -208,6 +212,7 @@ KArgs base_args(const hpmpc_mi355x_plan* P, int nprob, int p0) {
     a.sV16 = (long long)(P->N + 1) * V16;
     a.sV32 = (long long)(P->N + 1) * V32;
     a.sW = ws_doubles(P->N);
+    a.dbg = g_dbg_buf;
     return a;
 }
 
@@ -277,6 +282,24 @@ extern "C" int hpmpc_mi355x_ric_sv_batch(const hpmpc_mi355x_plan* plan, const hp
     int e = hk_launch(K_SV, &a, count, (hipStream_t)stream);
     if (e) {
         set_err(HPMPC_MI355X_EHIP, "hk_ric_sv launch failed");
+        return HPMPC_MI355X_EHIP;
+    }
+    return g_err = 0;
+}
+
+extern "C" int hpmpc_mi355x_ric_trf_batch(const hpmpc_mi355x_plan* plan, const hpmpc_mi355x_layout* lay, int nprob,
+                                          int p0, int count, const double* BAbt, const double* RSQrq, double* ws,
+                                          void* stream) {
+    auto* P = const_cast<hpmpc_mi355x_plan*>(plan);
+    if (!P) return g_err = HPMPC_MI355X_EUNSUPPORTED;
+    KArgs a = base_args(P, nprob, p0);
+    if (!layout_apply(P, lay, a)) return g_err;
+    a.BAbt = BAbt;
+    a.RSQ = RSQrq;
+    a.ws = ws;
+    int e = hk_launch(K_TRF, &a, count, (hipStream_t)stream);
+    if (e) {
+        set_err(HPMPC_MI355X_EHIP, "hk_ric_trf launch failed");
         return HPMPC_MI355X_EHIP;
     }
     return g_err = 0;

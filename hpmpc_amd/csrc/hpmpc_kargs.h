@@ -28,4 +28,5 @@ struct KArgs {
     int *kk, *ret;
     double* stat;    // 5*k_max per problem
     double* mu_out;  // per problem (residual kernel)
+    unsigned long long* dbg;  // diagnostic stamp buffer (HK_STAMPS builds only)
 };

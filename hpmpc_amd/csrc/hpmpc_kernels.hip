@@ -19,27 +19,72 @@ struct Ws {  // per-problem workspace carve (doubles), persistent between an IPM
 
 __device__ __forceinline__ Ws carve(double* W, int N) {
     Ws w;
-    const long n1 = N + 1;
+    const long n1 = N + 1, a = n1 * V16, b = n1 * V32;
     w.F = W;
     W += n1 * FSTRIDE;
-    double** v16[] = {&w.dux, &w.dpi, &w.Pb, &w.Qx, &w.qx, &w.res_q, &w.res_b, &w.ux_bkp, &w.pi_bkp};
-    for (double** p : v16) {
-        *p = W;
-        W += n1 * V16;
-    }
-    double** v32[] = {&w.dlam, &w.dt, &w.t_inv, &w.lamt, &w.res_d, &w.res_m, &w.t_bkp, &w.lam_bkp};
-    for (double** p : v32) {
-        *p = W;
-        W += n1 * V32;
-    }
+    w.dux = W;
+    w.dpi = W + a;
+    w.Pb = W + 2 * a;
+    w.Qx = W + 3 * a;
+    w.qx = W + 4 * a;
+    w.res_q = W + 5 * a;
+    w.res_b = W + 6 * a;
+    w.ux_bkp = W + 7 * a;
+    w.pi_bkp = W + 8 * a;
+    W += 9 * a;
+    w.dlam = W;
+    w.dt = W + b;
+    w.t_inv = W + 2 * b;
+    w.lamt = W + 3 * b;
+    w.res_d = W + 4 * b;
+    w.res_m = W + 5 * b;
+    w.t_bkp = W + 6 * b;
+    w.lam_bkp = W + 7 * b;
     return w;
 }
 
-__device__ __forceinline__ RicIO make_io(const KArgs& a, int p, double* F) {
+// Per-batch stage tables (StageInfo, tile->box slot, box slot->variable) are copied into LDS at
+// kernel start: every stage iteration reads them with ds_read (lgkmcnt), so the HBM prefetch queue
+// (vmcnt) is never drained just to learn the next stage's sizes.
+extern __shared__ __attribute__((aligned(16))) char hk_smem[];
+
+struct LdsTabs {
+    Scratch* sm;
+    const StageInfo* st;
+    const signed char* tileslot;
+    const signed char* slotvar;
+};
+
+__device__ __forceinline__ LdsTabs lds_tables(const KArgs& a) {
+    LdsTabs T;
+    T.sm = reinterpret_cast<Scratch*>(hk_smem);
+    StageInfo* st = reinterpret_cast<StageInfo*>(hk_smem + sizeof(Scratch));
+    signed char* ts = reinterpret_cast<signed char*>(st + (a.N + 1));
+    signed char* sv = ts + (a.N + 1) * 16;
+    const int l = lane_id(), n1 = a.N + 1;
+    const int* gst = reinterpret_cast<const int*>(a.st);
+    int* lst = reinterpret_cast<int*>(st);
+    for (int i = l; i < n1 * 16; i += 64) lst[i] = gst[i];
+    const int* gts = reinterpret_cast<const int*>(a.tileslot);
+    const int* gsv = reinterpret_cast<const int*>(a.slotvar);
+    int* lts = reinterpret_cast<int*>(ts);
+    int* lsv = reinterpret_cast<int*>(sv);
+    for (int i = l; i < n1 * 4; i += 64) {
+        lts[i] = gts[i];
+        lsv[i] = gsv[i];
+    }
+    __syncthreads();
+    T.st = st;
+    T.tileslot = ts;
+    T.slotvar = sv;
+    return T;
+}
+
+__device__ __forceinline__ RicIO make_io(const KArgs& a, const LdsTabs& T, int p, double* F) {
     RicIO io;
     io.N = a.N;
-    io.st = reinterpret_cast<const StageInfo*>(a.st);
-    io.tileslot = a.tileslot;
+    io.st = T.st;
+    io.tileslot = T.tileslot;
     io.BAbt = a.BAbt + (long)p * a.sB;
     io.RSQ = a.RSQ + (long)p * a.sR;
     io.F = F;
@@ -54,11 +99,12 @@ __device__ __forceinline__ void wsync() { __syncthreads(); }
 // d_back_ric_rec_sv_tv_res / _trf_ / _trs_ over a batch (one problem per workgroup)
 // ------------------------------------------------------------------------------------------------
 extern "C" __global__ __launch_bounds__(64) void hk_ric_sv(KArgs a) {
-    __shared__ Scratch sm;
+    const LdsTabs T = lds_tables(a);
+    Scratch& sm = *T.sm;
     const int p = blockIdx.x + a.p0;
     if (p >= a.nprob) return;
     double* F = a.ws + (long)p * a.sW;
-    RicIO io = make_io(a, p, F);
+    RicIO io = make_io(a, T, p, F);
     const long o16 = (long)p * a.sV16;
     const double* b = a.vb ? a.vb + o16 : nullptr;
     const double* q = a.vq ? a.vq + o16 : nullptr;
@@ -71,22 +117,24 @@ extern "C" __global__ __launch_bounds__(64) void hk_ric_sv(KArgs a) {
 }
 
 extern "C" __global__ __launch_bounds__(64) void hk_ric_trf(KArgs a) {
-    __shared__ Scratch sm;
+    const LdsTabs T = lds_tables(a);
+    Scratch& sm = *T.sm;
     const int p = blockIdx.x + a.p0;
     if (p >= a.nprob) return;
     double* F = a.ws + (long)p * a.sW;
-    RicIO io = make_io(a, p, F);
+    RicIO io = make_io(a, T, p, F);
     const long o16 = (long)p * a.sV16;
     const double* Qx = a.vQx ? a.vQx + o16 : nullptr;
     ric_backward<false>(io, &sm, 0, nullptr, 0, nullptr, a.use_box, Qx, nullptr, 0, nullptr);
 }
 
 extern "C" __global__ __launch_bounds__(64) void hk_ric_trs(KArgs a) {
-    __shared__ Scratch sm;
+    const LdsTabs T = lds_tables(a);
+    Scratch& sm = *T.sm;
     const int p = blockIdx.x + a.p0;
     if (p >= a.nprob) return;
     double* F = a.ws + (long)p * a.sW;
-    RicIO io = make_io(a, p, F);
+    RicIO io = make_io(a, T, p, F);
     const long o16 = (long)p * a.sV16;
     const double* qx = a.vqx ? a.vqx + o16 : nullptr;
     ric_trs(io, &sm, a.vb + o16, a.vq + o16, a.use_box, qx, a.ux + o16, a.compute_pi, a.pi + o16, a.compute_Pb,
@@ -94,11 +142,12 @@ extern "C" __global__ __launch_bounds__(64) void hk_ric_trs(KArgs a) {
 }
 
 extern "C" __global__ __launch_bounds__(64) void hk_res(KArgs a) {
-    __shared__ Scratch sm;
+    const LdsTabs T = lds_tables(a);
+    Scratch& sm = *T.sm;
     const int p = blockIdx.x + a.p0;
     if (p >= a.nprob) return;
-    RicIO io = make_io(a, p, nullptr);
-    BoxTab bt{a.tileslot, a.slotvar};
+    RicIO io = make_io(a, T, p, nullptr);
+    BoxTab bt{T.tileslot, T.slotvar};
     const long o16 = (long)p * a.sV16, o32 = (long)p * a.sV32;
     double* out = a.ws + (long)p * a.sW;  // [rq | rb] V16, [rd | rm] V32
     const long n1 = a.N + 1;
@@ -159,13 +208,14 @@ __device__ __forceinline__ void alpha_rule(double& al, double lam, double dlam, 
 }  // namespace
 
 extern "C" __global__ __launch_bounds__(64) void hk_ipm(KArgs a) {
-    __shared__ Scratch sm;
+    const LdsTabs T = lds_tables(a);
+    Scratch& sm = *T.sm;
     const int p = blockIdx.x + a.p0;
     if (p >= a.nprob) return;
     const int N = a.N;
     Ws w = carve(a.ws + (long)p * a.sW, N);
-    RicIO io = make_io(a, p, w.F);
-    BoxTab bt{a.tileslot, a.slotvar};
+    RicIO io = make_io(a, T, p, w.F);
+    BoxTab bt{T.tileslot, T.slotvar};
     const long o16 = (long)p * a.sV16, o32 = (long)p * a.sV32;
     double* ux = a.ux + o16;
     double* pi = a.pi + o16;
@@ -458,13 +508,14 @@ extern "C" __global__ __launch_bounds__(64) void hk_ipm(KArgs a) {
 // vb/vq hold the new b (state order) / q (variable order).
 // ------------------------------------------------------------------------------------------------
 extern "C" __global__ __launch_bounds__(64) void hk_kkt_new_rhs(KArgs a) {
-    __shared__ Scratch sm;
+    const LdsTabs T = lds_tables(a);
+    Scratch& sm = *T.sm;
     const int p = blockIdx.x + a.p0;
     if (p >= a.nprob) return;
     const int N = a.N;
     Ws w = carve(a.ws + (long)p * a.sW, N);
-    RicIO io = make_io(a, p, w.F);
-    BoxTab bt{a.tileslot, a.slotvar};
+    RicIO io = make_io(a, T, p, w.F);
+    BoxTab bt{T.tileslot, T.slotvar};
     const long o16 = (long)p * a.sV16, o32 = (long)p * a.sV32;
     double* ux = a.ux + o16;
     double* pi = a.pi + o16;
@@ -521,14 +572,23 @@ extern "C" __global__ __launch_bounds__(64) void hk_kkt_new_rhs(KArgs a) {
 // ------------------------------------------------------------------------------------------------
 extern "C" int hk_launch(int which, const KArgs* a, int count, hipStream_t stream) {
     if (count <= 0) return 0;
+#ifdef HK_STAMPS
+    if (a->dbg) {
+        unsigned long long* p = a->dbg;
+        int st = 50;
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_dbg), &p, sizeof(p));
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_stage), &st, sizeof(st));
+    }
+#endif
     dim3 grid(count), block(64);
+    const size_t lds = sizeof(Scratch) + (size_t)(a->N + 1) * (sizeof(StageInfo) + 32);
     switch (which) {
-        case 0: hipLaunchKernelGGL(hk_ric_sv, grid, block, 0, stream, *a); break;
-        case 1: hipLaunchKernelGGL(hk_ric_trf, grid, block, 0, stream, *a); break;
-        case 2: hipLaunchKernelGGL(hk_ric_trs, grid, block, 0, stream, *a); break;
-        case 3: hipLaunchKernelGGL(hk_res, grid, block, 0, stream, *a); break;
-        case 4: hipLaunchKernelGGL(hk_ipm, grid, block, 0, stream, *a); break;
-        case 5: hipLaunchKernelGGL(hk_kkt_new_rhs, grid, block, 0, stream, *a); break;
+        case 0: hipLaunchKernelGGL(hk_ric_sv, grid, block, lds, stream, *a); break;
+        case 1: hipLaunchKernelGGL(hk_ric_trf, grid, block, lds, stream, *a); break;
+        case 2: hipLaunchKernelGGL(hk_ric_trs, grid, block, lds, stream, *a); break;
+        case 3: hipLaunchKernelGGL(hk_res, grid, block, lds, stream, *a); break;
+        case 4: hipLaunchKernelGGL(hk_ipm, grid, block, lds, stream, *a); break;
+        case 5: hipLaunchKernelGGL(hk_kkt_new_rhs, grid, block, lds, stream, *a); break;
         default: return -1;
     }
     return (int)hipGetLastError();

@@ -148,12 +148,24 @@ def batch_x0(nx: int, batch: int, seed_base: int = 20261015) -> np.ndarray:
     return X
 
 
+def pack_lib4_batch(M: np.ndarray) -> np.ndarray:
+    """(..., m, n) dense -> (..., lib4_size(m, n)) lib4 buffers (vectorised pack_lib4)."""
+    m, n = M.shape[-2:]
+    sd, pm = rup(n, NCL), rup(m, BS)
+    lead = M.shape[:-2]
+    P = np.zeros(lead + (pm, sd))
+    P[..., :m, :n] = M
+    P = P.reshape(lead + (pm // BS, BS, sd))
+    return np.ascontiguousarray(np.swapaxes(P, -1, -2)).reshape(lead + (pm * sd,))
+
+
 def mass_spring_qp(N: int, nx: int, nu: int, *, boxes: bool = True, x0=None, batch: int | None = None,
                    time_variant: bool = False, seed: int = 0) -> OCPQP:
     """The reference drivers' mass-spring MPC QP (nx[0] = 0, nu[N] = 0).
 
-    ``batch`` stacks ``batch`` problems that differ in x0 (and, with ``time_variant``, in a small
-    seeded perturbation of every stage's A, B, Q so that no two stage buffers alias).
+    ``batch`` stacks ``batch`` problems that differ in x0 (problem 0 = the drivers' x0) and, with
+    ``time_variant``, in a seeded perturbation of every stage's A, B (1e-3 N(0,1)) and Q (+ G G',
+    G ~ 1e-3 N(0,1)) so that no two stage buffers alias (SURVEY.md §8d roofline accounting).
     """
     A, B = mass_spring_dynamics(nx, nu)
     b = np.full(nx, 0.1)
@@ -183,50 +195,44 @@ def mass_spring_qp(N: int, nx: int, nu: int, *, boxes: bool = True, x0=None, bat
         nux = nuk + nxk
         if k < N:
             nx1 = int(nxv[k + 1])
-            arr = np.empty((Bn, lib4_size(nux + 1, nx1)))
-            for p in range(Bn):
-                Ak, Bk = A, B
-                if time_variant:
-                    Ak = A + 1e-3 * rng.standard_normal(A.shape)
-                    Bk = B + 1e-3 * rng.standard_normal(B.shape)
-                M = np.zeros((nux + 1, nx1))
-                M[:nuk, :] = Bk.T
-                if k == 0:
-                    M[nuk, :] = Ak @ X0[p] + b  # b0 = A x0 + b  (test_d_ip_hard.c:306-322)
-                else:
-                    M[nuk:nux, :] = Ak.T
-                    M[nux, :] = b
-                arr[p] = pack_lib4(M)
-            BAbt.append(arr)
-        arr = np.empty((Bn, lib4_size(nux + 1, nux)))
-        for p in range(Bn):
-            Qk = Q[:nxk, :nxk]
-            if time_variant and nxk > 0:
-                G = 1e-3 * rng.standard_normal((nxk, nxk))
-                Qk = Q + G @ G.T
-            M = np.zeros((nux + 1, nux))
-            M[:nuk, :nuk] = R[:nuk, :nuk]
-            M[nuk:nux, nuk:nux] = Qk
-            M[nux, :nuk] = r[:nuk]
-            M[nux, nuk:nux] = q[:nxk]
-            arr[p] = pack_lib4(M)
-        RSQrq.append(arr)
+            Ak = np.broadcast_to(A, (Bn, nx, nx))
+            Bk = np.broadcast_to(B, (Bn, nx, nu))
+            if time_variant:
+                Ak = A + 1e-3 * rng.standard_normal((Bn, nx, nx))
+                Bk = B + 1e-3 * rng.standard_normal((Bn, nx, nu))
+            M = np.zeros((Bn, nux + 1, nx1))
+            M[:, :nuk, :] = np.swapaxes(Bk, 1, 2)
+            if k == 0:
+                M[:, nuk, :] = np.einsum("pij,pj->pi", Ak, X0) + b  # b0 = A x0 + b (test_d_ip_hard.c:306-322)
+            else:
+                M[:, nuk:nux, :] = np.swapaxes(Ak, 1, 2)
+                M[:, nux, :] = b
+            BAbt.append(pack_lib4_batch(M))
+        M = np.zeros((Bn, nux + 1, nux))
+        M[:, :nuk, :nuk] = R[:nuk, :nuk]
+        Qk = np.broadcast_to(Q[:nxk, :nxk], (Bn, nxk, nxk))
+        if time_variant and nxk > 0:
+            G = 1e-3 * rng.standard_normal((Bn, nxk, nxk))
+            Qk = Q[:nxk, :nxk] + G @ np.swapaxes(G, 1, 2)
+        M[:, nuk:nux, nuk:nux] = Qk
+        M[:, nux, :nuk] = r[:nuk]
+        M[:, nux, nuk:nux] = q[:nxk]
+        RSQrq.append(pack_lib4_batch(M))
         # boxes: u in [-0.5, 0.5]; first nx/2 states in [-4, 4]  (test_d_ip_hard.c:359-405)
         nbk = int(nbv[k])
         pnb = rup(nbk, BS)
         dk = np.zeros(max(2 * pnb, 1))
-        ik = np.arange(nbk, dtype=np.int32)
         for j in range(nbk):
             if j < nuk:
                 dk[j], dk[pnb + j] = -0.5, 0.5
             else:
                 dk[j], dk[pnb + j] = -4.0, 4.0
-        idxb.append(ik)
+        idxb.append(np.arange(nbk, dtype=np.int32))
         dv.append(np.broadcast_to(dk, (Bn, dk.size)).copy())
 
     qp = OCPQP(N, nxv, nuv, nbv, ngv, idxb, BAbt, RSQrq, dv, [], batch)
     if batch is None:
-        qp.BAbt = [a[0] for a in qp.BAbt]
-        qp.RSQrq = [a[0] for a in qp.RSQrq]
-        qp.d = [a[0] for a in qp.d]
+        qp.BAbt = [a[0].copy() for a in qp.BAbt]
+        qp.RSQrq = [a[0].copy() for a in qp.RSQrq]
+        qp.d = [a[0].copy() for a in qp.d]
     return qp

@@ -102,6 +102,10 @@ int hpmpc_mi355x_ric_sv_batch(const hpmpc_mi355x_plan *plan, const hpmpc_mi355x_
                               int count, const double *BAbt, const double *RSQrq, double *ux, double *pi, double *ws,
                               int compute_pi, int compute_Pb, double *Pb, void *stream);
 
+/* Batched d_back_ric_rec_trf_tv_res (factorisation only, no box terms) into ws. */
+int hpmpc_mi355x_ric_trf_batch(const hpmpc_mi355x_plan *plan, const hpmpc_mi355x_layout *lay, int nprob, int p0,
+                               int count, const double *BAbt, const double *RSQrq, double *ws, void *stream);
+
 /* Batched d_back_ric_rec_trs_tv_res re-using the factor in ws; b (16/stage, state order), q (16/stage,
  * variable order). */
 int hpmpc_mi355x_ric_trs_batch(const hpmpc_mi355x_plan *plan, const hpmpc_mi355x_layout *lay, int nprob, int p0,
