@@ -136,7 +136,8 @@ class HpmpcAPI:
         ux_, pi, lam, t = qp.alloc_solution()
         if ux is not None:
             for k in range(N + 1):
-                ux_[k][: len(ux[k])] = ux[k]
+                n = min(len(ux_[k]), len(ux[k]))
+                ux_[k][:n] = ux[k][:n]
         stat = np.zeros(5 * k_max + 5)
         kk = C.c_int(0)
         dct = qp.DCt if qp.DCt else [np.zeros(8)] * (N + 1)

@@ -1,0 +1,215 @@
+#!/usr/bin/env python3
+"""Generate the golden vectors of tests/golden/*.npz from the REAL reference c99 build.
+
+The reference (oracle/_ref/libhpmpc_ref.so, compiled from the sources under /root/reference by
+oracle/Makefile, TARGET_C99_4X4, no BLASFEO) is called through its own C entry points on
+deterministic inputs; inputs and outputs are stored as plain float64/int32 arrays (no pickles).
+This script needs the dev container (the reference source tree); the committed .npz files are what
+the tests read everywhere else.
+
+    python tests/golden/make_golden.py          # rewrites tests/golden/*.npz
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from hpmpc_amd.cabi import HpmpcAPI, bq_from_qp, load  # noqa: E402
+from hpmpc_amd.golden import save_case  # noqa: E402
+from hpmpc_amd.ocp import (BS, OCPQP, lib4_size, mass_spring_qp, pack_lib4, rup,  # noqa: E402
+                           unpack_lib4)
+
+
+def ref_api():
+    path = os.path.join(ROOT, "oracle", "_ref", "libhpmpc_ref.so")
+    return HpmpcAPI(load(path))
+
+
+def rand_vecs(rng, sizes, pad=4, scale=1.0):
+    return [np.concatenate([scale * rng.standard_normal(n), np.zeros(pad + (4 - n % 4) % 4)]) for n in sizes]
+
+
+def clamp_qp(N=10, nx=8, nu=3):
+    """Singular R and Q blocks: exercises the pivot clamp (kernel_dpotrf_c99_lib4.c:555-640)."""
+    qp = mass_spring_qp(N, nx, nu, boxes=False)
+    for k in range(N + 1):
+        nux = qp.nux(k)
+        M = unpack_lib4(qp.RSQrq[k], nux + 1, nux).copy()
+        nuk = int(qp.nu[k])
+        if nuk > 1:
+            M[1, :] = 0.0
+            M[:, 1] = 0.0
+        if k == N:
+            M[0, :] = 0.0
+            M[:, 0] = 0.0
+        qp.RSQrq[k] = pack_lib4(M)
+    return qp
+
+
+def x0_stage_qp(N=10, nx=8, nu=3):
+    """nx[0] = nx (x0 kept as a variable): stage 0 is solved over the whole nux block."""
+    base = mass_spring_qp(N, nx, nu, boxes=False)
+    qp = base.copy()
+    A = unpack_lib4(base.BAbt[1], nu + nx + 1, nx)
+    qp.nx = base.nx.copy()
+    qp.nx[0] = nx
+    qp.BAbt[0] = base.BAbt[1].copy()
+    qp.BAbt[0] = pack_lib4(A)
+    qp.RSQrq[0] = base.RSQrq[1].copy()
+    return qp
+
+
+def ng_qp(N=30, nx=8, nu=3):
+    """Terminal general constraints (ngN = nx, x_N in [-0.5, 0.5] via C = I), like the user guide's ngN example."""
+    qp = mass_spring_qp(N, nx, nu, boxes=True)
+    qp.ng = np.zeros(N + 1, dtype=np.int32)
+    qp.ng[N] = nx
+    qp.DCt = [np.zeros(8) for _ in range(N + 1)]
+    qp.DCt[N] = pack_lib4(np.eye(nx))
+    for k in range(N + 1):
+        pnb, png = qp.pnb(k), qp.png(k)
+        dk = np.zeros(2 * pnb + 2 * png)
+        dk[: 2 * pnb] = qp.d[k][: 2 * pnb]
+        if k == N:
+            dk[2 * pnb: 2 * pnb + nx] = -0.5
+            dk[2 * pnb + png: 2 * pnb + png + nx] = 0.5
+        qp.d[k] = dk
+    return qp
+
+
+def main():
+    ref = ref_api()
+    rng = np.random.default_rng(20261015)
+    out = []
+
+    # ---------------- d_back_ric_rec_sv_tv_res ----------------
+    for (N, nx, nu) in [(10, 8, 3), (30, 8, 3), (50, 8, 3), (100, 12, 4)]:
+        qp = mass_spring_qp(N, nx, nu, boxes=False)
+        ux, pi, Pb, _ = ref.ric_sv(qp.copy(), compute_pi=1, compute_Pb=1)
+        out.append(save_case(f"sv_ms_N{N}_nx{nx}_nu{nu}", "sv", qp, dict(compute_pi=1, compute_Pb=1),
+                             dict(ux=ux, pi=pi, Pb=Pb)))
+    qp = mass_spring_qp(20, 12, 4, boxes=False, batch=1, time_variant=True, seed=7).problem(0)
+    ux, pi, Pb, _ = ref.ric_sv(qp.copy(), compute_pi=1, compute_Pb=1)
+    out.append(save_case("sv_tv_N20_nx12_nu4", "sv", qp, dict(compute_pi=1, compute_Pb=1), dict(ux=ux, pi=pi, Pb=Pb)))
+
+    qp = clamp_qp()
+    ux, pi, Pb, _ = ref.ric_sv(qp.copy(), compute_pi=1, compute_Pb=1)
+    out.append(save_case("sv_clamp_N10_nx8_nu3", "sv", qp, dict(compute_pi=1, compute_Pb=1), dict(ux=ux, pi=pi, Pb=Pb)))
+
+    qp = x0_stage_qp()
+    ux, pi, Pb, _ = ref.ric_sv(qp.copy(), compute_pi=1, compute_Pb=1)
+    out.append(save_case("sv_x0_N10_nx8_nu3", "sv", qp, dict(compute_pi=1, compute_Pb=1), dict(ux=ux, pi=pi, Pb=Pb)))
+
+    # sv with update_b / update_q / box terms: also pins the in-place side effects on the caller's data
+    qp = mass_spring_qp(10, 8, 3, boxes=True)
+    N = qp.N
+    b = rand_vecs(rng, [int(qp.nx[k + 1]) for k in range(N)])
+    q = rand_vecs(rng, [qp.nux(k) for k in range(N + 1)])
+    bd = [np.concatenate([1.0 + rng.random(int(qp.nb[k])), np.zeros(8)]) for k in range(N + 1)]
+    Qx = [np.concatenate([0.5 + rng.random(int(qp.nb[k])), np.zeros(8)]) for k in range(N + 1)]
+    qx = [np.concatenate([rng.standard_normal(int(qp.nb[k])), np.zeros(8)]) for k in range(N + 1)]
+    q2 = qp.copy()
+    ux, pi, Pb, _ = ref.ric_sv(q2, update_b=1, b=b, update_q=1, q=q, bd=bd, Qx=Qx, qx=qx, compute_pi=1,
+                               compute_Pb=1)
+    out.append(save_case("sv_update_box_N10_nx8_nu3", "sv", qp,
+                         dict(compute_pi=1, compute_Pb=1, update_b=1, update_q=1),
+                         dict(ux=ux, pi=pi, Pb=Pb, BAbt_after=q2.BAbt, RSQrq_after=q2.RSQrq),
+                         extra=dict(b=b, q=q, bd=bd, Qx=Qx, qx=qx)))
+
+    # ---------------- trf + trs ----------------
+    qp = mass_spring_qp(30, 8, 3, boxes=True)
+    N = qp.N
+    b = rand_vecs(rng, [int(qp.nx[k + 1]) for k in range(N)])
+    q = rand_vecs(rng, [qp.nux(k) for k in range(N + 1)])
+    bd = [np.concatenate([1.0 + rng.random(int(qp.nb[k])), np.zeros(8)]) for k in range(N + 1)]
+    Qx = [np.concatenate([0.5 + rng.random(int(qp.nb[k])), np.zeros(8)]) for k in range(N + 1)]
+    qx = [np.concatenate([rng.standard_normal(int(qp.nb[k])), np.zeros(8)]) for k in range(N + 1)]
+    q2 = qp.copy()
+    mem = ref.ric_trf(q2, bd=bd, Qx=Qx)
+    ux, pi, Pb = ref.ric_trs(q2, mem, b=b, q=q, qx=qx, compute_pi=1, compute_Pb=1)
+    out.append(save_case("trf_trs_N30_nx8_nu3", "trf_trs", qp, dict(compute_pi=1, compute_Pb=1),
+                         dict(ux=ux, pi=pi, Pb=Pb), extra=dict(b=b, q=q, bd=bd, Qx=Qx, qx=qx)))
+
+    # ---------------- d_ip2_res_mpc_hard_tv ----------------
+    for (N, nx, nu) in [(10, 8, 3), (30, 8, 3), (100, 12, 4)]:
+        qp = mass_spring_qp(N, nx, nu, boxes=True)
+        r = ref.ipm(qp.copy(), k_max=50)
+        out.append(save_case(f"ipm_N{N}_nx{nx}_nu{nu}", "ipm", qp, dict(k_max=50, mu0=2.0, mu_tol=1e-12, alpha_min=1e-8),
+                             dict(ux=r["ux"], pi=r["pi"], lam=r["lam"], t=r["t"], stat=r["stat"], kk=r["kk"],
+                                  ret=r["ret"])))
+    bq = mass_spring_qp(30, 12, 4, boxes=True, batch=4, time_variant=True, seed=11)
+    for p in range(4):
+        qp = bq.problem(p)
+        r = ref.ipm(qp.copy(), k_max=50)
+        out.append(save_case(f"ipm_tv_N30_nx12_nu4_p{p}", "ipm", qp,
+                             dict(k_max=50, mu0=2.0, mu_tol=1e-12, alpha_min=1e-8),
+                             dict(ux=r["ux"], pi=r["pi"], lam=r["lam"], t=r["t"], stat=r["stat"], kk=r["kk"],
+                                  ret=r["ret"])))
+    # warm start
+    qp = mass_spring_qp(20, 8, 3, boxes=True)
+    ux0 = rand_vecs(rng, [qp.nux(k) for k in range(qp.N + 1)], scale=0.1)
+    r = ref.ipm(qp.copy(), k_max=50, warm_start=1, ux=ux0)
+    out.append(save_case("ipm_warm_N20_nx8_nu3", "ipm", qp,
+                         dict(k_max=50, mu0=2.0, mu_tol=1e-12, alpha_min=1e-8, warm_start=1),
+                         dict(ux=r["ux"], pi=r["pi"], lam=r["lam"], t=r["t"], stat=r["stat"], kk=r["kk"],
+                              ret=r["ret"]), extra=dict(ux0=ux0)))
+    # no constraints: mu_scal == 0 -> one sv (d_ip2_res_hard.c:428-450)
+    qp = mass_spring_qp(20, 8, 3, boxes=False)
+    r = ref.ipm(qp.copy(), k_max=50)
+    out.append(save_case("ipm_noconstr_N20_nx8_nu3", "ipm", qp, dict(k_max=50, mu0=2.0, mu_tol=1e-12, alpha_min=1e-8),
+                         dict(ux=r["ux"], pi=r["pi"], lam=r["lam"], t=r["t"], stat=r["stat"], kk=r["kk"],
+                              ret=r["ret"])))
+    # k_max reached (ret 1)
+    qp = mass_spring_qp(30, 8, 3, boxes=True)
+    r = ref.ipm(qp.copy(), k_max=4)
+    out.append(save_case("ipm_kmax4_N30_nx8_nu3", "ipm", qp, dict(k_max=4, mu0=2.0, mu_tol=1e-12, alpha_min=1e-8),
+                         dict(ux=r["ux"], pi=r["pi"], lam=r["lam"], t=r["t"], stat=r["stat"], kk=r["kk"],
+                              ret=r["ret"])))
+    # general constraints (oracle-only row: GPU path returns EUNSUPPORTED)
+    qp = ng_qp()
+    r = ref.ipm(qp.copy(), k_max=50)
+    out.append(save_case("ipm_ng_N30_nx8_nu3", "ipm", qp, dict(k_max=50, mu0=2.0, mu_tol=1e-12, alpha_min=1e-8),
+                         dict(ux=r["ux"], pi=r["pi"], lam=r["lam"], t=r["t"], stat=r["stat"], kk=r["kk"],
+                              ret=r["ret"])))
+
+    # ---------------- KKT re-solve + residuals + single Newton step ----------------
+    qp = mass_spring_qp(30, 8, 3, boxes=True)
+    r = ref.ipm(qp.copy(), k_max=50)
+    b, q = bq_from_qp(qp)
+    b2 = [x + 0.01 * rng.standard_normal(x.shape) for x in b]
+    q2v = [x + 0.01 * rng.standard_normal(x.shape) for x in q]
+    kk = ref.kkt_new_rhs(qp.copy(), r["work"], b2, q2v)
+    out.append(save_case("kkt_N30_nx8_nu3", "kkt", qp, dict(k_max=50, mu0=2.0, mu_tol=1e-12, alpha_min=1e-8),
+                         dict(ux=kk["ux"], pi=kk["pi"], lam=kk["lam"], t=kk["t"]), extra=dict(b2=b2, q2=q2v)))
+    uxp = [x + 0.01 * rng.standard_normal(x.shape) for x in r["ux"]]
+    pip = [x + 0.01 * rng.standard_normal(x.shape) for x in r["pi"]]
+    res = ref.residuals(qp.copy(), b, q, uxp, pip, r["lam"], r["t"])
+    out.append(save_case("res_N30_nx8_nu3", "res", qp, {},
+                         dict(rq=res["rq"], rb=res["rb"], rd=res["rd"], rm=res["rm"], mu=res["mu"]),
+                         extra=dict(b=b, q=q, ux=uxp, pi=pip, lam=r["lam"], t=r["t"])))
+    qp = mass_spring_qp(10, 8, 3, boxes=True)
+    r = ref.ipm(qp.copy(), k_max=50)
+    # interior starting point (t, lam away from 0) so the single Newton step is well conditioned
+    lam0, t0 = [], []
+    for k in range(qp.N + 1):
+        nb = int(qp.nb[k])
+        lam0.append(np.concatenate([1.0 + 0.1 * rng.random(2 * nb), np.zeros(4)]))
+        t0.append(np.concatenate([0.5 + 0.1 * rng.random(2 * nb), np.zeros(4)]))
+    ux0 = [0.9 * x for x in r["ux"]]
+    pi0 = [0.9 * x for x in r["pi"]]
+    sn = ref.single_newton(qp.copy(), ux0, pi0, lam0, t0, k_max=1, mu0=0.1)
+    out.append(save_case("newton_N10_nx8_nu3", "newton", qp, dict(k_max=1, mu0=0.1, mu_tol=1e-12, alpha_min=1e-8),
+                         dict(ux=sn["ux"], pi=sn["pi"], lam=sn["lam"], t=sn["t"], stat=sn["stat"], kk=sn["kk"],
+                              ret=sn["ret"]), extra=dict(ux0=ux0, pi0=pi0, lam0=lam0, t0=t0)))
+    total = sum(os.path.getsize(p) for p in out)
+    print(f"wrote {len(out)} cases, {total / 1e6:.2f} MB")
+
+
+if __name__ == "__main__":
+    main()
