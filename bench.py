@@ -94,35 +94,22 @@ def main():
 
     from hpmpc_amd.batch import (BatchSolver, algorithmic_bytes_per_ip_iter, algorithmic_bytes_per_sv,
                                  flops_ip_iter, flops_sv)
-    from hpmpc_amd.ocp import batch_x0, mass_spring_qp
+    from hpmpc_amd.shard import Reducer, make_shard
 
     B, N, nx, nu = args.batch, args.N, args.nx, args.nu
-    X0 = batch_x0(nx, B * world)[rank * B:(rank + 1) * B]
-    qp = mass_spring_qp(N, nx, nu, batch=B, x0=X0, time_variant=True, seed=1 + rank)
+    qp = make_shard(N, nx, nu, rank, world, B)
     solver = BatchSolver(qp, k_max=args.k_max)
-    qp_ric = mass_spring_qp(N, nx, nu, boxes=False, batch=B, x0=X0, time_variant=True, seed=1 + rank)
+    qp_ric = make_shard(N, nx, nu, rank, world, B, boxes=False)
     ric = BatchSolver(qp_ric, k_max=1)
     stream = torch.cuda.current_stream()
+    red = Reducer(dist, "cuda")
 
     def barrier():
         torch.cuda.synchronize()
-        if dist is not None:
-            dist.barrier()
+        red.barrier()
         torch.cuda.synchronize()
 
-    def max_over_ranks(x):
-        if dist is None:
-            return x
-        t = torch.tensor([x], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
-
-    def sum_over_ranks(x):
-        if dist is None:
-            return x
-        t = torch.tensor([x], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        return float(t.item())
+    max_over_ranks, sum_over_ranks = red.max, red.sum
 
     # ---------------- IPM (headline) ----------------
     for _ in range(args.warmup):

@@ -51,6 +51,20 @@ def build_stamps(verbose: bool = False) -> str:
     return out
 
 
+def build_calib(verbose: bool = False) -> str:
+    """HBM counter calibration kernel (tools/hbm_calib.hip; profiling tool, not part of the product)."""
+    os.makedirs(LIBDIR, exist_ok=True)
+    out = os.path.join(LIBDIR, "libhbm_calib.so")
+    src = os.path.join(ROOT, "tools", "hbm_calib.hip")
+    if _newer(out, [src, os.path.join(CSRC, "hk_prims.h")]):
+        return out
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", src, "-o", out]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    return out
+
+
 def build_oracle(force: bool = False) -> None:
     odir = os.path.join(ROOT, "oracle")
     targets = ["oracle"]
@@ -61,6 +75,7 @@ def build_oracle(force: bool = False) -> None:
 
 def build_all(force: bool = False, verbose: bool = False) -> None:
     build_hip(force=force, verbose=verbose)
+    build_calib(verbose=verbose)
     build_oracle(force=force)
 
 

@@ -625,12 +625,14 @@ extern "C" int d_ip2_res_mpc_hard_tv_work_space_size_bytes(int N, int* nx, int* 
     return (int)((ws_doubles(N) * 8 + 63) / 64 * 64);
 }
 
-extern "C" int d_ip2_res_mpc_hard_tv(int* kk, int k_max, double mu0, double mu_tol, double alpha_min, int warm_start,
-                                     double* stat, int N, int* nx, int* nu_N, int* nb, int** idxb, int* ng,
-                                     double** pBAbt, double** pQ, double** pDCt, double** d, double** ux,
-                                     int compute_mult, double** pi, double** lam, double** t,
-                                     double* double_work_memory) {
-    (void)pDCt;
+namespace {
+
+// Shared body of d_ip2_res_mpc_hard_tv and its single-Newton variant.  For the variant, ux0/pi0/lam0/t0
+// hold the start iterate (lam0/t0 as [lower(nb) | upper(nb)], d_aux_ip_hard_lib4.c:153-213).
+int ipm_entry(int single_newton, int* kk, int k_max, double mu0, double mu_tol, double alpha_min, int warm_start,
+              double* stat, int N, int* nx, int* nu_N, int* nb, int** idxb, int* ng, double** pBAbt, double** pQ,
+              double** d, double** ux, int compute_mult, double** pi, double** lam, double** t,
+              double* double_work_memory, double** ux0, double** pi0, double** lam0, double** t0) {
     g_err = 0;
     hpmpc_mi355x_plan* P = g_ctx.get_plan(N, nx, nu_N, nb, idxb, ng);
     if (!P) return g_err;
@@ -640,8 +642,21 @@ extern "C" int d_ip2_res_mpc_hard_tv(int* kk, int k_max, double mu0, double mu_t
     stage_BAbt(P, H, A, pBAbt);
     stage_RSQ(P, H, A, pQ);
     stage_d(P, H, A, d);
-    if (warm_start)
+    if (single_newton) {
+        for (int k = 0; k <= N; k++) {
+            memcpy(H + A.ux + k * V16, ux0[k], (P->st[k].nu + nx[k]) * sizeof(double));
+            if (k < N) memcpy(H + A.pi + k * V16, pi0[k], nx[k + 1] * sizeof(double));
+            const int pnb = P->st[k].pnb;
+            for (int l = 0; l < nb[k]; l++) {
+                H[A.lam + k * V32 + l] = lam0[k][l];
+                H[A.lam + k * V32 + pnb + l] = lam0[k][nb[k] + l];
+                H[A.t + k * V32 + l] = t0[k][l];
+                H[A.t + k * V32 + pnb + l] = t0[k][nb[k] + l];
+            }
+        }
+    } else if (warm_start) {
         for (int k = 0; k <= N; k++) memcpy(H + A.ux + k * V16, ux[k], (P->st[k].nu + nx[k]) * sizeof(double));
+    }
     KArgs a = arena_args(P, A, g_ctx.dev);
     a.k_max = k_max;
     a.mu0 = mu0;
@@ -649,6 +664,7 @@ extern "C" int d_ip2_res_mpc_hard_tv(int* kk, int k_max, double mu0, double mu_t
     a.alpha_min = alpha_min;
     a.warm_start = warm_start;
     a.compute_mult = compute_mult;
+    a.single_newton = single_newton;
     if (!up(A) || !run(K_IPM, a, "hk_ipm") || !down(A)) return g_err;
     const int* iv = reinterpret_cast<const int*>(H + A.ints);
     *kk = iv[0];
@@ -664,6 +680,30 @@ extern "C" int d_ip2_res_mpc_hard_tv(int* kk, int k_max, double mu0, double mu_t
     }
     memcpy(double_work_memory, H + A.ws, ws_doubles(N) * sizeof(double));
     return iv[1];
+}
+
+}  // namespace
+
+extern "C" int d_ip2_res_mpc_hard_tv(int* kk, int k_max, double mu0, double mu_tol, double alpha_min, int warm_start,
+                                     double* stat, int N, int* nx, int* nu_N, int* nb, int** idxb, int* ng,
+                                     double** pBAbt, double** pQ, double** pDCt, double** d, double** ux,
+                                     int compute_mult, double** pi, double** lam, double** t,
+                                     double* double_work_memory) {
+    (void)pDCt;
+    return ipm_entry(0, kk, k_max, mu0, mu_tol, alpha_min, warm_start, stat, N, nx, nu_N, nb, idxb, ng, pBAbt, pQ, d,
+                     ux, compute_mult, pi, lam, t, double_work_memory, nullptr, nullptr, nullptr, nullptr);
+}
+
+extern "C" int d_ip2_res_mpc_hard_tv_single_newton_step(int* kk, int k_max, double mu0, double mu_tol,
+                                                        double alpha_min, int warm_start, double* stat, int N,
+                                                        int* nx, int* nu_N, int* nb, int** idxb, int* ng,
+                                                        double** pBAbt, double** pQ, double** pDCt, double** d,
+                                                        double** ux, int compute_mult, double** pi, double** lam,
+                                                        double** t, double* double_work_memory, double** ux0,
+                                                        double** pi0, double** lam0, double** t0) {
+    (void)pDCt;
+    return ipm_entry(1, kk, k_max, mu0, mu_tol, alpha_min, warm_start, stat, N, nx, nu_N, nb, idxb, ng, pBAbt, pQ, d,
+                     ux, compute_mult, pi, lam, t, double_work_memory, ux0, pi0, lam0, t0);
 }
 
 extern "C" void d_kkt_solve_new_rhs_res_mpc_hard_tv(int N, int* nx, int* nu_N, int* nb, int** idxb, int* ng,

@@ -23,7 +23,7 @@ struct KArgs {
     double* vPb;
     int update_b, update_q, use_box, compute_pi, compute_Pb;
     // IPM
-    int k_max, warm_start, compute_mult;
+    int k_max, warm_start, compute_mult, single_newton;
     double mu0, mu_tol, alpha_min;
     int *kk, *ret;
     double* stat;    // 5*k_max per problem

@@ -245,14 +245,17 @@ extern "C" __global__ __launch_bounds__(64) void hk_ipm(KArgs a) {
         return;
     }
     const double mu_scal = 1.0 / (2.0 * nbt);
-    init_var(io, bt, dv, ux, pi, lam, t, a.mu0, a.warm_start);
+    // single Newton step (d_ip2_res_hard.c:1348-1919): the caller's ux/pi/lam/t already hold the start
+    // iterate (d_init_var_mpc_hard_tv_single_newton is a copy, done by the host), no phase 1.
+    const bool sn = a.single_newton != 0;
+    if (!sn) init_var(io, bt, dv, ux, pi, lam, t, a.mu0, a.warm_start);
     for (int i = l; i < (N + 1) * V16; i += 64) w.dpi[i] = 0.0;
 
     double mu = a.mu0, alpha = 1.0, sigma = 0.0;
     const double mu_tol_low = a.mu_tol < 1e-5 ? 1e-5 : a.mu_tol;
 
     // ------------------------------ phase 1 (d_ip2_res_hard.c:498-718) ------------------------------
-    while (kk < a.k_max && mu > mu_tol_low && alpha >= a.alpha_min) {
+    while (!sn && kk < a.k_max && mu > mu_tol_low && alpha >= a.alpha_min) {
         HK_FOR_BOX(io, k, {  // d_update_hessian_mpc_hard_tv, sigma_mu = 0
             const double til = 1.0 / t[lo], tiu = 1.0 / t[up];
             const double ltl = lam[lo] * til, ltu = lam[up] * tiu;
@@ -376,7 +379,7 @@ extern "C" __global__ __launch_bounds__(64) void hk_ipm(KArgs a) {
     // ------------------------------ phase 2 (d_ip2_res_hard.c:756-1273) ------------------------------
     residuals(io, bt, &sm, nullptr, nullptr, ux, pi, dv, lam, t, w.res_q, w.res_b, w.res_d, w.res_m, mu);
     wsync();
-    while (kk < a.k_max && mu > a.mu_tol && alpha >= a.alpha_min) {
+    while (kk < a.k_max && (sn || (mu > a.mu_tol && alpha >= a.alpha_min))) {
         HK_FOR_BOX(io, k, {  // d_update_hessian_gradient_res_mpc_hard_tv
             const double til = 1.0 / t[lo], tiu = 1.0 / t[up];
             w.t_inv[lo] = til;
@@ -386,9 +389,10 @@ extern "C" __global__ __launch_bounds__(64) void hk_ipm(KArgs a) {
                                    tiu * (w.res_m[up] + lam[up] * w.res_d[up]);
         });
         wsync();
-        ric_backward<true>(io, &sm, 1, w.res_b, 1, w.res_q, 1, w.Qx, w.qx, 1, w.Pb);
+        // the single-Newton variant factorises with the data's own b/q rows (d_ip2_res_hard.c:1700-1760)
+        ric_backward<true>(io, &sm, !sn, w.res_b, !sn, w.res_q, 1, w.Qx, w.qx, 1, w.Pb);
         wsync();
-        ric_forward_sv(io, &sm, 1, w.res_b, w.dux, a.compute_mult, w.dpi);
+        ric_forward_sv(io, &sm, !sn, w.res_b, w.dux, a.compute_mult, w.dpi);
         wsync();
         double al = 1.0;
         HK_FOR_BOX(io, k, {  // d_compute_alpha_res_mpc_hard_tv
@@ -420,9 +424,12 @@ extern "C" __global__ __launch_bounds__(64) void hk_ipm(KArgs a) {
         });
         const double mu_aff = wave_sum(ms) * mu_scal;
         if (l == 0) stat[5 * kk + 2] = mu_aff;
-        sigma = mu_aff / mu;
-        sigma = sigma * sigma * sigma;
-        const double smu = sigma * mu;
+        double smu = a.mu0;  // single Newton: sigma*mu is supplied by the caller as mu0 (:1788-1790)
+        if (!sn) {
+            sigma = mu_aff / mu;
+            sigma = sigma * sigma * sigma;
+            smu = sigma * mu;
+        }
         HK_FOR_BOX(io, k, {  // centering correction + d_update_gradient_res_mpc_hard_tv
             const double rml = w.res_m[lo] + (w.dt[lo] * w.dlam[lo] - smu);
             const double rmu = w.res_m[up] + (w.dt[up] * w.dlam[up] - smu);
@@ -489,7 +496,7 @@ extern "C" __global__ __launch_bounds__(64) void hk_ipm(KArgs a) {
         if (l == 0) stat[5 * kk + 4] = mu;
         kk++;
     }
-    if (mu <= a.mu_tol)
+    if (!sn && mu <= a.mu_tol)
         ret = 0;
     else if (kk >= a.k_max)
         ret = 1;

@@ -55,6 +55,14 @@ int d_ip2_res_mpc_hard_tv(int *kk, int k_max, double mu0, double mu_tol, double 
                           double *stat, int N, int *nx, int *nu_N, int *nb, int **idxb, int *ng, double **pBAbt,
                           double **pQ, double **pDCt, double **d, double **ux, int compute_mult, double **pi,
                           double **lam, double **t, double *double_work_memory);
+/* include/mpc_solvers.h:44 (d_ip2_res_hard.c:1348) -- k_max Newton steps from (ux0, pi0, lam0, t0), fixed
+ * centering target mu0, no exit test on mu; lam0/t0 as [lower(nb) | upper(nb)] */
+int d_ip2_res_mpc_hard_tv_single_newton_step(int *kk, int k_max, double mu0, double mu_tol, double alpha_min,
+                                             int warm_start, double *stat, int N, int *nx, int *nu_N, int *nb,
+                                             int **idxb, int *ng, double **pBAbt, double **pQ, double **pDCt,
+                                             double **d, double **ux, int compute_mult, double **pi, double **lam,
+                                             double **t, double *double_work_memory, double **ux0, double **pi0,
+                                             double **lam0, double **t0);
 /* include/mpc_solvers.h:46 (d_ip2_res_hard.c:1922) -- re-solve with the persisted factor/iterate */
 void d_kkt_solve_new_rhs_res_mpc_hard_tv(int N, int *nx, int *nu_N, int *nb, int **idxb, int *ng, double **pBAbt,
                                          double **b, double **pQ, double **q, double **pDCt, double **d,

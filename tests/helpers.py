@@ -99,3 +99,64 @@ def check_case(case, got):
             continue
         e = max_err(case, key, got[key], ref)
         assert e <= t, f"{case.name}: {key} err {e:.3e} > {t:.0e}"
+
+
+def random_qp(N, nx, nu, nb=None, seed=0, box=1.0):
+    """Random well-posed OCP QP with per-stage sizes (lists of length N+1; nu[N] is forced to 0),
+    random box subsets idxb (any variable order), SPD stage Hessians.  Exercises size patterns the
+    mass-spring workload does not (odd sizes, nu > nx, varying stage sizes, x-only boxes)."""
+    from hpmpc_amd.ocp import OCPQP, pack_lib4, rup
+
+    rng = np.random.default_rng(seed)
+    nx = np.asarray(nx, dtype=np.int32)
+    nu = np.asarray(nu, dtype=np.int32).copy()
+    nu[N] = 0
+    nx[0] = 0 if nx[0] == 0 else nx[0]
+    nb = np.zeros(N + 1, dtype=np.int32) if nb is None else np.asarray(nb, dtype=np.int32)
+    BAbt, RSQrq, d, idxb = [], [], [], []
+    for k in range(N + 1):
+        nuk, nxk = int(nu[k]), int(nx[k])
+        nux = nuk + nxk
+        if k < N:
+            nx1 = int(nx[k + 1])
+            M = np.zeros((nux + 1, nx1))
+            M[:nux] = 0.5 * rng.standard_normal((nux, nx1)) / np.sqrt(max(nux, 1))
+            M[nux] = 0.3 * rng.standard_normal(nx1)
+            BAbt.append(pack_lib4(M))
+        G = rng.standard_normal((nux, nux))
+        H = G @ G.T / max(nux, 1) + np.eye(nux)
+        M = np.zeros((nux + 1, nux))
+        M[:nux] = H
+        M[nux] = 0.5 * rng.standard_normal(nux)
+        RSQrq.append(pack_lib4(M))
+        nbk = int(nb[k])
+        ib = np.sort(rng.choice(nux, size=nbk, replace=False)).astype(np.int32) if nbk else np.zeros(0, np.int32)
+        idxb.append(ib)
+        pnb = rup(nbk, 4)
+        dk = np.zeros(max(2 * pnb, 1))
+        dk[:nbk] = -box * (0.5 + rng.random(nbk))
+        dk[pnb:pnb + nbk] = box * (0.5 + rng.random(nbk))
+        d.append(dk)
+    return OCPQP(N, nx, nu, nb, np.zeros(N + 1, dtype=np.int32), idxb, BAbt, RSQrq, d, [], None)
+
+
+def compare_ipm(case_like_qp, a, b, tol=TOL_IPM):
+    """max error of two ipm() results over valid parts."""
+    qp = case_like_qp
+    assert a["kk"] == b["kk"] and a["ret"] == b["ret"], (a["kk"], b["kk"], a["ret"], b["ret"])
+    e = 0.0
+    for k in range(qp.N + 1):
+        n = qp.nux(k)
+        e = max(e, float(np.max(np.abs(a["ux"][k][:n] - b["ux"][k][:n]) / np.maximum(1, np.abs(b["ux"][k][:n])),
+                                initial=0)))
+        if k < qp.N:
+            m = int(qp.nx[k + 1])
+            e = max(e, float(np.max(np.abs(a["pi"][k][:m] - b["pi"][k][:m]) / np.maximum(1, np.abs(b["pi"][k][:m])),
+                                    initial=0)))
+        nbk, pnb = int(qp.nb[k]), qp.pnb(k)
+        idx = np.r_[0:nbk, pnb:pnb + nbk].astype(int)
+        for key in ("lam", "t"):
+            g, r = a[key][k][idx], b[key][k][idx]
+            e = max(e, float(np.max(np.abs(g - r) / np.maximum(1, np.abs(r)), initial=0)))
+    assert e <= tol, e
+    return e

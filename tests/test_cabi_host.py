@@ -1,0 +1,169 @@
+"""CPU-side checks of the drop-in boundary and the host logic (no GPU compute is launched here).
+
+* libhpmpc_mi355x.so loads and exports every function include/hpmpc_mi355x.h declares;
+* the reference-named entry points reject what the GPU path does not support with the documented
+  error code before touching the device (ng > 0, stages wider than the 16-wide tile);
+* lib4 packing helpers, the synthetic workload generator and the roofline byte/flop formulas.
+"""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+from hpmpc_amd import batch
+from hpmpc_amd.ocp import (OCPQP, batch_x0, default_x0, lib4_size, mass_spring_qp, pack_lib4, pack_lib4_batch,
+                           unpack_lib4)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "hpmpc_mi355x.h")
+EUNSUPPORTED = -10
+
+
+def header_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    names = re.findall(r"^[A-Za-z_][\w\s\*]*?\b([A-Za-z_]\w*)\s*\(", text, flags=re.M)
+    return sorted(set(n for n in names if n not in ("defined",)))
+
+
+@pytest.fixture(scope="module")
+def hiplib():
+    if not os.path.exists(batch.LIBPATH):
+        from hpmpc_amd.build import build_hip
+
+        build_hip()
+    return C.CDLL(batch.LIBPATH, mode=os.RTLD_LOCAL)
+
+
+def test_header_declares_reference_entry_points():
+    names = header_functions()
+    for ref in ("d_back_ric_rec_sv_tv_res", "d_back_ric_rec_trf_tv_res", "d_back_ric_rec_trs_tv_res",
+                "d_back_ric_rec_sv_tv_work_space_size_bytes", "d_back_ric_rec_sv_tv_memory_space_size_bytes",
+                "d_ip2_res_mpc_hard_tv", "d_ip2_res_mpc_hard_tv_work_space_size_bytes",
+                "d_ip2_res_mpc_hard_tv_single_newton_step", "d_kkt_solve_new_rhs_res_mpc_hard_tv",
+                "d_res_res_mpc_hard_tv"):
+        assert ref in names, ref
+    assert len(names) >= 19, names
+
+
+def test_library_exports_every_declared_symbol(hiplib):
+    missing = [n for n in header_functions() if not hasattr(hiplib, n)]
+    assert not missing, missing
+
+
+def test_every_reference_citation_resolves():
+    """Each prototype cites the reference declaration it replaces; the cited headers exist in the
+    reference layout (checked by name only: the reference tree is not needed at run time)."""
+    text = open(HEADER).read()
+    cites = re.findall(r"/\* (include/\w+\.h):(\d+)", text)
+    assert len(cites) >= 10
+    assert {c[0] for c in cites} <= {"include/lqcp_solvers.h", "include/mpc_solvers.h"}
+
+
+def test_version_string(hiplib):
+    hiplib.hpmpc_mi355x_version.restype = C.c_char_p
+    assert b"gfx950" in hiplib.hpmpc_mi355x_version()
+
+
+def _sizes(qp):
+    iv = lambda a: np.ascontiguousarray(a, dtype=np.int32)
+    return iv(qp.nx), iv(qp.nu), iv(qp.nb), iv(qp.ng)
+
+
+def test_plan_rejects_unsupported_sizes(hiplib):
+    L = hiplib
+    L.hpmpc_mi355x_plan_create.restype = C.c_void_p
+    L.hpmpc_mi355x_plan_create.argtypes = [C.c_int] + [C.c_void_p] * 5
+    for nx, nu in ((20, 4), (12, 8), (13, 4)):  # nu+nx > 16 or round_up(nu,4)+nx > 16
+        N = 3
+        nxv = np.array([0] + [nx] * N, dtype=np.int32)
+        nuv = np.array([nu] * N + [0], dtype=np.int32)
+        z = np.zeros(N + 1, dtype=np.int32)
+        idx = (C.POINTER(C.c_int) * (N + 1))()
+        p = L.hpmpc_mi355x_plan_create(N, nxv.ctypes.data, nuv.ctypes.data, z.ctypes.data, C.cast(idx, C.c_void_p),
+                                       z.ctypes.data)
+        assert not p
+        assert L.hpmpc_mi355x_last_error() == EUNSUPPORTED
+
+
+def test_reference_entry_rejects_general_constraints(hiplib):
+    """ng > 0 is outside the GPU path: the IPM returns EUNSUPPORTED, no fallback."""
+    from hpmpc_amd.cabi import HpmpcAPI
+
+    api = HpmpcAPI(hiplib, "")
+    qp = mass_spring_qp(6, 4, 1)
+    qp.ng = np.array([0] * 6 + [4], dtype=np.int32)
+    qp.DCt = [np.zeros(8)] * 6 + [pack_lib4(np.eye(4))]
+    qp.d[6] = np.concatenate([qp.d[6][:4], -np.ones(4), np.ones(4)])
+    r = api.ipm(qp, k_max=5)
+    assert r["ret"] == EUNSUPPORTED
+    assert hiplib.hpmpc_mi355x_last_error() == EUNSUPPORTED
+
+
+def test_size_queries_are_host_only(hiplib):
+    from hpmpc_amd.cabi import HpmpcAPI
+
+    api = HpmpcAPI(hiplib, "")
+    qp = mass_spring_qp(100, 12, 4)
+    ws = api.ipm_ws_size(qp)
+    assert ws % 64 == 0 and ws >= 8 * 101 * (288 + 9 * 16 + 8 * 32)
+    w, m = api.ric_sizes(qp)
+    assert m >= 8 * 101 * 288 and w >= 0
+
+
+# ---------------------------------------------------------------- lib4 / workload generator
+@pytest.mark.parametrize("m,n", [(1, 1), (4, 4), (5, 3), (17, 16), (13, 12), (20, 12)])
+def test_lib4_roundtrip(m, n):
+    rng = np.random.default_rng(m * 100 + n)
+    A = rng.standard_normal((m, n))
+    buf = pack_lib4(A)
+    assert buf.size == lib4_size(m, n)
+    np.testing.assert_array_equal(unpack_lib4(buf, m, n), A)
+    # element (i,j) at (i/4)*4*sd + i%4 + 4*j  (include/block_size.h, blas_d_lib4.c:5659-5672)
+    sd = (n + 1) // 2 * 2
+    for i, j in ((m - 1, n - 1), (0, n - 1), (m - 1, 0)):
+        assert buf[(i // 4) * 4 * sd + i % 4 + 4 * j] == A[i, j]
+
+
+def test_pack_lib4_batch_matches_single():
+    rng = np.random.default_rng(7)
+    M = rng.standard_normal((5, 17, 12))
+    B = pack_lib4_batch(M)
+    for p in range(5):
+        np.testing.assert_array_equal(B[p], pack_lib4(M[p]))
+
+
+def test_workload_generator_shapes():
+    qp = mass_spring_qp(100, 12, 4, batch=8, time_variant=True, seed=1)
+    assert qp.nb.tolist() == [4] + [10] * 99 + [6]
+    assert qp.nx[0] == 0 and qp.nu[100] == 0
+    one = qp.problem(3)
+    assert isinstance(one, OCPQP) and one.batch is None
+    X0 = batch_x0(12, 8)
+    np.testing.assert_array_equal(X0[0], default_x0(12))
+    assert np.all(np.abs(X0[1:]) <= 2.5)
+
+
+def test_roofline_formulas_match_survey():
+    """flop_sv(N=100,nx=12,nu=4) = 843.5k.  Bytes are summed over the real stage
+    shapes (nx[0]=0, nu[N]=0), slightly below the survey's uniform-stage 441.6 KB estimate."""
+    assert abs(batch.flops_sv(100, 12, 4) - 843.5e3) < 0.5e3
+    assert abs(batch.flops_sv(50, 8, 3) - 144.8e3) < 0.5e3
+    qp = mass_spring_qp(100, 12, 4, boxes=False)
+    b = batch.algorithmic_bytes_per_sv(qp)
+    assert 0.98 * 441.6e3 < b <= 441.6e3
+    qpb = mass_spring_qp(100, 12, 4)
+    bi = batch.algorithmic_bytes_per_ip_iter(qpb)
+    assert 0.97 * 1318e3 < bi <= 1318e3 * 1.01
+
+
+def test_batch_solver_refuses_without_gpu():
+    """No CPU fallback: the batched front end raises when there is no HIP device."""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(RuntimeError):
+        batch.BatchSolver(mass_spring_qp(5, 4, 1, batch=2))

@@ -1,0 +1,255 @@
+"""Parity of the HIP path (libhpmpc_mi355x.so on the MI355X) with the reference.
+
+* every golden vector of the real reference (tests/golden) through the reference-named C ABI;
+* the CPU oracle on seeded problems the goldens do not cover (varying stage sizes, arbitrary box
+  index sets, aliased stage buffers, warm start, N = 1);
+* the batched device API against the oracle problem by problem, and at the benchmark's full size
+  (N=100 nx=12 nu=4, batch 1024) through size-independent properties: launch splitting and repeat
+  runs are bit-identical, and converged problems satisfy the KKT conditions.
+
+Tolerances: Riccati outputs 1e-12, IPM iterates 1e-10 relative to max(1,|ref|), with
+identical iteration counts and return codes.
+"""
+import numpy as np
+import pytest
+
+from hpmpc_amd.golden import load_all
+from hpmpc_amd.ocp import mass_spring_qp
+from helpers import TOL_IPM, TOL_RIC, check_case, compare_ipm, random_qp, run_case
+
+pytestmark = pytest.mark.gpu
+EUNSUPPORTED = -10
+
+CASES = load_all()
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c.name for c in CASES])
+def test_golden_through_c_abi(product, case):
+    if int(np.sum(case.qp.ng)) > 0:
+        r = product.ipm(case.fresh_qp(), k_max=int(case.args["k_max"]))
+        assert r["ret"] == EUNSUPPORTED  # ng > 0 is outside the GPU path: loud error, no fallback
+        return
+    check_case(case, run_case(product, case))
+
+
+SIZES = [
+    # (N, nx per stage, nu per stage, nb per stage)
+    (1, [0, 4], [2, 0], [2, 2]),
+    (2, [0, 1, 1], [1, 1, 0], [1, 2, 1]),
+    (7, [0, 3, 5, 5, 2, 7, 12, 9], [2, 4, 1, 3, 6, 4, 4, 0], [1, 3, 2, 0, 4, 5, 6, 3]),
+    (12, [0] + [8] * 12, [8] * 12 + [0], [3] * 13),
+    (20, [0] + [12] * 20, [4] * 20 + [0], [0] * 21),
+    (9, [0] + [16] * 9, [4] + [0] * 9, [0] + [2] * 9),
+    (5, [0, 12, 12, 11, 12, 12], [3, 3, 2, 4, 3, 0], [2, 15, 3, 10, 5, 12]),
+]
+
+
+@pytest.mark.parametrize("N,nx,nu,nb", SIZES, ids=[f"N{s[0]}_{i}" for i, s in enumerate(SIZES)])
+def test_ipm_random_sizes_vs_oracle(product, oracle, N, nx, nu, nb):
+    qp = random_qp(N, nx, nu, nb, seed=N * 31 + len(nx))
+    a = product.ipm(qp.copy(), k_max=40)
+    b = oracle.ipm(qp.copy(), k_max=40)
+    compare_ipm(qp, a, b)
+    np.testing.assert_allclose(a["stat"], b["stat"], rtol=1e-9, atol=1e-14)
+
+
+@pytest.mark.parametrize("N,nx,nu,nb", SIZES, ids=[f"N{s[0]}_{i}" for i, s in enumerate(SIZES)])
+def test_riccati_random_sizes_vs_oracle(product, oracle, N, nx, nu, nb):
+    qp = random_qp(N, nx, nu, nb, seed=N * 17 + 1)
+    rng = np.random.default_rng(N)
+    bd = [rng.random(max(int(n), 1)) + 0.5 for n in qp.nb]
+    Qx = [rng.random(max(int(n), 1)) for n in qp.nb]
+    qx = [rng.standard_normal(max(int(n), 1)) for n in qp.nb]
+    out = []
+    for api in (product, oracle):
+        q1 = qp.copy()
+        ux, pi, Pb, _ = api.ric_sv(q1, bd=bd, Qx=Qx, qx=qx, compute_pi=1, compute_Pb=1)
+        out.append((ux, pi, Pb, q1))
+    (u1, p1, b1, q1), (u2, p2, b2, q2) = out
+    for k in range(N + 1):
+        n = qp.nux(k)
+        np.testing.assert_allclose(u1[k][:n], u2[k][:n], rtol=TOL_RIC, atol=TOL_RIC)
+        if k < N:
+            m = int(qp.nx[k + 1])
+            np.testing.assert_allclose(p1[k][:m], p2[k][:m], rtol=TOL_RIC, atol=TOL_RIC)
+            np.testing.assert_allclose(b1[k][:m], b2[k][:m], rtol=TOL_RIC, atol=TOL_RIC)
+        # the in-place side effects on the caller's RSQrq (box diagonal / gradient) are the reference's
+        np.testing.assert_array_equal(q1.RSQrq[k], q2.RSQrq[k])
+
+
+def test_trf_trs_reuse_factor(product, oracle):
+    qp = random_qp(10, [0] + [6] * 10, [3] * 10 + [0], [2] * 11, seed=5)
+    rng = np.random.default_rng(5)
+    bd = [rng.random(2) + 1.0 for _ in range(11)]
+    Qx = [rng.random(2) for _ in range(11)]
+    res = []
+    for api in (product, oracle):
+        mem = api.ric_trf(qp.copy(), bd=bd, Qx=Qx)
+        outs = []
+        for trial in range(3):  # several right-hand sides against one factorisation
+            r2 = np.random.default_rng(100 + trial)
+            b = [r2.standard_normal(8) for _ in range(10)]
+            q = [r2.standard_normal(12) for _ in range(11)]
+            qx = [r2.standard_normal(4) for _ in range(11)]
+            outs.append(api.ric_trs(qp.copy(), mem, b=b, q=q, qx=qx, compute_pi=1, compute_Pb=1))
+        res.append(outs)
+    for (u1, p1, b1), (u2, p2, b2) in zip(*res):
+        for k in range(11):
+            np.testing.assert_allclose(u1[k][:qp.nux(k)], u2[k][:qp.nux(k)], rtol=TOL_RIC, atol=TOL_RIC)
+            if k < 10:
+                np.testing.assert_allclose(p1[k][:6], p2[k][:6], rtol=TOL_RIC, atol=TOL_RIC)
+                np.testing.assert_allclose(b1[k][:6], b2[k][:6], rtol=TOL_RIC, atol=TOL_RIC)
+
+
+def test_aliased_time_invariant_buffers(product, oracle):
+    """The reference drivers pass the SAME buffer for every inner stage (test_d_ip_hard.c:420-440)."""
+    qp = mass_spring_qp(25, 8, 3)
+    for k in range(2, 25):
+        qp.BAbt[k] = qp.BAbt[1]
+    for k in range(2, 25):
+        qp.RSQrq[k] = qp.RSQrq[1]
+        qp.d[k] = qp.d[1]
+    a = product.ipm(qp, k_max=50)
+    b = oracle.ipm(qp, k_max=50)
+    compare_ipm(qp, a, b)
+
+
+def test_warm_start_and_kkt_resolve(product, oracle):
+    qp = random_qp(15, [0] + [6] * 15, [2] * 15 + [0], [3] * 16, seed=11)
+    ux0 = [np.random.default_rng(k).standard_normal(12) * 0.1 for k in range(16)]
+    a = product.ipm(qp.copy(), k_max=30, warm_start=1, ux=ux0)
+    b = oracle.ipm(qp.copy(), k_max=30, warm_start=1, ux=ux0)
+    compare_ipm(qp, a, b)
+    rng = np.random.default_rng(2)
+    b2 = [rng.standard_normal(8) for _ in range(15)]
+    q2 = [rng.standard_normal(12) for _ in range(16)]
+    ka = product.kkt_new_rhs(qp.copy(), a["work"], b2, q2)
+    kb = oracle.kkt_new_rhs(qp.copy(), b["work"], b2, q2)
+    ka.update(kk=0, ret=0)
+    kb.update(kk=0, ret=0)
+    compare_ipm(qp, ka, kb)
+
+
+def test_single_newton_steps(product, oracle):
+    qp = mass_spring_qp(12, 8, 3)
+    rng = np.random.default_rng(4)
+    r = oracle.ipm(qp.copy(), k_max=50)
+    ux0 = [0.9 * x for x in r["ux"]]
+    pi0 = [0.9 * x for x in r["pi"]]
+    lam0 = [np.concatenate([1 + 0.1 * rng.random(2 * int(n)), np.zeros(4)]) for n in qp.nb]
+    t0 = [np.concatenate([0.5 + 0.1 * rng.random(2 * int(n)), np.zeros(4)]) for n in qp.nb]
+    a = product.single_newton(qp.copy(), ux0, pi0, lam0, t0, k_max=1, mu0=0.1)
+    b = oracle.single_newton(qp.copy(), ux0, pi0, lam0, t0, k_max=1, mu0=0.1)
+    compare_ipm(qp, a, b)
+    np.testing.assert_allclose(a["stat"], b["stat"], rtol=1e-9, atol=1e-14)
+
+
+# ------------------------------------------------------------------ batched device API
+@pytest.fixture(scope="module")
+def small_batch():
+    return mass_spring_qp(30, 8, 3, batch=64, time_variant=True, seed=9)
+
+
+def test_batch_ipm_vs_oracle(oracle, small_batch):
+    import torch
+
+    from hpmpc_amd.batch import BatchSolver
+
+    qp = small_batch
+    s = BatchSolver(qp, k_max=50)
+    s.ipm()
+    torch.cuda.synchronize()
+    kk, ret = s.kk.cpu().numpy(), s.ret.cpu().numpy()
+    ux, pi, lam, t = (x.cpu().numpy() for x in (s.ux, s.pi, s.lam, s.t))
+    for p in range(qp.batch):
+        one = qp.problem(p)
+        r = oracle.ipm(one, k_max=50)
+        got = dict(kk=int(kk[p]), ret=int(ret[p]), ux=[ux[p, k] for k in range(31)],
+                   pi=[pi[p, k] for k in range(30)], lam=[lam[p, k] for k in range(31)],
+                   t=[t[p, k] for k in range(31)])
+        compare_ipm(one, got, r)
+
+
+def test_batch_riccati_vs_oracle(oracle):
+    import torch
+
+    from hpmpc_amd.batch import BatchSolver
+
+    qp = mass_spring_qp(50, 8, 3, boxes=False, batch=32, time_variant=True, seed=2)
+    s = BatchSolver(qp, k_max=1)
+    s.ric_sv(compute_pi=1, compute_Pb=1)
+    torch.cuda.synchronize()
+    ux, pi, Pb = (x.cpu().numpy() for x in (s.ux, s.pi, s.Pb))
+    for p in range(qp.batch):
+        u2, p2, b2, _ = oracle.ric_sv(qp.problem(p), compute_pi=1, compute_Pb=1)
+        for k in range(51):
+            n = qp.nux(k)
+            np.testing.assert_allclose(ux[p, k, :n], u2[k][:n], rtol=TOL_RIC, atol=TOL_RIC)
+            if k < 50:
+                np.testing.assert_allclose(pi[p, k, :8], p2[k][:8], rtol=TOL_RIC, atol=TOL_RIC)
+                np.testing.assert_allclose(Pb[p, k, :8], b2[k][:8], rtol=TOL_RIC, atol=TOL_RIC)
+    # trf + trs with new right-hand sides == sv with those rows
+    s.ric_trf()
+    rng = np.random.default_rng(0)
+    b = torch.from_numpy(rng.standard_normal((32, 51, 16))).cuda()
+    q = torch.from_numpy(rng.standard_normal((32, 51, 16))).cuda()
+    s.ric_trs(b, q)
+    torch.cuda.synchronize()
+    ux = s.ux.cpu().numpy()
+    for p in (0, 7, 31):
+        one = qp.problem(p)
+        mem = oracle.ric_trf(one)
+        u2, _, _ = oracle.ric_trs(one, mem, b=[b[p, k].cpu().numpy().copy() for k in range(50)],
+                                  q=[q[p, k].cpu().numpy().copy() for k in range(51)])
+        for k in range(51):
+            n = qp.nux(k)
+            np.testing.assert_allclose(ux[p, k, :n], u2[k][:n], rtol=TOL_RIC, atol=TOL_RIC)
+
+
+def test_full_size_properties():
+    """N=100 nx=12 nu=4 batch=1024 (the benchmark workload): split launches and repeats are bitwise
+    identical; converged problems satisfy primal feasibility and complementarity."""
+    import torch
+
+    from hpmpc_amd.batch import BatchSolver
+    from hpmpc_amd.shard import make_shard
+
+    qp = make_shard(100, 12, 4, 0, 1, 1024)
+    s = BatchSolver(qp, k_max=50)
+    s.ipm()
+    torch.cuda.synchronize()
+    ux1, kk1, ret1 = s.ux.clone(), s.kk.clone(), s.ret.clone()
+    lam, t = s.lam.cpu().numpy(), s.t.cpu().numpy()
+    s.ux.zero_()
+    s.ipm(p0=0, count=300)
+    s.ipm(p0=300, count=724)
+    torch.cuda.synchronize()
+    assert torch.equal(s.ux, ux1) and torch.equal(s.kk, kk1) and torch.equal(s.ret, ret1)
+    ret = ret1.cpu().numpy()
+    kk = kk1.cpu().numpy()
+    assert (ret == 0).sum() > 900 and kk.max() <= 50
+    ux = ux1.cpu().numpy()
+    d = s.d.cpu().numpy()
+    conv = np.nonzero(ret == 0)[0]
+    for k in range(101):
+        nbk, pnb = int(qp.nb[k]), qp.pnb(k)
+        v = ux[conv][:, k, qp.idxb[k]]
+        lb, ub = d[conv, k, :nbk], d[conv, k, pnb:pnb + nbk]
+        assert np.all(v >= lb - 1e-8) and np.all(v <= ub + 1e-8)
+        lt = lam[conv, k, :nbk] * t[conv, k, :nbk] + lam[conv, k, pnb:pnb + nbk] * t[conv, k, pnb:pnb + nbk]
+        assert np.all(lt < 1e-8)
+    # exact parity for a sample spread over the batch
+    from hpmpc_amd.cabi import HpmpcAPI, load
+    import os
+
+    orc = HpmpcAPI(load(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle",
+                                      "liboracle.so")), "orc_")
+    lamt = s.lam.cpu().numpy(), s.t.cpu().numpy()
+    pi = s.pi.cpu().numpy()
+    for p in (0, 1, 511, 1023) + tuple(np.nonzero(ret != 0)[0][:2]):
+        one = qp.problem(int(p))
+        r = orc.ipm(one, k_max=50)
+        got = dict(kk=int(kk[p]), ret=int(ret[p]), ux=[ux[p, k] for k in range(101)],
+                   pi=[pi[p, k] for k in range(100)], lam=[lamt[0][p, k] for k in range(101)],
+                   t=[lamt[1][p, k] for k in range(101)])
+        compare_ipm(one, got, r, tol=TOL_IPM)

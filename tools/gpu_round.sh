@@ -1,0 +1,19 @@
+#!/bin/bash
+# Round-end evidence on the GPU box: GPU parity tests, smoke, bench line, rocprofv3 kernel stats,
+# and the two PMC passes for HBM traffic.  Every GPU step has its own time limit; the script stops at
+# the first failure.
+set -o pipefail
+mkdir -p gpurun_out/prof
+export TMPDIR=/tmp
+R=${1:-r01}
+step() { local name=$1; shift; echo "== $name"; "$@" > gpurun_out/$name.log 2>&1; local rc=$?; tail -${TAILN:-3} gpurun_out/$name.log; if [ $rc -ne 0 ]; then echo "$name failed rc=$rc"; exit $rc; fi; }
+step tests timeout -k 10 900 python3 -m pytest tests -m gpu -q -x
+step smoke timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()"
+step bench timeout -k 10 600 python3 bench.py
+step stats timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/stats -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu
+step pmc_fetch timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof/fetch -o run --output-format csv -- python3 tools/pmc_run.py
+step pmc_write timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof/write -o run --output-format csv -- python3 tools/pmc_run.py
+KK=$(grep kk_sum gpurun_out/pmc_write.log | awk '{print $2}')
+python3 tools/pmc_summarize.py gpurun_out/prof/fetch gpurun_out/prof/write gpurun_out/pmc_hk_ipm.json $KK
+find gpurun_out/prof/stats -name "*kernel_stats.csv" -exec cp {} gpurun_out/${R}_kernel_stats.csv \;
+cat gpurun_out/${R}_kernel_stats.csv

@@ -1,0 +1,41 @@
+#!/usr/bin/env python3
+"""Workload for the rocprofv3 --pmc passes (one counter group per pass, see tools/gpu_round.sh):
+1 GiB calibration copy (known bytes), then the benchmark's IPM and Riccati launches (N=100 nx=12
+nu=4, batch 1024), two launches each."""
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+
+    from hpmpc_amd.batch import BatchSolver
+    from hpmpc_amd.shard import make_shard
+
+    n = (1 << 30) // 8
+    x = torch.rand(n, dtype=torch.float64, device="cuda")
+    y = torch.empty_like(x)
+    cal = C.CDLL(os.path.join(ROOT, "hpmpc_amd", "lib", "libhbm_calib.so"))
+    cal.calib_run.argtypes = [C.c_void_p, C.c_void_p, C.c_long, C.c_void_p]
+    s = torch.cuda.current_stream().cuda_stream
+    for _ in range(2):
+        assert cal.calib_run(x.data_ptr(), y.data_ptr(), n, s) == 0
+    torch.cuda.synchronize()
+    del x, y
+    qp = make_shard(100, 12, 4, 0, 1, 1024)
+    sol = BatchSolver(qp, k_max=50)
+    ric = BatchSolver(make_shard(100, 12, 4, 0, 1, 1024, boxes=False), k_max=1)
+    for _ in range(2):
+        sol.ipm()
+    for _ in range(2):
+        ric.ric_sv()
+    torch.cuda.synchronize()
+    print("kk_sum", int(sol.kk.sum().item()))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Fold rocprofv3 --pmc counter CSVs into profiles/pmc_hk_ipm.json.
+
+FETCH_SIZE / WRITE_SIZE are scaled by the factors measured on calib_copy (known bytes: 1 GiB read,
+1 GiB written per launch, same 8-byte raw-buffer access width as the solver kernels)."""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def read_counters(d):
+    vals = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> [per dispatch]
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                k = row.get("Kernel_Name", "")
+                c = row.get("Counter_Name", "")
+                v = float(row.get("Counter_Value", "nan"))
+                vals[k.split("(")[0].strip()][c].append(v)
+    return vals
+
+
+def main(fetch_dir, write_dir, out, kk_sum):
+    F, W = read_counters(fetch_dir), read_counters(write_dir)
+    known = float(1 << 30)
+    cf = known / (sum(F["calib_copy"]["FETCH_SIZE"]) / len(F["calib_copy"]["FETCH_SIZE"]))
+    cw = known / (sum(W["calib_copy"]["WRITE_SIZE"]) / len(W["calib_copy"]["WRITE_SIZE"]))
+    res = {"workload": "ipm_N100_nx12_nu4_batch1024",
+           "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (tools/gpu_round.sh); "
+                     "per-launch values scaled by the calib_copy factors (1 GiB known bytes, 8-B/lane buffer ops)",
+           "calib": {"fetch_factor": cf, "write_factor": cw,
+                     "raw_fetch": F["calib_copy"]["FETCH_SIZE"], "raw_write": W["calib_copy"]["WRITE_SIZE"]},
+           "kernels": {}}
+    for k in ("hk_ipm", "hk_ric_sv"):
+        if k not in F or k not in W:
+            continue
+        fr = F[k]["FETCH_SIZE"]
+        wr = W[k]["WRITE_SIZE"]
+        fb = sum(fr) / len(fr) * cf
+        wb = sum(wr) / len(wr) * cw
+        res["kernels"][k] = {"raw_fetch": fr, "raw_write": wr, "fetch_bytes_per_launch": fb,
+                             "write_bytes_per_launch": wb, "hbm_bytes_per_launch": fb + wb}
+    if "hk_ipm" in res["kernels"]:
+        res["hbm_bytes_per_launch"] = res["kernels"]["hk_ipm"]["hbm_bytes_per_launch"]
+        res["kk_sum_per_launch"] = kk_sum
+        res["hbm_bytes_per_ip_iter_problem"] = res["hbm_bytes_per_launch"] / kk_sum if kk_sum else None
+    if "hk_ric_sv" in res["kernels"]:
+        res["sv_hbm_bytes_per_launch"] = res["kernels"]["hk_ric_sv"]["hbm_bytes_per_launch"]
+    with open(out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps({k: v for k, v in res.items() if k != "kernels"}, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]) if len(sys.argv) > 4 else 0)
