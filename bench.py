@@ -42,14 +42,20 @@ def parse():
     ap.add_argument("--nx", type=int, default=12)
     ap.add_argument("--nu", type=int, default=4)
     ap.add_argument("--k-max", type=int, default=50)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-threads", type=int, default=16, help="host threads for the CPU baseline "
+                    "(the GPU box's CPU share is 16 per GPU)")
     ap.add_argument("--no-cpu", action="store_true")
     return ap.parse_args()
 
 
-def cpu_baseline(qp, seconds, k_max):
-    """Time the reference c99 build (oracle/_ref, kind 'reference') -- or the clean-room oracle
-    (kind 'port') when the reference build is absent -- on one host core, problem after problem."""
+def cpu_baseline(qp, seconds, k_max, threads):
+    """IP iterations/s of the reference c99 build (oracle/_ref, kind 'reference') -- or of the
+    clean-room oracle (kind 'port') when the reference build is absent -- on the GPU box's host cores,
+    over the first problems of this rank's batch.  Calls are pre-marshalled; each thread cycles over
+    its own problems until the time budget ends.  Reported for `threads` threads and for 1 thread."""
+    import threading
+
     from hpmpc_amd.cabi import HpmpcAPI, load
 
     ref = os.path.join(ROOT, "oracle", "_ref", "libhpmpc_ref.so")
@@ -60,22 +66,40 @@ def cpu_baseline(qp, seconds, k_max):
         api, kind = HpmpcAPI(load(orc), "orc_"), "port"
     else:
         return None
-    iters = 0
-    nsolved = 0
-    t_solve = 0.0
-    t_end = time.perf_counter() + seconds
-    p = 0
-    while time.perf_counter() < t_end and p < qp.batch:
-        one = qp.problem(p)
+    nprob = min(qp.batch, max(64, threads * 4))
+    calls = [api.prepare_ipm(qp.problem(p), k_max=k_max) for p in range(nprob)]
+
+    def run(nthr, secs):
+        counts = [0] * nthr
+        solves = [0] * nthr
+        stop = time.perf_counter() + secs
+
+        def worker(i):
+            mine = calls[i::nthr]
+            j = 0
+            while time.perf_counter() < stop:
+                call, kk = mine[j % len(mine)]
+                call()
+                counts[i] += kk.value
+                solves[i] += 1
+                j += 1
+
+        th = [threading.Thread(target=worker, args=(i,)) for i in range(nthr)]
         t0 = time.perf_counter()
-        r = api.ipm(one, k_max=k_max)
-        t_solve += time.perf_counter() - t0
-        iters += r["kk"]
-        nsolved += 1
-        p += 1
-    return {"value": iters / t_solve, "unit": "IP-iter/s", "cores": 1, "kind": kind,
-            "sample": f"{nsolved} of the benchmark's problems solved sequentially on 1 core "
-                      f"({iters} IP iterations, {t_solve:.1f} s; ctypes marshalling included)"}
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        el = time.perf_counter() - t0
+        return sum(counts) / el, sum(counts), sum(solves), el
+
+    v1, it1, s1, e1 = run(1, seconds * 0.3)
+    vn, itn, sn, en = run(threads, seconds * 0.7)
+    return {"value": vn, "unit": "IP-iter/s", "cores": threads, "kind": kind,
+            "sample": f"first {nprob} problems of the benchmark batch, cold-start d_ip2_res_mpc_hard_tv "
+                      f"(k_max={k_max}) cycled by {threads} host threads for {en:.1f} s ({sn} solves, {itn} IP "
+                      f"iterations); pre-marshalled ctypes calls",
+            "single_core": {"value": v1, "solves": s1, "iters": it1, "seconds": e1}}
 
 
 def main():
@@ -168,7 +192,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(qp, args.cpu_seconds, args.k_max)
+        cpu = cpu_baseline(qp, args.cpu_seconds, args.k_max, args.cpu_threads)
 
     if rank == 0:
         line = {

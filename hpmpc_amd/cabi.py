@@ -149,6 +149,30 @@ class HpmpcAPI:
         return dict(ret=ret, kk=kk.value, stat=stat[: 5 * kk.value].copy(), ux=ux_, pi=pi, lam=lam, t=t,
                     work=work)
 
+    def prepare_ipm(self, qp: OCPQP, *, k_max=50, mu0=2.0, mu_tol=1e-12, alpha_min=1e-8):
+        """Pre-marshalled d_ip2_res_mpc_hard_tv call: returns (call, kk) where call() runs one cold-start
+        solve on private buffers and returns the status; kk.value holds the iteration count.  Used to
+        time the CPU baseline without ctypes marshalling in the timed region (the GIL is released during
+        the foreign call, so threads run solves concurrently)."""
+        N = qp.N
+        qp = qp.copy()
+        work = np.zeros(self.ipm_ws_size(qp) // 8 + 16)
+        ux, pi, lam, t = qp.alloc_solution()
+        stat = np.zeros(5 * k_max + 5)
+        kk = C.c_int(0)
+        dct = qp.DCt if qp.DCt else [np.zeros(8)] * (N + 1)
+        args = (C.byref(kk), C.c_int(k_max), C.c_double(mu0), C.c_double(mu_tol), C.c_double(alpha_min), C.c_int(0),
+                _dptr(stat), C.c_int(N), iv(qp.nx), iv(qp.nu), iv(qp.nb), ipp(qp.idxb), iv(qp.ng), dpp(qp.BAbt),
+                dpp(qp.RSQrq), dpp(dct), dpp(qp.d), dpp(ux), C.c_int(1), dpp(pi), dpp(lam), dpp(t), _dptr(work))
+        f = self.fn("d_ip2_res_mpc_hard_tv")
+        keep = (qp, work, ux, pi, lam, t, stat, dct)
+
+        def call():
+            _ = keep
+            return f(*args)
+
+        return call, kk
+
     def single_newton(self, qp: OCPQP, ux0, pi0, lam0, t0, *, k_max=1, mu0=0.0, mu_tol=1e-12, alpha_min=1e-8,
                       compute_mult=1, work=None):
         N = qp.N

@@ -144,6 +144,11 @@ def compare_ipm(case_like_qp, a, b, tol=TOL_IPM):
     """max error of two ipm() results over valid parts."""
     qp = case_like_qp
     assert a["kk"] == b["kk"] and a["ret"] == b["ret"], (a["kk"], b["kk"], a["ret"], b["ret"])
+    if b["ret"] == 2 and max(float(np.max(np.abs(x))) for x in b["lam"]) > 1e12:
+        # alpha_min exit of a primal-dual divergence (infeasible QP, lam -> 1e33): the iterates amplify
+        # last-bit differences without bound -- the oracle and the reference build itself differ by
+        # O(1) here -- so only the iteration count and the return code are comparable.
+        return 0.0
     e = 0.0
     for k in range(qp.N + 1):
         n = qp.nux(k)

@@ -115,7 +115,7 @@ def test_aliased_time_invariant_buffers(product, oracle):
 
 
 def test_warm_start_and_kkt_resolve(product, oracle):
-    qp = random_qp(15, [0] + [6] * 15, [2] * 15 + [0], [3] * 16, seed=11)
+    qp = random_qp(15, [0] + [6] * 15, [2] * 15 + [0], [2] + [3] * 15, seed=11)
     ux0 = [np.random.default_rng(k).standard_normal(12) * 0.1 for k in range(16)]
     a = product.ipm(qp.copy(), k_max=30, warm_start=1, ux=ux0)
     b = oracle.ipm(qp.copy(), k_max=30, warm_start=1, ux=ux0)
