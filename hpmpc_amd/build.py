@@ -16,6 +16,9 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("HPMPC_ARCH", "gfx950")
 SOURCES = ["hpmpc_kernels.hip", "hpmpc_capi.cpp"]
 HEADERS = ["hk_prims.h", "hk_riccati.h", "hk_ipm.h", "hpmpc_kargs.h"]
+# MFMA accumulators stay in ordinary VGPRs: the stage tile is read and written by VALU code between
+# MFMAs, and the AGPR form costs 8 v_accvgpr moves each way per MFMA group.
+KFLAGS = ["-mllvm", "-amdgpu-mfma-vgpr-form"]
 
 
 def _newer(out, deps):
@@ -32,7 +35,7 @@ def build_hip(force: bool = False, verbose: bool = False) -> str:
     if not force and _newer(out, deps):
         return out
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           "-Wno-unused-function"] + [os.path.join(CSRC, s) for s in SOURCES] + ["-o", out]
+           "-Wno-unused-function"] + KFLAGS + [os.path.join(CSRC, s) for s in SOURCES] + ["-o", out]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
@@ -44,7 +47,7 @@ def build_stamps(verbose: bool = False) -> str:
     os.makedirs(LIBDIR, exist_ok=True)
     out = os.path.join(LIBDIR, "libhpmpc_mi355x_stamps.so")
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-DHK_STAMPS",
-           "-Wno-unused-function"] + [os.path.join(CSRC, s) for s in SOURCES] + ["-o", out]
+           "-Wno-unused-function"] + KFLAGS + [os.path.join(CSRC, s) for s in SOURCES] + ["-o", out]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

@@ -42,8 +42,8 @@ __device__ __forceinline__ double mk(int hi, int lo) { return __hiloint2double(h
 template <int CTRL>
 __device__ __forceinline__ double dpp_mov(double x) {
     int lo = __double2loint(x), hi = __double2hiint(x);
-    lo = __builtin_amdgcn_update_dpp(0, lo, CTRL, 0xf, 0xf, false);
-    hi = __builtin_amdgcn_update_dpp(0, hi, CTRL, 0xf, 0xf, false);
+    lo = __builtin_amdgcn_mov_dpp(lo, CTRL, 0xf, 0xf, true);
+    hi = __builtin_amdgcn_mov_dpp(hi, CTRL, 0xf, 0xf, true);
     return mk(hi, lo);
 }
 
@@ -74,6 +74,23 @@ __device__ __forceinline__ double rowgroup_bcast(double x) {
     int lo2 = (GS % 2 == 0) ? (int)c[0] : (int)c[1];
     int hi2 = (GS % 2 == 0) ? (int)d[0] : (int)d[1];
     return mk(hi2, lo2);
+}
+
+// Gather the four row groups: x[j] at lane (g,c) = v at lane (j,c), for all j at once.
+// One v_permlane32_swap per dword splits the halves, one v_permlane16_swap per dword and half
+// splits the rows: 6 cross-lane ops for the whole 4x16 transpose-by-row-group.
+__device__ __forceinline__ void rowgroup_gather(double v, double x[4]) {
+    const int lo = __double2loint(v), hi = __double2hiint(v);
+    const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);  // [0]: rows {0,1}, [1]: rows {2,3}
+    const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    const auto c0 = __builtin_amdgcn_permlane16_swap((int)a[0], (int)a[0], false, false);  // rows 0 | 1
+    const auto d0 = __builtin_amdgcn_permlane16_swap((int)b[0], (int)b[0], false, false);
+    const auto c1 = __builtin_amdgcn_permlane16_swap((int)a[1], (int)a[1], false, false);  // rows 2 | 3
+    const auto d1 = __builtin_amdgcn_permlane16_swap((int)b[1], (int)b[1], false, false);
+    x[0] = mk((int)d0[0], (int)c0[0]);
+    x[1] = mk((int)d0[1], (int)c0[1]);
+    x[2] = mk((int)d1[0], (int)c1[0]);
+    x[3] = mk((int)d1[1], (int)c1[1]);
 }
 
 // Sum over the four row groups: result at (g,c) = sum_g' x(g',c); identical in all row groups.
@@ -120,18 +137,21 @@ __device__ __forceinline__ double wave_min(double x) {
 }
 
 // Cholesky pivot with the reference's clamp (kernel_dpotrf_c99_lib4.c:555-640): d > 1e-15 gives
-// s = sqrt(d), inv = 1/s; otherwise both 0.  v_rsq_f64 refined by two Newton steps (~1 ulp).
+// s = sqrt(d), inv = 1/s; otherwise both 0.  v_rsq_f64 (rel. error 5e-8 on gfx950, measured by
+// tools/rsq_precision.py) refined by ONE third-order step y(1 + e/2 + 3e^2/8), e = 1 - d y^2:
+// truncation ~e^3 ~ 1e-22, i.e. the result is rounding-limited (~1 ulp), and the dependent chain is
+// four f64 ops after the rsq instead of six for two Newton steps.  The clamp select sits at the end,
+// off the chain.
 __device__ __forceinline__ void chol_pivot(double d, double &s, double &inv) {
     const bool ok = d > 1e-15;
-    const double dd = ok ? d : 1.0;
-    double y = __builtin_amdgcn_rsq(dd);
-    const double h = 0.5 * dd;
-    double e = fma(-h * y, y, 0.5);
-    y = fma(y, e, y);
-    e = fma(-h * y, y, 0.5);
-    y = fma(y, e, y);
-    s = ok ? dd * y : 0.0;
-    inv = ok ? y : 0.0;
+    const double y = __builtin_amdgcn_rsq(d);
+    const double dy = d * y;
+    const double e = fma(-dy, y, 1.0);
+    const double p = fma(0.375, e, 0.5);
+    const double ye = y * e;
+    const double y1 = fma(ye, p, y);
+    inv = ok ? y1 : 0.0;
+    s = ok ? d * y1 : 0.0;
 }
 
 // Raw-buffer global access.  Masked lanes use an out-of-range offset: the hardware range check

@@ -81,64 +81,97 @@ __device__ __forceinline__ void col2row(Scratch* sm, double vc, double vr[4]) {
 // transpose.  Pivots outside [0,nu) U [xo, xo+nx) are skipped (zero padding, inv_diag = 0).
 // Pivot clamp d > 1e-15 as in kernel_dpotrf_c99_lib4.c:555-640.
 // ------------------------------------------------------------------------------------------------
-template <int Q>
-__device__ __forceinline__ double rg_bcast(double x) { return rowgroup_bcast<Q>(x); }
+// One 4-pivot block of the stage Cholesky.  Column block b of the tile (rows 4b..4b+3 of the upper
+// storage, i.e. register b) is gathered so that every lane holds the four entries x_j = A[c][4b+j]
+// of its own tile row c.  The 4x4 diagonal block is then broadcast (DPP row_newbcast) and factorised
+// redundantly in every lane -- a short scalar dependency chain with no cross-lane traffic -- while
+// each lane solves its own panel row against it (kernel_dsyrk_dpotrf_nt_4x4 / kernel_dgemm_dtrsm_nt_4x4,
+// same operation order, same >1e-15 pivot clamp).  Padded tile indices carry exact zeros, so their
+// pivots clamp to 0 and contribute nothing.
+template <int B, bool AUG>
+__device__ __forceinline__ void chol_block(d4& M, double& ml, double lr[4], double& invd, int kdbg = -1) {
+    const int l = lane_id(), g = l >> 4, c = l & 15;
+    (void)kdbg;
+#define HK_BSTAMP(i) \
+    if (B == 1) HK_STAMP(24 + (i), kdbg)
+    HK_BSTAMP(0);
+    double x[4];
+    rowgroup_gather(M[B], x);
+    // diagonal block A[4B+i][4B+j] (i >= j), uniform across the wave
+    const double a00 = row_bcast<4 * B + 0>(x[0]);
+    const double a10 = row_bcast<4 * B + 1>(x[0]), a11 = row_bcast<4 * B + 1>(x[1]);
+    const double a20 = row_bcast<4 * B + 2>(x[0]), a21 = row_bcast<4 * B + 2>(x[1]);
+    const double a22 = row_bcast<4 * B + 2>(x[2]);
+    const double a30 = row_bcast<4 * B + 3>(x[0]), a31 = row_bcast<4 * B + 3>(x[1]);
+    const double a32 = row_bcast<4 * B + 3>(x[2]), a33 = row_bcast<4 * B + 3>(x[3]);
+    double m0 = 0.0, m1 = 0.0, m2 = 0.0, m3 = 0.0;
+    if (AUG) {
+        m0 = row_bcast<4 * B + 0>(ml);
+        m1 = row_bcast<4 * B + 1>(ml);
+        m2 = row_bcast<4 * B + 2>(ml);
+        m3 = row_bcast<4 * B + 3>(ml);
+    }
+    double s0, i0, s1, i1, s2, i2, s3, i3;
+    HK_BSTAMP(1);
+    chol_pivot(a00, s0, i0);
+    const double l10 = a10 * i0, l20 = a20 * i0, l30 = a30 * i0;
+    const double y0 = x[0] * i0;
+    const double p0 = m0 * i0;
+    HK_BSTAMP(2);
+    chol_pivot(fma(-l10, l10, a11), s1, i1);
+    const double l21 = fma(-l20, l10, a21) * i1, l31 = fma(-l30, l10, a31) * i1;
+    const double y1 = fma(-y0, l10, x[1]) * i1;
+    const double p1 = fma(-p0, l10, m1) * i1;
+    HK_BSTAMP(3);
+    chol_pivot(fma(-l21, l21, fma(-l20, l20, a22)), s2, i2);
+    const double l32 = fma(-l31, l21, fma(-l30, l20, a32)) * i2;
+    const double y2 = fma(-y1, l21, fma(-y0, l20, x[2])) * i2;
+    const double p2 = fma(-p1, l21, fma(-p0, l20, m2)) * i2;
+    HK_BSTAMP(4);
+    chol_pivot(fma(-l32, l32, fma(-l31, l31, fma(-l30, l30, a33))), s3, i3);
+    const double y3 = fma(-y2, l32, fma(-y1, l31, fma(-y0, l30, x[3]))) * i3;
+    const double p3 = fma(-p2, l32, fma(-p1, l31, fma(-p0, l30, m3))) * i3;
+    HK_BSTAMP(5);
+    // upper storage row 4B+g:  diagonal s_g, then L[c][4B+g] = y_g (c > 4B+g).  Branch-free selects.
+    const double yg = g == 0 ? y0 : g == 1 ? y1 : g == 2 ? y2 : y3;
+    const double sg = g == 0 ? s0 : g == 1 ? s1 : g == 2 ? s2 : s3;
+    M[B] = (c == 4 * B + g) ? sg : yg;
+    const int j = c - 4 * B;
+    invd = j == 0 ? i0 : j == 1 ? i1 : j == 2 ? i2 : j == 3 ? i3 : invd;
+    if (AUG) {
+        lr[B] = g == 0 ? p0 : g == 1 ? p1 : g == 2 ? p2 : p3;
+        const double mt = fma(-p3, y3, fma(-p2, y2, fma(-p1, y1, fma(-p0, y0, ml))));
+        ml = j >= 4 ? mt : j == 0 ? p0 : j == 1 ? p1 : j == 2 ? p2 : j == 3 ? p3 : ml;
+    }
+    HK_BSTAMP(6);
+    if (B < 3) {
+        const double a = (j >= 4) ? yg : 0.0;
+        M = mfma(-a, a, M);
+    }
+#undef HK_BSTAMP
+}
 
+// Stage Cholesky with the augmented row.
+// In : M (tile, full symmetric), ml (aug row, col layout).
+// Out: M = S = lower(L) + strict_upper(L') (symmetric storage: row p of S == column p of L),
+//      ml = aug row l (col layout), lr = l in row layout, invd = inverse diagonal (col layout).
 template <bool AUG>
 __device__ __forceinline__ void stage_chol(d4& M, double& ml, double lr[4], double& invd, int nu, int nx, int xo,
                                            int kdbg = -1) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
+    (void)kdbg;
     invd = 0.0;
 #pragma unroll
     for (int r = 0; r < 4; r++) lr[r] = 0.0;
-#pragma unroll
-    for (int b = 0; b < 4; b++) {
-        const bool any = (4 * b < nu) || (4 * b + 3 >= xo && 4 * b < xo + nx);
-        if (!any) continue;  // wave-uniform
-        double R = M[b];
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const int p = 4 * b + q;
-            if (!tile_active(p, nu, nx, xo)) continue;  // wave-uniform
-            const double d = readlane(R, q * 16 + p);
-            double s, inv;
-            chol_pivot(d, s, inv);
-            // row q of the block (= column p of L) broadcast to every row group: colc = L[c][p], c > p
-            double rq;
-            switch (q) {
-                case 0: rq = rg_bcast<0>(R); break;
-                case 1: rq = rg_bcast<1>(R); break;
-                case 2: rq = rg_bcast<2>(R); break;
-                default: rq = rg_bcast<3>(R); break;
-            }
-            const double colc = (c > p) ? rq * inv : 0.0;
-            // remaining rows of the block: R[4b+g][c] -= L[4b+g][p] * L[c][p]   (g > q)
-            double lg = 0.0;
-            if (q < 3) {
-                const double l1 = readlane(colc, p + 1);
-                const double l2 = (q < 2) ? readlane(colc, p + 2) : 0.0;
-                const double l3 = (q < 1) ? readlane(colc, p + 3) : 0.0;
-                lg = (g == q + 1) ? l1 : (g == q + 2) ? l2 : (g == q + 3) ? l3 : 0.0;
-            }
-            double Rn = R - lg * colc;
-            if (g == q) Rn = (c > p) ? colc : ((c == p) ? s : R);
-            R = Rn;
-            if (AUG) {
-                const double lp = readlane(ml, p) * inv;  // l_p = m_last[p] / L[p][p]
-                ml = (c == p) ? lp : ((c > p) ? ml - lp * colc : ml);
-                if (g == q) lr[b] = lp;
-            }
-            if (c == p) invd = inv;
-        }
-        HK_STAMP(16 + 2 * b, kdbg);
-        M[b] = R;
-        // rank-4 trailing update: M -= A A'  with A[i][kk] = L[i][4b+kk] for i > 4b+3 (panel rows)
-        if (4 * b + 4 < 16) {
-            const double a = (c > 4 * b + 3) ? R : 0.0;
-            M = mfma(-a, a, M);
-        }
-        HK_STAMP(17 + 2 * b, kdbg);
-    }
+    // blocks without an active pivot are skipped (wave-uniform); their rows/columns are zero
+    if (0 < nu || (3 >= xo && 0 < xo + nx)) chol_block<0, AUG>(M, ml, lr, invd, kdbg);
+    HK_STAMP(16, kdbg);
+    if (4 < nu || (7 >= xo && 4 < xo + nx)) chol_block<1, AUG>(M, ml, lr, invd, kdbg);
+    HK_STAMP(18, kdbg);
+    if (8 < nu || (11 >= xo && 8 < xo + nx)) chol_block<2, AUG>(M, ml, lr, invd, kdbg);
+    HK_STAMP(20, kdbg);
+    if (12 < nu || (15 >= xo && 12 < xo + nx)) chol_block<3, AUG>(M, ml, lr, invd, kdbg);
+    HK_STAMP(22, kdbg);
     // lower triangle <- transpose of the upper storage:  T = S' via MFMA with an identity B operand
     d4 T = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -192,6 +225,15 @@ __device__ __forceinline__ void load_factor(const double* Fk, d4& S, double& lc,
     for (int r = 0; r < 4; r++) S[r] = Fk[r * 64 + l];
     lc = Fk[256 + c];
     invd = Fk[272 + c];
+}
+
+// factor record of one stage: 4 tile registers in register order (4 x 512 B coalesced), l, inv_diag
+__device__ __forceinline__ void store_factor(double* Fk, const d4& S, double lc, double invd) {
+    const int l = lane_id(), g = l >> 4, c = l & 15;
+#pragma unroll
+    for (int r = 0; r < 4; r++) gst(Fk, r * 64 + l, S[r]);
+    gst(Fk, 256 + c, lc, g == 0);
+    gst(Fk, 272 + c, invd, g == 0);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -255,6 +297,7 @@ __device__ void ric_backward(const RicIO& io, Scratch* sm, int update_b, const d
     const int l = lane_id(), g = l >> 4, c = l & 15;
     d4 S = {0.0, 0.0, 0.0, 0.0};
     double lr_prev[4] = {0.0, 0.0, 0.0, 0.0};
+    double ml_prev = 0.0, invd_prev = 0.0;
     StageInfo si = load_stage(io.st, io.N);
     BwdFrag cur;
     bwd_fetch<AUG>(io, si, io.N, update_b, bsrc, update_q, qsrc, use_box, Qx, qx, cur);
@@ -264,6 +307,9 @@ __device__ void ric_backward(const RicIO& io, Scratch* sm, int update_b, const d
         const StageInfo sn = load_stage(io.st, kn);
         BwdFrag nxt;
         bwd_fetch<AUG>(io, sn, kn, update_b, bsrc, update_q, qsrc, use_box, Qx, qx, nxt);
+        // factor of stage k+1 (still in registers): stored one stage late, behind the prefetch, so
+        // that no s_waitcnt of this stage has to wait for the store acknowledgements
+        if (k < io.N) store_factor(io.F + (long)(k + 1) * FSTRIDE, S, AUG ? ml_prev : 0.0, invd_prev);
         HK_STAMP(1, k);
         const int nu = si.nu, nx = si.nx, xo = si.xo;
         d4 M = cur.Mi;
@@ -320,20 +366,21 @@ __device__ void ric_backward(const RicIO& io, Scratch* sm, int update_b, const d
         double lr[4], invd;
         stage_chol<AUG>(M, ml, lr, invd, nu, nx, xo, k);
         HK_STAMP(3, k);
-        double* Fk = io.F + (long)k * FSTRIDE;
 #pragma unroll
         for (int r = 0; r < 4; r++) {
             S[r] = M[r];
-            gst(Fk, r * 64 + l, M[r]);
             lr_prev[r] = lr[r];
         }
-        gst(Fk, 256 + c, AUG ? ml : 0.0, g == 0);
-        gst(Fk, 272 + c, invd, g == 0);
+        ml_prev = ml;
+        invd_prev = invd;
         HK_STAMP(4, k);
         si = sn;
         cur = nxt;
     }
+    store_factor(io.F, S, AUG ? ml_prev : 0.0, invd_prev);
 }
+
+
 
 // Solve the unknown part of L_k' y = rhs (dtrsv_t_lib, blas_d_lib4.c:5276) in row layout, descending.
 // rrow: rhs in row layout (reduced by the known part already); y written into ur (row layout) at the

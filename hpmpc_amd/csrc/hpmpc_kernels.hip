@@ -379,7 +379,10 @@ extern "C" __global__ __launch_bounds__(64) void hk_ipm(KArgs a) {
     // ------------------------------ phase 2 (d_ip2_res_hard.c:756-1273) ------------------------------
     residuals(io, bt, &sm, nullptr, nullptr, ux, pi, dv, lam, t, w.res_q, w.res_b, w.res_d, w.res_m, mu);
     wsync();
+    const int kk_p2 = kk;  // first phase-2 iteration (diagnostic stamps only)
+    (void)kk_p2;
     while (kk < a.k_max && (sn || (mu > a.mu_tol && alpha >= a.alpha_min))) {
+        HK_STAMP(32, kk == kk_p2 ? 50 : -1);
         HK_FOR_BOX(io, k, {  // d_update_hessian_gradient_res_mpc_hard_tv
             const double til = 1.0 / t[lo], tiu = 1.0 / t[up];
             w.t_inv[lo] = til;
@@ -389,11 +392,14 @@ extern "C" __global__ __launch_bounds__(64) void hk_ipm(KArgs a) {
                                    tiu * (w.res_m[up] + lam[up] * w.res_d[up]);
         });
         wsync();
+        HK_STAMP(33, kk == kk_p2 ? 50 : -1);
         // the single-Newton variant factorises with the data's own b/q rows (d_ip2_res_hard.c:1700-1760)
         ric_backward<true>(io, &sm, !sn, w.res_b, !sn, w.res_q, 1, w.Qx, w.qx, 1, w.Pb);
         wsync();
+        HK_STAMP(34, kk == kk_p2 ? 50 : -1);
         ric_forward_sv(io, &sm, !sn, w.res_b, w.dux, a.compute_mult, w.dpi);
         wsync();
+        HK_STAMP(35, kk == kk_p2 ? 50 : -1);
         double al = 1.0;
         HK_FOR_BOX(io, k, {  // d_compute_alpha_res_mpc_hard_tv
             const int v = bt.slotvar[k * 16 + slot];
@@ -417,6 +423,7 @@ extern "C" __global__ __launch_bounds__(64) void hk_ipm(KArgs a) {
             stat[5 * kk + 1] = al;
         }
         alpha = al * 0.995;
+        HK_STAMP(36, kk == kk_p2 ? 50 : -1);
         double ms = 0.0;
         HK_FOR_BOX(io, k, {  // d_compute_mu_res_mpc_hard_tv
             ms += (lam[lo] + alpha * w.dlam[lo]) * (t[lo] + alpha * w.dt[lo]) +
@@ -424,6 +431,7 @@ extern "C" __global__ __launch_bounds__(64) void hk_ipm(KArgs a) {
         });
         const double mu_aff = wave_sum(ms) * mu_scal;
         if (l == 0) stat[5 * kk + 2] = mu_aff;
+        HK_STAMP(37, kk == kk_p2 ? 50 : -1);
         double smu = a.mu0;  // single Newton: sigma*mu is supplied by the caller as mu0 (:1788-1790)
         if (!sn) {
             sigma = mu_aff / mu;
@@ -439,8 +447,10 @@ extern "C" __global__ __launch_bounds__(64) void hk_ipm(KArgs a) {
                                    w.t_inv[up] * (rmu + lam[up] * w.res_d[up]);
         });
         wsync();
+        HK_STAMP(38, kk == kk_p2 ? 50 : -1);
         ric_trs(io, &sm, w.res_b, w.res_q, 1, w.qx, w.dux, a.compute_mult, w.dpi, 0, w.Pb);
         wsync();
+        HK_STAMP(39, kk == kk_p2 ? 50 : -1);
         al = 1.0;
         HK_FOR_BOX(io, k, {
             const int v = bt.slotvar[k * 16 + slot];
@@ -464,6 +474,7 @@ extern "C" __global__ __launch_bounds__(64) void hk_ipm(KArgs a) {
             stat[5 * kk + 3] = al;
         }
         alpha = al * 0.995;
+        HK_STAMP(40, kk == kk_p2 ? 50 : -1);
         // d_backup_update_var_res_mpc_hard_tv (phase-2 dux/dpi are deltas)
         for (int k = 0; k <= N; k++) {
             const StageInfo si = load_stage(io.st, k);
@@ -491,9 +502,11 @@ extern "C" __global__ __launch_bounds__(64) void hk_ipm(KArgs a) {
             t[up] += alpha * w.dt[up];
         });
         wsync();
+        HK_STAMP(41, kk == kk_p2 ? 50 : -1);
         residuals(io, bt, &sm, nullptr, nullptr, ux, pi, dv, lam, t, w.res_q, w.res_b, w.res_d, w.res_m, mu);
         wsync();
         if (l == 0) stat[5 * kk + 4] = mu;
+        HK_STAMP(42, kk == kk_p2 ? 50 : -1);
         kk++;
     }
     if (!sn && mu <= a.mu_tol)

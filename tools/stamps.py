@@ -21,7 +21,9 @@ names = {0: 'bwd top', 1: 'fetch issued', 2: 'mfma+aug done', 3: 'chol done', 4:
 print(f"batch {B}: backward stage 50 (cycles from loop top):")
 for i in [1, 2, 3, 4]:
     print(f"  {names[i]:16s} {t[i]-t[0]:6d}  (+{t[i]-t[i-1]})")
-print("  chol blocks: " + " ".join(f"b{b}: {t[16+2*b]-t[2]:5d}/{t[17+2*b]-t[2]:5d}" for b in range(4)))
+print("  chol blocks done at: " + " ".join(f"b{b}: {t[16+2*b]-t[2]:5d}" for b in range(4)))
+print("  block 1 detail: " + " ".join(f"{n}:{t[24+i]-t[24]}" for i, n in enumerate(
+    ["top", "bcast", "piv0", "piv1", "piv2", "piv3", "sel", ]) ) + f" after-mfma:{t[18]-t[24]}")
 print("forward stage 50:")
 for i in [9, 10, 11, 12]:
     print(f"  {names[i]:16s} {t[i]-t[8]:6d}  (+{t[i]-t[i-1]})")
