@@ -69,6 +69,21 @@ __device__ __forceinline__ void col2row(Scratch* sm, double vc, double vr[4]) {
     __builtin_amdgcn_wave_barrier();
 }
 
+// row layout (reg r holds v[g+4r], replicated over the columns) -> col layout (lane (g,c) holds v[c])
+__device__ __forceinline__ double row2col(Scratch* sm, const double vr[4]) {
+    const int l = lane_id(), g = l >> 4, c = l & 15;
+    if (c == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; r++) sm->v[16 + g + 4 * r] = vr[r];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const double v = sm->v[16 + c];
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    return v;
+}
+
 // ------------------------------------------------------------------------------------------------
 // Stage Cholesky with the augmented row, blocked by 4 (one tile register per block row).
 // In : M (tile, full symmetric), ml (aug row, col layout).
@@ -211,9 +226,52 @@ __device__ __forceinline__ StageInfo load_stage(const StageInfo* st, int k) {
     u.oR = __builtin_amdgcn_readfirstlane(v.oR);
     u.oD = __builtin_amdgcn_readfirstlane(v.oD);
     u.pnb = __builtin_amdgcn_readfirstlane(v.pnb);
-    u.r0 = 0;
+    u.r0 = __builtin_amdgcn_readfirstlane(v.r0);  // stage belongs to the compiled inner class
     u.r1 = 0;
     return u;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Stage-shape policies.  Every per-stage routine is written once against a shape object `sh`:
+//   DynSh          -- all sizes from the stage table (any problem the plan accepts);
+//   FixSh<NU, NX>  -- the batch's uniform inner stages (1 <= k <= N-2: nu = NU, nx = NX, next stage
+//                     the same), sizes as compile-time constants, so every tile mask, loop bound and
+//                     "is this pivot active" test folds away.
+// A kernel compiled for FixSh<NU,NX> takes the constant path on every stage the host flagged
+// (StageInfo.r0) and the runtime path elsewhere (first / last stages, irregular problems).
+// ------------------------------------------------------------------------------------------------
+struct DynSh {
+    static constexpr bool fixed = false;
+    int nu, nx, xo, nx1, nu1, xo1, sdB, sdR, nb, pnb, oB, oR;
+    __device__ __forceinline__ explicit DynSh(const StageInfo& s)
+        : nu(s.nu), nx(s.nx), xo(s.xo), nx1(s.nx1), nu1(s.nu1), xo1(s.xo1), sdB(s.sdB), sdR(s.sdR), nb(s.nb),
+          pnb(s.pnb), oB(s.oB), oR(s.oR) {}
+};
+
+template <int NU, int NX>
+struct FixSh {
+    static constexpr bool fixed = true, enabled = true;
+    static constexpr int nu = NU, nx = NX, xo = (NU + 3) / 4 * 4, nx1 = NX, nu1 = NU, xo1 = xo,
+                         sdB = (NX + 1) / 2 * 2, sdR = (NU + NX + 1) / 2 * 2;
+    int nb, pnb, oB, oR;
+    __device__ __forceinline__ explicit FixSh(const StageInfo& s) : nb(s.nb), pnb(s.pnb), oB(s.oB), oR(s.oR) {}
+};
+
+struct NoFix {  // generic kernels: no compile-time stage class
+    static constexpr bool enabled = false;
+    __device__ __forceinline__ explicit NoFix(const StageInfo&) {}
+};
+
+// Run f(sh) with the stage's shape object: the constant one when the stage belongs to FX's class.
+template <class FX, class F>
+__device__ __forceinline__ void with_shape(const StageInfo& s, F&& f) {
+    if constexpr (FX::enabled) {
+        if (s.r0) {
+            f(FX(s));
+            return;
+        }
+    }
+    f(DynSh(s));
 }
 
 // lower / upper part of the symmetric factor storage S (lane (g,c), reg r = S[g+4r][c])
@@ -228,151 +286,259 @@ __device__ __forceinline__ void load_factor(const double* Fk, d4& S, double& lc,
 }
 
 // factor record of one stage: 4 tile registers in register order (4 x 512 B coalesced), l, inv_diag
-__device__ __forceinline__ void store_factor(double* Fk, const d4& S, double lc, double invd) {
+// (ok == false still issues the six stores, out of range, so that every path through a stage loop has
+// the same number of vector-memory ops and the compiler's counted s_waitcnt stays exact)
+__device__ __forceinline__ void store_factor(double* Fk, const d4& S, double lc, double invd, bool ok = true) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
 #pragma unroll
-    for (int r = 0; r < 4; r++) gst(Fk, r * 64 + l, S[r]);
-    gst(Fk, 256 + c, lc, g == 0);
-    gst(Fk, 272 + c, invd, g == 0);
+    for (int r = 0; r < 4; r++) gst(Fk, r * 64 + l, S[r], ok);
+    gst(Fk, 256 + c, lc, ok && g == 0);
+    gst(Fk, 272 + c, invd, ok && g == 0);
 }
 
 // ------------------------------------------------------------------------------------------------
-// Stage-data fragments.  Every pass over the stages issues the HBM loads of the NEXT stage (into
+// IPM box terms fused into the stage passes (mpc_solvers/c99/d_aux_ip_hard_lib4.c).  Instead of
+// separate element-wise passes over all stages (each paying a full memory round trip per stage), the
+// box-constraint vectors of stage k are prefetched together with the stage's Riccati data and
+// combined where the stage pass needs them:
+//   backward (sv)  : Hessian / gradient terms   d_update_hessian_[res_]mpc_hard_tv
+//   forward        : step, dual step and alpha  d_compute_alpha_[res_]mpc_hard_tv
+//   backward (trs) : corrector gradient         d_update_gradient_[res_]mpc_hard_tv (+ centering)
+// A lane of tile column c handles the box attached to tile index c (if any); row group 0 stores.
+// ------------------------------------------------------------------------------------------------
+enum BoxMode { BX_NONE = 0, BX_GIVEN = 1, BX_P1 = 2, BX_P2 = 3 };
+
+struct BoxCtx {
+    const double* d;                                   // bounds [lb (pnb) | ub (pnb)], V32 per stage
+    double *lam, *t;                                   // iterate (V32)
+    double *dlam, *dt, *t_inv, *lamt, *res_d, *res_m;  // IPM work vectors (V32)
+    double* qxs;                                       // phase-1 gradient (V16, slot order)
+    const double *Qx, *qx;                             // BX_GIVEN terms (V16, slot order)
+    double smu;                                        // centering target of the trs box modes
+    int pred;                                          // forward BX_P1: predictor step (dlam = 0)
+};
+
+struct BoxLane {
+    int lo, up, s16;  // element indices of this lane's box in the V32 / V16 arrays
+    bool ok;          // tile index c carries a box
+};
+
+__device__ __forceinline__ BoxLane box_lane(const signed char* tileslot, int pnb, int k) {
+    const int c = lane_id() & 15;
+    const int slot = tileslot[k * 16 + c];
+    BoxLane b;
+    b.ok = slot >= 0;
+    b.lo = k * V32 + slot;
+    b.up = b.lo + pnb;
+    b.s16 = k * V16 + slot;
+    return b;
+}
+
+// sequential step-length rule of d_compute_alpha_* (d_aux_ip_hard_lib4.c:541-565), per lane
+__device__ __forceinline__ void alpha_rule(double& al, double v, double dv) {
+    if (-al * dv > v) al = -v / dv;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Backward factorisation.  Every pass over the stages issues the HBM loads of the NEXT stage (into
 // registers) before it computes the current one, so the dependent recursion never waits on memory.
 // ------------------------------------------------------------------------------------------------
 struct BwdFrag {
     d4 Mi;         // RSQrq tile (mirrored lower part), tile coords of stage k
     double mlq;    // augmented-row source: q (update_q) or the RSQrq last row
-    double dq;     // box Hessian term on this lane's diagonal slot (Qx), 0 if none
-    double qxv;    // box gradient term (qx), 0 if none
     d4 bop;        // MFMA B operand per K-chunk: BAbt_k[var(c)][4kc+g-xo1]
     d4 brow;       // b_k in row layout over the stage-(k+1) tile rows
+    double bx[8];  // box-mode inputs of tile c
+    BoxLane bl;
 };
 
-template <bool AUG>
-__device__ __forceinline__ void bwd_fetch(const RicIO& io, const StageInfo& si, int k, int update_b,
-                                          const double* bsrc, int update_q, const double* qsrc, int use_box,
-                                          const double* Qx, const double* qx, BwdFrag& f) {
+template <bool AUG, int BM, class SH>
+__device__ __forceinline__ void bwd_fetch(const RicIO& io, const SH& sh, int k, int update_b, const double* bsrc,
+                                          int update_q, const double* qsrc, const BoxCtx& bc, BwdFrag& f) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
-    const int nu = si.nu, nx = si.nx, xo = si.xo, nux = nu + nx;
-    const double* R = io.RSQ + si.oR;
-    const int vc = tile_var(c, nu, nx, xo);
+    const int nux = sh.nu + sh.nx;
+    const double* R = io.RSQ + sh.oR;
+    const int vc = tile_var(c, sh.nu, sh.nx, sh.xo);
 #pragma unroll
     for (int r = 0; r < 4; r++) {
-        const int vi = tile_var(g + 4 * r, nu, nx, xo);
+        const int vi = tile_var(g + 4 * r, sh.nu, sh.nx, sh.xo);
         const int hi = vi > vc ? vi : vc, lo = vi > vc ? vc : vi;
-        f.Mi[r] = ldsel(R, lib4_idx(si.sdR, hi, lo), vi >= 0 && vc >= 0);
+        f.Mi[r] = ldsel(R, lib4_idx(sh.sdR, hi, lo), vi >= 0 && vc >= 0);
     }
     f.mlq = 0.0;
     if (AUG) {
         const double* qp = update_q ? qsrc + k * V16 : R;
-        const int qi = update_q ? vc : lib4_idx(si.sdR, nux, vc);
+        const int qi = update_q ? vc : lib4_idx(sh.sdR, nux, vc);
         f.mlq = ldsel(qp, qi, vc >= 0);
     }
-    const int slot = io.tileslot[k * 16 + c];
-    const bool bx = use_box && slot >= 0;
-    f.dq = ldsel(use_box ? Qx : R, k * V16 + slot, bx);
-    f.qxv = AUG ? ldsel(use_box ? qx : R, k * V16 + slot, bx) : 0.0;
-    const int nx1 = si.nx1, xo1 = si.xo1;
-    const double* Bk = io.BAbt + si.oB;
+    const BoxLane b = box_lane(io.tileslot, sh.pnb, k);
+    f.bl = b;
+#pragma unroll
+    for (int i = 0; i < 8; i++) f.bx[i] = 0.0;
+    if (BM == BX_GIVEN) {
+        f.bx[0] = ldsel(bc.Qx, b.s16, b.ok);
+        f.bx[1] = AUG ? ldsel(bc.qx, b.s16, b.ok) : 0.0;
+    } else if (BM == BX_P1) {
+        f.bx[0] = ldsel(bc.lam, b.lo, b.ok);
+        f.bx[1] = ldsel(bc.lam, b.up, b.ok);
+        f.bx[2] = ldsel(bc.t, b.lo, b.ok);
+        f.bx[3] = ldsel(bc.t, b.up, b.ok);
+        f.bx[4] = ldsel(bc.d, b.lo, b.ok);
+        f.bx[5] = ldsel(bc.d, b.up, b.ok);
+    } else if (BM == BX_P2) {
+        f.bx[0] = ldsel(bc.lam, b.lo, b.ok);
+        f.bx[1] = ldsel(bc.lam, b.up, b.ok);
+        f.bx[2] = ldsel(bc.t, b.lo, b.ok);
+        f.bx[3] = ldsel(bc.t, b.up, b.ok);
+        f.bx[4] = ldsel(bc.res_m, b.lo, b.ok);
+        f.bx[5] = ldsel(bc.res_m, b.up, b.ok);
+        f.bx[6] = ldsel(bc.res_d, b.lo, b.ok);
+        f.bx[7] = ldsel(bc.res_d, b.up, b.ok);
+    }
+    const bool live = SH::fixed || k < io.N;
+    const double* Bk = io.BAbt + sh.oB;
     const double* bp = update_b ? bsrc + k * V16 : Bk;
 #pragma unroll
     for (int r = 0; r < 4; r++) {
-        const int s = 4 * r + g - xo1;
-        const bool ok = (k < io.N) && s >= 0 && s < nx1;
-        f.bop[r] = ldsel(Bk, lib4_idx(si.sdB, vc, s), ok && vc >= 0);
-        f.brow[r] = AUG ? ldsel(bp, update_b ? s : lib4_idx(si.sdB, nux, s), ok) : 0.0;
+        const int s = 4 * r + g - sh.xo1;
+        const bool ok = live && s >= 0 && s < sh.nx1;
+        f.bop[r] = ldsel(Bk, lib4_idx(sh.sdB, vc, s), ok && vc >= 0);
+        f.brow[r] = AUG ? ldsel(bp, update_b ? s : lib4_idx(sh.sdB, nux, s), ok) : 0.0;
     }
+}
+
+// Box Hessian (dq, on the tile diagonal) and gradient (qxv, on the augmented row) of tile c.
+template <bool AUG, int BM>
+__device__ __forceinline__ void box_hessian(const BoxCtx& bc, const BwdFrag& f, double& dq, double& qxv) {
+    const int g = lane_id() >> 4;
+    const BoxLane& b = f.bl;
+    const bool st = b.ok && g == 0;
+    dq = 0.0;
+    qxv = 0.0;
+    if (BM == BX_GIVEN) {
+        dq = f.bx[0];
+        qxv = f.bx[1];
+    } else if (BM == BX_P1) {  // d_update_hessian_mpc_hard_tv with sigma*mu = 0 (phase 1)
+        const double til = 1.0 / f.bx[2], tiu = 1.0 / f.bx[3];
+        const double ltl = f.bx[0] * til, ltu = f.bx[1] * tiu;
+        const double dll = til * 0.0, dlu = tiu * 0.0;
+        const double q = f.bx[1] - ltu * f.bx[5] + dlu - f.bx[0] - ltl * f.bx[4] - dll;
+        gst(bc.t_inv, b.lo, til, st);
+        gst(bc.t_inv, b.up, tiu, st);
+        gst(bc.lamt, b.lo, ltl, st);
+        gst(bc.lamt, b.up, ltu, st);
+        gst(bc.qxs, b.s16, q, st);
+        dq = b.ok ? ltl + ltu : 0.0;
+        qxv = (AUG && b.ok) ? q : 0.0;
+    } else if (BM == BX_P2) {  // d_update_hessian_gradient_res_mpc_hard_tv
+        const double til = 1.0 / f.bx[2], tiu = 1.0 / f.bx[3];
+        const double q = til * (f.bx[4] - f.bx[0] * f.bx[6]) - tiu * (f.bx[5] + f.bx[1] * f.bx[7]);
+        gst(bc.t_inv, b.lo, til, st);
+        gst(bc.t_inv, b.up, tiu, st);
+        dq = b.ok ? til * f.bx[0] + tiu * f.bx[1] : 0.0;
+        qxv = (AUG && b.ok) ? q : 0.0;
+    }
+}
+
+// One backward stage: M = RSQ + W W' (+ box terms) with W' = Lxx_{k+1}' BAbt_k', then the stage
+// Cholesky.  S (in: factor of stage k+1, out: factor of stage k), lr/ml/invd likewise.
+template <bool AUG, int BM, class SH>
+__device__ __forceinline__ void bwd_step(const RicIO& io, Scratch* sm, const SH& sh, int k, const BwdFrag& cur,
+                                         const BoxCtx& bc, int compute_Pb, double* Pb, d4& S, double lr_prev[4],
+                                         double& ml_prev, double& invd_prev) {
+    const int l = lane_id(), g = l >> 4, c = l & 15;
+    const bool live = SH::fixed || k < io.N;
+    double dq, qxv;
+    box_hessian<AUG, BM>(bc, cur, dq, qxv);
+    d4 M = cur.Mi;
+    double ml = cur.mlq + qxv;  // update_q row (or RSQrq row) + drowad qx
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+        if (g + 4 * r == c) M[r] += dq;  // ddiaadin: diag = bd + Qx
+    const int nx1 = sh.nx1, xo1 = sh.xo1;
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+    if (live) {
+        // W' = Lxx_{k+1}' BAbt_k'  (dtrmm_nt_u, d_back_ric_rec.c:262-264), rows in stage-(k+1) tile coords
+#pragma unroll
+        for (int kc = 0; kc < 4; kc++) {
+            if (4 * kc + 3 < xo1 || 4 * kc >= xo1 + nx1) continue;  // uniform
+            const double aop = (c >= xo1 && 4 * kc + g >= c) ? S[kc] : 0.0;
+            acc = mfma(aop, cur.bop[kc], acc);
+        }
+        // M += W W'  (dsyrk part of dsyrk_dpotrf_lib, :325)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            if (4 * r + 3 < xo1 || 4 * r >= xo1 + nx1) continue;
+            M = mfma(acc[r], acc[r], M);
+        }
+    }
+    if (AUG) {
+        // v = Lxx' b (col layout, stage k+1 tile); zero at k = N (no next stage)
+        double part = 0.0;
+#pragma unroll
+        for (int r = 0; r < 4; r++) part += (c >= xo1 ? lowS(S, r, g, c) : 0.0) * cur.brow[r];
+        const double vcol = xrow_sum(part);
+        double vrow[4];
+        col2row(sm, vcol, vrow);
+        // Pb_k = Lxx (Lxx' b)  (dtrmv_u_t on W's last row, :266-275); store masked, never skipped
+        double pp = 0.0;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int j = g + 4 * r;
+            pp += (j <= c && j >= xo1) ? S[r] * vrow[r] : 0.0;
+        }
+        const double pb = xrow_sum(pp);
+        gst(Pb, k * V16 + (c - xo1), pb, compute_Pb && live && g == 0 && c >= xo1 && c < xo1 + nx1);
+        // w_last = b' Lxx + l_{k+1,x}   (dgead, :276)  -> m_last += W w_last
+        double mp = 0.0;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const double w = (g + 4 * r >= xo1) ? vrow[r] + lr_prev[r] : 0.0;
+            mp += acc[r] * w;
+        }
+        if (live) ml += xrow_sum(mp);
+    }
+    HK_STAMP(2, k);
+    double lr[4], invd;
+    stage_chol<AUG>(M, ml, lr, invd, sh.nu, sh.nx, sh.xo, k);
+    HK_STAMP(3, k);
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        S[r] = M[r];
+        lr_prev[r] = lr[r];
+    }
+    ml_prev = ml;
+    invd_prev = invd;
 }
 
 // Backward Riccati recursion (sv when AUG, trf otherwise), d_back_ric_rec.c:186-335 / :447-558.
 //   b  (state order) / q (variable order) : update_b / update_q replacement rows
-//   Qx, qx (box-slot order)               : box Hessian / gradient terms (use_box)
+//   BM                                    : box Hessian / gradient terms (BoxMode)
 //   Pb (state order)                      : P_{k+1} b_k (compute_Pb, AUG only)
 // Vector arguments use a per-stage stride of V16.
-template <bool AUG>
+template <bool AUG, int BM, class FX>
 __device__ void ric_backward(const RicIO& io, Scratch* sm, int update_b, const double* bsrc, int update_q,
-                             const double* qsrc, int use_box, const double* Qx, const double* qx, int compute_Pb,
-                             double* Pb) {
-    const int l = lane_id(), g = l >> 4, c = l & 15;
+                             const double* qsrc, const BoxCtx& bc, int compute_Pb, double* Pb) {
     d4 S = {0.0, 0.0, 0.0, 0.0};
     double lr_prev[4] = {0.0, 0.0, 0.0, 0.0};
     double ml_prev = 0.0, invd_prev = 0.0;
     StageInfo si = load_stage(io.st, io.N);
     BwdFrag cur;
-    bwd_fetch<AUG>(io, si, io.N, update_b, bsrc, update_q, qsrc, use_box, Qx, qx, cur);
+    with_shape<FX>(si, [&](const auto& sh) { bwd_fetch<AUG, BM>(io, sh, io.N, update_b, bsrc, update_q, qsrc, bc, cur); });
     for (int k = io.N; k >= 0; k--) {
         HK_STAMP(0, k);
         const int kn = k > 0 ? k - 1 : 0;  // unconditional prefetch (stage 0 re-read on the last pass)
         const StageInfo sn = load_stage(io.st, kn);
         BwdFrag nxt;
-        bwd_fetch<AUG>(io, sn, kn, update_b, bsrc, update_q, qsrc, use_box, Qx, qx, nxt);
+        with_shape<FX>(sn, [&](const auto& sh) { bwd_fetch<AUG, BM>(io, sh, kn, update_b, bsrc, update_q, qsrc, bc, nxt); });
         // factor of stage k+1 (still in registers): stored one stage late, behind the prefetch, so
         // that no s_waitcnt of this stage has to wait for the store acknowledgements
-        if (k < io.N) store_factor(io.F + (long)(k + 1) * FSTRIDE, S, AUG ? ml_prev : 0.0, invd_prev);
+        store_factor(io.F + (long)(k + 1) * FSTRIDE, S, AUG ? ml_prev : 0.0, invd_prev, k < io.N);
+        asm volatile("" ::: "memory");  // keep those stores here, ahead of this stage's math
         HK_STAMP(1, k);
-        const int nu = si.nu, nx = si.nx, xo = si.xo;
-        d4 M = cur.Mi;
-        double ml = cur.mlq + cur.qxv;  // update_q row (or RSQrq row) + drowad qx
-#pragma unroll
-        for (int r = 0; r < 4; r++)
-            if (g + 4 * r == c) M[r] += cur.dq;  // ddiaadin: diag = bd + Qx
-        if (k < io.N) {
-            const int nx1 = si.nx1, xo1 = si.xo1;
-            // W' = Lxx_{k+1}' BAbt_k'  (dtrmm_nt_u, d_back_ric_rec.c:262-264), rows in stage-(k+1) tile coords
-            d4 acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-            for (int kc = 0; kc < 4; kc++) {
-                if (4 * kc + 3 < xo1 || 4 * kc >= xo1 + nx1) continue;  // uniform
-                const double aop = (c >= xo1 && 4 * kc + g >= c) ? S[kc] : 0.0;
-                acc = mfma(aop, cur.bop[kc], acc);
-            }
-            // M += W W'  (dsyrk part of dsyrk_dpotrf_lib, :325)
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                if (4 * r + 3 < xo1 || 4 * r >= xo1 + nx1) continue;
-                M = mfma(acc[r], acc[r], M);
-            }
-            if (AUG) {
-                // v = Lxx' b (col layout, stage k+1 tile)
-                double part = 0.0;
-#pragma unroll
-                for (int r = 0; r < 4; r++) part += (c >= xo1 ? lowS(S, r, g, c) : 0.0) * cur.brow[r];
-                const double vcol = xrow_sum(part);
-                double vrow[4];
-                col2row(sm, vcol, vrow);
-                if (compute_Pb) {
-                    // Pb_k = Lxx (Lxx' b)  (dtrmv_u_t on W's last row, :266-275)
-                    double pp = 0.0;
-#pragma unroll
-                    for (int r = 0; r < 4; r++) {
-                        const int j = g + 4 * r;
-                        pp += (j <= c && j >= xo1) ? S[r] * vrow[r] : 0.0;
-                    }
-                    const double pb = xrow_sum(pp);
-                    gst(Pb, k * V16 + (c - xo1), pb, g == 0 && c >= xo1 && c < xo1 + nx1);
-                }
-                // w_last = b' Lxx + l_{k+1,x}   (dgead, :276)  -> m_last += W w_last
-                double mp = 0.0;
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    const double w = (g + 4 * r >= xo1) ? vrow[r] + lr_prev[r] : 0.0;
-                    mp += acc[r] * w;
-                }
-                ml += xrow_sum(mp);
-            }
-        }
-        HK_STAMP(2, k);
-        double lr[4], invd;
-        stage_chol<AUG>(M, ml, lr, invd, nu, nx, xo, k);
-        HK_STAMP(3, k);
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            S[r] = M[r];
-            lr_prev[r] = lr[r];
-        }
-        ml_prev = ml;
-        invd_prev = invd;
+        with_shape<FX>(si, [&](const auto& sh) {
+            bwd_step<AUG, BM>(io, sm, sh, k, cur, bc, compute_Pb, Pb, S, lr_prev, ml_prev, invd_prev);
+        });
         HK_STAMP(4, k);
         si = sn;
         cur = nxt;
@@ -380,17 +546,19 @@ __device__ void ric_backward(const RicIO& io, Scratch* sm, int update_b, const d
     store_factor(io.F, S, AUG ? ml_prev : 0.0, invd_prev);
 }
 
-
-
+// ------------------------------------------------------------------------------------------------
+// Triangular solves on the stage factor (upper storage S: row p of S = column p of L).
+// ------------------------------------------------------------------------------------------------
 // Solve the unknown part of L_k' y = rhs (dtrsv_t_lib, blas_d_lib4.c:5276) in row layout, descending.
 // rrow: rhs in row layout (reduced by the known part already); y written into ur (row layout) at the
 // unknown tile indices.  unknown(t) = active(t) && (all || t < nu).
-__device__ __forceinline__ void solve_lt(const d4& S, double invd, double rrow[4], double ur[4], int nu, int nx,
-                                         int xo, bool all) {
+template <class SH>
+__device__ __forceinline__ void solve_lt(const SH& sh, const d4& S, double invd, double rrow[4], double ur[4],
+                                         bool all) {
     const int l = lane_id(), g = l >> 4;
 #pragma unroll
     for (int p = 15; p >= 0; p--) {
-        const bool unk = all ? tile_active(p, nu, nx, xo) : (p < nu);
+        const bool unk = all ? tile_active(p, sh.nu, sh.nx, sh.xo) : (p < sh.nu);
         if (!unk) continue;
         const int rp = p >> 2, gp = p & 3;
         const double rv = (rp == 0) ? rrow[0] : (rp == 1) ? rrow[1] : (rp == 2) ? rrow[2] : rrow[3];
@@ -414,11 +582,12 @@ __device__ __forceinline__ void solve_lt(const d4& S, double invd, double rrow[4
 
 // Forward solve of the unknown part of L_k y = h (dtrsv_n_lib, :5204) in col layout, ascending;
 // rows beyond the unknown block get the rectangular update.
-__device__ __forceinline__ double solve_ln(const d4& S, double invd, double h, int nu, int nx, int xo, bool all) {
+template <class SH>
+__device__ __forceinline__ double solve_ln(const SH& sh, const d4& S, double invd, double h, bool all) {
     const int l = lane_id(), c = l & 15;
 #pragma unroll
     for (int p = 0; p < 16; p++) {
-        const bool unk = all ? tile_active(p, nu, nx, xo) : (p < nu);
+        const bool unk = all ? tile_active(p, sh.nu, sh.nx, sh.xo) : (p < sh.nu);
         if (!unk) continue;
         const int rp = p >> 2, gp = p & 3;
         const double y = readlane(h, p) * readlane(invd, p);
@@ -453,20 +622,26 @@ __device__ __forceinline__ double pi_from_x(Scratch* sm, const d4& S1, int xo1, 
     return xrow_sum(p2);
 }
 
-// Forward-pass fragment of stage k: its factor, the BAbt_k' gemv operand and b_k.
+// ------------------------------------------------------------------------------------------------
+// Forward substitution (sv and trs).
+// ------------------------------------------------------------------------------------------------
 struct FwdFrag {
     d4 S;
     double lc, invd;
-    d4 bt;       // bt[r] = BAbt_k[var(g+4r)][c - xo1]
-    double bval; // b_k[c - xo1]
-    double hc;   // trs: backward vector hux_k[var(c)]
-    double pk;   // trs: p_{k+1} = hux_{k+1}[x part] (col layout over stage-(k+1) tile)
+    d4 bt;        // bt[r] = BAbt_k[var(g+4r)][c - xo1]
+    double bval;  // b_k[c - xo1]
+    double hc;    // trs: backward vector hux_k[var(c)]
+    double pk;    // trs: p_{k+1} = hux_{k+1}[x part] (col layout over stage-(k+1) tile)
+    double bx[10];
+    BoxLane bl;
 };
 
+// Fetch of stage k (sh: shape of stage min(k, N-1), whose BAbt block the pass reads; pnbk: pnb of k).
 // mode 0: sv (b from update_b source or the BAbt row); mode 1: trs (b from hb or the BAbt row, plus hc/pk)
-template <int MODE>
-__device__ __forceinline__ void fwd_fetch(const RicIO& io, int k, const double* bsrc, int use_bsrc,
-                                          const double* ux, int compute_pi, FwdFrag& f) {
+template <int MODE, int FM, class SH>
+__device__ __forceinline__ void fwd_fetch(const RicIO& io, const SH& sh, int k, int pnbk, const double* bsrc,
+                                          int use_bsrc, const double* ux, int compute_pi, const BoxCtx& bc,
+                                          FwdFrag& f) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
     const double* Fk = io.F + (long)k * FSTRIDE;
 #pragma unroll
@@ -475,82 +650,172 @@ __device__ __forceinline__ void fwd_fetch(const RicIO& io, int k, const double* 
     f.invd = gld(Fk, 272 + c);
     const int kk = k < io.N ? k : io.N - 1;  // stage N has no BAbt block: loads clamped, values masked
     const bool live = k < io.N;
-    const StageInfo si = load_stage(io.st, kk);
-    const double* Bk = io.BAbt + si.oB;
-    const int s = c - si.xo1;
-    const bool ok = live && s >= 0 && s < si.nx1;
+    const double* Bk = io.BAbt + sh.oB;
+    const int s = c - sh.xo1;
+    const bool ok = live && s >= 0 && s < sh.nx1;
 #pragma unroll
     for (int r = 0; r < 4; r++) {
-        const int vi = tile_var(g + 4 * r, si.nu, si.nx, si.xo);
-        f.bt[r] = ldsel(Bk, lib4_idx(si.sdB, vi, s), vi >= 0 && ok);
+        const int vi = tile_var(g + 4 * r, sh.nu, sh.nx, sh.xo);
+        f.bt[r] = ldsel(Bk, lib4_idx(sh.sdB, vi, s), vi >= 0 && ok);
     }
-    f.bval = use_bsrc ? ldsel(bsrc + kk * V16, s, ok) : ldsel(Bk, lib4_idx(si.sdB, si.nu + si.nx, s), ok);
+    f.bval = use_bsrc ? ldsel(bsrc + kk * V16, s, ok) : ldsel(Bk, lib4_idx(sh.sdB, sh.nu + sh.nx, s), ok);
     f.hc = 0.0;
     f.pk = 0.0;
     if (MODE == 1) {
-        const int vc = tile_var(c, si.nu, si.nx, si.xo);
+        const int vc = tile_var(c, sh.nu, sh.nx, sh.xo);
         f.hc = ldsel(ux + kk * V16, vc, live && vc >= 0);
-        f.pk = ldsel(ux + (kk + 1) * V16, si.nu1 + s, compute_pi && ok);
+        f.pk = ldsel(ux + (kk + 1) * V16, sh.nu1 + s, compute_pi && ok);
+    }
+#pragma unroll
+    for (int i = 0; i < 10; i++) f.bx[i] = 0.0;
+    if (FM != BX_NONE) {
+        const BoxLane b = box_lane(io.tileslot, pnbk, k);
+        f.bl = b;
+        if (FM == BX_P1) {
+            f.bx[0] = ldsel(bc.d, b.lo, b.ok);
+            f.bx[1] = ldsel(bc.d, b.up, b.ok);
+            f.bx[2] = ldsel(bc.t, b.lo, b.ok);
+            f.bx[3] = ldsel(bc.t, b.up, b.ok);
+            f.bx[4] = ldsel(bc.lamt, b.lo, b.ok);
+            f.bx[5] = ldsel(bc.lamt, b.up, b.ok);
+            f.bx[6] = ldsel(bc.lam, b.lo, b.ok);
+            f.bx[7] = ldsel(bc.lam, b.up, b.ok);
+            f.bx[8] = ldsel(bc.dlam, b.lo, b.ok && !bc.pred);
+            f.bx[9] = ldsel(bc.dlam, b.up, b.ok && !bc.pred);
+        } else if (FM == BX_P2) {
+            f.bx[0] = ldsel(bc.res_d, b.lo, b.ok);
+            f.bx[1] = ldsel(bc.res_d, b.up, b.ok);
+            f.bx[2] = ldsel(bc.t_inv, b.lo, b.ok);
+            f.bx[3] = ldsel(bc.t_inv, b.up, b.ok);
+            f.bx[4] = ldsel(bc.lam, b.lo, b.ok);
+            f.bx[5] = ldsel(bc.lam, b.up, b.ok);
+            f.bx[6] = ldsel(bc.res_m, b.lo, b.ok);
+            f.bx[7] = ldsel(bc.res_m, b.up, b.ok);
+            f.bx[8] = ldsel(bc.t, b.lo, b.ok);
+            f.bx[9] = ldsel(bc.t, b.up, b.ok);
+        }
     }
 }
 
+template <int MODE, int FM, class FX>
+__device__ __forceinline__ void fwd_fetch_k(const RicIO& io, int k, const double* bsrc, int use_bsrc,
+                                            const double* ux, int compute_pi, const BoxCtx& bc, FwdFrag& f) {
+    const int kk = k < io.N ? k : io.N - 1;
+    const StageInfo sk = load_stage(io.st, kk);
+    const int pnbk = k < io.N ? sk.pnb : load_stage(io.st, k).pnb;
+    with_shape<FX>(sk, [&](const auto& sh) {
+        fwd_fetch<MODE, FM>(io, sh, k, pnbk, bsrc, use_bsrc, ux, compute_pi, bc, f);
+    });
+}
+
+// Step of the box slacks / multipliers of tile c given the primal step x = dux_k[var(c)] (col layout)
+// and the per-lane step-length candidate (d_compute_alpha_mpc_hard_tv :489-614 / _res_ :1180-1313).
+template <int FM>
+__device__ __forceinline__ void box_alpha(const BoxCtx& bc, const FwdFrag& f, double x, double& al) {
+    if (FM == BX_NONE) return;
+    const int g = lane_id() >> 4;
+    const BoxLane& b = f.bl;
+    const bool st = b.ok && g == 0;
+    double dtl, dtu, dll, dlu, lml, lmu, tl, tu;
+    if (FM == BX_P1) {
+        dtl = x - f.bx[0] - f.bx[2];
+        dtu = -x + f.bx[1] - f.bx[3];
+        dll = f.bx[8] - (f.bx[4] * dtl + f.bx[6]);
+        dlu = f.bx[9] - (f.bx[5] * dtu + f.bx[7]);
+        lml = f.bx[6];
+        lmu = f.bx[7];
+        tl = f.bx[2];
+        tu = f.bx[3];
+    } else {
+        dtl = x - f.bx[0];
+        dtu = -x + f.bx[1];
+        dll = -f.bx[2] * (f.bx[4] * dtl + f.bx[6]);
+        dlu = -f.bx[3] * (f.bx[5] * dtu + f.bx[7]);
+        lml = f.bx[4];
+        lmu = f.bx[5];
+        tl = f.bx[8];
+        tu = f.bx[9];
+    }
+    gst(bc.dt, b.lo, dtl, st);
+    gst(bc.dt, b.up, dtu, st);
+    gst(bc.dlam, b.lo, dll, st);
+    gst(bc.dlam, b.up, dlu, st);
+    if (b.ok) {
+        alpha_rule(al, lml, dll);
+        alpha_rule(al, lmu, dlu);
+        alpha_rule(al, tl, dtl);
+        alpha_rule(al, tu, dtu);
+    }
+}
+
+// One forward stage k < N: u_k from the factor, x_{k+1} = b + BAbt' ux, pi_k, box steps.
+template <int MODE, int FM, class SH>
+__device__ __forceinline__ void fwd_step(const RicIO& io, Scratch* sm, const SH& sh, int k, const FwdFrag& cur,
+                                         const FwdFrag& nxt, double& xcol, double* ux, int compute_pi, double* pi,
+                                         const BoxCtx& bc, double& al) {
+    const int l = lane_id(), g = l >> 4, c = l & 15;
+    const bool all = !SH::fixed && k == 0;
+    double xrow[4];
+    col2row(sm, xcol, xrow);
+    double part = 0.0;
+    if (!all) {
+#pragma unroll
+        for (int r = 0; r < 4; r++) part += (g + 4 * r >= sh.xo) ? lowS(cur.S, r, g, c) * xrow[r] : 0.0;
+    }
+    const double rhs = (MODE == 0) ? cur.lc : cur.hc;
+    const double rc = -rhs - xrow_sum(part);
+    double rrow[4], ur[4];
+    col2row(sm, rc, rrow);
+#pragma unroll
+    for (int r = 0; r < 4; r++) ur[r] = all ? 0.0 : xrow[r];
+    HK_STAMP(9, k);
+    solve_lt(sh, cur.S, cur.invd, rrow, ur, all);
+    HK_STAMP(10, k);
+    // ux_k, col layout (tile c): one coalesced store from row group 0, and the box steps
+    const double ucol = row2col(sm, ur);
+    const int vcs = tile_var(c, sh.nu, sh.nx, sh.xo);
+    gst(ux, k * V16 + vcs, ucol, g == 0 && vcs >= 0);
+    box_alpha<FM>(bc, cur, ucol, al);
+    // x_{k+1} = b + BAbt_k' ux_k  (dgemv_t_lib alg 1, :347-351), col layout over stage-(k+1) tile
+    double gp = 0.0;
+#pragma unroll
+    for (int r = 0; r < 4; r++) gp += cur.bt[r] * ur[r];
+    const int s = c - sh.xo1;
+    const bool ok = s >= 0 && s < sh.nx1;
+    const double x1 = cur.bval + xrow_sum(gp);
+    xcol = ok ? x1 : 0.0;
+    HK_STAMP(11, k);
+    double pv = 0.0;
+    if (compute_pi) {
+        double x1row[4];
+        col2row(sm, xcol, x1row);
+        if (MODE == 0)
+            pv = pi_from_x(sm, nxt.S, sh.xo1, x1row, nxt.lc);  // pi_k = Lxx (Lxx' x + l_x)
+        else
+            pv = pi_from_x(sm, nxt.S, sh.xo1, x1row, 0.0) + cur.pk;  // pi_k = p_{k+1} + P x
+    }
+    gst(pi, k * V16 + s, pv, compute_pi && g == 0 && ok);
+}
+
 // Shared forward substitution (sv: rhs = -l_k ; trs: rhs = -hux_k), d_back_ric_rec.c:339-397 / :704-790.
-// ux: variable order; pi: state order.
-template <int MODE>
+// ux: variable order; pi: state order.  FM != BX_NONE also computes the box steps of every stage and
+// the per-lane step-length candidate `al` (caller reduces it with wave_min).
+template <int MODE, int FM, class FX>
 __device__ void ric_forward(const RicIO& io, Scratch* sm, const double* bsrc, int use_bsrc, double* ux,
-                            int compute_pi, double* pi) {
+                            int compute_pi, double* pi, const BoxCtx& bc, double& al) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
     double xcol = 0.0;  // x_k in col layout (stage-k tile coords)
     FwdFrag cur, nxt;
-    fwd_fetch<MODE>(io, 0, bsrc, use_bsrc, ux, compute_pi, cur);
-    fwd_fetch<MODE>(io, 1, bsrc, use_bsrc, ux, compute_pi, nxt);
+    fwd_fetch_k<MODE, FM, FX>(io, 0, bsrc, use_bsrc, ux, compute_pi, bc, cur);
+    fwd_fetch_k<MODE, FM, FX>(io, 1, bsrc, use_bsrc, ux, compute_pi, bc, nxt);
     for (int k = 0; k < io.N; k++) {
         HK_STAMP(8, k);
         FwdFrag nn;
-        fwd_fetch<MODE>(io, k + 2 <= io.N ? k + 2 : io.N, bsrc, use_bsrc, ux, compute_pi, nn);
+        fwd_fetch_k<MODE, FM, FX>(io, k + 2 <= io.N ? k + 2 : io.N, bsrc, use_bsrc, ux, compute_pi, bc, nn);
         const StageInfo si = load_stage(io.st, k);
-        const int nu = si.nu, nx = si.nx, xo = si.xo;
-        const bool all = (k == 0);
-        double xrow[4];
-        col2row(sm, xcol, xrow);
-        double part = 0.0;
-        if (!all) {
-#pragma unroll
-            for (int r = 0; r < 4; r++) part += (g + 4 * r >= xo) ? lowS(cur.S, r, g, c) * xrow[r] : 0.0;
-        }
-        const double rhs = (MODE == 0) ? cur.lc : cur.hc;
-        const double rc = -rhs - xrow_sum(part);
-        double rrow[4], ur[4];
-        col2row(sm, rc, rrow);
-#pragma unroll
-        for (int r = 0; r < 4; r++) ur[r] = all ? 0.0 : xrow[r];
-        HK_STAMP(9, k);
-        solve_lt(cur.S, cur.invd, rrow, ur, nu, nx, xo, all);
-        HK_STAMP(10, k);
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const int v = tile_var(g + 4 * r, nu, nx, xo);
-            gst(ux, k * V16 + v, ur[r], c == 0 && v >= 0);
-        }
-        // x_{k+1} = b + BAbt_k' ux_k  (dgemv_t_lib alg 1, :347-351), col layout over stage-(k+1) tile
-        double gp = 0.0;
-#pragma unroll
-        for (int r = 0; r < 4; r++) gp += cur.bt[r] * ur[r];
-        const int s = c - si.xo1;
-        const bool ok = s >= 0 && s < si.nx1;
-        const double x1 = cur.bval + xrow_sum(gp);
-        xcol = ok ? x1 : 0.0;
-        HK_STAMP(11, k);
-        if (compute_pi) {
-            double x1row[4];
-            col2row(sm, xcol, x1row);
-            double pv;
-            if (MODE == 0)
-                pv = pi_from_x(sm, nxt.S, si.xo1, x1row, nxt.lc);  // pi_k = Lxx (Lxx' x + l_x)
-            else
-                pv = pi_from_x(sm, nxt.S, si.xo1, x1row, 0.0) + cur.pk;  // pi_k = p_{k+1} + P x
-            gst(pi, k * V16 + s, pv, g == 0 && ok);
-        }
+        with_shape<FX>(si, [&](const auto& sh) {
+            fwd_step<MODE, FM>(io, sm, sh, k, cur, nxt, xcol, ux, compute_pi, pi, bc, al);
+        });
         HK_STAMP(12, k);
         cur = nxt;
         nxt = nn;
@@ -558,111 +823,186 @@ __device__ void ric_forward(const RicIO& io, Scratch* sm, const double* bsrc, in
     const StageInfo sN = load_stage(io.st, io.N);
     const int v = tile_var(c, sN.nu, sN.nx, sN.xo);
     gst(ux, io.N * V16 + v, xcol, g == 0 && v >= 0);
+    box_alpha<FM>(bc, cur, xcol, al);  // stage N: nu = 0, every tile is a state
 }
 
+template <class FX>
 __device__ __forceinline__ void ric_forward_sv(const RicIO& io, Scratch* sm, int update_b, const double* bsrc,
                                                double* ux, int compute_pi, double* pi) {
-    ric_forward<0>(io, sm, bsrc, update_b, ux, compute_pi, pi);
+    BoxCtx bc{};
+    double al = 1.0;
+    ric_forward<0, BX_NONE, FX>(io, sm, bsrc, update_b, ux, compute_pi, pi, bc, al);
 }
 
-// Backward fragment of the trs at stage k.
+// ------------------------------------------------------------------------------------------------
+// Riccati solve with an existing factor (trs).
+// ------------------------------------------------------------------------------------------------
 struct TrsFrag {
     d4 S;
     double invd;
     d4 bop;      // BAbt_k[var(c)][g+4r-xo1]
     d4 brow;     // hb_k in row layout over stage-(k+1) tile rows (compute_Pb)
-    double h0;   // gradient g_k[c] = q + qx (col layout)
+    double h0;   // gradient q (col layout), box term added at use
     double pbc;  // stored Pb_k (col layout over stage-(k+1) tile) when !compute_Pb
+    double bx[12];
+    BoxLane bl;
 };
 
-__device__ __forceinline__ void trs_fetch(const RicIO& io, int k, const double* hb, const double* hq, int use_box,
-                                          const double* qx, int compute_Pb, const double* Pb, TrsFrag& f) {
+template <int TM, class SH>
+__device__ __forceinline__ void trs_fetch(const RicIO& io, const SH& sh, int k, const double* hb, const double* hq,
+                                          const BoxCtx& bc, int compute_Pb, const double* Pb, TrsFrag& f) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
     const double* Fk = io.F + (long)k * FSTRIDE;
 #pragma unroll
     for (int r = 0; r < 4; r++) f.S[r] = gld(Fk, r * 64 + l);
     f.invd = gld(Fk, 272 + c);
-    const StageInfo si = load_stage(io.st, k);
-    const int nu = si.nu, nx = si.nx, xo = si.xo, nux = nu + nx;
-    const int vc = tile_var(c, nu, nx, xo);
-    const double* R = io.RSQ + si.oR;
-    double h = hq ? ldsel(hq + k * V16, vc, vc >= 0) : ldsel(R, lib4_idx(si.sdR, nux, vc), vc >= 0);
-    const int slot = io.tileslot[k * 16 + c];
-    h += ldsel(use_box ? qx : R, k * V16 + slot, use_box && slot >= 0);  // dvecad_libsp (:612-620)
-    f.h0 = h;
-    const int kb = k < io.N ? k : io.N - 1;
-    const StageInfo sb = load_stage(io.st, kb);
-    const double* Bk = io.BAbt + sb.oB;
-    const int xo1 = si.xo1, nx1 = si.nx1;
-    const double* bp = hb ? hb + kb * V16 : Bk;
+    const int nux = sh.nu + sh.nx;
+    const int vc = tile_var(c, sh.nu, sh.nx, sh.xo);
+    const double* R = io.RSQ + sh.oR;
+    f.h0 = hq ? ldsel(hq + k * V16, vc, vc >= 0) : ldsel(R, lib4_idx(sh.sdR, nux, vc), vc >= 0);
+    const BoxLane b = box_lane(io.tileslot, sh.pnb, k);
+    f.bl = b;
+#pragma unroll
+    for (int i = 0; i < 12; i++) f.bx[i] = 0.0;
+    if (TM == BX_GIVEN) {
+        f.bx[0] = ldsel(bc.qx, b.s16, b.ok);
+    } else if (TM == BX_P1) {
+        f.bx[0] = ldsel(bc.t_inv, b.lo, b.ok);
+        f.bx[1] = ldsel(bc.t_inv, b.up, b.ok);
+        f.bx[2] = ldsel(bc.dlam, b.lo, b.ok);
+        f.bx[3] = ldsel(bc.dlam, b.up, b.ok);
+        f.bx[4] = ldsel(bc.dt, b.lo, b.ok);
+        f.bx[5] = ldsel(bc.dt, b.up, b.ok);
+        f.bx[6] = ldsel(bc.qxs, b.s16, b.ok);
+    } else if (TM == BX_P2) {
+        f.bx[0] = ldsel(bc.res_m, b.lo, b.ok);
+        f.bx[1] = ldsel(bc.res_m, b.up, b.ok);
+        f.bx[2] = ldsel(bc.dt, b.lo, b.ok);
+        f.bx[3] = ldsel(bc.dt, b.up, b.ok);
+        f.bx[4] = ldsel(bc.dlam, b.lo, b.ok);
+        f.bx[5] = ldsel(bc.dlam, b.up, b.ok);
+        f.bx[6] = ldsel(bc.t_inv, b.lo, b.ok);
+        f.bx[7] = ldsel(bc.t_inv, b.up, b.ok);
+        f.bx[8] = ldsel(bc.lam, b.lo, b.ok);
+        f.bx[9] = ldsel(bc.lam, b.up, b.ok);
+        f.bx[10] = ldsel(bc.res_d, b.lo, b.ok);
+        f.bx[11] = ldsel(bc.res_d, b.up, b.ok);
+    }
+    const bool live = SH::fixed || k < io.N;
+    const double* Bk = io.BAbt + sh.oB;
+    const double* bp = hb ? hb + k * V16 : Bk;
 #pragma unroll
     for (int r = 0; r < 4; r++) {
-        const int sr = g + 4 * r - xo1;
-        const bool ok = k < io.N && sr >= 0 && sr < nx1;
-        f.bop[r] = ldsel(Bk, lib4_idx(sb.sdB, vc, sr), ok && vc >= 0);
-        f.brow[r] = ldsel(bp, hb ? sr : lib4_idx(sb.sdB, nux, sr), ok && compute_Pb);
+        const int sr = g + 4 * r - sh.xo1;
+        const bool ok = live && sr >= 0 && sr < sh.nx1;
+        f.bop[r] = ldsel(Bk, lib4_idx(sh.sdB, vc, sr), ok && vc >= 0);
+        f.brow[r] = ldsel(bp, hb ? sr : lib4_idx(sh.sdB, nux, sr), ok && compute_Pb);
     }
+    const int s = c - sh.xo1;
+    f.pbc = ldsel(Pb + k * V16, s, !compute_Pb && live && s >= 0 && s < sh.nx1);
+}
+
+// Corrector gradient of tile c (d_update_gradient_mpc_hard_tv :387-485 / centering correction +
+// d_update_gradient_res_mpc_hard_tv :1512-1600): the box term added to the trs gradient.
+template <int TM>
+__device__ __forceinline__ double box_gradient(const BoxCtx& bc, const TrsFrag& f) {
+    const int g = lane_id() >> 4;
+    const BoxLane& b = f.bl;
+    const bool st = b.ok && g == 0;
+    if (TM == BX_GIVEN) return f.bx[0];
+    if (TM == BX_P1) {
+        const double dll = f.bx[0] * (bc.smu - f.bx[2] * f.bx[4]);
+        const double dlu = f.bx[1] * (bc.smu - f.bx[3] * f.bx[5]);
+        gst(bc.dlam, b.lo, dll, st);
+        gst(bc.dlam, b.up, dlu, st);
+        return b.ok ? f.bx[6] + (dlu - dll) : 0.0;
+    }
+    if (TM == BX_P2) {
+        const double rml = f.bx[0] + (f.bx[2] * f.bx[4] - bc.smu);
+        const double rmu = f.bx[1] + (f.bx[3] * f.bx[5] - bc.smu);
+        gst(bc.res_m, b.lo, rml, st);
+        gst(bc.res_m, b.up, rmu, st);
+        return b.ok ? f.bx[6] * (rml - f.bx[8] * f.bx[10]) - f.bx[7] * (rmu + f.bx[9] * f.bx[11]) : 0.0;
+    }
+    return 0.0;
+}
+
+// One backward trs stage k < N: hux_k = q_k + box + BAbt_k (P_{k+1} b_k + p_{k+1}), then the solve.
+template <int TM, class SH>
+__device__ __forceinline__ void trs_step(const RicIO& io, Scratch* sm, const SH& sh, int k, const TrsFrag& cur,
+                                         const BoxCtx& bc, double* ux, int compute_Pb, double* Pb, d4& S1,
+                                         double& pcol) {
+    const int l = lane_id(), g = l >> 4, c = l & 15;
+    const int xo1 = sh.xo1, nx1 = sh.nx1;
+    const int vc = tile_var(c, sh.nu, sh.nx, sh.xo);
     const int s = c - xo1;
-    f.pbc = ldsel(Pb + kb * V16, s, !compute_Pb && k < io.N && s >= 0 && s < nx1);
+    double pbc = cur.pbc;
+    {
+        double part = 0.0;
+#pragma unroll
+        for (int r = 0; r < 4; r++) part += (c >= xo1 ? lowS(S1, r, g, c) : 0.0) * cur.brow[r];
+        const double vcol = xrow_sum(part);
+        double vrow[4];
+        col2row(sm, vcol, vrow);
+        double pp = 0.0;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int j = g + 4 * r;
+            pp += (j <= c && j >= xo1) ? S1[r] * vrow[r] : 0.0;
+        }
+        if (compute_Pb) pbc = xrow_sum(pp);
+        gst(Pb, k * V16 + s, pbc, compute_Pb && g == 0 && s >= 0 && s < nx1);
+    }
+    const double wc = (s >= 0 && s < nx1) ? pbc + pcol : 0.0;
+    double wrow[4];
+    col2row(sm, wc, wrow);
+    double part = 0.0;
+#pragma unroll
+    for (int r = 0; r < 4; r++) part += cur.bop[r] * wrow[r];
+    double h = cur.h0 + box_gradient<TM>(bc, cur);  // dvecad_libsp (:612-620)
+    h += xrow_sum(part);
+    h = solve_ln(sh, cur.S, cur.invd, h, !SH::fixed && k == 0);
+    gst(ux, k * V16 + vc, h, g == 0 && vc >= 0);
+    pcol = h;
+    S1 = cur.S;
 }
 
 // Riccati solve with an existing factor (d_back_ric_rec.c:564-791).
-// hb: state order, hq: variable order (null: the BAbt / RSQrq augmented rows), qx: slot order;
+// hb: state order, hq: variable order (null: the BAbt / RSQrq augmented rows), TM: box gradient term;
 // ux (variable order) doubles as the backward work vector exactly like hux in the reference.
-__device__ void ric_trs(const RicIO& io, Scratch* sm, const double* hb, const double* hq, int use_box,
-                        const double* qx, double* ux, int compute_pi, double* pi, int compute_Pb, double* Pb) {
+// FM != BX_NONE: box steps + step-length candidate `al` in the forward substitution.
+template <int TM, int FM, class FX>
+__device__ void ric_trs(const RicIO& io, Scratch* sm, const double* hb, const double* hq, const BoxCtx& bc,
+                        double* ux, int compute_pi, double* pi, int compute_Pb, double* Pb, double& al) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
     // ---- backward
     TrsFrag cur;
-    trs_fetch(io, io.N, hb, hq, use_box, qx, compute_Pb, Pb, cur);
+    const StageInfo sN = load_stage(io.st, io.N);
+    with_shape<FX>(sN, [&](const auto& sh) { trs_fetch<TM>(io, sh, io.N, hb, hq, bc, compute_Pb, Pb, cur); });
+    const double hN = cur.h0 + box_gradient<TM>(bc, cur);
     {
-        const StageInfo sn = load_stage(io.st, io.N);
-        const int v = tile_var(c, sn.nu, sn.nx, sn.xo);
-        gst(ux, io.N * V16 + v, cur.h0, g == 0 && v >= 0);
+        const int v = tile_var(c, sN.nu, sN.nx, sN.xo);
+        gst(ux, io.N * V16 + v, hN, g == 0 && v >= 0);
     }
-    double pcol = cur.h0;  // hux_{k+1} in col layout (stage-(k+1) tile coords)
+    double pcol = hN;  // hux_{k+1} in col layout (stage-(k+1) tile coords)
     d4 S1 = cur.S;
     TrsFrag nxt;
-    trs_fetch(io, io.N - 1, hb, hq, use_box, qx, compute_Pb, Pb, nxt);
+    {
+        const StageInfo s1 = load_stage(io.st, io.N - 1);
+        with_shape<FX>(s1, [&](const auto& sh) { trs_fetch<TM>(io, sh, io.N - 1, hb, hq, bc, compute_Pb, Pb, nxt); });
+    }
     for (int k = io.N - 1; k >= 0; k--) {
         cur = nxt;
-        trs_fetch(io, k > 0 ? k - 1 : 0, hb, hq, use_box, qx, compute_Pb, Pb, nxt);
+        const int kn = k > 0 ? k - 1 : 0;
+        const StageInfo sn = load_stage(io.st, kn);
+        with_shape<FX>(sn, [&](const auto& sh) { trs_fetch<TM>(io, sh, kn, hb, hq, bc, compute_Pb, Pb, nxt); });
+        asm volatile("" ::: "memory");
         const StageInfo si = load_stage(io.st, k);
-        const int nu = si.nu, nx = si.nx, xo = si.xo, xo1 = si.xo1, nx1 = si.nx1;
-        const int vc = tile_var(c, nu, nx, xo);
-        const int s = c - xo1;
-        double pbc = cur.pbc;
-        if (compute_Pb) {
-            double part = 0.0;
-#pragma unroll
-            for (int r = 0; r < 4; r++) part += (c >= xo1 ? lowS(S1, r, g, c) : 0.0) * cur.brow[r];
-            const double vcol = xrow_sum(part);
-            double vrow[4];
-            col2row(sm, vcol, vrow);
-            double pp = 0.0;
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const int j = g + 4 * r;
-                pp += (j <= c && j >= xo1) ? S1[r] * vrow[r] : 0.0;
-            }
-            pbc = xrow_sum(pp);
-            gst(Pb, k * V16 + s, pbc, g == 0 && s >= 0 && s < nx1);
-        }
-        const double wc = (s >= 0 && s < nx1) ? pbc + pcol : 0.0;
-        double wrow[4];
-        col2row(sm, wc, wrow);
-        double part = 0.0;
-#pragma unroll
-        for (int r = 0; r < 4; r++) part += cur.bop[r] * wrow[r];
-        double h = cur.h0 + xrow_sum(part);
-        h = solve_ln(cur.S, cur.invd, h, nu, nx, xo, k == 0);
-        gst(ux, k * V16 + vc, h, g == 0 && vc >= 0);
-        pcol = h;
-        S1 = cur.S;
+        with_shape<FX>(si, [&](const auto& sh) { trs_step<TM>(io, sm, sh, k, cur, bc, ux, compute_Pb, Pb, S1, pcol); });
     }
     __syncthreads();  // hux_k written by row group 0 is re-read by every lane below
     // ---- forward
-    ric_forward<1>(io, sm, hb, hb != nullptr, ux, compute_pi, pi);
+    ric_forward<1, FM, FX>(io, sm, hb, hb != nullptr, ux, compute_pi, pi, bc, al);
 }
 
 }  // namespace hk

@@ -23,6 +23,7 @@
 #include "hpmpc_kargs.h"
 
 extern "C" int hk_launch(int which, const KArgs* a, int count, hipStream_t stream);
+extern "C" int hk_fixcls(int nu, int nx);
 
 namespace {
 
@@ -67,6 +68,7 @@ struct hpmpc_mi355x_plan {
     void* d_st = nullptr;
     signed char *d_tileslot = nullptr, *d_slotvar = nullptr;
     std::vector<long long> dev_offB, dev_offR;  // offsets currently uploaded into d_st
+    int fixcls = 0;                             // compiled inner-stage class (kernel instance)
 };
 
 namespace {
@@ -110,7 +112,7 @@ bool plan_upload_stages(hpmpc_mi355x_plan* P, const long long* offB, const long 
                   "plan stage upload");
 }
 
-long long ws_doubles(int N) { return (long long)(N + 1) * (FSTRIDE + 9 * V16 + 8 * V32); }
+long long ws_doubles(int N) { return (long long)(N + 1) * (FSTRIDE + 9 * V16 + 8 * V32) + 16; }
 
 }  // namespace
 
@@ -164,6 +166,14 @@ extern "C" hpmpc_mi355x_plan* hpmpc_mi355x_plan_create(int N, const int* nx, con
             P->slotvar[k * 16 + l] = (signed char)v;
         }
     }
+    // Inner stages of one compiled class run the constant-shape kernel path (StageInfo.r0 = 1).
+    if (N >= 3) {
+        const int nuc = P->nu[1], nxc = nx[1];
+        P->fixcls = hk_fixcls(nuc, nxc);
+        if (P->fixcls)
+            for (int k = 1; k <= N - 2; k++)
+                P->st[k].r0 = (P->nu[k] == nuc && nx[k] == nxc && P->nu[k + 1] == nuc && nx[k + 1] == nxc) ? 1 : 0;
+    }
     bool ok = hip_ok(hipMalloc(&P->d_st, sizeof(StageInfoH) * (N + 1)), "plan alloc") &&
               hip_ok(hipMalloc((void**)&P->d_tileslot, (N + 1) * 16), "plan alloc") &&
               hip_ok(hipMalloc((void**)&P->d_slotvar, (N + 1) * 16), "plan alloc") &&
@@ -212,6 +222,7 @@ KArgs base_args(const hpmpc_mi355x_plan* P, int nprob, int p0) {
     a.sV16 = (long long)(P->N + 1) * V16;
     a.sV32 = (long long)(P->N + 1) * V32;
     a.sW = ws_doubles(P->N);
+    a.fixcls = P->fixcls;
     a.dbg = g_dbg_buf;
     return a;
 }

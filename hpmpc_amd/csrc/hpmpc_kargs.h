@@ -5,6 +5,7 @@
 
 struct KArgs {
     int N, nprob, p0;             // horizon, problems in the batch, first problem of this launch
+    int fixcls;                   // compiled inner-stage class of the plan (0: generic kernels)
     const void* st;               // hk::StageInfo[N+1]
     const signed char* tileslot;  // (N+1)*16
     const signed char* slotvar;   // (N+1)*16

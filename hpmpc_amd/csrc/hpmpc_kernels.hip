@@ -15,7 +15,11 @@ namespace {
 struct Ws {  // per-problem workspace carve (doubles), persistent between an IPM and a KKT re-solve
     double *F, *dux, *dpi, *Pb, *Qx, *qx, *res_q, *res_b, *ux_bkp, *pi_bkp;
     double *dlam, *dt, *t_inv, *lamt, *res_d, *res_m, *t_bkp, *lam_bkp;
+    double* state;  // IpmState (16 doubles) carried between the IPM pass kernels
 };
+
+// Per-problem IPM control state between the pass kernels of one batched solve.
+enum { S_MU = 0, S_ALPHA, S_SIGMA, S_SMU, S_KK, S_PHASE, S_ACTIVE, S_MUSCAL, S_RET };
 
 __device__ __forceinline__ Ws carve(double* W, int N) {
     Ws w;
@@ -40,6 +44,7 @@ __device__ __forceinline__ Ws carve(double* W, int N) {
     w.res_m = W + 5 * b;
     w.t_bkp = W + 6 * b;
     w.lam_bkp = W + 7 * b;
+    w.state = W + 8 * b;
     return w;
 }
 
@@ -98,7 +103,8 @@ __device__ __forceinline__ void wsync() { __syncthreads(); }
 // ------------------------------------------------------------------------------------------------
 // d_back_ric_rec_sv_tv_res / _trf_ / _trs_ over a batch (one problem per workgroup)
 // ------------------------------------------------------------------------------------------------
-extern "C" __global__ __launch_bounds__(64) void hk_ric_sv(KArgs a) {
+template <class FX>
+__global__ __launch_bounds__(64) void hk_ric_sv(KArgs a) {
     const LdsTabs T = lds_tables(a);
     Scratch& sm = *T.sm;
     const int p = blockIdx.x + a.p0;
@@ -108,15 +114,20 @@ extern "C" __global__ __launch_bounds__(64) void hk_ric_sv(KArgs a) {
     const long o16 = (long)p * a.sV16;
     const double* b = a.vb ? a.vb + o16 : nullptr;
     const double* q = a.vq ? a.vq + o16 : nullptr;
-    const double* Qx = a.vQx ? a.vQx + o16 : nullptr;
-    const double* qx = a.vqx ? a.vqx + o16 : nullptr;
+    BoxCtx bc{};
+    bc.Qx = a.vQx ? a.vQx + o16 : nullptr;
+    bc.qx = a.vqx ? a.vqx + o16 : nullptr;
     double* Pb = a.vPb ? a.vPb + o16 : nullptr;
-    ric_backward<true>(io, &sm, a.update_b, b, a.update_q, q, a.use_box, Qx, qx, a.compute_Pb, Pb);
+    if (a.use_box)
+        ric_backward<true, BX_GIVEN, FX>(io, &sm, a.update_b, b, a.update_q, q, bc, a.compute_Pb, Pb);
+    else
+        ric_backward<true, BX_NONE, FX>(io, &sm, a.update_b, b, a.update_q, q, bc, a.compute_Pb, Pb);
     wsync();
-    ric_forward_sv(io, &sm, a.update_b, b, a.ux + o16, a.compute_pi, a.pi + o16);
+    ric_forward_sv<FX>(io, &sm, a.update_b, b, a.ux + o16, a.compute_pi, a.pi + o16);
 }
 
-extern "C" __global__ __launch_bounds__(64) void hk_ric_trf(KArgs a) {
+template <class FX>
+__global__ __launch_bounds__(64) void hk_ric_trf(KArgs a) {
     const LdsTabs T = lds_tables(a);
     Scratch& sm = *T.sm;
     const int p = blockIdx.x + a.p0;
@@ -124,11 +135,16 @@ extern "C" __global__ __launch_bounds__(64) void hk_ric_trf(KArgs a) {
     double* F = a.ws + (long)p * a.sW;
     RicIO io = make_io(a, T, p, F);
     const long o16 = (long)p * a.sV16;
-    const double* Qx = a.vQx ? a.vQx + o16 : nullptr;
-    ric_backward<false>(io, &sm, 0, nullptr, 0, nullptr, a.use_box, Qx, nullptr, 0, nullptr);
+    BoxCtx bc{};
+    bc.Qx = a.vQx ? a.vQx + o16 : nullptr;
+    if (a.use_box)
+        ric_backward<false, BX_GIVEN, FX>(io, &sm, 0, nullptr, 0, nullptr, bc, 0, nullptr);
+    else
+        ric_backward<false, BX_NONE, FX>(io, &sm, 0, nullptr, 0, nullptr, bc, 0, nullptr);
 }
 
-extern "C" __global__ __launch_bounds__(64) void hk_ric_trs(KArgs a) {
+template <class FX>
+__global__ __launch_bounds__(64) void hk_ric_trs(KArgs a) {
     const LdsTabs T = lds_tables(a);
     Scratch& sm = *T.sm;
     const int p = blockIdx.x + a.p0;
@@ -136,30 +152,46 @@ extern "C" __global__ __launch_bounds__(64) void hk_ric_trs(KArgs a) {
     double* F = a.ws + (long)p * a.sW;
     RicIO io = make_io(a, T, p, F);
     const long o16 = (long)p * a.sV16;
-    const double* qx = a.vqx ? a.vqx + o16 : nullptr;
-    ric_trs(io, &sm, a.vb + o16, a.vq + o16, a.use_box, qx, a.ux + o16, a.compute_pi, a.pi + o16, a.compute_Pb,
-            a.vPb + o16);
+    BoxCtx bc{};
+    bc.qx = a.vqx ? a.vqx + o16 : nullptr;
+    double al = 1.0;
+    if (a.use_box)
+        ric_trs<BX_GIVEN, BX_NONE, FX>(io, &sm, a.vb + o16, a.vq + o16, bc, a.ux + o16, a.compute_pi, a.pi + o16,
+                                   a.compute_Pb, a.vPb + o16, al);
+    else
+        ric_trs<BX_NONE, BX_NONE, FX>(io, &sm, a.vb + o16, a.vq + o16, bc, a.ux + o16, a.compute_pi, a.pi + o16,
+                                  a.compute_Pb, a.vPb + o16, al);
 }
 
-extern "C" __global__ __launch_bounds__(64) void hk_res(KArgs a) {
+template <class FX>
+__global__ __launch_bounds__(64) void hk_res(KArgs a) {
     const LdsTabs T = lds_tables(a);
-    Scratch& sm = *T.sm;
     const int p = blockIdx.x + a.p0;
     if (p >= a.nprob) return;
     RicIO io = make_io(a, T, p, nullptr);
-    BoxTab bt{T.tileslot, T.slotvar};
     const long o16 = (long)p * a.sV16, o32 = (long)p * a.sV32;
     double* out = a.ws + (long)p * a.sW;  // [rq | rb] V16, [rd | rm] V32
     const long n1 = a.N + 1;
+    BoxCtx bc{};
+    bc.d = a.d + o32;
+    bc.lam = a.lam + o32;
+    bc.t = a.t + o32;
+    ResIO ro{};
+    ro.bsrc = a.vb ? a.vb + o16 : nullptr;
+    ro.qsrc = a.vq ? a.vq + o16 : nullptr;
+    ro.ux = a.ux + o16;
+    ro.pi = a.pi + o16;
+    ro.rq = out;
+    ro.rb = out + n1 * V16;
+    ro.rd = out + 2 * n1 * V16;
+    ro.rm = out + 2 * n1 * V16 + n1 * V32;
     double mu = 0.0;
-    const bool have = residuals(io, bt, &sm, a.vb ? a.vb + o16 : nullptr, a.vq ? a.vq + o16 : nullptr,
-                                a.ux + o16, a.pi + o16, a.d + o32, a.lam + o32, a.t + o32, out, out + n1 * V16,
-                                out + 2 * n1 * V16, out + 2 * n1 * V16 + n1 * V32, mu);
+    const bool have = residual_pass<false, FX>(io, bc, ro, mu);
     if (lane_id() == 0 && have) a.mu_out[p] = mu;
 }
 
 // ------------------------------------------------------------------------------------------------
-// IPM vector passes (d_aux_ip_hard_lib4.c), box constraints, four stages per pass.
+// IPM (d_ip2_res_mpc_hard_tv), persistent per problem.
 // ------------------------------------------------------------------------------------------------
 namespace {
 
@@ -198,336 +230,279 @@ __device__ void init_var(const RicIO& io, const BoxTab& bt, const double* dv, do
     wsync();
 }
 
-// sequential step-length rule of d_compute_alpha_* (:541-565): per lane, min-reduced afterwards
-__device__ __forceinline__ void alpha_rule(double& al, double lam, double dlam, double t, double dt) {
-    (void)t;
-    (void)dt;
-    if (-al * dlam > lam) al = -lam / dlam;
+__device__ __forceinline__ BoxCtx box_ctx(const Ws& w, const double* dv, double* lam, double* t) {
+    BoxCtx bc{};
+    bc.d = dv;
+    bc.lam = lam;
+    bc.t = t;
+    bc.dlam = w.dlam;
+    bc.dt = w.dt;
+    bc.t_inv = w.t_inv;
+    bc.lamt = w.lamt;
+    bc.res_d = w.res_d;
+    bc.res_m = w.res_m;
+    bc.qxs = w.qx;
+    bc.Qx = w.Qx;
+    bc.qx = w.qx;
+    return bc;
 }
 
 }  // namespace
 
-extern "C" __global__ __launch_bounds__(64) void hk_ipm(KArgs a) {
+// The IPM runs as one init kernel and then, per iteration, four pass kernels (factorisation, solve +
+// step length + mu_aff, corrector, update + residuals).  Every kernel handles the whole batch; a
+// problem that has finished returns at once.  Each pass kernel is a single stage loop, so it gets
+// its own register allocation, and rocprof reports the passes separately.
+namespace {
+
+struct IpmView {
+    int N, p, l;
+    Ws w;
+    RicIO io;
+    BoxTab bt;
+    double *ux, *pi, *lam, *t, *stat;
+    const double* dv;
+    BoxCtx bc;
+};
+
+__device__ __forceinline__ IpmView ipm_view(const KArgs& a, const LdsTabs& T, int p) {
+    IpmView v;
+    v.N = a.N;
+    v.p = p;
+    v.l = lane_id();
+    v.w = carve(a.ws + (long)p * a.sW, a.N);
+    v.io = make_io(a, T, p, v.w.F);
+    v.bt = BoxTab{T.tileslot, T.slotvar};
+    const long o16 = (long)p * a.sV16, o32 = (long)p * a.sV32;
+    v.ux = a.ux + o16;
+    v.pi = a.pi + o16;
+    v.lam = a.lam + o32;
+    v.t = a.t + o32;
+    v.dv = a.d + o32;
+    v.stat = a.stat + (long)p * 5 * a.k_max;
+    v.bc = box_ctx(v.w, v.dv, v.lam, v.t);
+    return v;
+}
+
+__device__ __forceinline__ ResIO res_io(const IpmView& v) {
+    ResIO ro{};
+    ro.ux = v.ux;
+    ro.pi = v.pi;
+    ro.dux = v.w.dux;
+    ro.dpi = v.w.dpi;
+    ro.ux_bkp = v.w.ux_bkp;
+    ro.pi_bkp = v.w.pi_bkp;
+    ro.lam_bkp = v.w.lam_bkp;
+    ro.t_bkp = v.w.t_bkp;
+    ro.rq = v.w.res_q;
+    ro.rb = v.w.res_b;
+    ro.rd = v.w.res_d;
+    ro.rm = v.w.res_m;
+    return ro;
+}
+
+// End of an iteration (or of init): decide whether the problem continues, switching from phase 1 to
+// phase 2 (with the phase-2 start residuals) when phase 1's loop condition fails.
+template <class FX>
+__device__ void ipm_continue(const KArgs& a, IpmView& v, int kk, double mu, double alpha, double sigma, int phase) {
+    const bool sn = a.single_newton != 0;
+    if (phase == 1) {
+        const double mu_tol_low = a.mu_tol < 1e-5 ? 1e-5 : a.mu_tol;
+        if (!(kk < a.k_max && mu > mu_tol_low && alpha >= a.alpha_min)) {
+            residual_pass<false, FX>(v.io, v.bc, res_io(v), mu);  // phase-2 start (d_ip2_res_hard.c:756-781)
+            wsync();
+            phase = 2;
+        }
+    }
+    bool active = phase == 1;
+    if (phase == 2) active = kk < a.k_max && (sn || (mu > a.mu_tol && alpha >= a.alpha_min));
+    int ret = 0;
+    if (!active) {
+        if (!sn && mu <= a.mu_tol)
+            ret = 0;
+        else if (kk >= a.k_max)
+            ret = 1;
+        else if (alpha < a.alpha_min)
+            ret = 2;
+        else
+            ret = -1;
+    }
+    if (v.l == 0) {
+        double* st = v.w.state;
+        st[S_MU] = mu;
+        st[S_ALPHA] = alpha;
+        st[S_SIGMA] = sigma;
+        st[S_KK] = kk;
+        st[S_PHASE] = phase;
+        st[S_ACTIVE] = active ? 1.0 : 0.0;
+        if (!active) {
+            a.kk[v.p] = kk;
+            a.ret[v.p] = ret;
+        }
+    }
+}
+
+}  // namespace
+
+template <class FX>
+__global__ __launch_bounds__(64) void hk_ipm_init(KArgs a) {
     const LdsTabs T = lds_tables(a);
     Scratch& sm = *T.sm;
     const int p = blockIdx.x + a.p0;
     if (p >= a.nprob) return;
-    const int N = a.N;
-    Ws w = carve(a.ws + (long)p * a.sW, N);
-    RicIO io = make_io(a, T, p, w.F);
-    BoxTab bt{T.tileslot, T.slotvar};
-    const long o16 = (long)p * a.sV16, o32 = (long)p * a.sV32;
-    double* ux = a.ux + o16;
-    double* pi = a.pi + o16;
-    double* lam = a.lam + o32;
-    double* t = a.t + o32;
-    const double* dv = a.d + o32;
-    double* stat = a.stat + (long)p * 5 * a.k_max;
-    const int l = lane_id();
-
+    IpmView v = ipm_view(a, T, p);
+    const int N = v.N, l = v.l;
     int nbt = 0;
-    for (int k = 0; k <= N; k++) nbt += io.st[k].nb;
-    int kk = 0, ret;
+    for (int k = 0; k <= N; k++) nbt += v.io.st[k].nb;
     if (nbt == 0) {
         // no constraints: one sv and return (d_ip2_res_hard.c:428-450)
-        ric_backward<true>(io, &sm, 0, nullptr, 0, nullptr, 0, nullptr, nullptr, 1, w.Pb);
+        ric_backward<true, BX_NONE, FX>(v.io, &sm, 0, nullptr, 0, nullptr, v.bc, 1, v.w.Pb);
         wsync();
-        ric_forward_sv(io, &sm, 0, nullptr, ux, a.compute_mult, pi);
+        ric_forward_sv<FX>(v.io, &sm, 0, nullptr, v.ux, a.compute_mult, v.pi);
         wsync();
         for (int i = l; i < (N + 1) * V16; i += 64) {
-            w.ux_bkp[i] = ux[i];
-            w.pi_bkp[i] = pi[i];
+            v.w.ux_bkp[i] = v.ux[i];
+            v.w.pi_bkp[i] = v.pi[i];
         }
         if (l == 0) {
+            v.w.state[S_ACTIVE] = 0.0;
             a.kk[p] = 0;
             a.ret[p] = 0;
         }
         return;
     }
-    const double mu_scal = 1.0 / (2.0 * nbt);
     // single Newton step (d_ip2_res_hard.c:1348-1919): the caller's ux/pi/lam/t already hold the start
     // iterate (d_init_var_mpc_hard_tv_single_newton is a copy, done by the host), no phase 1.
     const bool sn = a.single_newton != 0;
-    if (!sn) init_var(io, bt, dv, ux, pi, lam, t, a.mu0, a.warm_start);
-    for (int i = l; i < (N + 1) * V16; i += 64) w.dpi[i] = 0.0;
+    if (!sn) init_var(v.io, v.bt, v.dv, v.ux, v.pi, v.lam, v.t, a.mu0, a.warm_start);
+    for (int i = l; i < (N + 1) * V16; i += 64) v.w.dpi[i] = 0.0;
+    if (l == 0) v.w.state[S_MUSCAL] = 1.0 / (2.0 * nbt);
+    wsync();
+    double mu = a.mu0;
+    if (sn) {  // straight to phase 2: its start residuals
+        residual_pass<false, FX>(v.io, v.bc, res_io(v), mu);
+        wsync();
+    }
+    ipm_continue<FX>(a, v, 0, mu, 1.0, 0.0, sn ? 2 : 1);
+}
 
-    double mu = a.mu0, alpha = 1.0, sigma = 0.0;
-    const double mu_tol_low = a.mu_tol < 1e-5 ? 1e-5 : a.mu_tol;
+// Factorisation of the iteration's KKT system, Hessian / gradient box terms fused into the fetch.
+template <class FX>
+__global__ __launch_bounds__(64) void hk_ipm_fact(KArgs a) {
+    const LdsTabs T = lds_tables(a);
+    Scratch& sm = *T.sm;
+    const int p = blockIdx.x + a.p0;
+    if (p >= a.nprob) return;
+    IpmView v = ipm_view(a, T, p);
+    const double* st = v.w.state;
+    if (st[S_ACTIVE] == 0.0) return;
+    const bool sn = a.single_newton != 0;
+    if (st[S_PHASE] == 1.0)
+        ric_backward<true, BX_P1, FX>(v.io, &sm, 0, nullptr, 0, nullptr, v.bc, 1, v.w.Pb);
+    else  // the single-Newton variant factorises with the data's own b/q rows (d_ip2_res_hard.c:1700-1760)
+        ric_backward<true, BX_P2, FX>(v.io, &sm, !sn, v.w.res_b, !sn, v.w.res_q, v.bc, 1, v.w.Pb);
+}
 
-    // ------------------------------ phase 1 (d_ip2_res_hard.c:498-718) ------------------------------
-    while (!sn && kk < a.k_max && mu > mu_tol_low && alpha >= a.alpha_min) {
-        HK_FOR_BOX(io, k, {  // d_update_hessian_mpc_hard_tv, sigma_mu = 0
-            const double til = 1.0 / t[lo], tiu = 1.0 / t[up];
-            const double ltl = lam[lo] * til, ltu = lam[up] * tiu;
-            const double dll = til * 0.0, dlu = tiu * 0.0;
-            w.t_inv[lo] = til;
-            w.t_inv[up] = tiu;
-            w.lamt[lo] = ltl;
-            w.lamt[up] = ltu;
-            w.dlam[lo] = dll;
-            w.dlam[up] = dlu;
-            w.Qx[k * V16 + slot] = ltl + ltu;
-            w.qx[k * V16 + slot] = lam[up] - ltu * dv[up] + dlu - lam[lo] - ltl * dv[lo] - dll;
-        });
-        wsync();
-        ric_backward<true>(io, &sm, 0, nullptr, 0, nullptr, 1, w.Qx, w.qx, 1, w.Pb);
-        wsync();
-        ric_forward_sv(io, &sm, 0, nullptr, w.dux, a.compute_mult, w.dpi);
-        wsync();
-        double al = 1.0;
-        HK_FOR_BOX(io, k, {  // d_compute_alpha_mpc_hard_tv
-            const int v = bt.slotvar[k * 16 + slot];
-            const double x = w.dux[k * V16 + v];
-            const double dtl = x - dv[lo] - t[lo], dtu = -x + dv[up] - t[up];
-            const double dll = w.dlam[lo] - (w.lamt[lo] * dtl + lam[lo]);
-            const double dlu = w.dlam[up] - (w.lamt[up] * dtu + lam[up]);
-            w.dt[lo] = dtl;
-            w.dt[up] = dtu;
-            w.dlam[lo] = dll;
-            w.dlam[up] = dlu;
-            alpha_rule(al, lam[lo], dll, 0, 0);
-            alpha_rule(al, lam[up], dlu, 0, 0);
-            alpha_rule(al, t[lo], dtl, 0, 0);
-            alpha_rule(al, t[up], dtu, 0, 0);
-        });
-        al = wave_min(al);
-        wsync();
-        if (l == 0) {
-            stat[5 * kk] = sigma;
-            stat[5 * kk + 1] = al;
-        }
-        alpha = al * 0.995;
-        double ms = 0.0;
-        HK_FOR_BOX(io, k, {  // d_compute_mu_mpc_hard_tv
-            ms += (lam[lo] + alpha * w.dlam[lo]) * (t[lo] + alpha * w.dt[lo]) +
-                  (lam[up] + alpha * w.dlam[up]) * (t[up] + alpha * w.dt[up]);
-        });
-        const double mu_aff = wave_sum(ms) * mu_scal;
-        if (l == 0) stat[5 * kk + 2] = mu_aff;
+// Predictor solve with the box steps and step length fused in, then mu_aff and the centering target.
+template <class FX>
+__global__ __launch_bounds__(64) void hk_ipm_pred(KArgs a) {
+    const LdsTabs T = lds_tables(a);
+    Scratch& sm = *T.sm;
+    const int p = blockIdx.x + a.p0;
+    if (p >= a.nprob) return;
+    IpmView v = ipm_view(a, T, p);
+    double* st = v.w.state;
+    if (st[S_ACTIVE] == 0.0) return;
+    const bool sn = a.single_newton != 0;
+    const int phase = (int)st[S_PHASE], kk = (int)st[S_KK];
+    const double mu = st[S_MU];
+    double sigma = st[S_SIGMA];
+    double al = 1.0;
+    if (phase == 1) {
+        v.bc.pred = 1;
+        ric_forward<0, BX_P1, FX>(v.io, &sm, nullptr, 0, v.w.dux, a.compute_mult, v.w.dpi, v.bc, al);
+    } else {
+        ric_forward<0, BX_P2, FX>(v.io, &sm, v.w.res_b, !sn, v.w.dux, a.compute_mult, v.w.dpi, v.bc, al);
+    }
+    al = wave_min(al);
+    wsync();
+    const double alpha = al * 0.995;
+    const double mu_aff = mu_aff_pass<7>(v.io, v.bc, alpha, st[S_MUSCAL]);
+    double smu = a.mu0;  // single Newton: sigma*mu is supplied by the caller as mu0 (:1788-1790)
+    if (!sn) {
         sigma = mu_aff / mu;
         sigma = sigma * sigma * sigma;
-        const double smu = sigma * mu;
-        HK_FOR_BOX(io, k, {  // d_update_gradient_mpc_hard_tv
-            const double dll = w.t_inv[lo] * (smu - w.dlam[lo] * w.dt[lo]);
-            const double dlu = w.t_inv[up] * (smu - w.dlam[up] * w.dt[up]);
-            w.dlam[lo] = dll;
-            w.dlam[up] = dlu;
-            w.qx[k * V16 + slot] += dlu - dll;
-        });
-        wsync();
-        ric_trs(io, &sm, nullptr, nullptr, 1, w.qx, w.dux, a.compute_mult, w.dpi, 0, w.Pb);
-        wsync();
-        al = 1.0;
-        HK_FOR_BOX(io, k, {
-            const int v = bt.slotvar[k * 16 + slot];
-            const double x = w.dux[k * V16 + v];
-            const double dtl = x - dv[lo] - t[lo], dtu = -x + dv[up] - t[up];
-            const double dll = w.dlam[lo] - (w.lamt[lo] * dtl + lam[lo]);
-            const double dlu = w.dlam[up] - (w.lamt[up] * dtu + lam[up]);
-            w.dt[lo] = dtl;
-            w.dt[up] = dtu;
-            w.dlam[lo] = dll;
-            w.dlam[up] = dlu;
-            alpha_rule(al, lam[lo], dll, 0, 0);
-            alpha_rule(al, lam[up], dlu, 0, 0);
-            alpha_rule(al, t[lo], dtl, 0, 0);
-            alpha_rule(al, t[up], dtu, 0, 0);
-        });
-        al = wave_min(al);
-        wsync();
-        if (l == 0) {
-            stat[5 * kk] = sigma;
-            stat[5 * kk + 3] = al;
-        }
-        alpha = al * 0.995;
-        // backup + d_update_var_mpc_hard_tv (phase-1 dux/dpi are full iterates)
-        for (int k = 0; k <= N; k++) {
-            const StageInfo si = load_stage(io.st, k);
-            if (l < si.nu + si.nx) {
-                const int i = k * V16 + l;
-                const double x = ux[i];
-                w.ux_bkp[i] = x;
-                ux[i] = x + alpha * (w.dux[i] - x);
-            }
-            if (k < N && l < si.nx1) {
-                const int i = k * V16 + l;
-                const double y = pi[i];
-                w.pi_bkp[i] = y;
-                pi[i] = y + alpha * (w.dpi[i] - y);
-            }
-        }
-        ms = 0.0;
-        HK_FOR_BOX(io, k, {
-            w.lam_bkp[lo] = lam[lo];
-            w.lam_bkp[up] = lam[up];
-            w.t_bkp[lo] = t[lo];
-            w.t_bkp[up] = t[up];
-            const double ll = lam[lo] + alpha * w.dlam[lo], lu = lam[up] + alpha * w.dlam[up];
-            const double tl = t[lo] + alpha * w.dt[lo], tu = t[up] + alpha * w.dt[up];
-            lam[lo] = ll;
-            lam[up] = lu;
-            t[lo] = tl;
-            t[up] = tu;
-            ms += ll * tl + lu * tu;
-        });
-        mu = wave_sum(ms) * mu_scal;
-        if (l == 0) stat[5 * kk + 4] = mu;
-        kk++;
-        wsync();
+        smu = sigma * mu;
     }
+    if (v.l == 0) {
+        v.stat[5 * kk] = st[S_SIGMA];
+        v.stat[5 * kk + 1] = al;
+        v.stat[5 * kk + 2] = mu_aff;
+        st[S_SIGMA] = sigma;
+        st[S_SMU] = smu;
+    }
+}
 
-    // ------------------------------ phase 2 (d_ip2_res_hard.c:756-1273) ------------------------------
-    residuals(io, bt, &sm, nullptr, nullptr, ux, pi, dv, lam, t, w.res_q, w.res_b, w.res_d, w.res_m, mu);
-    wsync();
-    const int kk_p2 = kk;  // first phase-2 iteration (diagnostic stamps only)
-    (void)kk_p2;
-    while (kk < a.k_max && (sn || (mu > a.mu_tol && alpha >= a.alpha_min))) {
-        HK_STAMP(32, kk == kk_p2 ? 50 : -1);
-        HK_FOR_BOX(io, k, {  // d_update_hessian_gradient_res_mpc_hard_tv
-            const double til = 1.0 / t[lo], tiu = 1.0 / t[up];
-            w.t_inv[lo] = til;
-            w.t_inv[up] = tiu;
-            w.Qx[k * V16 + slot] = til * lam[lo] + tiu * lam[up];
-            w.qx[k * V16 + slot] = til * (w.res_m[lo] - lam[lo] * w.res_d[lo]) -
-                                   tiu * (w.res_m[up] + lam[up] * w.res_d[up]);
-        });
-        wsync();
-        HK_STAMP(33, kk == kk_p2 ? 50 : -1);
-        // the single-Newton variant factorises with the data's own b/q rows (d_ip2_res_hard.c:1700-1760)
-        ric_backward<true>(io, &sm, !sn, w.res_b, !sn, w.res_q, 1, w.Qx, w.qx, 1, w.Pb);
-        wsync();
-        HK_STAMP(34, kk == kk_p2 ? 50 : -1);
-        ric_forward_sv(io, &sm, !sn, w.res_b, w.dux, a.compute_mult, w.dpi);
-        wsync();
-        HK_STAMP(35, kk == kk_p2 ? 50 : -1);
-        double al = 1.0;
-        HK_FOR_BOX(io, k, {  // d_compute_alpha_res_mpc_hard_tv
-            const int v = bt.slotvar[k * 16 + slot];
-            const double x = w.dux[k * V16 + v];
-            const double dtl = x - w.res_d[lo], dtu = -x + w.res_d[up];
-            const double dll = -w.t_inv[lo] * (lam[lo] * dtl + w.res_m[lo]);
-            const double dlu = -w.t_inv[up] * (lam[up] * dtu + w.res_m[up]);
-            w.dt[lo] = dtl;
-            w.dt[up] = dtu;
-            w.dlam[lo] = dll;
-            w.dlam[up] = dlu;
-            alpha_rule(al, lam[lo], dll, 0, 0);
-            alpha_rule(al, lam[up], dlu, 0, 0);
-            alpha_rule(al, t[lo], dtl, 0, 0);
-            alpha_rule(al, t[up], dtu, 0, 0);
-        });
-        al = wave_min(al);
-        wsync();
-        if (l == 0) {
-            stat[5 * kk] = sigma;
-            stat[5 * kk + 1] = al;
-        }
-        alpha = al * 0.995;
-        HK_STAMP(36, kk == kk_p2 ? 50 : -1);
-        double ms = 0.0;
-        HK_FOR_BOX(io, k, {  // d_compute_mu_res_mpc_hard_tv
-            ms += (lam[lo] + alpha * w.dlam[lo]) * (t[lo] + alpha * w.dt[lo]) +
-                  (lam[up] + alpha * w.dlam[up]) * (t[up] + alpha * w.dt[up]);
-        });
-        const double mu_aff = wave_sum(ms) * mu_scal;
-        if (l == 0) stat[5 * kk + 2] = mu_aff;
-        HK_STAMP(37, kk == kk_p2 ? 50 : -1);
-        double smu = a.mu0;  // single Newton: sigma*mu is supplied by the caller as mu0 (:1788-1790)
-        if (!sn) {
-            sigma = mu_aff / mu;
-            sigma = sigma * sigma * sigma;
-            smu = sigma * mu;
-        }
-        HK_FOR_BOX(io, k, {  // centering correction + d_update_gradient_res_mpc_hard_tv
-            const double rml = w.res_m[lo] + (w.dt[lo] * w.dlam[lo] - smu);
-            const double rmu = w.res_m[up] + (w.dt[up] * w.dlam[up] - smu);
-            w.res_m[lo] = rml;
-            w.res_m[up] = rmu;
-            w.qx[k * V16 + slot] = w.t_inv[lo] * (rml - lam[lo] * w.res_d[lo]) -
-                                   w.t_inv[up] * (rmu + lam[up] * w.res_d[up]);
-        });
-        wsync();
-        HK_STAMP(38, kk == kk_p2 ? 50 : -1);
-        ric_trs(io, &sm, w.res_b, w.res_q, 1, w.qx, w.dux, a.compute_mult, w.dpi, 0, w.Pb);
-        wsync();
-        HK_STAMP(39, kk == kk_p2 ? 50 : -1);
-        al = 1.0;
-        HK_FOR_BOX(io, k, {
-            const int v = bt.slotvar[k * 16 + slot];
-            const double x = w.dux[k * V16 + v];
-            const double dtl = x - w.res_d[lo], dtu = -x + w.res_d[up];
-            const double dll = -w.t_inv[lo] * (lam[lo] * dtl + w.res_m[lo]);
-            const double dlu = -w.t_inv[up] * (lam[up] * dtu + w.res_m[up]);
-            w.dt[lo] = dtl;
-            w.dt[up] = dtu;
-            w.dlam[lo] = dll;
-            w.dlam[up] = dlu;
-            alpha_rule(al, lam[lo], dll, 0, 0);
-            alpha_rule(al, lam[up], dlu, 0, 0);
-            alpha_rule(al, t[lo], dtl, 0, 0);
-            alpha_rule(al, t[up], dtu, 0, 0);
-        });
-        al = wave_min(al);
-        wsync();
-        if (l == 0) {
-            stat[5 * kk] = sigma;
-            stat[5 * kk + 3] = al;
-        }
-        alpha = al * 0.995;
-        HK_STAMP(40, kk == kk_p2 ? 50 : -1);
-        // d_backup_update_var_res_mpc_hard_tv (phase-2 dux/dpi are deltas)
-        for (int k = 0; k <= N; k++) {
-            const StageInfo si = load_stage(io.st, k);
-            if (l < si.nu + si.nx) {
-                const int i = k * V16 + l;
-                const double x = ux[i];
-                w.ux_bkp[i] = x;
-                ux[i] = x + alpha * w.dux[i];
-            }
-            if (k < N && l < si.nx1) {
-                const int i = k * V16 + l;
-                const double y = pi[i];
-                w.pi_bkp[i] = y;
-                pi[i] = y + alpha * w.dpi[i];
-            }
-        }
-        HK_FOR_BOX(io, k, {
-            w.lam_bkp[lo] = lam[lo];
-            w.lam_bkp[up] = lam[up];
-            w.t_bkp[lo] = t[lo];
-            w.t_bkp[up] = t[up];
-            lam[lo] += alpha * w.dlam[lo];
-            lam[up] += alpha * w.dlam[up];
-            t[lo] += alpha * w.dt[lo];
-            t[up] += alpha * w.dt[up];
-        });
-        wsync();
-        HK_STAMP(41, kk == kk_p2 ? 50 : -1);
-        residuals(io, bt, &sm, nullptr, nullptr, ux, pi, dv, lam, t, w.res_q, w.res_b, w.res_d, w.res_m, mu);
-        wsync();
-        if (l == 0) stat[5 * kk + 4] = mu;
-        HK_STAMP(42, kk == kk_p2 ? 50 : -1);
-        kk++;
-    }
-    if (!sn && mu <= a.mu_tol)
-        ret = 0;
-    else if (kk >= a.k_max)
-        ret = 1;
-    else if (alpha < a.alpha_min)
-        ret = 2;
+// Corrector: centering / gradient update fused into the trs backward, box steps + alpha into its forward.
+template <class FX>
+__global__ __launch_bounds__(64) void hk_ipm_corr(KArgs a) {
+    const LdsTabs T = lds_tables(a);
+    Scratch& sm = *T.sm;
+    const int p = blockIdx.x + a.p0;
+    if (p >= a.nprob) return;
+    IpmView v = ipm_view(a, T, p);
+    double* st = v.w.state;
+    if (st[S_ACTIVE] == 0.0) return;
+    const int phase = (int)st[S_PHASE], kk = (int)st[S_KK];
+    v.bc.smu = st[S_SMU];
+    double al = 1.0;
+    if (phase == 1)
+        ric_trs<BX_P1, BX_P1, FX>(v.io, &sm, nullptr, nullptr, v.bc, v.w.dux, a.compute_mult, v.w.dpi, 0, v.w.Pb, al);
     else
-        ret = -1;
-    if (l == 0) {
-        a.kk[p] = kk;
-        a.ret[p] = ret;
+        ric_trs<BX_P2, BX_P2, FX>(v.io, &sm, v.w.res_b, v.w.res_q, v.bc, v.w.dux, a.compute_mult, v.w.dpi, 0, v.w.Pb,
+                              al);
+    al = wave_min(al);
+    if (v.l == 0) {
+        v.stat[5 * kk] = st[S_SIGMA];
+        v.stat[5 * kk + 3] = al;
+        st[S_ALPHA] = al * 0.995;
     }
+}
+
+// Update of the iterate (with backups) and, in phase 2, the residuals of the new iterate; loop control.
+template <class FX>
+__global__ __launch_bounds__(64) void hk_ipm_update(KArgs a) {
+    const LdsTabs T = lds_tables(a);
+    const int p = blockIdx.x + a.p0;
+    if (p >= a.nprob) return;
+    IpmView v = ipm_view(a, T, p);
+    double* st = v.w.state;
+    if (st[S_ACTIVE] == 0.0) return;
+    const int phase = (int)st[S_PHASE];
+    int kk = (int)st[S_KK];
+    const double alpha = st[S_ALPHA];
+    double mu;
+    if (phase == 1) {
+        mu = update_p1_pass<4>(v.io, v.bc, alpha, st[S_MUSCAL], v.ux, v.pi, v.w.dux, v.w.dpi, v.w.ux_bkp,
+                               v.w.pi_bkp, v.w.lam_bkp, v.w.t_bkp);
+    } else {
+        ResIO ro = res_io(v);
+        ro.alpha = alpha;
+        mu = st[S_MU];
+        residual_pass<true, FX>(v.io, v.bc, ro, mu);
+    }
+    wsync();
+    if (v.l == 0) v.stat[5 * kk + 4] = mu;
+    kk++;
+    ipm_continue<FX>(a, v, kk, mu, alpha, st[S_SIGMA], phase);
 }
 
 // ------------------------------------------------------------------------------------------------
 // d_kkt_solve_new_rhs_res_mpc_hard_tv: re-solve with the factor + iterate persisted in ws.
 // vb/vq hold the new b (state order) / q (variable order).
 // ------------------------------------------------------------------------------------------------
-extern "C" __global__ __launch_bounds__(64) void hk_kkt_new_rhs(KArgs a) {
+template <class FX>
+__global__ __launch_bounds__(64) void hk_kkt_new_rhs(KArgs a) {
     const LdsTabs T = lds_tables(a);
     Scratch& sm = *T.sm;
     const int p = blockIdx.x + a.p0;
@@ -543,6 +518,7 @@ extern "C" __global__ __launch_bounds__(64) void hk_kkt_new_rhs(KArgs a) {
     double* t = a.t + o32;
     const double* dv = a.d + o32;
     const int l = lane_id();
+    BoxCtx bc = box_ctx(w, dv, lam, t);
     for (int i = l; i < (N + 1) * V16; i += 64) {
         ux[i] = w.ux_bkp[i];
         pi[i] = w.pi_bkp[i];
@@ -553,14 +529,24 @@ extern "C" __global__ __launch_bounds__(64) void hk_kkt_new_rhs(KArgs a) {
     }
     wsync();
     double mu = 0.0;
-    residuals(io, bt, &sm, a.vb + o16, a.vq + o16, ux, pi, dv, lam, t, w.res_q, w.res_b, w.res_d, w.res_m, mu);
+    ResIO ro{};
+    ro.bsrc = a.vb + o16;
+    ro.qsrc = a.vq + o16;
+    ro.ux = ux;
+    ro.pi = pi;
+    ro.rq = w.res_q;
+    ro.rb = w.res_b;
+    ro.rd = w.res_d;
+    ro.rm = w.res_m;
+    residual_pass<false, FX>(io, bc, ro, mu);
     wsync();
     HK_FOR_BOX(io, k, {
         w.qx[k * V16 + slot] = w.t_inv[lo] * (w.res_m[lo] - lam[lo] * w.res_d[lo]) -
                                w.t_inv[up] * (w.res_m[up] + lam[up] * w.res_d[up]);
     });
     wsync();
-    ric_trs(io, &sm, w.res_b, w.res_q, 1, w.qx, w.dux, a.compute_mult, w.dpi, 1, w.Pb);
+    double al = 1.0;
+    ric_trs<BX_GIVEN, BX_NONE, FX>(io, &sm, w.res_b, w.res_q, bc, w.dux, a.compute_mult, w.dpi, 1, w.Pb, al);
     wsync();
     HK_FOR_BOX(io, k, {  // d_compute_dt_dlam_res + d_update_var_res (alpha = 1)
         const int v = bt.slotvar[k * 16 + slot];
@@ -590,6 +576,38 @@ extern "C" __global__ __launch_bounds__(64) void hk_kkt_new_rhs(KArgs a) {
 // ------------------------------------------------------------------------------------------------
 // Host launch helpers (called from the C-ABI translation unit).
 // ------------------------------------------------------------------------------------------------
+template <class FX>
+static int launch_t(int which, const KArgs* a, int count, hipStream_t stream) {
+    dim3 grid(count), block(64);
+    const size_t lds = sizeof(Scratch) + (size_t)(a->N + 1) * (sizeof(StageInfo) + 32);
+    switch (which) {
+        case 0: hipLaunchKernelGGL(hk_ric_sv<FX>, grid, block, lds, stream, *a); break;
+        case 1: hipLaunchKernelGGL(hk_ric_trf<FX>, grid, block, lds, stream, *a); break;
+        case 2: hipLaunchKernelGGL(hk_ric_trs<FX>, grid, block, lds, stream, *a); break;
+        case 3: hipLaunchKernelGGL(hk_res<FX>, grid, block, lds, stream, *a); break;
+        case 4:
+            hipLaunchKernelGGL(hk_ipm_init<FX>, grid, block, lds, stream, *a);
+            for (int it = 0; it < a->k_max; it++) {
+                hipLaunchKernelGGL(hk_ipm_fact<FX>, grid, block, lds, stream, *a);
+                hipLaunchKernelGGL(hk_ipm_pred<FX>, grid, block, lds, stream, *a);
+                hipLaunchKernelGGL(hk_ipm_corr<FX>, grid, block, lds, stream, *a);
+                hipLaunchKernelGGL(hk_ipm_update<FX>, grid, block, lds, stream, *a);
+            }
+            break;
+        case 5: hipLaunchKernelGGL(hk_kkt_new_rhs<FX>, grid, block, lds, stream, *a); break;
+        default: return -1;
+    }
+    return (int)hipGetLastError();
+}
+
+// Compiled inner-stage classes (KArgs.fixcls): 0 generic, 1 nu=4 nx=12, 2 nu=3 nx=8.  The plan picks
+// the class and flags its stages (StageInfo.r0); any other problem runs the generic kernels.
+extern "C" int hk_fixcls(int nu, int nx) {
+    if (nu == 4 && nx == 12) return 1;
+    if (nu == 3 && nx == 8) return 2;
+    return 0;
+}
+
 extern "C" int hk_launch(int which, const KArgs* a, int count, hipStream_t stream) {
     if (count <= 0) return 0;
 #ifdef HK_STAMPS
@@ -600,16 +618,9 @@ extern "C" int hk_launch(int which, const KArgs* a, int count, hipStream_t strea
         (void)hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_stage), &st, sizeof(st));
     }
 #endif
-    dim3 grid(count), block(64);
-    const size_t lds = sizeof(Scratch) + (size_t)(a->N + 1) * (sizeof(StageInfo) + 32);
-    switch (which) {
-        case 0: hipLaunchKernelGGL(hk_ric_sv, grid, block, lds, stream, *a); break;
-        case 1: hipLaunchKernelGGL(hk_ric_trf, grid, block, lds, stream, *a); break;
-        case 2: hipLaunchKernelGGL(hk_ric_trs, grid, block, lds, stream, *a); break;
-        case 3: hipLaunchKernelGGL(hk_res, grid, block, lds, stream, *a); break;
-        case 4: hipLaunchKernelGGL(hk_ipm, grid, block, lds, stream, *a); break;
-        case 5: hipLaunchKernelGGL(hk_kkt_new_rhs, grid, block, lds, stream, *a); break;
-        default: return -1;
+    switch (a->fixcls) {
+        case 1: return launch_t<FixSh<4, 12>>(which, a, count, stream);
+        case 2: return launch_t<FixSh<3, 8>>(which, a, count, stream);
+        default: return launch_t<NoFix>(which, a, count, stream);
     }
-    return (int)hipGetLastError();
 }
