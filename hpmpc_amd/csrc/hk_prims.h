@@ -76,6 +76,22 @@ __device__ __forceinline__ double rowgroup_bcast(double x) {
     return mk(hi2, lo2);
 }
 
+// Branch-free 4-way selects.  Written as bit tests on the lane index so that the optimiser keeps
+// them as v_cndmask (equality chains on one variable get turned into a switch, i.e. exec-mask
+// branches).  sel_g: by row group g = lane >> 4; sel_q: by q = c & 3 (c = lane & 15).
+__device__ __forceinline__ double sel_g(double a0, double a1, double a2, double a3) {
+    const int l = __builtin_amdgcn_workitem_id_x() & 63;
+    const bool b0 = (l & 16) != 0, b1 = (l & 32) != 0;
+    const double lo = b0 ? a1 : a0, hi = b0 ? a3 : a2;
+    return b1 ? hi : lo;
+}
+__device__ __forceinline__ double sel_q(double a0, double a1, double a2, double a3) {
+    const int l = __builtin_amdgcn_workitem_id_x() & 63;
+    const bool b0 = (l & 1) != 0, b1 = (l & 2) != 0;
+    const double lo = b0 ? a1 : a0, hi = b0 ? a3 : a2;
+    return b1 ? hi : lo;
+}
+
 // Gather the four row groups: x[j] at lane (g,c) = v at lane (j,c), for all j at once.
 // One v_permlane32_swap per dword splits the halves, one v_permlane16_swap per dword and half
 // splits the rows: 6 cross-lane ops for the whole 4x16 transpose-by-row-group.

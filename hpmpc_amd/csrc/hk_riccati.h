@@ -60,7 +60,7 @@ struct Scratch {
 // col layout value (lane (g,c) holds v[c]) -> row layout (reg r holds v[g+4r])
 __device__ __forceinline__ void col2row(Scratch* sm, double vc, double vr[4]) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
-    if (g == 0) sm->v[c] = vc;
+    sm->v[c] = vc;  // the four row groups write the same value (no exec-mask branch)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -72,10 +72,8 @@ __device__ __forceinline__ void col2row(Scratch* sm, double vc, double vr[4]) {
 // row layout (reg r holds v[g+4r], replicated over the columns) -> col layout (lane (g,c) holds v[c])
 __device__ __forceinline__ double row2col(Scratch* sm, const double vr[4]) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
-    if (c == 0) {
 #pragma unroll
-        for (int r = 0; r < 4; r++) sm->v[16 + g + 4 * r] = vr[r];
-    }
+    for (int r = 0; r < 4; r++) sm->v[16 + g + 4 * r] = vr[r];  // replicas write identical values
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     const double v = sm->v[16 + c];
@@ -148,19 +146,22 @@ __device__ __forceinline__ void chol_block(d4& M, double& ml, double lr[4], doub
     const double p3 = fma(-p2, l32, fma(-p1, l31, fma(-p0, l30, m3))) * i3;
     HK_BSTAMP(5);
     // upper storage row 4B+g:  diagonal s_g, then L[c][4B+g] = y_g (c > 4B+g).  Branch-free selects.
-    const double yg = g == 0 ? y0 : g == 1 ? y1 : g == 2 ? y2 : y3;
-    const double sg = g == 0 ? s0 : g == 1 ? s1 : g == 2 ? s2 : s3;
+    const double yg = sel_g(y0, y1, y2, y3);
+    const double sg = sel_g(s0, s1, s2, s3);
     M[B] = (c == 4 * B + g) ? sg : yg;
     const int j = c - 4 * B;
-    invd = j == 0 ? i0 : j == 1 ? i1 : j == 2 ? i2 : j == 3 ? i3 : invd;
+    const bool inb = (c >> 2) == B, below = c > 4 * B + 3;
+    invd = inb ? sel_q(i0, i1, i2, i3) : invd;
     if (AUG) {
-        lr[B] = g == 0 ? p0 : g == 1 ? p1 : g == 2 ? p2 : p3;
+        lr[B] = sel_g(p0, p1, p2, p3);
         const double mt = fma(-p3, y3, fma(-p2, y2, fma(-p1, y1, fma(-p0, y0, ml))));
-        ml = j >= 4 ? mt : j == 0 ? p0 : j == 1 ? p1 : j == 2 ? p2 : j == 3 ? p3 : ml;
+        const double mb = sel_q(p0, p1, p2, p3);
+        ml = below ? mt : (inb ? mb : ml);
     }
     HK_BSTAMP(6);
+    (void)j;
     if (B < 3) {
-        const double a = (j >= 4) ? yg : 0.0;
+        const double a = below ? yg : 0.0;
         M = mfma(-a, a, M);
     }
 #undef HK_BSTAMP
@@ -265,6 +266,9 @@ struct NoFix {  // generic kernels: no compile-time stage class
 // Run f(sh) with the stage's shape object: the constant one when the stage belongs to FX's class.
 template <class FX, class F>
 __device__ __forceinline__ void with_shape(const StageInfo& s, F&& f) {
+#ifdef HK_COUNT_FIXED
+    if constexpr (FX::enabled) { f(FX(s)); return; }
+#endif
     if constexpr (FX::enabled) {
         if (s.r0) {
             f(FX(s));
@@ -453,8 +457,7 @@ __device__ __forceinline__ void bwd_step(const RicIO& io, Scratch* sm, const SH&
     d4 M = cur.Mi;
     double ml = cur.mlq + qxv;  // update_q row (or RSQrq row) + drowad qx
 #pragma unroll
-    for (int r = 0; r < 4; r++)
-        if (g + 4 * r == c) M[r] += dq;  // ddiaadin: diag = bd + Qx
+    for (int r = 0; r < 4; r++) M[r] += (g + 4 * r == c) ? dq : 0.0;  // ddiaadin: diag = bd + Qx
     const int nx1 = sh.nx1, xo1 = sh.xo1;
     d4 acc = {0.0, 0.0, 0.0, 0.0};
     if (live) {
