@@ -6,8 +6,11 @@ MPC QPs per GPU, N=100, nx=12, nu=4 (nb = 4 / 10 / 6 on stage 0 / inner / N), fp
 stage data (no aliased buffers), solved by the residual-based Mehrotra IPM
 (d_ip2_res_mpc_hard_tv: mu0=2, mu_tol=1e-12, alpha_min=1e-8, k_max=50).
 
-A "step" is one batched IPM solve of the whole resident batch (one hk_ipm launch).  value = IP
-iterations per second over all ranks (sum of per-problem iteration counts / max-over-ranks time).
+A "step" is one batched IPM solve of the whole resident batch (pass kernels hk_ipm_init, then
+k_max x [hk_ipm_fact, hk_ipm_pred, hk_ipm_corr, hk_ipm_update]).  value = IP iterations per second
+over all ranks (sum of per-problem iteration counts / max-over-ranks time).  The roofline object is
+for the dominant kernel (the factorisation pass, hk_ipm_fact), timed with hipEvents around each of
+its launches inside the timed region.
 The Riccati factorisation rate (d_back_ric_rec_sv_tv_res, nb = 0, compute_pi = 1) of the same
 batch is reported in the same JSON line.
 
@@ -116,8 +119,8 @@ def main():
 
         dist.init_process_group("nccl")
 
-    from hpmpc_amd.batch import (BatchSolver, algorithmic_bytes_per_ip_iter, algorithmic_bytes_per_sv,
-                                 flops_ip_iter, flops_sv)
+    from hpmpc_amd.batch import (BatchSolver, algorithmic_bytes_per_fact, algorithmic_bytes_per_ip_iter,
+                                 algorithmic_bytes_per_sv, flops_ip_iter, flops_sv)
     from hpmpc_amd.shard import Reducer, make_shard
 
     B, N, nx, nu = args.batch, args.N, args.nx, args.nu
@@ -136,16 +139,15 @@ def main():
     max_over_ranks, sum_over_ranks = red.max, red.sum
 
     # ---------------- IPM (headline) ----------------
+    # One step = one batched solve (hpmpc_mi355x_ipm_batch_profiled: the same kernel sequence as
+    # hpmpc_mi355x_ipm_batch with a hipEvent pair around every pass kernel, on the solve's stream).
     for _ in range(args.warmup):
-        solver.ipm()
+        solver.ipm_profiled()
     barrier()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    barrier()
+    pass_ms = np.zeros(5)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        ev[i][0].record(stream)
-        solver.ipm()
-        ev[i][1].record(stream)
+        pass_ms += solver.ipm_profiled()
     barrier()
     t1 = time.perf_counter()
     dt = max_over_ranks(t1 - t0)
@@ -154,10 +156,16 @@ def main():
     iters_step = float(kk.sum())
     iters_total = sum_over_ranks(iters_step) * args.steps
     value = iters_total / dt
-    launch_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-
+    names = ["hk_ipm_init", "hk_ipm_fact", "hk_ipm_pred", "hk_ipm_corr", "hk_ipm_update"]
+    launches = np.array([1] + [args.k_max] * 4) * args.steps
+    dom = int(np.argmax(pass_ms))
+    bytes_fact = algorithmic_bytes_per_fact(qp)  # per problem-iteration of the factorisation pass
+    # algorithmic bytes of the factorisation kernel over the step / its device time over the step
+    fact_ms_step = pass_ms[1] / args.steps
+    achieved = iters_step * bytes_fact / (fact_ms_step * 1e-3) / 1e9
+    launch_ms = pass_ms[1] / launches[1]
     bytes_iter = algorithmic_bytes_per_ip_iter(qp)
-    achieved = iters_step * bytes_iter / (launch_ms * 1e-3) / 1e9  # GB/s of the hk_ipm launch
+    ipm_ms_step = pass_ms.sum() / args.steps
     fl_iter = flops_ip_iter(N, nx, nu)
 
     # ---------------- Riccati factorisation + solve ----------------
@@ -186,7 +194,7 @@ def main():
             with open(pmc) as f:
                 pm = json.load(f)
             if pm.get("workload") == f"ipm_N{N}_nx{nx}_nu{nu}_batch{B}":
-                traffic = pm.get("hbm_bytes_per_launch")
+                traffic = pm.get("kernels", {}).get("hk_ipm_fact", {}).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
 
@@ -216,9 +224,13 @@ def main():
                        "sum_kk_per_step": iters_total / args.steps, "ret_counts": {
                            str(int(r)): int((ret == r).sum()) for r in np.unique(ret)}},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": achieved / PEAK_HBM_GBS, "traffic": traffic, "kernel": "hk_ipm",
-                         "launch_ms": launch_ms, "algorithmic_bytes_per_ip_iter": bytes_iter,
-                         "fp64_tflops": iters_step * fl_iter / (launch_ms * 1e-3) / 1e12},
+                         "frac": achieved / PEAK_HBM_GBS, "traffic": traffic, "kernel": names[dom],
+                         "launch_ms": launch_ms, "launches_per_step": int(launches[1] // args.steps),
+                         "algorithmic_bytes_per_problem_iter": bytes_fact,
+                         "pass_ms_per_step": {n: float(v / args.steps) for n, v in zip(names, pass_ms)},
+                         "ipm_whole_solve": {"achieved_GBps": iters_step * bytes_iter / (ipm_ms_step * 1e-3) / 1e9,
+                                             "algorithmic_bytes_per_ip_iter": bytes_iter,
+                                             "fp64_tflops": iters_step * fl_iter / (ipm_ms_step * 1e-3) / 1e12}},
             "riccati": {"value": fact_total / rdt, "unit": "fact/s", "kernel": "hk_ric_sv", "launch_ms": sv_ms,
                         "roofline": {"bound": "hbm", "achieved": sv_achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                                      "frac": sv_achieved / PEAK_HBM_GBS,

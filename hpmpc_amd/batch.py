@@ -43,6 +43,12 @@ def lib() -> C.CDLL:
         L.hpmpc_mi355x_ipm_batch.restype = i
         L.hpmpc_mi355x_ipm_batch.argtypes = [vp, vp, i, i, i, vp, vp, vp, vp, vp, vp, vp, vp, i, d, d, d, i, i, vp,
                                              vp, vp, vp]
+        L.hpmpc_mi355x_ipm_pass.restype = i
+        L.hpmpc_mi355x_ipm_pass.argtypes = [vp, vp, i, i, i, vp, vp, vp, vp, vp, vp, vp, vp, i, d, d, d, i, i, vp,
+                                            vp, vp, i, vp]
+        L.hpmpc_mi355x_ipm_batch_profiled.restype = i
+        L.hpmpc_mi355x_ipm_batch_profiled.argtypes = [vp, vp, i, i, i, vp, vp, vp, vp, vp, vp, vp, vp, i, d, d, d, i,
+                                                      i, vp, vp, vp, vp, vp]
         L.hpmpc_mi355x_ric_sv_batch.restype = i
         L.hpmpc_mi355x_ric_sv_batch.argtypes = [vp, vp, i, i, i, vp, vp, vp, vp, vp, i, i, vp, vp]
         L.hpmpc_mi355x_ric_trf_batch.restype = i
@@ -146,6 +152,32 @@ class BatchSolver:
         if rc != 0:
             raise RuntimeError(f"hpmpc_mi355x_ipm_batch failed ({rc})")
 
+    def ipm_pass(self, pss, *, mu0=2.0, mu_tol=1e-12, alpha_min=1e-8, warm_start=0, compute_mult=1, p0=0,
+                 count=None):
+        """One pass of the batched IPM (0 init, 1 factorisation, 2 predictor, 3 corrector, 4 update);
+        ipm() == pass 0 then k_max rounds of passes 1..4."""
+        count = self.nprob - p0 if count is None else count
+        rc = lib().hpmpc_mi355x_ipm_pass(
+            self.plan, C.byref(self.layout), self.nprob, p0, count, self.BAbt.data_ptr(), self.RSQrq.data_ptr(),
+            self.d.data_ptr(), self.ux.data_ptr(), self.pi.data_ptr(), self.lam.data_ptr(), self.t.data_ptr(),
+            self.ws.data_ptr(), self.k_max, mu0, mu_tol, alpha_min, warm_start, compute_mult, self.kk.data_ptr(),
+            self.ret.data_ptr(), self.stat.data_ptr(), pss, self._stream())
+        if rc != 0:
+            raise RuntimeError(f"hpmpc_mi355x_ipm_pass failed ({rc})")
+
+    def ipm_profiled(self, *, mu0=2.0, mu_tol=1e-12, alpha_min=1e-8, warm_start=0, compute_mult=1):
+        """ipm() with hipEvents around every pass kernel (synchronous).  Returns the summed device time
+        (ms) of passes [init, factorisation, predictor, corrector, update]."""
+        out = np.zeros(5)
+        rc = lib().hpmpc_mi355x_ipm_batch_profiled(
+            self.plan, C.byref(self.layout), self.nprob, 0, self.nprob, self.BAbt.data_ptr(), self.RSQrq.data_ptr(),
+            self.d.data_ptr(), self.ux.data_ptr(), self.pi.data_ptr(), self.lam.data_ptr(), self.t.data_ptr(),
+            self.ws.data_ptr(), self.k_max, mu0, mu_tol, alpha_min, warm_start, compute_mult, self.kk.data_ptr(),
+            self.ret.data_ptr(), self.stat.data_ptr(), out.ctypes.data, self._stream())
+        if rc != 0:
+            raise RuntimeError(f"hpmpc_mi355x_ipm_batch_profiled failed ({rc})")
+        return out
+
     def ric_sv(self, *, compute_pi=1, compute_Pb=0, p0=0, count=None):
         """Batched d_back_ric_rec_sv_tv_res (nb = ng = 0, no update rows): factor into ws."""
         count = self.nprob - p0 if count is None else count
@@ -194,6 +226,20 @@ def algorithmic_bytes_per_ip_iter(qp: OCPQP) -> float:
         trs = L + babt + (nux + nx1) + (nux + nx1)
         res = rsq + babt + (nux + nx1) + (nux + nx1)
         tot += sv + trs + res + 24 * int(qp.nb[k])
+    return 8.0 * tot
+
+
+def algorithmic_bytes_per_fact(qp: OCPQP) -> float:
+    """Algorithmic HBM bytes of one problem through the IPM factorisation pass (hk_ipm_fact, phase 2):
+    BAbt and lower(RSQrq)+row read, update rows r_b / r_q read, box vectors lam, t, r_m, r_d read and
+    t_inv written (10 doubles per box), factor L lower + row + inv_diag and P b written."""
+    tot = 0
+    N = qp.N
+    for k in range(N + 1):
+        nux = qp.nux(k)
+        nx1 = int(qp.nx[k + 1]) if k < N else 0
+        T = nux * (nux + 1) // 2
+        tot += (nux + 1) * nx1 + (T + nux) + nx1 + nux + 10 * int(qp.nb[k]) + (T + 2 * nux) + nx1
     return 8.0 * tot
 
 

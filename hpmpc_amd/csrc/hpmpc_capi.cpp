@@ -240,11 +240,12 @@ bool layout_apply(hpmpc_mi355x_plan* P, const hpmpc_mi355x_layout* lay, KArgs& a
 
 }  // namespace
 
-extern "C" int hpmpc_mi355x_ipm_batch(const hpmpc_mi355x_plan* plan, const hpmpc_mi355x_layout* lay, int nprob,
-                                      int p0, int count, const double* BAbt, const double* RSQrq, const double* d,
-                                      double* ux, double* pi, double* lam, double* t, double* ws, int k_max,
-                                      double mu0, double mu_tol, double alpha_min, int warm_start, int compute_mult,
-                                      int* kk, int* ret, double* stat, void* stream) {
+namespace {
+
+int ipm_launch(const hpmpc_mi355x_plan* plan, const hpmpc_mi355x_layout* lay, int nprob, int p0, int count,
+               const double* BAbt, const double* RSQrq, const double* d, double* ux, double* pi, double* lam,
+               double* t, double* ws, int k_max, double mu0, double mu_tol, double alpha_min, int warm_start,
+               int compute_mult, int* kk, int* ret, double* stat, int which, void* stream) {
     auto* P = const_cast<hpmpc_mi355x_plan*>(plan);
     if (!P) return g_err = HPMPC_MI355X_EUNSUPPORTED;
     KArgs a = base_args(P, nprob, p0);
@@ -266,12 +267,66 @@ extern "C" int hpmpc_mi355x_ipm_batch(const hpmpc_mi355x_plan* plan, const hpmpc
     a.kk = kk;
     a.ret = ret;
     a.stat = stat;
-    int e = hk_launch(K_IPM, &a, count, (hipStream_t)stream);
+    int e = hk_launch(which, &a, count, (hipStream_t)stream);
     if (e) {
         set_err(HPMPC_MI355X_EHIP, "hk_ipm launch failed");
         return HPMPC_MI355X_EHIP;
     }
     return g_err = 0;
+}
+
+}  // namespace
+
+extern "C" int hpmpc_mi355x_ipm_batch(const hpmpc_mi355x_plan* plan, const hpmpc_mi355x_layout* lay, int nprob,
+                                      int p0, int count, const double* BAbt, const double* RSQrq, const double* d,
+                                      double* ux, double* pi, double* lam, double* t, double* ws, int k_max,
+                                      double mu0, double mu_tol, double alpha_min, int warm_start, int compute_mult,
+                                      int* kk, int* ret, double* stat, void* stream) {
+    return ipm_launch(plan, lay, nprob, p0, count, BAbt, RSQrq, d, ux, pi, lam, t, ws, k_max, mu0, mu_tol, alpha_min,
+                      warm_start, compute_mult, kk, ret, stat, K_IPM, stream);
+}
+
+extern "C" int hpmpc_mi355x_ipm_batch_profiled(const hpmpc_mi355x_plan* plan, const hpmpc_mi355x_layout* lay,
+                                               int nprob, int p0, int count, const double* BAbt, const double* RSQrq,
+                                               const double* d, double* ux, double* pi, double* lam, double* t,
+                                               double* ws, int k_max, double mu0, double mu_tol, double alpha_min,
+                                               int warm_start, int compute_mult, int* kk, int* ret, double* stat,
+                                               double* pass_ms, void* stream) {
+    // the same launch sequence as hpmpc_mi355x_ipm_batch, with a hipEvent pair around every pass kernel
+    static thread_local std::vector<hipEvent_t> ev;
+    const int npass = 1 + 4 * (k_max > 0 ? k_max : 0);
+    while ((int)ev.size() < 2 * npass) {
+        hipEvent_t e;
+        if (!hip_ok(hipEventCreate(&e), "event create")) return g_err;
+        ev.push_back(e);
+    }
+    hipStream_t st = (hipStream_t)stream;
+    for (int i = 0; i < npass; i++) {
+        const int which = i == 0 ? 10 : 11 + (i - 1) % 4;
+        if (!hip_ok(hipEventRecord(ev[2 * i], st), "event record")) return g_err;
+        int rc = ipm_launch(plan, lay, nprob, p0, count, BAbt, RSQrq, d, ux, pi, lam, t, ws, k_max, mu0, mu_tol,
+                            alpha_min, warm_start, compute_mult, kk, ret, stat, which, stream);
+        if (rc) return rc;
+        if (!hip_ok(hipEventRecord(ev[2 * i + 1], st), "event record")) return g_err;
+    }
+    if (!hip_ok(hipStreamSynchronize(st), "sync")) return g_err;
+    for (int p = 0; p < 5; p++) pass_ms[p] = 0.0;
+    for (int i = 0; i < npass; i++) {
+        float ms = 0.f;
+        if (!hip_ok(hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]), "event time")) return g_err;
+        pass_ms[i == 0 ? 0 : 1 + (i - 1) % 4] += ms;
+    }
+    return g_err = 0;
+}
+
+extern "C" int hpmpc_mi355x_ipm_pass(const hpmpc_mi355x_plan* plan, const hpmpc_mi355x_layout* lay, int nprob,
+                                     int p0, int count, const double* BAbt, const double* RSQrq, const double* d,
+                                     double* ux, double* pi, double* lam, double* t, double* ws, int k_max,
+                                     double mu0, double mu_tol, double alpha_min, int warm_start, int compute_mult,
+                                     int* kk, int* ret, double* stat, int pass, void* stream) {
+    if (pass < 0 || pass > 4) return g_err = HPMPC_MI355X_EUNSUPPORTED;
+    return ipm_launch(plan, lay, nprob, p0, count, BAbt, RSQrq, d, ux, pi, lam, t, ws, k_max, mu0, mu_tol, alpha_min,
+                      warm_start, compute_mult, kk, ret, stat, 10 + pass, stream);
 }
 
 extern "C" int hpmpc_mi355x_ric_sv_batch(const hpmpc_mi355x_plan* plan, const hpmpc_mi355x_layout* lay, int nprob,

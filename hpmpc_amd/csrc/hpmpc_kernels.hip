@@ -595,6 +595,12 @@ static int launch_t(int which, const KArgs* a, int count, hipStream_t stream) {
             }
             break;
         case 5: hipLaunchKernelGGL(hk_kkt_new_rhs<FX>, grid, block, lds, stream, *a); break;
+        // single IPM pass kernels (hpmpc_mi355x_ipm_pass): the batched solve is 10, then k_max x (11..14)
+        case 10: hipLaunchKernelGGL(hk_ipm_init<FX>, grid, block, lds, stream, *a); break;
+        case 11: hipLaunchKernelGGL(hk_ipm_fact<FX>, grid, block, lds, stream, *a); break;
+        case 12: hipLaunchKernelGGL(hk_ipm_pred<FX>, grid, block, lds, stream, *a); break;
+        case 13: hipLaunchKernelGGL(hk_ipm_corr<FX>, grid, block, lds, stream, *a); break;
+        case 14: hipLaunchKernelGGL(hk_ipm_update<FX>, grid, block, lds, stream, *a); break;
         default: return -1;
     }
     return (int)hipGetLastError();

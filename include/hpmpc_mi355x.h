@@ -105,6 +105,23 @@ int hpmpc_mi355x_ipm_batch(const hpmpc_mi355x_plan *plan, const hpmpc_mi355x_lay
                            double *lam, double *t, double *ws, int k_max, double mu0, double mu_tol, double alpha_min,
                            int warm_start, int compute_mult, int *kk, int *ret, double *stat, void *stream);
 
+/* One pass of the batched IPM, for callers that interleave their own work or timing: the batched
+ * solve above is pass 0 (init) followed by k_max rounds of passes 1 (factorisation), 2 (predictor
+ * solve + step length + mu_aff), 3 (corrector solve + step length), 4 (update + residuals); problems
+ * that have finished return immediately.  Same arguments as hpmpc_mi355x_ipm_batch plus `pass`. */
+int hpmpc_mi355x_ipm_pass(const hpmpc_mi355x_plan *plan, const hpmpc_mi355x_layout *lay, int nprob, int p0,
+                          int count, const double *BAbt, const double *RSQrq, const double *d, double *ux, double *pi,
+                          double *lam, double *t, double *ws, int k_max, double mu0, double mu_tol, double alpha_min,
+                          int warm_start, int compute_mult, int *kk, int *ret, double *stat, int pass, void *stream);
+
+/* hpmpc_mi355x_ipm_batch with a hipEvent pair around every pass kernel; synchronises `stream` and
+ * returns in pass_ms[0..4] the summed device time of passes 0..4 (benchmark / profiling use). */
+int hpmpc_mi355x_ipm_batch_profiled(const hpmpc_mi355x_plan *plan, const hpmpc_mi355x_layout *lay, int nprob,
+                                    int p0, int count, const double *BAbt, const double *RSQrq, const double *d,
+                                    double *ux, double *pi, double *lam, double *t, double *ws, int k_max, double mu0,
+                                    double mu_tol, double alpha_min, int warm_start, int compute_mult, int *kk,
+                                    int *ret, double *stat, double *pass_ms, void *stream);
+
 /* Batched d_back_ric_rec_sv_tv_res (no box / no update rows): factor into ws, ux/pi as above. */
 int hpmpc_mi355x_ric_sv_batch(const hpmpc_mi355x_plan *plan, const hpmpc_mi355x_layout *lay, int nprob, int p0,
                               int count, const double *BAbt, const double *RSQrq, double *ux, double *pi, double *ws,

@@ -7,6 +7,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 from collections import defaultdict
 
@@ -19,7 +20,8 @@ def read_counters(d):
                 k = row.get("Kernel_Name", "")
                 c = row.get("Counter_Name", "")
                 v = float(row.get("Counter_Value", "nan"))
-                vals[k.split("(")[0].strip()][c].append(v)
+                m = re.search(r"(hk_[a-z_]+|calib_copy)", k)
+                vals[m.group(1) if m else k.split("(")[0].strip()][c].append(v)
     return vals
 
 
@@ -34,7 +36,7 @@ def main(fetch_dir, write_dir, out, kk_sum):
            "calib": {"fetch_factor": cf, "write_factor": cw,
                      "raw_fetch": F["calib_copy"]["FETCH_SIZE"], "raw_write": W["calib_copy"]["WRITE_SIZE"]},
            "kernels": {}}
-    for k in ("hk_ipm", "hk_ric_sv"):
+    for k in ("hk_ipm_fact", "hk_ipm_pred", "hk_ipm_corr", "hk_ipm_update", "hk_ric_sv"):
         if k not in F or k not in W:
             continue
         fr = F[k]["FETCH_SIZE"]
@@ -43,10 +45,16 @@ def main(fetch_dir, write_dir, out, kk_sum):
         wb = sum(wr) / len(wr) * cw
         res["kernels"][k] = {"raw_fetch": fr, "raw_write": wr, "fetch_bytes_per_launch": fb,
                              "write_bytes_per_launch": wb, "hbm_bytes_per_launch": fb + wb}
-    if "hk_ipm" in res["kernels"]:
-        res["hbm_bytes_per_launch"] = res["kernels"]["hk_ipm"]["hbm_bytes_per_launch"]
-        res["kk_sum_per_launch"] = kk_sum
-        res["hbm_bytes_per_ip_iter_problem"] = res["hbm_bytes_per_launch"] / kk_sum if kk_sum else None
+    ipm = [k for k in res["kernels"] if k.startswith("hk_ipm_")]
+    if ipm and kk_sum:
+        # pmc_run.py runs two solves: per solve the passes run k_max times each
+        tot = sum(sum(F[k]["FETCH_SIZE"]) * cf + sum(W[k]["WRITE_SIZE"]) * cw for k in ipm) / 2.0
+        res["kk_sum_per_solve"] = kk_sum
+        res["hbm_bytes_per_ip_iter_problem"] = tot / kk_sum
+        fact = res["kernels"].get("hk_ipm_fact")
+        if fact:
+            res["fact_hbm_bytes_per_problem_iter"] = (sum(F["hk_ipm_fact"]["FETCH_SIZE"]) * cf +
+                                                      sum(W["hk_ipm_fact"]["WRITE_SIZE"]) * cw) / 2.0 / kk_sum
     if "hk_ric_sv" in res["kernels"]:
         res["sv_hbm_bytes_per_launch"] = res["kernels"]["hk_ric_sv"]["hbm_bytes_per_launch"]
     with open(out, "w") as fh:
