@@ -170,6 +170,28 @@ __device__ __forceinline__ void chol_pivot(double d, double &s, double &inv) {
     s = ok ? d * y1 : 0.0;
 }
 
+// Pivot inverse only (the diagonal entry itself comes out of the panel formula, see chol_block).
+__device__ __forceinline__ double chol_inv(double d) {
+    const bool ok = d > 1e-15;
+    const double y = __builtin_amdgcn_rsq(d);
+    const double dy = d * y;
+    const double e = fma(-dy, y, 1.0);
+    const double p = fma(0.375, e, 0.5);
+    const double ye = y * e;
+    const double y1 = fma(ye, p, y);
+    return ok ? y1 : 0.0;
+}
+
+// 1/x from v_rcp_f64 plus two Newton steps (<= 1 ulp from the IEEE quotient; the reference's 1.0/t and
+// -lam/dlam are reproduced to the parity tolerance, at 5 VALU ops instead of the 10-op IEEE divide).
+__device__ __forceinline__ double rcp_nr(double x) {
+    double y = __builtin_amdgcn_rcp(x);
+    double e = fma(-x, y, 1.0);
+    y = fma(y, e, y);
+    e = fma(-x, y, 1.0);
+    return fma(y, e, y);
+}
+
 // Raw-buffer global access.  Masked lanes use an out-of-range offset: the hardware range check
 // returns 0 for the load and drops the store, so no exec-masked branch is emitted around the memory
 // op and the vector-memory counter stays exact (hipcc can then wait with a counted vmcnt instead of

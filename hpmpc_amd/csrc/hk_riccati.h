@@ -102,7 +102,7 @@ __device__ __forceinline__ double row2col(Scratch* sm, const double vr[4]) {
 // same operation order, same >1e-15 pivot clamp).  Padded tile indices carry exact zeros, so their
 // pivots clamp to 0 and contribute nothing.
 template <int B, bool AUG>
-__device__ __forceinline__ void chol_block(d4& M, double& ml, double lr[4], double& invd, int kdbg = -1) {
+__device__ __forceinline__ void chol_block(d4& M, double& ml, double& invd, int kdbg = -1) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
     (void)kdbg;
 #define HK_BSTAMP(i) \
@@ -124,36 +124,34 @@ __device__ __forceinline__ void chol_block(d4& M, double& ml, double lr[4], doub
         m2 = row_bcast<4 * B + 2>(ml);
         m3 = row_bcast<4 * B + 3>(ml);
     }
-    double s0, i0, s1, i1, s2, i2, s3, i3;
-    HK_BSTAMP(1);
-    chol_pivot(a00, s0, i0);
+    // The diagonal entry is not formed separately: in lane c = 4B+g the panel formula for y_g is
+    // d_g * i_g with exactly the operations that produce d_g in the uniform chain, i.e. s_g bitwise.
+    const double i0 = chol_inv(a00);
     const double l10 = a10 * i0, l20 = a20 * i0, l30 = a30 * i0;
     const double y0 = x[0] * i0;
     const double p0 = m0 * i0;
     HK_BSTAMP(2);
-    chol_pivot(fma(-l10, l10, a11), s1, i1);
+    const double i1 = chol_inv(fma(-l10, l10, a11));
     const double l21 = fma(-l20, l10, a21) * i1, l31 = fma(-l30, l10, a31) * i1;
     const double y1 = fma(-y0, l10, x[1]) * i1;
     const double p1 = fma(-p0, l10, m1) * i1;
     HK_BSTAMP(3);
-    chol_pivot(fma(-l21, l21, fma(-l20, l20, a22)), s2, i2);
+    const double i2 = chol_inv(fma(-l21, l21, fma(-l20, l20, a22)));
     const double l32 = fma(-l31, l21, fma(-l30, l20, a32)) * i2;
     const double y2 = fma(-y1, l21, fma(-y0, l20, x[2])) * i2;
     const double p2 = fma(-p1, l21, fma(-p0, l20, m2)) * i2;
     HK_BSTAMP(4);
-    chol_pivot(fma(-l32, l32, fma(-l31, l31, fma(-l30, l30, a33))), s3, i3);
+    const double i3 = chol_inv(fma(-l32, l32, fma(-l31, l31, fma(-l30, l30, a33))));
     const double y3 = fma(-y2, l32, fma(-y1, l31, fma(-y0, l30, x[3]))) * i3;
     const double p3 = fma(-p2, l32, fma(-p1, l31, fma(-p0, l30, m3))) * i3;
     HK_BSTAMP(5);
-    // upper storage row 4B+g:  diagonal s_g, then L[c][4B+g] = y_g (c > 4B+g).  Branch-free selects.
+    // upper storage row 4B+g: L[c][4B+g] = y_g for c >= 4B+g (diagonal included).  Branch-free selects.
     const double yg = sel_g(y0, y1, y2, y3);
-    const double sg = sel_g(s0, s1, s2, s3);
-    M[B] = (c == 4 * B + g) ? sg : yg;
+    M[B] = yg;
     const int j = c - 4 * B;
     const bool inb = (c >> 2) == B, below = c > 4 * B + 3;
     invd = inb ? sel_q(i0, i1, i2, i3) : invd;
     if (AUG) {
-        lr[B] = sel_g(p0, p1, p2, p3);
         const double mt = fma(-p3, y3, fma(-p2, y2, fma(-p1, y1, fma(-p0, y0, ml))));
         const double mb = sel_q(p0, p1, p2, p3);
         ml = below ? mt : (inb ? mb : ml);
@@ -172,26 +170,27 @@ __device__ __forceinline__ void chol_block(d4& M, double& ml, double lr[4], doub
 // Out: M = S = lower(L) + strict_upper(L') (symmetric storage: row p of S == column p of L),
 //      ml = aug row l (col layout), lr = l in row layout, invd = inverse diagonal (col layout).
 template <bool AUG>
-__device__ __forceinline__ void stage_chol(d4& M, double& ml, double lr[4], double& invd, int nu, int nx, int xo,
-                                           int kdbg = -1) {
+__device__ __forceinline__ void stage_chol(d4& M, double& ml, double& invd, int nu, int nx, int xo, int kdbg = -1) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
     (void)kdbg;
     invd = 0.0;
-#pragma unroll
-    for (int r = 0; r < 4; r++) lr[r] = 0.0;
     // blocks without an active pivot are skipped (wave-uniform); their rows/columns are zero
-    if (0 < nu || (3 >= xo && 0 < xo + nx)) chol_block<0, AUG>(M, ml, lr, invd, kdbg);
+    if (0 < nu || (3 >= xo && 0 < xo + nx)) chol_block<0, AUG>(M, ml, invd, kdbg);
     HK_STAMP(16, kdbg);
-    if (4 < nu || (7 >= xo && 4 < xo + nx)) chol_block<1, AUG>(M, ml, lr, invd, kdbg);
+    if (4 < nu || (7 >= xo && 4 < xo + nx)) chol_block<1, AUG>(M, ml, invd, kdbg);
     HK_STAMP(18, kdbg);
-    if (8 < nu || (11 >= xo && 8 < xo + nx)) chol_block<2, AUG>(M, ml, lr, invd, kdbg);
+    if (8 < nu || (11 >= xo && 8 < xo + nx)) chol_block<2, AUG>(M, ml, invd, kdbg);
     HK_STAMP(20, kdbg);
-    if (12 < nu || (15 >= xo && 12 < xo + nx)) chol_block<3, AUG>(M, ml, lr, invd, kdbg);
+    if (12 < nu || (15 >= xo && 12 < xo + nx)) chol_block<3, AUG>(M, ml, invd, kdbg);
     HK_STAMP(22, kdbg);
     // lower triangle <- transpose of the upper storage:  T = S' via MFMA with an identity B operand
-    d4 T = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int r = 0; r < 4; r++) T = mfma(M[r], (c == 4 * r + g) ? 1.0 : 0.0, T);
+    // (two accumulator chains: the identity products are exact, so the split does not change T)
+    const d4 z = {0.0, 0.0, 0.0, 0.0};
+    d4 T0 = mfma(M[0], (c == g) ? 1.0 : 0.0, z);
+    d4 T1 = mfma(M[1], (c == 4 + g) ? 1.0 : 0.0, z);
+    T0 = mfma(M[2], (c == 8 + g) ? 1.0 : 0.0, T0);
+    T1 = mfma(M[3], (c == 12 + g) ? 1.0 : 0.0, T1);
+    const d4 T = T0 + T1;
 #pragma unroll
     for (int r = 0; r < 4; r++) M[r] = (g + 4 * r > c) ? T[r] : M[r];
 }
@@ -340,7 +339,8 @@ __device__ __forceinline__ BoxLane box_lane(const signed char* tileslot, int pnb
 
 // sequential step-length rule of d_compute_alpha_* (d_aux_ip_hard_lib4.c:541-565), per lane
 __device__ __forceinline__ void alpha_rule(double& al, double v, double dv) {
-    if (-al * dv > v) al = -v / dv;
+    const double cand = -v * rcp_nr(dv);
+    al = (-al * dv > v) ? cand : al;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -423,7 +423,7 @@ __device__ __forceinline__ void box_hessian(const BoxCtx& bc, const BwdFrag& f, 
         dq = f.bx[0];
         qxv = f.bx[1];
     } else if (BM == BX_P1) {  // d_update_hessian_mpc_hard_tv with sigma*mu = 0 (phase 1)
-        const double til = 1.0 / f.bx[2], tiu = 1.0 / f.bx[3];
+        const double til = rcp_nr(f.bx[2]), tiu = rcp_nr(f.bx[3]);
         const double ltl = f.bx[0] * til, ltu = f.bx[1] * tiu;
         const double dll = til * 0.0, dlu = tiu * 0.0;
         const double q = f.bx[1] - ltu * f.bx[5] + dlu - f.bx[0] - ltl * f.bx[4] - dll;
@@ -435,7 +435,7 @@ __device__ __forceinline__ void box_hessian(const BoxCtx& bc, const BwdFrag& f, 
         dq = b.ok ? ltl + ltu : 0.0;
         qxv = (AUG && b.ok) ? q : 0.0;
     } else if (BM == BX_P2) {  // d_update_hessian_gradient_res_mpc_hard_tv
-        const double til = 1.0 / f.bx[2], tiu = 1.0 / f.bx[3];
+        const double til = rcp_nr(f.bx[2]), tiu = rcp_nr(f.bx[3]);
         const double q = til * (f.bx[4] - f.bx[0] * f.bx[6]) - tiu * (f.bx[5] + f.bx[1] * f.bx[7]);
         gst(bc.t_inv, b.lo, til, st);
         gst(bc.t_inv, b.up, tiu, st);
@@ -461,19 +461,30 @@ __device__ __forceinline__ void bwd_step(const RicIO& io, Scratch* sm, const SH&
     const int nx1 = sh.nx1, xo1 = sh.xo1;
     d4 acc = {0.0, 0.0, 0.0, 0.0};
     if (live) {
-        // W' = Lxx_{k+1}' BAbt_k'  (dtrmm_nt_u, d_back_ric_rec.c:262-264), rows in stage-(k+1) tile coords
+        // W' = Lxx_{k+1}' BAbt_k'  (dtrmm_nt_u, d_back_ric_rec.c:262-264), rows in stage-(k+1) tile coords;
+        // two accumulator chains (even / odd K-chunks) halve the dependent MFMA latency
+        d4 a0 = {0.0, 0.0, 0.0, 0.0}, a1 = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int kc = 0; kc < 4; kc++) {
             if (4 * kc + 3 < xo1 || 4 * kc >= xo1 + nx1) continue;  // uniform
             const double aop = (c >= xo1 && 4 * kc + g >= c) ? S[kc] : 0.0;
-            acc = mfma(aop, cur.bop[kc], acc);
+            if (kc & 1)
+                a1 = mfma(aop, cur.bop[kc], a1);
+            else
+                a0 = mfma(aop, cur.bop[kc], a0);
         }
-        // M += W W'  (dsyrk part of dsyrk_dpotrf_lib, :325)
+        acc = a0 + a1;
+        // M += W W'  (dsyrk part of dsyrk_dpotrf_lib, :325), again on two chains
+        d4 m1 = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int r = 0; r < 4; r++) {
             if (4 * r + 3 < xo1 || 4 * r >= xo1 + nx1) continue;
-            M = mfma(acc[r], acc[r], M);
+            if (r & 1)
+                m1 = mfma(acc[r], acc[r], m1);
+            else
+                M = mfma(acc[r], acc[r], M);
         }
+        M = M + m1;
     }
     if (AUG) {
         // v = Lxx' b (col layout, stage k+1 tile); zero at k = N (no next stage)
@@ -502,14 +513,12 @@ __device__ __forceinline__ void bwd_step(const RicIO& io, Scratch* sm, const SH&
         if (live) ml += xrow_sum(mp);
     }
     HK_STAMP(2, k);
-    double lr[4], invd;
-    stage_chol<AUG>(M, ml, lr, invd, sh.nu, sh.nx, sh.xo, k);
+    double invd;
+    stage_chol<AUG>(M, ml, invd, sh.nu, sh.nx, sh.xo, k);
     HK_STAMP(3, k);
+    if (AUG) col2row(sm, ml, lr_prev);  // l in row layout, for the next stage's w_last
 #pragma unroll
-    for (int r = 0; r < 4; r++) {
-        S[r] = M[r];
-        lr_prev[r] = lr[r];
-    }
+    for (int r = 0; r < 4; r++) S[r] = M[r];
     ml_prev = ml;
     invd_prev = invd;
 }
