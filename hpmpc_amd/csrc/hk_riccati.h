@@ -29,7 +29,7 @@ struct StageInfo {
     int r0, r1;
 };
 
-constexpr int FSTRIDE = 288;  // factor doubles per stage: 4 regs x 64 lanes + l (16) + inv_diag (16)
+constexpr int FSTRIDE = 352;  // factor doubles per stage: 4 regs x 64 lanes + l (16) + inv_diag (16) + KG (64)
 constexpr int V16 = 16;       // per-stage stride of tile/state vectors
 constexpr int V32 = 32;       // per-stage stride of constraint vectors ([lb | pad | ub | pad])
 
@@ -101,8 +101,8 @@ __device__ __forceinline__ double row2col(Scratch* sm, const double vr[4]) {
 // each lane solves its own panel row against it (kernel_dsyrk_dpotrf_nt_4x4 / kernel_dgemm_dtrsm_nt_4x4,
 // same operation order, same >1e-15 pivot clamp).  Padded tile indices carry exact zeros, so their
 // pivots clamp to 0 and contribute nothing.
-template <int B, bool AUG>
-__device__ __forceinline__ void chol_block(d4& M, double& ml, double& invd, int kdbg = -1) {
+template <int B, bool AUG, bool KGEN = false>
+__device__ __forceinline__ void chol_block(d4& M, double& ml, double& invd, double* kg = nullptr, int kdbg = -1) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
     (void)kdbg;
 #define HK_BSTAMP(i) \
@@ -145,6 +145,20 @@ __device__ __forceinline__ void chol_block(d4& M, double& ml, double& invd, int 
     const double y3 = fma(-y2, l32, fma(-y1, l31, fma(-y0, l30, x[3]))) * i3;
     const double p3 = fma(-p2, l32, fma(-p1, l31, fma(-p0, l30, m3))) * i3;
     HK_BSTAMP(5);
+    if (KGEN && B == 0) {
+        // Gain form of the u-block (stages with nu <= 4, u in tile block 0): KG[g][c] = (-L_uu^{-T} y)_g with
+        // y = e_c for the u tiles (c < 4: G = -L_uu^{-T}) and y = L[c][0..3] for the state tiles
+        // (K = -L_uu^{-T} L_xu').  The forward then gets u = G rhs_u + K x as one 4x16 mat-vec
+        // instead of the dtrsv_t back-substitution (same quantity, d_back_ric_rec.c:339-346).
+        const bool ut = c < 4;
+        const double e0 = ut ? (c == 0 ? 1.0 : 0.0) : y0, e1 = ut ? (c == 1 ? 1.0 : 0.0) : y1;
+        const double e2 = ut ? (c == 2 ? 1.0 : 0.0) : y2, e3 = ut ? (c == 3 ? 1.0 : 0.0) : y3;
+        const double z3 = e3 * i3;
+        const double z2 = fma(-l32, z3, e2) * i2;
+        const double z1 = fma(-l31, z3, fma(-l21, z2, e1)) * i1;
+        const double z0 = fma(-l30, z3, fma(-l20, z2, fma(-l10, z1, e0))) * i0;
+        *kg = -sel_g(z0, z1, z2, z3);
+    }
     // upper storage row 4B+g: L[c][4B+g] = y_g for c >= 4B+g (diagonal included).  Branch-free selects.
     const double yg = sel_g(y0, y1, y2, y3);
     M[B] = yg;
@@ -169,19 +183,20 @@ __device__ __forceinline__ void chol_block(d4& M, double& ml, double& invd, int 
 // In : M (tile, full symmetric), ml (aug row, col layout).
 // Out: M = S = lower(L) + strict_upper(L') (symmetric storage: row p of S == column p of L),
 //      ml = aug row l (col layout), lr = l in row layout, invd = inverse diagonal (col layout).
-template <bool AUG>
-__device__ __forceinline__ void stage_chol(d4& M, double& ml, double& invd, int nu, int nx, int xo, int kdbg = -1) {
+template <bool AUG, bool KGEN = false>
+__device__ __forceinline__ void stage_chol(d4& M, double& ml, double& invd, int nu, int nx, int xo, double* kg = nullptr,
+                                           int kdbg = -1) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
     (void)kdbg;
     invd = 0.0;
     // blocks without an active pivot are skipped (wave-uniform); their rows/columns are zero
-    if (0 < nu || (3 >= xo && 0 < xo + nx)) chol_block<0, AUG>(M, ml, invd, kdbg);
+    if (0 < nu || (3 >= xo && 0 < xo + nx)) chol_block<0, AUG, KGEN>(M, ml, invd, kg, kdbg);
     HK_STAMP(16, kdbg);
-    if (4 < nu || (7 >= xo && 4 < xo + nx)) chol_block<1, AUG>(M, ml, invd, kdbg);
+    if (4 < nu || (7 >= xo && 4 < xo + nx)) chol_block<1, AUG>(M, ml, invd, nullptr, kdbg);
     HK_STAMP(18, kdbg);
-    if (8 < nu || (11 >= xo && 8 < xo + nx)) chol_block<2, AUG>(M, ml, invd, kdbg);
+    if (8 < nu || (11 >= xo && 8 < xo + nx)) chol_block<2, AUG>(M, ml, invd, nullptr, kdbg);
     HK_STAMP(20, kdbg);
-    if (12 < nu || (15 >= xo && 12 < xo + nx)) chol_block<3, AUG>(M, ml, invd, kdbg);
+    if (12 < nu || (15 >= xo && 12 < xo + nx)) chol_block<3, AUG>(M, ml, invd, nullptr, kdbg);
     HK_STAMP(22, kdbg);
     // lower triangle <- transpose of the upper storage:  T = S' via MFMA with an identity B operand
     // (two accumulator chains: the identity products are exact, so the split does not change T)
@@ -291,12 +306,14 @@ __device__ __forceinline__ void load_factor(const double* Fk, d4& S, double& lc,
 // factor record of one stage: 4 tile registers in register order (4 x 512 B coalesced), l, inv_diag
 // (ok == false still issues the six stores, out of range, so that every path through a stage loop has
 // the same number of vector-memory ops and the compiler's counted s_waitcnt stays exact)
-__device__ __forceinline__ void store_factor(double* Fk, const d4& S, double lc, double invd, bool ok = true) {
+__device__ __forceinline__ void store_factor(double* Fk, const d4& S, double lc, double invd, double kg,
+                                             bool ok = true) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
 #pragma unroll
     for (int r = 0; r < 4; r++) gst(Fk, r * 64 + l, S[r], ok);
     gst(Fk, 256 + c, lc, ok && g == 0);
     gst(Fk, 272 + c, invd, ok && g == 0);
+    gst(Fk, 288 + l, kg, ok);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -449,7 +466,7 @@ __device__ __forceinline__ void box_hessian(const BoxCtx& bc, const BwdFrag& f, 
 template <bool AUG, int BM, class SH>
 __device__ __forceinline__ void bwd_step(const RicIO& io, Scratch* sm, const SH& sh, int k, const BwdFrag& cur,
                                          const BoxCtx& bc, int compute_Pb, double* Pb, d4& S, double lr_prev[4],
-                                         double& ml_prev, double& invd_prev) {
+                                         double& ml_prev, double& invd_prev, double& kg_prev) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
     const bool live = SH::fixed || k < io.N;
     double dq, qxv;
@@ -513,8 +530,9 @@ __device__ __forceinline__ void bwd_step(const RicIO& io, Scratch* sm, const SH&
         if (live) ml += xrow_sum(mp);
     }
     HK_STAMP(2, k);
-    double invd;
-    stage_chol<AUG>(M, ml, invd, sh.nu, sh.nx, sh.xo, k);
+    double invd, kg = 0.0;
+    stage_chol<AUG, SH::fixed>(M, ml, invd, sh.nu, sh.nx, sh.xo, &kg, k);
+    kg_prev = kg;
     HK_STAMP(3, k);
     if (AUG) col2row(sm, ml, lr_prev);  // l in row layout, for the next stage's w_last
 #pragma unroll
@@ -533,7 +551,7 @@ __device__ void ric_backward(const RicIO& io, Scratch* sm, int update_b, const d
                              const double* qsrc, const BoxCtx& bc, int compute_Pb, double* Pb) {
     d4 S = {0.0, 0.0, 0.0, 0.0};
     double lr_prev[4] = {0.0, 0.0, 0.0, 0.0};
-    double ml_prev = 0.0, invd_prev = 0.0;
+    double ml_prev = 0.0, invd_prev = 0.0, kg_prev = 0.0;
     StageInfo si = load_stage(io.st, io.N);
     BwdFrag cur;
     with_shape<FX>(si, [&](const auto& sh) { bwd_fetch<AUG, BM>(io, sh, io.N, update_b, bsrc, update_q, qsrc, bc, cur); });
@@ -545,17 +563,17 @@ __device__ void ric_backward(const RicIO& io, Scratch* sm, int update_b, const d
         with_shape<FX>(sn, [&](const auto& sh) { bwd_fetch<AUG, BM>(io, sh, kn, update_b, bsrc, update_q, qsrc, bc, nxt); });
         // factor of stage k+1 (still in registers): stored one stage late, behind the prefetch, so
         // that no s_waitcnt of this stage has to wait for the store acknowledgements
-        store_factor(io.F + (long)(k + 1) * FSTRIDE, S, AUG ? ml_prev : 0.0, invd_prev, k < io.N);
+        store_factor(io.F + (long)(k + 1) * FSTRIDE, S, AUG ? ml_prev : 0.0, invd_prev, kg_prev, k < io.N);
         asm volatile("" ::: "memory");  // keep those stores here, ahead of this stage's math
         HK_STAMP(1, k);
         with_shape<FX>(si, [&](const auto& sh) {
-            bwd_step<AUG, BM>(io, sm, sh, k, cur, bc, compute_Pb, Pb, S, lr_prev, ml_prev, invd_prev);
+            bwd_step<AUG, BM>(io, sm, sh, k, cur, bc, compute_Pb, Pb, S, lr_prev, ml_prev, invd_prev, kg_prev);
         });
         HK_STAMP(4, k);
         si = sn;
         cur = nxt;
     }
-    store_factor(io.F, S, AUG ? ml_prev : 0.0, invd_prev);
+    store_factor(io.F, S, AUG ? ml_prev : 0.0, invd_prev, kg_prev);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -640,6 +658,7 @@ __device__ __forceinline__ double pi_from_x(Scratch* sm, const d4& S1, int xo1, 
 struct FwdFrag {
     d4 S;
     double lc, invd;
+    double kg;    // gain form: KG[g][c] (fixed stages)
     d4 bt;        // bt[r] = BAbt_k[var(g+4r)][c - xo1]
     double bval;  // b_k[c - xo1]
     double hc;    // trs: backward vector hux_k[var(c)]
@@ -660,6 +679,7 @@ __device__ __forceinline__ void fwd_fetch(const RicIO& io, const SH& sh, int k, 
     for (int r = 0; r < 4; r++) f.S[r] = gld(Fk, r * 64 + l);
     f.lc = gld(Fk, 256 + c);
     f.invd = gld(Fk, 272 + c);
+    f.kg = gld(Fk, 288 + l);
     const int kk = k < io.N ? k : io.N - 1;  // stage N has no BAbt block: loads clamped, values masked
     const bool live = k < io.N;
     const double* Bk = io.BAbt + sh.oB;
@@ -769,20 +789,31 @@ __device__ __forceinline__ void fwd_step(const RicIO& io, Scratch* sm, const SH&
     const bool all = !SH::fixed && k == 0;
     double xrow[4];
     col2row(sm, xcol, xrow);
-    double part = 0.0;
-    if (!all) {
-#pragma unroll
-        for (int r = 0; r < 4; r++) part += (g + 4 * r >= sh.xo) ? lowS(cur.S, r, g, c) * xrow[r] : 0.0;
-    }
     const double rhs = (MODE == 0) ? cur.lc : cur.hc;
-    const double rc = -rhs - xrow_sum(part);
-    double rrow[4], ur[4];
-    col2row(sm, rc, rrow);
+    double ur[4];
+    if constexpr (SH::fixed) {
+        // gain form (nu <= 4): u_g = sum_c KG[g][c] v[c], v = [rhs_u ; x] -- the reference's
+        // u = -L_uu^{-T} (rhs_u + L_xu' x) as one 4x16 mat-vec (row sums over the 16 columns)
+        const double v = (c < sh.xo) ? rhs : xcol;
+        ur[0] = row_sum16(cur.kg * v);
 #pragma unroll
-    for (int r = 0; r < 4; r++) ur[r] = all ? 0.0 : xrow[r];
-    HK_STAMP(9, k);
-    solve_lt(sh, cur.S, cur.invd, rrow, ur, all);
-    HK_STAMP(10, k);
+        for (int r = 1; r < 4; r++) ur[r] = xrow[r];
+        static_assert(SH::xo <= 4, "gain form needs the u block in tile block 0");
+    } else {
+        double part = 0.0;
+        if (!all) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) part += (g + 4 * r >= sh.xo) ? lowS(cur.S, r, g, c) * xrow[r] : 0.0;
+        }
+        const double rc = -rhs - xrow_sum(part);
+        double rrow[4];
+        col2row(sm, rc, rrow);
+#pragma unroll
+        for (int r = 0; r < 4; r++) ur[r] = all ? 0.0 : xrow[r];
+        HK_STAMP(9, k);
+        solve_lt(sh, cur.S, cur.invd, rrow, ur, all);
+        HK_STAMP(10, k);
+    }
     // ux_k, col layout (tile c): one coalesced store from row group 0, and the box steps
     const double ucol = row2col(sm, ur);
     const int vcs = tile_var(c, sh.nu, sh.nx, sh.xo);

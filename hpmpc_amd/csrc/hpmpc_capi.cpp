@@ -28,7 +28,7 @@ extern "C" int hk_fixcls(int nu, int nx);
 namespace {
 
 enum { K_SV = 0, K_TRF = 1, K_TRS = 2, K_RES = 3, K_IPM = 4, K_KKT = 5 };
-constexpr int FSTRIDE = 288, V16 = 16, V32 = 32, BS = 4, NCL = 2;
+constexpr int FSTRIDE = 352, V16 = 16, V32 = 32, BS = 4, NCL = 2;
 
 struct StageInfoH {  // mirror of hk::StageInfo
     int nu, nx, nb, ng, xo, nx1, nu1, xo1, sdB, sdR, oB, oR, oD, pnb, r0, r1;

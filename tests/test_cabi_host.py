@@ -108,9 +108,9 @@ def test_size_queries_are_host_only(hiplib):
     api = HpmpcAPI(hiplib, "")
     qp = mass_spring_qp(100, 12, 4)
     ws = api.ipm_ws_size(qp)
-    assert ws % 64 == 0 and ws >= 8 * 101 * (288 + 9 * 16 + 8 * 32)
+    assert ws % 64 == 0 and ws >= 8 * 101 * (352 + 9 * 16 + 8 * 32)
     w, m = api.ric_sizes(qp)
-    assert m >= 8 * 101 * 288 and w >= 0
+    assert m >= 8 * 101 * 352 and w >= 0
 
 
 # ---------------------------------------------------------------- lib4 / workload generator
