@@ -49,6 +49,9 @@ def lib() -> C.CDLL:
         L.hpmpc_mi355x_ipm_batch_profiled.restype = i
         L.hpmpc_mi355x_ipm_batch_profiled.argtypes = [vp, vp, i, i, i, vp, vp, vp, vp, vp, vp, vp, vp, i, d, d, d, i,
                                                       i, vp, vp, vp, vp, vp]
+        L.hpmpc_mi355x_ipm_queue.restype = i
+        L.hpmpc_mi355x_ipm_queue.argtypes = [vp, vp, i, i, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, i, d, d, d, i, i,
+                                             vp, vp, vp, vp, vp, vp]
         L.hpmpc_mi355x_ric_sv_batch.restype = i
         L.hpmpc_mi355x_ric_sv_batch.argtypes = [vp, vp, i, i, i, vp, vp, vp, vp, vp, i, i, vp, vp]
         L.hpmpc_mi355x_ric_trf_batch.restype = i
@@ -178,6 +181,10 @@ class BatchSolver:
             raise RuntimeError(f"hpmpc_mi355x_ipm_batch_profiled failed ({rc})")
         return out
 
+    def queue(self, nq: int, n_slots: int | None = None) -> "IpmQueue":
+        """A continuous-batching IPM over this batch's data (entry q solves problem q % nprob)."""
+        return IpmQueue(self, nq, self.nprob if n_slots is None else n_slots)
+
     def ric_sv(self, *, compute_pi=1, compute_Pb=0, p0=0, count=None):
         """Batched d_back_ric_rec_sv_tv_res (nb = ng = 0, no update rows): factor into ws."""
         count = self.nprob - p0 if count is None else count
@@ -266,3 +273,40 @@ def flops_ip_iter(N, nx, nu):
     trs = N * (6 * nx ** 2 + 8 * nx * nu + 2 * nu ** 2) + N * 2 * nx ** 2
     res = N * (2 * (nx + nu) ** 2 + 4 * (nx + nu) * nx)
     return flops_sv(N, nx, nu) + trs + res
+
+
+class IpmQueue:
+    """Problem queue over a BatchSolver's data (hpmpc_mi355x_ipm_queue): ``nq`` entries solved by
+    ``n_slots`` resident slots; a slot whose problem has finished takes the next entry at the next
+    iteration.  Iterates and outputs are per entry, workspaces per slot."""
+
+    def __init__(self, solver: BatchSolver, nq: int, n_slots: int):
+        torch = solver.torch
+        self.s = solver
+        self.nq, self.n_slots = int(nq), int(n_slots)
+        N, f64, dev = solver.N, torch.float64, solver.dev
+        self.ux = torch.zeros((nq, N + 1, 16), dtype=f64, device=dev)
+        self.pi = torch.zeros((nq, N + 1, 16), dtype=f64, device=dev)
+        self.lam = torch.zeros((nq, N + 1, 32), dtype=f64, device=dev)
+        self.t = torch.zeros((nq, N + 1, 32), dtype=f64, device=dev)
+        self.kk = torch.zeros(nq, dtype=torch.int32, device=dev)
+        self.ret = torch.zeros(nq, dtype=torch.int32, device=dev)
+        self.stat = torch.zeros((nq, 5 * solver.k_max), dtype=f64, device=dev)
+        self.ws = torch.zeros((n_slots, solver.wsd), dtype=f64, device=dev)
+        self.qctl = torch.zeros(2 + n_slots, dtype=torch.int32, device=dev)
+
+    def run(self, *, mu0=2.0, mu_tol=1e-12, alpha_min=1e-8, warm_start=0, compute_mult=1, profiled=False):
+        """Solve every entry.  Returns (pass_ms[5] or None, ticks).  Polls the device once per chunk;
+        the caller synchronises before reading results."""
+        s = self.s
+        out = np.zeros(5)
+        ticks = C.c_int(0)
+        rc = lib().hpmpc_mi355x_ipm_queue(
+            s.plan, C.byref(s.layout), s.nprob, self.nq, self.n_slots, s.BAbt.data_ptr(), s.RSQrq.data_ptr(),
+            s.d.data_ptr(), self.ux.data_ptr(), self.pi.data_ptr(), self.lam.data_ptr(), self.t.data_ptr(),
+            self.ws.data_ptr(), self.qctl.data_ptr(), s.k_max, mu0, mu_tol, alpha_min, warm_start, compute_mult,
+            self.kk.data_ptr(), self.ret.data_ptr(), self.stat.data_ptr(), out.ctypes.data if profiled else None,
+            C.byref(ticks), s._stream())
+        if rc != 0:
+            raise RuntimeError(f"hpmpc_mi355x_ipm_queue failed ({rc})")
+        return (out if profiled else None), ticks.value

@@ -144,6 +144,89 @@ __device__ double update_p1_pass(const RicIO& io, const BoxCtx& bc, double alpha
     return wave_sum(ms) * mu_scal;
 }
 
+// Phase-2 update (d_update_var_res_mpc_hard_tv with the backups of d_backup_update_var_res_mpc_hard_tv)
+// and the element-wise residuals of the new iterate, r_d = [lb - x + t_lo | ub - x - t_up], r_m = lam t;
+// returns mu = sum r_m * mu_scal.  With UPD false it only computes r_d, r_m and mu of the current
+// iterate (phase-2 start).  r_q and r_b, the residuals that need the stage matrices, are computed by
+// the next factorisation pass (BX_P2R).  The box variable's x is recomputed from (ux, dux) in the
+// slot lane with the same arithmetic as in its own lane.
+template <int CH, bool UPD>
+__device__ double update_p2_pass(const RicIO& io, const BoxCtx& bc, const signed char* slotvar, double alpha,
+                                 double mu_scal, double* ux, double* pi, const double* dux, const double* dpi,
+                                 double* ux_bkp, double* pi_bkp, double* lam_bkp, double* t_bkp, double* res_d,
+                                 double* res_m) {
+    const int l = lane_id(), g = l >> 4, c = l & 15;
+    const int nq = (io.N + 4) / 4;
+    double ms = 0.0;
+    for (int q0 = 0; q0 < nq; q0 += CH) {
+        double v[CH][16];
+        int i16[CH], iv[CH];
+        bool oku[CH], okp[CH];
+        QuadLane bl[CH];
+#pragma unroll
+        for (int j = 0; j < CH; j++) {
+            const int k = 4 * (q0 + j) + g;
+            const bool kv = k <= io.N;
+            const int kc = kv ? k : io.N;
+            const StageInfo& s = io.st[kc];
+            i16[j] = kc * V16 + c;
+            oku[j] = kv && c < s.nu + s.nx;
+            okp[j] = kv && k < io.N && c < s.nx1;
+            bl[j] = quad_lane(io, q0 + j);
+            const QuadLane& b = bl[j];
+            iv[j] = kc * V16 + (b.ok ? slotvar[kc * 16 + c] : 0);
+            v[j][0] = UPD ? gld(ux, i16[j], oku[j]) : 0.0;
+            v[j][1] = UPD ? gld(dux, i16[j], oku[j]) : 0.0;
+            v[j][2] = UPD ? gld(pi, i16[j], okp[j]) : 0.0;
+            v[j][3] = UPD ? gld(dpi, i16[j], okp[j]) : 0.0;
+            v[j][4] = gld(bc.lam, b.lo, b.ok);
+            v[j][5] = UPD ? gld(bc.dlam, b.lo, b.ok) : 0.0;
+            v[j][6] = gld(bc.t, b.lo, b.ok);
+            v[j][7] = UPD ? gld(bc.dt, b.lo, b.ok) : 0.0;
+            v[j][8] = gld(bc.lam, b.up, b.ok);
+            v[j][9] = UPD ? gld(bc.dlam, b.up, b.ok) : 0.0;
+            v[j][10] = gld(bc.t, b.up, b.ok);
+            v[j][11] = UPD ? gld(bc.dt, b.up, b.ok) : 0.0;
+            v[j][12] = gld(ux, iv[j], b.ok);
+            v[j][13] = UPD ? gld(dux, iv[j], b.ok) : 0.0;
+            v[j][14] = gld(bc.d, b.lo, b.ok);
+            v[j][15] = gld(bc.d, b.up, b.ok);
+        }
+#pragma unroll
+        for (int j = 0; j < CH; j++) {
+            const QuadLane& b = bl[j];
+            if (UPD) {
+                gst(ux_bkp, i16[j], v[j][0], oku[j]);
+                gst(ux, i16[j], v[j][0] + alpha * v[j][1], oku[j]);
+                gst(pi_bkp, i16[j], v[j][2], okp[j]);
+                gst(pi, i16[j], v[j][2] + alpha * v[j][3], okp[j]);
+                gst(lam_bkp, b.lo, v[j][4], b.ok);
+                gst(lam_bkp, b.up, v[j][8], b.ok);
+                gst(t_bkp, b.lo, v[j][6], b.ok);
+                gst(t_bkp, b.up, v[j][10], b.ok);
+            }
+            const double ll = UPD ? v[j][4] + alpha * v[j][5] : v[j][4];
+            const double lu = UPD ? v[j][8] + alpha * v[j][9] : v[j][8];
+            const double tl = UPD ? v[j][6] + alpha * v[j][7] : v[j][6];
+            const double tu = UPD ? v[j][10] + alpha * v[j][11] : v[j][10];
+            const double x = UPD ? v[j][12] + alpha * v[j][13] : v[j][12];
+            if (UPD) {
+                gst(bc.lam, b.lo, ll, b.ok);
+                gst(bc.lam, b.up, lu, b.ok);
+                gst(bc.t, b.lo, tl, b.ok);
+                gst(bc.t, b.up, tu, b.ok);
+            }
+            const double rml = ll * tl, rmu = lu * tu;
+            gst(res_d, b.lo, v[j][14] - x + tl, b.ok);
+            gst(res_d, b.up, v[j][15] - x - tu, b.ok);
+            gst(res_m, b.lo, rml, b.ok);
+            gst(res_m, b.up, rmu, b.ok);
+            ms += b.ok ? rml + rmu : 0.0;
+        }
+    }
+    return wave_sum(ms) * mu_scal;
+}
+
 // ------------------------------------------------------------------------------------------------
 // d_res_res_mpc_hard_tv as a prefetched stage pass.  With UPD it first applies the phase-2 update
 // x += alpha dx to (ux, pi, lam, t) and writes the backups (d_backup_update_var_res_mpc_hard_tv

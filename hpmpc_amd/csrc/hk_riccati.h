@@ -103,7 +103,7 @@ __device__ __forceinline__ double row2col(Scratch* sm, const double vr[4]) {
 // pivots clamp to 0 and contribute nothing.
 template <int B, bool AUG, bool KGEN = false>
 __device__ __forceinline__ void chol_block(d4& M, double& ml, double& invd, double* kg = nullptr, int kdbg = -1) {
-    const int l = lane_id(), g = l >> 4, c = l & 15;
+    const int l = lane_id(), c = l & 15;
     (void)kdbg;
 #define HK_BSTAMP(i) \
     if (B == 1) HK_STAMP(24 + (i), kdbg)
@@ -326,7 +326,9 @@ __device__ __forceinline__ void store_factor(double* Fk, const d4& S, double lc,
 //   backward (trs) : corrector gradient         d_update_gradient_[res_]mpc_hard_tv (+ centering)
 // A lane of tile column c handles the box attached to tile index c (if any); row group 0 stores.
 // ------------------------------------------------------------------------------------------------
-enum BoxMode { BX_NONE = 0, BX_GIVEN = 1, BX_P1 = 2, BX_P2 = 3 };
+// BX_P2R: BX_P2 whose update rows are the residuals r_q, r_b of the current iterate, computed (and
+// stored) inside the backward pass instead of by a separate residual pass (backward only).
+enum BoxMode { BX_NONE = 0, BX_GIVEN = 1, BX_P1 = 2, BX_P2 = 3, BX_P2R = 4 };
 
 struct BoxCtx {
     const double* d;                                   // bounds [lb (pnb) | ub (pnb)], V32 per stage
@@ -336,6 +338,11 @@ struct BoxCtx {
     const double *Qx, *qx;                             // BX_GIVEN terms (V16, slot order)
     double smu;                                        // centering target of the trs box modes
     int pred;                                          // forward BX_P1: predictor step (dlam = 0)
+    // BX_P2R: iterate, residual outputs, and whether the residuals (1) or the data rows (0) are the
+    // right-hand side of the factorisation
+    const double *ux, *pi;
+    double *res_q, *res_b;
+    int res_rhs;
 };
 
 struct BoxLane {
@@ -368,9 +375,12 @@ struct BwdFrag {
     d4 Mi;         // RSQrq tile (mirrored lower part), tile coords of stage k
     double mlq;    // augmented-row source: q (update_q) or the RSQrq last row
     d4 bop;        // MFMA B operand per K-chunk: BAbt_k[var(c)][4kc+g-xo1]
-    d4 brow;       // b_k in row layout over the stage-(k+1) tile rows
+    d4 brow;       // b_k in row layout over the stage-(k+1) tile rows (BX_P2R: b_k, col layout, in [0])
     double bx[8];  // box-mode inputs of tile c
     BoxLane bl;
+    // BX_P2R residual inputs: ux_k (col c / rows g+4r), pi_k (rows), pi_{k-1} (col), BAbt_k' (col
+    // c-xo1 over rows g+4r), x_{k+1} (col)
+    double uc, ur[4], pr[4], pim1, bt[4], x1;
 };
 
 template <bool AUG, int BM, class SH>
@@ -406,7 +416,7 @@ __device__ __forceinline__ void bwd_fetch(const RicIO& io, const SH& sh, int k, 
         f.bx[3] = ldsel(bc.t, b.up, b.ok);
         f.bx[4] = ldsel(bc.d, b.lo, b.ok);
         f.bx[5] = ldsel(bc.d, b.up, b.ok);
-    } else if (BM == BX_P2) {
+    } else if (BM == BX_P2 || BM == BX_P2R) {
         f.bx[0] = ldsel(bc.lam, b.lo, b.ok);
         f.bx[1] = ldsel(bc.lam, b.up, b.ok);
         f.bx[2] = ldsel(bc.t, b.lo, b.ok);
@@ -424,7 +434,25 @@ __device__ __forceinline__ void bwd_fetch(const RicIO& io, const SH& sh, int k, 
         const int s = 4 * r + g - sh.xo1;
         const bool ok = live && s >= 0 && s < sh.nx1;
         f.bop[r] = ldsel(Bk, lib4_idx(sh.sdB, vc, s), ok && vc >= 0);
-        f.brow[r] = AUG ? ldsel(bp, update_b ? s : lib4_idx(sh.sdB, nux, s), ok) : 0.0;
+        if (BM != BX_P2R) f.brow[r] = AUG ? ldsel(bp, update_b ? s : lib4_idx(sh.sdB, nux, s), ok) : 0.0;
+    }
+    if (BM == BX_P2R) {
+        static_assert(BM != BX_P2R || AUG, "residual right-hand sides need the augmented row");
+        const int sc = c - sh.xo1;
+        const bool oks = live && sc >= 0 && sc < sh.nx1;
+        f.uc = ldsel(bc.ux, k * V16 + vc, vc >= 0);
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int vi = tile_var(g + 4 * r, sh.nu, sh.nx, sh.xo);
+            const int sr = 4 * r + g - sh.xo1;
+            const bool okr = live && sr >= 0 && sr < sh.nx1;
+            f.ur[r] = ldsel(bc.ux, k * V16 + vi, vi >= 0);
+            f.pr[r] = ldsel(bc.pi, k * V16 + sr, okr);
+            f.bt[r] = ldsel(Bk, lib4_idx(sh.sdB, vi, sc), oks && vi >= 0);
+        }
+        f.pim1 = ldsel(bc.pi, (k - 1) * V16 + (vc - sh.nu), k > 0 && vc >= sh.nu);
+        f.x1 = ldsel(bc.ux, (k + 1) * V16 + sh.nu1 + sc, oks);
+        f.brow[0] = ldsel(Bk, lib4_idx(sh.sdB, nux, sc), oks);
     }
 }
 
@@ -451,7 +479,7 @@ __device__ __forceinline__ void box_hessian(const BoxCtx& bc, const BwdFrag& f, 
         gst(bc.qxs, b.s16, q, st);
         dq = b.ok ? ltl + ltu : 0.0;
         qxv = (AUG && b.ok) ? q : 0.0;
-    } else if (BM == BX_P2) {  // d_update_hessian_gradient_res_mpc_hard_tv
+    } else if (BM == BX_P2 || BM == BX_P2R) {  // d_update_hessian_gradient_res_mpc_hard_tv
         const double til = rcp_nr(f.bx[2]), tiu = rcp_nr(f.bx[3]);
         const double q = til * (f.bx[4] - f.bx[0] * f.bx[6]) - tiu * (f.bx[5] + f.bx[1] * f.bx[7]);
         gst(bc.t_inv, b.lo, til, st);
@@ -459,6 +487,46 @@ __device__ __forceinline__ void box_hessian(const BoxCtx& bc, const BwdFrag& f, 
         dq = b.ok ? til * f.bx[0] + tiu * f.bx[1] : 0.0;
         qxv = (AUG && b.ok) ? q : 0.0;
     }
+}
+
+// BX_P2R: residuals of the current iterate (d_res_res_mpc_hard_tv, d_res_ip_res_hard.c:39-319) for the
+// prefetched stage k, computed one stage ahead (at the end of stage k+1's step) so that only the
+// right-hand side it produces stays live across the next step:
+//   r_q = q - [0; pi_{k-1}] + (lam_up - lam_lo) + RSQ ux + BAbt pi,   r_b = b - x_{k+1} + BAbt' ux
+// The factorisation's rows become (mlq, brow) = (r_q, r_b) (res_rhs) or the data's own (q, b).
+template <class SH>
+__device__ __forceinline__ void bwd_residual(const RicIO& io, Scratch* sm, const SH& sh, int k, const BoxCtx& bc,
+                                             BwdFrag& f, bool store) {
+    const int l = lane_id(), g = l >> 4, c = l & 15;
+    const bool live = SH::fixed || k < io.N;
+    const int vc = tile_var(c, sh.nu, sh.nx, sh.xo);
+    const int sc = c - sh.xo1;
+    const bool oks = live && sc >= 0 && sc < sh.nx1;
+    double h = f.mlq;
+    if (k > 0 && vc >= sh.nu) h -= f.pim1;
+    if (f.bl.ok) h += -f.bx[0] + f.bx[1];
+    double part = 0.0, p2 = 0.0, p3 = 0.0;
+#pragma unroll
+    for (int r = 0; r < 4; r++) part += f.Mi[r] * f.ur[r];
+    h += xrow_sum(part);
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        p2 += f.bop[r] * f.pr[r];
+        p3 += f.bt[r] * f.ur[r];
+    }
+    const double bpi = xrow_sum(p2);
+    const double atu = xrow_sum(p3);
+    if (live) h += bpi;
+    const double rb = f.brow[0] - f.x1 + atu;
+    gst(bc.res_q, k * V16 + vc, h, store && g == 0 && vc >= 0);
+    gst(bc.res_b, k * V16 + sc, rb, store && g == 0 && oks);
+    f.mlq = bc.res_rhs ? h : f.mlq;
+    double bcol = bc.res_rhs ? rb : f.brow[0];
+    bcol = oks ? bcol : 0.0;
+    double br[4];
+    col2row(sm, bcol, br);
+#pragma unroll
+    for (int r = 0; r < 4; r++) f.brow[r] = br[r];
 }
 
 // One backward stage: M = RSQ + W W' (+ box terms) with W' = Lxx_{k+1}' BAbt_k', then the stage
@@ -471,8 +539,10 @@ __device__ __forceinline__ void bwd_step(const RicIO& io, Scratch* sm, const SH&
     const bool live = SH::fixed || k < io.N;
     double dq, qxv;
     box_hessian<AUG, BM>(bc, cur, dq, qxv);
+    const double mlq = cur.mlq;
+    const d4 brow = cur.brow;
     d4 M = cur.Mi;
-    double ml = cur.mlq + qxv;  // update_q row (or RSQrq row) + drowad qx
+    double ml = mlq + qxv;  // update_q row (or RSQrq row) + drowad qx
 #pragma unroll
     for (int r = 0; r < 4; r++) M[r] += (g + 4 * r == c) ? dq : 0.0;  // ddiaadin: diag = bd + Qx
     const int nx1 = sh.nx1, xo1 = sh.xo1;
@@ -507,7 +577,7 @@ __device__ __forceinline__ void bwd_step(const RicIO& io, Scratch* sm, const SH&
         // v = Lxx' b (col layout, stage k+1 tile); zero at k = N (no next stage)
         double part = 0.0;
 #pragma unroll
-        for (int r = 0; r < 4; r++) part += (c >= xo1 ? lowS(S, r, g, c) : 0.0) * cur.brow[r];
+        for (int r = 0; r < 4; r++) part += (c >= xo1 ? lowS(S, r, g, c) : 0.0) * brow[r];
         const double vcol = xrow_sum(part);
         double vrow[4];
         col2row(sm, vcol, vrow);
@@ -554,7 +624,10 @@ __device__ void ric_backward(const RicIO& io, Scratch* sm, int update_b, const d
     double ml_prev = 0.0, invd_prev = 0.0, kg_prev = 0.0;
     StageInfo si = load_stage(io.st, io.N);
     BwdFrag cur;
-    with_shape<FX>(si, [&](const auto& sh) { bwd_fetch<AUG, BM>(io, sh, io.N, update_b, bsrc, update_q, qsrc, bc, cur); });
+    with_shape<FX>(si, [&](const auto& sh) {
+        bwd_fetch<AUG, BM>(io, sh, io.N, update_b, bsrc, update_q, qsrc, bc, cur);
+        if constexpr (BM == BX_P2R) bwd_residual(io, sm, sh, io.N, bc, cur, true);
+    });
     for (int k = io.N; k >= 0; k--) {
         HK_STAMP(0, k);
         const int kn = k > 0 ? k - 1 : 0;  // unconditional prefetch (stage 0 re-read on the last pass)
@@ -569,6 +642,8 @@ __device__ void ric_backward(const RicIO& io, Scratch* sm, int update_b, const d
         with_shape<FX>(si, [&](const auto& sh) {
             bwd_step<AUG, BM>(io, sm, sh, k, cur, bc, compute_Pb, Pb, S, lr_prev, ml_prev, invd_prev, kg_prev);
         });
+        if constexpr (BM == BX_P2R)
+            with_shape<FX>(sn, [&](const auto& sh) { bwd_residual(io, sm, sh, kn, bc, nxt, k > 0); });
         HK_STAMP(4, k);
         si = sn;
         cur = nxt;

@@ -69,11 +69,13 @@ struct hpmpc_mi355x_plan {
     signed char *d_tileslot = nullptr, *d_slotvar = nullptr;
     std::vector<long long> dev_offB, dev_offR;  // offsets currently uploaded into d_st
     int fixcls = 0;                             // compiled inner-stage class (kernel instance)
+    int nbt = 0;                                // sum of nb
 };
 
 namespace {
 
-bool plan_supported(int N, const int* nx, const int* nu, const int* nb, const int* ng, const char** why) {
+bool plan_supported(int N, const int* nx, const int* nu, const int* nb, const int* const* idxb, const int* ng,
+                    const char** why) {
     for (int k = 0; k <= N; k++) {
         const int u = k < N ? nu[k] : 0;
         if (ng[k] != 0) {
@@ -87,6 +89,17 @@ bool plan_supported(int N, const int* nx, const int* nu, const int* nb, const in
         if (nb[k] < 0 || nb[k] > u + nx[k]) {
             *why = "nb[k] > nu[k]+nx[k]";
             return false;
+        }
+        if (idxb) {  // box indices: in range and distinct (one box per variable)
+            unsigned seen = 0;
+            for (int j = 0; j < nb[k]; j++) {
+                const int v = idxb[k][j];
+                if (v < 0 || v >= u + nx[k] || (seen >> v & 1u)) {
+                    *why = "idxb[k] must hold distinct variable indices in [0, nu[k]+nx[k])";
+                    return false;
+                }
+                seen |= 1u << v;
+            }
         }
     }
     if (N < 1) {
@@ -119,7 +132,7 @@ long long ws_doubles(int N) { return (long long)(N + 1) * (FSTRIDE + 9 * V16 + 8
 extern "C" hpmpc_mi355x_plan* hpmpc_mi355x_plan_create(int N, const int* nx, const int* nu, const int* nb,
                                                        const int* const* idxb, const int* ng) {
     const char* why = nullptr;
-    if (!plan_supported(N, nx, nu, nb, ng, &why)) {
+    if (!plan_supported(N, nx, nu, nb, idxb, ng, &why)) {
         set_err(HPMPC_MI355X_EUNSUPPORTED, why);
         return nullptr;
     }
@@ -159,6 +172,7 @@ extern "C" hpmpc_mi355x_plan* hpmpc_mi355x_plan_create(int N, const int* nx, con
         P->offR[k] = P->packR;
         P->packR += (long long)rup(nux + 1, BS) * s.sdR;
         P->idxb[k].assign(idxb[k], idxb[k] + nb[k]);
+        P->nbt += nb[k];
         for (int l = 0; l < nb[k]; l++) {
             const int v = idxb[k][l];
             const int t = v < s.nu ? v : s.xo + (v - s.nu);
@@ -223,6 +237,7 @@ KArgs base_args(const hpmpc_mi355x_plan* P, int nprob, int p0) {
     a.sV32 = (long long)(P->N + 1) * V32;
     a.sW = ws_doubles(P->N);
     a.fixcls = P->fixcls;
+    a.nbt = P->nbt;
     a.dbg = g_dbg_buf;
     return a;
 }
@@ -327,6 +342,117 @@ extern "C" int hpmpc_mi355x_ipm_pass(const hpmpc_mi355x_plan* plan, const hpmpc_
     if (pass < 0 || pass > 4) return g_err = HPMPC_MI355X_EUNSUPPORTED;
     return ipm_launch(plan, lay, nprob, p0, count, BAbt, RSQrq, d, ux, pi, lam, t, ws, k_max, mu0, mu_tol, alpha_min,
                       warm_start, compute_mult, kk, ret, stat, 10 + pass, stream);
+}
+
+// Problem queue: n_slots workgroups each solve queue entries back to back, so a slot whose problem has
+// converged starts the next entry at the following iteration instead of idling until the slowest
+// problem of a batch finishes.  The host enqueues ticks (fact, pred, corr, update) in chunks and stops
+// once the device-side finished counter reaches nq, checking a chunk behind so the stream never drains.
+extern "C" int hpmpc_mi355x_ipm_queue(const hpmpc_mi355x_plan* plan, const hpmpc_mi355x_layout* lay, int nprob,
+                                      int nq, int n_slots, const double* BAbt, const double* RSQrq, const double* d,
+                                      double* ux, double* pi, double* lam, double* t, double* ws, int* qctl,
+                                      int k_max, double mu0, double mu_tol, double alpha_min, int warm_start,
+                                      int compute_mult, int* kk, int* ret, double* stat, double* pass_ms,
+                                      int* n_ticks, void* stream) {
+    auto* P = const_cast<hpmpc_mi355x_plan*>(plan);
+    if (!P || nprob <= 0 || nq < 0 || n_slots <= 0 || !qctl) return g_err = HPMPC_MI355X_EUNSUPPORTED;
+    if (n_ticks) *n_ticks = 0;
+    if (pass_ms)
+        for (int i = 0; i < 5; i++) pass_ms[i] = 0.0;
+    if (nq == 0) return g_err = 0;
+    KArgs a = base_args(P, nprob, 0);
+    if (!layout_apply(P, lay, a)) return g_err;
+    a.BAbt = BAbt;
+    a.RSQ = RSQrq;
+    a.d = d;
+    a.ux = ux;
+    a.pi = pi;
+    a.lam = lam;
+    a.t = t;
+    a.ws = ws;
+    a.k_max = k_max;
+    a.mu0 = mu0;
+    a.mu_tol = mu_tol;
+    a.alpha_min = alpha_min;
+    a.warm_start = warm_start;
+    a.compute_mult = compute_mult;
+    a.kk = kk;
+    a.ret = ret;
+    a.stat = stat;
+    a.nq = nq;
+    a.qctl = qctl;
+    hipStream_t st = (hipStream_t)stream;
+    constexpr int R = 8;  // ticks per chunk
+    static thread_local int* hdone = nullptr;
+    static thread_local std::vector<hipEvent_t> ev;  // 2 chunk parities x (R*4 + 1) kernel boundaries
+    const int nev = R * 4 + 1;
+    if (!hdone && !hip_ok(hipHostMalloc((void**)&hdone, 2 * sizeof(int), hipHostMallocDefault), "host alloc"))
+        return g_err;
+    while ((int)ev.size() < 2 * nev + 2) {
+        hipEvent_t e;
+        if (!hip_ok(hipEventCreate(&e), "event create")) return g_err;
+        ev.push_back(e);
+    }
+    hipEvent_t* done_ev = &ev[2 * nev];
+    auto launch = [&](int which) {
+        if (hk_launch(which, &a, n_slots, st)) {
+            set_err(HPMPC_MI355X_EHIP, "hk_ipm_queue launch failed");
+            return false;
+        }
+        return true;
+    };
+    auto harvest = [&](int par) {  // chunk parity par has completed: accumulate its kernel times
+        hipEvent_t* e = &ev[par * nev];
+        for (int i = 0; i < R * 4; i++) {
+            float ms = 0.f;
+            if (!hip_ok(hipEventElapsedTime(&ms, e[i], e[i + 1]), "event time")) return false;
+            pass_ms[1 + i % 4] += ms;
+        }
+        return true;
+    };
+    if (!hip_ok(hipMemsetAsync(qctl, 0, 2 * sizeof(int), st), "memset")) return g_err;
+    if (pass_ms && !hip_ok(hipEventRecord(ev[0], st), "event record")) return g_err;
+    if (!launch(10)) return g_err;
+    if (pass_ms) {
+        if (!hip_ok(hipEventRecord(ev[1], st), "event record") || !hip_ok(hipStreamSynchronize(st), "sync"))
+            return g_err;
+        float ms = 0.f;
+        if (!hip_ok(hipEventElapsedTime(&ms, ev[0], ev[1]), "event time")) return g_err;
+        pass_ms[0] = ms;
+    }
+    // every entry retires within k_max ticks of being handed out, and a slot is handed a new entry at
+    // least every k_max ticks, so this bound is never reached by a correct run
+    const long cap = (long)k_max * ((nq + n_slots - 1) / n_slots + 1) + R;
+    long ticks = 0;
+    bool pending = false;
+    for (int c = 0;; c++) {
+        const int par = c & 1;
+        hipEvent_t* e = &ev[par * nev];
+        if (pass_ms && !hip_ok(hipEventRecord(e[0], st), "event record")) return g_err;
+        for (int i = 0; i < R; i++) {
+            for (int k = 0; k < 4; k++) {
+                if (!launch(11 + k)) return g_err;
+                if (pass_ms && !hip_ok(hipEventRecord(e[4 * i + k + 1], st), "event record")) return g_err;
+            }
+        }
+        ticks += R;
+        if (!hip_ok(hipMemcpyAsync(&hdone[par], qctl + 1, sizeof(int), hipMemcpyDeviceToHost, st), "copy") ||
+            !hip_ok(hipEventRecord(done_ev[par], st), "event record"))
+            return g_err;
+        if (pending) {  // look at the previous chunk while this one runs
+            if (!hip_ok(hipEventSynchronize(done_ev[par ^ 1]), "event sync")) return g_err;
+            if (pass_ms && !harvest(par ^ 1)) return g_err;
+            if (hdone[par ^ 1] >= nq) break;
+        }
+        pending = true;
+        if (ticks >= cap) {
+            set_err(HPMPC_MI355X_EHIP, "hk_ipm_queue did not drain");
+            return HPMPC_MI355X_EHIP;
+        }
+    }
+    // the chunk enqueued last finds every slot idle; it is left to complete on the stream, untimed
+    if (n_ticks) *n_ticks = (int)ticks;
+    return g_err = 0;
 }
 
 extern "C" int hpmpc_mi355x_ric_sv_batch(const hpmpc_mi355x_plan* plan, const hpmpc_mi355x_layout* lay, int nprob,

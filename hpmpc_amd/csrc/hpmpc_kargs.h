@@ -5,6 +5,7 @@
 
 struct KArgs {
     int N, nprob, p0;             // horizon, problems in the batch, first problem of this launch
+    int nbt;                      // sum of nb over the stages
     int fixcls;                   // compiled inner-stage class of the plan (0: generic kernels)
     const void* st;               // hk::StageInfo[N+1]
     const signed char* tileslot;  // (N+1)*16
@@ -29,5 +30,9 @@ struct KArgs {
     int *kk, *ret;
     double* stat;    // 5*k_max per problem
     double* mu_out;  // per problem (residual kernel)
+    // problem queue (hpmpc_mi355x_ipm_queue): nq > 0 makes the grid a set of slots; slot s solves queue
+    // entries one after another (entry q: data problem q % nprob, iterate/outputs at q, workspace s)
+    int nq;
+    int* qctl;  // [0] next entry to hand out, [1] entries finished, [2 + s] entry held by slot s (-1 none)
     unsigned long long* dbg;  // diagnostic stamp buffer (HK_STAMPS builds only)
 };

@@ -10,6 +10,10 @@
 
 using namespace hk;
 
+// IPM pass kernels fit two waves per SIMD (<= 256 VGPRs), so a problem queue with two slots per SIMD
+// interleaves two problems' dependency chains.
+#define HK_TWO_WAVES __attribute__((amdgpu_waves_per_eu(2)))
+
 namespace {
 
 struct Ws {  // per-problem workspace carve (doubles), persistent between an IPM and a KKT re-solve
@@ -195,39 +199,64 @@ __global__ __launch_bounds__(64) void hk_res(KArgs a) {
 // ------------------------------------------------------------------------------------------------
 namespace {
 
-__device__ void init_var(const RicIO& io, const BoxTab& bt, const double* dv, double* ux, double* pi, double* lam,
+// d_init_var_mpc_hard_tv (d_aux_ip_hard_lib4.c:59-130) as a quad pass: lane (g, c) owns variable c of
+// stage 4q+g and, when c is boxed, its box slot; CH quads are loaded before any is computed, so a
+// refill costs a few memory round trips instead of one per stage.  Also zeroes pi and dpi.
+template <int CH>
+__device__ void init_var(const RicIO& io, const double* dv, double* ux, double* pi, double* dpi, double* lam,
                          double* t, double mu0, int warm_start) {
-    const int l = lane_id();
+    const int l = lane_id(), g = l >> 4, c = l & 15;
     const double thr0 = 0.1;
-    if (!warm_start)
-        for (int i = l; i < (io.N + 1) * V16; i += 64) ux[i] = 0.0;
-    for (int i = l; i < io.N * V16; i += 64) pi[i] = 0.0;
-    wsync();
-    HK_FOR_BOX(io, k, {
-        const int v = bt.slotvar[k * 16 + slot];
-        double x = ux[k * V16 + v];
-        const double dl = dv[lo], du = dv[up];
-        double tl = -dl + x, tu = du - x;
-        if (tl < thr0) {
-            if (tu < thr0) {
-                x = (-du + dl) * 0.5;
-                tl = thr0;
-                tu = thr0;
-            } else {
-                tl = thr0;
-                x = dl + thr0;
-            }
-        } else if (tu < thr0) {
-            tu = thr0;
-            x = du - thr0;
+    const int nq = (io.N + 4) / 4;
+    for (int q0 = 0; q0 < nq; q0 += CH) {
+        double dl[CH], du[CH], xv[CH];
+        int lo[CH], up[CH], iv[CH];
+        bool kv[CH], bx[CH], kp[CH];
+#pragma unroll
+        for (int j = 0; j < CH; j++) {
+            const int k = 4 * (q0 + j) + g;
+            kv[j] = k <= io.N;
+            kp[j] = k < io.N;
+            const int kc = kv[j] ? k : io.N;
+            const StageInfo& si = io.st[kc];
+            const bool okv = c < si.nu + si.nx;
+            const int tile = c < si.nu ? c : si.xo + (c - si.nu);
+            const int slot = okv ? io.tileslot[kc * 16 + (okv ? tile : 0)] : -1;
+            bx[j] = kv[j] && slot >= 0;
+            lo[j] = kc * V32 + (slot >= 0 ? slot : 0);
+            up[j] = lo[j] + si.pnb;
+            iv[j] = kc * V16 + c;
+            dl[j] = gld(dv, lo[j], bx[j]);
+            du[j] = gld(dv, up[j], bx[j]);
+            xv[j] = warm_start ? gld(ux, iv[j], kv[j]) : 0.0;
         }
-        ux[k * V16 + v] = x;
-        t[lo] = tl;
-        t[up] = tu;
-        lam[lo] = mu0 / tl;
-        lam[up] = mu0 / tu;
-    });
-    wsync();
+#pragma unroll
+        for (int j = 0; j < CH; j++) {
+            double x = xv[j];
+            double tl = -dl[j] + x, tu = du[j] - x;
+            if (tl < thr0) {
+                if (tu < thr0) {
+                    x = (-du[j] + dl[j]) * 0.5;
+                    tl = thr0;
+                    tu = thr0;
+                } else {
+                    tl = thr0;
+                    x = dl[j] + thr0;
+                }
+            } else if (tu < thr0) {
+                tu = thr0;
+                x = du[j] - thr0;
+            }
+            x = bx[j] ? x : xv[j];
+            gst(ux, iv[j], x, kv[j]);
+            gst(pi, iv[j], 0.0, kp[j]);
+            gst(dpi, iv[j], 0.0, kv[j]);
+            gst(t, lo[j], tl, bx[j]);
+            gst(t, up[j], tu, bx[j]);
+            gst(lam, lo[j], mu0 / tl, bx[j]);
+            gst(lam, up[j], mu0 / tu, bx[j]);
+        }
+    }
 }
 
 __device__ __forceinline__ BoxCtx box_ctx(const Ws& w, const double* dv, double* lam, double* t) {
@@ -244,6 +273,8 @@ __device__ __forceinline__ BoxCtx box_ctx(const Ws& w, const double* dv, double*
     bc.qxs = w.qx;
     bc.Qx = w.Qx;
     bc.qx = w.qx;
+    bc.res_q = w.res_q;
+    bc.res_b = w.res_b;
     return bc;
 }
 
@@ -256,7 +287,7 @@ __device__ __forceinline__ BoxCtx box_ctx(const Ws& w, const double* dv, double*
 namespace {
 
 struct IpmView {
-    int N, p, l;
+    int N, q, l;  // q: iterate / output index (the problem in batch mode, the queue entry in queue mode)
     Ws w;
     RicIO io;
     BoxTab bt;
@@ -265,22 +296,41 @@ struct IpmView {
     BoxCtx bc;
 };
 
-__device__ __forceinline__ IpmView ipm_view(const KArgs& a, const LdsTabs& T, int p) {
+// Which workspace (s), iterate/output (q) and data problem (d) this workgroup works on.
+struct Who {
+    int s, q, d;
+};
+
+__device__ __forceinline__ bool who_am_i(const KArgs& a, Who& w) {
+    if (a.nq == 0) {
+        const int p = blockIdx.x + a.p0;
+        w.s = w.q = w.d = p;
+        return p < a.nprob;
+    }
+    w.s = blockIdx.x;
+    w.q = __builtin_amdgcn_readfirstlane(a.qctl[2 + w.s]);
+    w.d = w.q >= 0 ? w.q % a.nprob : 0;
+    return w.q >= 0;
+}
+
+__device__ __forceinline__ IpmView ipm_view(const KArgs& a, const LdsTabs& T, const Who& who) {
     IpmView v;
     v.N = a.N;
-    v.p = p;
+    v.q = who.q;
     v.l = lane_id();
-    v.w = carve(a.ws + (long)p * a.sW, a.N);
-    v.io = make_io(a, T, p, v.w.F);
+    v.w = carve(a.ws + (long)who.s * a.sW, a.N);
+    v.io = make_io(a, T, who.d, v.w.F);
     v.bt = BoxTab{T.tileslot, T.slotvar};
-    const long o16 = (long)p * a.sV16, o32 = (long)p * a.sV32;
+    const long o16 = (long)who.q * a.sV16, o32 = (long)who.q * a.sV32;
     v.ux = a.ux + o16;
     v.pi = a.pi + o16;
     v.lam = a.lam + o32;
     v.t = a.t + o32;
-    v.dv = a.d + o32;
-    v.stat = a.stat + (long)p * 5 * a.k_max;
+    v.dv = a.d + (long)who.d * a.sV32;
+    v.stat = a.stat + (long)who.q * 5 * a.k_max;
     v.bc = box_ctx(v.w, v.dv, v.lam, v.t);
+    v.bc.ux = v.ux;
+    v.bc.pi = v.pi;
     return v;
 }
 
@@ -301,16 +351,25 @@ __device__ __forceinline__ ResIO res_io(const IpmView& v) {
     return ro;
 }
 
+// Phase-2 start residuals: r_d, r_m and mu here; r_q, r_b in the first phase-2 factorisation.
+template <class FX>
+__device__ double p2_start(const KArgs& a, IpmView& v) {
+    const double mu = update_p2_pass<7, false>(v.io, v.bc, v.bt.slotvar, 0.0, 1.0 / (2.0 * a.nbt), v.ux, v.pi,
+                                               nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, v.w.res_d,
+                                               v.w.res_m);
+    wsync();
+    return mu;
+}
+
 // End of an iteration (or of init): decide whether the problem continues, switching from phase 1 to
 // phase 2 (with the phase-2 start residuals) when phase 1's loop condition fails.
 template <class FX>
-__device__ void ipm_continue(const KArgs& a, IpmView& v, int kk, double mu, double alpha, double sigma, int phase) {
+__device__ bool ipm_continue(const KArgs& a, IpmView& v, int kk, double mu, double alpha, double sigma, int phase) {
     const bool sn = a.single_newton != 0;
     if (phase == 1) {
         const double mu_tol_low = a.mu_tol < 1e-5 ? 1e-5 : a.mu_tol;
         if (!(kk < a.k_max && mu > mu_tol_low && alpha >= a.alpha_min)) {
-            residual_pass<false, FX>(v.io, v.bc, res_io(v), mu);  // phase-2 start (d_ip2_res_hard.c:756-781)
-            wsync();
+            mu = p2_start<FX>(a, v);  // phase-2 start (d_ip2_res_hard.c:756-781)
             phase = 2;
         }
     }
@@ -336,24 +395,19 @@ __device__ void ipm_continue(const KArgs& a, IpmView& v, int kk, double mu, doub
         st[S_PHASE] = phase;
         st[S_ACTIVE] = active ? 1.0 : 0.0;
         if (!active) {
-            a.kk[v.p] = kk;
-            a.ret[v.p] = ret;
+            a.kk[v.q] = kk;
+            a.ret[v.q] = ret;
         }
     }
+    return active;
 }
 
-}  // namespace
-
+// Start of a solve: init_var and the loop-control state.  Returns whether the problem iterates.
 template <class FX>
-__global__ __launch_bounds__(64) void hk_ipm_init(KArgs a) {
-    const LdsTabs T = lds_tables(a);
+__device__ bool ipm_start(const KArgs& a, const LdsTabs& T, IpmView& v) {
     Scratch& sm = *T.sm;
-    const int p = blockIdx.x + a.p0;
-    if (p >= a.nprob) return;
-    IpmView v = ipm_view(a, T, p);
     const int N = v.N, l = v.l;
-    int nbt = 0;
-    for (int k = 0; k <= N; k++) nbt += v.io.st[k].nb;
+    const int nbt = a.nbt;
     if (nbt == 0) {
         // no constraints: one sv and return (d_ip2_res_hard.c:428-450)
         ric_backward<true, BX_NONE, FX>(v.io, &sm, 0, nullptr, 0, nullptr, v.bc, 1, v.w.Pb);
@@ -366,51 +420,88 @@ __global__ __launch_bounds__(64) void hk_ipm_init(KArgs a) {
         }
         if (l == 0) {
             v.w.state[S_ACTIVE] = 0.0;
-            a.kk[p] = 0;
-            a.ret[p] = 0;
+            a.kk[v.q] = 0;
+            a.ret[v.q] = 0;
         }
-        return;
+        return false;
     }
     // single Newton step (d_ip2_res_hard.c:1348-1919): the caller's ux/pi/lam/t already hold the start
     // iterate (d_init_var_mpc_hard_tv_single_newton is a copy, done by the host), no phase 1.
     const bool sn = a.single_newton != 0;
-    if (!sn) init_var(v.io, v.bt, v.dv, v.ux, v.pi, v.lam, v.t, a.mu0, a.warm_start);
-    for (int i = l; i < (N + 1) * V16; i += 64) v.w.dpi[i] = 0.0;
+    if (!sn) {
+        init_var<7>(v.io, v.dv, v.ux, v.pi, v.w.dpi, v.lam, v.t, a.mu0, a.warm_start);
+    } else {
+        for (int i = l; i < (N + 1) * V16; i += 64) v.w.dpi[i] = 0.0;
+    }
     if (l == 0) v.w.state[S_MUSCAL] = 1.0 / (2.0 * nbt);
     wsync();
     double mu = a.mu0;
-    if (sn) {  // straight to phase 2: its start residuals
-        residual_pass<false, FX>(v.io, v.bc, res_io(v), mu);
-        wsync();
+    if (sn) mu = p2_start<FX>(a, v);  // straight to phase 2: its start residuals
+    return ipm_continue<FX>(a, v, 0, mu, 1.0, 0.0, sn ? 2 : 1);
+}
+
+// Queue mode: hand slot s the next queue entries until one of them iterates (or the queue is empty).
+template <class FX>
+__device__ void ipm_refill(const KArgs& a, const LdsTabs& T, int s) {
+    const bool l0 = lane_id() == 0;
+    for (;;) {
+        int q = 0;
+        if (l0) q = atomicAdd(&a.qctl[0], 1);
+        q = __builtin_amdgcn_readfirstlane(q);
+        if (q >= a.nq) {
+            if (l0) a.qctl[2 + s] = -1;
+            return;
+        }
+        if (l0) a.qctl[2 + s] = q;
+        const Who who{s, q, q % a.nprob};
+        IpmView v = ipm_view(a, T, who);
+        if (ipm_start<FX>(a, T, v)) return;
+        if (l0) atomicAdd(&a.qctl[1], 1);
     }
-    ipm_continue<FX>(a, v, 0, mu, 1.0, 0.0, sn ? 2 : 1);
+}
+
+}  // namespace
+
+template <class FX>
+__global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_init(KArgs a) {
+    const LdsTabs T = lds_tables(a);
+    if (a.nq) {
+        ipm_refill<FX>(a, T, blockIdx.x);
+        return;
+    }
+    Who who;
+    if (!who_am_i(a, who)) return;
+    IpmView v = ipm_view(a, T, who);
+    ipm_start<FX>(a, T, v);
 }
 
 // Factorisation of the iteration's KKT system, Hessian / gradient box terms fused into the fetch.
 template <class FX>
-__global__ __launch_bounds__(64) void hk_ipm_fact(KArgs a) {
+__global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_fact(KArgs a) {
     const LdsTabs T = lds_tables(a);
     Scratch& sm = *T.sm;
-    const int p = blockIdx.x + a.p0;
-    if (p >= a.nprob) return;
-    IpmView v = ipm_view(a, T, p);
+    Who who;
+    if (!who_am_i(a, who)) return;
+    IpmView v = ipm_view(a, T, who);
     const double* st = v.w.state;
     if (st[S_ACTIVE] == 0.0) return;
     const bool sn = a.single_newton != 0;
     if (st[S_PHASE] == 1.0)
         ric_backward<true, BX_P1, FX>(v.io, &sm, 0, nullptr, 0, nullptr, v.bc, 1, v.w.Pb);
-    else  // the single-Newton variant factorises with the data's own b/q rows (d_ip2_res_hard.c:1700-1760)
-        ric_backward<true, BX_P2, FX>(v.io, &sm, !sn, v.w.res_b, !sn, v.w.res_q, v.bc, 1, v.w.Pb);
+    else {  // the single-Newton variant factorises with the data's own b/q rows (d_ip2_res_hard.c:1700-1760)
+        v.bc.res_rhs = !sn;
+        ric_backward<true, BX_P2R, FX>(v.io, &sm, 0, nullptr, 0, nullptr, v.bc, 1, v.w.Pb);
+    }
 }
 
 // Predictor solve with the box steps and step length fused in, then mu_aff and the centering target.
 template <class FX>
-__global__ __launch_bounds__(64) void hk_ipm_pred(KArgs a) {
+__global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_pred(KArgs a) {
     const LdsTabs T = lds_tables(a);
     Scratch& sm = *T.sm;
-    const int p = blockIdx.x + a.p0;
-    if (p >= a.nprob) return;
-    IpmView v = ipm_view(a, T, p);
+    Who who;
+    if (!who_am_i(a, who)) return;
+    IpmView v = ipm_view(a, T, who);
     double* st = v.w.state;
     if (st[S_ACTIVE] == 0.0) return;
     const bool sn = a.single_newton != 0;
@@ -445,12 +536,12 @@ __global__ __launch_bounds__(64) void hk_ipm_pred(KArgs a) {
 
 // Corrector: centering / gradient update fused into the trs backward, box steps + alpha into its forward.
 template <class FX>
-__global__ __launch_bounds__(64) void hk_ipm_corr(KArgs a) {
+__global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_corr(KArgs a) {
     const LdsTabs T = lds_tables(a);
     Scratch& sm = *T.sm;
-    const int p = blockIdx.x + a.p0;
-    if (p >= a.nprob) return;
-    IpmView v = ipm_view(a, T, p);
+    Who who;
+    if (!who_am_i(a, who)) return;
+    IpmView v = ipm_view(a, T, who);
     double* st = v.w.state;
     if (st[S_ACTIVE] == 0.0) return;
     const int phase = (int)st[S_PHASE], kk = (int)st[S_KK];
@@ -471,11 +562,11 @@ __global__ __launch_bounds__(64) void hk_ipm_corr(KArgs a) {
 
 // Update of the iterate (with backups) and, in phase 2, the residuals of the new iterate; loop control.
 template <class FX>
-__global__ __launch_bounds__(64) void hk_ipm_update(KArgs a) {
+__global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_update(KArgs a) {
     const LdsTabs T = lds_tables(a);
-    const int p = blockIdx.x + a.p0;
-    if (p >= a.nprob) return;
-    IpmView v = ipm_view(a, T, p);
+    Who who;
+    if (!who_am_i(a, who)) return;
+    IpmView v = ipm_view(a, T, who);
     double* st = v.w.state;
     if (st[S_ACTIVE] == 0.0) return;
     const int phase = (int)st[S_PHASE];
@@ -486,15 +577,16 @@ __global__ __launch_bounds__(64) void hk_ipm_update(KArgs a) {
         mu = update_p1_pass<4>(v.io, v.bc, alpha, st[S_MUSCAL], v.ux, v.pi, v.w.dux, v.w.dpi, v.w.ux_bkp,
                                v.w.pi_bkp, v.w.lam_bkp, v.w.t_bkp);
     } else {
-        ResIO ro = res_io(v);
-        ro.alpha = alpha;
-        mu = st[S_MU];
-        residual_pass<true, FX>(v.io, v.bc, ro, mu);
+        mu = update_p2_pass<4, true>(v.io, v.bc, v.bt.slotvar, alpha, st[S_MUSCAL], v.ux, v.pi, v.w.dux, v.w.dpi,
+                                     v.w.ux_bkp, v.w.pi_bkp, v.w.lam_bkp, v.w.t_bkp, v.w.res_d, v.w.res_m);
     }
     wsync();
     if (v.l == 0) v.stat[5 * kk + 4] = mu;
     kk++;
-    ipm_continue<FX>(a, v, kk, mu, alpha, st[S_SIGMA], phase);
+    if (!ipm_continue<FX>(a, v, kk, mu, alpha, st[S_SIGMA], phase) && a.nq) {
+        if (v.l == 0) atomicAdd(&a.qctl[1], 1);
+        ipm_refill<FX>(a, T, who.s);  // queue mode: the slot takes the next entry
+    }
 }
 
 // ------------------------------------------------------------------------------------------------

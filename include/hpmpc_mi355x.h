@@ -122,6 +122,22 @@ int hpmpc_mi355x_ipm_batch_profiled(const hpmpc_mi355x_plan *plan, const hpmpc_m
                                     double mu_tol, double alpha_min, int warm_start, int compute_mult, int *kk,
                                     int *ret, double *stat, double *pass_ms, void *stream);
 
+/* Problem queue (continuous batching): solve nq problems with n_slots resident solver slots.  Queue
+ * entry q solves data problem q % nprob (BAbt/RSQrq/d as in hpmpc_mi355x_ipm_batch, nprob problems);
+ * ux/pi/lam/t/kk/ret/stat are per queue entry (nq of each, same strides); ws holds n_slots
+ * workspaces; qctl is device scratch of 2 + n_slots ints.  A slot whose problem has finished takes
+ * the next entry at the following iteration, so the GPU is not left idle behind the slowest problem
+ * of a batch.  Results are those of hpmpc_mi355x_ipm_batch on each entry (the per-slot workspace is
+ * reused, so a queue solve leaves no factor behind for d_kkt_solve_new_rhs_res_mpc_hard_tv).
+ * Synchronises with the device once per chunk of iterations (it polls the finished counter); on
+ * return the last chunk may still be running on `stream`.  pass_ms (nullable): device time of
+ * [init, fact, pred, corr, update] summed over the run; n_ticks (nullable): iterations enqueued. */
+int hpmpc_mi355x_ipm_queue(const hpmpc_mi355x_plan *plan, const hpmpc_mi355x_layout *lay, int nprob, int nq,
+                           int n_slots, const double *BAbt, const double *RSQrq, const double *d, double *ux,
+                           double *pi, double *lam, double *t, double *ws, int *qctl, int k_max, double mu0,
+                           double mu_tol, double alpha_min, int warm_start, int compute_mult, int *kk, int *ret,
+                           double *stat, double *pass_ms, int *n_ticks, void *stream);
+
 /* Batched d_back_ric_rec_sv_tv_res (no box / no update rows): factor into ws, ux/pi as above. */
 int hpmpc_mi355x_ric_sv_batch(const hpmpc_mi355x_plan *plan, const hpmpc_mi355x_layout *lay, int nprob, int p0,
                               int count, const double *BAbt, const double *RSQrq, double *ux, double *pi, double *ws,

@@ -253,3 +253,70 @@ def test_full_size_properties():
                    pi=[pi[p, k] for k in range(100)], lam=[lamt[0][p, k] for k in range(101)],
                    t=[lamt[1][p, k] for k in range(101)])
         compare_ipm(one, got, r, tol=TOL_IPM)
+
+
+# ------------------------------------------------------------------ problem queue (continuous batching)
+def _queue_equals_batch(s, Q, nq):
+    import torch
+
+    idx = torch.arange(nq, device=s.ux.device) % s.nprob
+    for name in ("ux", "pi", "lam", "t", "kk", "ret", "stat"):
+        a, b = getattr(Q, name), getattr(s, name)[idx]
+        assert torch.equal(a, b), name
+
+
+@pytest.mark.parametrize("n_slots,nq", [(16, 197), (64, 64), (100, 37)])
+def test_queue_matches_batch(small_batch, n_slots, nq):
+    """Every queue entry q is bitwise the batched solve of problem q % nprob, whatever the slot
+    count (fewer slots than entries, equal, more slots than entries)."""
+    import torch
+
+    from hpmpc_amd.batch import BatchSolver
+
+    s = BatchSolver(small_batch, k_max=50)
+    s.ipm()
+    Q = s.queue(nq, n_slots)
+    pass_ms, ticks = Q.run(profiled=True)
+    torch.cuda.synchronize()
+    _queue_equals_batch(s, Q, nq)
+    assert int(Q.qctl[1]) == nq and bool((Q.qctl[2:] == -1).all())
+    kk = s.kk.cpu().numpy()
+    assert ticks >= int(kk.max()) and pass_ms[1] > 0.0
+    Q.run()  # a second run over the same buffers gives the same answers
+    torch.cuda.synchronize()
+    _queue_equals_batch(s, Q, nq)
+
+
+def test_queue_unconstrained_entries_finish_at_init():
+    """nb = 0 problems are solved by one sv inside the refill (kk = 0): the queue drains without
+    any iteration doing work."""
+    import torch
+
+    from hpmpc_amd.batch import BatchSolver
+
+    qp = mass_spring_qp(20, 8, 3, boxes=False, batch=8, time_variant=True, seed=4)
+    s = BatchSolver(qp, k_max=10)
+    s.ipm()
+    Q = s.queue(40, 4)
+    Q.run()
+    torch.cuda.synchronize()
+    _queue_equals_batch(s, Q, 40)
+    assert int(Q.kk.max()) == 0
+
+
+def test_queue_full_size_matches_batch():
+    """The benchmark workload (N=100 nx=12 nu=4, 1024 problems) through a queue of two batches."""
+    import torch
+
+    from hpmpc_amd.batch import BatchSolver
+    from hpmpc_amd.shard import make_shard
+
+    qp = make_shard(100, 12, 4, 0, 1, 1024)
+    s = BatchSolver(qp, k_max=50)
+    s.ipm()
+    Q = s.queue(2048)
+    _, ticks = Q.run()
+    torch.cuda.synchronize()
+    _queue_equals_batch(s, Q, 2048)
+    # two batches back to back would take 2 x 50 iterations; the queue needs far fewer
+    assert ticks < 100
