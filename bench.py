@@ -6,11 +6,13 @@ MPC QPs per GPU, N=100, nx=12, nu=4 (nb = 4 / 10 / 6 on stage 0 / inner / N), fp
 stage data (no aliased buffers), solved by the residual-based Mehrotra IPM
 (d_ip2_res_mpc_hard_tv: mu0=2, mu_tol=1e-12, alpha_min=1e-8, k_max=50).
 
-A "step" is one batched IPM solve of the whole resident batch (pass kernels hk_ipm_init, then
-k_max x [hk_ipm_fact, hk_ipm_pred, hk_ipm_corr, hk_ipm_update]).  value = IP iterations per second
-over all ranks (sum of per-problem iteration counts / max-over-ranks time).  The roofline object is
-for the dominant kernel (the factorisation pass, hk_ipm_fact), timed with hipEvents around each of
-its launches inside the timed region.
+A "step" is one batch of 1024 problems.  The K timed steps are solved through one problem queue
+(hpmpc_mi355x_ipm_queue): 2 x 1024 resident solver slots, each taking the next problem as soon as its
+own has converged (iterations are ticks of the pass kernels hk_ipm_fact, hk_ipm_pred, hk_ipm_corr,
+hk_ipm_update over all slots).  value = IP iterations per second over all ranks (sum of per-problem
+iteration counts / max-over-ranks time).  The roofline object is for the dominant kernel (the
+factorisation pass, hk_ipm_fact), timed with hipEvents at every kernel boundary inside the timed
+region.  An isolated single-batch solve is reported beside it.
 The Riccati factorisation rate (d_back_ric_rec_sv_tv_res, nb = 0, compute_pi = 1) of the same
 batch is reported in the same JSON line.
 
@@ -45,10 +47,14 @@ def parse():
     ap.add_argument("--nx", type=int, default=12)
     ap.add_argument("--nu", type=int, default=4)
     ap.add_argument("--k-max", type=int, default=50)
+    ap.add_argument("--slots", type=int, default=0, help="resident solver slots (default 2 x batch: two "
+                    "problems per SIMD)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-threads", type=int, default=16, help="host threads for the CPU baseline "
                     "(the GPU box's CPU share is 16 per GPU)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-isolated", action="store_true", help="skip the isolated single-batch solve (profiling "
+                    "runs: then every hk_ipm_* launch of the command belongs to the timed queue)")
     return ap.parse_args()
 
 
@@ -139,34 +145,51 @@ def main():
     max_over_ranks, sum_over_ranks = red.max, red.sum
 
     # ---------------- IPM (headline) ----------------
-    # One step = one batched solve (hpmpc_mi355x_ipm_batch_profiled: the same kernel sequence as
-    # hpmpc_mi355x_ipm_batch with a hipEvent pair around every pass kernel, on the solve's stream).
-    for _ in range(args.warmup):
-        solver.ipm_profiled()
+    # A step is one batch of B problems.  The K timed steps go through one problem queue
+    # (hpmpc_mi355x_ipm_queue): `slots` resident solver slots, each taking the next problem of the
+    # queue as soon as its own has converged, so K batches cost ~K x (mean iterations), not
+    # K x (max iterations).  Profiled run: one hipEvent per kernel boundary on the solve's stream.
+    slots = args.slots if args.slots > 0 else 2 * B
+    if args.warmup > 0:
+        wq = solver.queue(args.warmup * B, slots)
+        wq.run()
+        torch.cuda.synchronize()
+        del wq
+    Q = solver.queue(args.steps * B, slots)
     barrier()
-    pass_ms = np.zeros(5)
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        pass_ms += solver.ipm_profiled()
+    pass_ms, ticks = Q.run(profiled=True)
     barrier()
     t1 = time.perf_counter()
     dt = max_over_ranks(t1 - t0)
-    kk = solver.kk.cpu().numpy()
-    ret = solver.ret.cpu().numpy()
-    iters_step = float(kk.sum())
-    iters_total = sum_over_ranks(iters_step) * args.steps
+    kk = Q.kk.cpu().numpy()
+    ret = Q.ret.cpu().numpy()
+    iters_rank = float(kk.sum())
+    iters_total = sum_over_ranks(iters_rank)
     value = iters_total / dt
     names = ["hk_ipm_init", "hk_ipm_fact", "hk_ipm_pred", "hk_ipm_corr", "hk_ipm_update"]
-    launches = np.array([1] + [args.k_max] * 4) * args.steps
     dom = int(np.argmax(pass_ms))
     bytes_fact = algorithmic_bytes_per_fact(qp)  # per problem-iteration of the factorisation pass
-    # algorithmic bytes of the factorisation kernel over the step / its device time over the step
-    fact_ms_step = pass_ms[1] / args.steps
-    achieved = iters_step * bytes_fact / (fact_ms_step * 1e-3) / 1e9
-    launch_ms = pass_ms[1] / launches[1]
+    # per launch of the factorisation kernel: the problem-iterations it processes (sum kk / launches)
+    # x their algorithmic bytes, over its average launch duration (both from this timed run)
+    launch_ms = pass_ms[1] / ticks
+    probs_per_launch = iters_rank / ticks
+    achieved = probs_per_launch * bytes_fact / (launch_ms * 1e-3) / 1e9
     bytes_iter = algorithmic_bytes_per_ip_iter(qp)
-    ipm_ms_step = pass_ms.sum() / args.steps
+    ipm_ms = float(pass_ms.sum())
     fl_iter = flops_ip_iter(N, nx, nu)
+    del Q
+
+    # one isolated batch (no queue): the latency of a batch solve, reported beside the queue rate
+    iso = None
+    if not args.no_isolated:
+        solver.ipm_profiled()
+        torch.cuda.synchronize()
+        iso_ms = float(solver.ipm_profiled().sum())
+        iso_iters = float(solver.kk.sum().item())
+        iso = {"ms": iso_ms, "value": iso_iters / (iso_ms * 1e-3), "unit": "IP-iter/s",
+               "note": "one batch solved alone (hpmpc_mi355x_ipm_batch): every pass runs k_max times, so the "
+                       "slowest problem sets the time"}
 
     # ---------------- Riccati factorisation + solve ----------------
     for _ in range(args.warmup):
@@ -193,8 +216,9 @@ def main():
         try:
             with open(pmc) as f:
                 pm = json.load(f)
-            if pm.get("workload") == f"ipm_N{N}_nx{nx}_nu{nu}_batch{B}":
-                traffic = pm.get("kernels", {}).get("hk_ipm_fact", {}).get("hbm_bytes_per_launch")
+            if pm.get("workload") == f"ipm_queue_N{N}_nx{nx}_nu{nu}_batch{B}_slots{slots}":
+                # measured HBM bytes per problem-iteration of hk_ipm_fact x this run's problems per launch
+                traffic = pm["fact_hbm_bytes_per_problem_iter"] * probs_per_launch
         except Exception:
             traffic = None
 
@@ -221,16 +245,20 @@ def main():
             "config": {"workload": f"ipm_N{N}_nx{nx}_nu{nu}_batch{B}", "N": N, "nx": nx, "nu": nu,
                        "batch_per_gpu": B, "global_batch": B * world, "k_max": args.k_max, "mu_tol": 1e-12,
                        "parallelism": f"dp{world}" if world > 1 else "single",
+                       "schedule": f"problem queue: {args.steps} batches per rank through {slots} resident "
+                                   f"slots (hpmpc_mi355x_ipm_queue)",
                        "sum_kk_per_step": iters_total / args.steps, "ret_counts": {
                            str(int(r)): int((ret == r).sum()) for r in np.unique(ret)}},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS, "traffic": traffic, "kernel": names[dom],
-                         "launch_ms": launch_ms, "launches_per_step": int(launches[1] // args.steps),
+                         "launch_ms": launch_ms, "launches": int(ticks),
+                         "problem_iters_per_launch": probs_per_launch,
                          "algorithmic_bytes_per_problem_iter": bytes_fact,
                          "pass_ms_per_step": {n: float(v / args.steps) for n, v in zip(names, pass_ms)},
-                         "ipm_whole_solve": {"achieved_GBps": iters_step * bytes_iter / (ipm_ms_step * 1e-3) / 1e9,
+                         "ipm_whole_solve": {"achieved_GBps": iters_rank * bytes_iter / (ipm_ms * 1e-3) / 1e9,
                                              "algorithmic_bytes_per_ip_iter": bytes_iter,
-                                             "fp64_tflops": iters_step * fl_iter / (ipm_ms_step * 1e-3) / 1e12}},
+                                             "fp64_tflops": iters_rank * fl_iter / (ipm_ms * 1e-3) / 1e12}},
+            "isolated_batch": iso,
             "riccati": {"value": fact_total / rdt, "unit": "fact/s", "kernel": "hk_ric_sv", "launch_ms": sv_ms,
                         "roofline": {"bound": "hbm", "achieved": sv_achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                                      "frac": sv_achieved / PEAK_HBM_GBS,

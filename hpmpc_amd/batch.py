@@ -237,16 +237,17 @@ def algorithmic_bytes_per_ip_iter(qp: OCPQP) -> float:
 
 
 def algorithmic_bytes_per_fact(qp: OCPQP) -> float:
-    """Algorithmic HBM bytes of one problem through the IPM factorisation pass (hk_ipm_fact, phase 2):
-    BAbt and lower(RSQrq)+row read, update rows r_b / r_q read, box vectors lam, t, r_m, r_d read and
-    t_inv written (10 doubles per box), factor L lower + row + inv_diag and P b written."""
+    """Algorithmic HBM bytes of one problem through the IPM factorisation pass (hk_ipm_fact, phase 2,
+    residuals fused): BAbt (with its b row) and lower(RSQrq)+q row read, the iterate ux / pi read and
+    the residuals r_q / r_b written, box vectors lam, t, r_m, r_d read and t_inv written (10 doubles
+    per box), factor L lower + row + inv_diag and P b written."""
     tot = 0
     N = qp.N
     for k in range(N + 1):
         nux = qp.nux(k)
         nx1 = int(qp.nx[k + 1]) if k < N else 0
         T = nux * (nux + 1) // 2
-        tot += (nux + 1) * nx1 + (T + nux) + nx1 + nux + 10 * int(qp.nb[k]) + (T + 2 * nux) + nx1
+        tot += (nux + 1) * nx1 + (T + nux) + 2 * (nux + nx1) + 10 * int(qp.nb[k]) + (T + 2 * nux) + nx1
     return 8.0 * tot
 
 

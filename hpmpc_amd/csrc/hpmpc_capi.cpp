@@ -450,7 +450,12 @@ extern "C" int hpmpc_mi355x_ipm_queue(const hpmpc_mi355x_plan* plan, const hpmpc
             return HPMPC_MI355X_EHIP;
         }
     }
-    // the chunk enqueued last finds every slot idle; it is left to complete on the stream, untimed
+    // the chunk enqueued last finds every slot idle; profiled runs wait for it so that pass_ms covers
+    // every launch (n_ticks of each pass kernel), otherwise it completes on the stream
+    if (pass_ms) {
+        const int par = (int)((ticks / R - 1) & 1);
+        if (!hip_ok(hipEventSynchronize(done_ev[par]), "event sync") || !harvest(par)) return g_err;
+    }
     if (n_ticks) *n_ticks = (int)ticks;
     return g_err = 0;
 }

@@ -1,7 +1,8 @@
 #!/bin/bash
-# Round-end evidence on the GPU box: GPU parity tests, smoke, bench line, rocprofv3 kernel stats,
-# and the two PMC passes for HBM traffic.  Every GPU step has its own time limit; the script stops at
-# the first failure.
+# Round-end evidence on the GPU box: GPU parity tests, smoke, the two PMC passes for HBM traffic
+# (folded into profiles/pmc_hk_ipm.json before the bench reads it), the bench line, and the
+# rocprofv3 kernel stats of the same bench command.  Every GPU step has its own time limit; the
+# script stops at the first failure.
 set -o pipefail
 mkdir -p gpurun_out/prof
 export TMPDIR=/tmp
@@ -9,11 +10,14 @@ R=${1:-r01}
 step() { local name=$1; shift; echo "== $name"; "$@" > gpurun_out/$name.log 2>&1; local rc=$?; tail -${TAILN:-3} gpurun_out/$name.log; if [ $rc -ne 0 ]; then echo "$name failed rc=$rc"; exit $rc; fi; }
 step tests timeout -k 10 900 python3 -m pytest tests -m gpu -q -x
 step smoke timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()"
-step bench timeout -k 10 600 python3 bench.py
-step stats timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/stats -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu
 step pmc_fetch timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof/fetch -o run --output-format csv -- python3 tools/pmc_run.py
 step pmc_write timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof/write -o run --output-format csv -- python3 tools/pmc_run.py
 KK=$(grep kk_sum gpurun_out/pmc_write.log | awk '{print $2}')
-python3 tools/pmc_summarize.py gpurun_out/prof/fetch gpurun_out/prof/write gpurun_out/pmc_hk_ipm.json $KK
+python3 tools/pmc_summarize.py gpurun_out/prof/fetch gpurun_out/prof/write gpurun_out/pmc_hk_ipm.json $KK || exit 1
+cp gpurun_out/pmc_hk_ipm.json profiles/pmc_hk_ipm.json
+step bench timeout -k 10 600 python3 bench.py
+# kernel stats of the timed region only: no warmup queue, no isolated batch, so every hk_ipm_* launch
+# in the trace is one of the timed queue's (its average matches the bench line's launch_ms)
+step stats timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/stats -o run --output-format csv -- python3 bench.py --no-cpu --warmup 0 --no-isolated
 find gpurun_out/prof/stats -name "*kernel_stats.csv" -exec cp {} gpurun_out/${R}_kernel_stats.csv \;
 cat gpurun_out/${R}_kernel_stats.csv

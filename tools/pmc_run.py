@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Workload for the rocprofv3 --pmc passes (one counter group per pass, see tools/gpu_round.sh):
-1 GiB calibration copy (known bytes), then the benchmark's IPM and Riccati launches (N=100 nx=12
-nu=4, batch 1024), two launches each."""
+1 GiB calibration copy (known bytes), then the benchmark's IPM (N=100 nx=12 nu=4, batch 1024: a
+problem queue of 4 batches through 2048 slots, run twice) and two Riccati sv launches."""
 import ctypes as C
 import os
 import sys
@@ -29,12 +29,14 @@ def main():
     qp = make_shard(100, 12, 4, 0, 1, 1024)
     sol = BatchSolver(qp, k_max=50)
     ric = BatchSolver(make_shard(100, 12, 4, 0, 1, 1024, boxes=False), k_max=1)
+    Q = sol.queue(4 * 1024, 2048)
     for _ in range(2):
-        sol.ipm()
+        Q.run()
+        torch.cuda.synchronize()
     for _ in range(2):
         ric.ric_sv()
     torch.cuda.synchronize()
-    print("kk_sum", int(sol.kk.sum().item()))
+    print("kk_sum", int(Q.kk.sum().item()))
 
 
 if __name__ == "__main__":

@@ -30,7 +30,7 @@ def main(fetch_dir, write_dir, out, kk_sum):
     known = float(1 << 30)
     cf = known / (sum(F["calib_copy"]["FETCH_SIZE"]) / len(F["calib_copy"]["FETCH_SIZE"]))
     cw = known / (sum(W["calib_copy"]["WRITE_SIZE"]) / len(W["calib_copy"]["WRITE_SIZE"]))
-    res = {"workload": "ipm_N100_nx12_nu4_batch1024",
+    res = {"workload": "ipm_queue_N100_nx12_nu4_batch1024_slots2048",
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (tools/gpu_round.sh); "
                      "per-launch values scaled by the calib_copy factors (1 GiB known bytes, 8-B/lane buffer ops)",
            "calib": {"fetch_factor": cf, "write_factor": cw,
@@ -47,7 +47,7 @@ def main(fetch_dir, write_dir, out, kk_sum):
                              "write_bytes_per_launch": wb, "hbm_bytes_per_launch": fb + wb}
     ipm = [k for k in res["kernels"] if k.startswith("hk_ipm_")]
     if ipm and kk_sum:
-        # pmc_run.py runs two solves: per solve the passes run k_max times each
+        # pmc_run.py runs the same queue twice; kk_sum is per run
         tot = sum(sum(F[k]["FETCH_SIZE"]) * cf + sum(W[k]["WRITE_SIZE"]) * cw for k in ipm) / 2.0
         res["kk_sum_per_solve"] = kk_sum
         res["hbm_bytes_per_ip_iter_problem"] = tot / kk_sum
