@@ -24,7 +24,7 @@ def main():
     loops = collections.OrderedDict()
     cur = None
     for ln in open(path):
-        m = re.match(r"^(_Z\w*?(hk_[a-z_]+)\w*|hk_\w+):", ln)
+        m = re.match(r"^(_Z\w*?(hk4?_[a-z_0-9]+)\w*|hk4?_\w+):", ln)
         if m:
             full = m.group(1)
             base = m.group(2) or full
@@ -46,7 +46,7 @@ def main():
         if cur and ln.startswith("\t") and not ln.strip().startswith((";", ".")):
             op = ln.split()[0]
             d = loops.setdefault(cur, collections.Counter())
-            k = ("nop" if op == "s_nop" else "wait" if op.startswith("s_waitcnt") else "mfma" if "mfma" in op else "vmem" if op.startswith("buffer") or op.startswith("global") else
+            k = ("scratch" if op.startswith("scratch_") else "nop" if op == "s_nop" else "wait" if op.startswith("s_waitcnt") else "mfma" if "mfma" in op else "vmem" if op.startswith("buffer") or op.startswith("global") else
                  "lds" if op.startswith("ds_") else "salu" if op.startswith("s_") else
                  "lane" if ("readlane" in op or "writelane" in op or "readfirstlane" in op) else
                  "xlane" if ("dpp" in op or "permlane" in op) else "valu")
@@ -57,7 +57,7 @@ def main():
             continue
         print(f"{k:26s} {lab:10s} total {d['total']:5d}  valu {d['valu']:4d} salu {d['salu']:4d} nop {d['nop']:3d} "
               f"wait {d['wait']:3d} lane {d['lane']:3d} xlane {d['xlane']:3d} vmem {d['vmem']:3d} lds {d['lds']:3d} "
-              f"mfma {d['mfma']:2d}")
+              f"mfma {d['mfma']:2d} scratch {d['scratch']:3d}")
 
 
 if __name__ == "__main__":
