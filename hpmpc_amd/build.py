@@ -18,7 +18,7 @@ SOURCES = ["hpmpc_kernels.hip", "hpmpc_capi.cpp"]
 HEADERS = ["hk_prims.h", "hk_riccati.h", "hk_ipm.h", "hpmpc_kargs.h"]
 # MFMA accumulators stay in ordinary VGPRs: the stage tile is read and written by VALU code between
 # MFMAs, and the AGPR form costs 8 v_accvgpr moves each way per MFMA group.
-KFLAGS = ["-mllvm", "-amdgpu-mfma-vgpr-form"]
+KFLAGS = ["-mllvm", "-amdgpu-mfma-vgpr-form"] + os.environ.get("HK_EXTRA_FLAGS", "").split()
 
 
 def _newer(out, deps):

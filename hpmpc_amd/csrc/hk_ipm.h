@@ -34,13 +34,33 @@ struct BoxTab {
         }                                                                              \
     }
 
+// Iterate (stage k, general constraint l) pairs four stages per pass (one-off passes only).
+#define HK_FOR_GEN(io, KV, ...)                                                       \
+    for (int j4_ = 0; j4_ <= (io).N; j4_ += 4) {                                       \
+        const int KV = j4_ + (lane_id() >> 4);                                         \
+        const int gl_ = lane_id() & 15;                                                \
+        if (KV <= (io).N) {                                                            \
+            const int ng_ = (io).st[KV].ng, pnb_ = (io).st[KV].pnb;                    \
+            if (gl_ < ng_) {                                                           \
+                const int png_ = (ng_ + 3) & ~3;                                       \
+                const int lo = KV * V32 + 2 * pnb_ + gl_, up = lo + png_;               \
+                const int s16 = KV * V16 + pnb_ + gl_;                                 \
+                (void)lo; (void)up; (void)s16;                                         \
+                __VA_ARGS__                                                            \
+            }                                                                          \
+        }                                                                              \
+    }
+
 // ------------------------------------------------------------------------------------------------
 // Element-wise box passes over quads of stages: lane (g, c) handles stage 4q+g, slot c.  CH quads
 // (4*CH stages) are loaded before any is used.
 // ------------------------------------------------------------------------------------------------
+// Lane c of row group g owns constraint pair c of stage 4q+g: box c (c < nb) or general constraint
+// c - nb (nb <= c < nb + ng), with its lower / upper slot in the [lb | ub | lg | ug] layout.
 struct QuadLane {
     int lo, up;
     bool ok;
+    bool box;  // a box pair (its variable is slotvar[c])
 };
 
 __device__ __forceinline__ QuadLane quad_lane(const RicIO& io, int q) {
@@ -50,9 +70,11 @@ __device__ __forceinline__ QuadLane quad_lane(const RicIO& io, int q) {
     const int kc = kv ? k : io.N;
     const StageInfo& s = io.st[kc];
     QuadLane b;
-    b.ok = kv && c < s.nb;
-    b.lo = kc * V32 + c;
-    b.up = b.lo + s.pnb;
+    b.ok = kv && c < s.nb + s.ng;
+    b.box = c < s.nb;
+    const int png = (s.ng + 3) & ~3;
+    b.lo = kc * V32 + (b.box ? c : 2 * s.pnb + (c - s.nb));
+    b.up = b.lo + (b.box ? s.pnb : png);
     return b;
 }
 
@@ -174,7 +196,7 @@ __device__ double update_p2_pass(const RicIO& io, const BoxCtx& bc, const signed
             okp[j] = kv && k < io.N && c < s.nx1;
             bl[j] = quad_lane(io, q0 + j);
             const QuadLane& b = bl[j];
-            iv[j] = kc * V16 + (b.ok ? slotvar[kc * 16 + c] : 0);
+            iv[j] = kc * V16 + ((b.ok && b.box) ? slotvar[kc * 16 + c] : 0);
             v[j][0] = UPD ? gld(ux, i16[j], oku[j]) : 0.0;
             v[j][1] = UPD ? gld(dux, i16[j], oku[j]) : 0.0;
             v[j][2] = UPD ? gld(pi, i16[j], okp[j]) : 0.0;
@@ -187,8 +209,8 @@ __device__ double update_p2_pass(const RicIO& io, const BoxCtx& bc, const signed
             v[j][9] = UPD ? gld(bc.dlam, b.up, b.ok) : 0.0;
             v[j][10] = gld(bc.t, b.up, b.ok);
             v[j][11] = UPD ? gld(bc.dt, b.up, b.ok) : 0.0;
-            v[j][12] = gld(ux, iv[j], b.ok);
-            v[j][13] = UPD ? gld(dux, iv[j], b.ok) : 0.0;
+            v[j][12] = gld(ux, iv[j], b.ok && b.box);
+            v[j][13] = UPD ? gld(dux, iv[j], b.ok && b.box) : 0.0;
             v[j][14] = gld(bc.d, b.lo, b.ok);
             v[j][15] = gld(bc.d, b.up, b.ok);
         }
@@ -217,8 +239,9 @@ __device__ double update_p2_pass(const RicIO& io, const BoxCtx& bc, const signed
                 gst(bc.t, b.up, tu, b.ok);
             }
             const double rml = ll * tl, rmu = lu * tu;
-            gst(res_d, b.lo, v[j][14] - x + tl, b.ok);
-            gst(res_d, b.up, v[j][15] - x - tu, b.ok);
+            // r_d of the general pairs needs D x: the next factorisation forms it (gen_hessian)
+            gst(res_d, b.lo, v[j][14] - x + tl, b.ok && b.box);
+            gst(res_d, b.up, v[j][15] - x - tu, b.ok && b.box);
             gst(res_m, b.lo, rml, b.ok);
             gst(res_m, b.up, rmu, b.ok);
             ms += b.ok ? rml + rmu : 0.0;
@@ -383,6 +406,30 @@ __device__ __forceinline__ void res_step(const RicIO& io, const SH& sh, int k, c
     gst(ro.rm, b.lo, rml, st0 && b.ok);
     gst(ro.rm, b.up, rmu, st0 && b.ok);
     ms += (st0 && b.ok) ? rml + rmu : 0.0;
+    if constexpr (!SH::fixed) {
+        if (sh.ng > 0) {  // general constraints (d_res_ip_res_hard.c:393-416); never on the UPD path
+            static_assert(!UPD || SH::fixed, "the update pass handles general slots element-wise");
+            const double tq = gen_rq(io, sh, k, bc.lam);
+            gst(ro.rq, k * V16 + vc, h + tq, st0 && vc >= 0);
+            double dg[4];
+            gen_dg(io, sh, dg);
+#pragma unroll
+            for (int lc = 0; lc < 4; lc++) {
+                if (4 * lc >= sh.ng) continue;
+                const GenLane q = gen_lane(k, sh.pnb, sh.ng, lc);
+                const bool st = q.ok && c == 0;
+                const double dx = row_sum16(dg[lc] * x);
+                const double tgl = gld(bc.t, q.lo, q.ok), tgu = gld(bc.t, q.up, q.ok);
+                const double lgl = gld(bc.lam, q.lo, q.ok), lgu = gld(bc.lam, q.up, q.ok);
+                gst(ro.rd, q.lo, gld(bc.d, q.lo, q.ok) - dx + tgl, st);
+                gst(ro.rd, q.up, gld(bc.d, q.up, q.ok) - dx - tgu, st);
+                const double gml = lgl * tgl, gmu = lgu * tgu;
+                gst(ro.rm, q.lo, gml, st);
+                gst(ro.rm, q.up, gmu, st);
+                ms += st ? gml + gmu : 0.0;  // constraint 4 lc + g is counted once, in lane (g, 0)
+            }
+        }
+    }
     pim1 = pcn;
 }
 
@@ -402,7 +449,7 @@ __device__ bool residual_pass(const RicIO& io, const BoxCtx& bc, const ResIO& ro
         with_shape<FX>(sn, [&](const auto& sh) { res_fetch<UPD>(io, sh, bc, ro, kn, nxt); });
         asm volatile("" ::: "memory");
         const StageInfo si = load_stage(io.st, k);
-        nbt += si.nb;
+        nbt += si.nb + si.ng;
         with_shape<FX>(si, [&](const auto& sh) { res_step<UPD>(io, sh, k, cur, bc, ro, pim1, ms); });
         cur = nxt;
     }

@@ -26,7 +26,8 @@ struct StageInfo {
     int sdB, sdR;       // lib4 panel strides of BAbt_k (cnx_{k+1}) and RSQrq_k (cnux_k)
     int oB, oR, oD;     // offsets (doubles) of BAbt_k / RSQrq_k / d_k inside one problem's arrays
     int pnb;            // round_up(nb, 4)
-    int r0, r1;
+    int r0;             // stage belongs to the compiled inner class (constant shapes)
+    int oG;             // offset (doubles) of DCt_k inside one problem's general-constraint array
 };
 
 constexpr int FSTRIDE = 352;  // factor doubles per stage: 4 regs x 64 lanes + l (16) + inv_diag (16) + KG (64)
@@ -220,6 +221,7 @@ struct RicIO {
     const double* BAbt;           // this problem's BAbt base (stage k block at st[k].oB)
     const double* RSQ;            // this problem's RSQrq base (stage k block at st[k].oR)
     double* F;                    // factor store (N+1)*FSTRIDE (private layout)
+    const double* DCt;            // this problem's general-constraint base (stage k block at st[k].oG)
 };
 
 // Stage record from the LDS table, forced into SGPRs (readfirstlane) so that every address derived
@@ -242,7 +244,7 @@ __device__ __forceinline__ StageInfo load_stage(const StageInfo* st, int k) {
     u.oD = __builtin_amdgcn_readfirstlane(v.oD);
     u.pnb = __builtin_amdgcn_readfirstlane(v.pnb);
     u.r0 = __builtin_amdgcn_readfirstlane(v.r0);  // stage belongs to the compiled inner class
-    u.r1 = 0;
+    u.oG = __builtin_amdgcn_readfirstlane(v.oG);
     return u;
 }
 
@@ -257,10 +259,10 @@ __device__ __forceinline__ StageInfo load_stage(const StageInfo* st, int k) {
 // ------------------------------------------------------------------------------------------------
 struct DynSh {
     static constexpr bool fixed = false;
-    int nu, nx, xo, nx1, nu1, xo1, sdB, sdR, nb, pnb, oB, oR;
+    int nu, nx, xo, nx1, nu1, xo1, sdB, sdR, nb, pnb, oB, oR, ng, oG;
     __device__ __forceinline__ explicit DynSh(const StageInfo& s)
         : nu(s.nu), nx(s.nx), xo(s.xo), nx1(s.nx1), nu1(s.nu1), xo1(s.xo1), sdB(s.sdB), sdR(s.sdR), nb(s.nb),
-          pnb(s.pnb), oB(s.oB), oR(s.oR) {}
+          pnb(s.pnb), oB(s.oB), oR(s.oR), ng(s.ng), oG(s.oG) {}
 };
 
 template <int NU, int NX>
@@ -365,6 +367,200 @@ __device__ __forceinline__ BoxLane box_lane(const signed char* tileslot, int pnb
 __device__ __forceinline__ void alpha_rule(double& al, double v, double dv) {
     const double cand = -v * rcp_nr(dv);
     al = (-al * dv > v) ? cand : al;
+}
+
+
+// ------------------------------------------------------------------------------------------------
+// General constraints lg <= D_k ux_k <= ug (ng_k > 0; such stages always run the generic shape).
+// DCt_k = D_k' is a lib4 block (nux x ng, sd = round_up(ng, 2)).  Constraint l = 4*lc + g belongs to
+// row group g in chunk lc, so a lane holds dg[lc] = DCt[var(c)][4 lc + g] and
+//   (D v)_l      = row_sum16(dg[lc] * v_col)             (every lane of row group g)
+//   (DCt w)_c    = xrow_sum(sum_lc dg[lc] * w_l)          (col layout)
+//   DCt W DCt'   = sum_lc mfma(dg[lc] * W_l, dg[lc])      (tile layout, W diagonal)
+// Slots: [lb (pnb) | ub (pnb) | lg (png) | ug (png)] in the V32 vectors, [box (pnb) | general (png)] in
+// Qx / qx (d_aux_ip_hard_lib4.c, the "general" halves of every box routine).
+// ------------------------------------------------------------------------------------------------
+struct GenLane {
+    int lo, up, s16;
+    bool ok;
+};
+
+__device__ __forceinline__ GenLane gen_lane(int k, int pnb, int ng, int lc) {
+    const int gl = 4 * lc + (lane_id() >> 4);
+    const int png = (ng + 3) & ~3;
+    GenLane q;
+    q.ok = gl < ng;
+    q.lo = k * V32 + 2 * pnb + gl;
+    q.up = q.lo + png;
+    q.s16 = k * V16 + pnb + gl;
+    return q;
+}
+
+__device__ __forceinline__ void gen_dg(const RicIO& io, const DynSh& sh, double dg[4]) {
+    const int l = lane_id(), g = l >> 4, c = l & 15;
+    const int vc = tile_var(c, sh.nu, sh.nx, sh.xo);
+    const int cng = (sh.ng + 1) & ~1;
+    const double* D = io.DCt + sh.oG;
+#pragma unroll
+    for (int lc = 0; lc < 4; lc++) {
+        const int gl = 4 * lc + g;
+        dg[lc] = (4 * lc < sh.ng) ? gld(D, lib4_idx(cng, vc, gl), vc >= 0 && gl < sh.ng) : 0.0;
+    }
+}
+
+// Backward: M += DCt diag(Qg) DCt', ml += DCt qg with the box routine of mode BM applied to the general
+// slots (d_update_hessian_mpc_hard_tv / d_update_hessian_gradient_res_mpc_hard_tv general halves).
+// BX_P2R also forms r_d of the general slots from the current iterate (x: ux_k in col layout).
+template <int BM>
+__device__ void gen_hessian(const RicIO& io, const DynSh& sh, int k, const BoxCtx& bc, double x, d4& M, double& ml,
+                            bool aug) {
+    const int c = lane_id() & 15;
+    double dg[4];
+    gen_dg(io, sh, dg);
+    double part = 0.0;
+#pragma unroll
+    for (int lc = 0; lc < 4; lc++) {
+        if (4 * lc >= sh.ng) continue;
+        const GenLane q = gen_lane(k, sh.pnb, sh.ng, lc);
+        const bool st = q.ok && c == 0;
+        double Q = 0.0, qv = 0.0;
+        if (BM == BX_GIVEN) {
+            Q = gld(bc.Qx, q.s16, q.ok);
+            qv = aug ? gld(bc.qx, q.s16, q.ok) : 0.0;
+        } else if (BM == BX_P1) {
+            const double lml = gld(bc.lam, q.lo, q.ok), lmu = gld(bc.lam, q.up, q.ok);
+            const double tl = gld(bc.t, q.lo, q.ok), tu = gld(bc.t, q.up, q.ok);
+            const double dl = gld(bc.d, q.lo, q.ok), du = gld(bc.d, q.up, q.ok);
+            const double til = rcp_nr(tl), tiu = rcp_nr(tu);
+            const double ltl = lml * til, ltu = lmu * tiu;
+            const double dll = til * 0.0, dlu = tiu * 0.0;
+            qv = lmu - ltu * du + dlu - lml - ltl * dl - dll;
+            Q = ltl + ltu;
+            gst(bc.t_inv, q.lo, til, st);
+            gst(bc.t_inv, q.up, tiu, st);
+            gst(bc.lamt, q.lo, ltl, st);
+            gst(bc.lamt, q.up, ltu, st);
+            gst(bc.qxs, q.s16, qv, st);
+        } else if (BM == BX_P2 || BM == BX_P2R) {
+            const double lml = gld(bc.lam, q.lo, q.ok), lmu = gld(bc.lam, q.up, q.ok);
+            const double tl = gld(bc.t, q.lo, q.ok), tu = gld(bc.t, q.up, q.ok);
+            const double rml = gld(bc.res_m, q.lo, q.ok), rmu = gld(bc.res_m, q.up, q.ok);
+            double rdl, rdu;
+            if (BM == BX_P2R) {  // r_d = [lg - D x + t_lg | ug - D x - t_ug]  (d_res_ip_res_hard.c:393-416)
+                const double dx = row_sum16(dg[lc] * x);
+                rdl = gld(bc.d, q.lo, q.ok) - dx + tl;
+                rdu = gld(bc.d, q.up, q.ok) - dx - tu;
+                gst(bc.res_d, q.lo, rdl, st);
+                gst(bc.res_d, q.up, rdu, st);
+            } else {
+                rdl = gld(bc.res_d, q.lo, q.ok);
+                rdu = gld(bc.res_d, q.up, q.ok);
+            }
+            const double til = rcp_nr(tl), tiu = rcp_nr(tu);
+            qv = til * (rml - lml * rdl) - tiu * (rmu + lmu * rdu);
+            Q = til * lml + tiu * lmu;
+            gst(bc.t_inv, q.lo, til, st);
+            gst(bc.t_inv, q.up, tiu, st);
+        }
+        Q = q.ok ? Q : 0.0;
+        qv = q.ok ? qv : 0.0;
+        M = mfma(dg[lc] * Q, dg[lc], M);
+        part += dg[lc] * qv;
+    }
+    if (aug) ml += xrow_sum(part);
+}
+
+// r_q term DCt (lam_ug - lam_lg) of the residuals (d_res_ip_res_hard.c:393-407), col layout.
+__device__ double gen_rq(const RicIO& io, const DynSh& sh, int k, const double* lam) {
+    double dg[4];
+    gen_dg(io, sh, dg);
+    double part = 0.0;
+#pragma unroll
+    for (int lc = 0; lc < 4; lc++) {
+        if (4 * lc >= sh.ng) continue;
+        const GenLane q = gen_lane(k, sh.pnb, sh.ng, lc);
+        const double w = gld(lam, q.up, q.ok) - gld(lam, q.lo, q.ok);
+        part += dg[lc] * (q.ok ? w : 0.0);
+    }
+    return xrow_sum(part);
+}
+
+// Forward: steps of the general slots from the primal step x (col layout) and their step-length
+// candidates (d_compute_alpha_mpc_hard_tv / d_compute_alpha_res_mpc_hard_tv general halves).
+template <int FM>
+__device__ void gen_alpha(const RicIO& io, const DynSh& sh, int k, const BoxCtx& bc, double x, double& al) {
+    if (FM == BX_NONE) return;
+    const int c = lane_id() & 15;
+    double dg[4];
+    gen_dg(io, sh, dg);
+#pragma unroll
+    for (int lc = 0; lc < 4; lc++) {
+        if (4 * lc >= sh.ng) continue;
+        const GenLane q = gen_lane(k, sh.pnb, sh.ng, lc);
+        const bool st = q.ok && c == 0;
+        const double dx = row_sum16(dg[lc] * x);
+        const double lml = gld(bc.lam, q.lo, q.ok), lmu = gld(bc.lam, q.up, q.ok);
+        const double tl = gld(bc.t, q.lo, q.ok), tu = gld(bc.t, q.up, q.ok);
+        double dtl, dtu, dll, dlu;
+        if (FM == BX_P1) {
+            dtl = dx - gld(bc.d, q.lo, q.ok) - tl;
+            dtu = -dx + gld(bc.d, q.up, q.ok) - tu;
+            const double d0l = gld(bc.dlam, q.lo, q.ok && !bc.pred), d0u = gld(bc.dlam, q.up, q.ok && !bc.pred);
+            dll = d0l - (gld(bc.lamt, q.lo, q.ok) * dtl + lml);
+            dlu = d0u - (gld(bc.lamt, q.up, q.ok) * dtu + lmu);
+        } else {
+            dtl = dx - gld(bc.res_d, q.lo, q.ok);
+            dtu = -dx + gld(bc.res_d, q.up, q.ok);
+            dll = -gld(bc.t_inv, q.lo, q.ok) * (lml * dtl + gld(bc.res_m, q.lo, q.ok));
+            dlu = -gld(bc.t_inv, q.up, q.ok) * (lmu * dtu + gld(bc.res_m, q.up, q.ok));
+        }
+        gst(bc.dt, q.lo, dtl, st);
+        gst(bc.dt, q.up, dtu, st);
+        gst(bc.dlam, q.lo, dll, st);
+        gst(bc.dlam, q.up, dlu, st);
+        if (q.ok) {
+            alpha_rule(al, lml, dll);
+            alpha_rule(al, lmu, dlu);
+            alpha_rule(al, tl, dtl);
+            alpha_rule(al, tu, dtu);
+        }
+    }
+}
+
+// trs backward: the general part of the gradient, DCt qg (col layout), with the corrector updates of
+// the general slots (d_update_gradient_mpc_hard_tv / centering correction + d_update_gradient_res).
+template <int TM>
+__device__ double gen_gradient(const RicIO& io, const DynSh& sh, int k, const BoxCtx& bc) {
+    if (TM == BX_NONE) return 0.0;
+    const int c = lane_id() & 15;
+    double dg[4];
+    gen_dg(io, sh, dg);
+    double part = 0.0;
+#pragma unroll
+    for (int lc = 0; lc < 4; lc++) {
+        if (4 * lc >= sh.ng) continue;
+        const GenLane q = gen_lane(k, sh.pnb, sh.ng, lc);
+        const bool st = q.ok && c == 0;
+        double qv = 0.0;
+        if (TM == BX_GIVEN) {
+            qv = gld(bc.qx, q.s16, q.ok);
+        } else if (TM == BX_P1) {
+            const double dll = gld(bc.t_inv, q.lo, q.ok) * (bc.smu - gld(bc.dlam, q.lo, q.ok) * gld(bc.dt, q.lo, q.ok));
+            const double dlu = gld(bc.t_inv, q.up, q.ok) * (bc.smu - gld(bc.dlam, q.up, q.ok) * gld(bc.dt, q.up, q.ok));
+            gst(bc.dlam, q.lo, dll, st);
+            gst(bc.dlam, q.up, dlu, st);
+            qv = gld(bc.qxs, q.s16, q.ok) + (dlu - dll);
+        } else if (TM == BX_P2) {
+            const double rml = gld(bc.res_m, q.lo, q.ok) + (gld(bc.dt, q.lo, q.ok) * gld(bc.dlam, q.lo, q.ok) - bc.smu);
+            const double rmu = gld(bc.res_m, q.up, q.ok) + (gld(bc.dt, q.up, q.ok) * gld(bc.dlam, q.up, q.ok) - bc.smu);
+            gst(bc.res_m, q.lo, rml, st);
+            gst(bc.res_m, q.up, rmu, st);
+            qv = gld(bc.t_inv, q.lo, q.ok) * (rml - gld(bc.lam, q.lo, q.ok) * gld(bc.res_d, q.lo, q.ok)) -
+                 gld(bc.t_inv, q.up, q.ok) * (rmu + gld(bc.lam, q.up, q.ok) * gld(bc.res_d, q.up, q.ok));
+        }
+        part += dg[lc] * (q.ok ? qv : 0.0);
+    }
+    return xrow_sum(part);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -517,6 +713,9 @@ __device__ __forceinline__ void bwd_residual(const RicIO& io, Scratch* sm, const
     const double bpi = xrow_sum(p2);
     const double atu = xrow_sum(p3);
     if (live) h += bpi;
+    if constexpr (!SH::fixed) {
+        if (sh.ng > 0) h += gen_rq(io, sh, k, bc.lam);
+    }
     const double rb = f.brow[0] - f.x1 + atu;
     gst(bc.res_q, k * V16 + vc, h, store && g == 0 && vc >= 0);
     gst(bc.res_b, k * V16 + sc, rb, store && g == 0 && oks);
@@ -545,6 +744,9 @@ __device__ __forceinline__ void bwd_step(const RicIO& io, Scratch* sm, const SH&
     double ml = mlq + qxv;  // update_q row (or RSQrq row) + drowad qx
 #pragma unroll
     for (int r = 0; r < 4; r++) M[r] += (g + 4 * r == c) ? dq : 0.0;  // ddiaadin: diag = bd + Qx
+    if constexpr (!SH::fixed && BM != BX_NONE) {
+        if (sh.ng > 0) gen_hessian<BM>(io, sh, k, bc, BM == BX_P2R ? cur.uc : 0.0, M, ml, AUG);
+    }
     const int nx1 = sh.nx1, xo1 = sh.xo1;
     d4 acc = {0.0, 0.0, 0.0, 0.0};
     if (live) {
@@ -894,6 +1096,9 @@ __device__ __forceinline__ void fwd_step(const RicIO& io, Scratch* sm, const SH&
     const int vcs = tile_var(c, sh.nu, sh.nx, sh.xo);
     gst(ux, k * V16 + vcs, ucol, g == 0 && vcs >= 0);
     box_alpha<FM>(bc, cur, ucol, al);
+    if constexpr (!SH::fixed && FM != BX_NONE) {
+        if (sh.ng > 0) gen_alpha<FM>(io, sh, k, bc, ucol, al);
+    }
     // x_{k+1} = b + BAbt_k' ux_k  (dgemv_t_lib alg 1, :347-351), col layout over stage-(k+1) tile
     double gp = 0.0;
 #pragma unroll
@@ -942,6 +1147,7 @@ __device__ void ric_forward(const RicIO& io, Scratch* sm, const double* bsrc, in
     const int v = tile_var(c, sN.nu, sN.nx, sN.xo);
     gst(ux, io.N * V16 + v, xcol, g == 0 && v >= 0);
     box_alpha<FM>(bc, cur, xcol, al);  // stage N: nu = 0, every tile is a state
+    if (FM != BX_NONE && sN.ng > 0) gen_alpha<FM>(io, DynSh(sN), io.N, bc, xcol, al);
 }
 
 template <class FX>
@@ -1078,6 +1284,9 @@ __device__ __forceinline__ void trs_step(const RicIO& io, Scratch* sm, const SH&
 #pragma unroll
     for (int r = 0; r < 4; r++) part += cur.bop[r] * wrow[r];
     double h = cur.h0 + box_gradient<TM>(bc, cur);  // dvecad_libsp (:612-620)
+    if constexpr (!SH::fixed) {
+        if (sh.ng > 0) h += gen_gradient<TM>(io, sh, k, bc);  // dgemv_n on DCt (:621-633)
+    }
     h += xrow_sum(part);
     h = solve_ln(sh, cur.S, cur.invd, h, !SH::fixed && k == 0);
     gst(ux, k * V16 + vc, h, g == 0 && vc >= 0);
@@ -1097,7 +1306,8 @@ __device__ void ric_trs(const RicIO& io, Scratch* sm, const double* hb, const do
     TrsFrag cur;
     const StageInfo sN = load_stage(io.st, io.N);
     with_shape<FX>(sN, [&](const auto& sh) { trs_fetch<TM>(io, sh, io.N, hb, hq, bc, compute_Pb, Pb, cur); });
-    const double hN = cur.h0 + box_gradient<TM>(bc, cur);
+    double hN = cur.h0 + box_gradient<TM>(bc, cur);
+    if (sN.ng > 0) hN += gen_gradient<TM>(io, DynSh(sN), io.N, bc);
     {
         const int v = tile_var(c, sN.nu, sN.nx, sN.xo);
         gst(ux, io.N * V16 + v, hN, g == 0 && v >= 0);

@@ -31,7 +31,7 @@ enum { K_SV = 0, K_TRF = 1, K_TRS = 2, K_RES = 3, K_IPM = 4, K_KKT = 5 };
 constexpr int FSTRIDE = 352, V16 = 16, V32 = 32, BS = 4, NCL = 2;
 
 struct StageInfoH {  // mirror of hk::StageInfo
-    int nu, nx, nb, ng, xo, nx1, nu1, xo1, sdB, sdR, oB, oR, oD, pnb, r0, r1;
+    int nu, nx, nb, ng, xo, nx1, nu1, xo1, sdB, sdR, oB, oR, oD, pnb, r0, oG;
 };
 
 inline int rup(int n, int m) { return (n + m - 1) / m * m; }
@@ -69,7 +69,10 @@ struct hpmpc_mi355x_plan {
     signed char *d_tileslot = nullptr, *d_slotvar = nullptr;
     std::vector<long long> dev_offB, dev_offR;  // offsets currently uploaded into d_st
     int fixcls = 0;                             // compiled inner-stage class (kernel instance)
-    int nbt = 0;                                // sum of nb
+    int nbt = 0;                                // sum of nb + ng
+    int ngt = 0;                                // sum of ng
+    std::vector<long long> offG;                // DCt_k offsets (packed), per stage
+    long long packG = 0;
 };
 
 namespace {
@@ -78,8 +81,8 @@ bool plan_supported(int N, const int* nx, const int* nu, const int* nb, const in
                     const char** why) {
     for (int k = 0; k <= N; k++) {
         const int u = k < N ? nu[k] : 0;
-        if (ng[k] != 0) {
-            *why = "general constraints (ng > 0) are not supported on the GPU path";
+        if (ng[k] < 0 || rup(nb[k], 4) + rup(ng[k], 4) > 16) {
+            *why = "round_up(nb[k],4) + round_up(ng[k],4) must be <= 16 (one 32-slot constraint vector per stage)";
             return false;
         }
         if (u < 0 || nx[k] < 0 || u + nx[k] > 16 || rup(u, 4) + nx[k] > 16) {
@@ -149,12 +152,13 @@ extern "C" hpmpc_mi355x_plan* hpmpc_mi355x_plan_create(int N, const int* nx, con
     P->slotvar.assign((N + 1) * 16, 0);
     P->offB.resize(N);
     P->offR.resize(N + 1);
+    P->offG.resize(N + 1);
     for (int k = 0; k <= N; k++) {
         StageInfoH& s = P->st[k];
         s.nu = P->nu[k];
         s.nx = nx[k];
         s.nb = nb[k];
-        s.ng = 0;
+        s.ng = ng[k];
         s.xo = rup(s.nu, 4);
         s.nx1 = k < N ? nx[k + 1] : 0;
         s.nu1 = k + 1 < N ? P->nu[k + 1] : 0;
@@ -163,7 +167,12 @@ extern "C" hpmpc_mi355x_plan* hpmpc_mi355x_plan_create(int N, const int* nx, con
         s.sdR = rup(s.nu + s.nx, NCL);
         s.pnb = rup(nb[k], BS);
         s.oD = k * V32;
-        s.r0 = s.r1 = 0;
+        s.r0 = 0;
+        s.oG = (int)P->packG;
+        P->offG[k] = P->packG;
+        if (ng[k] > 0) P->packG += (long long)rup(s.nu + s.nx, BS) * rup(ng[k], NCL);
+        P->nbt += ng[k];
+        P->ngt += ng[k];
         const int nux = s.nu + s.nx;
         if (k < N) {
             P->offB[k] = P->packB;
@@ -186,7 +195,10 @@ extern "C" hpmpc_mi355x_plan* hpmpc_mi355x_plan_create(int N, const int* nx, con
         P->fixcls = hk_fixcls(nuc, nxc);
         if (P->fixcls)
             for (int k = 1; k <= N - 2; k++)
-                P->st[k].r0 = (P->nu[k] == nuc && nx[k] == nxc && P->nu[k + 1] == nuc && nx[k + 1] == nxc) ? 1 : 0;
+                P->st[k].r0 = (P->nu[k] == nuc && nx[k] == nxc && P->nu[k + 1] == nuc && nx[k + 1] == nxc &&
+                               ng[k] == 0)
+                                  ? 1
+                                  : 0;
     }
     bool ok = hip_ok(hipMalloc(&P->d_st, sizeof(StageInfoH) * (N + 1)), "plan alloc") &&
               hip_ok(hipMalloc((void**)&P->d_tileslot, (N + 1) * 16), "plan alloc") &&
@@ -238,11 +250,18 @@ KArgs base_args(const hpmpc_mi355x_plan* P, int nprob, int p0) {
     a.sW = ws_doubles(P->N);
     a.fixcls = P->fixcls;
     a.nbt = P->nbt;
+    a.ngt = P->ngt;
+    a.sG = P->packG;
     a.dbg = g_dbg_buf;
     return a;
 }
 
 bool layout_apply(hpmpc_mi355x_plan* P, const hpmpc_mi355x_layout* lay, KArgs& a) {
+    if (P->ngt) {  // the batched entry points carry no DCt array
+        set_err(HPMPC_MI355X_EUNSUPPORTED, "batched entry points: general constraints (ng > 0) need the "
+                                           "reference-named entry points");
+        return false;
+    }
     if (lay && lay->BAbt_off && lay->RSQrq_off) {
         if (!plan_upload_stages(P, lay->BAbt_off, lay->RSQrq_off)) return false;
     } else if (!plan_upload_stages(P, P->offB.data(), P->offR.data())) {
@@ -590,7 +609,7 @@ thread_local Ctx g_ctx;
 
 // Arena carve (doubles) for one problem.
 struct Arena {
-    size_t BAbt, RSQ, d, ux, pi, lam, t, ws, vb, vq, vQx, vqx, vPb, stat, ints, total;
+    size_t BAbt, RSQ, DCt, d, ux, pi, lam, t, ws, vb, vq, vQx, vqx, vPb, stat, ints, total;
 };
 
 Arena arena(const hpmpc_mi355x_plan* P, int k_max) {
@@ -604,6 +623,7 @@ Arena arena(const hpmpc_mi355x_plan* P, int k_max) {
     const size_t n1 = P->N + 1;
     A.BAbt = take(P->packB);
     A.RSQ = take(P->packR);
+    A.DCt = take(P->packG > 0 ? P->packG : 1);
     A.d = take(n1 * V32);
     A.ux = take(n1 * V16);
     A.pi = take(n1 * V16);
@@ -627,6 +647,7 @@ KArgs arena_args(const hpmpc_mi355x_plan* P, const Arena& A, double* dev) {
     a.sR = P->packR;
     a.BAbt = dev + A.BAbt;
     a.RSQ = dev + A.RSQ;
+    a.DCt = P->ngt ? dev + A.DCt : nullptr;
     a.d = dev + A.d;
     a.ux = dev + A.ux;
     a.pi = dev + A.pi;
@@ -660,11 +681,25 @@ void stage_RSQ(const hpmpc_mi355x_plan* P, double* H, const Arena& A, double** h
         memcpy(H + A.RSQ + P->offR[k], hpQ[k], n * sizeof(double));
     }
 }
+// constraint vectors per stage: [lb (pnb) | ub (pnb) | lg (png) | ug (png)]
+int cvec_len(const hpmpc_mi355x_plan* P, int k) { return 2 * P->st[k].pnb + 2 * rup(P->ng[k], BS); }
 void stage_d(const hpmpc_mi355x_plan* P, double* H, const Arena& A, double** d) {
+    for (int k = 0; k <= P->N; k++)
+        if (P->nb[k] + P->ng[k] > 0) memcpy(H + A.d + k * V32, d[k], cvec_len(P, k) * sizeof(double));
+}
+void stage_DCt(const hpmpc_mi355x_plan* P, double* H, const Arena& A, double** hpDCt) {
     for (int k = 0; k <= P->N; k++) {
-        const int pnb = P->st[k].pnb;
-        if (P->nb[k] > 0) memcpy(H + A.d + k * V32, d[k], 2 * pnb * sizeof(double));
+        if (P->ng[k] == 0) continue;
+        const auto& s = P->st[k];
+        memcpy(H + A.DCt + P->offG[k], hpDCt[k],
+               (size_t)rup(s.nu + s.nx, BS) * rup(P->ng[k], NCL) * sizeof(double));
     }
+}
+// Qx / qx of the general constraints ([box (pnb) | general (png)]): the box halves are applied on the
+// host for sv / trf, so the device sees zeros there and only adds the general terms.
+void stage_gen_q(const hpmpc_mi355x_plan* P, double* H, size_t off, double** v) {
+    for (int k = 0; k <= P->N; k++)
+        for (int l = 0; l < P->ng[k]; l++) H[off + k * V16 + P->st[k].pnb + l] = v[k][P->st[k].pnb + l];
 }
 
 bool run(int which, const KArgs& a, const char* name) {
@@ -714,7 +749,6 @@ extern "C" void d_back_ric_rec_sv_tv_res(int N, int* nx, int* nu, int* nb, int**
                                          double** bd, double** hpDCt, double** Qx, double** qx, double** hux,
                                          int compute_pi, double** hpi, int compute_Pb, double** hPb, double* memory,
                                          double* work) {
-    (void)hpDCt;
     (void)work;
     g_err = 0;
     hpmpc_mi355x_plan* P = g_ctx.get_plan(N, nx, nu, nb, idxb, ng);
@@ -744,6 +778,12 @@ extern "C" void d_back_ric_rec_sv_tv_res(int N, int* nx, int* nu, int* nb, int**
     KArgs a = arena_args(P, A, g_ctx.dev);
     a.compute_pi = compute_pi;
     a.compute_Pb = compute_Pb;
+    if (P->ngt) {  // general constraints: DCt diag(Qx_g) DCt' and DCt qx_g on the device
+        stage_DCt(P, H, A, hpDCt);
+        stage_gen_q(P, H, A.vQx, Qx);
+        stage_gen_q(P, H, A.vqx, qx);
+        a.use_box = 1;
+    }
     if (!up(A) || !run(K_SV, a, "hk_ric_sv") || !down(A)) return;
     for (int k = 0; k <= N; k++) {
         const int nux = P->st[k].nu + P->st[k].nx;
@@ -757,7 +797,6 @@ extern "C" void d_back_ric_rec_sv_tv_res(int N, int* nx, int* nu, int* nb, int**
 extern "C" void d_back_ric_rec_trf_tv_res(int N, int* nx, int* nu, int* nb, int** idxb, int* ng, double** hpBAbt,
                                           double** hpQ, double** hpDCt, double** Qx, double** bd, double* memory,
                                           double* work) {
-    (void)hpDCt;
     (void)work;
     g_err = 0;
     hpmpc_mi355x_plan* P = g_ctx.get_plan(N, nx, nu, nb, idxb, ng);
@@ -776,6 +815,11 @@ extern "C" void d_back_ric_rec_trf_tv_res(int N, int* nx, int* nu, int* nb, int*
         if (k < N) memcpy(H + A.BAbt + P->offB[k], hpBAbt[k], (size_t)rup(nux + 1, BS) * s.sdB * sizeof(double));
     }
     KArgs a = arena_args(P, A, g_ctx.dev);
+    if (P->ngt) {
+        stage_DCt(P, H, A, hpDCt);
+        stage_gen_q(P, H, A.vQx, Qx);
+        a.use_box = 1;
+    }
     if (!up(A) || !run(K_TRF, a, "hk_ric_trf") || !down(A)) return;
     memcpy(memory, H + A.ws, (size_t)(N + 1) * FSTRIDE * sizeof(double));
 }
@@ -784,7 +828,6 @@ extern "C" void d_back_ric_rec_trs_tv_res(int N, int* nx, int* nu, int* nb, int*
                                           double** hb, double** hq, double** hpDCt, double** qx, double** hux,
                                           int compute_pi, double** hpi, int compute_Pb, double** hPb, double* memory,
                                           double* work) {
-    (void)hpDCt;
     (void)work;
     g_err = 0;
     hpmpc_mi355x_plan* P = g_ctx.get_plan(N, nx, nu, nb, idxb, ng);
@@ -800,6 +843,10 @@ extern "C" void d_back_ric_rec_trs_tv_res(int N, int* nx, int* nu, int* nb, int*
         if (k < N) memcpy(H + A.vb + k * V16, hb[k], nx[k + 1] * sizeof(double));
         if (k < N && !compute_Pb) memcpy(H + A.vPb + k * V16, hPb[k], nx[k + 1] * sizeof(double));
         if (nb[k] > 0) memcpy(H + A.vqx + k * V16, qx[k], nb[k] * sizeof(double));
+    }
+    if (P->ngt) {
+        stage_DCt(P, H, A, hpDCt);
+        stage_gen_q(P, H, A.vqx, qx);
     }
     KArgs a = arena_args(P, A, g_ctx.dev);
     a.use_box = 1;
@@ -828,17 +875,22 @@ namespace {
 // hold the start iterate (lam0/t0 as [lower(nb) | upper(nb)], d_aux_ip_hard_lib4.c:153-213).
 int ipm_entry(int single_newton, int* kk, int k_max, double mu0, double mu_tol, double alpha_min, int warm_start,
               double* stat, int N, int* nx, int* nu_N, int* nb, int** idxb, int* ng, double** pBAbt, double** pQ,
-              double** d, double** ux, int compute_mult, double** pi, double** lam, double** t,
+              double** pDCt, double** d, double** ux, int compute_mult, double** pi, double** lam, double** t,
               double* double_work_memory, double** ux0, double** pi0, double** lam0, double** t0) {
     g_err = 0;
     hpmpc_mi355x_plan* P = g_ctx.get_plan(N, nx, nu_N, nb, idxb, ng);
     if (!P) return g_err;
+    if (single_newton && P->ngt) {  // the reference stops here too (d_aux_ip_hard_lib4.c:197-208)
+        set_err(HPMPC_MI355X_EUNSUPPORTED, "single Newton step with general constraints");
+        return g_err;
+    }
     Arena A = arena(P, k_max);
     if (!g_ctx.ensure(A.total)) return g_err;
     double* H = g_ctx.host;
     stage_BAbt(P, H, A, pBAbt);
     stage_RSQ(P, H, A, pQ);
     stage_d(P, H, A, d);
+    stage_DCt(P, H, A, pDCt);
     if (single_newton) {
         for (int k = 0; k <= N; k++) {
             memcpy(H + A.ux + k * V16, ux0[k], (P->st[k].nu + nx[k]) * sizeof(double));
@@ -869,10 +921,9 @@ int ipm_entry(int single_newton, int* kk, int k_max, double mu0, double mu_tol, 
     for (int k = 0; k <= N; k++) {
         memcpy(ux[k], H + A.ux + k * V16, (P->st[k].nu + nx[k]) * sizeof(double));
         if (k < N) memcpy(pi[k], H + A.pi + k * V16, nx[k + 1] * sizeof(double));
-        const int pnb = P->st[k].pnb;
-        if (nb[k] > 0) {
-            memcpy(lam[k], H + A.lam + k * V32, 2 * pnb * sizeof(double));
-            memcpy(t[k], H + A.t + k * V32, 2 * pnb * sizeof(double));
+        if (nb[k] + ng[k] > 0) {
+            memcpy(lam[k], H + A.lam + k * V32, cvec_len(P, k) * sizeof(double));
+            memcpy(t[k], H + A.t + k * V32, cvec_len(P, k) * sizeof(double));
         }
     }
     memcpy(double_work_memory, H + A.ws, ws_doubles(N) * sizeof(double));
@@ -886,9 +937,8 @@ extern "C" int d_ip2_res_mpc_hard_tv(int* kk, int k_max, double mu0, double mu_t
                                      double** pBAbt, double** pQ, double** pDCt, double** d, double** ux,
                                      int compute_mult, double** pi, double** lam, double** t,
                                      double* double_work_memory) {
-    (void)pDCt;
-    return ipm_entry(0, kk, k_max, mu0, mu_tol, alpha_min, warm_start, stat, N, nx, nu_N, nb, idxb, ng, pBAbt, pQ, d,
-                     ux, compute_mult, pi, lam, t, double_work_memory, nullptr, nullptr, nullptr, nullptr);
+    return ipm_entry(0, kk, k_max, mu0, mu_tol, alpha_min, warm_start, stat, N, nx, nu_N, nb, idxb, ng, pBAbt, pQ,
+                     pDCt, d, ux, compute_mult, pi, lam, t, double_work_memory, nullptr, nullptr, nullptr, nullptr);
 }
 
 extern "C" int d_ip2_res_mpc_hard_tv_single_newton_step(int* kk, int k_max, double mu0, double mu_tol,
@@ -898,9 +948,8 @@ extern "C" int d_ip2_res_mpc_hard_tv_single_newton_step(int* kk, int k_max, doub
                                                         double** ux, int compute_mult, double** pi, double** lam,
                                                         double** t, double* double_work_memory, double** ux0,
                                                         double** pi0, double** lam0, double** t0) {
-    (void)pDCt;
-    return ipm_entry(1, kk, k_max, mu0, mu_tol, alpha_min, warm_start, stat, N, nx, nu_N, nb, idxb, ng, pBAbt, pQ, d,
-                     ux, compute_mult, pi, lam, t, double_work_memory, ux0, pi0, lam0, t0);
+    return ipm_entry(1, kk, k_max, mu0, mu_tol, alpha_min, warm_start, stat, N, nx, nu_N, nb, idxb, ng, pBAbt, pQ,
+                     pDCt, d, ux, compute_mult, pi, lam, t, double_work_memory, ux0, pi0, lam0, t0);
 }
 
 extern "C" void d_kkt_solve_new_rhs_res_mpc_hard_tv(int N, int* nx, int* nu_N, int* nb, int** idxb, int* ng,
@@ -908,7 +957,6 @@ extern "C" void d_kkt_solve_new_rhs_res_mpc_hard_tv(int N, int* nx, int* nu_N, i
                                                     double** pDCt, double** d, double** ux, int compute_mult,
                                                     double** pi, double** lam, double** t,
                                                     double* double_work_memory) {
-    (void)pDCt;
     g_err = 0;
     hpmpc_mi355x_plan* P = g_ctx.get_plan(N, nx, nu_N, nb, idxb, ng);
     if (!P) return;
@@ -918,6 +966,7 @@ extern "C" void d_kkt_solve_new_rhs_res_mpc_hard_tv(int N, int* nx, int* nu_N, i
     stage_BAbt(P, H, A, pBAbt);
     stage_RSQ(P, H, A, pQ);
     stage_d(P, H, A, d);
+    stage_DCt(P, H, A, pDCt);
     memcpy(H + A.ws, double_work_memory, ws_doubles(N) * sizeof(double));
     for (int k = 0; k <= N; k++) {
         memcpy(H + A.vq + k * V16, q[k], (P->st[k].nu + nx[k]) * sizeof(double));
@@ -929,10 +978,9 @@ extern "C" void d_kkt_solve_new_rhs_res_mpc_hard_tv(int N, int* nx, int* nu_N, i
     for (int k = 0; k <= N; k++) {
         memcpy(ux[k], H + A.ux + k * V16, (P->st[k].nu + nx[k]) * sizeof(double));
         if (k < N) memcpy(pi[k], H + A.pi + k * V16, nx[k + 1] * sizeof(double));
-        const int pnb = P->st[k].pnb;
-        if (nb[k] > 0) {
-            memcpy(lam[k], H + A.lam + k * V32, 2 * pnb * sizeof(double));
-            memcpy(t[k], H + A.t + k * V32, 2 * pnb * sizeof(double));
+        if (nb[k] + ng[k] > 0) {
+            memcpy(lam[k], H + A.lam + k * V32, cvec_len(P, k) * sizeof(double));
+            memcpy(t[k], H + A.t + k * V32, cvec_len(P, k) * sizeof(double));
         }
     }
 }
@@ -941,7 +989,6 @@ extern "C" void d_res_res_mpc_hard_tv(int N, int* nx, int* nu, int* nb, int** id
                                       double** hb, double** hpQ, double** hq, double** hux, double** hpDCt,
                                       double** hd, double** hpi, double** hlam, double** ht, double* work,
                                       double** hrq, double** hrb, double** hrd, double** hrm, double* mu) {
-    (void)hpDCt;
     (void)work;
     g_err = 0;
     hpmpc_mi355x_plan* P = g_ctx.get_plan(N, nx, nu, nb, idxb, ng);
@@ -952,6 +999,7 @@ extern "C" void d_res_res_mpc_hard_tv(int N, int* nx, int* nu, int* nb, int** id
     stage_BAbt(P, H, A, hpBAbt);
     stage_RSQ(P, H, A, hpQ);
     stage_d(P, H, A, hd);
+    stage_DCt(P, H, A, hpDCt);
     for (int k = 0; k <= N; k++) {
         const int nux = P->st[k].nu + nx[k];
         memcpy(H + A.vq + k * V16, hq[k], nux * sizeof(double));
@@ -960,10 +1008,9 @@ extern "C" void d_res_res_mpc_hard_tv(int N, int* nx, int* nu, int* nb, int** id
             memcpy(H + A.vb + k * V16, hb[k], nx[k + 1] * sizeof(double));
             memcpy(H + A.pi + k * V16, hpi[k], nx[k + 1] * sizeof(double));
         }
-        const int pnb = P->st[k].pnb;
-        if (nb[k] > 0) {
-            memcpy(H + A.lam + k * V32, hlam[k], 2 * pnb * sizeof(double));
-            memcpy(H + A.t + k * V32, ht[k], 2 * pnb * sizeof(double));
+        if (nb[k] + ng[k] > 0) {
+            memcpy(H + A.lam + k * V32, hlam[k], cvec_len(P, k) * sizeof(double));
+            memcpy(H + A.t + k * V32, ht[k], cvec_len(P, k) * sizeof(double));
         }
     }
     KArgs a = arena_args(P, A, g_ctx.dev);
@@ -978,10 +1025,9 @@ extern "C" void d_res_res_mpc_hard_tv(int N, int* nx, int* nu, int* nb, int** id
         const int nux = P->st[k].nu + nx[k];
         memcpy(hrq[k], rq + k * V16, nux * sizeof(double));
         if (k < N) memcpy(hrb[k], rb + k * V16, nx[k + 1] * sizeof(double));
-        const int pnb = P->st[k].pnb;
-        if (nb[k] > 0) {
-            memcpy(hrd[k], rd + k * V32, 2 * pnb * sizeof(double));
-            memcpy(hrm[k], rm + k * V32, 2 * pnb * sizeof(double));
+        if (nb[k] + ng[k] > 0) {
+            memcpy(hrd[k], rd + k * V32, cvec_len(P, k) * sizeof(double));
+            memcpy(hrm[k], rm + k * V32, cvec_len(P, k) * sizeof(double));
         }
     }
     *mu = H[A.ints + 2];

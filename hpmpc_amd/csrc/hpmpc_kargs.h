@@ -5,7 +5,8 @@
 
 struct KArgs {
     int N, nprob, p0;             // horizon, problems in the batch, first problem of this launch
-    int nbt;                      // sum of nb over the stages
+    int nbt;                      // sum of nb + ng over the stages
+    int ngt;                      // sum of ng over the stages
     int fixcls;                   // compiled inner-stage class of the plan (0: generic kernels)
     const void* st;               // hk::StageInfo[N+1]
     const signed char* tileslot;  // (N+1)*16
@@ -14,7 +15,9 @@ struct KArgs {
     long long sB;
     const double* RSQ;
     long long sR;
-    const double* d;  // bounds, V32 per stage: [lb (pnb) | ub (pnb)]
+    const double* d;  // bounds, V32 per stage: [lb (pnb) | ub (pnb) | lg (png) | ug (png)]
+    const double* DCt;  // general constraints D_k' (lib4 nux x ng per stage, offsets in the stage table)
+    long long sG;
     double* ws;       // per-problem workspace / factor memory
     long long sW;
     double *ux, *pi;  // V16 per stage (variable order / state order)

@@ -12,7 +12,10 @@ using namespace hk;
 
 // IPM pass kernels fit two waves per SIMD (<= 256 VGPRs), so a problem queue with two slots per SIMD
 // interleaves two problems' dependency chains.
-#define HK_TWO_WAVES __attribute__((amdgpu_waves_per_eu(2)))
+#ifndef HK_WAVES
+#define HK_WAVES 2
+#endif
+#define HK_TWO_WAVES __attribute__((amdgpu_waves_per_eu(HK_WAVES)))
 
 namespace {
 
@@ -97,6 +100,7 @@ __device__ __forceinline__ RicIO make_io(const KArgs& a, const LdsTabs& T, int p
     io.BAbt = a.BAbt + (long)p * a.sB;
     io.RSQ = a.RSQ + (long)p * a.sR;
     io.F = F;
+    io.DCt = a.DCt ? a.DCt + (long)p * a.sG : a.RSQ;  // never read when every ng = 0
     return io;
 }
 
@@ -255,6 +259,36 @@ __device__ void init_var(const RicIO& io, const double* dv, double* ux, double* 
             gst(t, up[j], tu, bx[j]);
             gst(lam, lo[j], mu0 / tl, bx[j]);
             gst(lam, up[j], mu0 / tu, bx[j]);
+        }
+    }
+}
+
+// General-constraint part of d_init_var_mpc_hard_tv (d_aux_ip_hard_lib4.c:131-149): slacks from D ux of
+// the (box-adjusted) start point, clipped at thr0.  Call after init_var's stores are visible.
+__device__ void init_var_gen(const RicIO& io, const double* dv, const double* ux, double* lam, double* t,
+                             double mu0) {
+    const int l = lane_id(), c = l & 15;
+    const double thr0 = 0.1;
+    for (int k = 0; k <= io.N; k++) {
+        const StageInfo si = load_stage(io.st, k);
+        if (si.ng == 0) continue;
+        const DynSh sh(si);
+        const int vc = tile_var(c, sh.nu, sh.nx, sh.xo);
+        const double x = gld(ux, k * V16 + vc, vc >= 0);
+        double dg[4];
+        gen_dg(io, sh, dg);
+#pragma unroll
+        for (int lc = 0; lc < 4; lc++) {
+            if (4 * lc >= sh.ng) continue;
+            const GenLane q = gen_lane(k, sh.pnb, sh.ng, lc);
+            const bool st = q.ok && c == 0;
+            const double dx = row_sum16(dg[lc] * x);
+            const double tl = fmax(thr0, dx + (-gld(dv, q.lo, q.ok)));
+            const double tu = fmax(thr0, -dx + gld(dv, q.up, q.ok));
+            gst(t, q.lo, tl, st);
+            gst(t, q.up, tu, st);
+            gst(lam, q.lo, mu0 / tl, st);
+            gst(lam, q.up, mu0 / tu, st);
         }
     }
 }
@@ -430,6 +464,10 @@ __device__ bool ipm_start(const KArgs& a, const LdsTabs& T, IpmView& v) {
     const bool sn = a.single_newton != 0;
     if (!sn) {
         init_var<7>(v.io, v.dv, v.ux, v.pi, v.w.dpi, v.lam, v.t, a.mu0, a.warm_start);
+        if (a.ngt) {
+            wsync();
+            init_var_gen(v.io, v.dv, v.ux, v.lam, v.t, a.mu0);
+        }
     } else {
         for (int i = l; i < (N + 1) * V16; i += 64) v.w.dpi[i] = 0.0;
     }
@@ -638,6 +676,10 @@ __global__ __launch_bounds__(64) void hk_kkt_new_rhs(KArgs a) {
         w.qx[k * V16 + slot] = w.t_inv[lo] * (w.res_m[lo] - lam[lo] * w.res_d[lo]) -
                                w.t_inv[up] * (w.res_m[up] + lam[up] * w.res_d[up]);
     });
+    HK_FOR_GEN(io, k, {
+        w.qx[s16] = w.t_inv[lo] * (w.res_m[lo] - lam[lo] * w.res_d[lo]) -
+                    w.t_inv[up] * (w.res_m[up] + lam[up] * w.res_d[up]);
+    });
     wsync();
     double al = 1.0;
     ric_trs<BX_GIVEN, BX_NONE, FX>(io, &sm, w.res_b, w.res_q, bc, w.dux, a.compute_mult, w.dpi, 1, w.Pb, al);
@@ -653,6 +695,16 @@ __global__ __launch_bounds__(64) void hk_kkt_new_rhs(KArgs a) {
         w.dlam[lo] = dll;
         w.dlam[up] = dlu;
     });
+    if (a.ngt) {  // the general slots: the same update from D dux (gen_alpha's phase-2 branch)
+        for (int k = 0; k <= N; k++) {
+            const StageInfo si = load_stage(io.st, k);
+            if (si.ng == 0) continue;
+            const DynSh sh(si);
+            const int vc = tile_var(l & 15, sh.nu, sh.nx, sh.xo);
+            double dummy = 1.0;
+            gen_alpha<BX_P2>(io, sh, k, bc, gld(w.dux, k * V16 + vc, vc >= 0), dummy);
+        }
+    }
     wsync();
     for (int k = 0; k <= N; k++) {
         const StageInfo si = load_stage(io.st, k);
@@ -660,6 +712,12 @@ __global__ __launch_bounds__(64) void hk_kkt_new_rhs(KArgs a) {
         if (k < N && l < si.nx1) pi[k * V16 + l] += 1.0 * w.dpi[k * V16 + l];
     }
     HK_FOR_BOX(io, k, {
+        lam[lo] += 1.0 * w.dlam[lo];
+        lam[up] += 1.0 * w.dlam[up];
+        t[lo] += 1.0 * w.dt[lo];
+        t[up] += 1.0 * w.dt[up];
+    });
+    HK_FOR_GEN(io, k, {
         lam[lo] += 1.0 * w.dlam[lo];
         lam[up] += 1.0 * w.dlam[up];
         t[lo] += 1.0 * w.dt[lo];

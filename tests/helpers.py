@@ -101,10 +101,11 @@ def check_case(case, got):
         assert e <= t, f"{case.name}: {key} err {e:.3e} > {t:.0e}"
 
 
-def random_qp(N, nx, nu, nb=None, seed=0, box=1.0):
+def random_qp(N, nx, nu, nb=None, seed=0, box=1.0, ng=None):
     """Random well-posed OCP QP with per-stage sizes (lists of length N+1; nu[N] is forced to 0),
     random box subsets idxb (any variable order), SPD stage Hessians.  Exercises size patterns the
-    mass-spring workload does not (odd sizes, nu > nx, varying stage sizes, x-only boxes)."""
+    mass-spring workload does not (odd sizes, nu > nx, varying stage sizes, x-only boxes).
+    ng: general constraints per stage, lg <= D ux <= ug with a random dense D (0 strictly feasible)."""
     from hpmpc_amd.ocp import OCPQP, pack_lib4, rup
 
     rng = np.random.default_rng(seed)
@@ -113,7 +114,8 @@ def random_qp(N, nx, nu, nb=None, seed=0, box=1.0):
     nu[N] = 0
     nx[0] = 0 if nx[0] == 0 else nx[0]
     nb = np.zeros(N + 1, dtype=np.int32) if nb is None else np.asarray(nb, dtype=np.int32)
-    BAbt, RSQrq, d, idxb = [], [], [], []
+    ngv = np.zeros(N + 1, dtype=np.int32) if ng is None else np.asarray(ng, dtype=np.int32)
+    BAbt, RSQrq, d, idxb, DCt = [], [], [], [], []
     for k in range(N + 1):
         nuk, nxk = int(nu[k]), int(nx[k])
         nux = nuk + nxk
@@ -133,11 +135,22 @@ def random_qp(N, nx, nu, nb=None, seed=0, box=1.0):
         ib = np.sort(rng.choice(nux, size=nbk, replace=False)).astype(np.int32) if nbk else np.zeros(0, np.int32)
         idxb.append(ib)
         pnb = rup(nbk, 4)
-        dk = np.zeros(max(2 * pnb, 1))
+        ngk = int(ngv[k])
+        png = rup(ngk, 4)
+        dk = np.zeros(max(2 * pnb + 2 * png, 1))
         dk[:nbk] = -box * (0.5 + rng.random(nbk))
         dk[pnb:pnb + nbk] = box * (0.5 + rng.random(nbk))
+        if ngk:
+            D = rng.standard_normal((ngk, nux)) / np.sqrt(max(nux, 1))
+            DCt.append(pack_lib4(D.T.copy()))
+            dk[2 * pnb:2 * pnb + ngk] = -box * (0.5 + rng.random(ngk))
+            dk[2 * pnb + png:2 * pnb + png + ngk] = box * (0.5 + rng.random(ngk))
+        else:
+            DCt.append(np.zeros(8))
         d.append(dk)
-    return OCPQP(N, nx, nu, nb, np.zeros(N + 1, dtype=np.int32), idxb, BAbt, RSQrq, d, [], None)
+    if not ngv.any():
+        DCt = []
+    return OCPQP(N, nx, nu, nb, ngv, idxb, BAbt, RSQrq, d, DCt, None)
 
 
 def compare_ipm(case_like_qp, a, b, tol=TOL_IPM):
@@ -158,8 +171,8 @@ def compare_ipm(case_like_qp, a, b, tol=TOL_IPM):
             m = int(qp.nx[k + 1])
             e = max(e, float(np.max(np.abs(a["pi"][k][:m] - b["pi"][k][:m]) / np.maximum(1, np.abs(b["pi"][k][:m])),
                                     initial=0)))
-        nbk, pnb = int(qp.nb[k]), qp.pnb(k)
-        idx = np.r_[0:nbk, pnb:pnb + nbk].astype(int)
+        nbk, pnb, ngk, png = int(qp.nb[k]), qp.pnb(k), int(qp.ng[k]), qp.png(k)
+        idx = np.r_[0:nbk, pnb:pnb + nbk, 2 * pnb:2 * pnb + ngk, 2 * pnb + png:2 * pnb + png + ngk].astype(int)
         for key in ("lam", "t"):
             g, r = a[key][k][idx], b[key][k][idx]
             e = max(e, float(np.max(np.abs(g - r) / np.maximum(1, np.abs(r)), initial=0)))

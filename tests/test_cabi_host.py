@@ -88,18 +88,23 @@ def test_plan_rejects_unsupported_sizes(hiplib):
         assert L.hpmpc_mi355x_last_error() == EUNSUPPORTED
 
 
-def test_reference_entry_rejects_general_constraints(hiplib):
-    """ng > 0 is outside the GPU path: the IPM returns EUNSUPPORTED, no fallback."""
-    from hpmpc_amd.cabi import HpmpcAPI
-
-    api = HpmpcAPI(hiplib, "")
-    qp = mass_spring_qp(6, 4, 1)
-    qp.ng = np.array([0] * 6 + [4], dtype=np.int32)
-    qp.DCt = [np.zeros(8)] * 6 + [pack_lib4(np.eye(4))]
-    qp.d[6] = np.concatenate([qp.d[6][:4], -np.ones(4), np.ones(4)])
-    r = api.ipm(qp, k_max=5)
-    assert r["ret"] == EUNSUPPORTED
-    assert hiplib.hpmpc_mi355x_last_error() == EUNSUPPORTED
+def test_plan_rejects_too_many_constraints(hiplib):
+    """Box and general constraints share one 32-slot vector per stage: round_up(nb,4) + round_up(ng,4)
+    <= 16, checked on the host before any device allocation."""
+    L = hiplib
+    L.hpmpc_mi355x_plan_create.restype = C.c_void_p
+    L.hpmpc_mi355x_plan_create.argtypes = [C.c_int] + [C.c_void_p] * 5
+    N = 3
+    nxv = np.array([0] + [12] * N, dtype=np.int32)
+    nuv = np.array([4] * N + [0], dtype=np.int32)
+    nbv = np.array([4, 10, 10, 6], dtype=np.int32)
+    ngv = np.array([0, 0, 8, 0], dtype=np.int32)  # stage 2: 12 + 8 > 16
+    idx_arrs = [np.arange(n, dtype=np.int32) for n in nbv]
+    idx = (C.POINTER(C.c_int) * (N + 1))(*[a.ctypes.data_as(C.POINTER(C.c_int)) for a in idx_arrs])
+    p = L.hpmpc_mi355x_plan_create(N, nxv.ctypes.data, nuv.ctypes.data, nbv.ctypes.data, C.cast(idx, C.c_void_p),
+                                   ngv.ctypes.data)
+    assert not p
+    assert L.hpmpc_mi355x_last_error() == EUNSUPPORTED
 
 
 def test_size_queries_are_host_only(hiplib):

@@ -1,4 +1,5 @@
 """Batch vs problem-queue throughput on the benchmark workload (diagnostic)."""
+import os
 import sys
 import time
 
@@ -19,7 +20,7 @@ torch.cuda.synchronize()
 tb = (time.perf_counter() - t0) / 3
 print(f"batch: {tb*1e3:.2f} ms/batch  {it_batch/tb/1e6:.3f} M IP-iter/s", flush=True)
 for steps in [int(x) for x in sys.argv[1:]] or [10]:
-    for slots in (1024, 2048):
+    for slots in [int(x) for x in os.environ.get("QP_SLOTS", "1024 2048").split()]:
         Q = s.queue(steps * 1024, slots)
         Q.run()
         torch.cuda.synchronize()
