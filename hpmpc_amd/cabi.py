@@ -47,12 +47,44 @@ def iv(a):
     return (C.c_int * len(a))(*a.tolist())
 
 
-class HpmpcAPI:
-    """Thin wrapper calling ``<prefix><reference symbol>`` of a loaded library on an OCPQP."""
+def _aligned_copy(a: np.ndarray, align: int = 64) -> np.ndarray:
+    buf = np.empty(a.size + align // 8, dtype=np.float64)
+    off = (-buf.ctypes.data % align) // 8
+    out = buf[off: off + a.size].reshape(a.shape)
+    out[...] = a
+    return out
 
-    def __init__(self, lib: C.CDLL, prefix: str = ""):
+
+class HpmpcAPI:
+    """Thin wrapper calling ``<prefix><reference symbol>`` of a loaded library on an OCPQP.
+
+    ``aligned=True`` hands the library 64-byte aligned copies of every double array (and copies them
+    back after the call): the reference's X64_AVX helpers use aligned 256-bit loads."""
+
+    def __init__(self, lib: C.CDLL, prefix: str = "", aligned: bool = False):
         self.lib = lib
         self.p = prefix
+        self.aligned = aligned
+        self._copies = []
+
+    def _pp(self, arrs):
+        if not self.aligned:
+            return dpp(arrs)
+        cps = [_aligned_copy(a) for a in arrs]
+        self._copies += list(zip(arrs, cps))
+        return dpp(cps)
+
+    def _p(self, a):
+        if not self.aligned:
+            return _dptr(a)
+        c = _aligned_copy(a)
+        self._copies.append((a, c))
+        return _dptr(c)
+
+    def _sync(self):
+        for a, c in self._copies:
+            a[...] = c
+        self._copies = []
 
     def fn(self, name: str):
         f = getattr(self.lib, self.p + name)
@@ -66,10 +98,10 @@ class HpmpcAPI:
         m = self.fn("d_back_ric_rec_sv_tv_memory_space_size_bytes")(*a)
         return w, m
 
-    def ipm_ws_size(self, qp: OCPQP):
+    def ipm_ws_size(self, qp: OCPQP, res=True):
         N = qp.N
-        return self.fn("d_ip2_res_mpc_hard_tv_work_space_size_bytes")(
-            C.c_int(N), iv(qp.nx), iv(qp.nu), iv(qp.nb), iv(qp.ng))
+        name = "d_ip2_res_mpc_hard_tv" if res else "d_ip2_mpc_hard_tv"
+        return self.fn(name + "_work_space_size_bytes")(C.c_int(N), iv(qp.nx), iv(qp.nu), iv(qp.nb), iv(qp.ng))
 
     # ---------------------------------------------------------------------------------------------
     def ric_sv(self, qp: OCPQP, *, update_b=0, b=None, update_q=0, q=None, bd=None, Qx=None, qx=None,
@@ -127,11 +159,12 @@ class HpmpcAPI:
 
     # ---------------------------------------------------------------------------------------------
     def ipm(self, qp: OCPQP, *, k_max=50, mu0=2.0, mu_tol=1e-12, alpha_min=1e-8, warm_start=0, compute_mult=1,
-            ux=None, work=None):
-        """d_ip2_res_mpc_hard_tv (mpc_solvers/d_ip2_res_hard.c:116).  Returns dict."""
+            ux=None, work=None, res=True):
+        """d_ip2_res_mpc_hard_tv (mpc_solvers/d_ip2_res_hard.c:116), or with res=False the alternate IPM
+        d_ip2_mpc_hard_tv (mpc_solvers/d_ip2_hard.c:88).  Returns dict."""
         N = qp.N
         nu_N = qp.nu.copy()
-        wsz = self.ipm_ws_size(qp)
+        wsz = self.ipm_ws_size(qp, res)
         work = np.zeros(wsz // 8 + 16) if work is None else work
         ux_, pi, lam, t = qp.alloc_solution()
         if ux is not None:
@@ -141,11 +174,12 @@ class HpmpcAPI:
         stat = np.zeros(5 * k_max + 5)
         kk = C.c_int(0)
         dct = qp.DCt if qp.DCt else [np.zeros(8)] * (N + 1)
-        ret = self.fn("d_ip2_res_mpc_hard_tv")(
+        ret = self.fn("d_ip2_res_mpc_hard_tv" if res else "d_ip2_mpc_hard_tv")(
             C.byref(kk), C.c_int(k_max), C.c_double(mu0), C.c_double(mu_tol), C.c_double(alpha_min),
-            C.c_int(warm_start), _dptr(stat), C.c_int(N), iv(qp.nx), iv(nu_N), iv(qp.nb), ipp(qp.idxb), iv(qp.ng),
-            dpp(qp.BAbt), dpp(qp.RSQrq), dpp(dct), dpp(qp.d), dpp(ux_), C.c_int(compute_mult), dpp(pi), dpp(lam),
-            dpp(t), _dptr(work))
+            C.c_int(warm_start), self._p(stat), C.c_int(N), iv(qp.nx), iv(nu_N), iv(qp.nb), ipp(qp.idxb),
+            iv(qp.ng), self._pp(qp.BAbt), self._pp(qp.RSQrq), self._pp(dct), self._pp(qp.d), self._pp(ux_),
+            C.c_int(compute_mult), self._pp(pi), self._pp(lam), self._pp(t), self._p(work))
+        self._sync()
         return dict(ret=ret, kk=kk.value, stat=stat[: 5 * kk.value].copy(), ux=ux_, pi=pi, lam=lam, t=t,
                     work=work)
 
@@ -215,6 +249,38 @@ class HpmpcAPI:
             dpp(qp.RSQrq), dpp(q), dpp(ux), dpp(dct), dpp(qp.d), dpp(pi), dpp(lam), dpp(t), _dptr(work), dpp(rq),
             dpp(rb), dpp(rd), dpp(rm), C.byref(mu))
         return dict(rq=rq, rb=rb, rd=rd, rm=rm, mu=mu.value)
+
+
+    def kkt_new_rhs_plain(self, qp: OCPQP, work, b, q, d, ux, compute_mult=1):
+        """d_kkt_solve_new_rhs_mpc_hard_tv (mpc_solvers/d_ip2_hard.c:626): re-solve with new b (r_A), q (r_H)
+        and bounds d (r_C), re-using ``work`` from ipm(res=False); ``ux`` holds the IPM solution (its
+        stage-0 state part is read when nx[0] > 0)."""
+        N = qp.N
+        ux_, pi, lam, t = qp.alloc_solution()
+        for k in range(N + 1):
+            n = min(len(ux_[k]), len(ux[k]))
+            ux_[k][:n] = ux[k][:n]
+        dct = qp.DCt if qp.DCt else [np.zeros(8)] * (N + 1)
+        self.fn("d_kkt_solve_new_rhs_mpc_hard_tv")(
+            C.c_int(N), iv(qp.nx), iv(qp.nu), iv(qp.nb), ipp(qp.idxb), iv(qp.ng), self._pp(qp.BAbt), self._pp(b),
+            self._pp(qp.RSQrq), self._pp(q), self._pp(dct), self._pp(d), self._pp(ux_), C.c_int(compute_mult),
+            self._pp(pi), self._pp(lam), self._pp(t), self._p(work))
+        self._sync()
+        return dict(ux=ux_, pi=pi, lam=lam, t=t)
+
+    def residuals_plain(self, qp: OCPQP, b, q, ux, pi, lam, t):
+        """d_res_mpc_hard_tv (mpc_solvers/d_res_ip_hard.c:38): r_q, r_b, r_d (no r_m) and mu."""
+        N = qp.N
+        rq = [np.zeros(rup(qp.nux(k) + 1, 4) + 4) for k in range(N + 1)]
+        rb = [np.zeros(rup(int(qp.nx[k + 1]), 4) + 4) for k in range(N)]
+        rd = [np.zeros(max(qp.nconstr(k), 1) + 4) for k in range(N + 1)]
+        mu = C.c_double(0.0)
+        dct = qp.DCt if qp.DCt else [np.zeros(8)] * (N + 1)
+        self.fn("d_res_mpc_hard_tv")(
+            C.c_int(N), iv(qp.nx), iv(qp.nu), iv(qp.nb), ipp(qp.idxb), iv(qp.ng), dpp(qp.BAbt), dpp(b),
+            dpp(qp.RSQrq), dpp(q), dpp(ux), dpp(dct), dpp(qp.d), dpp(pi), dpp(lam), dpp(t), dpp(rq), dpp(rb),
+            dpp(rd), C.byref(mu))
+        return dict(rq=rq, rb=rb, rd=rd, mu=mu.value)
 
 
 def bq_from_qp(qp: OCPQP):

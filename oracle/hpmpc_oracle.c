@@ -867,7 +867,7 @@ static void backup_iterate(int N, int *nx, int *nu, int *nb, int *ng, double **u
     ipws_t w_;                       \
     int nu_[(N) + 1];
 
-static int ipm_core(int single_newton, int *kk, int k_max, double mu0, double mu_tol, double alpha_min,
+static int ipm_core(int single_newton, int phase1_only, int *kk, int k_max, double mu0, double mu_tol, double alpha_min,
                     int warm_start, double *stat, int N, int *nx, int *nu_N, int *nb, int **idxb, int *ng,
                     double **pBAbt, double **pQ, double **pDCt, double **d, double **ux, int compute_mult,
                     double **pi, double **lam, double **t, double *double_work_memory, double **ux0, double **pi0,
@@ -882,6 +882,13 @@ static int ipm_core(int single_newton, int *kk, int k_max, double mu0, double mu
 
     double mu_scal = 0.0;
     for (int k = 0; k <= N; k++) mu_scal += 2 * nb[k] + 2 * ng[k];
+    if (mu_scal == 0.0 && phase1_only) {
+        /* d_ip2_hard.c:282-291: the sv solves into the workspace (dux, dpi); ux/pi/lam/t are untouched */
+        orc_d_back_ric_rec_sv_tv_res(N, nx, nu, nb, idxb, ng, 0, pBAbt, w->b, 0, pQ, w->q, NULL, NULL, NULL, NULL,
+                                     w->dux, compute_mult, w->dpi, 1, w->Pb, w->memory, w->work);
+        *kk = 0;
+        return 0;
+    }
     if (mu_scal == 0.0) {
         /* unconstrained: one sv and return (:428-450) */
         orc_d_back_ric_rec_sv_tv_res(N, nx, nu, nb, idxb, ng, 0, pBAbt, w->b, 0, pQ, w->q, NULL, NULL, NULL, NULL,
@@ -899,8 +906,9 @@ static int ipm_core(int single_newton, int *kk, int k_max, double mu0, double mu
 
     if (!single_newton) {
         init_var(N, nx, nu, nb, idxb, ng, ux, pi, pDCt, d, t, lam, mu0, warm_start);
-        /* phase 1: no residuals (:498-718) */
-        const double mu_tol_low = mu_tol < 1e-5 ? 1e-5 : mu_tol;
+        /* phase 1: no residuals (:498-718).  d_ip2_mpc_hard_tv (d_ip2_hard.c:329-520) is this loop alone, run
+         * to mu_tol itself */
+        const double mu_tol_low = phase1_only ? mu_tol : (mu_tol < 1e-5 ? 1e-5 : mu_tol);
         while (*kk < k_max && mu > mu_tol_low && alpha >= alpha_min) {
             update_hessian(N, nb, ng, d, 0.0, t, w->t_inv, lam, w->lamt, w->dlam, w->Qx, w->qx);
             orc_d_back_ric_rec_sv_tv_res(N, nx, nu, nb, idxb, ng, 0, pBAbt, w->b, 1, pQ, w->q, w->bd, pDCt, w->Qx,
@@ -928,6 +936,12 @@ static int ipm_core(int single_newton, int *kk, int k_max, double mu0, double mu
             (*kk)++;
         }
         restore_data(N, nx, nu, nb, idxb, pBAbt, pQ, w, 0);
+        if (phase1_only) { /* d_ip2_hard.c:604-612 */
+            if (mu <= mu_tol) return 0;
+            if (*kk >= k_max) return 1;
+            if (alpha < alpha_min) return 2;
+            return -1;
+        }
     } else {
         /* d_init_var_mpc_hard_tv_single_newton (d_aux_ip_hard_lib4.c:153-213) */
         for (int k = 0; k <= N; k++) {
@@ -1004,7 +1018,7 @@ int orc_d_ip2_res_mpc_hard_tv(int *kk, int k_max, double mu0, double mu_tol, dou
                               double *stat, int N, int *nx, int *nu_N, int *nb, int **idxb, int *ng, double **pBAbt,
                               double **pQ, double **pDCt, double **d, double **ux, int compute_mult, double **pi,
                               double **lam, double **t, double *double_work_memory) {
-    return ipm_core(0, kk, k_max, mu0, mu_tol, alpha_min, warm_start, stat, N, nx, nu_N, nb, idxb, ng, pBAbt, pQ,
+    return ipm_core(0, 0, kk, k_max, mu0, mu_tol, alpha_min, warm_start, stat, N, nx, nu_N, nb, idxb, ng, pBAbt, pQ,
                     pDCt, d, ux, compute_mult, pi, lam, t, double_work_memory, NULL, NULL, NULL, NULL);
 }
 
@@ -1014,7 +1028,7 @@ int orc_d_ip2_res_mpc_hard_tv_single_newton_step(int *kk, int k_max, double mu0,
                                                  double **d, double **ux, int compute_mult, double **pi,
                                                  double **lam, double **t, double *double_work_memory, double **ux0,
                                                  double **pi0, double **lam0, double **t0) {
-    return ipm_core(1, kk, k_max, mu0, mu_tol, alpha_min, warm_start, stat, N, nx, nu_N, nb, idxb, ng, pBAbt, pQ,
+    return ipm_core(1, 0, kk, k_max, mu0, mu_tol, alpha_min, warm_start, stat, N, nx, nu_N, nb, idxb, ng, pBAbt, pQ,
                     pDCt, d, ux, compute_mult, pi, lam, t, double_work_memory, ux0, pi0, lam0, t0);
 }
 
@@ -1050,4 +1064,152 @@ void orc_d_kkt_solve_new_rhs_res_mpc_hard_tv(int N, int *nx, int *nu_N, int *nb,
     dt_dlam_res(0, N, nx, nu, nb, idxb, ng, w->dux, t, w->t_inv, lam, pDCt, w->res_d, w->res_m, w->dt, w->dlam,
                 NULL);
     update_var_res(N, nx, nu, nb, ng, 1.0, NULL, ux, w->dux, NULL, pi, w->dpi, NULL, t, w->dt, NULL, lam, w->dlam);
+}
+
+/* ================================================================================================
+ * Alternate IPM (mpc_solvers/d_ip2_hard.c): the phase-1 Mehrotra loop alone, its KKT re-solve and
+ * the plain residuals of mpc_solvers/d_res_ip_hard.c.
+ * ============================================================================================== */
+int orc_d_ip2_mpc_hard_tv_work_space_size_bytes(int N, int *nx, int *nu, int *nb, int *ng) {
+    /* the oracle shares one private workspace carve between both IPMs (d_ip2_hard.c:31-87 sizes its own) */
+    return orc_d_ip2_res_mpc_hard_tv_work_space_size_bytes(N, nx, nu, nb, ng);
+}
+
+/* d_ip2_hard.c:88-614 */
+int orc_d_ip2_mpc_hard_tv(int *kk, int k_max, double mu0, double mu_tol, double alpha_min, int warm_start,
+                          double *stat, int N, int *nx, int *nu_N, int *nb, int **idxb, int *ng, double **pBAbt,
+                          double **pQ, double **pDCt, double **d, double **ux, int compute_mult, double **pi,
+                          double **lam, double **t, double *double_work_memory) {
+    return ipm_core(0, 1, kk, k_max, mu0, mu_tol, alpha_min, warm_start, stat, N, nx, nu_N, nb, idxb, ng, pBAbt, pQ,
+                    pDCt, d, ux, compute_mult, pi, lam, t, double_work_memory, NULL, NULL, NULL, NULL);
+}
+
+/* d_ip2_hard.c:626-825 as built for the reference's default target X64_AVX (Makefile.rule:38), where
+ * d_update_gradient_new_rhs_mpc_hard_tv takes (db, t_inv, lamt, qx) (avx/d_aux_ip_hard_lib4.c:1735-1838).
+ * lamt / the factor are those of the IPM's last iteration, left in the workspace. */
+void orc_d_kkt_solve_new_rhs_mpc_hard_tv(int N, int *nx, int *nu_N, int *nb, int **idxb, int *ng, double **pBAbt,
+                                         double **r_A, double **pQ, double **r_H, double **pDCt, double **r_C,
+                                         double **ux, int compute_mult, double **pi, double **lam, double **t,
+                                         double *double_work_memory) {
+    IPWS_DECL(N);
+    int *nu = nu_;
+    for (int k = 0; k < N; k++) nu[k] = nu_N[k];
+    nu[N] = 0;
+    ipws_t *w = &w_;
+    ipws_carve(N, nx, nu, nb, ng, double_work_memory, w, ptrs_);
+    /* d_update_gradient_new_rhs_mpc_hard_tv (avx/d_aux_ip_hard_lib4.c:1735-1838) */
+    for (int k = 0; k <= N; k++) {
+        cdim_t c = cdim(nb, ng, k);
+        for (int i = 0; i < c.nb; i++)
+            w->qx[k][i] = -w->lamt[k][c.pnb + i] * r_C[k][c.pnb + i] - w->lamt[k][i] * r_C[k][i];
+        const int o = 2 * c.pnb;
+        for (int i = 0; i < c.ng; i++)
+            w->qx[k][c.pnb + i] = -w->lamt[k][o + c.png + i] * r_C[k][o + c.png + i] - w->lamt[k][o + i] * r_C[k][o + i];
+    }
+    orc_d_back_ric_rec_trs_tv_res(N, nx, nu, nb, idxb, ng, pBAbt, r_A, r_H, pDCt, w->qx, ux, compute_mult, pi, 1,
+                                  w->Pb, w->memory, w->work);
+    /* d_compute_t_lam_new_rhs_mpc_hard_tv (c99/d_aux_ip_hard_lib4.c:864-935) */
+    for (int k = 0; k <= N; k++) {
+        cdim_t c = cdim(nb, ng, k);
+        for (int l = 0; l < c.nb; l++) {
+            const int ii = idxb[k][l];
+            t[k][l] = ux[k][ii] - r_C[k][l];
+            t[k][c.pnb + l] = -ux[k][ii] + r_C[k][c.pnb + l];
+            lam[k][l] = -w->lamt[k][l] * t[k][l];
+            lam[k][c.pnb + l] = -w->lamt[k][c.pnb + l] * t[k][c.pnb + l];
+        }
+        if (c.ng > 0) {
+            const int o = 2 * c.pnb;
+            double *tt = t[k] + o, *ll = lam[k] + o, *lt = w->lamt[k] + o, *dd = r_C[k] + o;
+            dct_t(k, nu, nx, ng, pDCt, ux[k], tt);
+            for (int l = 0; l < c.ng; l++) {
+                tt[l + c.png] = -tt[l];
+                tt[l] -= dd[l];
+                tt[l + c.png] += dd[l + c.png];
+                ll[l] = -lt[l] * tt[l];
+                ll[l + c.png] = -lt[l + c.png] * tt[l + c.png];
+            }
+        }
+    }
+}
+
+/* mpc_solvers/d_res_ip_hard.c:38-330: r_q, r_b, r_d of the KKT system (no r_m), mu = lam't / (2 sum(nb+ng)),
+ * 0 without constraints.  Computed with the reference's signs, then negated (:305-326). */
+void orc_d_res_mpc_hard_tv(int N, int *nx, int *nu, int *nb, int **idxb, int *ng, double **hpBAbt, double **hb,
+                           double **hpQ, double **hq, double **hux, double **hpDCt, double **hd, double **hpi,
+                           double **hlam, double **ht, double **hrq, double **hrb, double **hrd, double *mu) {
+    int nb_tot = 0;
+    mu[0] = 0.0;
+    for (int k = 0; k <= N; k++) {
+        const int nuk = nu[k], nxk = nx[k], nux = nuk + nxk, cnux = rup(nux, NCL); /* nu[N] == 0 */
+        cdim_t c = cdim(nb, ng, k);
+        nb_tot += c.nb + c.ng;
+        for (int j = 0; j < c.nb; j++) mu[0] += hlam[k][j] * ht[k][j] + hlam[k][c.pnb + j] * ht[k][c.pnb + j];
+        for (int j = 0; j < c.ng; j++)
+            mu[0] += hlam[k][2 * c.pnb + j] * ht[k][2 * c.pnb + j] +
+                     hlam[k][2 * c.pnb + c.png + j] * ht[k][2 * c.pnb + c.png + j];
+        for (int j = 0; j < c.nb; j++) {
+            const int ii = idxb[k][j];
+            hrd[k][j] = hux[k][ii] - hd[k][j] - ht[k][j];
+            hrd[k][c.pnb + j] = -hux[k][ii] + hd[k][c.pnb + j] - ht[k][c.pnb + j];
+        }
+        if (c.ng > 0) {
+            double *r = hrd[k] + 2 * c.pnb;
+            const double *dd = hd[k] + 2 * c.pnb, *tt = ht[k] + 2 * c.pnb;
+            dct_t(k, nu, nx, ng, hpDCt, hux[k], r);
+            for (int j = 0; j < c.ng; j++) {
+                r[c.png + j] = -r[j];
+                r[j] += -dd[j] - tt[j];
+                r[c.png + j] += dd[c.png + j] - tt[c.png + j];
+            }
+        }
+        for (int j = 0; j < nuk; j++) hrq[k][j] = -hq[k][j];
+        for (int j = 0; j < nxk; j++) hrq[k][nuk + j] = k > 0 ? -hq[k][nuk + j] + hpi[k - 1][j] : -hq[k][nuk + j];
+        for (int j = 0; j < c.nb; j++) hrq[k][idxb[k][j]] += hlam[k][j] - hlam[k][c.pnb + j];
+        for (int i = 0; i < nux; i++) { /* dsymv_lib, alg -1 */
+            double a = 0.0;
+            for (int j = 0; j < nux; j++) a += (i >= j ? *P4(hpQ[k], cnux, i, j) : *P4(hpQ[k], cnux, j, i)) * hux[k][j];
+            hrq[k][i] -= a;
+        }
+        if (c.ng > 0) {
+            const int cng = rup(c.ng, NCL);
+            for (int i = 0; i < nux; i++) {
+                double a = 0.0, b = 0.0;
+                for (int l = 0; l < c.ng; l++) a += *P4(hpDCt[k], cng, i, l) * hlam[k][2 * c.pnb + l];
+                for (int l = 0; l < c.ng; l++) b += *P4(hpDCt[k], cng, i, l) * hlam[k][2 * c.pnb + c.png + l];
+                hrq[k][i] += a;
+                hrq[k][i] -= b;
+            }
+        }
+        if (k < N) {
+            const int nx1 = nx[k + 1], nu1 = nu[k + 1], cnx1 = rup(nx1, NCL);
+            for (int j = 0; j < nx1; j++) hrb[k][j] = hux[k + 1][nu1 + j] - hb[k][j];
+            for (int i = 0; i < nux; i++) { /* dgemv_nt_lib, alg -1 / -1 */
+                double a = 0.0;
+                for (int j = 0; j < nx1; j++) a += *P4(hpBAbt[k], cnx1, i, j) * hpi[k][j];
+                hrq[k][i] -= a;
+            }
+            for (int j = 0; j < nx1; j++) {
+                double a = 0.0;
+                for (int i = 0; i < nux; i++) a += *P4(hpBAbt[k], cnx1, i, j) * hux[k][i];
+                hrb[k][j] -= a;
+            }
+        }
+    }
+    if (nb_tot != 0) mu[0] /= 2.0 * nb_tot;
+    for (int k = 0; k <= N; k++) {
+        const int nux = nu[k] + nx[k];
+        cdim_t c = cdim(nb, ng, k);
+        for (int j = 0; j < nux; j++) hrq[k][j] = -hrq[k][j];
+        if (k < N)
+            for (int j = 0; j < nx[k + 1]; j++) hrb[k][j] = -hrb[k][j];
+        for (int j = 0; j < c.nb; j++) {
+            hrd[k][j] = -hrd[k][j];
+            hrd[k][c.pnb + j] = -hrd[k][c.pnb + j];
+        }
+        for (int j = 0; j < c.ng; j++) {
+            hrd[k][2 * c.pnb + j] = -hrd[k][2 * c.pnb + j];
+            hrd[k][2 * c.pnb + c.png + j] = -hrd[k][2 * c.pnb + c.png + j];
+        }
+    }
 }

@@ -59,4 +59,18 @@ void orc_d_res_res_mpc_hard_tv(int N, int *nx, int *nu, int *nb, int **idxb, int
 #ifdef __cplusplus
 }
 #endif
+
+/* alternate IPM (mpc_solvers/d_ip2_hard.c) and its residuals (mpc_solvers/d_res_ip_hard.c) */
+int orc_d_ip2_mpc_hard_tv_work_space_size_bytes(int N, int *nx, int *nu, int *nb, int *ng);
+int orc_d_ip2_mpc_hard_tv(int *kk, int k_max, double mu0, double mu_tol, double alpha_min, int warm_start,
+                          double *stat, int N, int *nx, int *nu_N, int *nb, int **idxb, int *ng, double **pBAbt,
+                          double **pQ, double **pDCt, double **d, double **ux, int compute_mult, double **pi,
+                          double **lam, double **t, double *double_work_memory);
+void orc_d_kkt_solve_new_rhs_mpc_hard_tv(int N, int *nx, int *nu_N, int *nb, int **idxb, int *ng, double **pBAbt,
+                                         double **r_A, double **pQ, double **r_H, double **pDCt, double **r_C,
+                                         double **ux, int compute_mult, double **pi, double **lam, double **t,
+                                         double *double_work_memory);
+void orc_d_res_mpc_hard_tv(int N, int *nx, int *nu, int *nb, int **idxb, int *ng, double **hpBAbt, double **hb,
+                           double **hpQ, double **hq, double **hux, double **hpDCt, double **hd, double **hpi,
+                           double **hlam, double **ht, double **hrq, double **hrb, double **hrd, double *mu);
 #endif

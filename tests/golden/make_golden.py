@@ -31,6 +31,13 @@ def ref_api():
     return HpmpcAPI(load(path))
 
 
+def ref_avx_api():
+    """The reference's default-target (X64_AVX) build of the alternate IPM (oracle/Makefile ref_avx): its
+    d_kkt_solve_new_rhs_mpc_hard_tv binds the 9-parameter avx gradient helper.  Aligned marshalling."""
+    path = os.path.join(ROOT, "oracle", "_ref", "libhpmpc_ref_avx.so")
+    return HpmpcAPI(load(path), aligned=True)
+
+
 def rand_vecs(rng, sizes, pad=4, scale=1.0):
     return [np.concatenate([scale * rng.standard_normal(n), np.zeros(pad + (4 - n % 4) % 4)]) for n in sizes]
 
@@ -207,8 +214,46 @@ def main():
     out.append(save_case("newton_N10_nx8_nu3", "newton", qp, dict(k_max=1, mu0=0.1, mu_tol=1e-12, alpha_min=1e-8),
                          dict(ux=sn["ux"], pi=sn["pi"], lam=sn["lam"], t=sn["t"], stat=sn["stat"], kk=sn["kk"],
                               ret=sn["ret"]), extra=dict(ux0=ux0, pi0=pi0, lam0=lam0, t0=t0)))
+    # ---------------- alternate IPM: d_ip2_mpc_hard_tv, d_kkt_solve_new_rhs_mpc_hard_tv, d_res_mpc_hard_tv ----
+    alt(ref, ref_avx_api(), rng, out)
     total = sum(os.path.getsize(p) for p in out)
     print(f"wrote {len(out)} cases, {total / 1e6:.2f} MB")
+
+
+def alt(ref, refa, rng, out):
+    """Cases of the alternate (phase-1 only) IPM of mpc_solvers/d_ip2_hard.c and its residuals."""
+    def ipm_out(r):
+        return dict(ux=r["ux"], pi=r["pi"], lam=r["lam"], t=r["t"], stat=r["stat"], kk=r["kk"], ret=r["ret"])
+
+    cases = [("ms_N30_nx8_nu3", mass_spring_qp(30, 8, 3, boxes=True)), ("ng_N30_nx8_nu3", ng_qp())]
+    for name, qp in cases:
+        for tag, kw in (("tol1e-8", dict(mu_tol=1e-8)), ("kmax4", dict(k_max=4)), ("tol1e-12", dict(mu_tol=1e-12))):
+            args = dict(k_max=50, mu0=2.0, mu_tol=1e-12, alpha_min=1e-8)
+            args.update(kw)
+            r = ref.ipm(qp.copy(), res=False, **args)
+            out.append(save_case(f"ipm2_{tag}_{name}", "ipm2", qp, args, ipm_out(r)))
+    qp = mass_spring_qp(20, 8, 3, boxes=False)  # no constraints: sv into the workspace, outputs untouched
+    args = dict(k_max=50, mu0=2.0, mu_tol=1e-8, alpha_min=1e-8)
+    out.append(save_case("ipm2_noconstr_N20_nx8_nu3", "ipm2", qp, args, ipm_out(ref.ipm(qp.copy(), res=False, **args))))
+    qp = mass_spring_qp(30, 12, 4, boxes=True, batch=1, time_variant=True, seed=5).problem(0)
+    args = dict(k_max=50, mu0=2.0, mu_tol=1e-8, alpha_min=1e-8)
+    out.append(save_case("ipm2_tv_N30_nx12_nu4", "ipm2", qp, args, ipm_out(ref.ipm(qp.copy(), res=False, **args))))
+
+    for name, qp in cases + [("noconstr_N20_nx8_nu3", mass_spring_qp(20, 8, 3, boxes=False))]:
+        args = dict(k_max=50, mu0=2.0, mu_tol=1e-8, alpha_min=1e-8)
+        r = refa.ipm(qp.copy(), res=False, **args)
+        b, q = bq_from_qp(qp)
+        b2 = [x + 0.01 * rng.standard_normal(x.shape) for x in b]
+        q2 = [x + 0.01 * rng.standard_normal(x.shape) for x in q]
+        d2 = [x + 0.01 * rng.standard_normal(x.shape) for x in qp.d]
+        k = refa.kkt_new_rhs_plain(qp.copy(), r["work"], b2, q2, d2, r["ux"])
+        out.append(save_case(f"kkt2_{name}", "kkt2", qp, args, dict(ux=k["ux"], pi=k["pi"], lam=k["lam"], t=k["t"]),
+                             extra=dict(b2=b2, q2=q2, d2=d2)))
+        uxp = [x + 0.01 * rng.standard_normal(x.shape) for x in r["ux"]]
+        pip = [x + 0.01 * rng.standard_normal(x.shape) for x in r["pi"]]
+        res = ref.residuals_plain(qp.copy(), b, q, uxp, pip, r["lam"], r["t"])
+        out.append(save_case(f"res2_{name}", "res2", qp, {}, dict(rq=res["rq"], rb=res["rb"], rd=res["rd"], mu=res["mu"]),
+                             extra=dict(b=b, q=q, ux=uxp, pi=pip, lam=r["lam"], t=r["t"])))
 
 
 if __name__ == "__main__":
