@@ -27,7 +27,7 @@ extern "C" int hk_fixcls(int nu, int nx);
 
 namespace {
 
-enum { K_SV = 0, K_TRF = 1, K_TRS = 2, K_RES = 3, K_IPM = 4, K_KKT = 5 };
+enum { K_SV = 0, K_TRF = 1, K_TRS = 2, K_RES = 3, K_IPM = 4, K_KKT = 5, K_KKT_P1 = 6 };
 constexpr int FSTRIDE = 352, V16 = 16, V32 = 32, BS = 4, NCL = 2;
 
 struct StageInfoH {  // mirror of hk::StageInfo
@@ -873,7 +873,7 @@ namespace {
 
 // Shared body of d_ip2_res_mpc_hard_tv and its single-Newton variant.  For the variant, ux0/pi0/lam0/t0
 // hold the start iterate (lam0/t0 as [lower(nb) | upper(nb)], d_aux_ip_hard_lib4.c:153-213).
-int ipm_entry(int single_newton, int* kk, int k_max, double mu0, double mu_tol, double alpha_min, int warm_start,
+int ipm_entry(int single_newton, int phase1_only, int* kk, int k_max, double mu0, double mu_tol, double alpha_min, int warm_start,
               double* stat, int N, int* nx, int* nu_N, int* nb, int** idxb, int* ng, double** pBAbt, double** pQ,
               double** pDCt, double** d, double** ux, int compute_mult, double** pi, double** lam, double** t,
               double* double_work_memory, double** ux0, double** pi0, double** lam0, double** t0) {
@@ -914,11 +914,14 @@ int ipm_entry(int single_newton, int* kk, int k_max, double mu0, double mu_tol, 
     a.warm_start = warm_start;
     a.compute_mult = compute_mult;
     a.single_newton = single_newton;
+    a.phase1_only = phase1_only;
     if (!up(A) || !run(K_IPM, a, "hk_ipm") || !down(A)) return g_err;
     const int* iv = reinterpret_cast<const int*>(H + A.ints);
     *kk = iv[0];
     for (int i = 0; i < 5 * iv[0]; i++) stat[i] = H[A.stat + i];
-    for (int k = 0; k <= N; k++) {
+    // d_ip2_mpc_hard_tv without constraints solves into its workspace only (d_ip2_hard.c:282-291)
+    const bool outputs = !(phase1_only && P->nbt == 0);
+    for (int k = 0; outputs && k <= N; k++) {
         memcpy(ux[k], H + A.ux + k * V16, (P->st[k].nu + nx[k]) * sizeof(double));
         if (k < N) memcpy(pi[k], H + A.pi + k * V16, nx[k + 1] * sizeof(double));
         if (nb[k] + ng[k] > 0) {
@@ -937,7 +940,7 @@ extern "C" int d_ip2_res_mpc_hard_tv(int* kk, int k_max, double mu0, double mu_t
                                      double** pBAbt, double** pQ, double** pDCt, double** d, double** ux,
                                      int compute_mult, double** pi, double** lam, double** t,
                                      double* double_work_memory) {
-    return ipm_entry(0, kk, k_max, mu0, mu_tol, alpha_min, warm_start, stat, N, nx, nu_N, nb, idxb, ng, pBAbt, pQ,
+    return ipm_entry(0, 0, kk, k_max, mu0, mu_tol, alpha_min, warm_start, stat, N, nx, nu_N, nb, idxb, ng, pBAbt, pQ,
                      pDCt, d, ux, compute_mult, pi, lam, t, double_work_memory, nullptr, nullptr, nullptr, nullptr);
 }
 
@@ -948,7 +951,7 @@ extern "C" int d_ip2_res_mpc_hard_tv_single_newton_step(int* kk, int k_max, doub
                                                         double** ux, int compute_mult, double** pi, double** lam,
                                                         double** t, double* double_work_memory, double** ux0,
                                                         double** pi0, double** lam0, double** t0) {
-    return ipm_entry(1, kk, k_max, mu0, mu_tol, alpha_min, warm_start, stat, N, nx, nu_N, nb, idxb, ng, pBAbt, pQ,
+    return ipm_entry(1, 0, kk, k_max, mu0, mu_tol, alpha_min, warm_start, stat, N, nx, nu_N, nb, idxb, ng, pBAbt, pQ,
                      pDCt, d, ux, compute_mult, pi, lam, t, double_work_memory, ux0, pi0, lam0, t0);
 }
 
@@ -1029,6 +1032,102 @@ extern "C" void d_res_res_mpc_hard_tv(int N, int* nx, int* nu, int* nb, int** id
             memcpy(hrd[k], rd + k * V32, cvec_len(P, k) * sizeof(double));
             memcpy(hrm[k], rm + k * V32, cvec_len(P, k) * sizeof(double));
         }
+    }
+    *mu = H[A.ints + 2];
+}
+
+// ------------------------------------------------------------------------------------------------
+// The alternate IPM of mpc_solvers/d_ip2_hard.c (phase-1 Mehrotra loop alone), its KKT re-solve and the
+// plain residuals of mpc_solvers/d_res_ip_hard.c, on the same kernels (KArgs.phase1_only / res_plain).
+// ------------------------------------------------------------------------------------------------
+extern "C" int d_ip2_mpc_hard_tv_work_space_size_bytes(int N, int* nx, int* nu, int* nb, int* ng) {
+    return d_ip2_res_mpc_hard_tv_work_space_size_bytes(N, nx, nu, nb, ng);
+}
+
+extern "C" int d_ip2_mpc_hard_tv(int* kk, int k_max, double mu0, double mu_tol, double alpha_min, int warm_start,
+                                 double* stat, int N, int* nx, int* nu_N, int* nb, int** idxb, int* ng,
+                                 double** pBAbt, double** pQ, double** pDCt, double** d, double** ux,
+                                 int compute_mult, double** pi, double** lam, double** t,
+                                 double* double_work_memory) {
+    return ipm_entry(0, 1, kk, k_max, mu0, mu_tol, alpha_min, warm_start, stat, N, nx, nu_N, nb, idxb, ng, pBAbt,
+                     pQ, pDCt, d, ux, compute_mult, pi, lam, t, double_work_memory, nullptr, nullptr, nullptr,
+                     nullptr);
+}
+
+extern "C" void d_kkt_solve_new_rhs_mpc_hard_tv(int N, int* nx, int* nu_N, int* nb, int** idxb, int* ng,
+                                                double** pBAbt, double** r_A, double** pQ, double** r_H,
+                                                double** pDCt, double** r_C, double** ux, int compute_mult,
+                                                double** pi, double** lam, double** t, double* double_work_memory) {
+    (void)pQ;  // the factor of the IPM's last iteration is in the workspace
+    g_err = 0;
+    hpmpc_mi355x_plan* P = g_ctx.get_plan(N, nx, nu_N, nb, idxb, ng);
+    if (!P) return;
+    Arena A = arena(P, 1);
+    if (!g_ctx.ensure(A.total)) return;
+    double* H = g_ctx.host;
+    stage_BAbt(P, H, A, pBAbt);
+    stage_d(P, H, A, r_C);
+    stage_DCt(P, H, A, pDCt);
+    memcpy(H + A.ws, double_work_memory, ws_doubles(N) * sizeof(double));
+    for (int k = 0; k <= N; k++) {
+        memcpy(H + A.vq + k * V16, r_H[k], (P->st[k].nu + nx[k]) * sizeof(double));
+        memcpy(H + A.ux + k * V16, ux[k], (P->st[k].nu + nx[k]) * sizeof(double));
+        if (k < N) memcpy(H + A.vb + k * V16, r_A[k], nx[k + 1] * sizeof(double));
+    }
+    KArgs a = arena_args(P, A, g_ctx.dev);
+    a.compute_mult = compute_mult;
+    if (!up(A) || !run(K_KKT_P1, a, "hk_kkt_new_rhs_p1") || !down(A)) return;
+    for (int k = 0; k <= N; k++) {
+        memcpy(ux[k], H + A.ux + k * V16, (P->st[k].nu + nx[k]) * sizeof(double));
+        if (k < N && compute_mult) memcpy(pi[k], H + A.pi + k * V16, nx[k + 1] * sizeof(double));
+        if (nb[k] + ng[k] > 0) {
+            memcpy(lam[k], H + A.lam + k * V32, cvec_len(P, k) * sizeof(double));
+            memcpy(t[k], H + A.t + k * V32, cvec_len(P, k) * sizeof(double));
+        }
+    }
+    // the persisted factor / workspace is left as the IPM wrote it, apart from qx and Pb (as the reference)
+    memcpy(double_work_memory, H + A.ws, ws_doubles(N) * sizeof(double));
+}
+
+extern "C" void d_res_mpc_hard_tv(int N, int* nx, int* nu, int* nb, int** idxb, int* ng, double** hpBAbt,
+                                  double** hb, double** hpQ, double** hq, double** hux, double** hpDCt, double** hd,
+                                  double** hpi, double** hlam, double** ht, double** hrq, double** hrb, double** hrd,
+                                  double* mu) {
+    g_err = 0;
+    hpmpc_mi355x_plan* P = g_ctx.get_plan(N, nx, nu, nb, idxb, ng);
+    if (!P) return;
+    Arena A = arena(P, 1);
+    if (!g_ctx.ensure(A.total)) return;
+    double* H = g_ctx.host;
+    stage_BAbt(P, H, A, hpBAbt);
+    stage_RSQ(P, H, A, hpQ);
+    stage_d(P, H, A, hd);
+    stage_DCt(P, H, A, hpDCt);
+    for (int k = 0; k <= N; k++) {
+        const int nux = P->st[k].nu + nx[k];
+        memcpy(H + A.vq + k * V16, hq[k], nux * sizeof(double));
+        memcpy(H + A.ux + k * V16, hux[k], nux * sizeof(double));
+        if (k < N) {
+            memcpy(H + A.vb + k * V16, hb[k], nx[k + 1] * sizeof(double));
+            memcpy(H + A.pi + k * V16, hpi[k], nx[k + 1] * sizeof(double));
+        }
+        if (nb[k] + ng[k] > 0) {
+            memcpy(H + A.lam + k * V32, hlam[k], cvec_len(P, k) * sizeof(double));
+            memcpy(H + A.t + k * V32, ht[k], cvec_len(P, k) * sizeof(double));
+        }
+    }
+    KArgs a = arena_args(P, A, g_ctx.dev);
+    a.res_plain = 1;
+    if (!up(A) || !run(K_RES, a, "hk_res") || !down(A)) return;
+    const size_t n1 = N + 1;
+    const double* rq = H + A.ws;
+    const double* rb = rq + n1 * V16;
+    const double* rd = rb + n1 * V16;
+    for (int k = 0; k <= N; k++) {
+        const int nux = P->st[k].nu + nx[k];
+        memcpy(hrq[k], rq + k * V16, nux * sizeof(double));
+        if (k < N) memcpy(hrb[k], rb + k * V16, nx[k + 1] * sizeof(double));
+        if (nb[k] + ng[k] > 0) memcpy(hrd[k], rd + k * V32, cvec_len(P, k) * sizeof(double));
     }
     *mu = H[A.ints + 2];
 }

@@ -29,6 +29,8 @@ struct KArgs {
     int update_b, update_q, use_box, compute_pi, compute_Pb;
     // IPM
     int k_max, warm_start, compute_mult, single_newton;
+    int phase1_only;  // d_ip2_mpc_hard_tv (mpc_solvers/d_ip2_hard.c:88): the phase-1 loop alone, run to mu_tol
+    int res_plain;    // d_res_mpc_hard_tv sign convention (mpc_solvers/d_res_ip_hard.c:305-326), no r_m
     double mu0, mu_tol, alpha_min;
     int *kk, *ret;
     double* stat;    // 5*k_max per problem

@@ -195,6 +195,15 @@ __global__ __launch_bounds__(64) void hk_res(KArgs a) {
     ro.rm = out + 2 * n1 * V16 + n1 * V32;
     double mu = 0.0;
     const bool have = residual_pass<false, FX>(io, bc, ro, mu);
+    if (a.res_plain) {
+        // d_res_mpc_hard_tv (mpc_solvers/d_res_ip_hard.c:38-330): the same r_q, r_b and lower r_d; its
+        // upper r_d is (x - ub + t_up), the negation of the residual IPM's, and mu is 0 without constraints
+        wsync();
+        HK_FOR_BOX(io, k, { ro.rd[up] = -ro.rd[up]; });
+        HK_FOR_GEN(io, k, { ro.rd[up] = -ro.rd[up]; });
+        if (lane_id() == 0) a.mu_out[p] = have ? mu : 0.0;
+        return;
+    }
     if (lane_id() == 0 && have) a.mu_out[p] = mu;
 }
 
@@ -400,15 +409,20 @@ __device__ double p2_start(const KArgs& a, IpmView& v) {
 template <class FX>
 __device__ bool ipm_continue(const KArgs& a, IpmView& v, int kk, double mu, double alpha, double sigma, int phase) {
     const bool sn = a.single_newton != 0;
-    if (phase == 1) {
-        const double mu_tol_low = a.mu_tol < 1e-5 ? 1e-5 : a.mu_tol;
-        if (!(kk < a.k_max && mu > mu_tol_low && alpha >= a.alpha_min)) {
-            mu = p2_start<FX>(a, v);  // phase-2 start (d_ip2_res_hard.c:756-781)
-            phase = 2;
+    bool active;
+    if (a.phase1_only) {  // d_ip2_mpc_hard_tv: the phase-1 loop run to mu_tol (d_ip2_hard.c:329-520)
+        active = kk < a.k_max && mu > a.mu_tol && alpha >= a.alpha_min;
+    } else {
+        if (phase == 1) {
+            const double mu_tol_low = a.mu_tol < 1e-5 ? 1e-5 : a.mu_tol;
+            if (!(kk < a.k_max && mu > mu_tol_low && alpha >= a.alpha_min)) {
+                mu = p2_start<FX>(a, v);  // phase-2 start (d_ip2_res_hard.c:756-781)
+                phase = 2;
+            }
         }
+        active = phase == 1;
+        if (phase == 2) active = kk < a.k_max && (sn || (mu > a.mu_tol && alpha >= a.alpha_min));
     }
-    bool active = phase == 1;
-    if (phase == 2) active = kk < a.k_max && (sn || (mu > a.mu_tol && alpha >= a.alpha_min));
     int ret = 0;
     if (!active) {
         if (!sn && mu <= a.mu_tol)
@@ -442,6 +456,19 @@ __device__ bool ipm_start(const KArgs& a, const LdsTabs& T, IpmView& v) {
     Scratch& sm = *T.sm;
     const int N = v.N, l = v.l;
     const int nbt = a.nbt;
+    if (nbt == 0 && a.phase1_only) {
+        // d_ip2_mpc_hard_tv without constraints: one sv into the workspace's dux / dpi, the caller's
+        // ux / pi stay untouched (d_ip2_hard.c:282-291)
+        ric_backward<true, BX_NONE, FX>(v.io, &sm, 0, nullptr, 0, nullptr, v.bc, 1, v.w.Pb);
+        wsync();
+        ric_forward_sv<FX>(v.io, &sm, 0, nullptr, v.w.dux, a.compute_mult, v.w.dpi);
+        if (l == 0) {
+            v.w.state[S_ACTIVE] = 0.0;
+            a.kk[v.q] = 0;
+            a.ret[v.q] = 0;
+        }
+        return false;
+    }
     if (nbt == 0) {
         // no constraints: one sv and return (d_ip2_res_hard.c:428-450)
         ric_backward<true, BX_NONE, FX>(v.io, &sm, 0, nullptr, 0, nullptr, v.bc, 1, v.w.Pb);
@@ -726,6 +753,72 @@ __global__ __launch_bounds__(64) void hk_kkt_new_rhs(KArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// d_kkt_solve_new_rhs_mpc_hard_tv (mpc_solvers/d_ip2_hard.c:626-825): re-solve of the alternate IPM's
+// last KKT system for new b (r_A, in vb), q (r_H, in vq) and bounds (r_C, in d), on the factor and the
+// lamt = lam/t that d_ip2_mpc_hard_tv left in ws.  ux / pi are solved for directly (not as a step).
+// ------------------------------------------------------------------------------------------------
+template <class FX>
+__global__ __launch_bounds__(64) void hk_kkt_new_rhs_p1(KArgs a) {
+    const LdsTabs T = lds_tables(a);
+    Scratch& sm = *T.sm;
+    const int p = blockIdx.x + a.p0;
+    if (p >= a.nprob) return;
+    const int N = a.N;
+    Ws w = carve(a.ws + (long)p * a.sW, N);
+    RicIO io = make_io(a, T, p, w.F);
+    BoxTab bt{T.tileslot, T.slotvar};
+    const long o16 = (long)p * a.sV16, o32 = (long)p * a.sV32;
+    double* ux = a.ux + o16;
+    double* pi = a.pi + o16;
+    double* lam = a.lam + o32;
+    double* t = a.t + o32;
+    const double* rC = a.d + o32;
+    const int l = lane_id();
+    BoxCtx bc = box_ctx(w, rC, lam, t);
+    // d_update_gradient_new_rhs_mpc_hard_tv (the reference's default X64_AVX build,
+    // avx/d_aux_ip_hard_lib4.c:1735-1838): qx = -lamt_u r_C,u - lamt_l r_C,l
+    HK_FOR_BOX(io, k, { w.qx[k * V16 + slot] = -w.lamt[up] * rC[up] - w.lamt[lo] * rC[lo]; });
+    HK_FOR_GEN(io, k, { w.qx[s16] = -w.lamt[up] * rC[up] - w.lamt[lo] * rC[lo]; });
+    wsync();
+    double al = 1.0;
+    ric_trs<BX_GIVEN, BX_NONE, FX>(io, &sm, a.vb + o16, a.vq + o16, bc, ux, a.compute_mult, pi, 1, w.Pb, al);
+    wsync();
+    // d_compute_t_lam_new_rhs_mpc_hard_tv (c99/d_aux_ip_hard_lib4.c:864-935)
+    HK_FOR_BOX(io, k, {
+        const double x = ux[k * V16 + bt.slotvar[k * 16 + slot]];
+        const double tl = x - rC[lo], tu = -x + rC[up];
+        t[lo] = tl;
+        t[up] = tu;
+        lam[lo] = -w.lamt[lo] * tl;
+        lam[up] = -w.lamt[up] * tu;
+    });
+    if (a.ngt) {
+        const int c = l & 15;
+        for (int k = 0; k <= N; k++) {
+            const StageInfo si = load_stage(io.st, k);
+            if (si.ng == 0) continue;
+            const DynSh sh(si);
+            const int vc = tile_var(c, sh.nu, sh.nx, sh.xo);
+            const double x = gld(ux, k * V16 + vc, vc >= 0);
+            double dg[4];
+            gen_dg(io, sh, dg);
+#pragma unroll
+            for (int lc = 0; lc < 4; lc++) {
+                if (4 * lc >= sh.ng) continue;
+                const GenLane q = gen_lane(k, sh.pnb, sh.ng, lc);
+                const bool st = q.ok && c == 0;
+                const double dx = row_sum16(dg[lc] * x);
+                const double tl = dx - gld(rC, q.lo, q.ok), tu = -dx + gld(rC, q.up, q.ok);
+                gst(t, q.lo, tl, st);
+                gst(t, q.up, tu, st);
+                gst(lam, q.lo, -gld(w.lamt, q.lo, q.ok) * tl, st);
+                gst(lam, q.up, -gld(w.lamt, q.up, q.ok) * tu, st);
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Host launch helpers (called from the C-ABI translation unit).
 // ------------------------------------------------------------------------------------------------
 template <class FX>
@@ -747,6 +840,7 @@ static int launch_t(int which, const KArgs* a, int count, hipStream_t stream) {
             }
             break;
         case 5: hipLaunchKernelGGL(hk_kkt_new_rhs<FX>, grid, block, lds, stream, *a); break;
+        case 6: hipLaunchKernelGGL(hk_kkt_new_rhs_p1<FX>, grid, block, lds, stream, *a); break;
         // single IPM pass kernels (hpmpc_mi355x_ipm_pass): the batched solve is 10, then k_max x (11..14)
         case 10: hipLaunchKernelGGL(hk_ipm_init<FX>, grid, block, lds, stream, *a); break;
         case 11: hipLaunchKernelGGL(hk_ipm_fact<FX>, grid, block, lds, stream, *a); break;

@@ -14,7 +14,8 @@
  * already resident in device memory (HBM).
  *
  * GPU-path limits (checked; a violation is reported through hpmpc_mi355x_last_error()):
- *   nu[k] + nx[k] <= 16 and round_up(nu[k],4) + nx[k] <= 16 for every stage, ng[k] == 0.
+ *   nu[k] + nx[k] <= 16 and round_up(nu[k],4) + nx[k] <= 16 for every stage,
+ *   round_up(nb[k],4) + round_up(ng[k],4) <= 16.
  * Error reporting: the reference's int entry points keep their codes 0/1/2/-1; this library adds
  *   HPMPC_MI355X_EUNSUPPORTED (-10) and HPMPC_MI355X_EHIP (-11).  void entry points set the
  *   thread-local code returned by hpmpc_mi355x_last_error() and print one line to stderr.
@@ -73,6 +74,25 @@ void d_res_res_mpc_hard_tv(int N, int *nx, int *nu, int *nb, int **idxb, int *ng
                            double **hpQ, double **hq, double **hux, double **hpDCt, double **hd, double **hpi,
                            double **hlam, double **ht, double *work, double **hrq, double **hrb, double **hrd,
                            double **hrm, double *mu);
+
+/* The alternate IPM of mpc_solvers/d_ip2_hard.c: the phase-1 Mehrotra loop alone, run to mu_tol. */
+/* include/mpc_solvers.h:33 (mpc_solvers/d_ip2_hard.c:31) */
+int d_ip2_mpc_hard_tv_work_space_size_bytes(int N, int *nx, int *nu, int *nb, int *ng);
+/* include/mpc_solvers.h:34 (d_ip2_hard.c:88) */
+int d_ip2_mpc_hard_tv(int *kk, int k_max, double mu0, double mu_tol, double alpha_min, int warm_start, double *stat,
+                      int N, int *nx, int *nu, int *nb, int **idxb, int *ng, double **pBAbt, double **pQ,
+                      double **pDCt, double **d, double **ux, int compute_mult, double **pi, double **lam, double **t,
+                      double *double_work_memory);
+/* include/mpc_solvers.h:35 (d_ip2_hard.c:626) -- re-solve on the factor and lam/t that d_ip2_mpc_hard_tv left in
+ * the workspace, for new r_A (b), r_H (q) and r_C (bounds) */
+void d_kkt_solve_new_rhs_mpc_hard_tv(int N, int *nx, int *nu_N, int *nb, int **idxb, int *ng, double **pBAbt,
+                                     double **r_A, double **pQ, double **r_H, double **pDCt, double **r_C,
+                                     double **ux, int compute_mult, double **pi, double **lam, double **t,
+                                     double *double_work_memory);
+/* include/mpc_solvers.h:36 (mpc_solvers/d_res_ip_hard.c:38) -- r_q, r_b, r_d and mu (no r_m) */
+void d_res_mpc_hard_tv(int N, int *nx, int *nu, int *nb, int **idxb, int *ng, double **hpBAbt, double **hb,
+                       double **hpQ, double **hq, double **hux, double **hpDCt, double **hd, double **hpi,
+                       double **hlam, double **ht, double **hrq, double **hrb, double **hrd, double *mu);
 
 /* ================================ Part 2: batched device API ==================================== */
 
