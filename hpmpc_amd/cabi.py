@@ -283,6 +283,73 @@ class HpmpcAPI:
         return dict(rq=rq, rb=rb, rd=rd, mu=mu.value)
 
 
+    # --------------------------------------------------------------------------------------------- partial condensing
+    def part_cond_sizes(self, qp: OCPQP, N2: int):
+        """d_part_cond_compute_problem_size (lqcp_solvers/d_part_cond.c:694): condensed stage sizes."""
+        N = qp.N
+        out = [(C.c_int * (N2 + 1))() for _ in range(4)]
+        self.fn("d_part_cond_compute_problem_size")(C.c_int(N), iv(qp.nx), iv(qp.nu), iv(qp.nb), ipp(qp.idxb),
+                                                    iv(qp.ng), C.c_int(N2), *out)
+        return [np.array(o[:], dtype=np.int32) for o in out]
+
+    def part_cond(self, qp: OCPQP, N2: int):
+        """d_part_cond (d_part_cond.c:926): condense qp into N2 blocks.  Returns the condensed OCPQP (copied out of
+        the routine's memory) and the raw memory buffer.  Its last stage is the original's, as d_part_cond sets it
+        (:1052-1056); it is taken from qp rather than through the returned pointers because the reference build
+        writes one int past `int cnx[N]` (:978-982) and its terminal pointers come back clobbered."""
+        N = qp.N
+        idxb = [np.ascontiguousarray(i, dtype=np.int32) for i in qp.idxb]
+        nx2, nu2, nb2, ng2 = self.part_cond_sizes(qp, N2)
+        cn = [iv(a) for a in (nx2, nu2, nb2, ng2)]
+        head = (C.c_int(N), iv(qp.nx), iv(qp.nu), iv(qp.nb), ipp(idxb), iv(qp.ng), C.c_int(N2), *cn)
+        wsz = self.fn("d_part_cond_work_space_size_bytes")(*head)
+        msz = self.fn("d_part_cond_memory_space_size_bytes")(*head)
+        # 2x + 4 KiB headroom: the reference's own work-size formula under-counts for single-block horizons
+        # (d_part_cond.c:743-866; N2 = 1 with boxes overruns it)
+        memory = np.zeros(2 * (msz // 8) + 512)
+        work = np.zeros(2 * (wsz // 8) + 512)
+        hidxb2 = (IP * (N2 + 1))()
+        pB, pR, pG, pd = ((DP * (N2 + 1))() for _ in range(4))
+        dct = qp.DCt if qp.DCt else [np.zeros(8) for _ in range(N + 1)]
+        self.fn("d_part_cond")(C.c_int(N), iv(qp.nx), iv(qp.nu), iv(qp.nb), ipp(idxb), iv(qp.ng), self._pp(qp.BAbt),
+                               self._pp(qp.RSQrq), self._pp(dct), self._pp(qp.d), C.c_int(N2), cn[0], cn[1], cn[2],
+                               hidxb2, cn[3], pB, pR, pG, pd, self._p(memory), self._p(work))
+        self._sync()
+        arr = lambda ptr, n: np.ctypeslib.as_array(ptr, shape=(max(n, 1),)).copy() if n > 0 else np.zeros(8)
+        BAbt2, RSQ2, DCt2, d2, idx2 = [], [], [], [], []
+        for k in range(N2):
+            nux = int(nu2[k] + nx2[k])
+            if True:
+                BAbt2.append(arr(pB[k], rup(nux + 1, 4) * rup(int(nx2[k + 1]), 2)))
+            RSQ2.append(arr(pR[k], rup(nux + 1, 4) * rup(nux, 2)))
+            DCt2.append(arr(pG[k], rup(nux, 4) * rup(int(ng2[k]), 2)))
+            d2.append(arr(pd[k], 2 * rup(int(nb2[k]), 4) + 2 * rup(int(ng2[k]), 4)))
+            idx2.append(np.ctypeslib.as_array(hidxb2[k], shape=(int(nb2[k]),)).copy().astype(np.int32)
+                        if nb2[k] > 0 else np.zeros(0, np.int32))
+        RSQ2.append(qp.RSQrq[N].copy())
+        DCt2.append(dct[N].copy())
+        d2.append(qp.d[N].copy())
+        idx2.append(idxb[N].copy())
+        cqp = OCPQP(N2, nx2, nu2, nb2, ng2, idx2, BAbt2, RSQ2, d2, DCt2 if ng2.any() else [], None)
+        return cqp, memory
+
+    def part_expand(self, qp: OCPQP, cqp: OCPQP, ux2, pi2, lam2, t2):
+        """d_part_expand_solution (d_part_cond.c:1103): the full-space solution of qp from the condensed one."""
+        N, N2 = qp.N, cqp.N
+        b, q = bq_from_qp(qp)
+        ux, pi, lam, t = qp.alloc_solution()
+        wsz = self.fn("d_part_expand_work_space_size_bytes")(C.c_int(N), iv(qp.nx), iv(qp.nu), iv(qp.nb), iv(qp.ng))
+        work = np.zeros(wsz // 8 + 16)
+        dct = qp.DCt if qp.DCt else [np.zeros(8) for _ in range(N + 1)]
+        self.fn("d_part_expand_solution")(
+            C.c_int(N), iv(qp.nx), iv(qp.nu), iv(qp.nb), ipp(qp.idxb), iv(qp.ng), self._pp(qp.BAbt), self._pp(b),
+            self._pp(qp.RSQrq), self._pp(q), self._pp(dct), self._pp(ux), self._pp(pi), self._pp(lam), self._pp(t),
+            C.c_int(N2), iv(cqp.nx), iv(cqp.nu), iv(cqp.nb), ipp(cqp.idxb), iv(cqp.ng), self._pp(ux2), self._pp(pi2),
+            self._pp(lam2), self._pp(t2), self._p(work))
+        self._sync()
+        return dict(ux=ux, pi=pi, lam=lam, t=t)
+
+
 def bq_from_qp(qp: OCPQP):
     """b[k] and q[k] vectors extracted from the augmented rows (as the IPM does, d_ip2_res_hard.c:202-220)."""
     from .ocp import unpack_lib4

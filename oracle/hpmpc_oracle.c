@@ -77,6 +77,7 @@ int orc_d_back_ric_rec_sv_tv_work_space_size_bytes(int N, int *nx, int *nu, int 
 /* Cholesky of the leading n x n block of the dense symmetric M (lower part used), with the extra
  * rows n..m-1 solved against it (the "augmented row" trick, d_back_ric_rec.c:146,194,259,345).
  * Left-looking; pivot d > 1e-15 else the column is zeroed (kernel_dpotrf_c99_lib4.c:555-640). */
+void orc__chol_aug(int m, int n, double *M, int ldm, double *L, int ldl, double *dL);
 static void chol_aug(int m, int n, double *M, int ldm, double *L, int ldl, double *dL) {
     for (int j = 0; j < n; j++) {
         for (int i = j; i < m; i++) {
@@ -1213,3 +1214,6 @@ void orc_d_res_mpc_hard_tv(int N, int *nx, int *nu, int *nb, int **idxb, int *ng
         }
     }
 }
+
+/* shared with hpmpc_oracle_cond.c (partial condensing propagates the state cost-to-go with it) */
+void orc__chol_aug(int m, int n, double *M, int ldm, double *L, int ldl, double *dL) { chol_aug(m, n, M, ldm, L, ldl, dL); }

@@ -56,10 +56,6 @@ void orc_d_res_res_mpc_hard_tv(int N, int *nx, int *nu, int *nb, int **idxb, int
     double **hpQ, double **hq, double **hux, double **hpDCt, double **hd, double **hpi, double **hlam, double **ht,
     double *work, double **hrq, double **hrb, double **hrd, double **hrm, double *mu);
 
-#ifdef __cplusplus
-}
-#endif
-
 /* alternate IPM (mpc_solvers/d_ip2_hard.c) and its residuals (mpc_solvers/d_res_ip_hard.c) */
 int orc_d_ip2_mpc_hard_tv_work_space_size_bytes(int N, int *nx, int *nu, int *nb, int *ng);
 int orc_d_ip2_mpc_hard_tv(int *kk, int k_max, double mu0, double mu_tol, double alpha_min, int warm_start,
@@ -73,4 +69,24 @@ void orc_d_kkt_solve_new_rhs_mpc_hard_tv(int N, int *nx, int *nu_N, int *nb, int
 void orc_d_res_mpc_hard_tv(int N, int *nx, int *nu, int *nb, int **idxb, int *ng, double **hpBAbt, double **hb,
                            double **hpQ, double **hq, double **hux, double **hpDCt, double **hd, double **hpi,
                            double **hlam, double **ht, double **hrq, double **hrb, double **hrd, double *mu);
+
+/* partial condensing (lqcp_solvers/d_part_cond.c) */
+void orc_d_part_cond_compute_problem_size(int N, int *nx, int *nu, int *nb, int **hidxb, int *ng, int N2, int *nx2,
+                                          int *nu2, int *nb2, int *ng2);
+int orc_d_part_cond_work_space_size_bytes(int N, int *nx, int *nu, int *nb, int **hidxb, int *ng, int N2, int *nx2,
+                                          int *nu2, int *nb2, int *ng2);
+int orc_d_part_cond_memory_space_size_bytes(int N, int *nx, int *nu, int *nb, int **hidxb, int *ng, int N2,
+                                            int *nx2, int *nu2, int *nb2, int *ng2);
+void orc_d_part_cond(int N, int *nx, int *nu, int *nb, int **hidxb, int *ng, double **hpBAbt, double **hpRSQrq,
+                     double **hpDCt, double **hd, int N2, int *nx2, int *nu2, int *nb2, int **hidxb2, int *ng2,
+                     double **hpBAbt2, double **hpRSQrq2, double **hpDCt2, double **hd2, void *memory, void *work);
+int orc_d_part_expand_work_space_size_bytes(int N, int *nx, int *nu, int *nb, int *ng);
+void orc_d_part_expand_solution(int N, int *nx, int *nu, int *nb, int **hidxb, int *ng, double **hpBAbt, double **hb,
+                                double **hpRSQrq, double **hrq, double **hpDCt, double **hux, double **hpi,
+                                double **hlam, double **ht, int N2, int *nx2, int *nu2, int *nb2, int **hidxb2,
+                                int *ng2, double **hux2, double **hpi2, double **hlam2, double **ht2, void *work);
+
+#ifdef __cplusplus
+}
+#endif
 #endif

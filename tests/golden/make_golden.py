@@ -216,6 +216,7 @@ def main():
                               ret=sn["ret"]), extra=dict(ux0=ux0, pi0=pi0, lam0=lam0, t0=t0)))
     # ---------------- alternate IPM: d_ip2_mpc_hard_tv, d_kkt_solve_new_rhs_mpc_hard_tv, d_res_mpc_hard_tv ----
     alt(ref, ref_avx_api(), rng, out)
+    pcond(ref, out)
     total = sum(os.path.getsize(p) for p in out)
     print(f"wrote {len(out)} cases, {total / 1e6:.2f} MB")
 
@@ -256,5 +257,37 @@ def alt(ref, refa, rng, out):
                              extra=dict(b=b, q=q, ux=uxp, pi=pip, lam=r["lam"], t=r["t"])))
 
 
+def pcond(ref, out):
+    """Partial condensing (lqcp_solvers/d_part_cond.c): d_part_cond outputs and d_part_expand_solution of random
+    condensed-space vectors, on cases where the reference c99 build is right (nu <= 4: for nu > 4 its condensed
+    Hessian is wrong past the 4th column of each inner u block); the C5 workload (nu = 6) is pinned
+    by the reference's direct Riccati solution instead (kind pcond_sv: condense -> sv -> expand == direct sv)."""
+    rng = np.random.default_rng(20261016)
+    for (N, nx, nu, N2, boxes) in [(20, 8, 3, 4, False), (20, 8, 3, 4, True), (23, 6, 2, 5, True),
+                                   (30, 24, 4, 3, True), (12, 4, 1, 12, True), (9, 8, 4, 2, True)]:
+        qp = mass_spring_qp(N, nx, nu, boxes=boxes)
+        c, _ = ref.part_cond(qp.copy(), N2)
+        u2 = rand_vecs(rng, [c.nux(k) for k in range(N2 + 1)])
+        p2 = rand_vecs(rng, [int(c.nx[k + 1]) for k in range(N2)])
+        lam2 = [np.abs(x) for x in rand_vecs(rng, [c.nconstr(k) for k in range(N2 + 1)])]
+        t2 = [np.abs(x) for x in rand_vecs(rng, [c.nconstr(k) for k in range(N2 + 1)])]
+        e = ref.part_expand(qp, c, u2, p2, lam2, t2)
+        outs = dict(BAbt2=c.BAbt, RSQrq2=c.RSQrq[:N2], DCt2=c.DCt[:N2] if c.DCt else [], d2=c.d[:N2],
+                    idxb2=[i.astype(np.float64) for i in c.idxb[:N2]], nx2=c.nx, nu2=c.nu, nb2=c.nb, ng2=c.ng,
+                    ux=e["ux"], pi=e["pi"], lam=e["lam"], t=e["t"])
+        tag = "box" if boxes else "ms"
+        out.append(save_case(f"pcond_{tag}_N{N}_nx{nx}_nu{nu}_N2_{N2}", "pcond", qp, dict(N2=N2), outs,
+                             extra=dict(u2=u2, p2=p2, lam2=lam2, t2=t2)))
+    for (N, nx, nu, N2) in [(200, 24, 6, 20), (40, 12, 6, 8)]:
+        qp = mass_spring_qp(N, nx, nu, boxes=False)
+        ux, pi, _, _ = ref.ric_sv(qp.copy(), compute_pi=1, compute_Pb=0)
+        out.append(save_case(f"pcond_sv_N{N}_nx{nx}_nu{nu}_N2_{N2}", "pcond_sv", qp, dict(N2=N2), dict(ux=ux, pi=pi)))
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "pcond":
+        o = []
+        pcond(ref_api(), o)
+        print(f"wrote {len(o)} pcond cases, {sum(os.path.getsize(p) for p in o) / 1e6:.2f} MB")
+    else:
+        main()

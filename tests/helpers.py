@@ -60,7 +60,56 @@ def run_case(api, case):
         r = api.single_newton(qp, inp["ux0"], inp["pi0"], inp["lam0"], inp["t0"], k_max=int(a["k_max"]),
                               mu0=a["mu0"])
         return dict(ux=r["ux"], pi=r["pi"], lam=r["lam"], t=r["t"], stat=r["stat"], kk=r["kk"], ret=r["ret"])
+    if case.kind == "pcond":
+        c, _ = api.part_cond(qp, int(a["N2"]))
+        e = api.part_expand(qp, c, inp["u2"], inp["p2"], inp["lam2"], inp["t2"])
+        return dict(cqp=c, ux=e["ux"], pi=e["pi"], lam=e["lam"], t=e["t"])
+    if case.kind == "pcond_sv":
+        return pcond_sv(api, qp, int(a["N2"]))
     raise ValueError(case.kind)
+
+
+def pcond_sv(api, qp, N2):
+    """condense (d_part_cond) -> Riccati sv on the condensed problem -> expand (d_part_expand_solution)."""
+    c, _ = api.part_cond(qp, N2)
+    u2, p2, _, _ = api.ric_sv(c.copy(), compute_pi=1, compute_Pb=0)
+    z = [np.zeros(max(c.nconstr(k), 1)) for k in range(N2 + 1)]
+    e = api.part_expand(qp, c, u2, p2, z, z)
+    return dict(ux=e["ux"], pi=e["pi"])
+
+
+TOL_PCOND_SV = 1e-11  # condensed pipeline vs the reference's direct Riccati (oracle measured 4e-14 absolute)
+
+
+def check_pcond(case, got):
+    """Condensed data of d_part_cond (lower triangle of RSQrq2: the only part any consumer reads) and the
+    expanded solution."""
+    from hpmpc_amd.ocp import unpack_lib4
+
+    out, c = case.out, got["cqp"]
+    for f in ("nx2", "nu2", "nb2", "ng2"):
+        np.testing.assert_array_equal(getattr(c, f[:2]), out[f], err_msg=case.name + f)
+    N2 = c.N
+    for k in range(N2):
+        nux = c.nux(k)
+        A = unpack_lib4(c.BAbt[k], nux + 1, int(c.nx[k + 1]))
+        B = unpack_lib4(out["BAbt2"][k], nux + 1, int(c.nx[k + 1]))
+        np.testing.assert_allclose(A, B, rtol=TOL_RIC, atol=TOL_RIC, err_msg=f"{case.name} BAbt2[{k}]")
+        A = np.tril(unpack_lib4(c.RSQrq[k], nux + 1, nux))
+        B = np.tril(unpack_lib4(out["RSQrq2"][k], nux + 1, nux))
+        np.testing.assert_allclose(A, B, rtol=TOL_RIC, atol=TOL_RIC, err_msg=f"{case.name} RSQrq2[{k}]")
+        if c.ng[k]:
+            A = unpack_lib4(c.DCt[k], nux, int(c.ng[k]))
+            B = unpack_lib4(out["DCt2"][k], nux, int(c.ng[k]))
+            np.testing.assert_allclose(A, B, rtol=TOL_RIC, atol=TOL_RIC, err_msg=f"{case.name} DCt2[{k}]")
+        nb, pnb, ng, png = int(c.nb[k]), c.pnb(k), int(c.ng[k]), c.png(k)
+        idx = np.r_[0:nb, pnb:pnb + nb, 2 * pnb:2 * pnb + ng, 2 * pnb + png:2 * pnb + png + ng].astype(int)
+        np.testing.assert_allclose(c.d[k][idx], out["d2"][k][idx], rtol=TOL_RIC, atol=TOL_RIC,
+                                   err_msg=f"{case.name} d2[{k}]")
+        np.testing.assert_array_equal(c.idxb[k], out["idxb2"][k].astype(np.int32), err_msg=f"{case.name} idxb2")
+    for key in ("ux", "pi", "lam", "t"):
+        e = max_err(case, key, got[key], out[key])
+        assert e <= TOL_RIC, f"{case.name}: {key} err {e:.3e}"
 
 
 def _valid_len(case, key, k):
@@ -101,6 +150,13 @@ def max_err(case, key, got, ref):
 
 def check_case(case, got):
     """Assert parity of `got` against the golden outputs of `case`."""
+    if case.kind == "pcond":
+        return check_pcond(case, got)
+    if case.kind == "pcond_sv":
+        for key in ("ux", "pi"):
+            e = max_err(case, key, got[key], case.out[key])
+            assert e <= TOL_PCOND_SV, f"{case.name}: {key} err {e:.3e}"
+        return
     out = case.out
     if "kk" in out:
         assert int(got["kk"]) == int(out["kk"]), (case.name, got["kk"], out["kk"])
