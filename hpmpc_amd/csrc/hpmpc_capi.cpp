@@ -24,6 +24,12 @@
 
 extern "C" int hk_launch(int which, const KArgs* a, int count, hipStream_t stream);
 extern "C" int hk_fixcls(int nu, int nx);
+// wide-stage path (hpmpc_capi_wide.cpp)
+extern "C" long long hk_wide_factor_bytes(int N, const int* nx, const int* nu);
+extern "C" void hk_wide_sv_entry(int N, int* nx, int* nu, int* nb, int** idxb, int* ng, int update_b, double** hpBAbt,
+                                 double** b, int update_q, double** hpQ, double** q, double** bd, double** Qx,
+                                 double** qx, double** hux, int compute_pi, double** hpi, int compute_Pb, double** hPb,
+                                 double* memory);
 
 namespace {
 
@@ -53,6 +59,14 @@ bool hip_ok(hipError_t e, const char* what) {
 }
 
 }  // namespace
+
+// error reporting shared with the wide-stage translation unit
+extern "C" void hk_set_error(int code, const char* what) {
+    if (code)
+        set_err(code, what);
+    else
+        g_err = 0;
+}
 
 // ------------------------------------------------------------------------------------------------
 // Plan: stage tables shared by every problem of a batch.
@@ -741,7 +755,9 @@ extern "C" int d_back_ric_rec_sv_tv_memory_space_size_bytes(int N, int* nx, int*
     (void)nu;
     (void)nb;
     (void)ng;
-    return (int)(((long long)(N + 1) * FSTRIDE * 8 + 63) / 64 * 64);
+    // the larger of the tile image and the wide-stage factor (nu+nx > 16 stages run on the wide path)
+    const long long tile = (long long)(N + 1) * FSTRIDE * 8, wide = hk_wide_factor_bytes(N, nx, nu);
+    return (int)(((tile > wide ? tile : wide) + 63) / 64 * 64);
 }
 
 extern "C" void d_back_ric_rec_sv_tv_res(int N, int* nx, int* nu, int* nb, int** idxb, int* ng, int update_b,
@@ -751,6 +767,14 @@ extern "C" void d_back_ric_rec_sv_tv_res(int N, int* nx, int* nu, int* nb, int**
                                          double* work) {
     (void)work;
     g_err = 0;
+    {
+        const char* why = nullptr;
+        if (!plan_supported(N, nx, nu, nb, idxb, ng, &why)) {  // stages beyond the 16-wide tile
+            hk_wide_sv_entry(N, nx, nu, nb, idxb, ng, update_b, hpBAbt, b, update_q, hpQ, q, bd, Qx, qx, hux,
+                             compute_pi, hpi, compute_Pb, hPb, memory);
+            return;
+        }
+    }
     hpmpc_mi355x_plan* P = g_ctx.get_plan(N, nx, nu, nb, idxb, ng);
     if (!P) return;
     Arena A = arena(P, 1);

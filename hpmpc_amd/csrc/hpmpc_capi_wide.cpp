@@ -1,0 +1,805 @@
+// hpmpc_capi_wide.cpp -- host side of the wide-stage path (hk_wide.hip):
+//   * d_back_ric_rec_sv_tv_res for stages beyond the 16-wide register tile (routed here by hpmpc_capi.cpp);
+//   * partial condensing, the §8f #1 row: d_part_cond_compute_problem_size / _work_space_size_bytes /
+//     _memory_space_size_bytes / d_part_cond / d_part_expand_work_space_size_bytes / d_part_expand_solution
+//     (lqcp_solvers/d_part_cond.c:694-1308) with the reference prototypes, on host lib4 buffers;
+//   * the batched device API of the same pipeline (hpmpc_mi355x_pcond_*), data resident in HBM.
+// Every computation runs on the GPU; the host only packs stage tables and copies buffers.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "../../include/hpmpc_mi355x.h"
+#include "hk_wide_args.h"
+
+extern "C" int hk_wide_launch(int which, const void* args, int count, int lds_doubles, hipStream_t stream);
+extern "C" void hk_set_error(int code, const char* what);
+
+namespace {
+
+constexpr int BS = 4, NCL = 2;
+constexpr int LDS_MAX_DOUBLES = 65536 / 8;
+
+inline int rup(int n, int m) { return (n + m - 1) / m * m; }
+inline double& P4(double* A, int sd, int i, int j) { return A[(i / BS) * BS * sd + i % BS + BS * j]; }
+inline int poff(int j, int nz) { return j * nz - (j * (j - 1)) / 2; }
+
+bool hip_ok(hipError_t e, const char* what) {
+    if (e == hipSuccess) return true;
+    char msg[256];
+    snprintf(msg, sizeof msg, "HIP error in %s: %s", what, hipGetErrorString(e));
+    hk_set_error(HPMPC_MI355X_EHIP, msg);
+    return false;
+}
+
+// One problem's packed layout on the wide path (offsets in doubles; idxb in ints).
+struct WLayout {
+    int N = 0;
+    std::vector<WideStage> st;
+    long long nB = 0, nR = 0, nL = 0, nU = 0, nP = 0, nD = 0, nI = 0;
+    int lds = 0, offW = 0, offX = 0, offV = 0, ldW = 0, ldX = 0;
+    bool any_ng = false;
+};
+
+WLayout make_layout(int N, const int* nx, const int* nu, const int* nb, const int* ng) {
+    WLayout L;
+    L.N = N;
+    L.st.resize(N + 1);
+    int Mmax = 1, nzM = 1, nxM = 1;
+    for (int k = 0; k <= N; k++) {
+        WideStage& s = L.st[k];
+        memset(&s, 0, sizeof s);
+        s.nu = k < N ? nu[k] : 0;
+        s.nx = nx[k];
+        s.nx1 = k < N ? nx[k + 1] : 0;
+        s.nu1 = k + 1 < N ? nu[k + 1] : 0;
+        const int nux = s.nu + s.nx;
+        s.sdB = rup(s.nx1, NCL);
+        s.sdR = rup(nux, NCL);
+        s.oB = (int)L.nB;
+        if (k < N) L.nB += (long long)rup(nux + 1, BS) * s.sdB;
+        s.oR = (int)L.nR;
+        L.nR += (long long)rup(nux + 1, BS) * s.sdR;
+        s.oL = (int)L.nL;
+        L.nL += poff(nux, nux + 1) + nux;
+        L.nL = (L.nL + 7) / 8 * 8;
+        s.oU = (int)L.nU;
+        L.nU += rup(nux + 1, 8);
+        s.oP = (int)L.nP;
+        L.nP += rup(s.nx1 + 1, 8);
+        s.nb = nb[k];
+        s.pnb = rup(nb[k], BS);
+        s.ng = ng[k];
+        s.oD = (int)L.nD;
+        L.nD += 2 * s.pnb + 2 * rup(ng[k], BS);
+        s.oI = (int)L.nI;
+        L.nI += nb[k];
+        if (ng[k] > 0) L.any_ng = true;
+        Mmax = std::max(Mmax, poff(nux, nux + 1));
+        nzM = std::max(nzM, nux + 1);
+        nxM = std::max(nxM, std::max(s.nx1, s.nx));  // X also receives stage k's own Lxx
+    }
+    L.ldW = nzM;
+    L.ldX = nxM + 1;
+    L.offW = Mmax;
+    L.offX = L.offW + L.ldW * nxM;
+    L.offV = L.offX + L.ldX * nxM;
+    L.lds = L.offV + nzM;
+    if (L.nD == 0) L.nD = 1;
+    if (L.nI == 0) L.nI = 1;
+    if (L.nB == 0) L.nB = 1;
+    return L;
+}
+
+// Thread-local device context of the host-buffer entry points: one stream, a growable device arena and
+// its pinned staging twin.
+struct WCtx {
+    hipStream_t stream = nullptr;
+    char* dev = nullptr;
+    char* host = nullptr;
+    size_t cap = 0;
+    ~WCtx() {
+        if (dev) (void)hipFree(dev);
+        if (host) (void)hipHostFree(host);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+    bool ensure(size_t bytes) {
+        if (!stream && !hip_ok(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "stream create")) return false;
+        if (bytes > cap) {
+            if (dev) (void)hipFree(dev);
+            if (host) (void)hipHostFree(host);
+            dev = host = nullptr;
+            cap = 0;
+            if (!hip_ok(hipMalloc((void**)&dev, bytes), "wide device arena")) return false;
+            if (!hip_ok(hipHostMalloc((void**)&host, bytes, 0), "wide pinned arena")) return false;
+            cap = bytes;
+        }
+        memset(host, 0, bytes);
+        return true;
+    }
+    bool up(size_t bytes) {
+        return hip_ok(hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, stream), "H2D");
+    }
+    bool down(size_t bytes) {
+        return hip_ok(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, stream), "D2H") &&
+               hip_ok(hipStreamSynchronize(stream), "sync");
+    }
+};
+thread_local WCtx g_w;
+
+// Byte carve of the staging arena.
+struct Carve {
+    size_t o = 0;
+    size_t take(size_t bytes) {
+        size_t r = o;
+        o += (bytes + 255) / 256 * 256;
+        return r;
+    }
+};
+
+bool launch(int which, const void* args, int count, int lds, hipStream_t stream, const char* name) {
+    if (lds > LDS_MAX_DOUBLES) {
+        hk_set_error(HPMPC_MI355X_EUNSUPPORTED, "wide stage beyond the 64 KiB LDS tile budget");
+        return false;
+    }
+    int e = hk_wide_launch(which, args, count, lds, stream);
+    if (e) {
+        char msg[128];
+        snprintf(msg, sizeof msg, "%s launch failed (%d)", name, e);
+        hk_set_error(HPMPC_MI355X_EHIP, msg);
+        return false;
+    }
+    return true;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------
+// d_back_ric_rec_sv_tv_res on wide stages (called by hpmpc_capi.cpp when the tile path does not fit).
+// ------------------------------------------------------------------------------------------------
+extern "C" long long hk_wide_factor_bytes(int N, const int* nx, const int* nu) {
+    long long s = 0;
+    for (int k = 0; k <= N; k++) {
+        const int nux = (k < N ? nu[k] : 0) + nx[k];
+        s += poff(nux, nux + 1) + nux;
+        s = (s + 7) / 8 * 8;
+    }
+    return s * 8;
+}
+
+extern "C" void hk_wide_sv_entry(int N, int* nx, int* nu, int* nb, int** idxb, int* ng, int update_b, double** hpBAbt,
+                                 double** b, int update_q, double** hpQ, double** q, double** bd, double** Qx,
+                                 double** qx, double** hux, int compute_pi, double** hpi, int compute_Pb, double** hPb,
+                                 double* memory) {
+    hk_set_error(0, nullptr);
+    WLayout L = make_layout(N, nx, nu, nb, ng);
+    if (L.any_ng) {
+        hk_set_error(HPMPC_MI355X_EUNSUPPORTED, "wide stages (nu+nx > 16) with general constraints");
+        return;
+    }
+    if (L.lds > LDS_MAX_DOUBLES) {
+        hk_set_error(HPMPC_MI355X_EUNSUPPORTED, "wide stage beyond the 64 KiB LDS tile budget");
+        return;
+    }
+    Carve c;
+    const size_t oSt = c.take(sizeof(WideStage) * (N + 1)), oB = c.take(8 * L.nB), oR = c.take(8 * L.nR),
+                 oF = c.take(8 * L.nL), oU = c.take(8 * L.nU), oP = c.take(8 * L.nP), oPb = c.take(8 * L.nP);
+    if (!g_w.ensure(c.o)) return;
+    char* H = g_w.host;
+    memcpy(H + oSt, L.st.data(), sizeof(WideStage) * (N + 1));
+    double* HB = reinterpret_cast<double*>(H + oB);
+    double* HR = reinterpret_cast<double*>(H + oR);
+    // the reference's in-place side effects, in its stage order (d_back_ric_rec.c:197-209, :249-291)
+    for (int k = N; k >= 0; k--) {
+        const WideStage& s = L.st[k];
+        const int nux = s.nu + s.nx;
+        if (update_q)
+            for (int j = 0; j < nux; j++) P4(hpQ[k], s.sdR, nux, j) = q[k][j];
+        for (int l = 0; l < nb[k]; l++) {
+            const int ii = idxb[k][l];
+            P4(hpQ[k], s.sdR, ii, ii) = bd[k][l] + Qx[k][l];
+        }
+        for (int l = 0; l < nb[k]; l++) P4(hpQ[k], s.sdR, nux, idxb[k][l]) += qx[k][l];
+        memcpy(HR + s.oR, hpQ[k], (size_t)rup(nux + 1, BS) * s.sdR * sizeof(double));
+        if (k < N) {
+            if (update_b)
+                for (int j = 0; j < s.nx1; j++) P4(hpBAbt[k], s.sdB, nux, j) = b[k][j];
+            memcpy(HB + s.oB, hpBAbt[k], (size_t)rup(nux + 1, BS) * s.sdB * sizeof(double));
+        }
+    }
+    char* D = g_w.dev;
+    WideArgs a;
+    memset(&a, 0, sizeof a);
+    a.N = N;
+    a.nprob = 1;
+    a.st = reinterpret_cast<const WideStage*>(D + oSt);
+    a.BAbt = reinterpret_cast<const double*>(D + oB);
+    a.RSQ = reinterpret_cast<const double*>(D + oR);
+    a.ws = reinterpret_cast<double*>(D + oF);
+    a.ux = reinterpret_cast<double*>(D + oU);
+    a.pi = reinterpret_cast<double*>(D + oP);
+    a.Pb = reinterpret_cast<double*>(D + oPb);
+    a.compute_pi = compute_pi;
+    a.compute_Pb = compute_Pb;
+    a.offW = L.offW;
+    a.offX = L.offX;
+    a.offV = L.offV;
+    a.ldW = L.ldW;
+    a.ldX = L.ldX;
+    if (!g_w.up(c.o) || !launch(0, &a, 1, L.lds, g_w.stream, "hk_wide_sv") || !g_w.down(c.o)) return;
+    const double* HU = reinterpret_cast<const double*>(H + oU);
+    const double* HP = reinterpret_cast<const double*>(H + oP);
+    const double* HPb = reinterpret_cast<const double*>(H + oPb);
+    for (int k = 0; k <= N; k++) {
+        const WideStage& s = L.st[k];
+        memcpy(hux[k], HU + s.oU, (s.nu + s.nx) * sizeof(double));
+        if (k < N && compute_pi) memcpy(hpi[k], HP + s.oP, s.nx1 * sizeof(double));
+        if (k < N && compute_Pb) memcpy(hPb[k], HPb + s.oP, s.nx1 * sizeof(double));
+    }
+    memcpy(memory, H + oF, 8 * L.nL);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Partial condensing: host bookkeeping shared by the single-problem and the batched entry points.
+// ------------------------------------------------------------------------------------------------
+namespace {
+
+int block_len(int N, int N2, int ii) {
+    const int N1 = N / N2, R1 = N - N2 * N1, M1 = R1 > 0 ? N1 + 1 : N1;
+    return ii < R1 ? M1 : N1;
+}
+
+struct PcPlan {
+    int N = 0, N2 = 0;
+    WLayout orig, cond;
+    std::vector<int> nx2, nu2, nb2, ng2;
+    std::vector<PcBlock> blk;
+    std::vector<int> idxb;  // original idxb packed per stage (orig.st[k].oI)
+    long long nG = 0;       // Gamma scratch (doubles per problem)
+    long long nG2 = 0;      // condensed DCt2 (doubles per problem)
+    long long ref_d = 0;    // the reference's memory carve: doubles before the idxb2 ints
+    int pc_lds = 0, ldP = 0, ldX = 0, ldW = 0, ldB = 0, offP = 0, offX = 0, offW = 0, offB = 0;
+    int px_lds = 0;
+};
+
+void problem_size(int N, const int* nx, const int* nu, const int* nb, const int* const* hidxb, const int* ng, int N2,
+                  int* nx2, int* nu2, int* nb2, int* ng2) {
+    int N_tmp = 0;
+    for (int ii = 0; ii < N2; ii++) {
+        const int T1 = block_len(N, N2, ii);
+        nx2[ii] = nx[N_tmp];
+        nu2[ii] = nu[N_tmp];
+        nb2[ii] = nb[N_tmp];
+        ng2[ii] = ng[N_tmp];
+        for (int jj = 1; jj < T1; jj++) {
+            const int s = N_tmp + jj;
+            int nbb = 0, nbg = 0;
+            for (int kk = 0; kk < nb[s]; kk++) (hidxb[s][kk] < nu[s] ? nbb : nbg)++;
+            nu2[ii] += nu[s];
+            nb2[ii] += nbb;
+            ng2[ii] += ng[s] + nbg;
+        }
+        N_tmp += T1;
+    }
+    nx2[N2] = nx[N];
+    nu2[N2] = nu[N];
+    nb2[N2] = nb[N];
+    ng2[N2] = ng[N];
+}
+
+bool pc_plan(PcPlan& P, int N, const int* nx, const int* nu_in, const int* nb, const int* const* idxb, const int* ng,
+             int N2) {
+    if (N2 < 1 || N2 > N) {  // N2 == N: blocks of one stage (d_part_cond itself aliases instead, :936)
+        hk_set_error(HPMPC_MI355X_EUNSUPPORTED, "partial condensing needs 1 <= N2 <= N (:962-967)");
+        return false;
+    }
+    for (int k = 0; k < N; k++)
+        if (ng[k] > 0) {  // d_part_cond.c:971-976: only ng[N] > 0 is supported by the reference
+            hk_set_error(HPMPC_MI355X_EUNSUPPORTED, "partial condensing with ng > 0 before the last stage");
+            return false;
+        }
+    std::vector<int> nu(nu_in, nu_in + N + 1);
+    nu[N] = 0;
+    P.N = N;
+    P.N2 = N2;
+    P.orig = make_layout(N, nx, nu.data(), nb, ng);
+    P.idxb.assign(P.orig.nI, 0);
+    for (int k = 0; k <= N; k++)
+        for (int l = 0; l < nb[k]; l++) P.idxb[P.orig.st[k].oI + l] = idxb[k][l];
+    P.nx2.resize(N2 + 1);
+    P.nu2.resize(N2 + 1);
+    P.nb2.resize(N2 + 1);
+    P.ng2.resize(N2 + 1);
+    problem_size(N, nx, nu.data(), nb, idxb, ng, N2, P.nx2.data(), P.nu2.data(), P.nb2.data(), P.ng2.data());
+    P.cond = make_layout(N2, P.nx2.data(), P.nu2.data(), P.nb2.data(), P.ng2.data());
+    P.blk.resize(N2);
+    int N_tmp = 0, nzM = 1, nxM = 1;
+    long long oG2 = 0, ref_d = 0;
+    for (int ii = 0; ii < N2; ii++) {
+        PcBlock& b = P.blk[ii];
+        memset(&b, 0, sizeof b);
+        b.s0 = N_tmp;
+        b.T = block_len(N, N2, ii);
+        b.nx0 = nx[N_tmp];
+        b.nut = 0;
+        b.oG = (int)P.nG;
+        int rows = b.nx0 + 1;
+        for (int j = 0; j < b.T; j++) {
+            const int s = N_tmp + j;
+            b.nut += nu[s];
+            rows += nu[s];
+            P.nG += (long long)rows * nx[s + 1];
+            nzM = std::max(nzM, nu[s] + nx[s] + 1);
+            nxM = std::max(nxM, nx[s + 1]);
+        }
+        b.oB2 = P.cond.st[ii].oB;
+        b.oR2 = P.cond.st[ii].oR;
+        b.oD2 = P.cond.st[ii].oD;
+        b.oI2 = P.cond.st[ii].oI;
+        b.oG2 = (int)oG2;
+        oG2 += (long long)rup(P.nu2[ii] + P.nx2[ii], BS) * rup(P.ng2[ii], NCL);
+        b.nx2n = P.nx2[ii + 1];
+        b.nb2 = P.nb2[ii];
+        b.ng2 = P.ng2[ii];
+        N_tmp += b.T;
+        // the reference's carve of `memory` (d_part_cond.c:1013-1041), doubles part
+        const int pnz2 = rup(P.nu2[ii] + P.nx2[ii] + 1, BS);
+        ref_d += (long long)pnz2 * rup(P.nx2[ii + 1], NCL) + (long long)pnz2 * rup(P.nu2[ii] + P.nx2[ii], NCL) +
+                 (long long)rup(P.nu2[ii] + P.nx2[ii], BS) * rup(P.ng2[ii], NCL) + 2 * rup(P.nb2[ii], BS) +
+                 2 * rup(P.ng2[ii], BS);
+    }
+    P.nG2 = oG2 > 0 ? oG2 : 1;
+    P.ref_d = ref_d;
+    P.ldP = P.ldW = P.ldB = nzM;
+    P.ldX = nxM + 1;
+    P.offP = 0;
+    P.offX = P.ldP * nzM;
+    P.offW = P.offX + P.ldX * nxM;
+    P.offB = P.offW + P.ldW * nxM;
+    P.pc_lds = P.offB + P.ldB * nxM;
+    P.px_lds = nzM;
+    if (P.pc_lds > LDS_MAX_DOUBLES) {
+        hk_set_error(HPMPC_MI355X_EUNSUPPORTED, "condensing stage tiles beyond the 64 KiB LDS budget");
+        return false;
+    }
+    return true;
+}
+
+void fill_pc_args(const PcPlan& P, PcArgs& a) {
+    memset(&a, 0, sizeof a);
+    a.N = P.N;
+    a.N2 = P.N2;
+    a.sB = P.orig.nB;
+    a.sR = P.orig.nR;
+    a.sD = P.orig.nD;
+    a.sG = P.nG;
+    a.sB2 = P.cond.nB;
+    a.sR2 = P.cond.nR;
+    a.sG2 = P.nG2;
+    a.sD2 = P.cond.nD;
+    a.oR2N = P.cond.st[P.N2].oR;
+    a.sdRN = P.orig.st[P.N].sdR;
+    a.nzN = P.orig.st[P.N].nu + P.orig.st[P.N].nx + 1;
+    a.offP = P.offP;
+    a.offX = P.offX;
+    a.offW = P.offW;
+    a.offB = P.offB;
+    a.ldP = P.ldP;
+    a.ldX = P.ldX;
+    a.ldW = P.ldW;
+    a.ldB = P.ldB;
+}
+
+void fill_px_args(const PcPlan& P, PxArgs& a) {
+    memset(&a, 0, sizeof a);
+    a.N = P.N;
+    a.N2 = P.N2;
+    a.sB = P.orig.nB;
+    a.sR = P.orig.nR;
+    a.sU = P.orig.nU;
+    a.sP = P.orig.nP;
+    a.sC = P.orig.nD;
+    a.sU2 = P.cond.nU;
+    a.sP2 = P.cond.nP;
+    a.sC2 = P.cond.nD;
+    a.offV = 0;
+    a.offW = 0;
+}
+
+}  // namespace
+
+// d_part_cond.c:694-738 -- integer bookkeeping (no device work)
+extern "C" void d_part_cond_compute_problem_size(int N, int* nx, int* nu, int* nb, int** hidxb, int* ng, int N2,
+                                                 int* nx2, int* nu2, int* nb2, int* ng2) {
+    problem_size(N, nx, nu, nb, hidxb, ng, N2, nx2, nu2, nb2, ng2);
+}
+
+// every temporary of the condensing lives on the device
+extern "C" int d_part_cond_work_space_size_bytes(int N, int* nx, int* nu, int* nb, int** hidxb, int* ng, int N2,
+                                                 int* nx2, int* nu2, int* nb2, int* ng2) {
+    return 64;
+}
+
+// d_part_cond.c:868-924: the condensed data are written into `memory` with the reference's carve
+extern "C" int d_part_cond_memory_space_size_bytes(int N, int* nx, int* nu, int* nb, int** hidxb, int* ng, int N2,
+                                                   int* nx2, int* nu2, int* nb2, int* ng2) {
+    if (N2 == N) return 0;
+    long long d_size = 0, i_size = 0;
+    for (int ii = 0; ii < N2; ii++) {
+        const int pnz2 = rup(nu2[ii] + nx2[ii] + 1, BS), pnux2 = rup(nu2[ii] + nx2[ii], BS);
+        d_size += (long long)pnz2 * rup(nx2[ii + 1], NCL) + (long long)pnz2 * rup(nu2[ii] + nx2[ii], NCL) +
+                  (long long)pnux2 * rup(ng2[ii], NCL) + 2 * rup(nb2[ii], BS) + 2 * rup(ng2[ii], BS);
+        i_size += nb2[ii];
+    }
+    return (int)((d_size * 8 + i_size * 4 + 63) / 64 * 64);
+}
+
+// d_part_cond.c:926-1062
+extern "C" void d_part_cond(int N, int* nx, int* nu, int* nb, int** hidxb, int* ng, double** hpBAbt, double** hpRSQrq,
+                            double** hpDCt, double** hd, int N2, int* nx2, int* nu2, int* nb2, int** hidxb2, int* ng2,
+                            double** hpBAbt2, double** hpRSQrq2, double** hpDCt2, double** hd2, void* memory,
+                            void* work) {
+    (void)work;
+    hk_set_error(0, nullptr);
+    if (N2 == N) {  // :936-960: the condensed problem aliases the original
+        for (int ii = 0; ii <= N; ii++) {
+            nx2[ii] = nx[ii];
+            nu2[ii] = nu[ii];
+            nb2[ii] = nb[ii];
+            hidxb2[ii] = hidxb[ii];
+            ng2[ii] = ng[ii];
+            if (ii < N) hpBAbt2[ii] = hpBAbt[ii];
+            hpRSQrq2[ii] = hpRSQrq[ii];
+            hpDCt2[ii] = hpDCt[ii];
+            hd2[ii] = hd[ii];
+        }
+        return;
+    }
+    PcPlan P;
+    if (!pc_plan(P, N, nx, nu, nb, hidxb, ng, N2)) return;
+    const WLayout &O = P.orig, &C = P.cond;
+    // the condensed outputs go into one buffer with the reference's carve (BAbt2 | RSQrq2 | DCt2 | d2 | idxb2,
+    // d_part_cond.c:1013-1041), downloaded into `memory` as is; the kernel's copy of the terminal RSQrq
+    // lands past it (the reference aliases hpRSQrq[N] there instead)
+    const long long term_off = P.ref_d + (4 * C.nI + 7) / 8 + 8;
+    const long long mem_doubles = term_off + (long long)rup(O.st[N].nu + O.st[N].nx + 1, BS) * O.st[N].sdR;
+    Carve c;
+    const size_t oSt = c.take(sizeof(WideStage) * (N + 1)), oBlk = c.take(sizeof(PcBlock) * N2),
+                 oIdx = c.take(4 * O.nI), oB = c.take(8 * O.nB), oR = c.take(8 * O.nR), oD = c.take(8 * O.nD),
+                 oG = c.take(8 * P.nG), oMem = c.take(8 * mem_doubles);
+    if (!g_w.ensure(c.o)) return;
+    char* H = g_w.host;
+    memcpy(H + oSt, O.st.data(), sizeof(WideStage) * (N + 1));
+    // condensed outputs go straight into the reference carve inside one buffer (oMem): BAbt2 | RSQrq2 |
+    // DCt2 | d2 | idxb2, so the block offsets are absolute within that buffer
+    std::vector<PcBlock> blk = P.blk;
+    long long o = 0;
+    std::vector<long long> cB(N2), cR(N2), cG(N2), cD(N2);
+    for (int ii = 0; ii < N2; ii++) {
+        cB[ii] = o;
+        o += (long long)rup(P.nu2[ii] + P.nx2[ii] + 1, BS) * rup(P.nx2[ii + 1], NCL);
+    }
+    for (int ii = 0; ii < N2; ii++) {
+        cR[ii] = o;
+        o += (long long)rup(P.nu2[ii] + P.nx2[ii] + 1, BS) * rup(P.nu2[ii] + P.nx2[ii], NCL);
+    }
+    for (int ii = 0; ii < N2; ii++) {
+        cG[ii] = o;
+        o += (long long)rup(P.nu2[ii] + P.nx2[ii], BS) * rup(P.ng2[ii], NCL);
+    }
+    for (int ii = 0; ii < N2; ii++) {
+        cD[ii] = o;
+        o += 2 * rup(P.nb2[ii], BS) + 2 * rup(P.ng2[ii], BS);
+    }
+    int oi = 0;
+    for (int ii = 0; ii < N2; ii++) {
+        blk[ii].oB2 = (int)cB[ii];
+        blk[ii].oR2 = (int)cR[ii];
+        blk[ii].oG2 = (int)cG[ii];
+        blk[ii].oD2 = (int)cD[ii];
+        blk[ii].oI2 = oi;
+        oi += P.nb2[ii];
+    }
+    memcpy(H + oBlk, blk.data(), sizeof(PcBlock) * N2);
+    memcpy(H + oIdx, P.idxb.data(), 4 * O.nI);
+    double* HB = reinterpret_cast<double*>(H + oB);
+    double* HR = reinterpret_cast<double*>(H + oR);
+    double* HD = reinterpret_cast<double*>(H + oD);
+    for (int k = 0; k <= N; k++) {
+        const WideStage& s = O.st[k];
+        const int nux = s.nu + s.nx;
+        if (k < N) memcpy(HB + s.oB, hpBAbt[k], (size_t)rup(nux + 1, BS) * s.sdB * sizeof(double));
+        memcpy(HR + s.oR, hpRSQrq[k], (size_t)rup(nux + 1, BS) * s.sdR * sizeof(double));
+        if (nb[k] + ng[k] > 0) memcpy(HD + s.oD, hd[k], (size_t)(2 * s.pnb + 2 * rup(ng[k], BS)) * sizeof(double));
+    }
+    char* D = g_w.dev;
+    PcArgs a;
+    fill_pc_args(P, a);
+    a.nprob = 1;
+    a.st = reinterpret_cast<const WideStage*>(D + oSt);
+    a.blk = reinterpret_cast<const PcBlock*>(D + oBlk);
+    a.idxb = reinterpret_cast<const int*>(D + oIdx);
+    a.BAbt = reinterpret_cast<const double*>(D + oB);
+    a.RSQ = reinterpret_cast<const double*>(D + oR);
+    a.d = reinterpret_cast<const double*>(D + oD);
+    a.G = reinterpret_cast<double*>(D + oG);
+    double* mem = reinterpret_cast<double*>(D + oMem);
+    a.BAbt2 = a.RSQ2 = a.DCt2 = a.d2 = mem;
+    a.idxb2 = reinterpret_cast<int*>(mem + P.ref_d);
+    a.oR2N = (int)term_off;
+    if (!g_w.up(c.o) || !launch(1, &a, 1, P.pc_lds, g_w.stream, "hk_pcond") || !g_w.down(c.o)) return;
+    for (int ii = 0; ii <= N2; ii++) {
+        nx2[ii] = P.nx2[ii];
+        nu2[ii] = P.nu2[ii];
+        nb2[ii] = P.nb2[ii];
+        ng2[ii] = P.ng2[ii];
+    }
+    memcpy(memory, H + oMem, 8 * P.ref_d + 4 * (C.nI > 0 ? oi : 0));
+    double* m = static_cast<double*>(memory);
+    int* mi = reinterpret_cast<int*>(m + P.ref_d);
+    for (int ii = 0; ii < N2; ii++) {
+        hpBAbt2[ii] = m + cB[ii];
+        hpRSQrq2[ii] = m + cR[ii];
+        hpDCt2[ii] = m + cG[ii];
+        hd2[ii] = m + cD[ii];
+        hidxb2[ii] = mi + blk[ii].oI2;
+    }
+    hpRSQrq2[N2] = hpRSQrq[N];
+    hpDCt2[N2] = hpDCt[N];
+    hd2[N2] = hd[N];
+    hidxb2[N2] = hidxb[N];
+}
+
+extern "C" int d_part_expand_work_space_size_bytes(int N, int* nx, int* nu, int* nb, int* ng) { return 64; }
+
+// d_part_cond.c:1103-1308
+extern "C" void d_part_expand_solution(int N, int* nx, int* nu, int* nb, int** hidxb, int* ng, double** hpBAbt,
+                                       double** hb, double** hpRSQrq, double** hrq, double** hpDCt, double** hux,
+                                       double** hpi, double** hlam, double** ht, int N2, int* nx2, int* nu2, int* nb2,
+                                       int** hidxb2, int* ng2, double** hux2, double** hpi2, double** hlam2,
+                                       double** ht2, void* work) {
+    (void)work;
+    (void)hpDCt;  // only the last stage may carry general constraints (d_part_cond.c:971-976): copied, not used
+    (void)hidxb2;
+    hk_set_error(0, nullptr);
+    PcPlan P;
+    if (!pc_plan(P, N, nx, nu, nb, hidxb, ng, N2)) return;
+    const WLayout &O = P.orig, &C = P.cond;
+    Carve c;
+    const size_t oSt = c.take(sizeof(WideStage) * (N + 1)), oSt2 = c.take(sizeof(WideStage) * (N2 + 1)),
+                 oBlk = c.take(sizeof(PcBlock) * N2), oIdx = c.take(4 * O.nI), oB = c.take(8 * O.nB),
+                 oR = c.take(8 * O.nR), ohb = c.take(8 * O.nP), orq = c.take(8 * O.nU), oU2 = c.take(8 * C.nU),
+                 oP2 = c.take(8 * C.nP), oL2 = c.take(8 * C.nD), oT2 = c.take(8 * C.nD), oU = c.take(8 * O.nU),
+                 oP = c.take(8 * O.nP), oL = c.take(8 * O.nD), oT = c.take(8 * O.nD);
+    if (!g_w.ensure(c.o)) return;
+    char* H = g_w.host;
+    memcpy(H + oSt, O.st.data(), sizeof(WideStage) * (N + 1));
+    memcpy(H + oSt2, C.st.data(), sizeof(WideStage) * (N2 + 1));
+    memcpy(H + oBlk, P.blk.data(), sizeof(PcBlock) * N2);
+    memcpy(H + oIdx, P.idxb.data(), 4 * O.nI);
+    auto dp = [&](size_t off) { return reinterpret_cast<double*>(H + off); };
+    for (int k = 0; k <= N; k++) {
+        const WideStage& s = O.st[k];
+        const int nux = s.nu + s.nx;
+        if (k < N) {
+            memcpy(dp(oB) + s.oB, hpBAbt[k], (size_t)rup(nux + 1, BS) * s.sdB * sizeof(double));
+            memcpy(dp(ohb) + s.oP, hb[k], s.nx1 * sizeof(double));
+        }
+        memcpy(dp(oR) + s.oR, hpRSQrq[k], (size_t)rup(nux + 1, BS) * s.sdR * sizeof(double));
+        memcpy(dp(orq) + s.oU, hrq[k], nux * sizeof(double));
+    }
+    for (int k = 0; k <= N2; k++) {
+        const WideStage& s = C.st[k];
+        memcpy(dp(oU2) + s.oU, hux2[k], (s.nu + s.nx) * sizeof(double));
+        if (k < N2) memcpy(dp(oP2) + s.oP, hpi2[k], s.nx1 * sizeof(double));
+        const int nc = 2 * s.pnb + 2 * rup(s.ng, BS);
+        if (nc > 0) {
+            memcpy(dp(oL2) + s.oD, hlam2[k], nc * sizeof(double));
+            memcpy(dp(oT2) + s.oD, ht2[k], nc * sizeof(double));
+        }
+    }
+    char* D = g_w.dev;
+    auto dd = [&](size_t off) { return reinterpret_cast<double*>(D + off); };
+    PxArgs a;
+    fill_px_args(P, a);
+    a.nprob = 1;
+    a.st = reinterpret_cast<const WideStage*>(D + oSt);
+    a.st2 = reinterpret_cast<const WideStage*>(D + oSt2);
+    a.blk = reinterpret_cast<const PcBlock*>(D + oBlk);
+    a.idxb = reinterpret_cast<const int*>(D + oIdx);
+    a.BAbt = dd(oB);
+    a.RSQ = dd(oR);
+    a.hb = dd(ohb);
+    a.hrq = dd(orq);
+    a.ux2 = dd(oU2);
+    a.pi2 = dd(oP2);
+    a.lam2 = dd(oL2);
+    a.t2 = dd(oT2);
+    a.ux = dd(oU);
+    a.pi = dd(oP);
+    a.lam = dd(oL);
+    a.t = dd(oT);
+    if (!g_w.up(c.o) || !launch(2, &a, 1, P.px_lds, g_w.stream, "hk_pexpand") || !g_w.down(c.o)) return;
+    for (int k = 0; k <= N; k++) {
+        const WideStage& s = O.st[k];
+        memcpy(hux[k], dp(oU) + s.oU, (s.nu + s.nx) * sizeof(double));
+        if (k < N) memcpy(hpi[k], dp(oP) + s.oP, s.nx1 * sizeof(double));
+        const int nc = 2 * s.pnb + 2 * rup(s.ng, BS);
+        if (s.nb + s.ng > 0) {
+            // only the slots the reference writes: boxes [0, nb) / [pnb, pnb+nb) and, at N, the generals
+            for (int l = 0; l < s.nb; l++) {
+                hlam[k][l] = dp(oL)[s.oD + l];
+                hlam[k][s.pnb + l] = dp(oL)[s.oD + s.pnb + l];
+                ht[k][l] = dp(oT)[s.oD + l];
+                ht[k][s.pnb + l] = dp(oT)[s.oD + s.pnb + l];
+            }
+            if (k == N)
+                for (int l = 2 * s.pnb; l < nc; l++) {
+                    hlam[k][l] = dp(oL)[s.oD + l];
+                    ht[k][l] = dp(oT)[s.oD + l];
+                }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Batched device API of the partial-condensing pipeline (data resident in HBM, problem-major).
+// ------------------------------------------------------------------------------------------------
+struct hpmpc_mi355x_pcond_plan {
+    PcPlan P;
+    WideStage *d_st = nullptr, *d_st2 = nullptr;
+    PcBlock* d_blk = nullptr;
+    int* d_idxb = nullptr;
+    int* d_idxb2 = nullptr;
+};
+
+extern "C" void hpmpc_mi355x_pcond_plan_destroy(hpmpc_mi355x_pcond_plan* q) {
+    if (!q) return;
+    if (q->d_st) (void)hipFree(q->d_st);
+    if (q->d_st2) (void)hipFree(q->d_st2);
+    if (q->d_blk) (void)hipFree(q->d_blk);
+    if (q->d_idxb) (void)hipFree(q->d_idxb);
+    if (q->d_idxb2) (void)hipFree(q->d_idxb2);
+    delete q;
+}
+
+extern "C" hpmpc_mi355x_pcond_plan* hpmpc_mi355x_pcond_plan_create(int N, const int* nx, const int* nu, const int* nb,
+                                                                   const int* const* idxb, const int* ng, int N2) {
+    hk_set_error(0, nullptr);
+    auto* q = new hpmpc_mi355x_pcond_plan();
+    if (!pc_plan(q->P, N, nx, nu, nb, idxb, ng, N2)) {
+        delete q;
+        return nullptr;
+    }
+    const PcPlan& P = q->P;
+    bool ok = hip_ok(hipMalloc((void**)&q->d_st, sizeof(WideStage) * (N + 1)), "pcond plan") &&
+              hip_ok(hipMalloc((void**)&q->d_st2, sizeof(WideStage) * (N2 + 1)), "pcond plan") &&
+              hip_ok(hipMalloc((void**)&q->d_blk, sizeof(PcBlock) * N2), "pcond plan") &&
+              hip_ok(hipMalloc((void**)&q->d_idxb, 4 * P.orig.nI), "pcond plan") &&
+              hip_ok(hipMalloc((void**)&q->d_idxb2, 4 * P.cond.nI), "pcond plan") &&
+              hip_ok(hipMemcpy(q->d_st, P.orig.st.data(), sizeof(WideStage) * (N + 1), hipMemcpyHostToDevice), "plan") &&
+              hip_ok(hipMemcpy(q->d_st2, P.cond.st.data(), sizeof(WideStage) * (N2 + 1), hipMemcpyHostToDevice),
+                     "plan") &&
+              hip_ok(hipMemcpy(q->d_blk, P.blk.data(), sizeof(PcBlock) * N2, hipMemcpyHostToDevice), "plan") &&
+              hip_ok(hipMemcpy(q->d_idxb, P.idxb.data(), 4 * P.orig.nI, hipMemcpyHostToDevice), "plan");
+    if (!ok) {
+        hpmpc_mi355x_pcond_plan_destroy(q);
+        return nullptr;
+    }
+    return q;
+}
+
+// Per-problem sizes (doubles): [0] BAbt [1] RSQrq [2] d (=lam/t) [3] ux [4] pi of the original layout;
+// [5] BAbt2 [6] RSQrq2 [7] DCt2 [8] d2 [9] ux2 [10] pi2 [11] condensed factor [12] Gamma scratch;
+// [13] condensed stages N2, [14] max ng2 (the condensed Riccati needs 0).
+extern "C" int hpmpc_mi355x_pcond_sizes(const hpmpc_mi355x_pcond_plan* q, long long* out) {
+    if (!q) return HPMPC_MI355X_EUNSUPPORTED;
+    const PcPlan& P = q->P;
+    long long v[15] = {P.orig.nB, P.orig.nR, P.orig.nD, P.orig.nU, P.orig.nP, P.cond.nB, P.cond.nR, P.nG2,
+                       P.cond.nD, P.cond.nU, P.cond.nP, P.cond.nL, P.nG, P.N2, 0};
+    for (int k = 0; k <= P.N2; k++) v[14] = std::max<long long>(v[14], P.ng2[k]);
+    memcpy(out, v, sizeof v);
+    return 0;
+}
+
+// Stage offsets (doubles) of the layouts, for callers that fill / read the packed arrays:
+// which = 0 original, 1 condensed; out[k*6 + 0..5] = oB, oR, oD, oU, oP, oL of stage k.
+extern "C" int hpmpc_mi355x_pcond_offsets(const hpmpc_mi355x_pcond_plan* q, int which, long long* out) {
+    if (!q) return HPMPC_MI355X_EUNSUPPORTED;
+    const WLayout& L = which ? q->P.cond : q->P.orig;
+    for (int k = 0; k <= L.N; k++) {
+        const WideStage& s = L.st[k];
+        const long long v[6] = {s.oB, s.oR, s.oD, s.oU, s.oP, s.oL};
+        memcpy(out + 6 * k, v, sizeof v);
+    }
+    return 0;
+}
+
+extern "C" int hpmpc_mi355x_pcond_batch(const hpmpc_mi355x_pcond_plan* q, int nprob, int p0, int count,
+                                        const double* BAbt, const double* RSQrq, const double* d, double* G,
+                                        double* BAbt2, double* RSQrq2, double* DCt2, double* d2, void* stream) {
+    if (!q) return HPMPC_MI355X_EUNSUPPORTED;
+    hk_set_error(0, nullptr);
+    PcArgs a;
+    fill_pc_args(q->P, a);
+    a.nprob = nprob;
+    a.p0 = p0;
+    a.st = q->d_st;
+    a.blk = q->d_blk;
+    a.idxb = q->d_idxb;
+    a.BAbt = BAbt;
+    a.RSQ = RSQrq;
+    a.d = d;
+    a.G = G;
+    a.BAbt2 = BAbt2;
+    a.RSQ2 = RSQrq2;
+    a.DCt2 = DCt2;
+    a.d2 = d2;
+    a.idxb2 = q->d_idxb2;
+    return launch(1, &a, count, q->P.pc_lds, (hipStream_t)stream, "hk_pcond") ? 0 : HPMPC_MI355X_EHIP;
+}
+
+extern "C" int hpmpc_mi355x_pcond_ric_sv_batch(const hpmpc_mi355x_pcond_plan* q, int nprob, int p0, int count,
+                                               const double* BAbt2, const double* RSQrq2, double* ws, double* ux2,
+                                               double* pi2, int compute_pi, void* stream) {
+    if (!q) return HPMPC_MI355X_EUNSUPPORTED;
+    hk_set_error(0, nullptr);
+    const WLayout& C = q->P.cond;
+    if (C.any_ng) {
+        hk_set_error(HPMPC_MI355X_EUNSUPPORTED, "condensed Riccati with general constraints (state boxes)");
+        return HPMPC_MI355X_EUNSUPPORTED;
+    }
+    WideArgs a;
+    memset(&a, 0, sizeof a);
+    a.N = C.N;
+    a.nprob = nprob;
+    a.p0 = p0;
+    a.st = q->d_st2;
+    a.BAbt = BAbt2;
+    a.sB = C.nB;
+    a.RSQ = RSQrq2;
+    a.sR = C.nR;
+    a.ws = ws;
+    a.sW = C.nL;
+    a.ux = ux2;
+    a.pi = pi2;
+    a.sU = C.nU;
+    a.sP = C.nP;
+    a.compute_pi = compute_pi;
+    a.offW = C.offW;
+    a.offX = C.offX;
+    a.offV = C.offV;
+    a.ldW = C.ldW;
+    a.ldX = C.ldX;
+    return launch(0, &a, count, C.lds, (hipStream_t)stream, "hk_wide_sv") ? 0 : HPMPC_MI355X_EHIP;
+}
+
+extern "C" int hpmpc_mi355x_pexpand_batch(const hpmpc_mi355x_pcond_plan* q, int nprob, int p0, int count,
+                                          const double* BAbt, const double* RSQrq, const double* ux2,
+                                          const double* pi2, const double* lam2, const double* t2, double* ux,
+                                          double* pi, double* lam, double* t, void* stream) {
+    if (!q) return HPMPC_MI355X_EUNSUPPORTED;
+    hk_set_error(0, nullptr);
+    PxArgs a;
+    fill_px_args(q->P, a);
+    a.nprob = nprob;
+    a.p0 = p0;
+    a.st = q->d_st;
+    a.st2 = q->d_st2;
+    a.blk = q->d_blk;
+    a.idxb = q->d_idxb;
+    a.BAbt = BAbt;
+    a.RSQ = RSQrq;
+    a.ux2 = ux2;
+    a.pi2 = pi2;
+    a.lam2 = lam2;
+    a.t2 = t2;
+    a.ux = ux;
+    a.pi = pi;
+    a.lam = lam;
+    a.t = t;
+    return launch(2, &a, count, q->P.px_lds, (hipStream_t)stream, "hk_pexpand") ? 0 : HPMPC_MI355X_EHIP;
+}

@@ -1,0 +1,160 @@
+"""Device-resident batches of the partial-condensing pipeline (BASELINE configs[4]).
+
+``d_part_cond`` (lqcp_solvers/d_part_cond.c:926) condenses each problem's N stages into N2 blocks, the
+Riccati recursion ``d_back_ric_rec_sv_tv_res`` (lqcp_solvers/d_back_ric_rec.c:112) runs on the condensed
+(wide) stages, and ``d_part_expand_solution`` (d_part_cond.c:1103) recovers the full-space solution.  All
+three are HIP kernels of libhpmpc_mi355x.so (hk_wide.hip); torch only allocates the HBM arrays:
+
+    BAbt, RSQrq, d          (nprob, size)  original lib4 stage blocks / padded bounds at the plan's offsets
+    G                       (nprob, size)  Gamma scratch of the condensing
+    BAbt2, RSQrq2, DCt2, d2 (nprob, size)  condensed problem
+    ws2, ux2, pi2           (nprob, size)  condensed factor and solution
+    ux, pi, lam, t          (nprob, size)  expanded solution
+
+There is no CPU fallback: constructing a solver without a GPU raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from .batch import lib
+from .ocp import OCPQP
+
+_BOUND = False
+
+
+def _bind():
+    global _BOUND
+    L = lib()
+    if _BOUND:
+        return L
+    vp, i, ll = C.c_void_p, C.c_int, C.c_longlong
+    L.hpmpc_mi355x_pcond_plan_create.restype = vp
+    L.hpmpc_mi355x_pcond_plan_create.argtypes = [i, vp, vp, vp, vp, vp, i]
+    L.hpmpc_mi355x_pcond_plan_destroy.argtypes = [vp]
+    L.hpmpc_mi355x_pcond_sizes.argtypes = [vp, vp]
+    L.hpmpc_mi355x_pcond_offsets.argtypes = [vp, i, vp]
+    L.hpmpc_mi355x_pcond_batch.restype = i
+    L.hpmpc_mi355x_pcond_batch.argtypes = [vp, i, i, i, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.hpmpc_mi355x_pcond_ric_sv_batch.restype = i
+    L.hpmpc_mi355x_pcond_ric_sv_batch.argtypes = [vp, i, i, i, vp, vp, vp, vp, vp, i, vp]
+    L.hpmpc_mi355x_pexpand_batch.restype = i
+    L.hpmpc_mi355x_pexpand_batch.argtypes = [vp, i, i, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    _ = ll
+    _BOUND = True
+    return L
+
+
+class PcondSolver:
+    """A batch of OCP QPs (shared sizes), condensed into N2 blocks and solved by the condensed Riccati."""
+
+    def __init__(self, qp: OCPQP, N2: int, device="cuda"):
+        import torch
+
+        if not torch.cuda.is_available():
+            raise RuntimeError("PcondSolver needs a GPU (HIP device); there is no CPU fallback")
+        assert qp.batch is not None, "PcondSolver takes a batched OCPQP"
+        self.torch = torch
+        self.qp = qp
+        self.N, self.N2, self.nprob = qp.N, N2, qp.batch
+        self.dev = torch.device(device)
+        L = _bind()
+        N = qp.N
+        idx = [np.ascontiguousarray(i, dtype=np.int32) for i in qp.idxb]
+        idxp = (C.POINTER(C.c_int) * (N + 1))(*[a.ctypes.data_as(C.POINTER(C.c_int)) for a in idx])
+        ints = lambda a: np.ascontiguousarray(a, dtype=np.int32)
+        self._keep = [idx, idxp]
+        nx, nu, nb, ng = ints(qp.nx), ints(qp.nu), ints(qp.nb), ints(qp.ng)
+        self.plan = L.hpmpc_mi355x_pcond_plan_create(N, nx.ctypes.data, nu.ctypes.data, nb.ctypes.data,
+                                                     C.cast(idxp, C.c_void_p), ng.ctypes.data, N2)
+        if not self.plan:
+            raise ValueError(f"unsupported partial condensing (code {L.hpmpc_mi355x_last_error()})")
+        sz = (C.c_longlong * 15)()
+        L.hpmpc_mi355x_pcond_sizes(self.plan, sz)
+        self.sizes = [int(v) for v in sz]
+        o0 = (C.c_longlong * (6 * (N + 1)))()
+        o1 = (C.c_longlong * (6 * (N2 + 1)))()
+        L.hpmpc_mi355x_pcond_offsets(self.plan, 0, o0)
+        L.hpmpc_mi355x_pcond_offsets(self.plan, 1, o1)
+        self.off = np.array(o0[:], dtype=np.int64).reshape(N + 1, 6)
+        self.off2 = np.array(o1[:], dtype=np.int64).reshape(N2 + 1, 6)
+        P = self.nprob
+        s = self.sizes
+        hB = np.zeros((P, s[0]))
+        hR = np.zeros((P, s[1]))
+        hd = np.zeros((P, s[2]))
+        for k in range(N + 1):
+            if k < N:
+                n = qp.BAbt[k].shape[1]
+                hB[:, self.off[k, 0]:self.off[k, 0] + n] = qp.BAbt[k]
+            n = qp.RSQrq[k].shape[1]
+            hR[:, self.off[k, 1]:self.off[k, 1] + n] = qp.RSQrq[k]
+            if qp.nb[k] + qp.ng[k] > 0:
+                n = qp.d[k].shape[1]
+                hd[:, self.off[k, 2]:self.off[k, 2] + n] = qp.d[k]
+        f64 = torch.float64
+        z = lambda n: torch.zeros((P, max(n, 1)), dtype=f64, device=self.dev)
+        self.BAbt = torch.from_numpy(hB).to(self.dev)
+        self.RSQrq = torch.from_numpy(hR).to(self.dev)
+        self.d = torch.from_numpy(hd).to(self.dev)
+        self.G = z(s[12])
+        self.BAbt2, self.RSQrq2, self.DCt2, self.d2 = z(s[5]), z(s[6]), z(s[7]), z(s[8])
+        self.ux2, self.pi2, self.ws2 = z(s[9]), z(s[10]), z(s[11])
+        self.lam2, self.t2 = z(s[8]), z(s[8])
+        self.ux, self.pi, self.lam, self.t = z(s[3]), z(s[4]), z(s[2]), z(s[2])
+
+    def __del__(self):
+        try:
+            if getattr(self, "plan", None):
+                _bind().hpmpc_mi355x_pcond_plan_destroy(self.plan)
+        except Exception:
+            pass
+
+    def _stream(self):
+        return C.c_void_p(self.torch.cuda.current_stream(self.dev).cuda_stream)
+
+    @staticmethod
+    def _p(t):
+        return C.c_void_p(t.data_ptr())
+
+    def _check(self, rc, what):
+        if rc != 0:
+            raise RuntimeError(f"{what} failed (code {rc})")
+
+    def condense(self, p0=0, count=None):
+        count = self.nprob - p0 if count is None else count
+        p = self._p
+        self._check(_bind().hpmpc_mi355x_pcond_batch(self.plan, self.nprob, p0, count, p(self.BAbt), p(self.RSQrq),
+                                                     p(self.d), p(self.G), p(self.BAbt2), p(self.RSQrq2),
+                                                     p(self.DCt2), p(self.d2), self._stream()), "pcond")
+
+    def riccati(self, p0=0, count=None, compute_pi=1):
+        count = self.nprob - p0 if count is None else count
+        p = self._p
+        self._check(_bind().hpmpc_mi355x_pcond_ric_sv_batch(self.plan, self.nprob, p0, count, p(self.BAbt2),
+                                                            p(self.RSQrq2), p(self.ws2), p(self.ux2), p(self.pi2),
+                                                            compute_pi, self._stream()), "condensed sv")
+
+    def expand(self, p0=0, count=None):
+        count = self.nprob - p0 if count is None else count
+        p = self._p
+        self._check(_bind().hpmpc_mi355x_pexpand_batch(self.plan, self.nprob, p0, count, p(self.BAbt), p(self.RSQrq),
+                                                       p(self.ux2), p(self.pi2), p(self.lam2), p(self.t2), p(self.ux),
+                                                       p(self.pi), p(self.lam), p(self.t), self._stream()), "expand")
+
+    def solve(self):
+        """condense -> condensed Riccati -> expand for the whole batch (asynchronous on the current stream)."""
+        self.condense()
+        self.riccati()
+        self.expand()
+
+    def solution(self, p: int):
+        """Problem p's expanded ux[k] (nu+nx) and pi[k] (nx_{k+1}) as numpy lists."""
+        ux = self.ux[p].cpu().numpy()
+        pi = self.pi[p].cpu().numpy()
+        qp = self.qp
+        U = [ux[self.off[k, 3]:self.off[k, 3] + qp.nux(k)].copy() for k in range(self.N + 1)]
+        Pi = [pi[self.off[k, 4]:self.off[k, 4] + int(qp.nx[k + 1])].copy() for k in range(self.N)]
+        return U, Pi

@@ -94,6 +94,32 @@ void d_res_mpc_hard_tv(int N, int *nx, int *nu, int *nb, int **idxb, int *ng, do
                        double **hpQ, double **hq, double **hux, double **hpDCt, double **hd, double **hpi,
                        double **hlam, double **ht, double **hrq, double **hrb, double **hrd, double *mu);
 
+/* Partial condensing: N stages -> N2 blocks, block i keeping [u_{T-1}; ..; u_0; x_0] as its
+ * stage variable.  The condensed data are written into `memory` with the reference's own carve, the pointer
+ * arrays hpBAbt2 .. hidxb2 are set into it, and the terminal stage aliases the caller's (d_part_cond.c:1052-1056).
+ * Stages with nu+nx > 16 (e.g. the condensed nu2+nx2 = 84 of configs[4]) are solved by
+ * d_back_ric_rec_sv_tv_res on the wide-stage path. */
+/* include/lqcp_solvers.h:86 (lqcp_solvers/d_part_cond.c:694) */
+void d_part_cond_compute_problem_size(int N, int *nx, int *nu, int *nb, int **hidxb, int *ng, int N2, int *nx2,
+                                      int *nu2, int *nb2, int *ng2);
+/* include/lqcp_solvers.h:88 (d_part_cond.c:743) -- every temporary lives on the device: 64 bytes */
+int d_part_cond_work_space_size_bytes(int N, int *nx, int *nu, int *nb, int **hidxb, int *ng, int N2, int *nx2,
+                                      int *nu2, int *nb2, int *ng2);
+/* include/lqcp_solvers.h:90 (d_part_cond.c:868) */
+int d_part_cond_memory_space_size_bytes(int N, int *nx, int *nu, int *nb, int **hidxb, int *ng, int N2, int *nx2,
+                                        int *nu2, int *nb2, int *ng2);
+/* include/lqcp_solvers.h:92 (d_part_cond.c:926) */
+void d_part_cond(int N, int *nx, int *nu, int *nb, int **hidxb, int *ng, double **hpBAbt, double **hpRSQrq,
+                 double **hpDCt, double **hd, int N2, int *nx2, int *nu2, int *nb2, int **hidxb2, int *ng2,
+                 double **hpBAbt2, double **hpRSQrq2, double **hpDCt2, double **hd2, void *memory, void *work);
+/* include/lqcp_solvers.h:94 (d_part_cond.c:1066) */
+int d_part_expand_work_space_size_bytes(int N, int *nx, int *nu, int *nb, int *ng);
+/* include/lqcp_solvers.h:96 (d_part_cond.c:1103) */
+void d_part_expand_solution(int N, int *nx, int *nu, int *nb, int **hidxb, int *ng, double **hpBAbt, double **hb,
+                            double **hpRSQrq, double **hrq, double **hpDCt, double **hux, double **hpi,
+                            double **hlam, double **ht, int N2, int *nx2, int *nu2, int *nb2, int **hidxb2,
+                            int *ng2, double **hux2, double **hpi2, double **hlam2, double **ht2, void *work);
+
 /* ================================ Part 2: batched device API ==================================== */
 
 /* Opaque plan: stage sizes, box indices and device tables shared by every problem of a batch. */
@@ -178,6 +204,33 @@ int hpmpc_mi355x_ric_trs_batch(const hpmpc_mi355x_plan *plan, const hpmpc_mi355x
 int hpmpc_mi355x_last_error(void);
 /* Library build string (architecture, kernel variant). */
 const char *hpmpc_mi355x_version(void);
+
+
+/* ---- partial-condensing pipeline on device-resident batches (configs[4]) ----
+ * A pcond plan holds the original and the condensed stage layouts shared by a batch.  Arrays are
+ * problem-major with the per-problem sizes of hpmpc_mi355x_pcond_sizes and the stage offsets of
+ * hpmpc_mi355x_pcond_offsets (lib4 blocks / padded vectors at those offsets). */
+typedef struct hpmpc_mi355x_pcond_plan hpmpc_mi355x_pcond_plan;
+hpmpc_mi355x_pcond_plan *hpmpc_mi355x_pcond_plan_create(int N, const int *nx, const int *nu, const int *nb,
+                                                        const int *const *idxb, const int *ng, int N2);
+void hpmpc_mi355x_pcond_plan_destroy(hpmpc_mi355x_pcond_plan *plan);
+/* out[15]: original BAbt, RSQrq, d, ux, pi | condensed BAbt2, RSQrq2, DCt2, d2, ux2, pi2, factor | Gamma
+ * scratch | N2 | max ng2 (doubles per problem) */
+int hpmpc_mi355x_pcond_sizes(const hpmpc_mi355x_pcond_plan *plan, long long *out);
+/* out[6*(N+1)] (which 0: original) or out[6*(N2+1)] (which 1: condensed): oB, oR, oD, oU, oP, oL per stage */
+int hpmpc_mi355x_pcond_offsets(const hpmpc_mi355x_pcond_plan *plan, int which, long long *out);
+/* d_part_cond of problems [p0, p0+count): one workgroup per (block, problem); G is the Gamma scratch */
+int hpmpc_mi355x_pcond_batch(const hpmpc_mi355x_pcond_plan *plan, int nprob, int p0, int count, const double *BAbt,
+                             const double *RSQrq, const double *d, double *G, double *BAbt2, double *RSQrq2,
+                             double *DCt2, double *d2, void *stream);
+/* d_back_ric_rec_sv_tv_res on the condensed problems (wide stages; no constraints) */
+int hpmpc_mi355x_pcond_ric_sv_batch(const hpmpc_mi355x_pcond_plan *plan, int nprob, int p0, int count,
+                                    const double *BAbt2, const double *RSQrq2, double *ws, double *ux2, double *pi2,
+                                    int compute_pi, void *stream);
+/* d_part_expand_solution (b / rq read from the augmented rows of BAbt / RSQrq) */
+int hpmpc_mi355x_pexpand_batch(const hpmpc_mi355x_pcond_plan *plan, int nprob, int p0, int count, const double *BAbt,
+                               const double *RSQrq, const double *ux2, const double *pi2, const double *lam2,
+                               const double *t2, double *ux, double *pi, double *lam, double *t, void *stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,134 @@
+"""Partial condensing and the wide-stage Riccati on the HIP path against the oracle.
+
+The reference's own pins are the pcond / pcond_sv goldens (run through test_gpu_parity.py): d_part_cond /
+d_part_expand_solution outputs of the reference c99 build where it is right (nu <= 4), and its direct Riccati
+solution at the configs[4] size (N=200 nx=24 nu=6 -> 20 blocks), which condense -> sv -> expand must
+reproduce.  These cases add the nu > 4 condensing (where the oracle, not the reference build, is the
+checker -- DESIGN.md), boxes that become general constraints, wide stages of arbitrary sizes through
+d_back_ric_rec_sv_tv_res, and the batched device pipeline.  Tolerances: Riccati 1e-12;
+condensed pipeline vs direct solve 1e-11.
+"""
+import numpy as np
+import pytest
+
+from helpers import TOL_PCOND_SV, TOL_RIC, check_pcond, pcond_sv, random_qp
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return float(np.max(np.abs(a - b) / np.maximum(1.0, np.abs(b)), initial=0.0))
+
+
+WIDE = [
+    # N, nx, nu, nb
+    (4, [0] + [20] * 4, [6] * 4 + [0], None),
+    (3, [0, 24, 24, 24], [60, 60, 60, 0], None),
+    (5, [7, 30, 12, 17, 9, 25], [3, 11, 40, 2, 5, 0], None),
+    (6, [0] + [18] * 6, [5] * 6 + [0], [3] + [6] * 5 + [4]),
+]
+
+
+@pytest.mark.parametrize("case", WIDE, ids=[f"N{c[0]}_{i}" for i, c in enumerate(WIDE)])
+def test_wide_sv_vs_oracle(product, oracle, case):
+    """d_back_ric_rec_sv_tv_res with nu+nx > 16 (the wide-stage path), with box terms and update rows."""
+    N, nx, nu, nb = case
+    qp = random_qp(N, nx, nu, nb, seed=41 + N)
+    rng = np.random.default_rng(N)
+    kw = dict(compute_pi=1, compute_Pb=1)
+    if nb is not None:
+        kw.update(bd=[rng.random(max(int(n), 1)) + 0.5 for n in qp.nb], Qx=[rng.random(max(int(n), 1)) for n in qp.nb],
+                  qx=[rng.standard_normal(max(int(n), 1)) for n in qp.nb],
+                  update_b=1, b=[rng.standard_normal(int(qp.nx[k + 1]) + 8) for k in range(N)],
+                  update_q=1, q=[rng.standard_normal(qp.nux(k) + 8) for k in range(N + 1)])
+    q1, q2 = qp.copy(), qp.copy()
+    u1, p1, b1, _ = product.ric_sv(q1, **kw)
+    u2, p2, b2, _ = oracle.ric_sv(q2, **kw)
+    for k in range(N + 1):
+        assert _rel(u1[k][:qp.nux(k)], u2[k][:qp.nux(k)]) <= TOL_RIC, k
+        if k < N:
+            m = int(qp.nx[k + 1])
+            assert _rel(p1[k][:m], p2[k][:m]) <= TOL_RIC and _rel(b1[k][:m], b2[k][:m]) <= TOL_RIC, k
+        np.testing.assert_array_equal(q1.RSQrq[k], q2.RSQrq[k])
+        if k < N:
+            np.testing.assert_array_equal(q1.BAbt[k], q2.BAbt[k])
+
+
+PCOND = [
+    # N, nx, nu, N2, boxes
+    (40, 12, 6, 8, True),     # nu > 4: the reference c99 build is wrong here, the oracle is the checker
+    (30, 24, 6, 3, False),
+    (23, 10, 5, 5, True),     # uneven blocks (first R1 blocks one stage longer)
+    (10, 6, 3, 1, True),      # a single block
+]
+
+
+@pytest.mark.parametrize("case", PCOND, ids=[f"N{c[0]}_nu{c[2]}_N2_{c[3]}" for c in PCOND])
+def test_pcond_entry_points_vs_oracle(product, oracle, case):
+    """d_part_cond + d_part_expand_solution through the C ABI against the oracle (condensed data and the
+    expansion of random condensed-space vectors)."""
+    from hpmpc_amd.golden import Case
+    from hpmpc_amd.ocp import mass_spring_qp
+
+    N, nx, nu, N2, boxes = case
+    qp = mass_spring_qp(N, nx, nu, boxes=boxes)
+    c, _ = oracle.part_cond(qp.copy(), N2)
+    rng = np.random.default_rng(N)
+    rv = lambda n: np.concatenate([rng.standard_normal(n), np.zeros(8)])
+    u2 = [rv(c.nux(k)) for k in range(N2 + 1)]
+    p2 = [rv(int(c.nx[k + 1])) for k in range(N2)]
+    lam2 = [np.abs(rv(c.nconstr(k))) for k in range(N2 + 1)]
+    t2 = [np.abs(rv(c.nconstr(k))) for k in range(N2 + 1)]
+    e = oracle.part_expand(qp, c, u2, p2, lam2, t2)
+    case_like = Case.__new__(Case)
+    case_like.name, case_like.qp = f"pcond_N{N}_nu{nu}", qp
+    case_like.out = dict(BAbt2=c.BAbt, RSQrq2=c.RSQrq[:N2], DCt2=c.DCt[:N2] if c.DCt else [], d2=c.d[:N2],
+                         idxb2=[i.astype(np.float64) for i in c.idxb[:N2]], nx2=c.nx, nu2=c.nu, nb2=c.nb, ng2=c.ng,
+                         ux=e["ux"], pi=e["pi"], lam=e["lam"], t=e["t"])
+    gc, _ = product.part_cond(qp.copy(), N2)
+    ge = product.part_expand(qp, gc, u2, p2, lam2, t2)
+    check_pcond(case_like, dict(cqp=gc, ux=ge["ux"], pi=ge["pi"], lam=ge["lam"], t=ge["t"]))
+
+
+def test_pcond_sv_pipeline_nu6(product, oracle):
+    """condense -> wide sv -> expand through the C ABI == the oracle's direct Riccati (nu = 6)."""
+    from hpmpc_amd.ocp import mass_spring_qp
+
+    qp = mass_spring_qp(40, 12, 6, boxes=False)
+    got = pcond_sv(product, qp.copy(), 8)
+    u, p, _, _ = oracle.ric_sv(qp.copy(), compute_pi=1, compute_Pb=0)
+    for k in range(41):
+        assert _rel(got["ux"][k][:qp.nux(k)], u[k][:qp.nux(k)]) <= TOL_PCOND_SV, k
+        if k < 40:
+            assert _rel(got["pi"][k][:12], p[k][:12]) <= TOL_PCOND_SV, k
+
+
+@pytest.mark.parametrize("N,nx,nu,N2,batch", [(40, 12, 6, 8, 16), (200, 24, 6, 20, 512)])
+def test_pcond_batch_pipeline(oracle, N, nx, nu, N2, batch):
+    """The batched device pipeline (configs[4] at full size: 512 x N=200 nx=24 nu=6 -> 20 blocks): sampled
+    problems equal the oracle's direct Riccati solution; repeated and split launches are bitwise identical."""
+    import torch
+
+    from hpmpc_amd.ocp import mass_spring_qp
+    from hpmpc_amd.pcond import PcondSolver
+
+    qp = mass_spring_qp(N, nx, nu, boxes=False, batch=batch, time_variant=True, seed=3)
+    s = PcondSolver(qp, N2)
+    s.solve()
+    torch.cuda.synchronize()
+    ux1 = s.ux.clone()
+    s.ux.zero_()
+    h = batch // 2
+    for p0, cnt in ((0, h), (h, batch - h)):
+        s.condense(p0, cnt)
+        s.riccati(p0, cnt)
+        s.expand(p0, cnt)
+    torch.cuda.synchronize()
+    assert torch.equal(s.ux, ux1)
+    for p in sorted({0, 1, batch // 2, batch - 1}):
+        U, Pi = s.solution(p)
+        u, pi, _, _ = oracle.ric_sv(qp.problem(p), compute_pi=1, compute_Pb=0)
+        for k in range(N + 1):
+            assert _rel(U[k], u[k][:qp.nux(k)]) <= TOL_PCOND_SV, (p, k)
+            if k < N:
+                assert _rel(Pi[k], pi[k][:nx]) <= TOL_PCOND_SV, (p, k)
