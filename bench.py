@@ -14,7 +14,8 @@ iteration counts / max-over-ranks time).  The roofline object is for the dominan
 factorisation pass, hk_ipm_fact), timed with hipEvents at every kernel boundary inside the timed
 region.  An isolated single-batch solve is reported beside it.
 The Riccati factorisation rate (d_back_ric_rec_sv_tv_res, nb = 0, compute_pi = 1) of the same
-batch is reported in the same JSON line.
+batch is reported in the same JSON line, and so is configs[4] ("pcond": 512 x N=200 nx=24 nu=6 condensed into
+20 blocks, the condensed Riccati and the expansion, with its own roofline and CPU baseline).
 
 Multi-GPU: one process per GPU (torch.distributed.run); every rank generates its own shard of
 problems from the global problem seeds (no data-path collective: weak scaling); RCCL is used only
@@ -53,6 +54,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16, help="host threads for the CPU baseline "
                     "(the GPU box's CPU share is 16 per GPU)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-pcond", action="store_true", help="skip the configs[4] partial-condensing leg")
+    ap.add_argument("--pcond-batch", type=int, default=512)
     ap.add_argument("--no-isolated", action="store_true", help="skip the isolated single-batch solve (profiling "
                     "runs: then every hk_ipm_* launch of the command belongs to the timed queue)")
     return ap.parse_args()
@@ -109,6 +112,102 @@ def cpu_baseline(qp, seconds, k_max, threads):
                       f"(k_max={k_max}) cycled by {threads} host threads for {en:.1f} s ({sn} solves, {itn} IP "
                       f"iterations); pre-marshalled ctypes calls",
             "single_core": {"value": v1, "solves": s1, "iters": it1, "seconds": e1}}
+
+
+def cpu_pcond_baseline(qp, N2, seconds, threads):
+    """Pipelines/s of the reference c99 build (oracle/_ref: d_part_cond + d_back_ric_rec_sv_tv_res on the
+    condensed problem + d_part_expand_solution), or of the oracle (kind 'port') without it, on the host cores:
+    a bounded sample of this rank's configs[4] batch, `threads` host threads and 1 thread."""
+    import threading
+
+    from hpmpc_amd.cabi import HpmpcAPI, load
+
+    ref = os.path.join(ROOT, "oracle", "_ref", "libhpmpc_ref.so")
+    orc = os.path.join(ROOT, "oracle", "liboracle.so")
+    if os.path.exists(ref):
+        api, kind = HpmpcAPI(load(ref)), "reference"
+    elif os.path.exists(orc):
+        api, kind = HpmpcAPI(load(orc), "orc_"), "port"
+    else:
+        return None
+    calls = [api.prepare_pcond(qp.problem(p), N2) for p in range(min(qp.batch, 2 * threads))]
+
+    def run(nthr, secs):
+        done = [0] * nthr
+        stop = time.perf_counter() + secs
+
+        def worker(i):
+            j = 0
+            while time.perf_counter() < stop:
+                calls[(i + nthr * j) % len(calls)]()
+                done[i] += 1
+                j += 1
+
+        th = [threading.Thread(target=worker, args=(i,)) for i in range(nthr)]
+        t0 = time.perf_counter()
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        return sum(done) / (time.perf_counter() - t0), sum(done)
+
+    v1, n1 = run(1, seconds * 0.3)
+    vn, nn = run(threads, seconds * 0.7)
+    return {"value": vn, "unit": "solves/s", "cores": threads, "kind": kind,
+            "sample": f"{len(calls)} problems of the configs[4] batch, d_part_cond + condensed "
+                      f"d_back_ric_rec_sv_tv_res + d_part_expand_solution, pre-marshalled ctypes calls, {threads} host threads "
+                      f"({nn} pipelines) and 1 thread ({n1}); the reference c99 condensing is numerically wrong "
+                      f"for nu > 4 (DESIGN.md) but does the same work",
+            "single_core": {"value": v1, "solves": n1}}
+
+
+def bench_pcond(args, torch, red, rank, world, barrier):
+    """configs[4]: 512 problems per GPU, N=200 nx=24 nu=6 condensed into N2=20 blocks of 10, then the
+    condensed Riccati factorisation + solve and the expansion (d_part_cond -> d_back_ric_rec_sv_tv_res ->
+    d_part_expand_solution).  A step is the whole pipeline over the batch; per-kernel hipEvents on the solve
+    stream give the roofline of the dominant kernel."""
+    from hpmpc_amd.pcond import PcondSolver, pcond_algorithmic_bytes, pcond_flops
+    from hpmpc_amd.shard import make_shard
+
+    B, N, nx, nu, N2 = args.pcond_batch, 200, 24, 6, 20
+    qp = make_shard(N, nx, nu, rank, world, B, boxes=False)
+    s = PcondSolver(qp, N2)
+    for _ in range(max(args.warmup, 1)):
+        s.solve()
+    stream = torch.cuda.current_stream()
+    K = args.steps
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(K)]
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(K):
+        ev[i][0].record(stream)
+        s.condense()
+        ev[i][1].record(stream)
+        s.riccati()
+        ev[i][2].record(stream)
+        s.expand()
+        ev[i][3].record(stream)
+    barrier()
+    dt = red.max(time.perf_counter() - t0)
+    ms = np.array([[e[j].elapsed_time(e[j + 1]) for j in range(3)] for e in ev]).mean(axis=0)
+    names = ["hk_pcond", "hk_wide_sv", "hk_pexpand"]
+    by = pcond_algorithmic_bytes(qp, N2)
+    fl = pcond_flops(qp, N2)
+    dom = int(np.argmax(ms))
+    ach = B * by[dom] / (ms[dom] * 1e-3) / 1e9
+    kern = {n: {"ms": float(m), "algorithmic_bytes_per_problem": b, "flops_per_problem": f,
+                "achieved_GBps": B * b / (m * 1e-3) / 1e9, "fp64_tflops": B * f / (m * 1e-3) / 1e12}
+            for n, m, b, f in zip(names, ms, by, fl)}
+    out = {"workload": f"pcond_N{N}_nx{nx}_nu{nu}_N2_{N2}_batch{B}", "value": B * world * K / dt,
+           "unit": "solves/s", "ms_per_step": dt / K * 1e3, "batch_per_gpu": B,
+           "condensed": {"N2": N2, "nu2": 60, "nx2": 24},
+           "riccati_fact_per_s": B * world / (ms[1] * 1e-3),
+           "roofline": {"bound": "hbm", "kernel": names[dom], "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                        "frac": ach / PEAK_HBM_GBS, "traffic": None, "launch_ms": float(ms[dom])},
+           "kernels": kern}
+    if rank == 0 and world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_pcond_baseline(qp, N2, args.cpu_seconds * 0.5, args.cpu_threads)
+    return out
 
 
 def main():
@@ -226,6 +325,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(qp, args.cpu_seconds, args.k_max, args.cpu_threads)
 
+    pc = None if args.no_pcond else bench_pcond(args, torch, red, rank, world, barrier)
+
     if rank == 0:
         line = {
             "metric": "IP iterations/sec (Riccati-based IPM, d_ip2_res_mpc_hard_tv), fp64, N=100 nx=12 nu=4 "
@@ -265,6 +366,7 @@ def main():
                                      "algorithmic_bytes_per_sv": sv_bytes,
                                      "fp64_tflops": B * flops_sv(N, nx, nu) / (sv_ms * 1e-3) / 1e12}},
             "cpu_baseline": cpu,
+            "pcond": pc,
         }
         print(json.dumps(line), flush=True)
     if dist is not None:

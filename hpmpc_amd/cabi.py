@@ -349,6 +349,63 @@ class HpmpcAPI:
         self._sync()
         return dict(ux=ux, pi=pi, lam=lam, t=t)
 
+    def prepare_pcond(self, qp: OCPQP, N2: int):
+        """Pre-marshalled configs[4] pipeline for CPU timing: returns call() running d_part_cond ->
+        d_back_ric_rec_sv_tv_res (condensed, compute_pi) -> d_part_expand_solution on private buffers with
+        ctypes argument tuples built once (the GIL is released inside each foreign call).  The terminal
+        condensed pointers are re-pointed at the caller's stage N after every d_part_cond (the reference
+        build clobbers them, see part_cond)."""
+        N = qp.N
+        qp = qp.copy()
+        idxb = [np.ascontiguousarray(i, dtype=np.int32) for i in qp.idxb]
+        nx2, nu2, nb2, ng2 = self.part_cond_sizes(qp, N2)
+        cn = [iv(a) for a in (nx2, nu2, nb2, ng2)]
+        head = (C.c_int(N), iv(qp.nx), iv(qp.nu), iv(qp.nb), ipp(idxb), iv(qp.ng), C.c_int(N2), *cn)
+        msz = self.fn("d_part_cond_memory_space_size_bytes")(*head)
+        wsz = self.fn("d_part_cond_work_space_size_bytes")(*head)
+        memory = np.zeros(2 * (msz // 8) + 512)
+        work = np.zeros(2 * (wsz // 8) + 512)
+        hidxb2 = (IP * (N2 + 1))()
+        pB, pR, pG, pd = ((DP * (N2 + 1))() for _ in range(4))
+        dct = qp.DCt if qp.DCt else [np.zeros(8) for _ in range(N + 1)]
+        pBAbt, pRSQ, pDCt, pdd, pidx = dpp(qp.BAbt), dpp(qp.RSQrq), dpp(dct), dpp(qp.d), ipp(idxb)
+        cond_args = (C.c_int(N), iv(qp.nx), iv(qp.nu), iv(qp.nb), pidx, iv(qp.ng), pBAbt, pRSQ, pDCt, pdd,
+                     C.c_int(N2), cn[0], cn[1], cn[2], hidxb2, cn[3], pB, pR, pG, pd, _dptr(memory), _dptr(work))
+        z1 = (C.c_int * (N2 + 1))()
+        mem2 = np.zeros(self.fn("d_back_ric_rec_sv_tv_memory_space_size_bytes")(C.c_int(N2), cn[0], cn[1], z1, z1)
+                        // 8 + 64)
+        wrk2 = np.zeros(self.fn("d_back_ric_rec_sv_tv_work_space_size_bytes")(C.c_int(N2), cn[0], cn[1], z1, z1)
+                        // 8 + 64)
+        ux2 = [np.zeros(rup(int(nu2[k] + nx2[k]) + 1, 4)) for k in range(N2 + 1)]
+        pi2 = [np.zeros(rup(int(nx2[k + 1]), 4) + 4) for k in range(N2)]
+        Pb2 = [np.zeros(rup(int(nx2[k + 1]), 4) + 4) for k in range(N2)]
+        dummy = [np.zeros(8) for _ in range(N2 + 1)]
+        sv_args = (C.c_int(N2), cn[0], cn[1], z1, hidxb2, z1, C.c_int(0), pB, dpp(dummy), C.c_int(0), pR,
+                   dpp(dummy), dpp(dummy), pG, dpp(dummy), dpp(dummy), dpp(ux2), C.c_int(1), dpp(pi2), C.c_int(0),
+                   dpp(Pb2), _dptr(mem2), _dptr(wrk2))
+        b, q = bq_from_qp(qp)
+        ux, pi, lam, t = qp.alloc_solution()
+        lam2 = [np.zeros(2 * rup(int(nb2[k]), 4) + 2 * rup(int(ng2[k]), 4) + 4) for k in range(N2 + 1)]
+        t2 = [x.copy() for x in lam2]
+        wx = np.zeros(self.fn("d_part_expand_work_space_size_bytes")(C.c_int(N), iv(qp.nx), iv(qp.nu), iv(qp.nb),
+                                                                    iv(qp.ng)) // 8 + 64)
+        ex_args = (C.c_int(N), iv(qp.nx), iv(qp.nu), iv(qp.nb), pidx, iv(qp.ng), pBAbt, dpp(b), pRSQ, dpp(q), pDCt,
+                   dpp(ux), dpp(pi), dpp(lam), dpp(t), C.c_int(N2), cn[0], cn[1], cn[2], hidxb2, cn[3], dpp(ux2),
+                   dpp(pi2), dpp(lam2), dpp(t2), _dptr(wx))
+        f_cond, f_sv, f_ex = self.fn("d_part_cond"), self.fn("d_back_ric_rec_sv_tv_res"), \
+            self.fn("d_part_expand_solution")
+        keep = (qp, idxb, memory, work, mem2, wrk2, ux2, pi2, Pb2, dummy, b, q, ux, pi, lam, t, lam2, t2, wx, dct)
+        last = (pRSQ[N], pDCt[N], pdd[N], pidx[N])
+
+        def call():
+            _ = keep
+            f_cond(*cond_args)
+            pR[N2], pG[N2], pd[N2], hidxb2[N2] = last
+            f_sv(*sv_args)
+            f_ex(*ex_args)
+
+        return call
+
 
 def bq_from_qp(qp: OCPQP):
     """b[k] and q[k] vectors extracted from the augmented rows (as the IPM does, d_ip2_res_hard.c:202-220)."""

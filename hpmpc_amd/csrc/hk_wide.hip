@@ -3,7 +3,7 @@
 //               256-thread workgroup per problem, the stage Hessian in LDS as packed lower columns;
 //   hk_pcond    d_part_cond (lqcp_solvers/d_part_cond.c:926-1062): one workgroup per (block, problem),
 //               every block of every problem condensed concurrently;
-//   hk_pexpand  d_part_expand_solution (d_part_cond.c:1103-1308): one workgroup per problem.
+//   hk_pexpand  d_part_expand_solution (d_part_cond.c:1103-1308): one workgroup per (block, problem).
 //
 // These are the "next" rows of SURVEY.md §8f #1 (configs[4]: N=200 -> 20 blocks of 10, nx=24 nu=6).
 // Every stage matrix is read from HBM once per pass in the reference's lib4 layout and staged into LDS
@@ -11,12 +11,17 @@
 // one barrier per dependency step (one per Cholesky column).
 #include <hip/hip_runtime.h>
 
+#include "hk_prims.h"
 #include "hk_wide_args.h"
 
 namespace {
 
+using hk::gld;
+
 constexpr int WT = 256;  // threads per workgroup
 constexpr int BS = 4;
+
+__device__ __forceinline__ int p4i(int i, int j, int sd) { return (i / BS) * BS * sd + i % BS + BS * j; }
 
 __device__ __forceinline__ double P4(const double* A, int sd, int i, int j) {
     return A[(i / BS) * BS * sd + i % BS + BS * j];
@@ -28,6 +33,68 @@ __device__ __forceinline__ double* P4w(double* A, int sd, int i, int j) {
 __device__ __forceinline__ int poff(int j, int nz) { return j * nz - (j * (j - 1)) / 2; }
 
 __device__ __forceinline__ void bar() { __syncthreads(); }
+
+// Global -> LDS staging with CH loads in flight per lane: every load of a batch is issued before the first
+// LDS store (raw buffer loads, masked lanes read out of range), so a stage tile costs one or two memory
+// round trips instead of one per element.
+template <int CH>
+__device__ void load_flat(double* D, const double* src, int n) {
+    const int tid = threadIdx.x;
+    for (int base = 0; base < n; base += WT * CH) {
+        double r[CH];
+#pragma unroll
+        for (int u = 0; u < CH; u++) r[u] = gld(src, base + u * WT + tid, base + u * WT + tid < n);
+#pragma unroll
+        for (int u = 0; u < CH; u++)
+            if (base + u * WT + tid < n) D[base + u * WT + tid] = r[u];
+    }
+}
+// lib4 block rows [0, nr) x cols [0, nc) -> dense column-major (ld)
+template <int CH>
+__device__ void load_dense(double* D, int ld, const double* src, int sd, int nr, int nc) {
+    const int tid = threadIdx.x, n = nr * nc;
+    for (int base = 0; base < n; base += WT * CH) {
+        double r[CH];
+#pragma unroll
+        for (int u = 0; u < CH; u++) {
+            const int e = base + u * WT + tid, i = e % nr, c = e / nr;
+            r[u] = gld(src, p4i(i, c, sd), e < n);
+        }
+#pragma unroll
+        for (int u = 0; u < CH; u++) {
+            const int e = base + u * WT + tid, i = e % nr, c = e / nr;
+            if (e < n) D[i + c * ld] = r[u];
+        }
+    }
+}
+// lib4 lower trapezoid rows [j, nz) of cols [0, nc) -> packed lower columns (nz <= 128: two rows per lane)
+template <int CU>
+__device__ void load_lower(double* M, const double* src, int sd, int nz, int nc) {
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    for (int j0 = w; j0 < nc; j0 += 4 * CU) {
+        double r[CU][2];
+#pragma unroll
+        for (int u = 0; u < CU; u++)
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int j = j0 + 4 * u, i = j + l + 64 * h;
+                r[u][h] = gld(src, p4i(i, j, sd), j < nc && i < nz);
+            }
+#pragma unroll
+        for (int u = 0; u < CU; u++)
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int j = j0 + 4 * u, i = j + l + 64 * h;
+                if (j < nc && i < nz) M[poff(j, nz) + i - j] = r[u][h];
+            }
+    }
+}
+// in-wave ordering of LDS traffic between lanes (single-wave phases need no workgroup barrier)
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 }  // namespace
 
@@ -62,15 +129,9 @@ __global__ __launch_bounds__(WT) void hk_wide_sv(WideArgs a) {
     for (int k = a.N; k >= 0; k--) {
         const WideStage s = a.st[k];
         const int nu = s.nu, nux = s.nu + s.nx, nz = nux + 1, nx1 = s.nx1;
-        const double* R = RSQ + s.oR;
-        for (int j = tid >> 6; j < nux; j += WT / 64)
-            for (int i = j + (tid & 63); i < nz; i += 64) M[poff(j, nz) + i - j] = P4(R, s.sdR, i, j);
+        load_lower<4>(M, RSQ + s.oR, s.sdR, nz, nux);
         if (k < a.N) {
-            const double* B = BAbt + s.oB;
-            for (int e = tid; e < nz * nx1; e += WT) {
-                const int i = e % nz, c = e / nz;
-                W[i + c * ldW] = P4(B, s.sdB, i, c);
-            }
+            load_dense<8>(W, ldW, BAbt + s.oB, s.sdB, nz, nx1);
             bar();
             // W = BAbt Lxx (in place, row i by thread: w_c needs W[i, l >= c] only)
             for (int i = tid; i < nz; i += WT)
@@ -127,58 +188,65 @@ __global__ __launch_bounds__(WT) void hk_wide_sv(WideArgs a) {
         bar();
     }
 
-    // forward substitution
+    // forward substitution: L_k (packed + 1/diag) and BAbt_k are staged into LDS (M, W) per stage
+    double* tmp = X;  // Lxx is no longer needed: nx1 doubles of scratch for pi
+    {
+        const WideStage s0 = a.st[0];
+        const int nz0 = s0.nu + s0.nx + 1;
+        load_flat<16>(M, F + s0.oL, poff(nz0 - 1, nz0) + nz0 - 1);
+    }
     for (int k = 0; k < a.N; k++) {
         const WideStage s = a.st[k];
         const int nux = s.nu + s.nx, nz = nux + 1, nx1 = s.nx1, nu1 = s.nu1;
         const int ns = k == 0 ? nux : s.nu;
-        const double* Lk = F + s.oL;
-        const double* dL = Lk + poff(nux, nz);
+        const double* dL = M + poff(nux, nz);
+        load_dense<8>(W, ldW, BAbt + s.oB, s.sdB, nz, nx1);
+        bar();
         // v[0:ns] = -l[0:ns] - L[ns:nux, 0:ns]' v[ns:nux]   (v[ns:nux] = x_k from the previous stage)
         for (int j = tid; j < ns; j += WT) {
-            double r = -Lk[poff(j, nz) + nux - j];
-            for (int m = ns; m < nux; m++) r -= Lk[poff(j, nz) + m - j] * v[m];
+            const int cj = poff(j, nz) - j;
+            double r = -M[cj + nux];
+            for (int m = ns; m < nux; m++) r -= M[cj + m] * v[m];
             v[j] = r;
         }
         bar();
-        // back substitution with L[0:ns, 0:ns]' (column-oriented, inv_diag multiply)
-        for (int i = ns - 1; i >= 0; i--) {
-            const double y = v[i] * dL[i];
-            bar();
-            for (int j = tid; j < i; j += WT) v[j] -= Lk[poff(j, nz) + i - j] * y;
-            if (tid == 0) v[i] = y;
-            bar();
+        // back substitution with L[0:ns, 0:ns]' (inv_diag multiply), column-oriented inside wave 0
+        if (tid < 64) {
+            for (int i = ns - 1; i >= 0; i--) {
+                const double y = v[i] * dL[i];
+                for (int j = tid; j < i; j += 64) v[j] -= M[poff(j, nz) + i - j] * y;
+                if (tid == 0) v[i] = y;
+                wave_sync();
+            }
         }
+        bar();
         for (int j = tid; j < nux; j += WT) ux[s.oU + j] = v[j];
         // x_{k+1} = b_k + BAbt_k' ux_k
-        const double* B = BAbt + s.oB;
         double xn = 0.0;
         if (tid < nx1) {
-            xn = P4(B, s.sdB, nux, tid);
-            for (int i = 0; i < nux; i++) xn += P4(B, s.sdB, i, tid) * v[i];
+            xn = W[nux + tid * ldW];
+            for (int i = 0; i < nux; i++) xn += W[i + tid * ldW] * v[i];
         }
         bar();
         const WideStage s1 = a.st[k + 1];
+        const int nux1 = nu1 + nx1, nz1 = nux1 + 1;
         if (tid < nx1) {
             v[nu1 + tid] = xn;
             ux[s1.oU + nu1 + tid] = xn;
         }
+        load_flat<16>(M, F + s1.oL, poff(nux1, nz1) + nux1);
         bar();
-        if (a.compute_pi) {  // pi_k = Lxx (Lxx' x + l), Lxx of stage k+1 (rows / cols nu1.., packed)
-            const int nux1 = nu1 + nx1, nz1 = nux1 + 1;
-            const double* L1 = F + s1.oL;
-            double tj = 0.0;
+        if (a.compute_pi) {  // pi_k = Lxx (Lxx' x + l), Lxx of stage k+1 (rows / cols nu1..)
             if (tid < nx1) {
-                const int cj = poff(nu1 + tid, nz1);
-                tj = L1[cj + nux1 - (nu1 + tid)];
-                for (int i = tid; i < nx1; i++) tj += L1[cj + i - tid] * v[nu1 + i];
+                const int cj = poff(nu1 + tid, nz1) - (nu1 + tid);
+                double tj = M[cj + nux1];
+                for (int i = tid; i < nx1; i++) tj += M[cj + nu1 + i] * v[nu1 + i];
+                tmp[tid] = tj;
             }
-            bar();
-            if (tid < nx1) W[tid] = tj;
             bar();
             if (tid < nx1) {
                 double acc = 0.0;
-                for (int j = 0; j <= tid; j++) acc += L1[poff(nu1 + j, nz1) + tid - j] * W[j];
+                for (int j = 0; j <= tid; j++) acc += M[poff(nu1 + j, nz1) + tid - j] * tmp[j];
                 pi[s.oP + tid] = acc;
             }
             bar();
@@ -229,28 +297,22 @@ __global__ __launch_bounds__(WT) void hk_pcond(PcArgs a) {
         return o;
     };
 
-    // ---- d_cond_BAbt ----
+    // ---- d_cond_BAbt: Gamma_{j-1} stays in LDS (GA) while Gamma_j is built in GB and streamed to HBM ----
+    double* GA = sm + a.offGA;
+    double* GB = sm + a.offGB;
     {
         const WideStage s = st[0];
         const int r0 = s.nu + s.nx + 1;
-        const double* B = BAbt + s.oB;
-        for (int e = tid; e < r0 * s.nx1; e += WT) {
-            const int i = e % r0, c = e / r0;
-            G[i + c * r0] = P4(B, s.sdB, i, c);
-        }
+        load_dense<8>(GA, r0, BAbt + s.oB, s.sdB, r0, s.nx1);
+        bar();
+        for (int e = tid; e < r0 * s.nx1; e += WT) G[e] = GA[e];
     }
-    bar();
     for (int j = 1; j < T; j++) {
         const WideStage s = st[j];
         const int nuj = s.nu, nxj = s.nx, nx1 = s.nx1, nzj = nuj + nxj + 1;
         const int rp = rows(j - 1), rj = rp + nuj;
-        const double* Gp = G + goff(j - 1);
         double* Gj = G + goff(j);
-        const double* B = BAbt + s.oB;
-        for (int e = tid; e < nzj * nx1; e += WT) {
-            const int i = e % nzj, c = e / nzj;
-            Bt[i + c * ldB] = P4(B, s.sdB, i, c);
-        }
+        load_dense<8>(Bt, ldB, BAbt + s.oB, s.sdB, nzj, nx1);
         bar();
         for (int e = tid; e < rj * nx1; e += WT) {
             const int i = e % rj, c = e / rj;
@@ -260,21 +322,24 @@ __global__ __launch_bounds__(WT) void hk_pcond(PcArgs a) {
             } else {
                 const int ip = i - nuj;
                 double acc = 0.0;
-                for (int l = 0; l < nxj; l++) acc += Gp[ip + l * rp] * Bt[nuj + l + c * ldB];
+                for (int l = 0; l < nxj; l++) acc += GA[ip + l * rp] * Bt[nuj + l + c * ldB];
                 val = acc;
                 if (i == rj - 1) val += Bt[nuj + nxj + c * ldB];
             }
+            GB[i + c * rj] = val;
             Gj[i + c * rj] = val;
         }
         bar();
+        double* sw = GA;
+        GA = GB;
+        GB = sw;
     }
     {
         const int rT = rows(T - 1), nxT = st[T - 1].nx1;
-        const double* GT = G + goff(T - 1);
         const int sd = (nxT + 1) / 2 * 2;
         for (int e = tid; e < rT * nxT; e += WT) {
             const int i = e % rT, c = e / rT;
-            *P4w(B2, sd, i, c) = GT[i + c * rT];
+            *P4w(B2, sd, i, c) = GA[i + c * rT];
         }
     }
 
@@ -299,9 +364,7 @@ __global__ __launch_bounds__(WT) void hk_pcond(PcArgs a) {
     } else {
         {
             const WideStage s = st[T - 1];
-            const int nux = s.nu + s.nx;
-            for (int j = tid >> 6; j < nux; j += WT / 64)
-                for (int i = j + (tid & 63); i <= nux; i += 64) Pl[i + j * ldP] = P4(RSQ + s.oR, s.sdR, i, j);
+            load_dense<8>(Pl, ldP, RSQ + s.oR, s.sdR, s.nu + s.nx + 1, s.nu + s.nx);
         }
         bar();
         for (int sI = T - 1;; sI--) {
@@ -318,7 +381,9 @@ __global__ __launch_bounds__(WT) void hk_pcond(PcArgs a) {
             // M: Gamma_{s-1} times the x_s x u_s block of pL; m: + the r row on the gradient row
             {
                 const int r0 = rows(sI - 1);
-                const double* Gp = G + goff(sI - 1);
+                load_flat<8>(GA, G + goff(sI - 1), r0 * nxs);
+                bar();
+                const double* Gp = GA;
                 for (int e = tid; e < r0 * nus; e += WT) {
                     const int i = e % r0, c = e / r0;
                     double acc = 0.0;
@@ -350,13 +415,9 @@ __global__ __launch_bounds__(WT) void hk_pcond(PcArgs a) {
             // W = BAbt_{s-1} Lx, last row += l; pL = RSQ_{s-1} + W W'
             const WideStage sp = st[sI - 1];
             const int nuxp = sp.nu + sp.nx, nzp = nuxp + 1;
-            {
-                const double* B = BAbt + sp.oB;
-                for (int e = tid; e < nzp * nxs; e += WT) {
-                    const int i = e % nzp, c = e / nzp;
-                    Bt[i + c * ldB] = P4(B, sp.sdB, i, c);
-                }
-            }
+            load_dense<8>(Bt, ldB, BAbt + sp.oB, sp.sdB, nzp, nxs);
+            // RSQrq_{s-1} lower (+ gradient row) into GB as a dense tile (ld nzp)
+            load_dense<8>(GB, nzp, RSQ + sp.oR, sp.sdR, nzp, nuxp);
             bar();
             for (int e = tid; e < nzp * nxs; e += WT) {
                 const int i = e % nzp, c = e / nzp;
@@ -370,7 +431,7 @@ __global__ __launch_bounds__(WT) void hk_pcond(PcArgs a) {
                 for (int i = j + (tid & 63); i <= nuxp; i += 64) {
                     double acc = 0.0;
                     for (int l = 0; l < nxs; l++) acc += W[i + l * ldW] * W[j + l * ldW];
-                    Pl[i + j * ldP] = P4(RSQ + sp.oR, sp.sdR, i, j) + acc;
+                    Pl[i + j * ldP] = GB[i + j * nzp] + acc;
                 }
             bar();
         }
@@ -430,19 +491,21 @@ __global__ __launch_bounds__(WT) void hk_pcond(PcArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// Expansion of the condensed solution (d_part_expand_solution).
+// Expansion of the condensed solution (d_part_expand_solution), one workgroup per (block, problem):
+// the blocks are independent (each starts from its own x_0 and ends at the condensed pi).
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(WT) void hk_pexpand(PxArgs a) {
     extern __shared__ double sm[];
-    const int p = blockIdx.x + a.p0;
-    if (p >= a.nprob) return;
+    const int ii = blockIdx.x, p = blockIdx.y + a.p0;
+    if (p >= a.nprob || ii >= a.N2) return;
     const int tid = threadIdx.x;
     const WideStage* st = a.st;
     const WideStage* st2 = a.st2;
+    const PcBlock blk = a.blk[ii];
+    const int T = blk.T, s0 = blk.s0;
     const double* BAbt = a.BAbt + (long)p * a.sB;
     const double* RSQ = a.RSQ + (long)p * a.sR;
-    const double* ux2 = a.ux2 + (long)p * a.sU2;
-    const double* pi2 = a.pi2 + (long)p * a.sP2;
+    const double* u2 = a.ux2 + (long)p * a.sU2 + st2[ii].oU;
     const double* lam2 = a.lam2 + (long)p * a.sC2;
     const double* t2 = a.t2 + (long)p * a.sC2;
     double* ux = a.ux + (long)p * a.sU;
@@ -451,46 +514,53 @@ __global__ __launch_bounds__(WT) void hk_pexpand(PxArgs a) {
     double* t = a.t + (long)p * a.sC;
     const double* hb = a.hb ? a.hb + (long)p * a.sP : nullptr;
     const double* hrq = a.hrq ? a.hrq + (long)p * a.sU : nullptr;
-    double* w = sm + a.offW;
+    const int ld = a.ldT;
+    double* Bt = sm + a.offB;  // BAbt_j tile (ld x nxM)
+    double* Rt = sm + a.offR;  // RSQrq_j tile (ld x ld)
+    double* vu = sm + a.offV;  // ux_j (ld)
+    double* w = sm + a.offW;   // box terms (ld)
+    double* vp = sm + a.offQ;  // pi_j (ld)
 
-    // inputs (reverse stage order) and the blocks' first states; the final state
-    for (int ii = 0; ii < a.N2; ii++) {
-        const PcBlock blk = a.blk[ii];
-        const double* u2 = ux2 + st2[ii].oU;
-        int nu_tmp = 0;
-        for (int jj = 0; jj < blk.T - 1; jj++) {
-            const WideStage s = st[blk.s0 + blk.T - 1 - jj];
-            for (int l = tid; l < s.nu; l += WT) ux[s.oU + l] = u2[nu_tmp + l];
-            nu_tmp += s.nu;
+    // u of the block's later stages come first in the condensed vector (reverse order), then u_0, x_0
+    auto upos = [&](int j) {  // position of u_{s0+j} in u2
+        int o = 0;
+        for (int r = T - 1; r > j; r--) o += st[s0 + r].nu;
+        return o;
+    };
+    // stage s0: u and x straight from u2
+    {
+        const WideStage s = st[s0];
+        const int o = upos(0);
+        for (int l = tid; l < s.nu + s.nx; l += WT) {
+            const double x = u2[o + l];
+            vu[l] = x;
+            ux[s.oU + l] = x;
         }
-        const WideStage s = st[blk.s0];
-        for (int l = tid; l < s.nu + s.nx; l += WT) ux[s.oU + l] = u2[nu_tmp + l];
     }
-    for (int l = tid; l < st[a.N].nx; l += WT) ux[st[a.N].oU + l] = ux2[st2[a.N2].oU + l];
-    bar();
-    // states inside the blocks by simulation, x_{j+1} = b_j + BAbt_j' ux_j
-    for (int ii = 0; ii < a.N2; ii++) {
-        const PcBlock blk = a.blk[ii];
-        for (int jj = 0; jj < blk.T - 1; jj++) {
-            const WideStage s = st[blk.s0 + jj], s1 = st[blk.s0 + jj + 1];
-            const int nux = s.nu + s.nx;
-            const double* B = BAbt + s.oB;
-            if (tid < s.nx1) {
-                double acc = 0.0;
-                for (int i = 0; i < nux; i++) acc += P4(B, s.sdB, i, tid) * ux[s.oU + i];
-                const double b = hb ? hb[s.oP + tid] : P4(B, s.sdB, nux, tid);
-                ux[s1.oU + s1.nu + tid] = b + acc;
+    if (ii == a.N2 - 1) {  // the final state, and stage N's multipliers (box and general slots)
+        const WideStage sN = st[a.N], c = st2[a.N2];
+        for (int l = tid; l < sN.nx; l += WT) ux[sN.oU + l] = a.ux2[(long)p * a.sU2 + c.oU + l];
+        if (tid == 0) {
+            const int png = (sN.ng + 3) / 4 * 4, png2 = (c.ng + 3) / 4 * 4;
+            for (int j = 0; j < sN.nb; j++) {
+                lam[sN.oD + j] = lam2[c.oD + j];
+                lam[sN.oD + sN.pnb + j] = lam2[c.oD + c.pnb + j];
+                t[sN.oD + j] = t2[c.oD + j];
+                t[sN.oD + sN.pnb + j] = t2[c.oD + c.pnb + j];
             }
-            bar();
+            for (int j = 0; j < sN.ng; j++) {
+                lam[sN.oD + 2 * sN.pnb + j] = lam2[c.oD + 2 * c.pnb + j];
+                lam[sN.oD + 2 * sN.pnb + png + j] = lam2[c.oD + 2 * c.pnb + png2 + j];
+                t[sN.oD + 2 * sN.pnb + j] = t2[c.oD + 2 * c.pnb + j];
+                t[sN.oD + 2 * sN.pnb + png + j] = t2[c.oD + 2 * c.pnb + png2 + j];
+            }
         }
     }
-    // slacks and inequality multipliers (one thread per block: the slot order is a prefix scan)
-    for (int ii = tid; ii < a.N2; ii += WT) {
-        const PcBlock blk = a.blk[ii];
+    if (tid == 0) {  // slacks and multipliers of the block's stages (the slot order is a prefix scan)
         const int pnb2 = st2[ii].pnb, png2 = (st2[ii].ng + 3) / 4 * 4, o2 = st2[ii].oD;
         int nbb2_tmp = 0, nbg2_tmp = 0;
-        for (int jj = 0; jj < blk.T - 1; jj++) {
-            const WideStage s = st[blk.s0 + blk.T - 1 - jj];
+        for (int jj = 0; jj < T - 1; jj++) {
+            const WideStage s = st[s0 + T - 1 - jj];
             int nbb2 = 0, nbg2 = 0;
             for (int l = 0; l < s.nb; l++) {
                 if (a.idxb[s.oI + l] < s.nu)
@@ -513,7 +583,7 @@ __global__ __launch_bounds__(WT) void hk_pexpand(PxArgs a) {
             nbb2_tmp += nbb2;
             nbg2_tmp += nbg2;
         }
-        const WideStage s = st[blk.s0];
+        const WideStage s = st[s0];
         for (int l = 0; l < s.nb; l++) {
             lam[s.oD + l] = lam2[o2 + nbb2_tmp + l];
             lam[s.oD + s.pnb + l] = lam2[o2 + pnb2 + nbb2_tmp + l];
@@ -521,54 +591,70 @@ __global__ __launch_bounds__(WT) void hk_pexpand(PxArgs a) {
             t[s.oD + s.pnb + l] = t2[o2 + pnb2 + nbb2_tmp + l];
         }
     }
-    if (tid == 0) {  // last stage: box and general slots copied
-        const WideStage s = st[a.N], c = st2[a.N2];
-        const int png = (s.ng + 3) / 4 * 4, png2 = (c.ng + 3) / 4 * 4;
-        for (int j = 0; j < s.nb; j++) {
-            lam[s.oD + j] = lam2[c.oD + j];
-            lam[s.oD + s.pnb + j] = lam2[c.oD + c.pnb + j];
-            t[s.oD + j] = t2[c.oD + j];
-            t[s.oD + s.pnb + j] = t2[c.oD + c.pnb + j];
+    // states inside the block by simulation, x_{j+1} = b_j + BAbt_j' ux_j; u_{j+1} from u2
+    for (int jj = 0; jj < T - 1; jj++) {
+        const WideStage s = st[s0 + jj], s1 = st[s0 + jj + 1];
+        const int nux = s.nu + s.nx;
+        load_dense<4>(Bt, ld, BAbt + s.oB, s.sdB, nux + 1, s.nx1);
+        bar();
+        double xn = 0.0;
+        if (tid < s.nx1) {
+            double acc = 0.0;
+            for (int i = 0; i < nux; i++) acc += Bt[i + tid * ld] * vu[i];
+            xn = (hb ? hb[s.oP + tid] : Bt[nux + tid * ld]) + acc;
         }
-        for (int j = 0; j < s.ng; j++) {
-            lam[s.oD + 2 * s.pnb + j] = lam2[c.oD + 2 * c.pnb + j];
-            lam[s.oD + 2 * s.pnb + png + j] = lam2[c.oD + 2 * c.pnb + png2 + j];
-            t[s.oD + 2 * s.pnb + j] = t2[c.oD + 2 * c.pnb + j];
-            t[s.oD + 2 * s.pnb + png + j] = t2[c.oD + 2 * c.pnb + png2 + j];
+        bar();
+        const int o = upos(jj + 1);
+        for (int l = tid; l < s1.nu; l += WT) {
+            const double x = u2[o + l];
+            vu[l] = x;
+            ux[s1.oU + l] = x;
+        }
+        if (tid < s.nx1) {
+            vu[s1.nu + tid] = xn;
+            ux[s1.oU + s1.nu + tid] = xn;
         }
     }
     bar();
-    // equality multipliers: pi_{s-1} = [rq_s + box terms + RSQ_s ux_s + BAbt_s pi_s]_x inside each block
-    for (int ii = 0; ii < a.N2; ii++) {
-        const PcBlock blk = a.blk[ii];
-        const WideStage sl = st[blk.s0 + blk.T - 1];
-        for (int l = tid; l < sl.nx1; l += WT) pi[sl.oP + l] = pi2[st2[ii].oP + l];
+    // equality multipliers: the block's last pi is the condensed one; inner ones by the backward
+    // stationarity recursion pi_{s-1} = [rq_s + box terms + RSQ_s ux_s + BAbt_s pi_s]_x
+    {
+        const WideStage sl = st[s0 + T - 1];
+        const double* p2 = a.pi2 + (long)p * a.sP2 + st2[ii].oP;
+        for (int l = tid; l < sl.nx1; l += WT) {
+            const double x = p2[l];
+            vp[l] = x;
+            pi[sl.oP + l] = x;
+        }
+    }
+    for (int jj = 0; jj < T - 1; jj++) {
+        const int sI = s0 + T - 1 - jj;
+        const WideStage s = st[sI], sm1 = st[sI - 1];
+        const int nux = s.nu + s.nx;
+        load_dense<4>(Bt, ld, BAbt + s.oB, s.sdB, nux, s.nx1);
+        load_dense<4>(Rt, ld, RSQ + s.oR, s.sdR, nux + 1, nux);
+        load_flat<2>(vu, ux + s.oU, nux);
+        for (int l = tid; l < nux; l += WT) w[l] = 0.0;
         bar();
-        for (int jj = 0; jj < blk.T - 1; jj++) {
-            const int sI = blk.s0 + blk.T - 1 - jj;
-            const WideStage s = st[sI], sm1 = st[sI - 1];
-            const int nux = s.nu + s.nx;
-            // box terms by variable (w holds -lam_l + lam_u at idxb, 0 elsewhere)
-            for (int l = tid; l < nux; l += WT) w[l] = 0.0;
-            bar();
-            if (tid == 0)
-                for (int l = 0; l < s.nb; l++) w[a.idxb[s.oI + l]] += -lam[s.oD + l] + lam[s.oD + s.pnb + l];
-            bar();
-            const double* R = RSQ + s.oR;
-            const double* B = BAbt + s.oB;
-            if (tid < s.nx) {
-                const int i = s.nu + tid;
-                double acc = hrq ? hrq[s.oU + i] : P4(R, s.sdR, nux, i);
-                acc += w[i];
-                double sy = 0.0;
-                for (int j = 0; j < nux; j++) sy += (i >= j ? P4(R, s.sdR, i, j) : P4(R, s.sdR, j, i)) * ux[s.oU + j];
-                acc += sy;
-                double sg = 0.0;
-                for (int j = 0; j < s.nx1; j++) sg += P4(B, s.sdB, i, j) * pi[s.oP + j];
-                acc += sg;
-                pi[sm1.oP + tid] = acc;
-            }
-            bar();
+        if (tid == 0)
+            for (int l = 0; l < s.nb; l++) w[a.idxb[s.oI + l]] += -lam[s.oD + l] + lam[s.oD + s.pnb + l];
+        bar();
+        double acc = 0.0;
+        if (tid < s.nx) {
+            const int i = s.nu + tid;
+            acc = hrq ? hrq[s.oU + i] : Rt[nux + i * ld];
+            acc += w[i];
+            double sy = 0.0;
+            for (int j = 0; j < nux; j++) sy += (i >= j ? Rt[i + j * ld] : Rt[j + i * ld]) * vu[j];
+            acc += sy;
+            double sg = 0.0;
+            for (int j = 0; j < s.nx1; j++) sg += Bt[i + j * ld] * vp[j];
+            acc += sg;
+        }
+        bar();
+        if (tid < s.nx) {
+            vp[tid] = acc;
+            pi[sm1.oP + tid] = acc;
         }
     }
 }
@@ -592,7 +678,7 @@ extern "C" int hk_wide_launch(int which, const void* args, int count, int lds_do
         }
         case 2: {
             const PxArgs& a = *static_cast<const PxArgs*>(args);
-            hipLaunchKernelGGL(hk_pexpand, dim3(count), dim3(WT), lds, stream, a);
+            hipLaunchKernelGGL(hk_pexpand, dim3(a.N2, count), dim3(WT), lds, stream, a);
             break;
         }
         default:

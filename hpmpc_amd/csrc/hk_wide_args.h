@@ -60,9 +60,10 @@ struct PcArgs {
     int oR2N;                // terminal condensed RSQrq2 (a copy of RSQrq_N) in the packed condensed array
     int sdRN, nzN;           // its lib4 panel stride and rows
     int offP, offX, offW, offB, ldP, ldX, ldW, ldB;  // dynamic LDS carve
+    int offGA, offGB;                                // Gamma_{j-1} / Gamma_j tiles (and stage scratch)
 };
 
-// Expansion (d_part_expand_solution): one workgroup per problem.
+// Expansion (d_part_expand_solution): one workgroup per (block, problem).
 struct PxArgs {
     int N, N2, nprob, p0;
     const WideStage* st;     // original stages (oU, oP for the full-space vectors)
@@ -75,5 +76,5 @@ struct PxArgs {
     const double *ux2, *pi2, *lam2, *t2;
     long long sU2, sP2, sC2;
     double *ux, *pi, *lam, *t;
-    int offV, offW;          // dynamic LDS carve
+    int offB, offR, offV, offW, offQ, ldT;  // dynamic LDS carve: BAbt tile, RSQrq tile, ux_j, box terms, pi_j
 };

@@ -84,7 +84,7 @@ WLayout make_layout(int N, const int* nx, const int* nu, const int* nb, const in
     }
     L.ldW = nzM;
     L.ldX = nxM + 1;
-    L.offW = Mmax;
+    L.offW = Mmax + nzM;  // the forward stages L_k with its 1/diag tail into M
     L.offX = L.offW + L.ldW * nxM;
     L.offV = L.offX + L.ldX * nxM;
     L.lds = L.offV + nzM;
@@ -261,8 +261,8 @@ struct PcPlan {
     long long nG = 0;       // Gamma scratch (doubles per problem)
     long long nG2 = 0;      // condensed DCt2 (doubles per problem)
     long long ref_d = 0;    // the reference's memory carve: doubles before the idxb2 ints
-    int pc_lds = 0, ldP = 0, ldX = 0, ldW = 0, ldB = 0, offP = 0, offX = 0, offW = 0, offB = 0;
-    int px_lds = 0;
+    int pc_lds = 0, ldP = 0, ldX = 0, ldW = 0, ldB = 0, offP = 0, offX = 0, offW = 0, offB = 0, offGA = 0, offGB = 0;
+    int px_lds = 0, ldT = 0, xoB = 0, xoR = 0, xoV = 0, xoW = 0, xoQ = 0;
 };
 
 void problem_size(int N, const int* nx, const int* nu, const int* nb, const int* const* hidxb, const int* ng, int N2,
@@ -353,15 +353,37 @@ bool pc_plan(PcPlan& P, int N, const int* nx, const int* nu_in, const int* nb, c
     }
     P.nG2 = oG2 > 0 ? oG2 : 1;
     P.ref_d = ref_d;
+    // Gamma tiles: the largest (rows x nx_{j+1}) of any block, also used as the RSQrq_{s-1} tile
+    long long gmax = (long long)nzM * nzM;
+    {
+        int Nt = 0;
+        for (int ii = 0; ii < N2; ii++) {
+            int rows = nx[Nt] + 1;
+            for (int j = 0; j < P.blk[ii].T; j++) {
+                rows += nu[Nt + j];
+                gmax = std::max(gmax, (long long)rows * nx[Nt + j + 1]);
+            }
+            Nt += P.blk[ii].T;
+        }
+    }
     P.ldP = P.ldW = P.ldB = nzM;
     P.ldX = nxM + 1;
     P.offP = 0;
     P.offX = P.ldP * nzM;
     P.offW = P.offX + P.ldX * nxM;
     P.offB = P.offW + P.ldW * nxM;
-    P.pc_lds = P.offB + P.ldB * nxM;
-    P.px_lds = nzM;
-    if (P.pc_lds > LDS_MAX_DOUBLES) {
+    P.offGA = P.offB + P.ldB * nxM;
+    P.offGB = P.offGA + (int)gmax;
+    P.pc_lds = P.offGB + (int)gmax;
+    // expansion tiles: BAbt (nzM x nxM), RSQrq (nzM x nzM), ux_j, box terms, pi_j
+    P.ldT = nzM;
+    P.xoB = 0;
+    P.xoR = P.xoB + nzM * nxM;
+    P.xoV = P.xoR + nzM * nzM;
+    P.xoW = P.xoV + nzM;
+    P.xoQ = P.xoW + nzM;
+    P.px_lds = P.xoQ + std::max(nzM, nxM);
+    if (P.pc_lds > LDS_MAX_DOUBLES || P.px_lds > LDS_MAX_DOUBLES) {
         hk_set_error(HPMPC_MI355X_EUNSUPPORTED, "condensing stage tiles beyond the 64 KiB LDS budget");
         return false;
     }
@@ -391,6 +413,8 @@ void fill_pc_args(const PcPlan& P, PcArgs& a) {
     a.ldX = P.ldX;
     a.ldW = P.ldW;
     a.ldB = P.ldB;
+    a.offGA = P.offGA;
+    a.offGB = P.offGB;
 }
 
 void fill_px_args(const PcPlan& P, PxArgs& a) {
@@ -405,8 +429,12 @@ void fill_px_args(const PcPlan& P, PxArgs& a) {
     a.sU2 = P.cond.nU;
     a.sP2 = P.cond.nP;
     a.sC2 = P.cond.nD;
-    a.offV = 0;
-    a.offW = 0;
+    a.offB = P.xoB;
+    a.offR = P.xoR;
+    a.offV = P.xoV;
+    a.offW = P.xoW;
+    a.offQ = P.xoQ;
+    a.ldT = P.ldT;
 }
 
 }  // namespace

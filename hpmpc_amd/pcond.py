@@ -158,3 +158,76 @@ class PcondSolver:
         U = [ux[self.off[k, 3]:self.off[k, 3] + qp.nux(k)].copy() for k in range(self.N + 1)]
         Pi = [pi[self.off[k, 4]:self.off[k, 4] + int(qp.nx[k + 1])].copy() for k in range(self.N)]
         return U, Pi
+
+
+# ------------------------------------------------------------------------------------------------
+# Algorithmic work of the pipeline (SURVEY.md §8d accounting: each datum once per kernel pass, fp64)
+# ------------------------------------------------------------------------------------------------
+def _tri(n):
+    return n * (n + 1) // 2
+
+
+def pcond_algorithmic_bytes(qp: OCPQP, N2: int):
+    """Bytes per problem of [hk_pcond, hk_wide_sv (condensed), hk_pexpand]:
+    condense: BAbt and lower(RSQrq)+gradient row of every stage in, BAbt2 and lower(RSQrq2)+row out;
+    condensed sv: BAbt2, lower(RSQrq2)+row in; packed L + 1/diag, ux2, pi2 out;
+    expand: BAbt, lower(RSQrq)+row of the inner stages, ux2, pi2 in; ux, pi out."""
+    N = qp.N
+    nux = [qp.nux(k) for k in range(N + 1)]
+    nx = [int(v) for v in qp.nx]
+    bB = sum((nux[k] + 1) * nx[k + 1] for k in range(N))
+    bR = sum(_tri(nux[k]) + nux[k] for k in range(N + 1))
+    blocks = _blocks(N, N2)
+    nv, nx2 = [], []
+    s = 0
+    for T in blocks:
+        nv.append(sum(int(qp.nu[s + j]) for j in range(T)) + nx[s])
+        nx2.append(nx[s + T])
+        s += T
+    b2B = sum((nv[i] + 1) * nx2[i] for i in range(N2))
+    b2R = sum(_tri(nv[i]) + nv[i] for i in range(N2)) + _tri(nux[N]) + nux[N]
+    fac = sum(_tri(nv[i]) + nv[i] + nv[i] for i in range(N2)) + _tri(nux[N]) + 2 * nux[N]
+    u2 = sum(nv) + nux[N]
+    p2 = sum(nx2)
+    cond = 8.0 * (bB + bR + b2B + b2R)
+    sv = 8.0 * (b2B + b2R + fac + u2 + p2)
+    expand = 8.0 * (bB + bR + u2 + p2 + sum(nux) + sum(nx[1:]))
+    return cond, sv, expand
+
+
+def _blocks(N, N2):
+    N1, R1 = N // N2, N - N2 * (N // N2)
+    return [N1 + 1 if i < R1 else N1 for i in range(N2)]
+
+
+def pcond_flops(qp: OCPQP, N2: int):
+    """Flops per problem of [condense, condensed sv, expand] by the restated algorithm (d_part_cond.c,
+    lqcp_solvers/d_back_ric_rec.c; sv by the reference's closed form test_d_ric_mpc.c:578-590 on the condensed
+    sizes)."""
+    from .batch import flops_sv
+
+    N = qp.N
+    nx = [int(v) for v in qp.nx]
+    nu = [int(v) for v in qp.nu]
+    cond = 0.0
+    s = 0
+    nv_l, nx2_l = [], []
+    for T in _blocks(N, N2):
+        rows = nx[s] + 1
+        for j in range(T):
+            rows += nu[s + j]
+            if j > 0:  # Gamma_j = Gamma_{j-1} A_j
+                cond += 2.0 * (rows - nu[s + j]) * nx[s + j] * nx[s + j + 1]
+        rows = nx[s] + 1 + nu[s]
+        for j in range(1, T):  # state cost-to-go propagation + cross terms per stage
+            st = s + j
+            nxs, nus, nuxp = nx[st], nu[st], nu[st - 1] + nx[st - 1]
+            r_prev = nx[s] + 1 + sum(nu[s:st])
+            cond += 2.0 * r_prev * nxs * nus + nxs ** 3 / 3.0 + (nuxp + 1) * nxs * nxs + (nuxp + 1) * nuxp * nxs
+        nv_l.append(sum(nu[s:s + T]) + nx[s])
+        nx2_l.append(nx[s + T])
+        s += T
+    nv = int(round(np.mean(nv_l[1:] if len(nv_l) > 1 else nv_l)))
+    sv = flops_sv(N2, nx2_l[-1], nv - nx2_l[-1])
+    expand = sum(2.0 * (nu[k] + nx[k]) * nx[k + 1] * 2 + 2.0 * nx[k] * (nu[k] + nx[k]) for k in range(N))
+    return cond, sv, expand
