@@ -19,6 +19,7 @@ namespace {
 using hk::gld;
 
 constexpr int WT = 256;  // threads per workgroup
+constexpr int PC_GCH = 12;  // Gamma outputs per lane in the condensing (rows x nx <= 3072, host-checked)
 constexpr int BS = 4;
 
 __device__ __forceinline__ int p4i(int i, int j, int sd) { return (i / BS) * BS * sd + i % BS + BS * j; }
@@ -278,9 +279,8 @@ __global__ __launch_bounds__(WT) void hk_pcond(PcArgs a) {
     double* d2 = a.d2 + (long)p * a.sD2 + blk.oD2;
     double* Pl = sm + a.offP;  // pL (dense, ld ldP)
     double* X = sm + a.offX;   // Lx / chol scratch (ld ldX)
-    double* W = sm + a.offW;   // W (ld ldW)
-    double* Bt = sm + a.offB;  // stage BAbt tile (ld ldB)
-    const int ldP = a.ldP, ldX = a.ldX, ldW = a.ldW, ldB = a.ldB;
+    double* Bt = sm + a.offB;  // stage BAbt tile, then W in place (ld ldB)
+    const int ldP = a.ldP, ldX = a.ldX, ldB = a.ldB;
 
     // Gamma row counts / offsets (rows r_j = sum_{i<=j} nu_i + nx0 + 1)
     auto rows = [&](int j) {
@@ -297,9 +297,9 @@ __global__ __launch_bounds__(WT) void hk_pcond(PcArgs a) {
         return o;
     };
 
-    // ---- d_cond_BAbt: Gamma_{j-1} stays in LDS (GA) while Gamma_j is built in GB and streamed to HBM ----
+    // ---- d_cond_BAbt: Gamma_{j-1} stays in LDS (GA); Gamma_j is accumulated in registers (<= PC_GCH
+    // outputs per lane, checked by the host), then overwrites GA and streams to HBM ----
     double* GA = sm + a.offGA;
-    double* GB = sm + a.offGB;
     {
         const WideStage s = st[0];
         const int r0 = s.nu + s.nx + 1;
@@ -310,29 +310,38 @@ __global__ __launch_bounds__(WT) void hk_pcond(PcArgs a) {
     for (int j = 1; j < T; j++) {
         const WideStage s = st[j];
         const int nuj = s.nu, nxj = s.nx, nx1 = s.nx1, nzj = nuj + nxj + 1;
-        const int rp = rows(j - 1), rj = rp + nuj;
+        const int rp = rows(j - 1), rj = rp + nuj, n = rj * nx1;
         double* Gj = G + goff(j);
         load_dense<8>(Bt, ldB, BAbt + s.oB, s.sdB, nzj, nx1);
         bar();
-        for (int e = tid; e < rj * nx1; e += WT) {
-            const int i = e % rj, c = e / rj;
-            double val;
-            if (i < nuj) {
-                val = Bt[i + c * ldB];
-            } else {
-                const int ip = i - nuj;
-                double acc = 0.0;
-                for (int l = 0; l < nxj; l++) acc += GA[ip + l * rp] * Bt[nuj + l + c * ldB];
-                val = acc;
-                if (i == rj - 1) val += Bt[nuj + nxj + c * ldB];
+        double val[PC_GCH];
+#pragma unroll
+        for (int u = 0; u < PC_GCH; u++) {
+            const int e = tid + u * WT, i = e % rj, c = e / rj;
+            double v = 0.0;
+            if (e < n) {
+                if (i < nuj) {
+                    v = Bt[i + c * ldB];
+                } else {
+                    const int ip = i - nuj;
+                    double acc = 0.0;
+                    for (int l = 0; l < nxj; l++) acc += GA[ip + l * rp] * Bt[nuj + l + c * ldB];
+                    v = acc;
+                    if (i == rj - 1) v += Bt[nuj + nxj + c * ldB];
+                }
             }
-            GB[i + c * rj] = val;
-            Gj[i + c * rj] = val;
+            val[u] = v;
         }
         bar();
-        double* sw = GA;
-        GA = GB;
-        GB = sw;
+#pragma unroll
+        for (int u = 0; u < PC_GCH; u++) {
+            const int e = tid + u * WT;
+            if (e < n) {
+                GA[e] = val[u];
+                Gj[e] = val[u];
+            }
+        }
+        bar();
     }
     {
         const int rT = rows(T - 1), nxT = st[T - 1].nx1;
@@ -378,60 +387,62 @@ __global__ __launch_bounds__(WT) void hk_pcond(PcArgs a) {
             // D: the u_s x u_s block
             for (int j = tid >> 6; j < nus; j += WT / 64)
                 for (int i = j + (tid & 63); i < nus; i += 64) *P4w(R2, cnux2, os + i, os + j) = Pl[i + j * ldP];
-            // M: Gamma_{s-1} times the x_s x u_s block of pL; m: + the r row on the gradient row
-            {
-                const int r0 = rows(sI - 1);
-                load_flat<8>(GA, G + goff(sI - 1), r0 * nxs);
-                bar();
-                const double* Gp = GA;
-                for (int e = tid; e < r0 * nus; e += WT) {
-                    const int i = e % r0, c = e / r0;
-                    double acc = 0.0;
-                    for (int l = 0; l < nxs; l++) acc += Gp[i + l * r0] * Pl[nus + l + c * ldP];
-                    if (i == r0 - 1) acc += Pl[nux + c * ldP];
-                    *P4w(R2, cnux2, os + nus + i, os + c) = acc;
-                }
-            }
-            // Lx = chol_aug(pL[x, x] with its gradient row), right-looking in X
+            // Gamma_{s-1} into GA; the state block of pL (with its gradient row) into X
+            const int r0 = rows(sI - 1);
+            load_flat<8>(GA, G + goff(sI - 1), r0 * nxs);
             for (int j = tid >> 6; j < nxs; j += WT / 64)
                 for (int i = j + (tid & 63); i <= nxs; i += 64) X[i + j * ldX] = Pl[nus + i + (nus + j) * ldP];
             bar();
-            for (int j = 0; j < nxs; j++) {
-                const double d = X[j + j * ldX];
-                double sq = 0.0, inv = 0.0;
-                if (d > 1e-15) {
-                    sq = sqrt(d);
-                    inv = 1.0 / sq;
-                }
-                // trailing update reads the unscaled column j, then the column is scaled (after a barrier)
-                for (int c = j + 1 + (tid >> 6); c < nxs; c += WT / 64) {
-                    const double lc = X[c + j * ldX] * inv;
-                    for (int i = c + (tid & 63); i <= nxs; i += 64) X[i + c * ldX] -= (X[i + j * ldX] * inv) * lc;
-                }
-                bar();
-                for (int i = j + tid; i <= nxs; i += WT) X[i + j * ldX] = i == j ? sq : X[i + j * ldX] * inv;
-                bar();
+            // M: Gamma_{s-1} times the x_s x u_s block of pL; m: + the r row on the gradient row
+            for (int e = tid; e < r0 * nus; e += WT) {
+                const int i = e % r0, c = e / r0;
+                double acc = 0.0;
+                for (int l = 0; l < nxs; l++) acc += GA[i + l * r0] * Pl[nus + l + c * ldP];
+                if (i == r0 - 1) acc += Pl[nux + c * ldP];
+                *P4w(R2, cnux2, os + nus + i, os + c) = acc;
             }
-            // W = BAbt_{s-1} Lx, last row += l; pL = RSQ_{s-1} + W W'
+            // Lx = chol_aug(X) inside wave 0 (row i on lane i, nxs + 1 <= 64 rows), right-looking
+            if (tid < 64) {
+                const int i = tid;
+                for (int j = 0; j < nxs; j++) {
+                    const double d = X[j + j * ldX];
+                    double sq = 0.0, inv = 0.0;
+                    if (d > 1e-15) {
+                        sq = sqrt(d);
+                        inv = 1.0 / sq;
+                    }
+                    const bool live = i > j && i <= nxs;
+                    const double li = live ? X[i + j * ldX] * inv : 0.0;
+                    wave_sync();
+                    if (live) X[i + j * ldX] = li;
+                    if (i == j) X[j + j * ldX] = sq;
+                    for (int c = j + 1; c < nxs; c++) {
+                        const double lc = __shfl(li, c);
+                        if (i >= c && i <= nxs) X[i + c * ldX] -= li * lc;
+                    }
+                    wave_sync();
+                }
+            }
+            bar();
+            // W = BAbt_{s-1} Lx (in place in Bt, row i by one thread), last row += l; pL = RSQ_{s-1} + W W'
             const WideStage sp = st[sI - 1];
             const int nuxp = sp.nu + sp.nx, nzp = nuxp + 1;
             load_dense<8>(Bt, ldB, BAbt + sp.oB, sp.sdB, nzp, nxs);
-            // RSQrq_{s-1} lower (+ gradient row) into GB as a dense tile (ld nzp)
-            load_dense<8>(GB, nzp, RSQ + sp.oR, sp.sdR, nzp, nuxp);
+            load_dense<8>(Pl, ldP, RSQ + sp.oR, sp.sdR, nzp, nuxp);
             bar();
-            for (int e = tid; e < nzp * nxs; e += WT) {
-                const int i = e % nzp, c = e / nzp;
-                double acc = 0.0;
-                for (int l = c; l < nxs; l++) acc += Bt[i + l * ldB] * X[l + c * ldX];
-                if (i == nuxp) acc += X[nxs + c * ldX];
-                W[i + c * ldW] = acc;
-            }
+            for (int i = tid; i < nzp; i += WT)
+                for (int c = 0; c < nxs; c++) {
+                    double acc = 0.0;
+                    for (int l = c; l < nxs; l++) acc += Bt[i + l * ldB] * X[l + c * ldX];
+                    if (i == nuxp) acc += X[nxs + c * ldX];
+                    Bt[i + c * ldB] = acc;
+                }
             bar();
             for (int j = tid >> 6; j < nuxp; j += WT / 64)
                 for (int i = j + (tid & 63); i <= nuxp; i += 64) {
                     double acc = 0.0;
-                    for (int l = 0; l < nxs; l++) acc += W[i + l * ldW] * W[j + l * ldW];
-                    Pl[i + j * ldP] = GB[i + j * nzp] + acc;
+                    for (int l = 0; l < nxs; l++) acc += Bt[i + l * ldB] * Bt[j + l * ldB];
+                    Pl[i + j * ldP] += acc;
                 }
             bar();
         }

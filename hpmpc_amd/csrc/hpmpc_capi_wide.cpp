@@ -370,11 +370,16 @@ bool pc_plan(PcPlan& P, int N, const int* nx, const int* nu_in, const int* nb, c
     P.ldX = nxM + 1;
     P.offP = 0;
     P.offX = P.ldP * nzM;
-    P.offW = P.offX + P.ldX * nxM;
-    P.offB = P.offW + P.ldW * nxM;
+    P.offB = P.offX + P.ldX * nxM;
+    P.offW = P.offB;  // W is formed in place in the BAbt tile
     P.offGA = P.offB + P.ldB * nxM;
-    P.offGB = P.offGA + (int)gmax;
-    P.pc_lds = P.offGB + (int)gmax;
+    P.offGB = 0;
+    P.pc_lds = P.offGA + (int)gmax;
+    if (gmax > 12 * 256 || nxM > 63) {  // hk_pcond: PC_GCH Gamma outputs per lane; the state Cholesky in one wave
+        hk_set_error(HPMPC_MI355X_EUNSUPPORTED, "condensing block beyond the kernel's tile limits "
+                                                "(Gamma rows x nx <= 3072, nx <= 63)");
+        return false;
+    }
     // expansion tiles: BAbt (nzM x nxM), RSQrq (nzM x nzM), ux_j, box terms, pi_j
     P.ldT = nzM;
     P.xoB = 0;
