@@ -406,6 +406,74 @@ class HpmpcAPI:
 
         return call
 
+    # --------------------------------------------------------------------------------------------- c_interface.h
+    def _iface_args(self, P, order):
+        """Dense interface-form problem (oracle/iface_oracle.py) -> the wrappers' double** arguments; column-major
+        for order 'F' (fortran_order_*), row-major for 'C' (c_order_*)."""
+        flat = lambda M: np.ascontiguousarray(np.asarray(M, dtype=np.float64).flatten(order)).reshape(-1)
+        pad = lambda v: np.concatenate([np.asarray(v, dtype=np.float64).reshape(-1), np.zeros(4)])
+        keep = {}
+        for key in ("A", "B", "Q", "S", "R", "C", "D"):
+            keep[key] = [pad(flat(M)) for M in P[key]]
+        for key in ("b", "q", "r", "lb", "ub", "lg", "ug"):
+            keep[key] = [pad(v) for v in P[key]]
+        return keep
+
+    def ip_ocp(self, P, N2, *, order="F", k_max=50, mu0=2.0, mu_tol=1e-10, warm=None):
+        """fortran_order_d_ip_ocp_hard_tv / c_order_d_ip_ocp_hard_tv (include/c_interface.h:62,65)."""
+        N = P["N"]
+        nx, nu, nb, ng = iv(P["nx"]), iv(P["nu"]), iv(P["nb"]), iv(P["ng"])
+        idx = [np.ascontiguousarray(i, dtype=np.int32) for i in P["hidxb"]]
+        a = self._iface_args(P, order)
+        x = [np.zeros(P["nx"][k] + 4) for k in range(N + 1)]
+        u = [np.zeros(P["nu"][k] + 4) for k in range(N + 1)]
+        if warm is not None:
+            for k in range(N + 1):
+                x[k][:P["nx"][k]] = warm["x"][k]
+                if k < N:
+                    u[k][:P["nu"][k]] = warm["u"][k]
+        pi = [np.zeros(P["nx"][k + 1] + 4) for k in range(N)]
+        lam = [np.zeros(2 * P["nb"][k] + 2 * P["ng"][k] + 4) for k in range(N + 1)]
+        inf = np.zeros(4)
+        stat = np.zeros(5 * k_max + 5)
+        wsz = self.fn("hpmpc_d_ip_ocp_hard_tv_work_space_size_bytes")(C.c_int(N), nx, nu, nb, ipp(idx), ng,
+                                                                      C.c_int(N2))
+        work0 = np.zeros(wsz // 8 + 16)
+        kk = C.c_int(0)
+        f = self.fn("fortran_order_d_ip_ocp_hard_tv" if order == "F" else "c_order_d_ip_ocp_hard_tv")
+        ret = f(C.byref(kk), C.c_int(k_max), C.c_double(mu0), C.c_double(mu_tol), C.c_int(N), nx, nu, nb, ipp(idx),
+                ng, C.c_int(N2), C.c_int(1 if warm is not None else 0), dpp(a["A"]), dpp(a["B"]), dpp(a["b"]),
+                dpp(a["Q"]), dpp(a["S"]), dpp(a["R"]), dpp(a["q"]), dpp(a["r"]), dpp(a["lb"]), dpp(a["ub"]),
+                dpp(a["C"]), dpp(a["D"]), dpp(a["lg"]), dpp(a["ug"]), dpp(x), dpp(u), dpp(pi), dpp(lam), _dptr(inf),
+                _dptr(work0), _dptr(stat))
+        nxv, nuv = P["nx"], P["nu"]
+        return dict(status=ret, kk=kk.value, stat=stat[:5 * kk.value].copy(), inf_norm_res=inf,
+                    u=[u[k][:nuv[k]] for k in range(N)], x=[x[k][:nxv[k]] for k in range(N + 1)],
+                    pi=[pi[k][:nxv[k + 1]] for k in range(N)],
+                    lam=[lam[k][:2 * P["nb"][k] + 2 * P["ng"][k]] for k in range(N + 1)], work0=work0)
+
+    def kkt_ocp(self, P, work0, *, order="F"):
+        """fortran_order_d_solve_kkt_new_rhs_ocp_hard_tv / c_order_ twin (include/c_interface.h:63,67): new b, q,
+        r and bounds of P on the factor ip_ocp left in work0 (full-space solve)."""
+        N = P["N"]
+        nx, nu, nb, ng = iv(P["nx"]), iv(P["nu"]), iv(P["nb"]), iv(P["ng"])
+        idx = [np.ascontiguousarray(i, dtype=np.int32) for i in P["hidxb"]]
+        a = self._iface_args(P, order)
+        x = [np.zeros(P["nx"][k] + 4) for k in range(N + 1)]
+        u = [np.zeros(P["nu"][k] + 4) for k in range(N + 1)]
+        pi = [np.zeros(P["nx"][k + 1] + 4) for k in range(N)]
+        lam = [np.zeros(2 * P["nb"][k] + 2 * P["ng"][k] + 4) for k in range(N + 1)]
+        inf = np.zeros(4)
+        f = self.fn("fortran_order_d_solve_kkt_new_rhs_ocp_hard_tv" if order == "F"
+                    else "c_order_d_solve_kkt_new_rhs_ocp_hard_tv")
+        f(C.c_int(N), nx, nu, nb, ipp(idx), ng, dpp(a["A"]), dpp(a["B"]), dpp(a["b"]), dpp(a["Q"]), dpp(a["S"]),
+          dpp(a["R"]), dpp(a["q"]), dpp(a["r"]), dpp(a["lb"]), dpp(a["ub"]), dpp(a["C"]), dpp(a["D"]), dpp(a["lg"]),
+          dpp(a["ug"]), dpp(x), dpp(u), dpp(pi), dpp(lam), _dptr(inf), _dptr(work0))
+        nxv, nuv = P["nx"], P["nu"]
+        return dict(inf_norm_res=inf, u=[u[k][:nuv[k]] for k in range(N)], x=[x[k][:nxv[k]] for k in range(N + 1)],
+                    pi=[pi[k][:nxv[k + 1]] for k in range(N)],
+                    lam=[lam[k][:2 * P["nb"][k] + 2 * P["ng"][k]] for k in range(N + 1)])
+
 
 def bq_from_qp(qp: OCPQP):
     """b[k] and q[k] vectors extracted from the augmented rows (as the IPM does, d_ip2_res_hard.c:202-220)."""

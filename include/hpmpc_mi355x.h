@@ -120,6 +120,41 @@ void d_part_expand_solution(int N, int *nx, int *nu, int *nb, int **hidxb, int *
                             double **hlam, double **ht, int N2, int *nx2, int *nu2, int *nb2, int **hidxb2,
                             int *ng2, double **hux2, double **hpi2, double **hlam2, double **ht2, void *work);
 
+/* High-level wrappers of include/c_interface.h: dense problem data in column-major
+ * (fortran_order_*) or row-major (c_order_*) layout, packed to lib4 on the host, then partial condensing (N2 < N,
+ * ng == 0 before stage N) or not, the residual IPM, the expansion and the residual infinity norms
+ * inf_norm_res = [max|r_q|, max|r_b|, max|r_d|, mu], all through the entry points above (on the GPU).
+ * lam is returned compact as [lam_lb (nb) | lam_ub (nb) | lam_lg (ng) | lam_ug (ng)].  The KKT re-solve wrappers
+ * re-use the factor the IPM wrapper left in work0 (full-space solves only). */
+/* include/c_interface.h:59 (interfaces/c/c_interface_work_space.c:70) */
+int hpmpc_d_ip_ocp_hard_tv_work_space_size_bytes(int N, int *nx, int *nu, int *nb, int **hidxb, int *ng, int N2);
+/* include/c_interface.h:62 (interfaces/c/c_order_interface.c:53) */
+int c_order_d_ip_ocp_hard_tv(int *kk, int k_max, double mu0, double mu_tol, int N, int *nx, int *nu, int *nb,
+                             int **hidxb, int *ng, int N2, int warm_start, double **A, double **B, double **b,
+                             double **Q, double **S, double **R, double **q, double **r, double **lb, double **ub,
+                             double **C, double **D, double **lg, double **ug, double **x, double **u, double **pi,
+                             double **lam, double *inf_norm_res, void *work0, double *stat);
+/* include/c_interface.h:63 (interfaces/c/c_order_interface.c:692) */
+void c_order_d_solve_kkt_new_rhs_ocp_hard_tv(int N, int *nx, int *nu, int *nb, int **hidxb, int *ng, double **A,
+                                             double **B, double **b, double **Q, double **S, double **R, double **q,
+                                             double **r, double **lb, double **ub, double **C, double **D, double **lg,
+                                             double **ug, double **x, double **u, double **pi, double **lam,
+                                             double *inf_norm_res, double *work0);
+/* include/c_interface.h:65 (interfaces/c/fortran_order_interface.c:53) */
+int fortran_order_d_ip_ocp_hard_tv(int *kk, int k_max, double mu0, double mu_tol, int N, int *nx, int *nu, int *nb,
+                                   int **hidxb, int *ng, int N2, int warm_start, double **A, double **B, double **b,
+                                   double **Q, double **S, double **R, double **q, double **r, double **lb,
+                                   double **ub, double **C, double **D, double **lg, double **ug, double **x,
+                                   double **u, double **pi, double **lam, double *inf_norm_res, void *work0,
+                                   double *stat);
+/* include/c_interface.h:67 (interfaces/c/fortran_order_interface.c:1082) */
+void fortran_order_d_solve_kkt_new_rhs_ocp_hard_tv(int N, int *nx, int *nu, int *nb, int **hidxb, int *ng,
+                                                   double **A, double **B, double **b, double **Q, double **S,
+                                                   double **R, double **q, double **r, double **lb, double **ub,
+                                                   double **C, double **D, double **lg, double **ug, double **x,
+                                                   double **u, double **pi, double **lam, double *inf_norm_res,
+                                                   double *work0);
+
 /* ================================ Part 2: batched device API ==================================== */
 
 /* Opaque plan: stage sizes, box indices and device tables shared by every problem of a batch. */

@@ -1,0 +1,220 @@
+"""TEST INFRASTRUCTURE ONLY -- restatement of the high-level wrappers of include/c_interface.h.
+
+fortran_order_d_ip_ocp_hard_tv (interfaces/c/fortran_order_interface.c:53-688) and its c_order twin
+(interfaces/c/c_order_interface.c:53-691) are packing code around the hot path: dense problem data -> lib4
+stage blocks (:257-380), the cost-based mu0 when mu0 <= 0 (:311-329), partial condensing when N2 < N and no
+general constraints before stage N (:86-101, :388-545), the residual IPM d_ip2_res_mpc_hard_tv, the
+expansion, the plain residuals d_res_mpc_hard_tv and their infinity norms (:590-686).  This module restates
+that composition in numpy over ANY library exporting the low-level reference prototypes (hpmpc_amd.cabi.HpmpcAPI):
+over oracle/liboracle.so it is the checker of the product's wrappers, over the reference c99 build
+(oracle/_ref) it produces the goldens.  The reference wrapper sources themselves need the reference build
+system's generated include/target.h and are unbuildable here, so the wrappers are pinned by this
+composition over the reference's own low-level entry points.
+
+Problems are given in "interface form": lists of dense numpy matrices A[k] (nx[k+1] x nx[k]), B[k]
+(nx[k+1] x nu[k]), b[k], Q[k], S[k] (nu x nx), R[k], q[k], r[k], lb/ub[k] (nb[k]) with hidxb[k], C[k] (ng x nx),
+D[k] (ng x nu), lg/ug[k].
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from hpmpc_amd.cabi import bq_from_qp
+from hpmpc_amd.ocp import OCPQP, pack_lib4, rup
+
+
+def random_iface_problem(N, nx, nu, nb_u, nb_x, ng=None, seed=0):
+    """Random well-posed OCP in interface form; stage 0 keeps x0 as a variable unless nx[0] == 0.
+    nb_u / nb_x: boxed inputs / states per stage (the first ones)."""
+    rng = np.random.default_rng(seed)
+    nx = list(nx)
+    nu = list(nu) + [0] if len(nu) == N else list(nu)
+    nu[N] = 0
+    ng = [0] * (N + 1) if ng is None else list(ng)
+    P = dict(N=N, nx=nx, nu=nu, ng=ng, A=[], B=[], b=[], Q=[], S=[], R=[], q=[], r=[], lb=[], ub=[], hidxb=[],
+             nb=[], C=[], D=[], lg=[], ug=[])
+    for k in range(N + 1):
+        nxk, nuk = nx[k], nu[k]
+        if k < N:
+            nx1 = nx[k + 1]
+            P["A"].append(np.eye(nx1, nxk) + 0.2 * rng.standard_normal((nx1, nxk)) / np.sqrt(max(nxk, 1)))
+            P["B"].append(rng.standard_normal((nx1, nuk)) / np.sqrt(max(nuk, 1)))
+            P["b"].append(0.1 * rng.standard_normal(nx1))
+        G = rng.standard_normal((nxk + nuk, nxk + nuk))
+        H = G @ G.T / max(nxk + nuk, 1) + np.eye(nxk + nuk)
+        P["R"].append(H[:nuk, :nuk].copy())
+        P["S"].append(H[:nuk, nuk:].copy())
+        P["Q"].append(H[nuk:, nuk:].copy())
+        P["r"].append(0.2 * rng.standard_normal(nuk))
+        P["q"].append(0.2 * rng.standard_normal(nxk))
+        bu = min(nb_u[k] if isinstance(nb_u, (list, tuple)) else nb_u, nuk)
+        bx = min(nb_x[k] if isinstance(nb_x, (list, tuple)) else nb_x, nxk)
+        idx = np.r_[np.arange(bu), nuk + np.arange(bx)].astype(np.int32)
+        P["hidxb"].append(idx)
+        P["nb"].append(len(idx))
+        P["lb"].append(-(0.3 + rng.random(len(idx))))
+        P["ub"].append(0.3 + rng.random(len(idx)))
+        g = ng[k]
+        P["C"].append(rng.standard_normal((g, nxk)) / np.sqrt(max(nxk, 1)))
+        P["D"].append(rng.standard_normal((g, nuk)) / np.sqrt(max(nuk, 1)) if k < N else np.zeros((g, 0)))
+        P["lg"].append(-(0.5 + rng.random(g)))
+        P["ug"].append(0.5 + rng.random(g))
+    return P
+
+
+def to_qp(P) -> OCPQP:
+    """Interface form -> lib4 OCPQP exactly as the wrappers pack it (fortran_order_interface.c:257-380)."""
+    N, nx, nu, ng = P["N"], P["nx"], P["nu"], P["ng"]
+    BAbt, RSQ, DCt, d = [], [], [], []
+    for k in range(N + 1):
+        nuk, nxk = nu[k], nx[k]
+        if k < N:
+            M = np.zeros((nuk + nxk + 1, nx[k + 1]))
+            M[:nuk] = P["B"][k].T
+            M[nuk:nuk + nxk] = P["A"][k].T
+            M[nuk + nxk] = P["b"][k]
+            BAbt.append(pack_lib4(M))
+        M = np.zeros((nuk + nxk + 1, nuk + nxk))
+        M[:nuk, :nuk] = P["R"][k]
+        M[nuk:nuk + nxk, :nuk] = P["S"][k].T
+        M[:nuk, nuk:nuk + nxk] = P["S"][k]
+        M[nuk:nuk + nxk, nuk:nuk + nxk] = P["Q"][k]
+        M[nuk + nxk, :nuk] = P["r"][k]
+        M[nuk + nxk, nuk:] = P["q"][k]
+        RSQ.append(pack_lib4(M))
+        g = ng[k]
+        if g:
+            Dt = np.zeros((nuk + nxk, g))
+            Dt[:nuk] = P["D"][k].T
+            Dt[nuk:] = P["C"][k].T
+            DCt.append(pack_lib4(Dt))
+        else:
+            DCt.append(np.zeros(8))
+        nbk = P["nb"][k]
+        pnb, png = rup(nbk, 4), rup(g, 4)
+        dk = np.zeros(max(2 * pnb + 2 * png, 1))
+        dk[:nbk] = P["lb"][k]
+        dk[pnb:pnb + nbk] = P["ub"][k]
+        dk[2 * pnb:2 * pnb + g] = P["lg"][k]
+        dk[2 * pnb + png:2 * pnb + png + g] = P["ug"][k]
+        d.append(dk)
+    return OCPQP(N, np.array(nx, np.int32), np.array(nu, np.int32), np.array(P["nb"], np.int32),
+                 np.array(ng, np.int32), [i.copy() for i in P["hidxb"]], BAbt, RSQ, d,
+                 DCt if any(ng) else [], None)
+
+
+def auto_mu0(P):
+    """:311-329: mu0 <= 0 -> the largest entry of R, S, Q, r, q (stage N: Q, q)."""
+    m = 0.0
+    for k in range(P["N"] + 1):
+        for key in ("R", "S", "Q", "r", "q"):
+            a = np.asarray(P[key][k])
+            if a.size:
+                m = max(m, float(a.max()))
+    return m
+
+
+def ip_ocp(api, P, N2, k_max=50, mu0=2.0, mu_tol=1e-10, warm=None):
+    """fortran_order_d_ip_ocp_hard_tv restated over `api` (the row-major twin computes the same)."""
+    N, nx, nu, ng, nb = P["N"], P["nx"], P["nu"], P["ng"], P["nb"]
+    qp = to_qp(P)
+    if mu0 <= 0:
+        mu0 = auto_mu0(P)
+    if N2 > N or any(g > 0 for g in ng[:N]):
+        N2 = N
+    if N2 < N:
+        c, _ = api.part_cond(qp.copy(), N2)
+        r = api.ipm(c, k_max=k_max, mu0=mu0, mu_tol=mu_tol, alpha_min=1e-8)
+        e = api.part_expand(qp, c, r["ux"], r["pi"], r["lam"], r["t"])
+        ux, pi, lam, t = e["ux"], e["pi"], e["lam"], e["t"]
+    else:
+        kw = {}
+        if warm is not None:
+            kw = dict(warm_start=1, ux=[np.r_[warm["u"][k] if k < N else [], warm["x"][k]] for k in range(N + 1)])
+        r = api.ipm(qp.copy(), k_max=k_max, mu0=mu0, mu_tol=mu_tol, alpha_min=1e-8, **kw)
+        ux, pi, lam, t = r["ux"], r["pi"], r["lam"], r["t"]
+    out = finish(api, P, qp, ux, pi, lam, t)
+    out.update(status=r["ret"], kk=r["kk"], stat=r["stat"])
+    return out
+
+
+def finish(api, P, qp, ux, pi, lam, t):
+    """Outputs (:590-686): u, x, the equality-box fix, residual infinity norms, pi, compact lam."""
+    N, nx, nu, ng, nb = P["N"], P["nx"], P["nu"], P["ng"], P["nb"]
+    u = [np.array(ux[k][:nu[k]]) for k in range(N)]
+    x = [np.array(ux[k][nu[k]:nu[k] + nx[k]]) for k in range(N + 1)]
+    for k in range(N):
+        for j in range(nb[k]):
+            if P["hidxb"][k][j] >= nu[k]:
+                break
+            if P["lb"][k][j] == P["ub"][k][j]:
+                u[k][P["hidxb"][k][j]] = P["lb"][k][j]
+    b, q = bq_from_qp(qp)
+    res = api.residuals_plain(qp, b, q, ux, pi, lam, t)
+    n0 = max(abs(res["rq"][0][0]), max(float(np.max(np.abs(res["rq"][k][:nu[k] + nx[k]]), initial=0)) for k in range(N)),
+             float(np.max(np.abs(res["rq"][N][:nx[N]]), initial=0)))
+    n1 = max(abs(res["rb"][0][0]), max(float(np.max(np.abs(res["rb"][k][:nx[k + 1]]), initial=0)) for k in range(N)))
+    n2 = abs(res["rd"][0][0])
+    for k in range(N + 1):
+        pnb, png = rup(nb[k], 4), rup(ng[k], 4)
+        idx = np.r_[0:nb[k], pnb:pnb + nb[k], 2 * pnb:2 * pnb + ng[k], 2 * pnb + png:2 * pnb + png + ng[k]].astype(int)
+        if idx.size:
+            n2 = max(n2, float(np.max(np.abs(res["rd"][k][idx]))))
+    lam_c = []
+    for k in range(N + 1):
+        pnb, png = rup(nb[k], 4), rup(ng[k], 4)
+        lam_c.append(np.r_[lam[k][:nb[k]], lam[k][pnb:pnb + nb[k]], lam[k][2 * pnb:2 * pnb + ng[k]],
+                           lam[k][2 * pnb + png:2 * pnb + png + ng[k]]])
+    return dict(u=u, x=x, pi=[np.array(pi[k][:nx[k + 1]]) for k in range(N)], lam=lam_c,
+                inf_norm_res=np.array([n0, n1, n2, res["mu"]]))
+
+
+def kkt_ocp(api, P, P2, k_max=50, mu0=2.0, mu_tol=1e-10):
+    """fortran_order_d_ip_ocp_hard_tv on P (full space), then fortran_order_d_solve_kkt_new_rhs_ocp_hard_tv with
+    the right-hand sides of P2 (b, q, r, bounds; same matrices): d_kkt_solve_new_rhs_res_mpc_hard_tv on the IPM's
+    persisted factor and iterate (d_ip2_res_hard.c:1922-2299), then the wrapper's outputs."""
+    qp = to_qp(P)
+    r = api.ipm(qp.copy(), k_max=k_max, mu0=mu0 if mu0 > 0 else auto_mu0(P), mu_tol=mu_tol, alpha_min=1e-8)
+    qp2 = to_qp(P2)
+    b2, q2 = bq_from_qp(qp2)
+    k = api.kkt_new_rhs(qp2.copy(), r["work"], b2, q2)
+    return finish(api, P2, qp2, k["ux"], k["pi"], k["lam"], k["t"])
+
+
+def new_rhs(P, seed=1):
+    """P with perturbed b, q, r and bounds (the data a KKT re-solve takes)."""
+    rng = np.random.default_rng(seed)
+    Q = {k: ([np.array(a, copy=True) for a in v] if isinstance(v, list) else v) for k, v in P.items()}
+    for key in ("b", "q", "r"):
+        Q[key] = [v + 0.05 * rng.standard_normal(v.shape) for v in P[key]]
+    for key in ("lb", "lg"):
+        Q[key] = [v - 0.05 * rng.random(v.shape) for v in P[key]]
+    for key in ("ub", "ug"):
+        Q[key] = [v + 0.05 * rng.random(v.shape) for v in P[key]]
+    return Q
+
+
+SHAPES = {"A": lambda P, k: (P["nx"][k + 1], P["nx"][k]), "B": lambda P, k: (P["nx"][k + 1], P["nu"][k]),
+          "Q": lambda P, k: (P["nx"][k], P["nx"][k]), "S": lambda P, k: (P["nu"][k], P["nx"][k]),
+          "R": lambda P, k: (P["nu"][k], P["nu"][k]), "C": lambda P, k: (P["ng"][k], P["nx"][k]),
+          "D": lambda P, k: (P["ng"][k], P["nu"][k])}
+
+
+def to_flat(P):
+    """Interface-form problem -> dict of lists of flat float arrays (golden storage)."""
+    out = {}
+    for key in ("A", "B", "Q", "S", "R", "C", "D", "b", "q", "r", "lb", "ub", "lg", "ug"):
+        out["P_" + key] = [np.asarray(M, dtype=np.float64).reshape(-1) for M in P[key]]
+    out["P_hidxb"] = [np.asarray(i, dtype=np.float64) for i in P["hidxb"]]
+    return out
+
+
+def from_flat(N, nx, nu, nb, ng, inp):
+    P = dict(N=N, nx=[int(v) for v in nx], nu=[int(v) for v in nu], nb=[int(v) for v in nb],
+             ng=[int(v) for v in ng])
+    for key in ("b", "q", "r", "lb", "ub", "lg", "ug"):
+        P[key] = [np.array(v) for v in inp["P_" + key]]
+    P["hidxb"] = [np.array(v).astype(np.int32) for v in inp["P_hidxb"]]
+    for key, shp in SHAPES.items():
+        P[key] = [np.array(v).reshape(shp(P, k)) for k, v in enumerate(inp["P_" + key])]
+    return P

@@ -217,6 +217,7 @@ def main():
     # ---------------- alternate IPM: d_ip2_mpc_hard_tv, d_kkt_solve_new_rhs_mpc_hard_tv, d_res_mpc_hard_tv ----
     alt(ref, ref_avx_api(), rng, out)
     pcond(ref, out)
+    iface(ref, out)
     total = sum(os.path.getsize(p) for p in out)
     print(f"wrote {len(out)} cases, {total / 1e6:.2f} MB")
 
@@ -284,8 +285,42 @@ def pcond(ref, out):
         out.append(save_case(f"pcond_sv_N{N}_nx{nx}_nu{nu}_N2_{N2}", "pcond_sv", qp, dict(N2=N2), dict(ux=ux, pi=pi)))
 
 
+def iface(ref, out):
+    """High-level wrappers of include/c_interface.h, restated by oracle/iface_oracle.py over the reference's own
+    low-level entry points (the reference wrapper sources need the generated include/target.h and are
+    unbuildable here): full space, partially condensed, stage-0 state as a variable with general constraints at
+    N, the cost-based mu0, and the KKT re-solve with new right-hand sides."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import iface_oracle as IO
+
+    cases = [("full_N10_nx4_nu2", (10, [0] + [4] * 10, [2] * 10, 2, 2, None, 0), 10, 2.0),
+             ("cond_N12_nx4_nu1_N2_4", (12, [0] + [4] * 12, [1] * 12, 1, 2, None, 1), 4, 2.0),
+             ("x0var_ngN_N8_nx3_nu2", (8, [3] * 9, [2] * 8, 1, 1, [0] * 8 + [2], 2), 8, 2.0),
+             ("automu0_N15_nx6_nu3", (15, [0] + [6] * 15, [3] * 15, 3, 3, None, 3), 15, -1.0)]
+    for name, (N, nx, nu, bu, bx, ng, seed), N2, mu0 in cases:
+        P = IO.random_iface_problem(N, nx, nu, bu, bx, ng, seed=seed)
+        r = IO.ip_ocp(ref, P, N2, k_max=50, mu0=mu0, mu_tol=1e-10)
+        qp = IO.to_qp(P)
+        outs = dict(u=r["u"], x=r["x"], pi=r["pi"], lam=r["lam"], inf_norm_res=r["inf_norm_res"], kk=r["kk"],
+                    ret=r["status"], stat=r["stat"])
+        out.append(save_case(f"iface_{name}", "iface", qp, dict(N2=N2, mu0=mu0, mu_tol=1e-10, k_max=50), outs,
+                             extra=IO.to_flat(P)))
+    P = IO.random_iface_problem(10, [0] + [4] * 10, [2] * 10, 2, 2, None, seed=5)
+    P2 = IO.new_rhs(P, seed=6)
+    k = IO.kkt_ocp(ref, P, P2, mu_tol=1e-10)
+    extra = IO.to_flat(P)
+    extra.update({"N" + key: v for key, v in IO.to_flat(P2).items()})
+    out.append(save_case("iface_kkt_N10_nx4_nu2", "iface_kkt", IO.to_qp(P), dict(mu0=2.0, mu_tol=1e-10, k_max=50),
+                         dict(u=k["u"], x=k["x"], pi=k["pi"], lam=k["lam"], inf_norm_res=k["inf_norm_res"]),
+                         extra=extra))
+
+
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] == "pcond":
+    if len(sys.argv) > 1 and sys.argv[1] == "iface":
+        o = []
+        iface(ref_api(), o)
+        print(f"wrote {len(o)} iface cases, {sum(os.path.getsize(p) for p in o) / 1e6:.2f} MB")
+    elif len(sys.argv) > 1 and sys.argv[1] == "pcond":
         o = []
         pcond(ref_api(), o)
         print(f"wrote {len(o)} pcond cases, {sum(os.path.getsize(p) for p in o) / 1e6:.2f} MB")

@@ -66,7 +66,56 @@ def run_case(api, case):
         return dict(cqp=c, ux=e["ux"], pi=e["pi"], lam=e["lam"], t=e["t"])
     if case.kind == "pcond_sv":
         return pcond_sv(api, qp, int(a["N2"]))
+    if case.kind in ("iface", "iface_kkt"):
+        return run_iface(api, case)
     raise ValueError(case.kind)
+
+
+def _iface_oracle():
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    import iface_oracle
+
+    return iface_oracle
+
+
+def run_iface(api, case, order="F"):
+    """The c_interface.h wrappers: through the library's own wrapper symbols when it has them (the product),
+    else the restatement oracle/iface_oracle.py over the library's low-level entry points (the oracle)."""
+    IO = _iface_oracle()
+    qp, a = case.qp, case.args
+    P = IO.from_flat(qp.N, qp.nx, qp.nu, qp.nb, qp.ng, case.inp)
+    kw = dict(k_max=int(a["k_max"]), mu0=a["mu0"], mu_tol=a["mu_tol"])
+    has = hasattr(api.lib, api.p + "fortran_order_d_ip_ocp_hard_tv")
+    if case.kind == "iface":
+        r = api.ip_ocp(P, int(a["N2"]), order=order, **kw) if has else IO.ip_ocp(api, P, int(a["N2"]), **kw)
+        out = {k: r[k] for k in ("u", "x", "pi", "lam", "inf_norm_res", "kk", "stat")}
+        out["ret"] = r["status"]
+        return out
+    P2 = IO.from_flat(qp.N, qp.nx, qp.nu, qp.nb, qp.ng, {k[1:]: v for k, v in case.inp.items() if k.startswith("NP_")})
+    if has:
+        r = api.ip_ocp(P, qp.N, order=order, **kw)
+        k = api.kkt_ocp(P2, r["work0"], order=order)
+    else:
+        k = IO.kkt_ocp(api, P, P2, **kw)
+    return {key: k[key] for key in ("u", "x", "pi", "lam", "inf_norm_res")}
+
+
+def check_iface(case, got):
+    out = case.out
+    if "kk" in out:
+        assert int(got["kk"]) == int(out["kk"]) and int(got["ret"]) == int(out["ret"]), (case.name, got["kk"], out["kk"])
+        np.testing.assert_allclose(got["stat"], out["stat"], rtol=TOL_STAT, atol=1e-14, err_msg=case.name)
+    for key in ("u", "x", "pi", "lam"):
+        for k, (g, r) in enumerate(zip(got[key], out[key])):
+            g, r = np.asarray(g), np.asarray(r)
+            if r.size:
+                e = float(np.max(np.abs(g - r) / np.maximum(1.0, np.abs(r))))
+                assert e <= TOL_IPM, f"{case.name}: {key}[{k}] err {e:.3e}"
+    # residual infinity norms of a converged solve are rounding-level (~1e-12): absolute comparison
+    np.testing.assert_allclose(got["inf_norm_res"], out["inf_norm_res"], rtol=0, atol=1e-9, err_msg=case.name)
 
 
 def pcond_sv(api, qp, N2):
@@ -152,6 +201,8 @@ def check_case(case, got):
     """Assert parity of `got` against the golden outputs of `case`."""
     if case.kind == "pcond":
         return check_pcond(case, got)
+    if case.kind in ("iface", "iface_kkt"):
+        return check_iface(case, got)
     if case.kind == "pcond_sv":
         for key in ("ux", "pi"):
             e = max_err(case, key, got[key], case.out[key])

@@ -43,7 +43,11 @@ def test_header_declares_reference_entry_points():
                 "d_back_ric_rec_sv_tv_work_space_size_bytes", "d_back_ric_rec_sv_tv_memory_space_size_bytes",
                 "d_ip2_res_mpc_hard_tv", "d_ip2_res_mpc_hard_tv_work_space_size_bytes",
                 "d_ip2_res_mpc_hard_tv_single_newton_step", "d_kkt_solve_new_rhs_res_mpc_hard_tv",
-                "d_res_res_mpc_hard_tv"):
+                "d_res_res_mpc_hard_tv", "d_ip2_mpc_hard_tv", "d_kkt_solve_new_rhs_mpc_hard_tv", "d_res_mpc_hard_tv",
+                "d_part_cond", "d_part_cond_compute_problem_size", "d_part_cond_memory_space_size_bytes",
+                "d_part_expand_solution", "fortran_order_d_ip_ocp_hard_tv", "c_order_d_ip_ocp_hard_tv",
+                "hpmpc_d_ip_ocp_hard_tv_work_space_size_bytes", "fortran_order_d_solve_kkt_new_rhs_ocp_hard_tv",
+                "c_order_d_solve_kkt_new_rhs_ocp_hard_tv"):
         assert ref in names, ref
     assert len(names) >= 19, names
 
@@ -59,7 +63,7 @@ def test_every_reference_citation_resolves():
     text = open(HEADER).read()
     cites = re.findall(r"/\* (include/\w+\.h):(\d+)", text)
     assert len(cites) >= 10
-    assert {c[0] for c in cites} <= {"include/lqcp_solvers.h", "include/mpc_solvers.h"}
+    assert {c[0] for c in cites} <= {"include/lqcp_solvers.h", "include/mpc_solvers.h", "include/c_interface.h"}
 
 
 def test_version_string(hiplib):
