@@ -19,7 +19,8 @@ namespace {
 using hk::gld;
 
 constexpr int WT = 256;  // threads per workgroup
-constexpr int PC_GCH = 12;  // Gamma outputs per lane in the condensing (rows x nx <= 3072, host-checked)
+constexpr int PC_GCH = 12;
+constexpr int WS_TILES = 8;  // W = BAbt Lxx output tiles per wave (nz <= 128, nx <= 64: <= 32 tiles, host-checked)  // Gamma outputs per lane in the condensing (rows x nx <= 3072, host-checked)
 constexpr int BS = 4;
 
 __device__ __forceinline__ int p4i(int i, int j, int sd) { return (i / BS) * BS * sd + i % BS + BS * j; }
@@ -90,11 +91,18 @@ __device__ void load_lower(double* M, const double* src, int sd, int nz, int nc)
             }
     }
 }
-// in-wave ordering of LDS traffic between lanes (single-wave phases need no workgroup barrier)
+// broadcast lane l's double (l wave-uniform) through SGPRs
+__device__ __forceinline__ double rdlane(double v, int l) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+    return __hiloint2double(hi, lo);
+}
+
+// In-wave ordering of LDS traffic between lanes (single-wave phases need no workgroup barrier): wait for this
+// wave's LDS operations only (a release fence would also drain its outstanding global stores).
 __device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 }  // namespace
@@ -120,6 +128,7 @@ __global__ __launch_bounds__(WT) void hk_wide_sv(WideArgs a) {
     double* X = sm + a.offX;
     double* v = sm + a.offV;
     const int ldW = a.ldW, ldX = a.ldX;
+    const int lane = tid & 63, wv = tid >> 6, c16 = lane & 15, g4 = lane >> 4;  // MFMA lane coordinates
     const double* BAbt = a.BAbt + (long)p * a.sB;
     const double* RSQ = a.RSQ + (long)p * a.sR;
     double* F = a.ws + (long)p * a.sW;
@@ -131,16 +140,42 @@ __global__ __launch_bounds__(WT) void hk_wide_sv(WideArgs a) {
         const WideStage s = a.st[k];
         const int nu = s.nu, nux = s.nu + s.nx, nz = nux + 1, nx1 = s.nx1;
         load_lower<4>(M, RSQ + s.oR, s.sdR, nz, nux);
-        if (k < a.N) {
+        if (k < a.N && !(a.skip & 4)) {
             load_dense<8>(W, ldW, BAbt + s.oB, s.sdB, nz, nx1);
             bar();
-            // W = BAbt Lxx (in place, row i by thread: w_c needs W[i, l >= c] only)
-            for (int i = tid; i < nz; i += WT)
-                for (int c = 0; c < nx1; c++) {
-                    double acc = 0.0;
-                    for (int l = c; l < nx1; l++) acc += W[i + l * ldW] * X[l + c * ldX];
-                    W[i + c * ldW] = acc;
+            // W = BAbt_k Lxx_{k+1} (dtrmm_nt_u) on MFMA: 16x16 output tiles, K over the nx1 columns of BAbt; the
+            // tiles are kept in registers and written back over BAbt after a barrier
+            {
+                const int nI = (nz + 15) >> 4, nJ = (nx1 + 15) >> 4, nK = (nx1 + 3) >> 2;
+                hk::d4 acc[WS_TILES];
+#pragma unroll
+                for (int u = 0; u < WS_TILES; u++) {
+                    acc[u] = hk::d4{0.0, 0.0, 0.0, 0.0};
+                    const int t = wv + 4 * u;
+                    if (t < nI * nJ) {
+                        const int I = t % nI, J = t / nI, ra = 16 * I + c16, cb = 16 * J + c16;
+                        for (int kc = 0; kc < nK; kc++) {
+                            const int kk = 4 * kc + g4;
+                            const double av = (ra < nz && kk < nx1) ? W[ra + kk * ldW] : 0.0;
+                            const double bv = (cb < nx1 && kk < nx1) ? X[kk + cb * ldX] : 0.0;
+                            acc[u] = hk::mfma(av, bv, acc[u]);
+                        }
+                    }
                 }
+                bar();
+#pragma unroll
+                for (int u = 0; u < WS_TILES; u++) {
+                    const int t = wv + 4 * u;
+                    if (t < nI * nJ) {
+                        const int I = t % nI, J = t / nI, col = 16 * J + c16;
+#pragma unroll
+                        for (int r = 0; r < 4; r++) {
+                            const int row = 16 * I + g4 + 4 * r;
+                            if (row < nz && col < nx1) W[row + col * ldW] = acc[u][r];
+                        }
+                    }
+                }
+            }
             bar();
             if (a.compute_Pb && tid < nx1) {  // Pb_k = Lxx (Lxx' b_k) from W's last row before + l
                 double acc = 0.0;
@@ -150,41 +185,118 @@ __global__ __launch_bounds__(WT) void hk_wide_sv(WideArgs a) {
             bar();
             if (tid < nx1) W[nux + tid * ldW] += X[nx1 + tid * ldX];
             bar();
-            for (int j = tid >> 6; j < nux; j += WT / 64)
-                for (int i = j + (tid & 63); i < nz; i += 64) {
-                    double acc = 0.0;
-                    for (int r = 0; r < nx1; r++) acc += W[i + r * ldW] * W[j + r * ldW];
-                    M[poff(j, nz) + i - j] += acc;
+            // M += W W' (dsyrk) on MFMA over the lower 16x16 tiles
+            {
+                const int nI = (nz + 15) >> 4, nK = (nx1 + 3) >> 2, nT = nI * (nI + 1) / 2;
+                for (int t = wv; t < nT; t += 4) {
+                    int I = 0;
+                    while ((I + 1) * (I + 2) / 2 <= t) I++;
+                    const int J = t - I * (I + 1) / 2;
+                    const int ra = 16 * I + c16, rb = 16 * J + c16;
+                    hk::d4 acc = {0.0, 0.0, 0.0, 0.0};
+                    for (int kc = 0; kc < nK; kc++) {
+                        const int kk = 4 * kc + g4;
+                        const double av = (ra < nz && kk < nx1) ? W[ra + kk * ldW] : 0.0;
+                        const double bv = (rb < nux && kk < nx1) ? W[rb + kk * ldW] : 0.0;
+                        acc = hk::mfma(av, bv, acc);
+                    }
+                    const int col = 16 * J + c16;
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const int row = 16 * I + g4 + 4 * r;
+                        if (row < nz && col < nux && row >= col) M[poff(col, nz) + row - col] += acc[r];
+                    }
                 }
+            }
         }
         bar();
+        // Cholesky with the augmented row, blocked by 16-column panels: wave 0 factors the panel (row i on
+        // lanes i - j0 and i - j0 + 64, shuffles for the pivot row, no workgroup barrier), then all waves
+        // apply the panel's rank-16 update to the trailing lower tiles on MFMA
         double* Lk = F + s.oL;
         double* dL = Lk + poff(nux, nz);
-        for (int j = 0; j < nux; j++) {
-            const int cj = poff(j, nz);
-            const double d = M[cj];
-            double sq = 0.0, inv = 0.0;
-            if (d > 1e-15) {
-                sq = sqrt(d);
-                inv = 1.0 / sq;
-            }
-            for (int i = j + tid; i < nz; i += WT) {
-                const double l = i == j ? sq : M[cj + i - j] * inv;
-                Lk[cj + i - j] = l;
-                if (j >= nu) X[(i - nu) + (j - nu) * ldX] = l;
-            }
-            if (tid == 0) dL[j] = inv;
-            for (int c = j + 1 + (tid >> 6); c < nux; c += WT / 64) {
-                const double lc = M[cj + c - j] * inv;
-                const int cc = poff(c, nz);
-                for (int i = c + (tid & 63); i < nz; i += 64) M[cc + i - c] -= (M[cj + i - j] * inv) * lc;
+        for (int p0 = 0; p0 < ((a.skip & 2) ? 0 : nux); p0 += 16) {
+            const int pe = p0 + 16 < nux ? p0 + 16 : nux;
+            if (wv == 0) {
+                // the panel (rows p0.., its <= 16 columns) in registers: lane L holds rows p0+L and p0+L+64
+                const int pw = pe - p0, r0 = p0 + lane, r1 = r0 + 64;
+                double c0[16], c1[16];
+#pragma unroll
+                for (int jj = 0; jj < 16; jj++) {
+                    const int j = p0 + jj, cj = poff(j < nux ? j : 0, nz);
+                    c0[jj] = (jj < pw && r0 >= j && r0 < nz) ? M[cj + r0 - j] : 0.0;
+                    c1[jj] = (jj < pw && r1 < nz) ? M[cj + r1 - j] : 0.0;
+                }
+#pragma unroll
+                for (int jj = 0; jj < 16; jj++) {
+                    if (jj < pw) {
+                        const double d = rdlane(c0[jj], jj);
+                        double sq = 0.0, inv = 0.0;
+                        if (d > 1e-15) {
+                            sq = sqrt(d);
+                            inv = 1.0 / sq;
+                        }
+                        c0[jj] = lane == jj ? sq : (lane > jj ? c0[jj] * inv : 0.0);
+                        c1[jj] = c1[jj] * inv;
+                        if (lane == 0) M[poff(nux, nz) + p0 + jj] = inv;
+#pragma unroll
+                        for (int cc = jj + 1; cc < 16; cc++) {
+                            const double lc = rdlane(c0[jj], cc);
+                            c0[cc] -= c0[jj] * lc;
+                            c1[cc] -= c1[jj] * lc;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int jj = 0; jj < 16; jj++) {
+                    const int j = p0 + jj;
+                    if (jj < pw) {
+                        const int cj = poff(j, nz);
+                        if (r0 >= j && r0 < nz) {
+                            M[cj + r0 - j] = c0[jj];
+                            if (j >= nu) X[(r0 - nu) + (j - nu) * ldX] = c0[jj];
+                        }
+                        if (r1 < nz) {
+                            M[cj + r1 - j] = c1[jj];
+                            if (j >= nu) X[(r1 - nu) + (j - nu) * ldX] = c1[jj];
+                        }
+                    }
+                }
             }
             bar();
+            if (pe < nux) {  // trailing update: M[i, jj] -= sum_{k in panel} L[i, k] L[jj, k], tiles from pe
+                const int T0 = pe >> 4, nI = (nz + 15) >> 4, nTI = nI - T0;
+                const int nT = nTI * (nTI + 1) / 2, nK = (pe - p0 + 3) >> 2;
+                for (int t = wv; t < nT; t += 4) {
+                    int I = 0;
+                    while ((I + 1) * (I + 2) / 2 <= t) I++;
+                    const int J = t - I * (I + 1) / 2;
+                    const int ra = 16 * (T0 + I) + c16, rb = 16 * (T0 + J) + c16;
+                    hk::d4 acc = {0.0, 0.0, 0.0, 0.0};
+                    for (int kc = 0; kc < nK; kc++) {
+                        const int kk = p0 + 4 * kc + g4;
+                        const bool kok = kk < pe;
+                        const double av = (ra < nz && kok) ? M[poff(kk, nz) + ra - kk] : 0.0;
+                        const double bv = (rb < nux && kok) ? M[poff(kk, nz) + rb - kk] : 0.0;
+                        acc = hk::mfma(av, bv, acc);
+                    }
+                    const int col = 16 * (T0 + J) + c16;
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const int row = 16 * (T0 + I) + g4 + 4 * r;
+                        if (row < nz && col < nux && row >= col) M[poff(col, nz) + row - col] -= acc[r];
+                    }
+                }
+                bar();
+            }
         }
-        // strictly upper part of the copied Lxx stays zero
+        // the factor (packed columns + 1/diag) to HBM in one coalesced sweep
+        for (int e = tid; e < poff(nux, nz) + nux; e += WT) Lk[e] = M[e];
+        (void)dL;
+        // strictly upper part of the copied Lxx stays zero (the next stage's MFMA trmm reads whole tiles)
         for (int e = tid; e < s.nx * s.nx; e += WT) {
-            const int i = e % s.nx, c = e / s.nx;
-            if (i < c) X[i + c * ldX] = 0.0;
+            const int i = e % s.nx, cc = e / s.nx;
+            if (i < cc) X[i + cc * ldX] = 0.0;
         }
         bar();
     }
@@ -196,7 +308,7 @@ __global__ __launch_bounds__(WT) void hk_wide_sv(WideArgs a) {
         const int nz0 = s0.nu + s0.nx + 1;
         load_flat<16>(M, F + s0.oL, poff(nz0 - 1, nz0) + nz0 - 1);
     }
-    for (int k = 0; k < a.N; k++) {
+    for (int k = 0; k < ((a.skip & 1) ? 0 : a.N); k++) {
         const WideStage s = a.st[k];
         const int nux = s.nu + s.nx, nz = nux + 1, nx1 = s.nx1, nu1 = s.nu1;
         const int ns = k == 0 ? nux : s.nu;
@@ -401,24 +513,38 @@ __global__ __launch_bounds__(WT) void hk_pcond(PcArgs a) {
                 if (i == r0 - 1) acc += Pl[nux + c * ldP];
                 *P4w(R2, cnux2, os + nus + i, os + c) = acc;
             }
-            // Lx = chol_aug(X) inside wave 0 (row i on lane i, nxs + 1 <= 64 rows), right-looking
+            // Lx = chol_aug(X) inside wave 0 (row i on lane i, nxs + 1 <= 64 rows): 16-column panels factored in
+            // registers (pivot values broadcast by readlane), each followed by its update of the later columns
             if (tid < 64) {
                 const int i = tid;
-                for (int j = 0; j < nxs; j++) {
-                    const double d = X[j + j * ldX];
-                    double sq = 0.0, inv = 0.0;
-                    if (d > 1e-15) {
-                        sq = sqrt(d);
-                        inv = 1.0 / sq;
+                for (int p0 = 0; p0 < nxs; p0 += 16) {
+                    const int pw = nxs - p0 < 16 ? nxs - p0 : 16;
+                    double cl[16];
+#pragma unroll
+                    for (int jj = 0; jj < 16; jj++)
+                        cl[jj] = (jj < pw && i >= p0 + jj && i <= nxs) ? X[i + (p0 + jj) * ldX] : 0.0;
+#pragma unroll
+                    for (int jj = 0; jj < 16; jj++) {
+                        if (jj < pw) {
+                            const double d = rdlane(cl[jj], p0 + jj);
+                            double sq = 0.0, inv = 0.0;
+                            if (d > 1e-15) {
+                                sq = sqrt(d);
+                                inv = 1.0 / sq;
+                            }
+                            cl[jj] = i == p0 + jj ? sq : (i > p0 + jj ? cl[jj] * inv : 0.0);
+#pragma unroll
+                            for (int cc = jj + 1; cc < 16; cc++) cl[cc] -= cl[jj] * rdlane(cl[jj], p0 + cc);
+                        }
                     }
-                    const bool live = i > j && i <= nxs;
-                    const double li = live ? X[i + j * ldX] * inv : 0.0;
-                    wave_sync();
-                    if (live) X[i + j * ldX] = li;
-                    if (i == j) X[j + j * ldX] = sq;
-                    for (int c = j + 1; c < nxs; c++) {
-                        const double lc = __shfl(li, c);
-                        if (i >= c && i <= nxs) X[i + c * ldX] -= li * lc;
+#pragma unroll
+                    for (int jj = 0; jj < 16; jj++)
+                        if (jj < pw && i >= p0 + jj && i <= nxs) X[i + (p0 + jj) * ldX] = cl[jj];
+                    for (int c = p0 + 16; c < nxs; c++) {  // the panel's update of column c (rows >= c)
+                        double acc = 0.0;
+#pragma unroll
+                        for (int jj = 0; jj < 16; jj++) acc += cl[jj] * rdlane(cl[jj], c);
+                        if (i >= c && i <= nxs) X[i + c * ldX] -= acc;
                     }
                     wave_sync();
                 }

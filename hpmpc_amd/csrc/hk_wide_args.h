@@ -31,6 +31,7 @@ struct WideArgs {
     int compute_pi, compute_Pb;
     int offW, offX, offV;  // dynamic LDS carve (doubles): M packed | W | X | v
     int ldW, ldX;
+    int skip;  // profiling only (HK_WIDE_SKIP): bit 0 forward, bit 1 Cholesky, bit 2 trmm/syrk -- results invalid
 };
 
 // Partial condensing (d_part_cond): one workgroup per (block ii, problem p).

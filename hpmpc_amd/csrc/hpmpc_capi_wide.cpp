@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <algorithm>
 #include <cstring>
 #include <vector>
@@ -42,6 +43,7 @@ struct WLayout {
     long long nB = 0, nR = 0, nL = 0, nU = 0, nP = 0, nD = 0, nI = 0;
     int lds = 0, offW = 0, offX = 0, offV = 0, ldW = 0, ldX = 0;
     bool any_ng = false;
+    bool fits = true;  // hk_wide_sv limits: nu+nx+1 <= 128 (two rows per lane), nx <= 64 (MFMA tiles per wave)
 };
 
 WLayout make_layout(int N, const int* nx, const int* nu, const int* nb, const int* ng) {
@@ -82,6 +84,7 @@ WLayout make_layout(int N, const int* nx, const int* nu, const int* nb, const in
         nzM = std::max(nzM, nux + 1);
         nxM = std::max(nxM, std::max(s.nx1, s.nx));  // X also receives stage k's own Lxx
     }
+    L.fits = nzM <= 128 && nxM <= 64;
     L.ldW = nzM;
     L.ldX = nxM + 1;
     L.offW = Mmax + nzM;  // the forward stages L_k with its 1/diag tail into M
@@ -180,8 +183,9 @@ extern "C" void hk_wide_sv_entry(int N, int* nx, int* nu, int* nb, int** idxb, i
         hk_set_error(HPMPC_MI355X_EUNSUPPORTED, "wide stages (nu+nx > 16) with general constraints");
         return;
     }
-    if (L.lds > LDS_MAX_DOUBLES) {
-        hk_set_error(HPMPC_MI355X_EUNSUPPORTED, "wide stage beyond the 64 KiB LDS tile budget");
+    if (L.lds > LDS_MAX_DOUBLES || !L.fits) {
+        hk_set_error(HPMPC_MI355X_EUNSUPPORTED, "wide stage beyond the kernel's tile limits (64 KiB LDS, "
+                                                "nu+nx < 128, nx <= 64)");
         return;
     }
     Carve c;
@@ -781,8 +785,9 @@ extern "C" int hpmpc_mi355x_pcond_ric_sv_batch(const hpmpc_mi355x_pcond_plan* q,
     if (!q) return HPMPC_MI355X_EUNSUPPORTED;
     hk_set_error(0, nullptr);
     const WLayout& C = q->P.cond;
-    if (C.any_ng) {
-        hk_set_error(HPMPC_MI355X_EUNSUPPORTED, "condensed Riccati with general constraints (state boxes)");
+    if (C.any_ng || !C.fits) {
+        hk_set_error(HPMPC_MI355X_EUNSUPPORTED, "condensed Riccati with general constraints (state boxes) or "
+                                                "beyond the wide-stage tile limits");
         return HPMPC_MI355X_EUNSUPPORTED;
     }
     WideArgs a;
@@ -807,6 +812,7 @@ extern "C" int hpmpc_mi355x_pcond_ric_sv_batch(const hpmpc_mi355x_pcond_plan* q,
     a.offV = C.offV;
     a.ldW = C.ldW;
     a.ldX = C.ldX;
+    if (const char* e = getenv("HK_WIDE_SKIP")) a.skip = atoi(e);  // profiling only
     return launch(0, &a, count, C.lds, (hipStream_t)stream, "hk_wide_sv") ? 0 : HPMPC_MI355X_EHIP;
 }
 
