@@ -105,6 +105,44 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
+// C (m x n) = A (m x K) B (K x n) on v_mfma_f64_16x16x4: wave w takes output tiles w, w+4, ..; a(i, k) / b(k, j)
+// read the operands (0 outside), out(i, j, v) stores a result after a workgroup barrier, so C may overwrite
+// an operand.  All threads of the workgroup must call it.  At most 4 * GM_TILES output tiles.
+constexpr int GM_TILES = 8;
+template <class FA, class FB, class FO>
+__device__ __forceinline__ void mfma_gemm(int m, int n, int K, FA a, FB b, FO out) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, c16 = lane & 15, g4 = lane >> 4;
+    const int nI = (m + 15) >> 4, nT = nI * ((n + 15) >> 4), nK = (K + 3) >> 2;
+    hk::d4 acc[GM_TILES];
+#pragma unroll
+    for (int u = 0; u < GM_TILES; u++) {
+        acc[u] = hk::d4{0.0, 0.0, 0.0, 0.0};
+        const int t = wv + 4 * u;
+        if (t < nT) {
+            const int ra = 16 * (t % nI) + c16, cb = 16 * (t / nI) + c16;
+            for (int kc = 0; kc < nK; kc++) {
+                const int kk = 4 * kc + g4;
+                const double av = (ra < m && kk < K) ? a(ra, kk) : 0.0;
+                const double bv = (cb < n && kk < K) ? b(kk, cb) : 0.0;
+                acc[u] = hk::mfma(av, bv, acc[u]);
+            }
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < GM_TILES; u++) {
+        const int t = wv + 4 * u;
+        if (t < nT) {
+            const int col = 16 * (t / nI) + c16;
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int row = 16 * (t % nI) + g4 + 4 * r;
+                if (row < m && col < n) out(row, col, acc[u][r]);
+            }
+        }
+    }
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------------------------------------
@@ -409,8 +447,8 @@ __global__ __launch_bounds__(WT) void hk_pcond(PcArgs a) {
         return o;
     };
 
-    // ---- d_cond_BAbt: Gamma_{j-1} stays in LDS (GA); Gamma_j is accumulated in registers (<= PC_GCH
-    // outputs per lane, checked by the host), then overwrites GA and streams to HBM ----
+    // ---- d_cond_BAbt: Gamma_{j-1} stays in LDS (GA); Gamma_j = [B_j; Gamma_{j-1} A_j] comes from MFMA tiles
+    // held in registers, then overwrites GA and streams to HBM ----
     double* GA = sm + a.offGA;
     {
         const WideStage s = st[0];
@@ -419,40 +457,29 @@ __global__ __launch_bounds__(WT) void hk_pcond(PcArgs a) {
         bar();
         for (int e = tid; e < r0 * s.nx1; e += WT) G[e] = GA[e];
     }
-    for (int j = 1; j < T; j++) {
+    for (int j = 1; j < ((a.skip & 1) ? 1 : T); j++) {
         const WideStage s = st[j];
         const int nuj = s.nu, nxj = s.nx, nx1 = s.nx1, nzj = nuj + nxj + 1;
         const int rp = rows(j - 1), rj = rp + nuj, n = rj * nx1;
         double* Gj = G + goff(j);
         load_dense<8>(Bt, ldB, BAbt + s.oB, s.sdB, nzj, nx1);
         bar();
-        double val[PC_GCH];
-#pragma unroll
-        for (int u = 0; u < PC_GCH; u++) {
-            const int e = tid + u * WT, i = e % rj, c = e / rj;
-            double v = 0.0;
-            if (e < n) {
-                if (i < nuj) {
-                    v = Bt[i + c * ldB];
-                } else {
-                    const int ip = i - nuj;
-                    double acc = 0.0;
-                    for (int l = 0; l < nxj; l++) acc += GA[ip + l * rp] * Bt[nuj + l + c * ldB];
-                    v = acc;
-                    if (i == rj - 1) v += Bt[nuj + nxj + c * ldB];
-                }
-            }
-            val[u] = v;
+        // rows nuj.. : Gamma_{j-1} A_j (+ b_j on the last row) on MFMA; rows ..nuj: B_j.  The results overwrite
+        // GA (leading dimension rp -> rj) after mfma_gemm's barrier, when every operand read is done.
+        mfma_gemm(
+            rp, nx1, nxj, [&](int i, int l) { return GA[i + l * rp]; },
+            [&](int l, int c) { return Bt[nuj + l + c * ldB]; },
+            [&](int i, int c, double v) {
+                if (i == rp - 1) v += Bt[nuj + nxj + c * ldB];
+                GA[nuj + i + c * rj] = v;
+                Gj[nuj + i + c * rj] = v;
+            });
+        for (int e = tid; e < nuj * nx1; e += WT) {
+            const int i = e % nuj, c = e / nuj;
+            GA[i + c * rj] = Bt[i + c * ldB];
+            Gj[i + c * rj] = Bt[i + c * ldB];
         }
-        bar();
-#pragma unroll
-        for (int u = 0; u < PC_GCH; u++) {
-            const int e = tid + u * WT;
-            if (e < n) {
-                GA[e] = val[u];
-                Gj[e] = val[u];
-            }
-        }
+        (void)n;
         bar();
     }
     {
@@ -488,7 +515,7 @@ __global__ __launch_bounds__(WT) void hk_pcond(PcArgs a) {
             load_dense<8>(Pl, ldP, RSQ + s.oR, s.sdR, s.nu + s.nx + 1, s.nu + s.nx);
         }
         bar();
-        for (int sI = T - 1;; sI--) {
+        for (int sI = (a.skip & 2) ? 0 : T - 1;; sI--) {
             const WideStage s = st[sI];
             const int nus = s.nu, nxs = s.nx, nux = nus + nxs, os = uoff(sI);
             if (sI == 0) {
@@ -506,7 +533,7 @@ __global__ __launch_bounds__(WT) void hk_pcond(PcArgs a) {
                 for (int i = j + (tid & 63); i <= nxs; i += 64) X[i + j * ldX] = Pl[nus + i + (nus + j) * ldP];
             bar();
             // M: Gamma_{s-1} times the x_s x u_s block of pL; m: + the r row on the gradient row
-            for (int e = tid; e < r0 * nus; e += WT) {
+            for (int e = tid; e < ((a.skip & 8) ? 0 : r0 * nus); e += WT) {
                 const int i = e % r0, c = e / r0;
                 double acc = 0.0;
                 for (int l = 0; l < nxs; l++) acc += GA[i + l * r0] * Pl[nus + l + c * ldP];
@@ -515,7 +542,7 @@ __global__ __launch_bounds__(WT) void hk_pcond(PcArgs a) {
             }
             // Lx = chol_aug(X) inside wave 0 (row i on lane i, nxs + 1 <= 64 rows): 16-column panels factored in
             // registers (pivot values broadcast by readlane), each followed by its update of the later columns
-            if (tid < 64) {
+            if (tid < 64 && !(a.skip & 4)) {
                 const int i = tid;
                 for (int p0 = 0; p0 < nxs; p0 += 16) {
                     const int pw = nxs - p0 < 16 ? nxs - p0 : 16;
@@ -556,20 +583,23 @@ __global__ __launch_bounds__(WT) void hk_pcond(PcArgs a) {
             load_dense<8>(Bt, ldB, BAbt + sp.oB, sp.sdB, nzp, nxs);
             load_dense<8>(Pl, ldP, RSQ + sp.oR, sp.sdR, nzp, nuxp);
             bar();
-            for (int i = tid; i < nzp; i += WT)
-                for (int c = 0; c < nxs; c++) {
-                    double acc = 0.0;
-                    for (int l = c; l < nxs; l++) acc += Bt[i + l * ldB] * X[l + c * ldX];
-                    if (i == nuxp) acc += X[nxs + c * ldX];
-                    Bt[i + c * ldB] = acc;
-                }
-            bar();
-            for (int j = tid >> 6; j < nuxp; j += WT / 64)
-                for (int i = j + (tid & 63); i <= nuxp; i += 64) {
-                    double acc = 0.0;
-                    for (int l = 0; l < nxs; l++) acc += Bt[i + l * ldB] * Bt[j + l * ldB];
-                    Pl[i + j * ldP] += acc;
-                }
+            if (!(a.skip & 16)) {
+                // W = BAbt_{s-1} Lx (+ l on the last row) in place over Bt, then pL += W W' (lower), both on MFMA
+                mfma_gemm(
+                    nzp, nxs, nxs, [&](int i, int l) { return Bt[i + l * ldB]; },
+                    [&](int l, int c) { return l >= c ? X[l + c * ldX] : 0.0; },
+                    [&](int i, int c, double v) {
+                        if (i == nuxp) v += X[nxs + c * ldX];
+                        Bt[i + c * ldB] = v;
+                    });
+                bar();
+                mfma_gemm(
+                    nzp, nuxp, nxs, [&](int i, int l) { return Bt[i + l * ldB]; },
+                    [&](int l, int j) { return Bt[j + l * ldB]; },
+                    [&](int i, int j, double v) {
+                        if (i >= j) Pl[i + j * ldP] += v;
+                    });
+            }
             bar();
         }
     }

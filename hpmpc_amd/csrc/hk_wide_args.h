@@ -62,6 +62,7 @@ struct PcArgs {
     int sdRN, nzN;           // its lib4 panel stride and rows
     int offP, offX, offW, offB, ldP, ldX, ldW, ldB;  // dynamic LDS carve
     int offGA, offGB;                                // Gamma_{j-1} / Gamma_j tiles (and stage scratch)
+    int skip;  // profiling only (HK_PCOND_SKIP): bit 0 Gamma, 1 RSQ phase, 2 its Cholesky, 3 M product, 4 W/syrk
 };
 
 // Expansion (d_part_expand_solution): one workgroup per (block, problem).

@@ -776,6 +776,7 @@ extern "C" int hpmpc_mi355x_pcond_batch(const hpmpc_mi355x_pcond_plan* q, int np
     a.DCt2 = DCt2;
     a.d2 = d2;
     a.idxb2 = q->d_idxb2;
+    if (const char* e = getenv("HK_PCOND_SKIP")) a.skip = atoi(e);  // profiling only
     return launch(1, &a, count, q->P.pc_lds, (hipStream_t)stream, "hk_pcond") ? 0 : HPMPC_MI355X_EHIP;
 }
 
