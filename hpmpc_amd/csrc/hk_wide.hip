@@ -19,8 +19,7 @@ namespace {
 using hk::gld;
 
 constexpr int WT = 256;  // threads per workgroup
-constexpr int PC_GCH = 12;
-constexpr int WS_TILES = 8;  // W = BAbt Lxx output tiles per wave (nz <= 128, nx <= 64: <= 32 tiles, host-checked)  // Gamma outputs per lane in the condensing (rows x nx <= 3072, host-checked)
+constexpr int WS_TILES = 8;  // W = BAbt Lxx output tiles per wave (nz <= 128, nx <= 64: <= 32 tiles, host-checked)
 constexpr int BS = 4;
 
 __device__ __forceinline__ int p4i(int i, int j, int sd) { return (i / BS) * BS * sd + i % BS + BS * j; }
@@ -181,6 +180,13 @@ __global__ __launch_bounds__(WT) void hk_wide_sv(WideArgs a) {
         if (k < a.N && !(a.skip & 4)) {
             load_dense<8>(W, ldW, BAbt + s.oB, s.sdB, nz, nx1);
             bar();
+            if (a.trf) {  // trf factorises without the augmented row: the b row and the gradient row read as 0
+                for (int j = tid; j < nux + nx1; j += WT) {
+                    if (j < nx1) W[nux + j * ldW] = 0.0;
+                    if (j < nux) M[poff(j, nz) + nux - j] = 0.0;
+                }
+                bar();
+            }
             // W = BAbt_k Lxx_{k+1} (dtrmm_nt_u) on MFMA: 16x16 output tiles, K over the nx1 columns of BAbt; the
             // tiles are kept in registers and written back over BAbt after a barrier
             {
@@ -246,6 +252,9 @@ __global__ __launch_bounds__(WT) void hk_wide_sv(WideArgs a) {
                     }
                 }
             }
+        } else if (a.trf) {
+            bar();
+            for (int j = tid; j < nux; j += WT) M[poff(j, nz) + nux - j] = 0.0;
         }
         bar();
         // Cholesky with the augmented row, blocked by 16-column panels: wave 0 factors the panel (row i on
@@ -346,7 +355,7 @@ __global__ __launch_bounds__(WT) void hk_wide_sv(WideArgs a) {
         const int nz0 = s0.nu + s0.nx + 1;
         load_flat<16>(M, F + s0.oL, poff(nz0 - 1, nz0) + nz0 - 1);
     }
-    for (int k = 0; k < ((a.skip & 1) ? 0 : a.N); k++) {
+    for (int k = 0; k < ((a.skip & 1) || a.trf ? 0 : a.N); k++) {
         const WideStage s = a.st[k];
         const int nux = s.nu + s.nx, nz = nux + 1, nx1 = s.nx1, nu1 = s.nu1;
         const int ns = k == 0 ? nux : s.nu;
@@ -827,6 +836,151 @@ __global__ __launch_bounds__(WT) void hk_pexpand(PxArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// d_back_ric_rec_trs_tv_res on wide stages (d_back_ric_rec.c:564-791, restated in oracle/hpmpc_oracle.c):
+// backward, per stage k = N..0: g_k = q_k + qx at idxb; v_k = g_k + BAbt_k (Pb_k + v_{k+1,x}) (k < N), with
+// Pb_k = Lxx_{k+1}(Lxx_{k+1}' b_k); then L_k's n-form solve on the first nu_k columns (all of stage 0) with the
+// rectangular update of the later rows.  Forward as the sv forward, pi_k = Lxx(Lxx' x_{k+1}) + v_{k+1,x}.
+// The processed v_k are parked in ux (the forward overwrites them).  No general constraints (host-checked).
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(WT) void hk_wide_trs(WideArgs a) {
+    extern __shared__ double sm[];
+    const int p = blockIdx.x + a.p0;
+    if (p >= a.nprob) return;
+    const int tid = threadIdx.x, lane = tid & 63;
+    double* M = sm;
+    double* W = sm + a.offW;
+    double* X = sm + a.offX;  // w = Pb + v_{k+1,x} (backward) / pi scratch (forward)
+    double* v = sm + a.offV;
+    const int ldW = a.ldW;
+    const double* BAbt = a.BAbt + (long)p * a.sB;
+    const double* F = a.ws + (long)p * a.sW;
+    double* ux = a.ux + (long)p * a.sU;
+    double* pi = a.pi + (long)p * a.sP;
+    double* Pb = a.Pb + (long)p * a.sP;
+    const double* hb = a.hb + (long)p * a.sP;
+    const double* hq = a.hq + (long)p * a.sU;
+    const double* qx = a.qx + (long)p * a.sC;
+    for (int k = a.N; k >= 0; k--) {
+        const WideStage s = a.st[k];
+        const int nux = s.nu + s.nx, nz = nux + 1, nx1 = s.nx1;
+        const int ns = k == 0 ? nux : s.nu;
+        load_flat<16>(M, F + s.oL, poff(nux, nz) + nux);
+        if (k < a.N) load_dense<8>(W, ldW, BAbt + s.oB, s.sdB, nux, nx1);
+        for (int i = tid; i < nux; i += WT) v[i] = hq[s.oU + i];
+        bar();
+        if (tid == 0)
+            for (int l = 0; l < s.nb; l++) v[a.idxb[s.oI + l]] += qx[s.oD + l];
+        bar();
+        if (k < a.N) {
+            double c = 0.0;
+            if (tid < nux)
+                for (int j = 0; j < nx1; j++) c += W[tid + j * ldW] * X[j];
+            bar();
+            if (tid < nux) v[tid] += c;
+            bar();
+            // n-form solve on the first ns columns with the rectangular update (column-oriented, one wave)
+            const double* dL = M + poff(nux, nz);
+            if (tid < 64) {
+                for (int j = 0; j < ns; j++) {
+                    const double y = v[j] * dL[j];
+                    const int cj = poff(j, nz) - j;
+                    for (int i = j + 1 + lane; i < nux; i += 64) v[i] -= M[cj + i] * y;
+                    if (lane == 0) v[j] = y;
+                    wave_sync();
+                }
+            }
+            bar();
+        }
+        for (int i = tid; i < nux; i += WT) ux[s.oU + i] = v[i];
+        if (k > 0) {  // w for stage k-1: Pb_{k-1} = Lxx_k (Lxx_k' b_{k-1}), plus v_{k,x}
+            const WideStage sp = a.st[k - 1];
+            const int nu = s.nu, nx = s.nx;
+            double t = 0.0;
+            if (tid < nx) {
+                const int cj = poff(nu + tid, nz) - (nu + tid);
+                for (int i = tid; i < nx; i++) t += M[cj + nu + i] * hb[sp.oP + i];
+            }
+            bar();
+            if (tid < nx) W[tid] = t;  // W is free: scratch
+            bar();
+            if (tid < nx) {
+                double acc = 0.0;
+                for (int j = 0; j <= tid; j++) acc += M[poff(nu + j, nz) + tid - j] * W[j];
+                if (a.compute_Pb) Pb[sp.oP + tid] = acc;
+                X[tid] = (a.compute_Pb ? acc : Pb[sp.oP + tid]) + v[nu + tid];
+            }
+        }
+        bar();
+    }
+    // forward
+    {
+        const WideStage s0 = a.st[0];
+        const int nz0 = s0.nu + s0.nx + 1;
+        load_flat<16>(M, F + s0.oL, poff(nz0 - 1, nz0) + nz0 - 1);
+        load_flat<4>(v, ux + s0.oU, nz0 - 1);
+        bar();
+    }
+    for (int k = 0; k < a.N; k++) {
+        const WideStage s = a.st[k], s1 = a.st[k + 1];
+        const int nux = s.nu + s.nx, nz = nux + 1, nx1 = s.nx1, nu1 = s.nu1;
+        const int ns = k == 0 ? nux : s.nu;
+        const double* dL = M + poff(nux, nz);
+        load_dense<8>(W, ldW, BAbt + s.oB, s.sdB, nux, nx1);
+        double pk = 0.0;
+        if (tid < nx1) pk = ux[s1.oU + nu1 + tid];  // v_{k+1,x} of the backward, before x_{k+1} replaces it
+        for (int j = tid; j < ns; j += WT) v[j] = -v[j];
+        bar();
+        double r = 0.0;
+        if (tid < ns) {  // - L[ns:nux, 0:ns]' x_k
+            const int cj = poff(tid, nz) - tid;
+            r = v[tid];
+            for (int m = ns; m < nux; m++) r -= M[cj + m] * v[m];
+        }
+        bar();
+        if (tid < ns) v[tid] = r;
+        bar();
+        if (tid < 64) {
+            for (int i = ns - 1; i >= 0; i--) {
+                const double y = v[i] * dL[i];
+                for (int j = tid; j < i; j += 64) v[j] -= M[poff(j, nz) + i - j] * y;
+                if (tid == 0) v[i] = y;
+                wave_sync();
+            }
+        }
+        bar();
+        for (int j = tid; j < nux; j += WT) ux[s.oU + j] = v[j];
+        double xn = 0.0;
+        if (tid < nx1) {
+            xn = hb[s.oP + tid];
+            for (int i = 0; i < nux; i++) xn += W[i + tid * ldW] * v[i];
+        }
+        bar();
+        const int nux1 = nu1 + nx1, nz1 = nux1 + 1;
+        load_flat<16>(M, F + s1.oL, poff(nux1, nz1) + nux1);
+        // v <- stage k+1: the backward's processed u part, and the actual state x_{k+1}
+        for (int j = tid; j < nu1; j += WT) v[j] = ux[s1.oU + j];
+        if (tid < nx1) v[nu1 + tid] = xn;
+        bar();
+        if (a.compute_pi) {
+            if (tid < nx1) {
+                const int cj = poff(nu1 + tid, nz1) - (nu1 + tid);
+                double tj = 0.0;
+                for (int i = tid; i < nx1; i++) tj += M[cj + nu1 + i] * v[nu1 + i];
+                X[tid] = tj;
+            }
+            bar();
+            if (tid < nx1) {
+                double acc = 0.0;
+                for (int j = 0; j <= tid; j++) acc += M[poff(nu1 + j, nz1) + tid - j] * X[j];
+                pi[s.oP + tid] = acc + pk;
+            }
+            bar();
+        }
+    }
+    if (tid < a.st[a.N].nx) ux[a.st[a.N].oU + tid] = v[tid];
+}
+
+// ------------------------------------------------------------------------------------------------
 // Host launchers
 // ------------------------------------------------------------------------------------------------
 extern "C" int hk_wide_launch(int which, const void* args, int count, int lds_doubles, hipStream_t stream) {
@@ -846,6 +1000,11 @@ extern "C" int hk_wide_launch(int which, const void* args, int count, int lds_do
         case 2: {
             const PxArgs& a = *static_cast<const PxArgs*>(args);
             hipLaunchKernelGGL(hk_pexpand, dim3(a.N2, count), dim3(WT), lds, stream, a);
+            break;
+        }
+        case 3: {
+            const WideArgs& a = *static_cast<const WideArgs*>(args);
+            hipLaunchKernelGGL(hk_wide_trs, dim3(count), dim3(WT), lds, stream, a);
             break;
         }
         default:

@@ -32,6 +32,11 @@ struct WideArgs {
     int offW, offX, offV;  // dynamic LDS carve (doubles): M packed | W | X | v
     int ldW, ldX;
     int skip;  // profiling only (HK_WIDE_SKIP): bit 0 forward, bit 1 Cholesky, bit 2 trmm/syrk -- results invalid
+    int trf;   // d_back_ric_rec_trf_tv_res: no augmented row (stored as zeros), no forward
+    // d_back_ric_rec_trs_tv_res (hk_wide_trs): b (offsets oP), q (offsets oU), qx (offsets oD, stride sC), idxb (oI)
+    const double *hb, *hq, *qx;
+    const int* idxb;
+    long long sC;
 };
 
 // Partial condensing (d_part_cond): one workgroup per (block ii, problem p).

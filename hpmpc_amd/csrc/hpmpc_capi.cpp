@@ -30,6 +30,11 @@ extern "C" void hk_wide_sv_entry(int N, int* nx, int* nu, int* nb, int** idxb, i
                                  double** b, int update_q, double** hpQ, double** q, double** bd, double** Qx,
                                  double** qx, double** hux, int compute_pi, double** hpi, int compute_Pb, double** hPb,
                                  double* memory);
+extern "C" void hk_wide_trf_entry(int N, int* nx, int* nu, int* nb, int** idxb, int* ng, double** hpBAbt,
+                                  double** hpQ, double** Qx, double** bd, double* memory);
+extern "C" void hk_wide_trs_entry(int N, int* nx, int* nu, int* nb, int** idxb, int* ng, double** hpBAbt,
+                                  double** hb, double** hq, double** qx, double** hux, int compute_pi, double** hpi,
+                                  int compute_Pb, double** hPb, double* memory);
 
 namespace {
 
@@ -823,6 +828,13 @@ extern "C" void d_back_ric_rec_trf_tv_res(int N, int* nx, int* nu, int* nb, int*
                                           double* work) {
     (void)work;
     g_err = 0;
+    {
+        const char* why = nullptr;
+        if (!plan_supported(N, nx, nu, nb, idxb, ng, &why)) {  // stages beyond the 16-wide tile
+            hk_wide_trf_entry(N, nx, nu, nb, idxb, ng, hpBAbt, hpQ, Qx, bd, memory);
+            return;
+        }
+    }
     hpmpc_mi355x_plan* P = g_ctx.get_plan(N, nx, nu, nb, idxb, ng);
     if (!P) return;
     Arena A = arena(P, 1);
@@ -854,6 +866,14 @@ extern "C" void d_back_ric_rec_trs_tv_res(int N, int* nx, int* nu, int* nb, int*
                                           double* work) {
     (void)work;
     g_err = 0;
+    {
+        const char* why = nullptr;
+        if (!plan_supported(N, nx, nu, nb, idxb, ng, &why)) {  // stages beyond the 16-wide tile
+            hk_wide_trs_entry(N, nx, nu, nb, idxb, ng, hpBAbt, hb, hq, qx, hux, compute_pi, hpi, compute_Pb,
+                              hPb, memory);
+            return;
+        }
+    }
     hpmpc_mi355x_plan* P = g_ctx.get_plan(N, nx, nu, nb, idxb, ng);
     if (!P) return;
     Arena A = arena(P, 1);

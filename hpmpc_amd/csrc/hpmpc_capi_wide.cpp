@@ -246,6 +246,130 @@ extern "C" void hk_wide_sv_entry(int N, int* nx, int* nu, int* nb, int** idxb, i
     memcpy(memory, H + oF, 8 * L.nL);
 }
 
+namespace {
+bool wide_check(const WLayout& L) {
+    if (L.any_ng) {
+        hk_set_error(HPMPC_MI355X_EUNSUPPORTED, "wide stages (nu+nx > 16) with general constraints");
+        return false;
+    }
+    if (L.lds > LDS_MAX_DOUBLES || !L.fits) {
+        hk_set_error(HPMPC_MI355X_EUNSUPPORTED, "wide stage beyond the kernel's tile limits (64 KiB LDS, "
+                                                "nu+nx < 128, nx <= 64)");
+        return false;
+    }
+    return true;
+}
+void wide_args(const WLayout& L, WideArgs& a) {
+    memset(&a, 0, sizeof a);
+    a.N = L.N;
+    a.nprob = 1;
+    a.offW = L.offW;
+    a.offX = L.offX;
+    a.offV = L.offV;
+    a.ldW = L.ldW;
+    a.ldX = L.ldX;
+}
+}  // namespace
+
+// d_back_ric_rec_trf_tv_res on wide stages: hk_wide_sv in factor-only mode (no augmented row, no forward).
+extern "C" void hk_wide_trf_entry(int N, int* nx, int* nu, int* nb, int** idxb, int* ng, double** hpBAbt,
+                                  double** hpQ, double** Qx, double** bd, double* memory) {
+    hk_set_error(0, nullptr);
+    WLayout L = make_layout(N, nx, nu, nb, ng);
+    if (!wide_check(L)) return;
+    Carve c;
+    const size_t oSt = c.take(sizeof(WideStage) * (N + 1)), oB = c.take(8 * L.nB), oR = c.take(8 * L.nR),
+                 oF = c.take(8 * L.nL), oU = c.take(8 * L.nU), oP = c.take(8 * L.nP);
+    if (!g_w.ensure(c.o)) return;
+    char* H = g_w.host;
+    memcpy(H + oSt, L.st.data(), sizeof(WideStage) * (N + 1));
+    double* HB = reinterpret_cast<double*>(H + oB);
+    double* HR = reinterpret_cast<double*>(H + oR);
+    for (int k = N; k >= 0; k--) {  // the reference's side effect: box diagonal = bd + Qx (d_back_ric_rec.c:468, :520)
+        const WideStage& s = L.st[k];
+        const int nux = s.nu + s.nx;
+        for (int l = 0; l < nb[k]; l++) {
+            const int ii = idxb[k][l];
+            P4(hpQ[k], s.sdR, ii, ii) = bd[k][l] + Qx[k][l];
+        }
+        memcpy(HR + s.oR, hpQ[k], (size_t)rup(nux + 1, BS) * s.sdR * sizeof(double));
+        if (k < N) memcpy(HB + s.oB, hpBAbt[k], (size_t)rup(nux + 1, BS) * s.sdB * sizeof(double));
+    }
+    char* D = g_w.dev;
+    WideArgs a;
+    wide_args(L, a);
+    a.trf = 1;
+    a.st = reinterpret_cast<const WideStage*>(D + oSt);
+    a.BAbt = reinterpret_cast<const double*>(D + oB);
+    a.RSQ = reinterpret_cast<const double*>(D + oR);
+    a.ws = reinterpret_cast<double*>(D + oF);
+    a.ux = reinterpret_cast<double*>(D + oU);
+    a.pi = a.Pb = reinterpret_cast<double*>(D + oP);
+    if (!g_w.up(c.o) || !launch(0, &a, 1, L.lds, g_w.stream, "hk_wide_sv(trf)") || !g_w.down(c.o)) return;
+    memcpy(memory, H + oF, 8 * L.nL);
+}
+
+// d_back_ric_rec_trs_tv_res on wide stages (hk_wide_trs) over the factor hk_wide_trf_entry left in memory.
+extern "C" void hk_wide_trs_entry(int N, int* nx, int* nu, int* nb, int** idxb, int* ng, double** hpBAbt,
+                                  double** hb, double** hq, double** qx, double** hux, int compute_pi, double** hpi,
+                                  int compute_Pb, double** hPb, double* memory) {
+    hk_set_error(0, nullptr);
+    WLayout L = make_layout(N, nx, nu, nb, ng);
+    if (!wide_check(L)) return;
+    Carve c;
+    const size_t oSt = c.take(sizeof(WideStage) * (N + 1)), oB = c.take(8 * L.nB), oF = c.take(8 * L.nL),
+                 oU = c.take(8 * L.nU), oP = c.take(8 * L.nP), oPb = c.take(8 * L.nP), ob = c.take(8 * L.nP),
+                 oq = c.take(8 * L.nU), oqx = c.take(8 * L.nD), oI = c.take(4 * L.nI);
+    if (!g_w.ensure(c.o)) return;
+    char* H = g_w.host;
+    memcpy(H + oSt, L.st.data(), sizeof(WideStage) * (N + 1));
+    memcpy(H + oF, memory, 8 * L.nL);
+    double* HB = reinterpret_cast<double*>(H + oB);
+    double* HPb = reinterpret_cast<double*>(H + oPb);
+    double* Hb = reinterpret_cast<double*>(H + ob);
+    double* Hq = reinterpret_cast<double*>(H + oq);
+    double* Hqx = reinterpret_cast<double*>(H + oqx);
+    int* HI = reinterpret_cast<int*>(H + oI);
+    for (int k = 0; k <= N; k++) {
+        const WideStage& s = L.st[k];
+        const int nux = s.nu + s.nx;
+        memcpy(Hq + s.oU, hq[k], nux * sizeof(double));
+        if (nb[k] > 0) {
+            memcpy(Hqx + s.oD, qx[k], nb[k] * sizeof(double));
+            memcpy(HI + s.oI, idxb[k], nb[k] * sizeof(int));
+        }
+        if (k < N) {
+            memcpy(HB + s.oB, hpBAbt[k], (size_t)rup(nux + 1, BS) * s.sdB * sizeof(double));
+            memcpy(Hb + s.oP, hb[k], s.nx1 * sizeof(double));
+            if (!compute_Pb) memcpy(HPb + s.oP, hPb[k], s.nx1 * sizeof(double));
+        }
+    }
+    char* D = g_w.dev;
+    WideArgs a;
+    wide_args(L, a);
+    a.st = reinterpret_cast<const WideStage*>(D + oSt);
+    a.BAbt = reinterpret_cast<const double*>(D + oB);
+    a.ws = reinterpret_cast<double*>(D + oF);
+    a.ux = reinterpret_cast<double*>(D + oU);
+    a.pi = reinterpret_cast<double*>(D + oP);
+    a.Pb = reinterpret_cast<double*>(D + oPb);
+    a.hb = reinterpret_cast<const double*>(D + ob);
+    a.hq = reinterpret_cast<const double*>(D + oq);
+    a.qx = reinterpret_cast<const double*>(D + oqx);
+    a.idxb = reinterpret_cast<const int*>(D + oI);
+    a.compute_pi = compute_pi;
+    a.compute_Pb = compute_Pb;
+    if (!g_w.up(c.o) || !launch(3, &a, 1, L.lds, g_w.stream, "hk_wide_trs") || !g_w.down(c.o)) return;
+    const double* HU = reinterpret_cast<const double*>(H + oU);
+    const double* HP = reinterpret_cast<const double*>(H + oP);
+    for (int k = 0; k <= N; k++) {
+        const WideStage& s = L.st[k];
+        memcpy(hux[k], HU + s.oU, (s.nu + s.nx) * sizeof(double));
+        if (k < N && compute_pi) memcpy(hpi[k], HP + s.oP, s.nx1 * sizeof(double));
+        if (k < N && compute_Pb) memcpy(hPb[k], HPb + s.oP, s.nx1 * sizeof(double));
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // Partial condensing: host bookkeeping shared by the single-problem and the batched entry points.
 // ------------------------------------------------------------------------------------------------

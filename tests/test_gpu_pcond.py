@@ -54,6 +54,42 @@ def test_wide_sv_vs_oracle(product, oracle, case):
             np.testing.assert_array_equal(q1.BAbt[k], q2.BAbt[k])
 
 
+@pytest.mark.parametrize("case", WIDE, ids=[f"N{c[0]}_{i}" for i, c in enumerate(WIDE)])
+def test_wide_trf_trs_vs_oracle(product, oracle, case):
+    """d_back_ric_rec_trf_tv_res once, then d_back_ric_rec_trs_tv_res for several right-hand sides, on wide
+    stages; the last trial passes Pb in (compute_Pb = 0)."""
+    N, nx, nu, nb = case
+    qp = random_qp(N, nx, nu, nb, seed=73 + N)
+    rng = np.random.default_rng(7 * N)
+    bd = [rng.random(max(int(n), 1)) + 0.5 for n in qp.nb]
+    Qx = [rng.random(max(int(n), 1)) for n in qp.nb]
+    res = []
+    for api in (product, oracle):
+        q0 = qp.copy()
+        mem = api.ric_trf(q0, bd=bd, Qx=Qx)
+        outs = []
+        for trial in range(3):
+            r2 = np.random.default_rng(200 + trial)
+            b = [r2.standard_normal(int(qp.nx[k + 1]) + 8) for k in range(N)]
+            q = [r2.standard_normal(qp.nux(k) + 8) for k in range(N + 1)]
+            qx = [r2.standard_normal(max(int(n), 1)) for n in qp.nb]
+            kw = dict(compute_pi=1, compute_Pb=1)
+            if trial == 2:
+                kw = dict(compute_pi=1, compute_Pb=0,
+                          Pb=[r2.standard_normal(int(qp.nx[k + 1]) + 8) for k in range(N)])
+            outs.append(api.ric_trs(q0, mem, b=b, q=q, qx=qx, **kw))
+        res.append((outs, q0))
+    (o1, g1), (o2, g2) = res
+    for k in range(N + 1):
+        np.testing.assert_array_equal(g1.RSQrq[k], g2.RSQrq[k])
+    for (u1, p1, b1), (u2, p2, b2) in zip(o1, o2):
+        for k in range(N + 1):
+            assert _rel(u1[k][:qp.nux(k)], u2[k][:qp.nux(k)]) <= TOL_RIC, k
+            if k < N:
+                m = int(qp.nx[k + 1])
+                assert _rel(p1[k][:m], p2[k][:m]) <= TOL_RIC and _rel(b1[k][:m], b2[k][:m]) <= TOL_RIC, k
+
+
 PCOND = [
     # N, nx, nu, N2, boxes
     (40, 12, 6, 8, True),     # nu > 4: the reference c99 build is wrong here, the oracle is the checker
