@@ -183,6 +183,30 @@ class HpmpcAPI:
         return dict(ret=ret, kk=kk.value, stat=stat[: 5 * kk.value].copy(), ux=ux_, pi=pi, lam=lam, t=t,
                     work=work)
 
+    def ipm_soft(self, sq, *, k_max=50, mu0=100.0, mu_tol=1e-8, alpha_min=1e-8, warm_start=0, compute_mult=1,
+                 ux=None, work_extra=0):
+        """d_ip2_mpc_soft_tv (mpc_solvers/d_ip2_soft.c:83) on a SoftQP (hpmpc_amd/soft.py).  Returns dict."""
+        N = sq.N
+        a = (C.c_int(N), iv(sq.nx), iv(sq.nu), iv(sq.nb), iv(sq.ng), iv(sq.ns))
+        wsz = self.fn("d_ip2_mpc_soft_tv_work_space_size_bytes")(*a)
+        work = np.zeros(wsz // 8 + 16 + work_extra)
+        ux_, pi, lam, t = sq.alloc_solution()
+        if ux is not None:
+            for k in range(N + 1):
+                n = min(len(ux_[k]), len(ux[k]))
+                ux_[k][:n] = ux[k][:n]
+        stat = np.zeros(5 * k_max + 5)
+        kk = C.c_int(0)
+        dct = [np.zeros(8)] * (N + 1)
+        ret = self.fn("d_ip2_mpc_soft_tv")(
+            C.byref(kk), C.c_int(k_max), C.c_double(mu0), C.c_double(mu_tol), C.c_double(alpha_min),
+            C.c_int(warm_start), self._p(stat), C.c_int(N), iv(sq.nx), iv(sq.nu), iv(sq.nb), ipp(sq.idxb),
+            iv(sq.ng), iv(sq.ns), self._pp(sq.BAbt), self._pp(sq.RSQrq), self._pp(sq.Z), self._pp(sq.z),
+            self._pp(dct), self._pp(sq.d), self._pp(ux_), C.c_int(compute_mult), self._pp(pi), self._pp(lam),
+            self._pp(t), self._p(work))
+        self._sync()
+        return dict(ret=ret, kk=kk.value, stat=stat[: 5 * max(kk.value, 0)].copy(), ux=ux_, pi=pi, lam=lam, t=t)
+
     def prepare_ipm(self, qp: OCPQP, *, k_max=50, mu0=2.0, mu_tol=1e-12, alpha_min=1e-8):
         """Pre-marshalled d_ip2_res_mpc_hard_tv call: returns (call, kk) where call() runs one cold-start
         solve on private buffers and returns the status; kk.value holds the iteration count.  Used to

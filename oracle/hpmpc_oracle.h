@@ -86,6 +86,15 @@ void orc_d_part_expand_solution(int N, int *nx, int *nu, int *nb, int **hidxb, i
                                 double **hlam, double **ht, int N2, int *nx2, int *nu2, int *nb2, int **hidxb2,
                                 int *ng2, double **hux2, double **hpi2, double **hlam2, double **ht2, void *work);
 
+/* soft-constraint IPM (hpmpc_oracle_soft.c; mpc_solvers/d_ip2_soft.c:42-547) */
+int orc_soft_supported(int N, int *nx, int *nu, int *ng);
+int orc_d_ip2_mpc_soft_tv_work_space_size_bytes(int N, int *nx, int *nu, int *nb, int *ng, int *ns);
+int orc_d_ip2_mpc_soft_tv(int *kk, int k_max, double mu0, double mu_tol, double alpha_min, int warm_start,
+                          double *stat, int N, int *nx, int *nu, int *nb, int **idxb, int *ng, int *ns,
+                          double **pBAbt, double **pQ, double **Z, double **z, double **pDCt, double **d,
+                          double **ux, int compute_mult, double **pi, double **lam, double **t,
+                          double *double_work_memory);
+
 #ifdef __cplusplus
 }
 #endif

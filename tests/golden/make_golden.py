@@ -315,8 +315,42 @@ def iface(ref, out):
                          extra=extra))
 
 
+def soft(ref, out):
+    """Soft-constraint IPM d_ip2_mpc_soft_tv (mpc_solvers/d_ip2_soft.c:83): the reference driver's problem
+    (test_d_ip_soft.c: Q = 0, Z = 0, z = 100, mu0 = 100) at three sizes, stopped at mu_tol = 1e-5 -- below that its
+    end game is rounding-chaotic (the reference's own -mfma -ffp-contract=fast build stops at a different iterate,
+    DESIGN.md) -- plus an iteration cap, hard boxes at stage N (alpha collapses at iteration 3, through the
+    soft-gradient write the reference makes past qx_N into Zl / zl), a time-variant Q = I, Z = 1 case, only hard
+    boxes, and no constraints at all."""
+    from hpmpc_amd.soft import mass_spring_soft
+
+    cases = [("ms_N10_nx4_nu1", mass_spring_soft(10, 4, 1), dict(mu_tol=1e-5)),
+             ("ms_N10_nx8_nu3", mass_spring_soft(10, 8, 3), dict(mu_tol=1e-5)),
+             ("ms_N15_nx12_nu4", mass_spring_soft(15, 12, 4), dict(mu_tol=1e-5)),
+             ("kmax4_N15_nx12_nu4", mass_spring_soft(15, 12, 4), dict(k_max=4, mu_tol=1e-5)),
+             ("hardN_N12_nx8_nu2", mass_spring_soft(12, 8, 2, hard_last=2), dict(mu_tol=1e-5)),
+             ("hardN_N10_nx4_nu2", mass_spring_soft(10, 4, 2, hard_last=4), dict(mu_tol=1e-5)),
+             ("tv_N8_nx12_nu4", mass_spring_soft(8, 12, 4, time_variant=True, Zq=1.0, zl=10.0, Q_diag=1.0),
+              dict(mu_tol=1e-6)),
+             ("q1_N20_nx8_nu2", mass_spring_soft(20, 8, 2, Q_diag=1.0, Zq=0.5, zl=20.0), dict(mu_tol=1e-6)),
+             ("hardonly_N10_nx8_nu3", mass_spring_soft(10, 8, 3, soft=False, Q_diag=1.0), dict(mu_tol=1e-6)),
+             ("noconstr_N10_nx8_nu3", mass_spring_soft(10, 8, 3, soft=False, hard=False, Q_diag=1.0),
+              dict(mu_tol=1e-6))]
+    for name, sq, kw in cases:
+        args = dict(k_max=50, mu0=100.0, mu_tol=1e-8, alpha_min=1e-8)
+        args.update(kw)
+        r = ref.ipm_soft(sq.copy(), work_extra=1 << 16, **args)
+        outs = dict(ux=r["ux"], pi=r["pi"], lam=r["lam"], t=r["t"], stat=r["stat"], kk=r["kk"], ret=r["ret"])
+        out.append(save_case(f"soft_{name}", "soft", sq, args, outs,
+                             extra=dict(ns=[sq.ns.astype(np.float64)], Z=sq.Z, z=sq.z)))
+
+
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] == "iface":
+    if len(sys.argv) > 1 and sys.argv[1] == "soft":
+        o = []
+        soft(ref_api(), o)
+        print(f"wrote {len(o)} soft cases, {sum(os.path.getsize(p) for p in o) / 1e6:.2f} MB")
+    elif len(sys.argv) > 1 and sys.argv[1] == "iface":
         o = []
         iface(ref_api(), o)
         print(f"wrote {len(o)} iface cases, {sum(os.path.getsize(p) for p in o) / 1e6:.2f} MB")
