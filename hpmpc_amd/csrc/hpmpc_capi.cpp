@@ -13,6 +13,7 @@
 //     IPM iterate) so that trs and d_kkt_solve_new_rhs_res_mpc_hard_tv can re-use it.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -1174,4 +1175,224 @@ extern "C" void d_res_mpc_hard_tv(int N, int* nx, int* nu, int* nb, int** idxb, 
         if (nb[k] + ng[k] > 0) memcpy(hrd[k], rd + k * V32, cvec_len(P, k) * sizeof(double));
     }
     *mu = H[A.ints + 2];
+}
+
+// ================================================================================================
+// Soft-constraint IPM d_ip2_mpc_soft_tv (mpc_solvers/d_ip2_soft.c:42-547, include/mpc_solvers.h:69-70):
+// the constraint passes of hk_soft.hip around the tile Riccati kernels, one host round trip (the exit
+// flag) per iteration.  Limits (HPMPC_MI355X_EUNSUPPORTED, DESIGN.md soft constraints): ng = 0, nu[N] = 0,
+// round_up(nb + ns, 4) <= 16 per stage, b_k read inside BAbt_k with the reference's stride
+// (d_ip2_soft.c:172), and no soft-gradient write of the reference into a Zl its pass still reads.
+// ================================================================================================
+#include "hk_soft_args.h"
+
+extern "C" int hk_soft_launch(int which, const SoftArgs* a, int count, hipStream_t stream);
+
+namespace {
+
+const char* soft_unsupported(int N, const int* nx, const int* nu, const int* ng) {
+    if (N < 1 || nu[N] != 0) return "soft IPM: N >= 1 and nu[N] = 0 required";
+    for (int k = 0; k <= N; k++)
+        if (ng[k] != 0) return "soft IPM with general constraints (ng > 0)";
+    for (int k = 0; k < N; k++) {
+        const int nux = nu[k] + nx[k], nx1 = nx[k + 1];
+        const long idx = (long)(nux / BS) * BS * rup(nx1, BS) + nux % BS + BS * (long)(nx1 > 0 ? nx1 - 1 : 0);
+        if (nx1 > 0 && idx >= (long)rup(nux + 1, BS) * rup(nx1, NCL))
+            return "soft IPM: the reference reads b_k outside BAbt_k here (stride round_up(nx,4), d_ip2_soft.c:172)";
+    }
+    return nullptr;
+}
+
+bool soft_launch(int which, const SoftArgs& s) {
+    if (hk_soft_launch(which, &s, 1, g_ctx.stream)) {
+        set_err(HPMPC_MI355X_EHIP, "hk_soft_pass launch failed");
+        return false;
+    }
+    return true;
+}
+
+}  // namespace
+
+extern "C" int d_ip2_mpc_soft_tv_work_space_size_bytes(int N, int* nx, int* nu, int* nb, int* ng, int* ns) {
+    (void)N;
+    (void)nx;
+    (void)nu;
+    (void)nb;
+    (void)ng;
+    (void)ns;
+    return 64;  // iterate, factor and work vectors live on the device
+}
+
+extern "C" int d_ip2_mpc_soft_tv(int* kk, int k_max, double mu0, double mu_tol, double alpha_min, int warm_start,
+                                 double* stat, int N, int* nx, int* nu, int* nb, int** idxb, int* ng, int* ns,
+                                 double** pBAbt, double** pQ, double** Z, double** z, double** pDCt, double** d,
+                                 double** ux, int compute_mult, double** pi, double** lam, double** t,
+                                 double* double_work_memory) {
+    (void)pDCt;
+    (void)double_work_memory;
+    g_err = 0;
+    if (const char* why = soft_unsupported(N, nx, nu, ng)) {
+        set_err(HPMPC_MI355X_EUNSUPPORTED, why);
+        return g_err;
+    }
+    double mu_scal = 0.0;
+    for (int k = 0; k <= N; k++) mu_scal += 2 * nb[k] + 2 * ng[k] + 4 * ns[k];
+    if (mu_scal == 0.0) {  // the reference solves into its workspace and leaves every output untouched (:273-284)
+        *kk = 0;
+        return 0;
+    }
+    mu_scal = 1.0 / mu_scal;
+    std::vector<int> nbs(N + 1);
+    for (int k = 0; k <= N; k++) nbs[k] = nb[k] + ns[k];
+    hpmpc_mi355x_plan* P = g_ctx.get_plan(N, nx, nu, nbs.data(), idxb, ng);
+    if (!P) return g_err;
+    // soft layout (doubles): per-stage constraint vectors, then the flat Qx / qx | Zl / zl block
+    std::vector<SoftStage> ss(N + 1);
+    long sC = 0, sD = 0, sZ = 0, F = 0;
+    int padM = 0;
+    for (int k = 0; k <= N; k++) {
+        SoftStage& s = ss[k];
+        memset(&s, 0, sizeof s);
+        s.nu = P->st[k].nu;
+        s.nx = nx[k];
+        s.nx1 = k < N ? nx[k + 1] : 0;
+        s.nb = nb[k];
+        s.ns = ns[k];
+        s.pnb = rup(nb[k], BS);
+        s.pns = rup(ns[k], BS);
+        s.oC = (int)sC;
+        sC += 2 * s.pnb + 4 * s.pns;
+        s.oD = (int)sD;
+        sD += 2 * s.pnb + 2 * s.pns;
+        s.oZ = (int)sZ;
+        sZ += 2 * s.pns;
+        s.oQ = (int)F;
+        F += 2 * (s.pnb + s.pns);
+        padM = std::max(padM, 2 * (s.pnb + s.pns));
+    }
+    for (int k = 0; k <= N; k++) {
+        ss[k].oZl = (int)F;
+        F += 4 * ss[k].pns;
+    }
+    const long sF = F + padM + 16;
+    for (int k = 0; k <= N; k++) {  // where the soft gradient term goes (d_aux_ip_soft_lib4.c:557, :601)
+        SoftStage& s = ss[k];
+        const int pnbs = rup(s.nb + s.ns, BS);
+        s.oS = s.oQ + s.pnb + s.pns + (s.nb > 0 ? pnbs + s.nb : s.nb);
+        for (int i = 0; s.nb > 0 && i < s.ns; i++)
+            for (int j = k; j <= N; j++)
+                if (s.oS + i >= ss[j].oZl && s.oS + i < ss[j].oZl + 2 * ss[j].pns) {
+                    set_err(HPMPC_MI355X_EUNSUPPORTED,
+                            "soft IPM: the reference's soft-gradient write lands in a Zl read later in the same pass");
+                    return g_err;
+                }
+    }
+    Arena A = arena(P, 1);
+    const size_t n1 = N + 1, v16 = n1 * V16;
+    size_t o = A.total;
+    auto take = [&](size_t n) {
+        size_t r = o;
+        o += (n + 7) / 8 * 8;
+        return r;
+    };
+    const size_t oScal = take(4), oIst = take(4), oStat = take(5 * (size_t)(k_max > 0 ? k_max : 1) + 8),
+                 oTab = take((sizeof(SoftStage) * n1 + 7) / 8), oIdx = take((n1 * 16 * sizeof(int) + 7) / 8),
+                 oD = take(sD + 1), oZ = take(sZ + 1), oz = take(sZ + 1), oF = take(sF), oUx = take(v16),
+                 oPi = take(v16);
+    size_t oCv[6];
+    for (int i = 0; i < 6; i++) oCv[i] = take(sC + 1);
+    const size_t total = o;
+    if (!g_ctx.ensure(total)) return g_err;
+    double* H = g_ctx.host;
+    stage_BAbt(P, H, A, pBAbt);
+    stage_RSQ(P, H, A, pQ);
+    memcpy(H + oTab, ss.data(), sizeof(SoftStage) * n1);
+    int* hidx = reinterpret_cast<int*>(H + oIdx);
+    for (int k = 0; k <= N; k++) {
+        const SoftStage& s = ss[k];
+        const int nux = s.nu + s.nx;
+        for (int l = 0; l < nbs[k]; l++) hidx[k * 16 + l] = idxb[k][l];
+        for (int l = 0; l < nux; l++) H[A.vq + k * V16 + l] = P4(pQ[k], rup(nux, NCL), nux, l);
+        if (k < N) {  // b_k with the reference's stride round_up(nx_{k+1}, 4) (d_ip2_soft.c:172)
+            const double* row = pBAbt[k] + (nux / BS) * BS * rup(s.nx1, BS) + nux % BS;
+            for (int j = 0; j < s.nx1; j++) H[A.vb + k * V16 + j] = row[BS * j];
+        }
+        memcpy(H + oD + s.oD, d[k], (2 * s.pnb + 2 * s.pns) * sizeof(double));
+        if (s.ns > 0) {
+            memcpy(H + oZ + s.oZ, Z[k], 2 * s.pns * sizeof(double));
+            memcpy(H + oz + s.oZ, z[k], 2 * s.pns * sizeof(double));
+        }
+        if (warm_start) memcpy(H + oUx + k * V16, ux[k], nux * sizeof(double));
+    }
+    double* D = g_ctx.dev;
+    KArgs a = arena_args(P, A, D);
+    a.use_box = 1;
+    a.update_q = 1;
+    a.update_b = 0;
+    a.compute_pi = compute_mult;
+    a.compute_Pb = 1;
+    KArgs a2 = a;
+    a2.compute_Pb = 0;
+    SoftArgs s;
+    memset(&s, 0, sizeof s);
+    s.N = N;
+    s.nprob = 1;
+    s.k_max = k_max;
+    s.warm_start = warm_start;
+    s.nq = (N + 4) / 4;
+    s.st = reinterpret_cast<const SoftStage*>(D + oTab);
+    s.idxb = reinterpret_cast<const int*>(D + oIdx);
+    s.d = D + oD;
+    s.Z = D + oZ;
+    s.z = D + oz;
+    s.t = D + oCv[0];
+    s.lam = D + oCv[1];
+    s.dt = D + oCv[2];
+    s.dlam = D + oCv[3];
+    s.lamt = D + oCv[4];
+    s.tinv = D + oCv[5];
+    s.flat = D + oF;
+    s.ux = D + oUx;
+    s.pi = D + oPi;
+    s.dux = D + A.ux;
+    s.dpi = D + A.pi;
+    s.vQx = D + A.vQx;
+    s.vqx = D + A.vqx;
+    s.mu0 = mu0;
+    s.mu_tol = mu_tol;
+    s.alpha_min = alpha_min;
+    s.mu_scal = mu_scal;
+    s.scal = D + oScal;
+    s.ist = reinterpret_cast<int*>(D + oIst);
+    s.stat = D + oStat;
+    if (!hip_ok(hipMemcpyAsync(D, H, total * sizeof(double), hipMemcpyHostToDevice, g_ctx.stream), "H2D") ||
+        !soft_launch(0, s))
+        return g_err;
+    const int* hist = reinterpret_cast<const int*>(H + oIst);
+    for (int it = 0; it < k_max; it++) {
+        if (!soft_launch(1, s) || !run(K_SV, a, "hk_ric_sv") || !soft_launch(2, s) || !run(K_TRS, a2, "hk_ric_trs") ||
+            !soft_launch(3, s))
+            return g_err;
+        if (!hip_ok(hipMemcpyAsync(H + oIst, D + oIst, 4 * sizeof(int), hipMemcpyDeviceToHost, g_ctx.stream),
+                    "D2H") ||
+            !hip_ok(hipStreamSynchronize(g_ctx.stream), "sync"))
+            return g_err;
+        if (!hist[1]) break;
+    }
+    if (!hip_ok(hipMemcpyAsync(H, D, total * sizeof(double), hipMemcpyDeviceToHost, g_ctx.stream), "D2H") ||
+        !hip_ok(hipStreamSynchronize(g_ctx.stream), "sync"))
+        return g_err;
+    *kk = hist[0];
+    for (int i = 0; i < 5 * hist[0]; i++) stat[i] = H[oStat + i];
+    for (int k = 0; k <= N; k++) {
+        const SoftStage& st = ss[k];
+        memcpy(ux[k], H + oUx + k * V16, (st.nu + st.nx) * sizeof(double));
+        if (k < N) memcpy(pi[k], H + oPi + k * V16, st.nx1 * sizeof(double));
+        const int nc = 2 * st.pnb + 4 * st.pns;
+        if (nc > 0) {
+            memcpy(lam[k], H + oCv[1] + st.oC, nc * sizeof(double));
+            memcpy(t[k], H + oCv[0] + st.oC, nc * sizeof(double));
+        }
+    }
+    return hist[2];
 }

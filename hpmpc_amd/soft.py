@@ -73,8 +73,9 @@ def mass_spring_soft(N: int, nx: int, nu: int, *, x0=None, Zq: float = 0.0, zl: 
     x0 = [3.5, 3.5, 0, ...], Q = Q_diag I (0 in the driver), R = 2 I, q = 0.1, r = 0.2; hard input boxes at
     stages 0..N-1 (nb = nu), soft state boxes at stages 1..N (ns = nx), Z = Zq, z = zl.
     ``soft`` / ``hard`` = False drop the soft / hard boxes.
-    ``hard_last`` > 0 adds hard boxes on the first ``hard_last`` states of the terminal stage (a shape the
-    driver does not use: it exercises the reference's soft-gradient index for nb > 0 at k = N)."""
+    ``hard_last`` > 0 puts hard boxes on the first ``hard_last`` states of the terminal stage and soft ones on
+    the others (a shape the driver does not use: it exercises the reference's soft-gradient index for nb > 0
+    at k = N, whose write lands in Zl / zl of stage 1)."""
     A, B = mass_spring_dynamics(nx, nu)
     rng = np.random.Generator(np.random.PCG64(seed))
     if x0 is None:
@@ -87,7 +88,7 @@ def mass_spring_soft(N: int, nx: int, nu: int, *, x0=None, Zq: float = 0.0, zl: 
     nxv = np.array([0] + [nx] * N, dtype=np.int32)
     nuv = np.array([nu] * N + [0], dtype=np.int32)
     nbv = np.array([nu if hard else 0] * N + [hard_last], dtype=np.int32)
-    nsv = np.array([0] + [nx if soft else 0] * N, dtype=np.int32)
+    nsv = np.array([0] + [nx if soft else 0] * (N - 1) + [(nx - hard_last) if soft else 0], dtype=np.int32)
     BAbt, RSQrq, dv, idxb, Zv, zv = [], [], [], [], [], []
     for k in range(N + 1):
         nuk, nxk = int(nuv[k]), int(nxv[k])
@@ -114,7 +115,7 @@ def mass_spring_soft(N: int, nx: int, nu: int, *, x0=None, Zq: float = 0.0, zl: 
         nbk, nsk = int(nbv[k]), int(nsv[k])
         pnb, pns = rup(nbk, 4), rup(nsk, 4)
         ib = list(range(min(nuk, nbk))) + [nuk + j for j in range(nbk - min(nuk, nbk))]
-        ib += [nuk + j for j in range(nsk)]
+        ib += [nuk + nxk - nsk + j for j in range(nsk)]  # soft boxes on the last nsk states (no variable twice)
         idxb.append(np.array(ib, dtype=np.int32) if ib else np.zeros(1, dtype=np.int32))
         dk = np.zeros(2 * pnb + 2 * pns + 4)
         for j in range(nbk):

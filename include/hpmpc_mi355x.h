@@ -89,6 +89,16 @@ void d_kkt_solve_new_rhs_mpc_hard_tv(int N, int *nx, int *nu_N, int *nb, int **i
                                      double **r_A, double **pQ, double **r_H, double **pDCt, double **r_C,
                                      double **ux, int compute_mult, double **pi, double **lam, double **t,
                                      double *double_work_memory);
+/* Soft-constraint IPM (phase-1 Mehrotra loop with slack variables for the ns soft boxes listed after the nb
+ * hard ones in idxb; d = [lb | ub | ls | us], lam / t = [lo | up | 4 soft blocks], Z / z slack penalties).
+ * include/mpc_solvers.h:69 (mpc_solvers/d_ip2_soft.c:42) */
+int d_ip2_mpc_soft_tv_work_space_size_bytes(int N, int *nx, int *nu, int *nb, int *ng, int *ns);
+/* include/mpc_solvers.h:70 (d_ip2_soft.c:83).  HPMPC_MI355X_EUNSUPPORTED for ng > 0, nu[N] != 0, and the sizes
+ * where the reference itself reads outside BAbt (soft constraints). */
+int d_ip2_mpc_soft_tv(int *kk, int k_max, double mu0, double mu_tol, double alpha_min, int warm_start, double *stat,
+                      int N, int *nx, int *nu, int *nb, int **idxb, int *ng, int *ns, double **pBAbt, double **pQ,
+                      double **Z, double **z, double **pDCt, double **d, double **ux, int compute_mult, double **pi,
+                      double **lam, double **t, double *double_work_memory);
 /* include/mpc_solvers.h:36 (mpc_solvers/d_res_ip_hard.c:38) -- r_q, r_b, r_d and mu (no r_m) */
 void d_res_mpc_hard_tv(int N, int *nx, int *nu, int *nb, int **idxb, int *ng, double **hpBAbt, double **hb,
                        double **hpQ, double **hq, double **hux, double **hpDCt, double **hd, double **hpi,

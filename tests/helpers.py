@@ -204,8 +204,9 @@ def max_err(case, key, got, ref):
 
 
 # d_ip2_mpc_soft_tv, identical kk / ret: the reference's own -mfma -ffp-contract=fast build differs from its
-# default build by up to ux 4e-9, pi 1.5e-7, lam 4e-8, stat 1e-9 on the golden cases (soft constraints)
-TOL_SOFT = dict(ux=5e-8, t=5e-8, pi=1e-6, lam=1e-6, stat=1e-8)
+# default build by up to ux 4e-9, pi 1.5e-7, lam 4e-8, stat 1e-9 on the golden cases and stat 1.3e-7 at mu_tol 1e-8
+# (soft constraints)
+TOL_SOFT = dict(ux=5e-8, t=5e-8, pi=1e-6, lam=1e-6, stat=1e-7)
 
 
 def check_soft(case, got):
