@@ -210,6 +210,66 @@ def bench_pcond(args, torch, red, rank, world, barrier):
     return out
 
 
+def bench_single_qp(args, torch, stream):
+    """configs[1]: one QP (the drivers' x0, test_d_ip_hard.c:306-322) solved alone on the GPU: the device time of
+    a batched-API solve of a batch of one (data resident in HBM), and the drop-in d_ip2_res_mpc_hard_tv call on
+    host lib4 buffers (PCIe staging included).  Latency-bound: one wavefront walks the N stages serially."""
+    from hpmpc_amd.batch import LIBPATH, BatchSolver
+    from hpmpc_amd.cabi import HpmpcAPI, load
+    from hpmpc_amd.ocp import mass_spring_qp
+
+    one = mass_spring_qp(args.N, args.nx, args.nu, batch=1)
+    s = BatchSolver(one, k_max=args.k_max)
+    reps = max(args.steps, 5)
+    for _ in range(2):
+        s.ipm()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for a, b in ev:
+        a.record(stream)
+        s.ipm()
+        b.record(stream)
+    torch.cuda.synchronize()
+    ms = float(np.median([a.elapsed_time(b) for a, b in ev]))
+    kk = int(s.kk[0].item())
+    call, kkc = HpmpcAPI(load(LIBPATH)).prepare_ipm(one.problem(0), k_max=args.k_max)
+    call()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        call()
+    host_ms = (time.perf_counter() - t0) / reps * 1e3
+    return {"workload": f"single_qp_N{args.N}_nx{args.nx}_nu{args.nu}", "kk": kk, "device_ms_per_solve": ms,
+            "device_us_per_ip_iter": ms * 1e3 / max(kk, 1), "dropin_ms_per_solve": host_ms,
+            "dropin_kk": int(kkc.value)}
+
+
+def bench_riccati_small(args, torch, red, rank, world, barrier, stream):
+    """configs[2]: batch x mass-spring N=50 nx=8 nu=3, Riccati only (d_back_ric_rec_sv_tv_res, nb = 0,
+    compute_pi = 1); fact/s over all ranks, hipEvents around each batched launch for the roofline."""
+    from hpmpc_amd.batch import BatchSolver, algorithmic_bytes_per_sv
+    from hpmpc_amd.shard import make_shard
+
+    B, N, nx, nu = args.batch, 50, 8, 3
+    qp = make_shard(N, nx, nu, rank, world, B, boxes=False)
+    s = BatchSolver(qp, k_max=1)
+    for _ in range(max(args.warmup, 1)):
+        s.ric_sv()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    barrier()
+    t0 = time.perf_counter()
+    for a, b in ev:
+        a.record(stream)
+        s.ric_sv()
+        b.record(stream)
+    barrier()
+    dt = red.max(time.perf_counter() - t0)
+    ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    by = algorithmic_bytes_per_sv(qp)
+    ach = B * by / (ms * 1e-3) / 1e9
+    return {"workload": f"riccati_N{N}_nx{nx}_nu{nu}_batch{B}", "value": B * world * args.steps / dt, "unit": "fact/s",
+            "launch_ms": ms, "roofline": {"bound": "hbm", "kernel": "hk_ric_sv", "achieved": ach, "peak": PEAK_HBM_GBS,
+                                          "unit": "GB/s", "frac": ach / PEAK_HBM_GBS, "algorithmic_bytes_per_sv": by}}
+
+
 def main():
     args = parse()
     import torch
@@ -326,6 +386,9 @@ def main():
         cpu = cpu_baseline(qp, args.cpu_seconds, args.k_max, args.cpu_threads)
 
     pc = None if args.no_pcond else bench_pcond(args, torch, red, rank, world, barrier)
+    # configs[2] and configs[1]; skipped in profiling runs so every hk_ipm_* launch belongs to the timed queue
+    rs = None if args.no_isolated else bench_riccati_small(args, torch, red, rank, world, barrier, stream)
+    sq = bench_single_qp(args, torch, stream) if (rank == 0 and not args.no_isolated) else None
 
     if rank == 0:
         line = {
@@ -367,6 +430,8 @@ def main():
                                      "fp64_tflops": B * flops_sv(N, nx, nu) / (sv_ms * 1e-3) / 1e12}},
             "cpu_baseline": cpu,
             "pcond": pc,
+            "riccati_batch_N50": rs,
+            "single_qp": sq,
         }
         print(json.dumps(line), flush=True)
     if dist is not None:

@@ -784,13 +784,16 @@ __device__ __forceinline__ void bwd_step(const RicIO& io, Scratch* sm, const SH&
         double vrow[4];
         col2row(sm, vcol, vrow);
         // Pb_k = Lxx (Lxx' b)  (dtrmv_u_t on W's last row, :266-275); store masked, never skipped
-        double pp = 0.0;
+        double pb = 0.0;
+        if (compute_Pb) {  // wave-uniform: the Riccati-only sv (compute_Pb = 0) skips P b
+            double pp = 0.0;
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const int j = g + 4 * r;
-            pp += (j <= c && j >= xo1) ? S[r] * vrow[r] : 0.0;
+            for (int r = 0; r < 4; r++) {
+                const int j = g + 4 * r;
+                pp += (j <= c && j >= xo1) ? S[r] * vrow[r] : 0.0;
+            }
+            pb = xrow_sum(pp);
         }
-        const double pb = xrow_sum(pp);
         gst(Pb, k * V16 + (c - xo1), pb, compute_Pb && live && g == 0 && c >= xo1 && c < xo1 + nx1);
         // w_last = b' Lxx + l_{k+1,x}   (dgead, :276)  -> m_last += W w_last
         double mp = 0.0;
@@ -952,10 +955,14 @@ __device__ __forceinline__ void fwd_fetch(const RicIO& io, const SH& sh, int k, 
                                           FwdFrag& f) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
     const double* Fk = io.F + (long)k * FSTRIDE;
+    // The factor tile is read by the u-block solve of generic stages and by pi (compute_pi) only, inv_diag by
+    // the generic solve, l by the sv forward: the gain-form predictor masks the rest off (a masked lane reads
+    // nothing, and every path keeps the same load count for the counted vmcnt waits).
+    const bool needS = !SH::fixed || compute_pi;
 #pragma unroll
-    for (int r = 0; r < 4; r++) f.S[r] = gld(Fk, r * 64 + l);
-    f.lc = gld(Fk, 256 + c);
-    f.invd = gld(Fk, 272 + c);
+    for (int r = 0; r < 4; r++) f.S[r] = gld(Fk, r * 64 + l, needS);
+    f.lc = gld(Fk, 256 + c, MODE == 0);
+    f.invd = gld(Fk, 272 + c, !SH::fixed);
     f.kg = gld(Fk, 288 + l);
     const int kk = k < io.N ? k : io.N - 1;  // stage N has no BAbt block: loads clamped, values masked
     const bool live = k < io.N;
@@ -1261,7 +1268,9 @@ __device__ __forceinline__ void trs_step(const RicIO& io, Scratch* sm, const SH&
     const int vc = tile_var(c, sh.nu, sh.nx, sh.xo);
     const int s = c - xo1;
     double pbc = cur.pbc;
-    {
+    // P_{k+1} b_k is recomputed only on request (wave-uniform branch): the IPM corrector passes
+    // compute_Pb = 0 and reuses the Pb its factorisation stored (d_ip2_res_hard.c:628, :1168)
+    if (compute_Pb) {
         double part = 0.0;
 #pragma unroll
         for (int r = 0; r < 4; r++) part += (c >= xo1 ? lowS(S1, r, g, c) : 0.0) * cur.brow[r];
@@ -1274,9 +1283,9 @@ __device__ __forceinline__ void trs_step(const RicIO& io, Scratch* sm, const SH&
             const int j = g + 4 * r;
             pp += (j <= c && j >= xo1) ? S1[r] * vrow[r] : 0.0;
         }
-        if (compute_Pb) pbc = xrow_sum(pp);
-        gst(Pb, k * V16 + s, pbc, compute_Pb && g == 0 && s >= 0 && s < nx1);
+        pbc = xrow_sum(pp);
     }
+    gst(Pb, k * V16 + s, pbc, compute_Pb && g == 0 && s >= 0 && s < nx1);
     const double wc = (s >= 0 && s < nx1) ? pbc + pcol : 0.0;
     double wrow[4];
     col2row(sm, wc, wrow);

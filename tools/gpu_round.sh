@@ -8,7 +8,7 @@ mkdir -p gpurun_out/prof
 export TMPDIR=/tmp
 R=${1:-r01}
 step() { local name=$1; shift; echo "== $name"; "$@" > gpurun_out/$name.log 2>&1; local rc=$?; tail -${TAILN:-3} gpurun_out/$name.log; if [ $rc -ne 0 ]; then echo "$name failed rc=$rc"; exit $rc; fi; }
-step tests timeout -k 10 900 python3 -m pytest tests -m gpu -q -x
+step tests timeout -k 10 900 python3 -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread
 step smoke timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()"
 step pmc_fetch timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof/fetch -o run --output-format csv -- python3 tools/pmc_run.py
 step pmc_write timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof/write -o run --output-format csv -- python3 tools/pmc_run.py
