@@ -356,6 +356,13 @@ __device__ __forceinline__ bool who_am_i(const KArgs& a, Who& w) {
     return w.q >= 0;
 }
 
+// Whether this workgroup's problem still iterates (its control state in the slot's workspace); read before
+// the stage tables are staged, so the finished problems of a batch and the idle slots of a draining queue
+// return at once.
+__device__ __forceinline__ bool slot_active(const KArgs& a, const Who& who) {
+    return carve(a.ws + (long)who.s * a.sW, a.N).state[S_ACTIVE] != 0.0;
+}
+
 __device__ __forceinline__ IpmView ipm_view(const KArgs& a, const LdsTabs& T, const Who& who) {
     IpmView v;
     v.N = a.N;
@@ -543,10 +550,10 @@ __global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_init(KArgs a) {
 // Factorisation of the iteration's KKT system, Hessian / gradient box terms fused into the fetch.
 template <class FX>
 __global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_fact(KArgs a) {
+    Who who;
+    if (!who_am_i(a, who) || !slot_active(a, who)) return;  // idle slots leave before staging the tables
     const LdsTabs T = lds_tables(a);
     Scratch& sm = *T.sm;
-    Who who;
-    if (!who_am_i(a, who)) return;
     IpmView v = ipm_view(a, T, who);
     const double* st = v.w.state;
     if (st[S_ACTIVE] == 0.0) return;
@@ -562,10 +569,10 @@ __global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_fact(KArgs a) {
 // Predictor solve with the box steps and step length fused in, then mu_aff and the centering target.
 template <class FX>
 __global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_pred(KArgs a) {
+    Who who;
+    if (!who_am_i(a, who) || !slot_active(a, who)) return;  // idle slots leave before staging the tables
     const LdsTabs T = lds_tables(a);
     Scratch& sm = *T.sm;
-    Who who;
-    if (!who_am_i(a, who)) return;
     IpmView v = ipm_view(a, T, who);
     double* st = v.w.state;
     if (st[S_ACTIVE] == 0.0) return;
@@ -604,10 +611,10 @@ __global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_pred(KArgs a) {
 // Corrector: centering / gradient update fused into the trs backward, box steps + alpha into its forward.
 template <class FX>
 __global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_corr(KArgs a) {
+    Who who;
+    if (!who_am_i(a, who) || !slot_active(a, who)) return;  // idle slots leave before staging the tables
     const LdsTabs T = lds_tables(a);
     Scratch& sm = *T.sm;
-    Who who;
-    if (!who_am_i(a, who)) return;
     IpmView v = ipm_view(a, T, who);
     double* st = v.w.state;
     if (st[S_ACTIVE] == 0.0) return;
@@ -630,9 +637,9 @@ __global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_corr(KArgs a) {
 // Update of the iterate (with backups) and, in phase 2, the residuals of the new iterate; loop control.
 template <class FX>
 __global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_update(KArgs a) {
-    const LdsTabs T = lds_tables(a);
     Who who;
-    if (!who_am_i(a, who)) return;
+    if (!who_am_i(a, who) || !slot_active(a, who)) return;  // idle slots leave before staging the tables
+    const LdsTabs T = lds_tables(a);
     IpmView v = ipm_view(a, T, who);
     double* st = v.w.state;
     if (st[S_ACTIVE] == 0.0) return;
