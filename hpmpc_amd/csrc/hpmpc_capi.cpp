@@ -420,6 +420,8 @@ extern "C" int hpmpc_mi355x_ipm_queue(const hpmpc_mi355x_plan* plan, const hpmpc
     a.stat = stat;
     a.nq = nq;
     a.qctl = qctl;
+    a.nslots = n_slots;
+    a.qpar = 0;  // hk_ipm_init fills active list 0; iteration t runs list t & 1
     hipStream_t st = (hipStream_t)stream;
     constexpr int R = 8;  // ticks per chunk
     static thread_local int* hdone = nullptr;
@@ -449,7 +451,9 @@ extern "C" int hpmpc_mi355x_ipm_queue(const hpmpc_mi355x_plan* plan, const hpmpc
         }
         return true;
     };
-    if (!hip_ok(hipMemsetAsync(qctl, 0, 2 * sizeof(int), st), "memset")) return g_err;
+    if (!hip_ok(hipMemsetAsync(qctl, 0, 2 * sizeof(int), st), "memset") ||
+        !hip_ok(hipMemsetAsync(qctl + 2 + n_slots, 0, 2 * sizeof(int), st), "memset"))
+        return g_err;
     if (pass_ms && !hip_ok(hipEventRecord(ev[0], st), "event record")) return g_err;
     if (!launch(10)) return g_err;
     if (pass_ms) {
@@ -469,6 +473,7 @@ extern "C" int hpmpc_mi355x_ipm_queue(const hpmpc_mi355x_plan* plan, const hpmpc
         hipEvent_t* e = &ev[par * nev];
         if (pass_ms && !hip_ok(hipEventRecord(e[0], st), "event record")) return g_err;
         for (int i = 0; i < R; i++) {
+            a.qpar = (int)((ticks + i) & 1);  // active-slot list of this iteration (kernel args are copied at launch)
             for (int k = 0; k < 4; k++) {
                 if (!launch(11 + k)) return g_err;
                 if (pass_ms && !hip_ok(hipEventRecord(e[4 * i + k + 1], st), "event record")) return g_err;

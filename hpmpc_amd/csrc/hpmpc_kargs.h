@@ -38,6 +38,10 @@ struct KArgs {
     // problem queue (hpmpc_mi355x_ipm_queue): nq > 0 makes the grid a set of slots; slot s solves queue
     // entries one after another (entry q: data problem q % nprob, iterate/outputs at q, workspace s)
     int nq;
-    int* qctl;  // [0] next entry to hand out, [1] entries finished, [2 + s] entry held by slot s (-1 none)
+    int* qctl;  // [0] next entry to hand out, [1] entries finished, [2 + s] entry held by slot s (-1 none),
+                // [2 + nslots + p] length of active-slot list p, [4 + nslots + p nslots ..] list p (p = 0, 1)
     unsigned long long* dbg;  // diagnostic stamp buffer (HK_STAMPS builds only)
+    int nslots;  // queue slots
+    int qpar;    // queue tick parity: workgroup i of an iteration kernel runs slot list[qpar][i]; the update
+                 // pass lists the slots that iterate again in list qpar ^ 1 (hk_ipm_init fills list qpar)
 };

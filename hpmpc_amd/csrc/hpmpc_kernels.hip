@@ -339,6 +339,13 @@ struct IpmView {
     BoxCtx bc;
 };
 
+// Queue active-slot lists (KArgs.qctl layout): length and entries of list p.
+__device__ __forceinline__ int* qcount(const KArgs& a, int p) { return a.qctl + 2 + a.nslots + p; }
+__device__ __forceinline__ int* qlist(const KArgs& a, int p) { return a.qctl + 4 + a.nslots + p * a.nslots; }
+__device__ __forceinline__ void qlist_push(const KArgs& a, int p, int s) {
+    if (lane_id() == 0) qlist(a, p)[atomicAdd(qcount(a, p), 1)] = s;
+}
+
 // Which workspace (s), iterate/output (q) and data problem (d) this workgroup works on.
 struct Who {
     int s, q, d;
@@ -350,7 +357,11 @@ __device__ __forceinline__ bool who_am_i(const KArgs& a, Who& w) {
         w.s = w.q = w.d = p;
         return p < a.nprob;
     }
-    w.s = blockIdx.x;
+    // queue: workgroup i takes the i-th listed active slot, so a draining queue runs a dense grid prefix (one
+    // wave per SIMD once fewer slots than SIMDs iterate) instead of scattered slots that share SIMDs
+    const int n = __builtin_amdgcn_readfirstlane(*qcount(a, a.qpar));
+    if ((int)blockIdx.x >= n) return false;
+    w.s = __builtin_amdgcn_readfirstlane(qlist(a, a.qpar)[blockIdx.x]);
     w.q = __builtin_amdgcn_readfirstlane(a.qctl[2 + w.s]);
     w.d = w.q >= 0 ? w.q % a.nprob : 0;
     return w.q >= 0;
@@ -512,9 +523,9 @@ __device__ bool ipm_start(const KArgs& a, const LdsTabs& T, IpmView& v) {
     return ipm_continue<FX>(a, v, 0, mu, 1.0, 0.0, sn ? 2 : 1);
 }
 
-// Queue mode: hand slot s the next queue entries until one of them iterates (or the queue is empty).
+// Queue mode: hand slot s the next queue entries until one of them iterates (true) or the queue is empty.
 template <class FX>
-__device__ void ipm_refill(const KArgs& a, const LdsTabs& T, int s) {
+__device__ bool ipm_refill(const KArgs& a, const LdsTabs& T, int s) {
     const bool l0 = lane_id() == 0;
     for (;;) {
         int q = 0;
@@ -522,12 +533,12 @@ __device__ void ipm_refill(const KArgs& a, const LdsTabs& T, int s) {
         q = __builtin_amdgcn_readfirstlane(q);
         if (q >= a.nq) {
             if (l0) a.qctl[2 + s] = -1;
-            return;
+            return false;
         }
         if (l0) a.qctl[2 + s] = q;
         const Who who{s, q, q % a.nprob};
         IpmView v = ipm_view(a, T, who);
-        if (ipm_start<FX>(a, T, v)) return;
+        if (ipm_start<FX>(a, T, v)) return true;
         if (l0) atomicAdd(&a.qctl[1], 1);
     }
 }
@@ -537,8 +548,8 @@ __device__ void ipm_refill(const KArgs& a, const LdsTabs& T, int s) {
 template <class FX>
 __global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_init(KArgs a) {
     const LdsTabs T = lds_tables(a);
-    if (a.nq) {
-        ipm_refill<FX>(a, T, blockIdx.x);
+    if (a.nq) {  // every slot takes its first entry; the iterating ones form the first active list
+        if (ipm_refill<FX>(a, T, blockIdx.x)) qlist_push(a, a.qpar, blockIdx.x);
         return;
     }
     Who who;
@@ -550,6 +561,8 @@ __global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_init(KArgs a) {
 // Factorisation of the iteration's KKT system, Hessian / gradient box terms fused into the fetch.
 template <class FX>
 __global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_fact(KArgs a) {
+    // queue: empty the list this iteration's update pass fills (nothing reads it before then)
+    if (a.nq && blockIdx.x == 0 && lane_id() == 0) *qcount(a, a.qpar ^ 1) = 0;
     Who who;
     if (!who_am_i(a, who) || !slot_active(a, who)) return;  // idle slots leave before staging the tables
     const LdsTabs T = lds_tables(a);
@@ -657,10 +670,12 @@ __global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_update(KArgs a) {
     wsync();
     if (v.l == 0) v.stat[5 * kk + 4] = mu;
     kk++;
-    if (!ipm_continue<FX>(a, v, kk, mu, alpha, st[S_SIGMA], phase) && a.nq) {
+    bool again = ipm_continue<FX>(a, v, kk, mu, alpha, st[S_SIGMA], phase);
+    if (!again && a.nq) {
         if (v.l == 0) atomicAdd(&a.qctl[1], 1);
-        ipm_refill<FX>(a, T, who.s);  // queue mode: the slot takes the next entry
+        again = ipm_refill<FX>(a, T, who.s);  // queue mode: the slot takes the next entry
     }
+    if (a.nq && again) qlist_push(a, a.qpar ^ 1, who.s);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -216,7 +216,9 @@ int hpmpc_mi355x_ipm_batch_profiled(const hpmpc_mi355x_plan *plan, const hpmpc_m
 /* Problem queue (continuous batching): solve nq problems with n_slots resident solver slots.  Queue
  * entry q solves data problem q % nprob (BAbt/RSQrq/d as in hpmpc_mi355x_ipm_batch, nprob problems);
  * ux/pi/lam/t/kk/ret/stat are per queue entry (nq of each, same strides); ws holds n_slots
- * workspaces; qctl is device scratch of 2 + n_slots ints.  A slot whose problem has finished takes
+ * workspaces; qctl is device scratch of 4 + 3 * n_slots ints (counters, the entry each slot holds, and two
+ * lists of the slots that iterate: workgroup i of an iteration runs the i-th listed slot, so a draining queue
+ * keeps one slot per SIMD).  A slot whose problem has finished takes
  * the next entry at the following iteration, so the GPU is not left idle behind the slowest problem
  * of a batch.  Results are those of hpmpc_mi355x_ipm_batch on each entry (the per-slot workspace is
  * reused, so a queue solve leaves no factor behind for d_kkt_solve_new_rhs_res_mpc_hard_tv).

@@ -275,7 +275,7 @@ def test_queue_matches_batch(small_batch, n_slots, nq):
     pass_ms, ticks = Q.run(profiled=True)
     torch.cuda.synchronize()
     _queue_equals_batch(s, Q, nq)
-    assert int(Q.qctl[1]) == nq and bool((Q.qctl[2:] == -1).all())
+    assert int(Q.qctl[1]) == nq and bool((Q.qctl[2:2 + n_slots] == -1).all())
     kk = s.kk.cpu().numpy()
     assert ticks >= int(kk.max()) and pass_ms[1] > 0.0
     Q.run()  # a second run over the same buffers gives the same answers
