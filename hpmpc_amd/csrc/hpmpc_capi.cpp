@@ -329,6 +329,35 @@ int ipm_launch(const hpmpc_mi355x_plan* plan, const hpmpc_mi355x_layout* lay, in
     return g_err = 0;
 }
 
+// hipEvents (and optionally a small pinned host buffer) owned by one API call.  The destructor first
+// waits for every event recorded on them, so no queued copy or record can outlive its storage.
+struct CallEvents {
+    std::vector<hipEvent_t> e;
+    int* hint = nullptr;
+    bool create(int n) {
+        e.reserve(n);
+        for (int i = 0; i < n; i++) {
+            hipEvent_t x;
+            if (!hip_ok(hipEventCreate(&x), "event create")) return false;
+            e.push_back(x);
+        }
+        return true;
+    }
+    bool host_ints(int n) {
+        if (!hip_ok(hipHostMalloc((void**)&hint, n * sizeof(int), hipHostMallocDefault), "host alloc")) return false;
+        for (int i = 0; i < n; i++) hint[i] = 0;
+        return true;
+    }
+    hipEvent_t& operator[](size_t i) { return e[i]; }
+    ~CallEvents() {
+        for (hipEvent_t x : e) {
+            (void)hipEventSynchronize(x);
+            (void)hipEventDestroy(x);
+        }
+        if (hint) (void)hipHostFree(hint);
+    }
+};
+
 }  // namespace
 
 extern "C" int hpmpc_mi355x_ipm_batch(const hpmpc_mi355x_plan* plan, const hpmpc_mi355x_layout* lay, int nprob,
@@ -347,13 +376,10 @@ extern "C" int hpmpc_mi355x_ipm_batch_profiled(const hpmpc_mi355x_plan* plan, co
                                                int warm_start, int compute_mult, int* kk, int* ret, double* stat,
                                                double* pass_ms, void* stream) {
     // the same launch sequence as hpmpc_mi355x_ipm_batch, with a hipEvent pair around every pass kernel
-    static thread_local std::vector<hipEvent_t> ev;
+    // (events are per call: they belong to the current device, and nothing outlives the call)
     const int npass = 1 + 4 * (k_max > 0 ? k_max : 0);
-    while ((int)ev.size() < 2 * npass) {
-        hipEvent_t e;
-        if (!hip_ok(hipEventCreate(&e), "event create")) return g_err;
-        ev.push_back(e);
-    }
+    CallEvents ev;
+    if (!ev.create(2 * npass)) return g_err;
     hipStream_t st = (hipStream_t)stream;
     for (int i = 0; i < npass; i++) {
         const int which = i == 0 ? 10 : 11 + (i - 1) % 4;
@@ -424,16 +450,14 @@ extern "C" int hpmpc_mi355x_ipm_queue(const hpmpc_mi355x_plan* plan, const hpmpc
     a.qpar = 0;  // hk_ipm_init fills active list 0; iteration t runs list t & 1
     hipStream_t st = (hipStream_t)stream;
     constexpr int R = 8;  // ticks per chunk
-    static thread_local int* hdone = nullptr;
-    static thread_local std::vector<hipEvent_t> ev;  // 2 chunk parities x (R*4 + 1) kernel boundaries
+    // Per-call polling state: 2 chunk parities x (R*4 + 1) kernel boundaries + 2 "finished count copied"
+    // events, and the pinned host copy of the device's finished counter.  Nothing is shared between calls
+    // (so a later call on another stream or device can never read a stale count of this one); the
+    // destructor waits for the copies this call left queued before it frees their target.
     const int nev = R * 4 + 1;
-    if (!hdone && !hip_ok(hipHostMalloc((void**)&hdone, 2 * sizeof(int), hipHostMallocDefault), "host alloc"))
-        return g_err;
-    while ((int)ev.size() < 2 * nev + 2) {
-        hipEvent_t e;
-        if (!hip_ok(hipEventCreate(&e), "event create")) return g_err;
-        ev.push_back(e);
-    }
+    CallEvents ev;
+    if (!ev.create(2 * nev + 2) || !ev.host_ints(2)) return g_err;
+    int* hdone = ev.hint;
     hipEvent_t* done_ev = &ev[2 * nev];
     auto launch = [&](int which) {
         if (hk_launch(which, &a, n_slots, st)) {

@@ -731,7 +731,8 @@ static void update_var_res(int N, int *nx, int *nu, int *nb, int *ng, double alp
         cdim_t c = cdim(nb, ng, k);
         int nx1 = k < N ? nx[k + 1] : 0;
         axpy_bkp(nu[k] + nx[k], alpha, dux[k], ux[k], ux_bkp ? ux_bkp[k] : NULL);
-        axpy_bkp(nx1, alpha, dpi[k], pi[k], pi_bkp ? pi_bkp[k] : NULL);
+        if (k < N) /* pi, dpi, pi_bkp hold N stage pointers: there is no pi[N] to touch */
+            axpy_bkp(nx1, alpha, dpi[k], pi[k], pi_bkp ? pi_bkp[k] : NULL);
         int offs[4] = {0, c.pnb, 2 * c.pnb, 2 * c.pnb + c.png};
         int lens[4] = {c.nb, c.nb, c.ng, c.ng};
         for (int s = 0; s < 4; s++) {

@@ -326,15 +326,27 @@ def random_qp(N, nx, nu, nb=None, seed=0, box=1.0, ng=None):
     return OCPQP(N, nx, nu, nb, ngv, idxb, BAbt, RSQrq, d, DCt, None)
 
 
-def compare_ipm(case_like_qp, a, b, tol=TOL_IPM):
-    """max error of two ipm() results over valid parts."""
+# Every comparison that took compare_ipm's divergence escape, as (kk, max |lam|): tests that allow the escape
+# bound how many of their cases may take it.
+DIVERGENT_SKIPS = []
+
+
+def compare_ipm(case_like_qp, a, b, tol=TOL_IPM, allow_divergent=False):
+    """max error of two ipm() results over valid parts.
+
+    A primal-dual divergence (the oracle stops on alpha_min, ret 2, with |lam| > 1e12: an infeasible QP whose
+    lam runs to 1e33) amplifies last-bit differences without bound -- the oracle and the reference build itself
+    differ by O(1) there -- so only kk and ret are comparable.  That escape is taken only where the caller
+    allows it (allow_divergent, for deliberately sampled non-converged problems), and every use is recorded in
+    DIVERGENT_SKIPS; a converged problem (ret 0) can never take it."""
     qp = case_like_qp
     assert a["kk"] == b["kk"] and a["ret"] == b["ret"], (a["kk"], b["kk"], a["ret"], b["ret"])
-    if b["ret"] == 2 and max(float(np.max(np.abs(x))) for x in b["lam"]) > 1e12:
-        # alpha_min exit of a primal-dual divergence (infeasible QP, lam -> 1e33): the iterates amplify
-        # last-bit differences without bound -- the oracle and the reference build itself differ by
-        # O(1) here -- so only the iteration count and the return code are comparable.
-        return 0.0
+    if b["ret"] == 2:
+        lam_max = max(float(np.max(np.abs(x))) for x in b["lam"])
+        if lam_max > 1e12:
+            assert allow_divergent, f"oracle diverged (ret 2, |lam| = {lam_max:.1e}) on a case that must compare"
+            DIVERGENT_SKIPS.append((int(b["kk"]), lam_max))
+            return 0.0
     e = 0.0
     for k in range(qp.N + 1):
         n = qp.nux(k)

@@ -242,13 +242,19 @@ def test_full_size_properties():
                                       "liboracle.so")), "orc_")
     lamt = s.lam.cpu().numpy(), s.t.cpu().numpy()
     pi = s.pi.cpu().numpy()
-    for p in (0, 1, 511, 1023) + tuple(np.nonzero(ret != 0)[0][:2]):
+    from helpers import DIVERGENT_SKIPS
+
+    skips0 = len(DIVERGENT_SKIPS)
+    unconverged = tuple(int(p) for p in np.nonzero(ret != 0)[0][:2])
+    for p in (0, 1, 511, 1023) + unconverged:
         one = qp.problem(int(p))
         r = orc.ipm(one, k_max=50)
         got = dict(kk=int(kk[p]), ret=int(ret[p]), ux=[ux[p, k] for k in range(101)],
                    pi=[pi[p, k] for k in range(100)], lam=[lamt[0][p, k] for k in range(101)],
                    t=[lamt[1][p, k] for k in range(101)])
-        compare_ipm(one, got, r, tol=TOL_IPM)
+        # only the deliberately sampled non-converged problems may be divergent (compare kk/ret only)
+        compare_ipm(one, got, r, tol=TOL_IPM, allow_divergent=p in unconverged and ret[p] == 2)
+    assert len(DIVERGENT_SKIPS) - skips0 <= len(unconverged)
 
 
 # ------------------------------------------------------------------ problem queue (continuous batching)
@@ -281,6 +287,28 @@ def test_queue_matches_batch(small_batch, n_slots, nq):
     Q.run()  # a second run over the same buffers gives the same answers
     torch.cuda.synchronize()
     _queue_equals_batch(s, Q, nq)
+
+
+def test_queue_back_to_back_on_two_streams(small_batch):
+    """Two queue runs issued back to back from one thread on different streams, without a synchronise in
+    between: each call's finished-count polling state is its own, so neither sees the other's count."""
+    import torch
+
+    from hpmpc_amd.batch import BatchSolver
+
+    s = BatchSolver(small_batch, k_max=50)
+    s.ipm()
+    torch.cuda.synchronize()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    Q1, Q2 = s.queue(97, 16), s.queue(131, 32)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s1):
+        Q1.run()
+    with torch.cuda.stream(s2):
+        Q2.run()
+    torch.cuda.synchronize()
+    _queue_equals_batch(s, Q1, 97)
+    _queue_equals_batch(s, Q2, 131)
 
 
 def test_queue_unconstrained_entries_finish_at_init():
