@@ -35,6 +35,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
+BASELINE_METRIC = "Riccati factorisations/sec + IP iters/sec, fp64, N=100 nx=12 nu=4 batch=1024"  # BASELINE.json
 PEAK_FP64_TFS = 78.6   # MI355X fp64 (vector = MFMA dense)
 
 
@@ -58,7 +59,45 @@ def parse():
     ap.add_argument("--pcond-batch", type=int, default=512)
     ap.add_argument("--no-isolated", action="store_true", help="skip the isolated single-batch solve (profiling "
                     "runs: then every hk_ipm_* launch of the command belongs to the timed queue)")
+    ap.add_argument("--global-batch", type=int, default=0, help="fixed total problems split over the ranks "
+                    "(strong scaling, e.g. configs[3]: 4096 over 8 GPUs = 512 per GPU); default: --batch per GPU "
+                    "(weak scaling)")
+    ap.add_argument("--no-scatter", action="store_true", help="skip the rank-0 scatter / gather leg (N > 1)")
+    ap.add_argument("--no-queue-batch-slots", action="store_true", help="skip the queue run with one slot per "
+                    "problem of the batch")
+    ap.add_argument("--check-launch", action="store_true", help="start the ranks, join the process group (gloo) "
+                    "and print each rank's world size, without touching the GPU (launcher test)")
     return ap.parse_args()
+
+
+def launch_ranks(args):
+    """--gpus N > 1 outside a torch.distributed launcher: run this script under torch.distributed.run with N
+    ranks as a child process (nothing here has touched the GPU) and exit with its code."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd))
+
+
+def host_cpu():
+    """Host CPU model and logical CPU count (the lscpu facts SURVEY.md §8d asks for beside the baseline)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"model": model, "nproc": os.cpu_count(),
+            "affinity": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None}
 
 
 def cpu_baseline(qp, seconds, k_max, threads):
@@ -107,7 +146,7 @@ def cpu_baseline(qp, seconds, k_max, threads):
 
     v1, it1, s1, e1 = run(1, seconds * 0.3)
     vn, itn, sn, en = run(threads, seconds * 0.7)
-    return {"value": vn, "unit": "IP-iter/s", "cores": threads, "kind": kind,
+    return {"value": vn, "unit": "IP-iter/s", "cores": threads, "kind": kind, "host": host_cpu(),
             "sample": f"first {nprob} problems of the benchmark batch, cold-start d_ip2_res_mpc_hard_tv "
                       f"(k_max={k_max}) cycled by {threads} host threads for {en:.1f} s ({sn} solves, {itn} IP "
                       f"iterations); pre-marshalled ctypes calls",
@@ -153,7 +192,7 @@ def cpu_pcond_baseline(qp, N2, seconds, threads):
 
     v1, n1 = run(1, seconds * 0.3)
     vn, nn = run(threads, seconds * 0.7)
-    return {"value": vn, "unit": "solves/s", "cores": threads, "kind": kind,
+    return {"value": vn, "unit": "solves/s", "cores": threads, "kind": kind, "host": host_cpu(),
             "sample": f"{len(calls)} problems of the configs[4] batch, d_part_cond + condensed "
                       f"d_back_ric_rec_sv_tv_res + d_part_expand_solution, pre-marshalled ctypes calls, {threads} host threads "
                       f"({nn} pipelines) and 1 thread ({n1}); the reference c99 condensing is numerically wrong "
@@ -270,31 +309,96 @@ def bench_riccati_small(args, torch, red, rank, world, barrier, stream):
                                           "unit": "GB/s", "frac": ach / PEAK_HBM_GBS, "algorithmic_bytes_per_sv": by}}
 
 
+def bench_scatter(args, torch, dist, rank, world, solver, template, B, barrier):
+    """configs[3]'s data path (SURVEY.md §8e scatter mode): rank 0 holds every rank's block in HBM and sends
+    it over RCCL point-to-point (xGMI), each rank solves its block through the problem queue, and ux / pi /
+    kk / ret come back to rank 0.  Times the scatter, the solve and the gather separately (max over ranks)."""
+    from hpmpc_amd.batch import pack_batch
+    from hpmpc_amd.shard import gather_to_root, make_shard, scatter_from_root
+
+    N, nx, nu = args.N, args.nx, args.nu
+    local = [solver.BAbt, solver.RSQrq, solver.d]
+    blocks = None
+    if rank == 0:
+        blocks = [[torch.from_numpy(a).cuda() for a in pack_batch(make_shard(N, nx, nu, r, world, B))]
+                  for r in range(world)]
+    ref = [t.clone() for t in local]  # the seed-mode block of this rank: the scatter must reproduce it
+    for t in local:
+        t.zero_()
+    red = solver._red
+
+    def timed(fn):
+        barrier()
+        t0 = time.perf_counter()
+        out = fn()
+        barrier()
+        return red.max(time.perf_counter() - t0), out
+
+    t_sc, _ = timed(lambda: scatter_from_root(dist, rank, world, local, blocks))
+    same = all(torch.equal(a, b) for a, b in zip(local, ref))
+    del blocks, ref
+    Q = solver.queue(B, 2 * B)
+    t_solve, _ = timed(lambda: Q.run())
+    res = [Q.ux, Q.pi, Q.kk, Q.ret]
+    t_ga, got = timed(lambda: gather_to_root(dist, rank, world, res))
+    iters = red.sum(float(Q.kk.sum().item()))
+    out = {"scatter_ms": t_sc * 1e3, "solve_ms": t_solve * 1e3, "gather_ms": t_ga * 1e3,
+           "scattered_bytes_per_rank": int(sum(t.numel() * t.element_size() for t in local)),
+           "gathered_bytes_per_rank": int(sum(t.numel() * t.element_size() for t in res)),
+           "scatter_matches_seed_block": bool(red.min(1.0 if same else 0.0) == 1.0),
+           "value_with_scatter_gather": iters / (t_sc + t_solve + t_ga), "value_solve_only": iters / t_solve,
+           "unit": "IP-iter/s", "note": "one batch per rank; value_* over all ranks"}
+    if rank == 0:
+        out["gathered_iters"] = int(sum(int(g[2].sum().item()) for g in got))
+    return out
+
+
 def main():
     args = parse()
-    import torch
-
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        launch_ranks(args)  # does not return
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: rank {rank}: WORLD_SIZE={world} but --gpus {args.gpus}; using the launcher's "
+              f"world size", file=sys.stderr)
+    if args.check_launch:
+        import torch.distributed as cdist
+
+        if world > 1:
+            cdist.init_process_group("gloo")
+        print(json.dumps({"rank": rank, "world": cdist.get_world_size() if world > 1 else 1}), flush=True)
+        if world > 1:
+            cdist.destroy_process_group()
+        return
+    import torch
+
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
         dist.init_process_group("nccl")
+    print(f"bench.py: rank {rank} of world {world} on cuda:{local}", file=sys.stderr, flush=True)
 
     from hpmpc_amd.batch import (BatchSolver, algorithmic_bytes_per_fact, algorithmic_bytes_per_ip_iter,
                                  algorithmic_bytes_per_sv, flops_ip_iter, flops_sv)
     from hpmpc_amd.shard import Reducer, make_shard
 
+    from hpmpc_amd.shard import split_batch
+
     B, N, nx, nu = args.batch, args.N, args.nx, args.nu
+    strong = args.global_batch > 0
+    if strong:
+        B = split_batch(args.global_batch, world)
     qp = make_shard(N, nx, nu, rank, world, B)
     solver = BatchSolver(qp, k_max=args.k_max)
     qp_ric = make_shard(N, nx, nu, rank, world, B, boxes=False)
     ric = BatchSolver(qp_ric, k_max=1)
     stream = torch.cuda.current_stream()
     red = Reducer(dist, "cuda")
+    solver._red = red
 
     def barrier():
         torch.cuda.synchronize()
@@ -338,6 +442,20 @@ def main():
     ipm_ms = float(pass_ms.sum())
     fl_iter = flops_ip_iter(N, nx, nu)
     del Q
+
+    # the same K batches through a queue with one resident slot per problem of the batch (B slots: the
+    # metric's literal batch resident at once), beside the headline's 2 x B slots
+    qb = None
+    if not args.no_queue_batch_slots and slots != B:
+        Q = solver.queue(args.steps * B, B)
+        barrier()
+        q0 = time.perf_counter()
+        Q.run()
+        barrier()
+        qdt = max_over_ranks(time.perf_counter() - q0)
+        qb = {"slots": B, "value": sum_over_ranks(float(Q.kk.sum().item())) / qdt, "unit": "IP-iter/s",
+              "ms_per_step": qdt / args.steps * 1e3}
+        del Q
 
     # one isolated batch (no queue): the latency of a batch solve, reported beside the queue rate
     iso = None
@@ -385,6 +503,9 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(qp, args.cpu_seconds, args.k_max, args.cpu_threads)
 
+    sc = None
+    if world > 1 and not args.no_scatter:
+        sc = bench_scatter(args, torch, dist, rank, world, solver, qp, B, barrier)
     pc = None if args.no_pcond else bench_pcond(args, torch, red, rank, world, barrier)
     # configs[2] and configs[1]; skipped in profiling runs so every hk_ipm_* launch belongs to the timed queue
     rs = None if args.no_isolated else bench_riccati_small(args, torch, red, rank, world, barrier, stream)
@@ -392,8 +513,7 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": "IP iterations/sec (Riccati-based IPM, d_ip2_res_mpc_hard_tv), fp64, N=100 nx=12 nu=4 "
-                      "batch=1024 per GPU",
+            "metric": BASELINE_METRIC,
             "value": value,
             "unit": "IP-iter/s",
             "n_gpus": world,
@@ -401,16 +521,19 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (mass-spring MPC, per-problem x0 ~ U(-2.5,2.5) from PCG64(20261015+p), time-variant "
-                    "A/B/Q perturbations; generated on each rank, no scatter)",
+                    "A/B/Q perturbations; each rank generates its block (seed mode); the rank-0 scatter / gather of "
+                    "the same blocks is timed separately in 'scatter')",
             "config": {"workload": f"ipm_N{N}_nx{nx}_nu{nu}_batch{B}", "N": N, "nx": nx, "nu": nu,
                        "batch_per_gpu": B, "global_batch": B * world, "k_max": args.k_max, "mu_tol": 1e-12,
                        "parallelism": f"dp{world}" if world > 1 else "single",
-                       "schedule": f"problem queue: {args.steps} batches per rank through {slots} resident "
-                                   f"slots (hpmpc_mi355x_ipm_queue)",
+                       "resident_slots": slots,
+                       "schedule": f"problem queue: {args.steps} batches of {B} per rank through {slots} resident "
+                                   f"slots (hpmpc_mi355x_ipm_queue); 'queue_batch_slots' is the same run with "
+                                   f"{B} slots",
                        "sum_kk_per_step": iters_total / args.steps, "ret_counts": {
                            str(int(r)): int((ret == r).sum()) for r in np.unique(ret)}},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
@@ -422,7 +545,9 @@ def main():
                          "ipm_whole_solve": {"achieved_GBps": iters_rank * bytes_iter / (ipm_ms * 1e-3) / 1e9,
                                              "algorithmic_bytes_per_ip_iter": bytes_iter,
                                              "fp64_tflops": iters_rank * fl_iter / (ipm_ms * 1e-3) / 1e12}},
+            "queue_batch_slots": qb,
             "isolated_batch": iso,
+            "scatter": sc,
             "riccati": {"value": fact_total / rdt, "unit": "fact/s", "kernel": "hk_ric_sv", "launch_ms": sv_ms,
                         "roofline": {"bound": "hbm", "achieved": sv_achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                                      "frac": sv_achieved / PEAK_HBM_GBS,

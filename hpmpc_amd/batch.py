@@ -69,19 +69,67 @@ class _Layout(C.Structure):
                 ("BAbt_off", C.POINTER(C.c_longlong)), ("RSQrq_off", C.POINTER(C.c_longlong))]
 
 
-class BatchSolver:
-    """Device-resident batch of OCP QPs + the batched HPMPC entry points."""
+def stage_offsets(qp: OCPQP):
+    """Offsets (doubles) of every stage block inside one problem's packed BAbt / RSQrq arrays, and the
+    packed lengths: stage k of BAbt at offB[k], of RSQrq at offR[k] (the reference's lib4 blocks, unchanged)."""
+    N = qp.N
+    offB = np.zeros(N, dtype=np.int64)
+    offR = np.zeros(N + 1, dtype=np.int64)
+    o = 0
+    for k in range(N):
+        offB[k] = o
+        o += qp.BAbt[k].shape[-1]
+    packB = o
+    o = 0
+    for k in range(N + 1):
+        offR[k] = o
+        o += qp.RSQrq[k].shape[-1]
+    return offB, offR, packB, o
 
-    def __init__(self, qp: OCPQP, device="cuda", k_max: int = 50):
+
+def pack_batch(qp: OCPQP):
+    """Problem-major host arrays of a batched OCPQP: BAbt (nprob, packB), RSQrq (nprob, packR), d (nprob, N+1, 32)
+    -- the layout BatchSolver keeps in HBM and hpmpc_amd.shard scatters."""
+    N = qp.N
+    hB = np.ascontiguousarray(np.concatenate([a for a in qp.BAbt], axis=1))
+    hR = np.ascontiguousarray(np.concatenate([a for a in qp.RSQrq], axis=1))
+    hd = np.zeros((qp.batch, N + 1, 32))
+    for k in range(N + 1):
+        n = qp.d[k].shape[1]
+        hd[:, k, :n] = qp.d[k]
+    return hB, hR, hd
+
+
+def unpack_batch(template: OCPQP, hB, hR, hd) -> OCPQP:
+    """Inverse of pack_batch: the batched OCPQP whose stage sizes / idxb are the template's and whose data are
+    the packed arrays (numpy or CPU tensors)."""
+    hB, hR, hd = (np.asarray(x) for x in (hB, hR, hd))
+    offB, offR, _, _ = stage_offsets(template)
+    N = template.N
+    BAbt = [hB[:, offB[k]:offB[k] + template.BAbt[k].shape[-1]].copy() for k in range(N)]
+    RSQrq = [hR[:, offR[k]:offR[k] + template.RSQrq[k].shape[-1]].copy() for k in range(N + 1)]
+    d = [hd[:, k, :template.d[k].shape[-1]].copy() for k in range(N + 1)]
+    return OCPQP(N, template.nx.copy(), template.nu.copy(), template.nb.copy(), template.ng.copy(),
+                 [i.copy() for i in template.idxb], BAbt, RSQrq, d, [], hB.shape[0])
+
+
+class BatchSolver:
+    """Device-resident batch of OCP QPs + the batched HPMPC entry points.
+
+    ``nprob`` given: the batch's data are not uploaded from ``qp`` (which then only supplies stage sizes and
+    idxb); BAbt / RSQrq / d are allocated for ``nprob`` problems and filled by the caller, e.g. by the rank-0
+    scatter of hpmpc_amd.shard."""
+
+    def __init__(self, qp: OCPQP, device="cuda", k_max: int = 50, nprob: int | None = None):
         import torch
 
         if not torch.cuda.is_available():
             raise RuntimeError("BatchSolver needs a GPU (HIP device); there is no CPU fallback")
-        assert qp.batch is not None, "BatchSolver takes a batched OCPQP"
+        assert nprob is not None or qp.batch is not None, "BatchSolver takes a batched OCPQP"
         self.torch = torch
         self.qp = qp
         self.N = N = qp.N
-        self.nprob = qp.batch
+        self.nprob = qp.batch if nprob is None else int(nprob)
         self.k_max = k_max
         self.dev = torch.device(device)
         L = lib()
@@ -97,32 +145,21 @@ class BatchSolver:
         if not self.plan:
             raise ValueError(f"unsupported problem sizes for the GPU path (code {L.hpmpc_mi355x_last_error()})")
         # problem-major packed inputs
-        offB = np.zeros(N, dtype=np.int64)
-        offR = np.zeros(N + 1, dtype=np.int64)
-        o = 0
-        for k in range(N):
-            offB[k] = o
-            o += qp.BAbt[k].shape[1]
-        packB = o
-        o = 0
-        for k in range(N + 1):
-            offR[k] = o
-            o += qp.RSQrq[k].shape[1]
-        packR = o
+        offB, offR, packB, packR = stage_offsets(qp)
         self.offB, self.offR = offB, offR
         self.layout = _Layout(packB, packR, offB.ctypes.data_as(C.POINTER(C.c_longlong)),
                               offR.ctypes.data_as(C.POINTER(C.c_longlong)))
-        hB = np.concatenate([a for a in qp.BAbt], axis=1)
-        hR = np.concatenate([a for a in qp.RSQrq], axis=1)
-        hd = np.zeros((self.nprob, N + 1, 32))
-        for k in range(N + 1):
-            n = qp.d[k].shape[1]
-            hd[:, k, :n] = qp.d[k]
         f64 = torch.float64
-        self.BAbt = torch.from_numpy(hB).to(self.dev)
-        self.RSQrq = torch.from_numpy(hR).to(self.dev)
-        self.d = torch.from_numpy(hd).to(self.dev)
         P = self.nprob
+        if nprob is None:
+            hB, hR, hd = pack_batch(qp)
+            self.BAbt = torch.from_numpy(hB).to(self.dev)
+            self.RSQrq = torch.from_numpy(hR).to(self.dev)
+            self.d = torch.from_numpy(hd).to(self.dev)
+        else:
+            self.BAbt = torch.zeros((P, packB), dtype=f64, device=self.dev)
+            self.RSQrq = torch.zeros((P, packR), dtype=f64, device=self.dev)
+            self.d = torch.zeros((P, N + 1, 32), dtype=f64, device=self.dev)
         self.ux = torch.zeros((P, N + 1, 16), dtype=f64, device=self.dev)
         self.pi = torch.zeros((P, N + 1, 16), dtype=f64, device=self.dev)
         self.lam = torch.zeros((P, N + 1, 32), dtype=f64, device=self.dev)

@@ -1,14 +1,68 @@
 """Data-parallel sharding of a batch of independent QPs over ranks.
 
 Problems are independent, so a solve has no exchange step: each rank owns a contiguous block of the
-global batch, generates that block itself from the global per-problem seeds (no scatter), and the
-only collectives are the barrier and two scalar reductions (max of elapsed time, sum of iteration
+global batch.  Two ways to get a block onto its rank:
+
+* seed mode -- every rank generates its own block from the global per-problem seeds (no data-path
+  collective at all);
+* scatter mode -- rank 0 holds the whole batch and sends each rank its block with point-to-point sends
+  (one batched isend/irecv group: over xGMI every rank-0 -> rank-r transfer has its own link), and the
+  results (ux, pi, kk, ret) come back to rank 0 the same way (gather_to_root).
+
+The timing collectives are the barrier and two scalar reductions (max of elapsed time, sum of iteration
 counts).  The same code runs over RCCL (backend "nccl", device tensors) on the GPU box and over gloo
 (CPU tensors) in the multi-process CPU tests.
 """
 from __future__ import annotations
 
 from .ocp import OCPQP, batch_x0, mass_spring_qp
+
+
+def split_batch(global_batch: int, world: int) -> int:
+    """Problems per rank for a fixed global batch (strong scaling): contiguous equal blocks."""
+    if global_batch <= 0 or global_batch % world:
+        raise ValueError(f"global batch {global_batch} does not split evenly over {world} ranks")
+    return global_batch // world
+
+
+def scatter_from_root(dist, rank: int, world: int, local, blocks=None):
+    """Rank 0 sends blocks[r] (a list of tensors) to rank r and copies blocks[0] into its own `local`;
+    every other rank receives into `local` (preallocated tensors of the same shapes and dtypes).  One
+    batch_isend_irecv group, so rank 0's sends to different ranks proceed concurrently."""
+    if world == 1 or dist is None:
+        if blocks is not None:
+            for dst, src in zip(local, blocks[0]):
+                dst.copy_(src)
+        return
+    ops = []
+    if rank == 0:
+        assert blocks is not None and len(blocks) == world
+        for r in range(1, world):
+            assert len(blocks[r]) == len(local)
+            ops += [dist.P2POp(dist.isend, t.contiguous(), r) for t in blocks[r]]
+        for dst, src in zip(local, blocks[0]):
+            dst.copy_(src)
+    else:
+        ops = [dist.P2POp(dist.irecv, t, 0) for t in local]
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+
+
+def gather_to_root(dist, rank: int, world: int, local):
+    """The inverse of scatter_from_root: rank 0 returns [local of rank 0, ..., of rank world-1] (fresh
+    tensors for the remote ranks), the others send theirs and return None."""
+    if world == 1 or dist is None:
+        return [list(local)]
+    if rank == 0:
+        out = [list(local)] + [[t.new_empty(t.shape) for t in local] for _ in range(1, world)]
+        ops = [dist.P2POp(dist.irecv, out[r][i], r) for r in range(1, world) for i in range(len(local))]
+    else:
+        out = None
+        ops = [dist.P2POp(dist.isend, t.contiguous(), 0) for t in local]
+    for req in dist.batch_isend_irecv(ops):
+        req.wait()
+    return out
 
 
 def shard_range(rank: int, world: int, per_rank: int) -> tuple[int, int]:
@@ -50,6 +104,9 @@ class Reducer:
 
     def max(self, x: float) -> float:
         return self._all_reduce(x, None if self.dist is None else self.dist.ReduceOp.MAX)
+
+    def min(self, x: float) -> float:
+        return self._all_reduce(x, None if self.dist is None else self.dist.ReduceOp.MIN)
 
     def sum(self, x: float) -> float:
         return self._all_reduce(x, None if self.dist is None else self.dist.ReduceOp.SUM)

@@ -157,13 +157,19 @@ def test_batch_ipm_vs_oracle(oracle, small_batch):
     torch.cuda.synchronize()
     kk, ret = s.kk.cpu().numpy(), s.ret.cpu().numpy()
     ux, pi, lam, t = (x.cpu().numpy() for x in (s.ux, s.pi, s.lam, s.t))
+    from helpers import DIVERGENT_SKIPS
+
+    skips0 = len(DIVERGENT_SKIPS)
     for p in range(qp.batch):
         one = qp.problem(p)
         r = oracle.ipm(one, k_max=50)
         got = dict(kk=int(kk[p]), ret=int(ret[p]), ux=[ux[p, k] for k in range(31)],
                    pi=[pi[p, k] for k in range(30)], lam=[lam[p, k] for k in range(31)],
                    t=[t[p, k] for k in range(31)])
-        compare_ipm(one, got, r)
+        # infeasible draws of x0 diverge (ret 2, lam -> 1e33) in the oracle and on the GPU alike: kk/ret only
+        compare_ipm(one, got, r, allow_divergent=True)
+    n_div = len(DIVERGENT_SKIPS) - skips0
+    assert n_div <= int((ret == 2).sum()) and n_div <= qp.batch // 8, n_div
 
 
 def test_batch_riccati_vs_oracle(oracle):

@@ -71,3 +71,88 @@ def test_gloo_world2_matches_single_process():
         assert out[r][1] == float(WORLD)
     # rank blocks differ (global x0 seeds), i.e. ranks did not solve the same problems
     assert not np.allclose(out[0][2], out[1][2])
+
+
+# ---------------------------------------------------------------- scatter mode
+def _solve_block(qp):
+    """Solve a received block problem by problem; pack the results like the device API's outputs."""
+    import torch
+
+    res = _solve(qp)
+    B, N = qp.batch, qp.N
+    ux = torch.zeros((B, N + 1, 16), dtype=torch.float64)
+    pi = torch.zeros((B, N + 1, 16), dtype=torch.float64)
+    kk = torch.zeros(B, dtype=torch.int32)
+    ret = torch.zeros(B, dtype=torch.int32)
+    for p, r in enumerate(res):
+        for k in range(N + 1):
+            n = qp.nux(k)
+            ux[p, k, :n] = torch.from_numpy(np.asarray(r["ux"][k][:n]))
+            if k < N:
+                m = int(qp.nx[k + 1])
+                pi[p, k, :m] = torch.from_numpy(np.asarray(r["pi"][k][:m]))
+        kk[p], ret[p] = r["kk"], r["ret"]
+    return [ux, pi, kk, ret]
+
+
+def _scatter_worker(rank, port, out):
+    import torch
+    import torch.distributed as dist
+
+    from hpmpc_amd.batch import pack_batch, unpack_batch
+    from hpmpc_amd.ocp import mass_spring_qp
+    from hpmpc_amd.shard import gather_to_root, scatter_from_root
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    template = mass_spring_qp(N, NX, NU)  # sizes and idxb only: every rank knows the problem class
+    shapes = [a.shape[1:] for a in pack_batch(make_shard(N, NX, NU, 0, 1, 1))]
+    local = [torch.zeros((PER_RANK,) + tuple(s), dtype=torch.float64) for s in shapes]
+    blocks = None
+    if rank == 0:  # rank 0 holds the whole global batch, block r for rank r
+        blocks = [[torch.from_numpy(a) for a in pack_batch(make_shard(N, NX, NU, r, WORLD, PER_RANK))]
+                  for r in range(WORLD)]
+    scatter_from_root(dist, rank, WORLD, local, blocks)
+    qp = unpack_batch(template, *local)
+    got = gather_to_root(dist, rank, WORLD, _solve_block(qp))
+    if rank == 0:
+        out["res"] = [[t.numpy().copy() for t in g] for g in got]
+    out[rank] = [t.numpy().copy() for t in local]
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_scatter_solve_gather_matches_single_process():
+    """Rank 0 scatters the blocks of the global batch, each rank solves its block, the results are
+    gathered on rank 0: bit for bit what one process solving every block produces."""
+    if not os.path.exists(os.path.join(ROOT, "oracle", "liboracle.so")):
+        pytest.skip("oracle not built")
+    from hpmpc_amd.batch import pack_batch
+
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_scatter_worker, args=(port, out), nprocs=WORLD, join=True)
+        out = dict(out)
+    for r in range(WORLD):
+        blk = make_shard(N, NX, NU, r, WORLD, PER_RANK)
+        # the scattered data are the rank's block, unchanged
+        for a, b in zip(out[r], pack_batch(blk)):
+            np.testing.assert_array_equal(a, b)
+        ref = [t.numpy() for t in _solve_block(blk)]
+        for a, b in zip(out["res"][r], ref):
+            np.testing.assert_array_equal(a, b)
+    assert not np.array_equal(out["res"][0][0], out["res"][1][0])
+
+
+def test_bench_launches_world2_ranks():
+    """`bench.py --gpus 2` starts two ranks (torch.distributed.run child) that reach init_process_group
+    with world size 2 before any GPU call (--check-launch: gloo, no device)."""
+    import json
+    import subprocess
+    import sys
+
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--check-launch"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert sorted(x["rank"] for x in lines) == [0, 1] and all(x["world"] == 2 for x in lines), lines
