@@ -14,8 +14,9 @@ CSRC = os.path.join(ROOT, "hpmpc_amd", "csrc")
 LIBDIR = os.path.join(ROOT, "hpmpc_amd", "lib")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("HPMPC_ARCH", "gfx950")
-SOURCES = ["hpmpc_kernels.hip", "hk_wide.hip", "hk_soft.hip", "hpmpc_capi.cpp", "hpmpc_capi_wide.cpp", "hpmpc_capi_iface.cpp"]
-HEADERS = ["hk_prims.h", "hk_riccati.h", "hk_ipm.h", "hpmpc_kargs.h", "hk_wide_args.h", "hk_soft_args.h"]
+SOURCES = ["hpmpc_kernels.hip", "hk_wide.hip", "hk_wide_ipm.hip", "hk_soft.hip", "hpmpc_capi.cpp", "hpmpc_capi_wide.cpp",
+           "hpmpc_capi_wide_ipm.cpp", "hpmpc_capi_iface.cpp"]
+HEADERS = ["hk_prims.h", "hk_riccati.h", "hk_ipm.h", "hpmpc_kargs.h", "hk_wide_args.h", "hk_wide_core.h", "hk_wide_host.h", "hk_soft_args.h"]
 # MFMA accumulators stay in ordinary VGPRs: the stage tile is read and written by VALU code between
 # MFMAs, and the AGPR form costs 8 v_accvgpr moves each way per MFMA group.
 KFLAGS = ["-mllvm", "-amdgpu-mfma-vgpr-form"] + os.environ.get("HK_EXTRA_FLAGS", "").split()
@@ -29,16 +30,31 @@ def _newer(out, deps):
 
 
 def build_hip(force: bool = False, verbose: bool = False) -> str:
+    """Each source compiles to its own object under build/ (rebuilt when it or a header is newer), then one
+    link; a one-file change recompiles one translation unit."""
     os.makedirs(LIBDIR, exist_ok=True)
+    objdir = os.path.join(ROOT, "build", "obj")
+    os.makedirs(objdir, exist_ok=True)
     out = os.path.join(LIBDIR, "libhpmpc_mi355x.so")
-    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [os.path.join(ROOT, "include", "hpmpc_mi355x.h")]
-    if not force and _newer(out, deps):
-        return out
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           "-Wno-unused-function"] + KFLAGS + [os.path.join(CSRC, s) for s in SOURCES] + ["-o", out]
-    if verbose:
-        print(" ".join(cmd), flush=True)
-    subprocess.run(cmd, check=True)
+    hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, "include", "hpmpc_mi355x.h")]
+    common = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function"] + KFLAGS
+    objs, procs = [], []
+    for src in SOURCES:
+        obj = os.path.join(objdir, src + ".o")
+        objs.append(obj)
+        if force or not _newer(obj, [os.path.join(CSRC, src)] + hdrs):
+            cmd = common + ["-c", os.path.join(CSRC, src), "-o", obj]
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            procs.append((src, subprocess.Popen(cmd)))
+    for src, pr in procs:
+        if pr.wait() != 0:
+            raise subprocess.CalledProcessError(pr.returncode, src)
+    if procs or force or not _newer(out, objs):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC"] + objs + ["-o", out]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
     return out
 
 

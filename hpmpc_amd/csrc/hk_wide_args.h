@@ -14,7 +14,8 @@ struct WideStage {
     int oL;                // factor of stage k in ws: packed lower columns (nux+1 rows) then 1/diag (nux)
     int oU, oP;            // ux_k / pi_k (and Pb_k) in the problem's solution vectors
     int nb, pnb, oD, oI;   // boxes: count, padded count, d_k offset, idxb_k offset (ints)
-    int ng;                // general constraints (wide Riccati: 0)
+    int ng;                // general constraints
+    int oG, sdG;           // DCt_k (lib4, nux x ng, panel stride round_up(ng, 2)) in the problem's DCt array
 };
 
 struct WideArgs {
@@ -37,6 +38,14 @@ struct WideArgs {
     const double *hb, *hq, *qx;
     const int* idxb;
     long long sC;
+    // optional device-side terms of hk_wide_sv (the drop-in path applies them on the host instead):
+    //   vb / vq: b_k / q_k from vectors (offsets oP / oU) instead of the augmented rows of BAbt_k / RSQrq_k;
+    //   Qx (with qx): box terms diag[idxb] += Qx, row[idxb] += qx (dev_box), and the general terms
+    //   DCt diag(Qx_g) DCt' / DCt qx_g, in the reference's [box (pnb) | general (png)] layout at offset oD;
+    //   DCt: the general-constraint blocks (offsets oG, stride sG).  hk_wide_trs adds DCt qx_g when DCt is set.
+    const double *vb, *vq, *Qx, *DCt;
+    long long sG;
+    int dev_box;  // hk_wide_sv: box terms from Qx / qx at idxb (else pre-applied in the staged RSQrq)
 };
 
 // Partial condensing (d_part_cond): one workgroup per (block ii, problem p).
@@ -84,4 +93,51 @@ struct PxArgs {
     long long sU2, sP2, sC2;
     double *ux, *pi, *lam, *t;
     int offB, offR, offV, offW, offQ, ldT;  // dynamic LDS carve: BAbt tile, RSQrq tile, ux_j, box terms, pi_j
+};
+
+// ------------------------------------------------------------------------------------------------
+// The IPM on wide stages (hk_wide_ipm.hip): one workgroup runs a whole solve of one problem.
+// ------------------------------------------------------------------------------------------------
+// One constraint pair (lower / upper) of a problem's flattened constraint list (shared by the batch).
+struct WideCSlot {
+    int lo, up;  // its lower / upper slot in the constraint vectors ([lb | ub | lg | ug] at stage offset oD)
+    int q;       // its Qx / qx entry ([box (pnb) | general (png)] at stage offset oD)
+    int var;     // box: offset of its variable in ux (>= 0); general: -1 - stage
+    int g;       // general: constraint index in the stage (column of DCt_k)
+};
+
+enum {
+    WI_IPM_RES = 0,    // d_ip2_res_mpc_hard_tv            (mpc_solvers/d_ip2_res_hard.c:116-1345)
+    WI_IPM_P1 = 1,     // d_ip2_mpc_hard_tv                (mpc_solvers/d_ip2_hard.c:88-614)
+    WI_NEWTON = 2,     // d_ip2_res_mpc_hard_tv_single_newton_step (d_ip2_res_hard.c:1348-1919)
+    WI_KKT_RES = 3,    // d_kkt_solve_new_rhs_res_mpc_hard_tv (d_ip2_res_hard.c:1922-2299)
+    WI_KKT_P1 = 4,     // d_kkt_solve_new_rhs_mpc_hard_tv  (d_ip2_hard.c:626-825)
+    WI_RES = 5,        // d_res_res_mpc_hard_tv            (mpc_solvers/c99/d_res_ip_res_hard.c:39-319)
+    WI_RES_PLAIN = 6,  // d_res_mpc_hard_tv                (mpc_solvers/d_res_ip_hard.c:38-330)
+};
+
+struct WideIpmArgs {
+    WideArgs w;  // stage table, LDS carve, BAbt / RSQ / DCt (+ strides), idxb; its vector slots are unused
+    int mode, k_max, warm_start, compute_mult;
+    double mu0, mu_tol, alpha_min;
+    double mu_scal;  // 1 / (2 sum(nb + ng)); 0 without constraints
+    double nbt2;     // 2 sum(nb + ng) (the residual routines divide by it)
+    int ncs;
+    const WideCSlot* cs;
+    const int* vbox;  // per ux entry: lo slot of the box on that variable, -1 if none (problem-relative)
+    int nU, nP;       // per-problem vector lengths (ux / pi layouts)
+    const double* d;  // bounds (or r_C of the phase-1 KKT re-solve), stride sC
+    double *ux, *pi, *lam, *t;  // iterate: strides w.sU, w.sP, sC
+    long long sC;
+    const double *vb, *vq;  // b / q vectors of the KKT re-solves and the residual routines (strides w.sP / w.sU)
+    double* iw;             // per-problem work image (stride sI), offsets below
+    long long sI;
+    int oF, oDux, oDpi, oPb, oRq, oRb, oUb, oPib;
+    int oDlam, oDt, oTinv, oLamt, oRd, oRm, oTb, oLb, oQx, oqx;
+    double* stat;  // 5 * k_max per problem (stride sS)
+    long long sS;
+    int* kk;       // per problem: kk, return code
+    int* ret;
+    double* mu;    // per problem: final mu (residual routines: in / out)
+    int offR;      // LDS reduction scratch (8 doubles) after the Riccati carve
 };

@@ -22,20 +22,34 @@
 
 #include "../../include/hpmpc_mi355x.h"
 #include "hpmpc_kargs.h"
+#include "hk_wide_args.h"
 
 extern "C" int hk_launch(int which, const KArgs* a, int count, hipStream_t stream);
 extern "C" int hk_fixcls(int nu, int nx);
-// wide-stage path (hpmpc_capi_wide.cpp)
+// wide-stage path (hpmpc_capi_wide.cpp, hpmpc_capi_wide_ipm.cpp)
+extern "C" long long hk_wide_ipm_bytes(int N, const int* nx, const int* nu, const int* nb, const int* ng);
+extern "C" int hk_wide_ipm_entry(int mode, int* kk, int k_max, double mu0, double mu_tol, double alpha_min,
+                                 int warm_start, double* stat, int N, int* nx, int* nu_N, int* nb, int** idxb, int* ng,
+                                 double** pBAbt, double** pQ, double** pDCt, double** d, double** ux,
+                                 int compute_mult, double** pi, double** lam, double** t, double* work, double** ux0,
+                                 double** pi0, double** lam0, double** t0);
+extern "C" void hk_wide_kkt_entry(int p1, int N, int* nx, int* nu_N, int* nb, int** idxb, int* ng, double** pBAbt,
+                                  double** b, double** pQ, double** q, double** pDCt, double** d, double** ux,
+                                  int compute_mult, double** pi, double** lam, double** t, double* work);
+extern "C" void hk_wide_res_entry(int plain, int N, int* nx, int* nu, int* nb, int** idxb, int* ng, double** hpBAbt,
+                                  double** hb, double** hpQ, double** hq, double** hux, double** hpDCt, double** hd,
+                                  double** hpi, double** hlam, double** ht, double** hrq, double** hrb, double** hrd,
+                                  double** hrm, double* mu);
 extern "C" long long hk_wide_factor_bytes(int N, const int* nx, const int* nu);
 extern "C" void hk_wide_sv_entry(int N, int* nx, int* nu, int* nb, int** idxb, int* ng, int update_b, double** hpBAbt,
-                                 double** b, int update_q, double** hpQ, double** q, double** bd, double** Qx,
-                                 double** qx, double** hux, int compute_pi, double** hpi, int compute_Pb, double** hPb,
-                                 double* memory);
+                                 double** b, int update_q, double** hpQ, double** q, double** bd, double** hpDCt,
+                                 double** Qx, double** qx, double** hux, int compute_pi, double** hpi, int compute_Pb,
+                                 double** hPb, double* memory);
 extern "C" void hk_wide_trf_entry(int N, int* nx, int* nu, int* nb, int** idxb, int* ng, double** hpBAbt,
-                                  double** hpQ, double** Qx, double** bd, double* memory);
+                                  double** hpQ, double** hpDCt, double** Qx, double** bd, double* memory);
 extern "C" void hk_wide_trs_entry(int N, int* nx, int* nu, int* nb, int** idxb, int* ng, double** hpBAbt,
-                                  double** hb, double** hq, double** qx, double** hux, int compute_pi, double** hpi,
-                                  int compute_Pb, double** hPb, double* memory);
+                                  double** hb, double** hq, double** hpDCt, double** qx, double** hux, int compute_pi,
+                                  double** hpi, int compute_Pb, double** hPb, double* memory);
 
 namespace {
 
@@ -805,7 +819,7 @@ extern "C" void d_back_ric_rec_sv_tv_res(int N, int* nx, int* nu, int* nb, int**
     {
         const char* why = nullptr;
         if (!plan_supported(N, nx, nu, nb, idxb, ng, &why)) {  // stages beyond the 16-wide tile
-            hk_wide_sv_entry(N, nx, nu, nb, idxb, ng, update_b, hpBAbt, b, update_q, hpQ, q, bd, Qx, qx, hux,
+            hk_wide_sv_entry(N, nx, nu, nb, idxb, ng, update_b, hpBAbt, b, update_q, hpQ, q, bd, hpDCt, Qx, qx, hux,
                              compute_pi, hpi, compute_Pb, hPb, memory);
             return;
         }
@@ -861,7 +875,7 @@ extern "C" void d_back_ric_rec_trf_tv_res(int N, int* nx, int* nu, int* nb, int*
     {
         const char* why = nullptr;
         if (!plan_supported(N, nx, nu, nb, idxb, ng, &why)) {  // stages beyond the 16-wide tile
-            hk_wide_trf_entry(N, nx, nu, nb, idxb, ng, hpBAbt, hpQ, Qx, bd, memory);
+            hk_wide_trf_entry(N, nx, nu, nb, idxb, ng, hpBAbt, hpQ, hpDCt, Qx, bd, memory);
             return;
         }
     }
@@ -899,7 +913,7 @@ extern "C" void d_back_ric_rec_trs_tv_res(int N, int* nx, int* nu, int* nb, int*
     {
         const char* why = nullptr;
         if (!plan_supported(N, nx, nu, nb, idxb, ng, &why)) {  // stages beyond the 16-wide tile
-            hk_wide_trs_entry(N, nx, nu, nb, idxb, ng, hpBAbt, hb, hq, qx, hux, compute_pi, hpi, compute_Pb,
+            hk_wide_trs_entry(N, nx, nu, nb, idxb, ng, hpBAbt, hb, hq, hpDCt, qx, hux, compute_pi, hpi, compute_Pb,
                               hPb, memory);
             return;
         }
@@ -936,12 +950,20 @@ extern "C" void d_back_ric_rec_trs_tv_res(int N, int* nx, int* nu, int* nb, int*
 }
 
 extern "C" int d_ip2_res_mpc_hard_tv_work_space_size_bytes(int N, int* nx, int* nu, int* nb, int* ng) {
-    (void)nx;
-    (void)nu;
-    (void)nb;
-    (void)ng;
-    return (int)((ws_doubles(N) * 8 + 63) / 64 * 64);
+    // the larger of the tile path's image and the wide-stage IPM's (problems beyond the tile run there)
+    std::vector<int> nuN(nu, nu + N + 1);
+    nuN[N] = 0;
+    const long long tile = ws_doubles(N) * 8, wide = hk_wide_ipm_bytes(N, nx, nuN.data(), nb, ng);
+    return (int)(((tile > wide ? tile : wide) + 63) / 64 * 64);
 }
+
+namespace {
+// stages beyond the 16-wide tile (or its 32 constraint slots) run on the wide-stage path
+bool wide_path(int N, const int* nx, const int* nu, const int* nb, int** idxb, const int* ng) {
+    const char* why = nullptr;
+    return !plan_supported(N, nx, nu, nb, idxb, ng, &why);
+}
+}  // namespace
 
 namespace {
 
@@ -952,6 +974,10 @@ int ipm_entry(int single_newton, int phase1_only, int* kk, int k_max, double mu0
               double** pDCt, double** d, double** ux, int compute_mult, double** pi, double** lam, double** t,
               double* double_work_memory, double** ux0, double** pi0, double** lam0, double** t0) {
     g_err = 0;
+    if (wide_path(N, nx, nu_N, nb, idxb, ng))
+        return hk_wide_ipm_entry(single_newton ? WI_NEWTON : phase1_only ? WI_IPM_P1 : WI_IPM_RES, kk, k_max, mu0,
+                                 mu_tol, alpha_min, warm_start, stat, N, nx, nu_N, nb, idxb, ng, pBAbt, pQ, pDCt, d, ux,
+                                 compute_mult, pi, lam, t, double_work_memory, ux0, pi0, lam0, t0);
     hpmpc_mi355x_plan* P = g_ctx.get_plan(N, nx, nu_N, nb, idxb, ng);
     if (!P) return g_err;
     if (single_newton && P->ngt) {  // the reference stops here too (d_aux_ip_hard_lib4.c:197-208)
@@ -1035,6 +1061,11 @@ extern "C" void d_kkt_solve_new_rhs_res_mpc_hard_tv(int N, int* nx, int* nu_N, i
                                                     double** pi, double** lam, double** t,
                                                     double* double_work_memory) {
     g_err = 0;
+    if (wide_path(N, nx, nu_N, nb, idxb, ng)) {
+        hk_wide_kkt_entry(0, N, nx, nu_N, nb, idxb, ng, pBAbt, b, pQ, q, pDCt, d, ux, compute_mult, pi, lam, t,
+                          double_work_memory);
+        return;
+    }
     hpmpc_mi355x_plan* P = g_ctx.get_plan(N, nx, nu_N, nb, idxb, ng);
     if (!P) return;
     Arena A = arena(P, 1);
@@ -1068,6 +1099,11 @@ extern "C" void d_res_res_mpc_hard_tv(int N, int* nx, int* nu, int* nb, int** id
                                       double** hrq, double** hrb, double** hrd, double** hrm, double* mu) {
     (void)work;
     g_err = 0;
+    if (wide_path(N, nx, nu, nb, idxb, ng)) {
+        hk_wide_res_entry(0, N, nx, nu, nb, idxb, ng, hpBAbt, hb, hpQ, hq, hux, hpDCt, hd, hpi, hlam, ht, hrq, hrb, hrd,
+                          hrm, mu);
+        return;
+    }
     hpmpc_mi355x_plan* P = g_ctx.get_plan(N, nx, nu, nb, idxb, ng);
     if (!P) return;
     Arena A = arena(P, 1);
@@ -1132,8 +1168,13 @@ extern "C" void d_kkt_solve_new_rhs_mpc_hard_tv(int N, int* nx, int* nu_N, int* 
                                                 double** pBAbt, double** r_A, double** pQ, double** r_H,
                                                 double** pDCt, double** r_C, double** ux, int compute_mult,
                                                 double** pi, double** lam, double** t, double* double_work_memory) {
-    (void)pQ;  // the factor of the IPM's last iteration is in the workspace
     g_err = 0;
+    if (wide_path(N, nx, nu_N, nb, idxb, ng)) {
+        hk_wide_kkt_entry(1, N, nx, nu_N, nb, idxb, ng, pBAbt, r_A, pQ, r_H, pDCt, r_C, ux, compute_mult, pi, lam, t,
+                          double_work_memory);
+        return;
+    }
+    (void)pQ;  // the factor of the IPM's last iteration is in the workspace
     hpmpc_mi355x_plan* P = g_ctx.get_plan(N, nx, nu_N, nb, idxb, ng);
     if (!P) return;
     Arena A = arena(P, 1);
@@ -1168,6 +1209,11 @@ extern "C" void d_res_mpc_hard_tv(int N, int* nx, int* nu, int* nb, int** idxb, 
                                   double** hpi, double** hlam, double** ht, double** hrq, double** hrb, double** hrd,
                                   double* mu) {
     g_err = 0;
+    if (wide_path(N, nx, nu, nb, idxb, ng)) {
+        hk_wide_res_entry(1, N, nx, nu, nb, idxb, ng, hpBAbt, hb, hpQ, hq, hux, hpDCt, hd, hpi, hlam, ht, hrq, hrb, hrd,
+                          nullptr, mu);
+        return;
+    }
     hpmpc_mi355x_plan* P = g_ctx.get_plan(N, nx, nu, nb, idxb, ng);
     if (!P) return;
     Arena A = arena(P, 1);

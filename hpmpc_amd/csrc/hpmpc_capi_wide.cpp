@@ -5,160 +5,8 @@
 //     (lqcp_solvers/d_part_cond.c:694-1308) with the reference prototypes, on host lib4 buffers;
 //   * the batched device API of the same pipeline (hpmpc_mi355x_pcond_*), data resident in HBM.
 // Every computation runs on the GPU; the host only packs stage tables and copies buffers.
-#include <hip/hip_runtime.h>
+#include "hk_wide_host.h"
 
-#include <cstdio>
-#include <cstdlib>
-#include <algorithm>
-#include <cstring>
-#include <vector>
-
-#include "../../include/hpmpc_mi355x.h"
-#include "hk_wide_args.h"
-
-extern "C" int hk_wide_launch(int which, const void* args, int count, int lds_doubles, hipStream_t stream);
-extern "C" void hk_set_error(int code, const char* what);
-
-namespace {
-
-constexpr int BS = 4, NCL = 2;
-constexpr int LDS_MAX_DOUBLES = 65536 / 8;
-
-inline int rup(int n, int m) { return (n + m - 1) / m * m; }
-inline double& P4(double* A, int sd, int i, int j) { return A[(i / BS) * BS * sd + i % BS + BS * j]; }
-inline int poff(int j, int nz) { return j * nz - (j * (j - 1)) / 2; }
-
-bool hip_ok(hipError_t e, const char* what) {
-    if (e == hipSuccess) return true;
-    char msg[256];
-    snprintf(msg, sizeof msg, "HIP error in %s: %s", what, hipGetErrorString(e));
-    hk_set_error(HPMPC_MI355X_EHIP, msg);
-    return false;
-}
-
-// One problem's packed layout on the wide path (offsets in doubles; idxb in ints).
-struct WLayout {
-    int N = 0;
-    std::vector<WideStage> st;
-    long long nB = 0, nR = 0, nL = 0, nU = 0, nP = 0, nD = 0, nI = 0;
-    int lds = 0, offW = 0, offX = 0, offV = 0, ldW = 0, ldX = 0;
-    bool any_ng = false;
-    bool fits = true;  // hk_wide_sv limits: nu+nx+1 <= 128 (two rows per lane), nx <= 64 (MFMA tiles per wave)
-};
-
-WLayout make_layout(int N, const int* nx, const int* nu, const int* nb, const int* ng) {
-    WLayout L;
-    L.N = N;
-    L.st.resize(N + 1);
-    int Mmax = 1, nzM = 1, nxM = 1;
-    for (int k = 0; k <= N; k++) {
-        WideStage& s = L.st[k];
-        memset(&s, 0, sizeof s);
-        s.nu = k < N ? nu[k] : 0;
-        s.nx = nx[k];
-        s.nx1 = k < N ? nx[k + 1] : 0;
-        s.nu1 = k + 1 < N ? nu[k + 1] : 0;
-        const int nux = s.nu + s.nx;
-        s.sdB = rup(s.nx1, NCL);
-        s.sdR = rup(nux, NCL);
-        s.oB = (int)L.nB;
-        if (k < N) L.nB += (long long)rup(nux + 1, BS) * s.sdB;
-        s.oR = (int)L.nR;
-        L.nR += (long long)rup(nux + 1, BS) * s.sdR;
-        s.oL = (int)L.nL;
-        L.nL += poff(nux, nux + 1) + nux;
-        L.nL = (L.nL + 7) / 8 * 8;
-        s.oU = (int)L.nU;
-        L.nU += rup(nux + 1, 8);
-        s.oP = (int)L.nP;
-        L.nP += rup(s.nx1 + 1, 8);
-        s.nb = nb[k];
-        s.pnb = rup(nb[k], BS);
-        s.ng = ng[k];
-        s.oD = (int)L.nD;
-        L.nD += 2 * s.pnb + 2 * rup(ng[k], BS);
-        s.oI = (int)L.nI;
-        L.nI += nb[k];
-        if (ng[k] > 0) L.any_ng = true;
-        Mmax = std::max(Mmax, poff(nux, nux + 1));
-        nzM = std::max(nzM, nux + 1);
-        nxM = std::max(nxM, std::max(s.nx1, s.nx));  // X also receives stage k's own Lxx
-    }
-    L.fits = nzM <= 128 && nxM <= 64;
-    L.ldW = nzM;
-    L.ldX = nxM + 1;
-    L.offW = Mmax + nzM;  // the forward stages L_k with its 1/diag tail into M
-    L.offX = L.offW + L.ldW * nxM;
-    L.offV = L.offX + L.ldX * nxM;
-    L.lds = L.offV + nzM;
-    if (L.nD == 0) L.nD = 1;
-    if (L.nI == 0) L.nI = 1;
-    if (L.nB == 0) L.nB = 1;
-    return L;
-}
-
-// Thread-local device context of the host-buffer entry points: one stream, a growable device arena and
-// its pinned staging twin.
-struct WCtx {
-    hipStream_t stream = nullptr;
-    char* dev = nullptr;
-    char* host = nullptr;
-    size_t cap = 0;
-    ~WCtx() {
-        if (dev) (void)hipFree(dev);
-        if (host) (void)hipHostFree(host);
-        if (stream) (void)hipStreamDestroy(stream);
-    }
-    bool ensure(size_t bytes) {
-        if (!stream && !hip_ok(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "stream create")) return false;
-        if (bytes > cap) {
-            if (dev) (void)hipFree(dev);
-            if (host) (void)hipHostFree(host);
-            dev = host = nullptr;
-            cap = 0;
-            if (!hip_ok(hipMalloc((void**)&dev, bytes), "wide device arena")) return false;
-            if (!hip_ok(hipHostMalloc((void**)&host, bytes, 0), "wide pinned arena")) return false;
-            cap = bytes;
-        }
-        memset(host, 0, bytes);
-        return true;
-    }
-    bool up(size_t bytes) {
-        return hip_ok(hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, stream), "H2D");
-    }
-    bool down(size_t bytes) {
-        return hip_ok(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, stream), "D2H") &&
-               hip_ok(hipStreamSynchronize(stream), "sync");
-    }
-};
-thread_local WCtx g_w;
-
-// Byte carve of the staging arena.
-struct Carve {
-    size_t o = 0;
-    size_t take(size_t bytes) {
-        size_t r = o;
-        o += (bytes + 255) / 256 * 256;
-        return r;
-    }
-};
-
-bool launch(int which, const void* args, int count, int lds, hipStream_t stream, const char* name) {
-    if (lds > LDS_MAX_DOUBLES) {
-        hk_set_error(HPMPC_MI355X_EUNSUPPORTED, "wide stage beyond the 64 KiB LDS tile budget");
-        return false;
-    }
-    int e = hk_wide_launch(which, args, count, lds, stream);
-    if (e) {
-        char msg[128];
-        snprintf(msg, sizeof msg, "%s launch failed (%d)", name, e);
-        hk_set_error(HPMPC_MI355X_EHIP, msg);
-        return false;
-    }
-    return true;
-}
-
-}  // namespace
 
 // ------------------------------------------------------------------------------------------------
 // d_back_ric_rec_sv_tv_res on wide stages (called by hpmpc_capi.cpp when the tile path does not fit).
@@ -173,24 +21,61 @@ extern "C" long long hk_wide_factor_bytes(int N, const int* nx, const int* nu) {
     return s * 8;
 }
 
-extern "C" void hk_wide_sv_entry(int N, int* nx, int* nu, int* nb, int** idxb, int* ng, int update_b, double** hpBAbt,
-                                 double** b, int update_q, double** hpQ, double** q, double** bd, double** Qx,
-                                 double** qx, double** hux, int compute_pi, double** hpi, int compute_Pb, double** hPb,
-                                 double* memory) {
-    hk_set_error(0, nullptr);
-    WLayout L = make_layout(N, nx, nu, nb, ng);
-    if (L.any_ng) {
-        hk_set_error(HPMPC_MI355X_EUNSUPPORTED, "wide stages (nu+nx > 16) with general constraints");
-        return;
+namespace {
+// General constraints of the drop-in Riccati calls: DCt_k and the general halves of Qx / qx ([box (pnb) |
+// general (png)]) staged for the device (DCt diag(Qx_g) DCt' and DCt qx_g are added there, d_back_ric_rec.c:
+// 210-231, :292-317, :620-633); the box halves stay on the host path (the reference's in-place side effects).
+struct GenStage {
+    size_t oG = 0, oQx = 0, oqx = 0;
+};
+GenStage carve_general(const WLayout& L, Carve& c) {
+    GenStage g;
+    if (!L.any_ng) return g;
+    g.oG = c.take(8 * L.nG);
+    g.oQx = c.take(8 * L.nD);
+    g.oqx = c.take(8 * L.nD);
+    return g;
+}
+void stage_general(const WLayout& L, const GenStage& g, char* H, double** hpDCt, double** Qx, double** qx) {
+    if (!L.any_ng) return;
+    double* HG = reinterpret_cast<double*>(H + g.oG);
+    for (int k = 0; k <= L.N; k++) {
+        const WideStage& s = L.st[k];
+        if (s.ng == 0) continue;
+        memcpy(HG + s.oG, hpDCt[k], (size_t)rup(s.nu + s.nx, BS) * s.sdG * sizeof(double));
+        for (int l = 0; l < s.ng; l++) {
+            if (Qx) reinterpret_cast<double*>(H + g.oQx)[s.oD + s.pnb + l] = Qx[k][s.pnb + l];
+            if (qx) reinterpret_cast<double*>(H + g.oqx)[s.oD + s.pnb + l] = qx[k][s.pnb + l];
+        }
     }
+}
+void general_args(const WLayout& L, const GenStage& g, char* D, WideArgs& a) {
+    if (!L.any_ng) return;
+    a.DCt = reinterpret_cast<const double*>(D + g.oG);
+    a.Qx = reinterpret_cast<const double*>(D + g.oQx);
+    a.qx = reinterpret_cast<const double*>(D + g.oqx);
+}
+bool fits_check(const WLayout& L) {
     if (L.lds > LDS_MAX_DOUBLES || !L.fits) {
         hk_set_error(HPMPC_MI355X_EUNSUPPORTED, "wide stage beyond the kernel's tile limits (64 KiB LDS, "
                                                 "nu+nx < 128, nx <= 64)");
-        return;
+        return false;
     }
+    return true;
+}
+}  // namespace
+
+extern "C" void hk_wide_sv_entry(int N, int* nx, int* nu, int* nb, int** idxb, int* ng, int update_b, double** hpBAbt,
+                                 double** b, int update_q, double** hpQ, double** q, double** bd, double** hpDCt,
+                                 double** Qx, double** qx, double** hux, int compute_pi, double** hpi, int compute_Pb,
+                                 double** hPb, double* memory) {
+    hk_set_error(0, nullptr);
+    WLayout L = make_layout(N, nx, nu, nb, ng);
+    if (!fits_check(L)) return;
     Carve c;
     const size_t oSt = c.take(sizeof(WideStage) * (N + 1)), oB = c.take(8 * L.nB), oR = c.take(8 * L.nR),
                  oF = c.take(8 * L.nL), oU = c.take(8 * L.nU), oP = c.take(8 * L.nP), oPb = c.take(8 * L.nP);
+    const GenStage gs = carve_general(L, c);
     if (!g_w.ensure(c.o)) return;
     char* H = g_w.host;
     memcpy(H + oSt, L.st.data(), sizeof(WideStage) * (N + 1));
@@ -214,9 +99,11 @@ extern "C" void hk_wide_sv_entry(int N, int* nx, int* nu, int* nb, int** idxb, i
             memcpy(HB + s.oB, hpBAbt[k], (size_t)rup(nux + 1, BS) * s.sdB * sizeof(double));
         }
     }
+    stage_general(L, gs, H, hpDCt, Qx, qx);
     char* D = g_w.dev;
     WideArgs a;
     memset(&a, 0, sizeof a);
+    general_args(L, gs, D, a);
     a.N = N;
     a.nprob = 1;
     a.st = reinterpret_cast<const WideStage*>(D + oSt);
@@ -247,18 +134,7 @@ extern "C" void hk_wide_sv_entry(int N, int* nx, int* nu, int* nb, int** idxb, i
 }
 
 namespace {
-bool wide_check(const WLayout& L) {
-    if (L.any_ng) {
-        hk_set_error(HPMPC_MI355X_EUNSUPPORTED, "wide stages (nu+nx > 16) with general constraints");
-        return false;
-    }
-    if (L.lds > LDS_MAX_DOUBLES || !L.fits) {
-        hk_set_error(HPMPC_MI355X_EUNSUPPORTED, "wide stage beyond the kernel's tile limits (64 KiB LDS, "
-                                                "nu+nx < 128, nx <= 64)");
-        return false;
-    }
-    return true;
-}
+bool wide_check(const WLayout& L) { return fits_check(L); }
 void wide_args(const WLayout& L, WideArgs& a) {
     memset(&a, 0, sizeof a);
     a.N = L.N;
@@ -273,13 +149,14 @@ void wide_args(const WLayout& L, WideArgs& a) {
 
 // d_back_ric_rec_trf_tv_res on wide stages: hk_wide_sv in factor-only mode (no augmented row, no forward).
 extern "C" void hk_wide_trf_entry(int N, int* nx, int* nu, int* nb, int** idxb, int* ng, double** hpBAbt,
-                                  double** hpQ, double** Qx, double** bd, double* memory) {
+                                  double** hpQ, double** hpDCt, double** Qx, double** bd, double* memory) {
     hk_set_error(0, nullptr);
     WLayout L = make_layout(N, nx, nu, nb, ng);
     if (!wide_check(L)) return;
     Carve c;
     const size_t oSt = c.take(sizeof(WideStage) * (N + 1)), oB = c.take(8 * L.nB), oR = c.take(8 * L.nR),
                  oF = c.take(8 * L.nL), oU = c.take(8 * L.nU), oP = c.take(8 * L.nP);
+    const GenStage gs = carve_general(L, c);
     if (!g_w.ensure(c.o)) return;
     char* H = g_w.host;
     memcpy(H + oSt, L.st.data(), sizeof(WideStage) * (N + 1));
@@ -295,9 +172,11 @@ extern "C" void hk_wide_trf_entry(int N, int* nx, int* nu, int* nb, int** idxb, 
         memcpy(HR + s.oR, hpQ[k], (size_t)rup(nux + 1, BS) * s.sdR * sizeof(double));
         if (k < N) memcpy(HB + s.oB, hpBAbt[k], (size_t)rup(nux + 1, BS) * s.sdB * sizeof(double));
     }
+    stage_general(L, gs, H, hpDCt, Qx, nullptr);
     char* D = g_w.dev;
     WideArgs a;
     wide_args(L, a);
+    general_args(L, gs, D, a);
     a.trf = 1;
     a.st = reinterpret_cast<const WideStage*>(D + oSt);
     a.BAbt = reinterpret_cast<const double*>(D + oB);
@@ -311,15 +190,15 @@ extern "C" void hk_wide_trf_entry(int N, int* nx, int* nu, int* nb, int** idxb, 
 
 // d_back_ric_rec_trs_tv_res on wide stages (hk_wide_trs) over the factor hk_wide_trf_entry left in memory.
 extern "C" void hk_wide_trs_entry(int N, int* nx, int* nu, int* nb, int** idxb, int* ng, double** hpBAbt,
-                                  double** hb, double** hq, double** qx, double** hux, int compute_pi, double** hpi,
-                                  int compute_Pb, double** hPb, double* memory) {
+                                  double** hb, double** hq, double** hpDCt, double** qx, double** hux, int compute_pi,
+                                  double** hpi, int compute_Pb, double** hPb, double* memory) {
     hk_set_error(0, nullptr);
     WLayout L = make_layout(N, nx, nu, nb, ng);
     if (!wide_check(L)) return;
     Carve c;
     const size_t oSt = c.take(sizeof(WideStage) * (N + 1)), oB = c.take(8 * L.nB), oF = c.take(8 * L.nL),
                  oU = c.take(8 * L.nU), oP = c.take(8 * L.nP), oPb = c.take(8 * L.nP), ob = c.take(8 * L.nP),
-                 oq = c.take(8 * L.nU), oqx = c.take(8 * L.nD), oI = c.take(4 * L.nI);
+                 oq = c.take(8 * L.nU), oqx = c.take(8 * L.nD), oI = c.take(4 * L.nI), oG = c.take(8 * L.nG);
     if (!g_w.ensure(c.o)) return;
     char* H = g_w.host;
     memcpy(H + oSt, L.st.data(), sizeof(WideStage) * (N + 1));
@@ -337,6 +216,11 @@ extern "C" void hk_wide_trs_entry(int N, int* nx, int* nu, int* nb, int** idxb, 
         if (nb[k] > 0) {
             memcpy(Hqx + s.oD, qx[k], nb[k] * sizeof(double));
             memcpy(HI + s.oI, idxb[k], nb[k] * sizeof(int));
+        }
+        if (ng[k] > 0) {  // DCt qx_g on the device (general half of qx at pnb)
+            memcpy(Hqx + s.oD + s.pnb, qx[k] + s.pnb, ng[k] * sizeof(double));
+            memcpy(reinterpret_cast<double*>(H + oG) + s.oG, hpDCt[k],
+                   (size_t)rup(nux, BS) * s.sdG * sizeof(double));
         }
         if (k < N) {
             memcpy(HB + s.oB, hpBAbt[k], (size_t)rup(nux + 1, BS) * s.sdB * sizeof(double));
@@ -357,6 +241,7 @@ extern "C" void hk_wide_trs_entry(int N, int* nx, int* nu, int* nb, int** idxb, 
     a.hq = reinterpret_cast<const double*>(D + oq);
     a.qx = reinterpret_cast<const double*>(D + oqx);
     a.idxb = reinterpret_cast<const int*>(D + oI);
+    if (L.any_ng) a.DCt = reinterpret_cast<const double*>(D + oG);
     a.compute_pi = compute_pi;
     a.compute_Pb = compute_Pb;
     if (!g_w.up(c.o) || !launch(3, &a, 1, L.lds, g_w.stream, "hk_wide_trs") || !g_w.down(c.o)) return;

@@ -13,9 +13,14 @@
  * Part 2 is the additive batched API: many independent QPs that share stage sizes, with all data
  * already resident in device memory (HBM).
  *
- * GPU-path limits (checked; a violation is reported through hpmpc_mi355x_last_error()):
- *   nu[k] + nx[k] <= 16 and round_up(nu[k],4) + nx[k] <= 16 for every stage,
- *   round_up(nb[k],4) + round_up(ng[k],4) <= 16.
+ * GPU paths (selected per call from the stage sizes):
+ *   tile path -- nu[k] + nx[k] <= 16, round_up(nu[k],4) + nx[k] <= 16 and round_up(nb[k],4) + round_up(ng[k],4)
+ *     <= 16 for every stage: one wavefront per problem, the stage in MFMA registers;
+ *   wide path -- every other problem with nu[k] + nx[k] + 1 <= 128, nx[k] <= 64 and the stage tiles within
+ *     64 KiB of LDS (any nb <= nu+nx, any ng): one 256-thread workgroup per problem, stage tiles in LDS; the
+ *     IPMs run whole on the device in one launch.
+ *   Part 1 serves both; the batched Part 2 takes tile-path plans (plus the partial-condensing pipeline).
+ *   Beyond these limits, and for duplicate box indices, calls report HPMPC_MI355X_EUNSUPPORTED.
  * Error reporting: the reference's int entry points keep their codes 0/1/2/-1; this library adds
  *   HPMPC_MI355X_EUNSUPPORTED (-10) and HPMPC_MI355X_EHIP (-11).  void entry points set the
  *   thread-local code returned by hpmpc_mi355x_last_error() and print one line to stderr.

@@ -218,6 +218,7 @@ def main():
     alt(ref, ref_avx_api(), rng, out)
     pcond(ref, out)
     iface(ref, out)
+    wide(ref, ref_avx_api(), out)
     total = sum(os.path.getsize(p) for p in out)
     print(f"wrote {len(out)} cases, {total / 1e6:.2f} MB")
 
@@ -315,6 +316,90 @@ def iface(ref, out):
                          extra=extra))
 
 
+def wide(ref, refa, out):
+    """Problems beyond the 16-wide register tile of the product's narrow kernels (they run on its wide-stage IPM,
+    hk_wide_ipm.hip): configs[4]'s stage shape nx=24 nu=6 (mass-spring, time-variant, warm start, k_max, no
+    constraints), random problems with more than 16 constraint slots per stage (dense general constraints, also
+    on narrow stages), the KKT re-solve, the residuals, a single Newton step, the alternate IPM with its KKT
+    re-solve and residuals, and the c_interface wrappers with a partially condensed horizon whose condensed
+    stages (nu2 = 40) exceed the tile, with the inner state boxes turned into general constraints."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from helpers import random_qp
+    import iface_oracle as IO
+
+    rng = np.random.default_rng(20261017)
+    args = dict(k_max=50, mu0=2.0, mu_tol=1e-12, alpha_min=1e-8)
+
+    def ipm_out(r):
+        return dict(ux=r["ux"], pi=r["pi"], lam=r["lam"], t=r["t"], stat=r["stat"], kk=r["kk"], ret=r["ret"])
+
+    ms = mass_spring_qp(20, 24, 6, boxes=True)
+    tv = mass_spring_qp(15, 24, 6, boxes=True, batch=1, time_variant=True, seed=7).problem(0)
+    gen = random_qp(12, [0] + [20] * 12, [4] * 12 + [0], [4] + [8] * 11 + [6], seed=41,
+                    ng=[6] + [20] * 11 + [24])
+    slots = random_qp(20, [0] + [8] * 20, [3] * 20 + [0], [3] + [11] * 19 + [8], seed=46,
+                      ng=[2] + [8] * 19 + [9])
+    for name, qp, a in (("N20_nx24_nu6", ms, args), ("tv_N15_nx24_nu6", tv, args),
+                        ("ng_N12_nx20_nu4", gen, dict(args, k_max=60)), ("slots_N20_nx8_nu3", slots, args),
+                        ("kmax4_N20_nx24_nu6", ms, dict(args, k_max=4))):
+        out.append(save_case(f"ipmw_{name}", "ipm", qp, a, ipm_out(ref.ipm(qp.copy(), **a))))
+    ux0 = rand_vecs(rng, [ms.nux(k) for k in range(ms.N + 1)], scale=0.1)
+    r = ref.ipm(ms.copy(), warm_start=1, ux=ux0, **args)
+    out.append(save_case("ipmw_warm_N20_nx24_nu6", "ipm", ms, dict(args, warm_start=1), ipm_out(r),
+                         extra=dict(ux0=ux0)))
+    qp = mass_spring_qp(15, 24, 6, boxes=False)
+    out.append(save_case("ipmw_noconstr_N15_nx24_nu6", "ipm", qp, args, ipm_out(ref.ipm(qp.copy(), **args))))
+    for name, qp in (("N20_nx24_nu6", ms), ("ng_N12_nx20_nu4", gen)):
+        r = ref.ipm(qp.copy(), **dict(args, k_max=60))
+        b, q = bq_from_qp(qp)
+        b2 = [x + 0.01 * rng.standard_normal(x.shape) for x in b]
+        q2 = [x + 0.01 * rng.standard_normal(x.shape) for x in q]
+        k = ref.kkt_new_rhs(qp.copy(), r["work"], b2, q2)
+        out.append(save_case(f"kktw_{name}", "kkt", qp, dict(args, k_max=60),
+                             dict(ux=k["ux"], pi=k["pi"], lam=k["lam"], t=k["t"]), extra=dict(b2=b2, q2=q2)))
+        uxp = [x + 0.01 * rng.standard_normal(x.shape) for x in r["ux"]]
+        pip = [x + 0.01 * rng.standard_normal(x.shape) for x in r["pi"]]
+        res = ref.residuals(qp.copy(), b, q, uxp, pip, r["lam"], r["t"])
+        out.append(save_case(f"resw_{name}", "res", qp, {},
+                             dict(rq=res["rq"], rb=res["rb"], rd=res["rd"], rm=res["rm"], mu=res["mu"]),
+                             extra=dict(b=b, q=q, ux=uxp, pi=pip, lam=r["lam"], t=r["t"])))
+        res = ref.residuals_plain(qp.copy(), b, q, uxp, pip, r["lam"], r["t"])
+        out.append(save_case(f"res2w_{name}", "res2", qp, {},
+                             dict(rq=res["rq"], rb=res["rb"], rd=res["rd"], mu=res["mu"]),
+                             extra=dict(b=b, q=q, ux=uxp, pi=pip, lam=r["lam"], t=r["t"])))
+        a2 = dict(args, mu_tol=1e-8)
+        out.append(save_case(f"ipm2w_{name}", "ipm2", qp, a2, ipm_out(ref.ipm(qp.copy(), res=False, **a2))))
+        r2 = refa.ipm(qp.copy(), res=False, **a2)
+        d2 = [x + 0.01 * rng.standard_normal(x.shape) for x in qp.d]
+        k2 = refa.kkt_new_rhs_plain(qp.copy(), r2["work"], b2, q2, d2, r2["ux"])
+        out.append(save_case(f"kkt2w_{name}", "kkt2", qp, a2, dict(ux=k2["ux"], pi=k2["pi"], lam=k2["lam"], t=k2["t"]),
+                             extra=dict(b2=b2, q2=q2, d2=d2)))
+    qp = mass_spring_qp(10, 24, 6, boxes=True)
+    r = ref.ipm(qp.copy(), **args)
+    lam0, t0 = [], []
+    for k in range(qp.N + 1):
+        nb = int(qp.nb[k])
+        lam0.append(np.concatenate([1.0 + 0.1 * rng.random(2 * nb), np.zeros(4)]))
+        t0.append(np.concatenate([0.5 + 0.1 * rng.random(2 * nb), np.zeros(4)]))
+    ux0 = [0.9 * x for x in r["ux"]]
+    pi0 = [0.9 * x for x in r["pi"]]
+    sn = ref.single_newton(qp.copy(), ux0, pi0, lam0, t0, k_max=1, mu0=0.1)
+    out.append(save_case("newtonw_N10_nx24_nu6", "newton", qp, dict(k_max=1, mu0=0.1, mu_tol=1e-12, alpha_min=1e-8),
+                         ipm_out(sn), extra=dict(ux0=ux0, pi0=pi0, lam0=lam0, t0=t0)))
+    # c_interface wrappers, condensed N2 < N with condensed stages beyond the tile (nu <= 4: the reference's
+    # c99 condensing is right there), and a full-space wide problem
+    for name, (N, nx, nu, bu, bx, ng, seed), N2 in (
+            ("condw_N40_nx12_nu4_N2_4", (40, [0] + [12] * 40, [4] * 40, 4, 6, None, 11), 4),
+            ("fullw_N10_nx20_nu4", (10, [0] + [20] * 10, [4] * 10, 4, 8, None, 12), 10)):
+        P = IO.random_iface_problem(N, nx, nu, bu, bx, ng, seed=seed)
+        r = IO.ip_ocp(ref, P, N2, k_max=50, mu0=2.0, mu_tol=1e-10)
+        outs = dict(u=r["u"], x=r["x"], pi=r["pi"], lam=r["lam"], inf_norm_res=r["inf_norm_res"], kk=r["kk"],
+                    ret=r["status"], stat=r["stat"])
+        out.append(save_case(f"iface_{name}", "iface", IO.to_qp(P), dict(N2=N2, mu0=2.0, mu_tol=1e-10, k_max=50),
+                             outs, extra=IO.to_flat(P)))
+
+
 def soft(ref, out):
     """Soft-constraint IPM d_ip2_mpc_soft_tv (mpc_solvers/d_ip2_soft.c:83): the reference driver's problem
     (test_d_ip_soft.c: Q = 0, Z = 0, z = 100, mu0 = 100) at three sizes, stopped at mu_tol = 1e-5 -- below that its
@@ -354,6 +439,10 @@ if __name__ == "__main__":
         o = []
         iface(ref_api(), o)
         print(f"wrote {len(o)} iface cases, {sum(os.path.getsize(p) for p in o) / 1e6:.2f} MB")
+    elif len(sys.argv) > 1 and sys.argv[1] == "wide":
+        o = []
+        wide(ref_api(), ref_avx_api(), o)
+        print(f"wrote {len(o)} wide cases, {sum(os.path.getsize(p) for p in o) / 1e6:.2f} MB")
     elif len(sys.argv) > 1 and sys.argv[1] == "pcond":
         o = []
         pcond(ref_api(), o)

@@ -3,7 +3,7 @@
 The goldens (iface_*, run through test_gpu_parity.py) pin the column-major wrapper against the restatement
 oracle/iface_oracle.py over the reference's own low-level entry points.  These cases add the row-major
 twin, random problems against the restatement over the oracle, warm start, the KKT re-solve in both orders, and
-the partially condensed path whose condensed stages exceed the IPM tile (an error code, not an abort).
+the partially condensed path whose condensed stages exceed the narrow tile (solved by the wide-stage IPM).
 Tolerances as the IPM goldens: ux/pi/lam 1e-10 with identical kk; residual norms 1e-9 absolute.
 """
 import os
@@ -71,9 +71,19 @@ def test_kkt_new_rhs_wrapper(product, oracle, order):
     _cmp(got, IO.kkt_ocp(oracle, P, P2, mu_tol=1e-10))
 
 
-def test_condensed_ipm_beyond_the_tile_is_an_error(product):
-    """N2 < N with condensed stages wider than the IPM tile (nu2 + nx2 = 5*4 + 8 > 16): the wrapper returns
-    HPMPC_MI355X_EUNSUPPORTED (-10) instead of aborting."""
-    P = IO.random_iface_problem(10, [0] + [8] * 10, [4] * 10, 2, 2, None, seed=1)
-    r = product.ip_ocp(P, 2)
-    assert r["status"] == -10
+@pytest.mark.parametrize("case", [(10, [0] + [8] * 10, [4] * 10, 2, 2, None, 2),
+                                  (40, [0] + [12] * 40, [4] * 40, 4, 6, None, 4),
+                                  (30, [0] + [24] * 30, [6] * 30, 3, 5, None, 3)],
+                         ids=["N10_N2_2", "N40_N2_4", "N30_nx24_nu6_N2_3"])
+def test_condensed_ipm_beyond_the_tile(product, oracle, case):
+    """N2 < N with condensed stages wider than the narrow tile (nu2 + nx2 = 5*4 + 8 .. 10*6 + 24): the wrapper
+    condenses (inner state boxes become general constraints), runs the wide-stage IPM (hk_wide_ipm) on the
+    condensed problem and expands, in both orders, against the restatement over the oracle."""
+    N, nx, nu, bu, bx, ng, N2 = case
+    P = IO.random_iface_problem(N, nx, nu, bu, bx, ng, seed=N + 7)
+    ref = IO.ip_ocp(oracle, P, N2, mu_tol=1e-10)
+    assert ref["status"] == 0
+    for order in ("F", "C"):
+        got = product.ip_ocp(P, N2, order=order, mu_tol=1e-10)
+        assert (got["status"], got["kk"]) == (ref["status"], ref["kk"]), order
+        _cmp(got, ref)
