@@ -959,8 +959,10 @@ __device__ __forceinline__ void fwd_fetch(const RicIO& io, const SH& sh, int k, 
     // the generic solve, l by the sv forward: the gain-form predictor masks the rest off (a masked lane reads
     // nothing, and every path keeps the same load count for the counted vmcnt waits).
     const bool needS = !SH::fixed || compute_pi;
+    // S[0] (tile rows 0..3) holds the u block's columns of L: a fixed-shape stage (nu <= 4, xo = 4) solves
+    // its u block in gain form, and pi_from_x reads rows >= xo only, so S[0] is never needed there
 #pragma unroll
-    for (int r = 0; r < 4; r++) f.S[r] = gld(Fk, r * 64 + l, needS);
+    for (int r = 0; r < 4; r++) f.S[r] = gld(Fk, r * 64 + l, needS && (r > 0 || !SH::fixed));
     f.lc = gld(Fk, 256 + c, MODE == 0);
     f.invd = gld(Fk, 272 + c, !SH::fixed);
     f.kg = gld(Fk, 288 + l);
@@ -1184,8 +1186,10 @@ __device__ __forceinline__ void trs_fetch(const RicIO& io, const SH& sh, int k, 
                                           const BoxCtx& bc, int compute_Pb, const double* Pb, TrsFrag& f) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
     const double* Fk = io.F + (long)k * FSTRIDE;
+    // the n-form solve of a fixed-shape stage runs over its u pivots (< 4), i.e. reads S[0] only; rows
+    // 4..15 are needed by the generic solve and by P_{k} b_{k-1} (compute_Pb, the KKT re-solve)
 #pragma unroll
-    for (int r = 0; r < 4; r++) f.S[r] = gld(Fk, r * 64 + l);
+    for (int r = 0; r < 4; r++) f.S[r] = gld(Fk, r * 64 + l, r == 0 || !SH::fixed || compute_Pb);
     f.invd = gld(Fk, 272 + c);
     const int nux = sh.nu + sh.nx;
     const int vc = tile_var(c, sh.nu, sh.nx, sh.xo);

@@ -412,10 +412,12 @@ __device__ __forceinline__ ResIO res_io(const IpmView& v) {
     return ro;
 }
 
-// Phase-2 start residuals: r_d, r_m and mu here; r_q, r_b in the first phase-2 factorisation.
-template <class FX>
+// Phase-2 start residuals: r_d, r_m and mu here; r_q, r_b in the first phase-2 factorisation.  CI: stages
+// per chunk of the element-wise passes (7 in hk_ipm_init; 2 inside hk_ipm_update, where the problem-start and
+// phase-switch paths run once per problem and must not raise the update loop's register allocation).
+template <class FX, int CI>
 __device__ double p2_start(const KArgs& a, IpmView& v) {
-    const double mu = update_p2_pass<7, false>(v.io, v.bc, v.bt.slotvar, 0.0, 1.0 / (2.0 * a.nbt), v.ux, v.pi,
+    const double mu = update_p2_pass<CI, false>(v.io, v.bc, v.bt.slotvar, 0.0, 1.0 / (2.0 * a.nbt), v.ux, v.pi,
                                                nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, v.w.res_d,
                                                v.w.res_m);
     wsync();
@@ -424,7 +426,7 @@ __device__ double p2_start(const KArgs& a, IpmView& v) {
 
 // End of an iteration (or of init): decide whether the problem continues, switching from phase 1 to
 // phase 2 (with the phase-2 start residuals) when phase 1's loop condition fails.
-template <class FX>
+template <class FX, int CI>
 __device__ bool ipm_continue(const KArgs& a, IpmView& v, int kk, double mu, double alpha, double sigma, int phase) {
     const bool sn = a.single_newton != 0;
     bool active;
@@ -434,7 +436,7 @@ __device__ bool ipm_continue(const KArgs& a, IpmView& v, int kk, double mu, doub
         if (phase == 1) {
             const double mu_tol_low = a.mu_tol < 1e-5 ? 1e-5 : a.mu_tol;
             if (!(kk < a.k_max && mu > mu_tol_low && alpha >= a.alpha_min)) {
-                mu = p2_start<FX>(a, v);  // phase-2 start (d_ip2_res_hard.c:756-781)
+                mu = p2_start<FX, CI>(a, v);  // phase-2 start (d_ip2_res_hard.c:756-781)
                 phase = 2;
             }
         }
@@ -469,12 +471,16 @@ __device__ bool ipm_continue(const KArgs& a, IpmView& v, int kk, double mu, doub
 }
 
 // Start of a solve: init_var and the loop-control state.  Returns whether the problem iterates.
-template <class FX>
+// SHORTCUT: compile the unconstrained one-Riccati-solve exits (nbt == 0, a plan-wide constant).  hk_ipm_update
+// leaves them out: with nbt == 0 every entry finishes inside ipm_start, so hk_ipm_init's refill loop drains the
+// whole queue and no update pass ever refills a slot.
+template <class FX, int CI, bool SHORTCUT>
 __device__ bool ipm_start(const KArgs& a, const LdsTabs& T, IpmView& v) {
     Scratch& sm = *T.sm;
     const int N = v.N, l = v.l;
     const int nbt = a.nbt;
-    if (nbt == 0 && a.phase1_only) {
+    if (!SHORTCUT && nbt == 0) return false;
+    if (SHORTCUT && nbt == 0 && a.phase1_only) {
         // d_ip2_mpc_hard_tv without constraints: one sv into the workspace's dux / dpi, the caller's
         // ux / pi stay untouched (d_ip2_hard.c:282-291)
         ric_backward<true, BX_NONE, FX>(v.io, &sm, 0, nullptr, 0, nullptr, v.bc, 1, v.w.Pb);
@@ -487,7 +493,7 @@ __device__ bool ipm_start(const KArgs& a, const LdsTabs& T, IpmView& v) {
         }
         return false;
     }
-    if (nbt == 0) {
+    if (SHORTCUT && nbt == 0) {
         // no constraints: one sv and return (d_ip2_res_hard.c:428-450)
         ric_backward<true, BX_NONE, FX>(v.io, &sm, 0, nullptr, 0, nullptr, v.bc, 1, v.w.Pb);
         wsync();
@@ -508,7 +514,7 @@ __device__ bool ipm_start(const KArgs& a, const LdsTabs& T, IpmView& v) {
     // iterate (d_init_var_mpc_hard_tv_single_newton is a copy, done by the host), no phase 1.
     const bool sn = a.single_newton != 0;
     if (!sn) {
-        init_var<7>(v.io, v.dv, v.ux, v.pi, v.w.dpi, v.lam, v.t, a.mu0, a.warm_start);
+        init_var<CI>(v.io, v.dv, v.ux, v.pi, v.w.dpi, v.lam, v.t, a.mu0, a.warm_start);
         if (a.ngt) {
             wsync();
             init_var_gen(v.io, v.dv, v.ux, v.lam, v.t, a.mu0);
@@ -519,12 +525,12 @@ __device__ bool ipm_start(const KArgs& a, const LdsTabs& T, IpmView& v) {
     if (l == 0) v.w.state[S_MUSCAL] = 1.0 / (2.0 * nbt);
     wsync();
     double mu = a.mu0;
-    if (sn) mu = p2_start<FX>(a, v);  // straight to phase 2: its start residuals
-    return ipm_continue<FX>(a, v, 0, mu, 1.0, 0.0, sn ? 2 : 1);
+    if (sn) mu = p2_start<FX, CI>(a, v);  // straight to phase 2: its start residuals
+    return ipm_continue<FX, CI>(a, v, 0, mu, 1.0, 0.0, sn ? 2 : 1);
 }
 
 // Queue mode: hand slot s the next queue entries until one of them iterates (true) or the queue is empty.
-template <class FX>
+template <class FX, int CI, bool SHORTCUT>
 __device__ bool ipm_refill(const KArgs& a, const LdsTabs& T, int s) {
     const bool l0 = lane_id() == 0;
     for (;;) {
@@ -538,7 +544,7 @@ __device__ bool ipm_refill(const KArgs& a, const LdsTabs& T, int s) {
         if (l0) a.qctl[2 + s] = q;
         const Who who{s, q, q % a.nprob};
         IpmView v = ipm_view(a, T, who);
-        if (ipm_start<FX>(a, T, v)) return true;
+        if (ipm_start<FX, CI, SHORTCUT>(a, T, v)) return true;
         if (l0) atomicAdd(&a.qctl[1], 1);
     }
 }
@@ -549,13 +555,13 @@ template <class FX>
 __global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_init(KArgs a) {
     const LdsTabs T = lds_tables(a);
     if (a.nq) {  // every slot takes its first entry; the iterating ones form the first active list
-        if (ipm_refill<FX>(a, T, blockIdx.x)) qlist_push(a, a.qpar, blockIdx.x);
+        if (ipm_refill<FX, 7, true>(a, T, blockIdx.x)) qlist_push(a, a.qpar, blockIdx.x);
         return;
     }
     Who who;
     if (!who_am_i(a, who)) return;
     IpmView v = ipm_view(a, T, who);
-    ipm_start<FX>(a, T, v);
+    ipm_start<FX, 7, true>(a, T, v);
 }
 
 // Factorisation of the iteration's KKT system, Hessian / gradient box terms fused into the fetch.
@@ -670,10 +676,10 @@ __global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_update(KArgs a) {
     wsync();
     if (v.l == 0) v.stat[5 * kk + 4] = mu;
     kk++;
-    bool again = ipm_continue<FX>(a, v, kk, mu, alpha, st[S_SIGMA], phase);
+    bool again = ipm_continue<FX, 4>(a, v, kk, mu, alpha, st[S_SIGMA], phase);
     if (!again && a.nq) {
         if (v.l == 0) atomicAdd(&a.qctl[1], 1);
-        again = ipm_refill<FX>(a, T, who.s);  // queue mode: the slot takes the next entry
+        again = ipm_refill<FX, 4, false>(a, T, who.s);  // queue mode: the slot takes the next entry
     }
     if (a.nq && again) qlist_push(a, a.qpar ^ 1, who.s);
 }

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Workload for the rocprofv3 --pmc passes (one counter group per pass, see tools/gpu_round.sh):
 1 GiB calibration copy (known bytes), then the benchmark's IPM (N=100 nx=12 nu=4, batch 1024: a
-problem queue of 4 batches through 2048 slots, run twice) and two Riccati sv launches."""
+problem queue of 4 batches through 2048 slots, run twice), two Riccati sv launches, and the configs[4]
+partial-condensing pipeline (512 x N=200 nx=24 nu=6 -> 20 blocks: hk_pcond, hk_wide_sv, hk_pexpand) twice."""
 import ctypes as C
 import os
 import sys
@@ -37,6 +38,14 @@ def main():
         ric.ric_sv()
     torch.cuda.synchronize()
     print("kk_sum", int(Q.kk.sum().item()))
+    if "--no-pcond" not in sys.argv:
+        from hpmpc_amd.ocp import mass_spring_qp
+        from hpmpc_amd.pcond import PcondSolver
+
+        pc = PcondSolver(mass_spring_qp(200, 24, 6, boxes=False, batch=512, time_variant=True, seed=4), 20)
+        for _ in range(2):
+            pc.solve()
+        torch.cuda.synchronize()
 
 
 if __name__ == "__main__":
