@@ -6,7 +6,7 @@ MPC QPs per GPU, N=100, nx=12, nu=4 (nb = 4 / 10 / 6 on stage 0 / inner / N), fp
 stage data (no aliased buffers), solved by the residual-based Mehrotra IPM
 (d_ip2_res_mpc_hard_tv: mu0=2, mu_tol=1e-12, alpha_min=1e-8, k_max=50).
 
-A "step" is one batch of 1024 problems.  The K timed steps are solved through one problem queue
+A "step" is one batch of 1024 problems (default K = 40 steps).  The K timed steps are solved through one problem queue
 (hpmpc_mi355x_ipm_queue): 2 x 1024 resident solver slots, each taking the next problem as soon as its
 own has converged (iterations are ticks of the pass kernels hk_ipm_fact, hk_ipm_pred, hk_ipm_corr,
 hk_ipm_update over all slots).  value = IP iterations per second over all ranks (sum of per-problem
@@ -42,7 +42,10 @@ PEAK_FP64_TFS = 78.6   # MI355X fp64 (vector = MFMA dense)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    # 40 batches: the queue's drain (the last problems, ~9 % of which run to k_max or alpha_min, finishing at one
+    # wave per SIMD) is a fixed cost per run; 40 batches amortise it towards the steady state of a continuously fed
+    # queue without hiding it (DESIGN.md §6 reports the K dependence)
+    ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=1024, help="problems per GPU")
     ap.add_argument("--N", type=int, default=100)
@@ -200,6 +203,18 @@ def cpu_pcond_baseline(qp, N2, seconds, threads):
             "single_core": {"value": v1, "solves": n1}}
 
 
+def pcond_traffic(kernel, B):
+    """Calibrated HBM bytes per launch of a configs[4] kernel (profiles/pmc_hk_ipm.json, tools/pmc_mix.sh: the
+    same pipeline at batch 512 under rocprofv3 FETCH_SIZE / WRITE_SIZE passes), scaled to this run's batch."""
+    pmc = os.path.join(ROOT, "profiles", "pmc_hk_ipm.json")
+    try:
+        with open(pmc) as f:
+            k = json.load(f)["kernels"][kernel]
+        return k["hbm_bytes_per_launch"] * B / 512.0
+    except Exception:
+        return None
+
+
 def bench_pcond(args, torch, red, rank, world, barrier):
     """configs[4]: 512 problems per GPU, N=200 nx=24 nu=6 condensed into N2=20 blocks of 10, then the
     condensed Riccati factorisation + solve and the expansion (d_part_cond -> d_back_ric_rec_sv_tv_res ->
@@ -242,8 +257,11 @@ def bench_pcond(args, torch, red, rank, world, barrier):
            "condensed": {"N2": N2, "nu2": 60, "nx2": 24},
            "riccati_fact_per_s": B * world / (ms[1] * 1e-3),
            "roofline": {"bound": "hbm", "kernel": names[dom], "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                        "frac": ach / PEAK_HBM_GBS, "traffic": None, "launch_ms": float(ms[dom])},
+                        "frac": ach / PEAK_HBM_GBS, "traffic": pcond_traffic(names[dom], B),
+                        "launch_ms": float(ms[dom])},
            "kernels": kern}
+    for n in names:
+        kern[n]["traffic_bytes_per_launch"] = pcond_traffic(n, B)
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_pcond_baseline(qp, N2, args.cpu_seconds * 0.5, args.cpu_threads)
     return out
