@@ -269,25 +269,38 @@ def bench_pcond(args, torch, red, rank, world, barrier):
 
 def bench_single_qp(args, torch, stream):
     """configs[1]: one QP (the drivers' x0, test_d_ip_hard.c:306-322) solved alone on the GPU: the device time of
-    a batched-API solve of a batch of one (data resident in HBM), and the drop-in d_ip2_res_mpc_hard_tv call on
-    host lib4 buffers (PCIe staging included).  Latency-bound: one wavefront walks the N stages serially."""
+    a one-entry problem queue (data resident in HBM; the same run as the drop-in's), of the batched API with a
+    batch of one, and the drop-in d_ip2_res_mpc_hard_tv call on host lib4 buffers (PCIe staging included).
+    Latency-bound: one wavefront walks the N stages serially."""
     from hpmpc_amd.batch import LIBPATH, BatchSolver
     from hpmpc_amd.cabi import HpmpcAPI, load
     from hpmpc_amd.ocp import mass_spring_qp
 
     one = mass_spring_qp(args.N, args.nx, args.nu, batch=1)
     s = BatchSolver(one, k_max=args.k_max)
-    reps = max(args.steps, 5)
+    reps = max(min(args.steps, 20), 5)
+    # a queue of one entry in one slot: the passes stop a chunk after convergence (the batched solve
+    # hpmpc_mi355x_ipm_batch enqueues k_max x 4 pass launches; its time is reported beside)
+    Q = s.queue(1, 1)
     for _ in range(2):
+        Q.run()
         s.ipm()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
     for a, b in ev:
         a.record(stream)
-        s.ipm()
+        Q.run()
         b.record(stream)
     torch.cuda.synchronize()
     ms = float(np.median([a.elapsed_time(b) for a, b in ev]))
-    kk = int(s.kk[0].item())
+    kk = int(Q.kk[0].item())
+    evb = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for a, b in evb:
+        a.record(stream)
+        s.ipm()
+        b.record(stream)
+    torch.cuda.synchronize()
+    ms_batch = float(np.median([a.elapsed_time(b) for a, b in evb]))
+    assert int(s.kk[0].item()) == kk
     call, kkc = HpmpcAPI(load(LIBPATH)).prepare_ipm(one.problem(0), k_max=args.k_max)
     call()
     t0 = time.perf_counter()
@@ -295,8 +308,8 @@ def bench_single_qp(args, torch, stream):
         call()
     host_ms = (time.perf_counter() - t0) / reps * 1e3
     return {"workload": f"single_qp_N{args.N}_nx{args.nx}_nu{args.nu}", "kk": kk, "device_ms_per_solve": ms,
-            "device_us_per_ip_iter": ms * 1e3 / max(kk, 1), "dropin_ms_per_solve": host_ms,
-            "dropin_kk": int(kkc.value)}
+            "device_us_per_ip_iter": ms * 1e3 / max(kk, 1), "batch_api_ms_per_solve": ms_batch,
+            "dropin_ms_per_solve": host_ms, "dropin_kk": int(kkc.value)}
 
 
 def bench_riccati_small(args, torch, red, rank, world, barrier, stream):

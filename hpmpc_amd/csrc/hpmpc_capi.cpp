@@ -427,43 +427,20 @@ extern "C" int hpmpc_mi355x_ipm_pass(const hpmpc_mi355x_plan* plan, const hpmpc_
 // converged starts the next entry at the following iteration instead of idling until the slowest
 // problem of a batch finishes.  The host enqueues ticks (fact, pred, corr, update) in chunks and stops
 // once the device-side finished counter reaches nq, checking a chunk behind so the stream never drains.
-extern "C" int hpmpc_mi355x_ipm_queue(const hpmpc_mi355x_plan* plan, const hpmpc_mi355x_layout* lay, int nprob,
-                                      int nq, int n_slots, const double* BAbt, const double* RSQrq, const double* d,
-                                      double* ux, double* pi, double* lam, double* t, double* ws, int* qctl,
-                                      int k_max, double mu0, double mu_tol, double alpha_min, int warm_start,
-                                      int compute_mult, int* kk, int* ret, double* stat, double* pass_ms,
-                                      int* n_ticks, void* stream) {
-    auto* P = const_cast<hpmpc_mi355x_plan*>(plan);
-    if (!P || nprob <= 0 || nq < 0 || n_slots <= 0 || !qctl) return g_err = HPMPC_MI355X_EUNSUPPORTED;
+namespace {
+// The queue driver shared by hpmpc_mi355x_ipm_queue and the single-problem entry points (which run their one
+// problem as a queue of one entry in one slot, so no pass is enqueued after it has converged).  `a` carries the
+// problem data and solver parameters; R ticks per chunk.
+template <int R>
+int queue_run(KArgs a, int nq, int n_slots, int* qctl, int k_max, double* pass_ms, int* n_ticks, hipStream_t st) {
     if (n_ticks) *n_ticks = 0;
     if (pass_ms)
         for (int i = 0; i < 5; i++) pass_ms[i] = 0.0;
     if (nq == 0) return g_err = 0;
-    KArgs a = base_args(P, nprob, 0);
-    if (!layout_apply(P, lay, a)) return g_err;
-    a.BAbt = BAbt;
-    a.RSQ = RSQrq;
-    a.d = d;
-    a.ux = ux;
-    a.pi = pi;
-    a.lam = lam;
-    a.t = t;
-    a.ws = ws;
-    a.k_max = k_max;
-    a.mu0 = mu0;
-    a.mu_tol = mu_tol;
-    a.alpha_min = alpha_min;
-    a.warm_start = warm_start;
-    a.compute_mult = compute_mult;
-    a.kk = kk;
-    a.ret = ret;
-    a.stat = stat;
     a.nq = nq;
     a.qctl = qctl;
     a.nslots = n_slots;
     a.qpar = 0;  // hk_ipm_init fills active list 0; iteration t runs list t & 1
-    hipStream_t st = (hipStream_t)stream;
-    constexpr int R = 8;  // ticks per chunk
     // Per-call polling state: 2 chunk parities x (R*4 + 1) kernel boundaries + 2 "finished count copied"
     // events, and the pinned host copy of the device's finished counter.  Nothing is shared between calls
     // (so a later call on another stream or device can never read a stale count of this one); the
@@ -540,6 +517,37 @@ extern "C" int hpmpc_mi355x_ipm_queue(const hpmpc_mi355x_plan* plan, const hpmpc
     }
     if (n_ticks) *n_ticks = (int)ticks;
     return g_err = 0;
+}
+}  // namespace
+
+extern "C" int hpmpc_mi355x_ipm_queue(const hpmpc_mi355x_plan* plan, const hpmpc_mi355x_layout* lay, int nprob,
+                                      int nq, int n_slots, const double* BAbt, const double* RSQrq, const double* d,
+                                      double* ux, double* pi, double* lam, double* t, double* ws, int* qctl,
+                                      int k_max, double mu0, double mu_tol, double alpha_min, int warm_start,
+                                      int compute_mult, int* kk, int* ret, double* stat, double* pass_ms,
+                                      int* n_ticks, void* stream) {
+    auto* P = const_cast<hpmpc_mi355x_plan*>(plan);
+    if (!P || nprob <= 0 || nq < 0 || n_slots <= 0 || !qctl) return g_err = HPMPC_MI355X_EUNSUPPORTED;
+    KArgs a = base_args(P, nprob, 0);
+    if (!layout_apply(P, lay, a)) return g_err;
+    a.BAbt = BAbt;
+    a.RSQ = RSQrq;
+    a.d = d;
+    a.ux = ux;
+    a.pi = pi;
+    a.lam = lam;
+    a.t = t;
+    a.ws = ws;
+    a.k_max = k_max;
+    a.mu0 = mu0;
+    a.mu_tol = mu_tol;
+    a.alpha_min = alpha_min;
+    a.warm_start = warm_start;
+    a.compute_mult = compute_mult;
+    a.kk = kk;
+    a.ret = ret;
+    a.stat = stat;
+    return queue_run<8>(a, nq, n_slots, qctl, k_max, pass_ms, n_ticks, (hipStream_t)stream);
 }
 
 extern "C" int hpmpc_mi355x_ric_sv_batch(const hpmpc_mi355x_plan* plan, const hpmpc_mi355x_layout* lay, int nprob,
@@ -672,7 +680,7 @@ thread_local Ctx g_ctx;
 
 // Arena carve (doubles) for one problem.
 struct Arena {
-    size_t BAbt, RSQ, DCt, d, ux, pi, lam, t, ws, vb, vq, vQx, vqx, vPb, stat, ints, total;
+    size_t BAbt, RSQ, DCt, d, ux, pi, lam, t, ws, vb, vq, vQx, vqx, vPb, stat, ints, qctl, total;
 };
 
 Arena arena(const hpmpc_mi355x_plan* P, int k_max) {
@@ -700,6 +708,7 @@ Arena arena(const hpmpc_mi355x_plan* P, int k_max) {
     A.vPb = take(n1 * V16);
     A.stat = take(5 * (size_t)(k_max > 0 ? k_max : 1) + 8);
     A.ints = take(8);
+    A.qctl = take(8);  // queue control of the one-entry queue the IPM entry points run (16 ints >= 4 + 3 slots)
     A.total = o;
     return A;
 }
@@ -1015,7 +1024,12 @@ int ipm_entry(int single_newton, int phase1_only, int* kk, int k_max, double mu0
     a.compute_mult = compute_mult;
     a.single_newton = single_newton;
     a.phase1_only = phase1_only;
-    if (!up(A) || !run(K_IPM, a, "hk_ipm") || !down(A)) return g_err;
+    // the solve runs as a queue of one entry in one slot: passes are enqueued in chunks of 4 iterations and
+    // stop one chunk after the problem has finished, instead of k_max x 4 launches
+    if (!up(A)) return g_err;
+    if (queue_run<4>(a, 1, 1, reinterpret_cast<int*>(g_ctx.dev + A.qctl), k_max, nullptr, nullptr, g_ctx.stream))
+        return g_err;
+    if (!down(A)) return g_err;
     const int* iv = reinterpret_cast<const int*>(H + A.ints);
     *kk = iv[0];
     for (int i = 0; i < 5 * iv[0]; i++) stat[i] = H[A.stat + i];
