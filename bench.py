@@ -52,8 +52,8 @@ def parse():
     ap.add_argument("--nx", type=int, default=12)
     ap.add_argument("--nu", type=int, default=4)
     ap.add_argument("--k-max", type=int, default=50)
-    ap.add_argument("--slots", type=int, default=0, help="resident solver slots (default 2 x batch: two "
-                    "problems per SIMD)")
+    ap.add_argument("--slots", type=int, default=0, help="resident solver slots (default max(2 x batch, 2048): "
+                    "two problems per SIMD)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-threads", type=int, default=16, help="host threads for the CPU baseline "
                     "(the GPU box's CPU share is 16 per GPU)")
@@ -443,7 +443,9 @@ def main():
     # (hpmpc_mi355x_ipm_queue): `slots` resident solver slots, each taking the next problem of the
     # queue as soon as its own has converged, so K batches cost ~K x (mean iterations), not
     # K x (max iterations).  Profiled run: one hipEvent per kernel boundary on the solve's stream.
-    slots = args.slots if args.slots > 0 else 2 * B
+    # two resident problems per SIMD of the chip (256 CUs x 4 SIMDs): a per-GPU batch below 1024 (the strong-
+    # scaling split of configs[3], 4096 over 8 GPUs = 512 per GPU) still fills every SIMD twice from the queue
+    slots = args.slots if args.slots > 0 else max(2 * B, 2048)
     if args.warmup > 0:
         wq = solver.queue(args.warmup * B, slots)
         wq.run()
@@ -487,6 +489,27 @@ def main():
         qb = {"slots": B, "value": sum_over_ranks(float(Q.kk.sum().item())) / qdt, "unit": "IP-iter/s",
               "ms_per_step": qdt / args.steps * 1e3}
         del Q
+
+    # the generic-shape kernels (DynSh: stage sizes read from the stage table, no compile-time class) on a shape
+    # with no compiled class, nx = 10 nu = 3, same N / constraints / queue: what any other caller shape runs at
+    dyn = None
+    if not args.no_isolated and rank == 0:
+        qd = make_shard(N, 10, 3, 0, 1, B)
+        sd = BatchSolver(qd, k_max=args.k_max)
+        Kd = min(args.steps, 10)
+        sd.queue(B, slots).run()
+        Qd = sd.queue(Kd * B, slots)
+        torch.cuda.synchronize()
+        d0 = time.perf_counter()
+        pd, td = Qd.run(profiled=True)
+        torch.cuda.synchronize()
+        ddt = time.perf_counter() - d0
+        itd = float(Qd.kk.sum().item())
+        dyn = {"workload": f"ipm_N{N}_nx10_nu3_batch{B}_generic_kernels", "value": itd / ddt, "unit": "IP-iter/s",
+               "steps": Kd, "fact_us_per_problem_iter": pd[1] * 1e3 / itd,
+               "headline_fact_us_per_problem_iter": pass_ms[1] * 1e3 / iters_rank,
+               "pass_ms_per_step": {n: float(v) / Kd for n, v in zip(names, pd)}}
+        del Qd, sd
 
     # one isolated batch (no queue): the latency of a batch solve, reported beside the queue rate
     iso = None
@@ -577,6 +600,7 @@ def main():
                                              "algorithmic_bytes_per_ip_iter": bytes_iter,
                                              "fp64_tflops": iters_rank * fl_iter / (ipm_ms * 1e-3) / 1e12}},
             "queue_batch_slots": qb,
+            "generic_shape": dyn,
             "isolated_batch": iso,
             "scatter": sc,
             "riccati": {"value": fact_total / rdt, "unit": "fact/s", "kernel": "hk_ric_sv", "launch_ms": sv_ms,
