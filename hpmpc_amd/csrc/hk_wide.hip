@@ -170,11 +170,11 @@ __global__ __launch_bounds__(WT) void hk_pcond(PcArgs a) {
                     for (int jj = 0; jj < 16; jj++) {
                         if (jj < pw) {
                             const double d = rdlane(cl[jj], p0 + jj);
-                            double sq = 0.0, inv = 0.0;
-                            if (d > 1e-15) {
-                                sq = sqrt(d);
-                                inv = 1.0 / sq;
-                            }
+                            // the pivot clamp d > 1e-15 else 0 (kernel_dpotrf_c99_lib4.c:555-640) with s = sqrt(d), 1/s from
+                            // v_rsq_f64 plus one third-order refinement (hk::chol_pivot, <= 1.2 half-ulp) instead of an IEEE
+                            // sqrt and divide on the pivot chain
+                            double sq, inv;
+                            hk::chol_pivot(d, sq, inv);
                             cl[jj] = i == p0 + jj ? sq : (i > p0 + jj ? cl[jj] * inv : 0.0);
 #pragma unroll
                             for (int cc = jj + 1; cc < 16; cc++) cl[cc] -= cl[jj] * rdlane(cl[jj], p0 + cc);
@@ -270,6 +270,8 @@ __global__ __launch_bounds__(WT) void hk_pcond(PcArgs a) {
         const int n = (a.nzN + 3) / 4 * 4 * a.sdRN;
         double* RN = a.RSQ2 + (long)p * a.sR2 + a.oR2N;
         for (int e = tid; e < n; e += WT) RN[e] = RSQ[sN.oR + e];
+        double* dN = a.d2 + (long)p * a.sD2 + a.oD2N;  // and its bounds (the IPM on the condensed problem reads them)
+        for (int e = tid; e < a.nDN; e += WT) dN[e] = dv[sN.oD + e];
     }
 }
 

@@ -77,6 +77,7 @@ struct PcArgs {
     int offP, offX, offW, offB, ldP, ldX, ldW, ldB;  // dynamic LDS carve
     int offGA, offGB;                                // Gamma_{j-1} / Gamma_j tiles (and stage scratch)
     int skip;  // profiling only (HK_PCOND_SKIP): bit 0 Gamma, 1 RSQ phase, 2 its Cholesky, 3 M product, 4 W/syrk
+    int oD2N, nDN;  // terminal stage: its bounds d_N (original offset st[N].oD, nDN doubles) -> d2 at oD2N
 };
 
 // Expansion (d_part_expand_solution): one workgroup per (block, problem).

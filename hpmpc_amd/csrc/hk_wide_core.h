@@ -348,11 +348,11 @@ __device__ void wide_sv_body(const WideArgs& a, const WideProb& q) {
                 for (int jj = 0; jj < 16; jj++) {
                     if (jj < pw) {
                         const double d = rdlane(c0[jj], jj);
-                        double sq = 0.0, inv = 0.0;
-                        if (d > 1e-15) {
-                            sq = sqrt(d);
-                            inv = 1.0 / sq;
-                        }
+                        // the pivot clamp d > 1e-15 else 0 (kernel_dpotrf_c99_lib4.c:555-640) with s = sqrt(d), 1/s from
+                        // v_rsq_f64 plus one third-order refinement (hk::chol_pivot, <= 1.2 half-ulp) instead of an IEEE
+                        // sqrt and divide on the pivot chain
+                        double sq, inv;
+                        hk::chol_pivot(d, sq, inv);
                         c0[jj] = lane == jj ? sq : (lane > jj ? c0[jj] * inv : 0.0);
                         c1[jj] = c1[jj] * inv;
                         if (lane == 0) M[poff(nux, nz) + p0 + jj] = inv;

@@ -504,12 +504,12 @@ __global__ __launch_bounds__(WT) void hk_wide_ipm(WideIpmArgs A) {
         if (tid == 0) {
             A.kk[p] = kk;
             A.ret[p] = ret;
-            A.mu[p] = mu;
+            if (A.mu) A.mu[p] = mu;
         }
     };
 
     if (mode == WI_RES || mode == WI_RES_PLAIN) {
-        const double mu = residuals(A, P, mode == WI_RES_PLAIN, A.mu[p], red);
+        const double mu = residuals(A, P, mode == WI_RES_PLAIN, A.mu ? A.mu[p] : 0.0, red);
         finish(0, 0, mu);
         return;
     }

@@ -269,6 +269,7 @@ struct PcPlan {
     int N = 0, N2 = 0;
     WLayout orig, cond;
     std::vector<int> nx2, nu2, nb2, ng2;
+    std::vector<int> idxb2;  // condensed box indices packed per stage (cond.st[ii].oI), as hk_pcond writes them
     std::vector<PcBlock> blk;
     std::vector<int> idxb;  // original idxb packed per stage (orig.st[k].oI)
     long long nG = 0;       // Gamma scratch (doubles per problem)
@@ -366,6 +367,23 @@ bool pc_plan(PcPlan& P, int N, const int* nx, const int* nu_in, const int* nb, c
     }
     P.nG2 = oG2 > 0 ? oG2 : 1;
     P.ref_d = ref_d;
+    // condensed box indices (d_cond_DCtd, d_part_cond.c:579-688): input boxes of the block's later stages keep
+    // their position in [u_{T-1}; ..; u_0; x_0], stage 0's boxes stay boxes, inner state boxes become general
+    P.idxb2.assign(P.cond.nI, 0);
+    for (int ii = 0; ii < N2; ii++) {
+        const PcBlock& b = P.blk[ii];
+        int* i2 = P.idxb2.data() + P.cond.st[ii].oI;
+        int ib = 0, nu_tmp = 0;
+        for (int sI = b.T - 1; sI >= 1; sI--) {
+            const int s = b.s0 + sI;
+            nu_tmp += nu[s];
+            for (int jj = 0; jj < nb[s]; jj++)
+                if (idxb[s][jj] < nu[s]) i2[ib++] = nu_tmp - nu[s] + idxb[s][jj];
+        }
+        nu_tmp += nu[b.s0];
+        for (int jj = 0; jj < nb[b.s0]; jj++) i2[ib++] = nu_tmp - nu[b.s0] + idxb[b.s0][jj];
+    }
+    for (int l = 0; l < nb[N]; l++) P.idxb2[P.cond.st[N2].oI + l] = idxb[N][l];
     // Gamma tiles: the largest (rows x nx_{j+1}) of any block, also used as the RSQrq_{s-1} tile
     long long gmax = (long long)nzM * nzM;
     {
@@ -421,6 +439,8 @@ void fill_pc_args(const PcPlan& P, PcArgs& a) {
     a.sG2 = P.nG2;
     a.sD2 = P.cond.nD;
     a.oR2N = P.cond.st[P.N2].oR;
+    a.oD2N = P.cond.st[P.N2].oD;
+    a.nDN = 2 * P.orig.st[P.N].pnb + 2 * rup(P.orig.st[P.N].ng, BS);
     a.sdRN = P.orig.st[P.N].sdR;
     a.nzN = P.orig.st[P.N].nu + P.orig.st[P.N].nx + 1;
     a.offP = P.offP;
@@ -576,6 +596,7 @@ extern "C" void d_part_cond(int N, int* nx, int* nu, int* nb, int** hidxb, int* 
     a.BAbt2 = a.RSQ2 = a.DCt2 = a.d2 = mem;
     a.idxb2 = reinterpret_cast<int*>(mem + P.ref_d);
     a.oR2N = (int)term_off;
+    a.nDN = 0;  // the reference aliases hd2[N2] = hd[N] (d_part_cond.c), nothing to copy into the carve
     if (!g_w.up(c.o) || !launch(1, &a, 1, P.pc_lds, g_w.stream, "hk_pcond") || !g_w.down(c.o)) return;
     for (int ii = 0; ii <= N2; ii++) {
         nx2[ii] = P.nx2[ii];
@@ -694,8 +715,13 @@ extern "C" void d_part_expand_solution(int N, int* nx, int* nu, int* nb, int** h
 // ------------------------------------------------------------------------------------------------
 // Batched device API of the partial-condensing pipeline (data resident in HBM, problem-major).
 // ------------------------------------------------------------------------------------------------
+extern "C" hpmpc_mi355x_wide_plan* hpmpc_mi355x_wide_plan_create(int N, const int* nx, const int* nu, const int* nb,
+                                                                 const int* const* idxb, const int* ng);
+extern "C" void hpmpc_mi355x_wide_plan_destroy(hpmpc_mi355x_wide_plan* q);
+
 struct hpmpc_mi355x_pcond_plan {
     PcPlan P;
+    hpmpc_mi355x_wide_plan* wide = nullptr;  // the condensed problem's IPM plan (null: beyond the wide IPM)
     WideStage *d_st = nullptr, *d_st2 = nullptr;
     PcBlock* d_blk = nullptr;
     int* d_idxb = nullptr;
@@ -709,6 +735,7 @@ extern "C" void hpmpc_mi355x_pcond_plan_destroy(hpmpc_mi355x_pcond_plan* q) {
     if (q->d_blk) (void)hipFree(q->d_blk);
     if (q->d_idxb) (void)hipFree(q->d_idxb);
     if (q->d_idxb2) (void)hipFree(q->d_idxb2);
+    hpmpc_mi355x_wide_plan_destroy(q->wide);
     delete q;
 }
 
@@ -735,7 +762,27 @@ extern "C" hpmpc_mi355x_pcond_plan* hpmpc_mi355x_pcond_plan_create(int N, const 
         hpmpc_mi355x_pcond_plan_destroy(q);
         return nullptr;
     }
+    // the condensed problem's wide-stage IPM plan (hpmpc_mi355x_pcond_wide_plan); its DCt2 holds the blocks'
+    // general constraints only, so a terminal stage with ng[N] > 0 leaves the plan without it
+    if (ng[N] == 0) {
+        std::vector<int*> i2(N2 + 1);
+        for (int k = 0; k <= N2; k++) i2[k] = q->P.idxb2.data() + P.cond.st[k].oI;
+        q->wide = hpmpc_mi355x_wide_plan_create(N2, P.nx2.data(), P.nu2.data(), P.nb2.data(), i2.data(),
+                                                P.ng2.data());
+    }
+    hk_set_error(0, nullptr);  // a condensed problem beyond the wide IPM keeps the condense / Riccati pipeline
     return q;
+}
+
+// The condensed problem's IPM plan (owned by the pcond plan; null when the condensed stages exceed the wide
+// IPM's limits or ng[N] > 0): hpmpc_mi355x_wide_ipm_batch on BAbt2 / RSQrq2 / DCt2 / d2 solves the condensed
+// problems, hpmpc_mi355x_pexpand_batch expands their solution and multipliers.
+extern "C" const hpmpc_mi355x_wide_plan* hpmpc_mi355x_pcond_wide_plan(const hpmpc_mi355x_pcond_plan* q) {
+    if (!q || !q->wide) {
+        hk_set_error(HPMPC_MI355X_EUNSUPPORTED, "no wide IPM plan for this condensed problem");
+        return nullptr;
+    }
+    return q->wide;
 }
 
 // Per-problem sizes (doubles): [0] BAbt [1] RSQrq [2] d (=lam/t) [3] ux [4] pi of the original layout;

@@ -396,3 +396,162 @@ extern "C" void hk_wide_res_entry(int plain, int N, int* nx, int* nu, int* nb, i
     if (!plain) cvec_out(W, IW + W.oC[5], N, hrm);
     *mu = reinterpret_cast<const double*>(H + S.oCtl + 8)[0];
 }
+
+// ------------------------------------------------------------------------------------------------
+// Batched device API of the wide-stage IPM (include/hpmpc_mi355x.h, Part 2): many problems that share the
+// stage sizes and box index sets, data resident in HBM, one workgroup per problem, one launch per batch.
+// ------------------------------------------------------------------------------------------------
+struct hpmpc_mi355x_wide_plan {
+    WIpm W;
+    int N = 0;
+    WideStage* d_st = nullptr;
+    WideCSlot* d_cs = nullptr;
+    int* d_vbox = nullptr;
+    int* d_idxb = nullptr;
+};
+
+extern "C" void hpmpc_mi355x_wide_plan_destroy(hpmpc_mi355x_wide_plan* q) {
+    if (!q) return;
+    if (q->d_st) (void)hipFree(q->d_st);
+    if (q->d_cs) (void)hipFree(q->d_cs);
+    if (q->d_vbox) (void)hipFree(q->d_vbox);
+    if (q->d_idxb) (void)hipFree(q->d_idxb);
+    delete q;
+}
+
+extern "C" hpmpc_mi355x_wide_plan* hpmpc_mi355x_wide_plan_create(int N, const int* nx, const int* nu_in, const int* nb,
+                                                                 const int* const* idxb, const int* ng) {
+    hk_set_error(0, nullptr);
+    std::vector<int> nu(nu_in, nu_in + N + 1);
+    nu[N] = 0;
+    auto* q = new hpmpc_mi355x_wide_plan();
+    q->N = N;
+    q->W = make_ipm(N, nx, nu.data(), nb, ng);
+    int** ib = const_cast<int**>(idxb);
+    if (!ipm_check(q->W, N, nx, nu.data(), nb, ib, ng)) {
+        delete q;
+        return nullptr;
+    }
+    fill_slots(q->W, N, ib);
+    const WLayout& L = q->W.L;
+    std::vector<int> hidx(L.nI, 0);
+    for (int k = 0; k <= N; k++)
+        for (int l = 0; l < nb[k]; l++) hidx[L.st[k].oI + l] = idxb[k][l];
+    const size_t ncs = q->W.cs.size() + 1;
+    bool ok = hip_ok(hipMalloc((void**)&q->d_st, sizeof(WideStage) * (N + 1)), "wide plan") &&
+              hip_ok(hipMalloc((void**)&q->d_cs, sizeof(WideCSlot) * ncs), "wide plan") &&
+              hip_ok(hipMalloc((void**)&q->d_vbox, sizeof(int) * L.nU), "wide plan") &&
+              hip_ok(hipMalloc((void**)&q->d_idxb, sizeof(int) * L.nI), "wide plan") &&
+              hip_ok(hipMemcpy(q->d_st, L.st.data(), sizeof(WideStage) * (N + 1), hipMemcpyHostToDevice), "plan") &&
+              (q->W.cs.empty() || hip_ok(hipMemcpy(q->d_cs, q->W.cs.data(), sizeof(WideCSlot) * q->W.cs.size(),
+                                                   hipMemcpyHostToDevice), "plan")) &&
+              hip_ok(hipMemcpy(q->d_vbox, q->W.vbox.data(), sizeof(int) * L.nU, hipMemcpyHostToDevice), "plan") &&
+              hip_ok(hipMemcpy(q->d_idxb, hidx.data(), sizeof(int) * L.nI, hipMemcpyHostToDevice), "plan");
+    if (!ok) {
+        hpmpc_mi355x_wide_plan_destroy(q);
+        return nullptr;
+    }
+    return q;
+}
+
+// out[8]: doubles per problem of BAbt, RSQrq, DCt, d (= lam = t), ux, pi, the work image; N
+extern "C" int hpmpc_mi355x_wide_sizes(const hpmpc_mi355x_wide_plan* q, long long* out) {
+    if (!q) return HPMPC_MI355X_EUNSUPPORTED;
+    const WLayout& L = q->W.L;
+    const long long v[8] = {L.nB, L.nR, L.nG, L.nD, L.nU, L.nP, q->W.nIW, q->N};
+    memcpy(out, v, sizeof v);
+    return 0;
+}
+
+// out[6*(N+1)]: oB, oR, oG, oD, oU, oP of every stage (doubles inside one problem's arrays)
+extern "C" int hpmpc_mi355x_wide_offsets(const hpmpc_mi355x_wide_plan* q, long long* out) {
+    if (!q) return HPMPC_MI355X_EUNSUPPORTED;
+    for (int k = 0; k <= q->N; k++) {
+        const WideStage& s = q->W.L.st[k];
+        const long long v[6] = {s.oB, s.oR, s.oG, s.oD, s.oU, s.oP};
+        memcpy(out + 6 * k, v, sizeof v);
+    }
+    return 0;
+}
+
+// d_ip2_res_mpc_hard_tv on problems [p0, p0 + count) of a device-resident batch (problem-major arrays with the
+// per-problem sizes of hpmpc_mi355x_wide_sizes); kk / ret per problem, stat 5 * k_max per problem; `work` holds
+// each problem's work image (the factor and iterate backup of its last iteration).  Asynchronous on `stream`.
+extern "C" int hpmpc_mi355x_wide_ipm_batch(const hpmpc_mi355x_wide_plan* q, int nprob, int p0, int count,
+                                           const double* BAbt, const double* RSQrq, const double* DCt, const double* d,
+                                           double* ux, double* pi, double* lam, double* t, double* work, int k_max,
+                                           double mu0, double mu_tol, double alpha_min, int warm_start,
+                                           int compute_mult, int* kk, int* ret, double* stat, void* stream) {
+    hk_set_error(0, nullptr);
+    if (!q || nprob <= 0 || p0 < 0 || count < 0 || p0 + count > nprob || k_max < 0)
+        return HPMPC_MI355X_EUNSUPPORTED;
+    const WIpm& W = q->W;
+    const WLayout& L = W.L;
+    WideIpmArgs a;
+    memset(&a, 0, sizeof a);
+    a.w.N = q->N;
+    a.w.nprob = nprob;
+    a.w.p0 = p0;
+    a.w.st = q->d_st;
+    a.w.BAbt = BAbt;
+    a.w.sB = L.nB;
+    a.w.RSQ = RSQrq;
+    a.w.sR = L.nR;
+    a.w.DCt = DCt;
+    a.w.sG = L.nG;
+    a.w.idxb = q->d_idxb;
+    a.w.offW = L.offW;
+    a.w.offX = L.offX;
+    a.w.offV = L.offV;
+    a.w.ldW = L.ldW;
+    a.w.ldX = L.ldX;
+    a.w.sU = L.nU;
+    a.w.sP = L.nP;
+    a.mode = WI_IPM_RES;
+    a.k_max = k_max;
+    a.warm_start = warm_start;
+    a.compute_mult = compute_mult;
+    a.mu0 = mu0;
+    a.mu_tol = mu_tol;
+    a.alpha_min = alpha_min;
+    a.mu_scal = W.nbt ? 1.0 / (2.0 * (double)W.nbt) : 0.0;
+    a.nbt2 = 2.0 * (double)W.nbt;
+    a.ncs = (int)W.cs.size();
+    a.cs = q->d_cs;
+    a.vbox = q->d_vbox;
+    a.nU = (int)L.nU;
+    a.nP = (int)L.nP;
+    a.d = d;
+    a.ux = ux;
+    a.pi = pi;
+    a.lam = lam;
+    a.t = t;
+    a.sC = L.nD;
+    a.iw = work;
+    a.sI = W.nIW;
+    a.oF = W.oF;
+    a.oDux = W.oDux;
+    a.oDpi = W.oDpi;
+    a.oPb = W.oPb;
+    a.oRq = W.oRq;
+    a.oRb = W.oRb;
+    a.oUb = W.oUb;
+    a.oPib = W.oPib;
+    int* oc[10] = {&a.oDlam, &a.oDt, &a.oTinv, &a.oLamt, &a.oRd, &a.oRm, &a.oTb, &a.oLb, &a.oQx, &a.oqx};
+    for (int i = 0; i < 10; i++) *oc[i] = W.oC[i];
+    a.stat = stat;
+    a.sS = 5LL * (k_max > 0 ? k_max : 1);
+    a.kk = kk;
+    a.ret = ret;
+    a.mu = nullptr;
+    a.offR = L.lds;
+    if (count == 0) return 0;
+    const int e = hk_wide_ipm_launch(&a, count, L.lds + 8, (hipStream_t)stream);
+    if (e) {
+        char msg[96];
+        snprintf(msg, sizeof msg, "hk_wide_ipm launch failed (%d)", e);
+        hk_set_error(HPMPC_MI355X_EHIP, msg);
+        return HPMPC_MI355X_EHIP;
+    }
+    return 0;
+}

@@ -42,6 +42,13 @@ def _bind():
     L.hpmpc_mi355x_pcond_ric_sv_batch.argtypes = [vp, i, i, i, vp, vp, vp, vp, vp, i, vp]
     L.hpmpc_mi355x_pexpand_batch.restype = i
     L.hpmpc_mi355x_pexpand_batch.argtypes = [vp, i, i, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.hpmpc_mi355x_pcond_wide_plan.restype = vp
+    L.hpmpc_mi355x_pcond_wide_plan.argtypes = [vp]
+    L.hpmpc_mi355x_wide_sizes.argtypes = [vp, vp]
+    L.hpmpc_mi355x_wide_ipm_batch.restype = i
+    d = C.c_double
+    L.hpmpc_mi355x_wide_ipm_batch.argtypes = [vp, i, i, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, i, d, d, d, i, i, vp,
+                                              vp, vp, vp]
     _ = ll
     _BOUND = True
     return L
@@ -149,6 +156,49 @@ class PcondSolver:
         self.condense()
         self.riccati()
         self.expand()
+
+    def ipm(self, k_max=50, mu0=2.0, mu_tol=1e-12, alpha_min=1e-8, p0=0, count=None):
+        """d_ip2_res_mpc_hard_tv on the condensed problems (hpmpc_mi355x_wide_ipm_batch, the wide-stage IPM: one
+        workgroup per problem, one launch): ux2 / pi2 / lam2 / t2, and kk2 / ret2 / stat2 per problem."""
+        L = _bind()
+        torch = self.torch
+        if not getattr(self, "wplan", None):
+            self.wplan = L.hpmpc_mi355x_pcond_wide_plan(self.plan)
+            if not self.wplan:
+                raise ValueError(f"no wide IPM plan for the condensed problem (code {L.hpmpc_mi355x_last_error()})")
+            ws = (C.c_longlong * 8)()
+            L.hpmpc_mi355x_wide_sizes(self.wplan, ws)
+            self.wsizes = [int(v) for v in ws]
+            assert self.wsizes[3] == self.sizes[8] and self.wsizes[4] == self.sizes[9], (self.wsizes, self.sizes)
+        P = self.nprob
+        if getattr(self, "_kmax", None) != k_max:
+            self.work2 = torch.zeros((P, self.wsizes[6]), dtype=torch.float64, device=self.dev)
+            self.kk2 = torch.zeros(P, dtype=torch.int32, device=self.dev)
+            self.ret2 = torch.zeros(P, dtype=torch.int32, device=self.dev)
+            self.stat2 = torch.zeros((P, 5 * max(k_max, 1)), dtype=torch.float64, device=self.dev)
+            self._kmax = k_max
+        count = self.nprob - p0 if count is None else count
+        p = self._p
+        self._check(L.hpmpc_mi355x_wide_ipm_batch(self.wplan, P, p0, count, p(self.BAbt2), p(self.RSQrq2),
+                                                  p(self.DCt2), p(self.d2), p(self.ux2), p(self.pi2), p(self.lam2),
+                                                  p(self.t2), p(self.work2), k_max, mu0, mu_tol, alpha_min, 0, 1,
+                                                  p(self.kk2), p(self.ret2), p(self.stat2), self._stream()),
+                    "condensed IPM")
+
+    def solve_ipm(self, **kw):
+        """condense -> IPM on the condensed problems -> expand (solution and multipliers), asynchronous."""
+        self.condense()
+        self.ipm(**kw)
+        self.expand()
+
+    def multipliers(self, p: int):
+        """Problem p's expanded lam[k], t[k] (the padded [lb | ub | lg | ug] vectors) as numpy lists."""
+        lam = self.lam[p].cpu().numpy()
+        t = self.t[p].cpu().numpy()
+        qp = self.qp
+        n = [qp.nconstr(k) for k in range(self.N + 1)]
+        return ([lam[self.off[k, 2]:self.off[k, 2] + n[k]].copy() for k in range(self.N + 1)],
+                [t[self.off[k, 2]:self.off[k, 2] + n[k]].copy() for k in range(self.N + 1)])
 
     def solution(self, p: int):
         """Problem p's expanded ux[k] (nu+nx) and pi[k] (nx_{k+1}) as numpy lists."""

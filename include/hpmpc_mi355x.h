@@ -284,6 +284,32 @@ int hpmpc_mi355x_pexpand_batch(const hpmpc_mi355x_pcond_plan *plan, int nprob, i
                                const double *RSQrq, const double *ux2, const double *pi2, const double *lam2,
                                const double *t2, double *ux, double *pi, double *lam, double *t, void *stream);
 
+/* ---- the IPM on wide stages for device-resident batches ----
+ * d_ip2_res_mpc_hard_tv (mpc_solvers/d_ip2_res_hard.c:116) for problems whose stages exceed the 16-wide tile
+ * (nu+nx+1 <= 128, nx <= 64, stage tiles within 64 KiB of LDS; any nb <= nu+nx, any ng): one 256-thread
+ * workgroup runs a whole solve, one launch per batch.  Arrays are problem-major with the per-problem sizes of
+ * hpmpc_mi355x_wide_sizes and the stage offsets of hpmpc_mi355x_wide_offsets; the lib4 blocks, the padded
+ * [lb | ub | lg | ug] vectors and the DCt blocks sit at those offsets. */
+typedef struct hpmpc_mi355x_wide_plan hpmpc_mi355x_wide_plan;
+hpmpc_mi355x_wide_plan *hpmpc_mi355x_wide_plan_create(int N, const int *nx, const int *nu, const int *nb,
+                                                      const int *const *idxb, const int *ng);
+void hpmpc_mi355x_wide_plan_destroy(hpmpc_mi355x_wide_plan *plan);
+/* out[8]: doubles per problem of BAbt, RSQrq, DCt, d (= lam = t), ux, pi, the work image; N */
+int hpmpc_mi355x_wide_sizes(const hpmpc_mi355x_wide_plan *plan, long long *out);
+/* out[6*(N+1)]: oB, oR, oG, oD, oU, oP per stage */
+int hpmpc_mi355x_wide_offsets(const hpmpc_mi355x_wide_plan *plan, long long *out);
+/* problems [p0, p0+count) of the batch; kk / ret per problem, stat 5*k_max per problem, work: each problem's work
+ * image (factor, iterate backup).  Asynchronous on `stream` (a hipStream_t, or null). */
+int hpmpc_mi355x_wide_ipm_batch(const hpmpc_mi355x_wide_plan *plan, int nprob, int p0, int count, const double *BAbt,
+                                const double *RSQrq, const double *DCt, const double *d, double *ux, double *pi,
+                                double *lam, double *t, double *work, int k_max, double mu0, double mu_tol,
+                                double alpha_min, int warm_start, int compute_mult, int *kk, int *ret, double *stat,
+                                void *stream);
+/* the condensed problem's wide plan of a pcond plan (owned by it; null when ng[N] > 0 or beyond the limits):
+ * condense -> hpmpc_mi355x_wide_ipm_batch on BAbt2 / RSQrq2 / DCt2 / d2 -> hpmpc_mi355x_pexpand_batch is the
+ * IPM on a partially condensed batch (the c_interface wrappers' N2 < N path, batched) */
+const hpmpc_mi355x_wide_plan *hpmpc_mi355x_pcond_wide_plan(const hpmpc_mi355x_pcond_plan *plan);
+
 #ifdef __cplusplus
 }
 #endif
