@@ -180,25 +180,38 @@ __device__ __forceinline__ void chol_block(d4& M, double& ml, double& invd, doub
 #undef HK_BSTAMP
 }
 
-// Stage Cholesky with the augmented row.
+// Stage factorisation with the augmented row.
 // In : M (tile, full symmetric), ml (aug row, col layout).
-// Out: M = S = lower(L) + strict_upper(L') (symmetric storage: row p of S == column p of L),
-//      ml = aug row l (col layout), lr = l in row layout, invd = inverse diagonal (col layout).
+// full == true : the whole stage Cholesky (d_back_ric_rec.c:325, dsyrk_dpotrf_lib), M = S = lower(L) +
+//                strict_upper(L'), ml = l, invd = inverse diagonal of every pivot.
+// full == false: "P form" -- only the u pivots are factorised.  The rank-|u| trailing update that the last
+//                u block applies leaves the Schur complement P_k = M_xx - L_xu L_xu' in the x block and
+//                p_k = m_x - L_xu l_u in the x part of ml: exactly the value function's Hessian and gradient
+//                that the reference carries as Lxx Lxx' and Lxx l_x (:262-276 multiply them back), so the
+//                x pivots (and their triangular factor) are never needed on stages k >= 1: the next
+//                stage uses P and p directly (M += BAbt P BAbt', ml += BAbt (P b + p)), pi = P x + p, and
+//                the trs / KKT recursions only ever solve the u pivots.  Stage 0 keeps the full factor (its
+//                forward may solve for x_0 too).  u-block rows keep L's columns in upper storage (row p of S
+//                == column p of L, p < nu), invd holds the u pivots only.
+// Generic shapes restore the lower triangle by an identity-MFMA transpose (L_xu for the generic forward,
+// and P symmetrised); fixed shapes skip it (their consumers read the upper u rows and the P block only).
 template <bool AUG, bool KGEN = false>
-__device__ __forceinline__ void stage_chol(d4& M, double& ml, double& invd, int nu, int nx, int xo, double* kg = nullptr,
-                                           int kdbg = -1) {
+__device__ __forceinline__ void stage_chol(d4& M, double& ml, double& invd, int nu, int nx, int xo, bool full,
+                                           bool transpose, double* kg = nullptr, int kdbg = -1) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
     (void)kdbg;
     invd = 0.0;
     // blocks without an active pivot are skipped (wave-uniform); their rows/columns are zero
-    if (0 < nu || (3 >= xo && 0 < xo + nx)) chol_block<0, AUG, KGEN>(M, ml, invd, kg, kdbg);
+    const int hi = full ? xo + nx : nu;  // pivots [0, hi) are factorised (padding ones clamp to 0)
+    if (0 < nu || (full && 3 >= xo && 0 < hi)) chol_block<0, AUG, KGEN>(M, ml, invd, kg, kdbg);
     HK_STAMP(16, kdbg);
-    if (4 < nu || (7 >= xo && 4 < xo + nx)) chol_block<1, AUG>(M, ml, invd, nullptr, kdbg);
+    if (4 < nu || (full && 7 >= xo && 4 < hi)) chol_block<1, AUG>(M, ml, invd, nullptr, kdbg);
     HK_STAMP(18, kdbg);
-    if (8 < nu || (11 >= xo && 8 < xo + nx)) chol_block<2, AUG>(M, ml, invd, nullptr, kdbg);
+    if (8 < nu || (full && 11 >= xo && 8 < hi)) chol_block<2, AUG>(M, ml, invd, nullptr, kdbg);
     HK_STAMP(20, kdbg);
-    if (12 < nu || (15 >= xo && 12 < xo + nx)) chol_block<3, AUG>(M, ml, invd, nullptr, kdbg);
+    if (12 < nu || (full && 15 >= xo && 12 < hi)) chol_block<3, AUG>(M, ml, invd, nullptr, kdbg);
     HK_STAMP(22, kdbg);
+    if (!transpose) return;
     // lower triangle <- transpose of the upper storage:  T = S' via MFMA with an identity B operand
     // (two accumulator chains: the identity products are exact, so the split does not change T)
     const d4 z = {0.0, 0.0, 0.0, 0.0};
@@ -728,12 +741,14 @@ __device__ __forceinline__ void bwd_residual(const RicIO& io, Scratch* sm, const
     for (int r = 0; r < 4; r++) f.brow[r] = br[r];
 }
 
-// One backward stage: M = RSQ + W W' (+ box terms) with W' = Lxx_{k+1}' BAbt_k', then the stage
-// Cholesky.  S (in: factor of stage k+1, out: factor of stage k), lr/ml/invd likewise.
+// One backward stage: M = RSQ + BAbt P BAbt' (+ box terms), then the stage factorisation (P form on
+// stages k >= 1, see stage_chol).  S (in: record of stage k+1, whose x block is P_{k+1}; out: record of
+// stage k), ml/invd/kg likewise.  The reference forms the same M as RSQ + W W' with W = BAbt Lxx
+// (dtrmm_nt_u + dsyrk, d_back_ric_rec.c:262-264, :325) and the same row as W (Lxx' b + l_x) (:266-276).
 template <bool AUG, int BM, class SH>
 __device__ __forceinline__ void bwd_step(const RicIO& io, Scratch* sm, const SH& sh, int k, const BwdFrag& cur,
-                                         const BoxCtx& bc, int compute_Pb, double* Pb, d4& S, double lr_prev[4],
-                                         double& ml_prev, double& invd_prev, double& kg_prev) {
+                                         const BoxCtx& bc, int compute_Pb, double* Pb, d4& S, double& ml_prev,
+                                         double& invd_prev, double& kg_prev) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
     const bool live = SH::fixed || k < io.N;
     double dq, qxv;
@@ -748,68 +763,58 @@ __device__ __forceinline__ void bwd_step(const RicIO& io, Scratch* sm, const SH&
         if (sh.ng > 0) gen_hessian<BM>(io, sh, k, bc, BM == BX_P2R ? cur.uc : 0.0, M, ml, AUG);
     }
     const int nx1 = sh.nx1, xo1 = sh.xo1;
-    d4 acc = {0.0, 0.0, 0.0, 0.0};
+    const bool xc = c >= xo1;  // tile column c is a state of stage k+1 (padding beyond xo1+nx1 is zero)
     if (live) {
-        // W' = Lxx_{k+1}' BAbt_k'  (dtrmm_nt_u, d_back_ric_rec.c:262-264), rows in stage-(k+1) tile coords;
+        // T' = P_{k+1} BAbt_k'  (rows in stage-(k+1) tile coords): the A fragment of K-chunk kc is P's
+        // register kc itself (P symmetric: lane (g,c) holds P[4kc+g][c] = P[c][4kc+g]), its u columns masked;
         // two accumulator chains (even / odd K-chunks) halve the dependent MFMA latency
         d4 a0 = {0.0, 0.0, 0.0, 0.0}, a1 = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int kc = 0; kc < 4; kc++) {
             if (4 * kc + 3 < xo1 || 4 * kc >= xo1 + nx1) continue;  // uniform
-            const double aop = (c >= xo1 && 4 * kc + g >= c) ? S[kc] : 0.0;
+            const double aop = xc ? S[kc] : 0.0;
             if (kc & 1)
                 a1 = mfma(aop, cur.bop[kc], a1);
             else
                 a0 = mfma(aop, cur.bop[kc], a0);
         }
-        acc = a0 + a1;
-        // M += W W'  (dsyrk part of dsyrk_dpotrf_lib, :325), again on two chains
+        const d4 acc = a0 + a1;
+        // M += BAbt_k T'  (A fragment of chunk r = the BAbt operand already in registers), two chains
         d4 m1 = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int r = 0; r < 4; r++) {
             if (4 * r + 3 < xo1 || 4 * r >= xo1 + nx1) continue;
             if (r & 1)
-                m1 = mfma(acc[r], acc[r], m1);
+                m1 = mfma(cur.bop[r], acc[r], m1);
             else
-                M = mfma(acc[r], acc[r], M);
+                M = mfma(cur.bop[r], acc[r], M);
         }
         M = M + m1;
     }
     if (AUG) {
-        // v = Lxx' b (col layout, stage k+1 tile); zero at k = N (no next stage)
+        // Pb_k = P_{k+1} b_k (col layout, stage-(k+1) tile); zero at k = N (S = 0, b = 0).  Stored masked,
+        // never skipped: the row update below needs it anyway
         double part = 0.0;
 #pragma unroll
-        for (int r = 0; r < 4; r++) part += (c >= xo1 ? lowS(S, r, g, c) : 0.0) * brow[r];
-        const double vcol = xrow_sum(part);
-        double vrow[4];
-        col2row(sm, vcol, vrow);
-        // Pb_k = Lxx (Lxx' b)  (dtrmv_u_t on W's last row, :266-275); store masked, never skipped
-        double pb = 0.0;
-        if (compute_Pb) {  // wave-uniform: the Riccati-only sv (compute_Pb = 0) skips P b
-            double pp = 0.0;
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const int j = g + 4 * r;
-                pp += (j <= c && j >= xo1) ? S[r] * vrow[r] : 0.0;
-            }
-            pb = xrow_sum(pp);
-        }
-        gst(Pb, k * V16 + (c - xo1), pb, compute_Pb && live && g == 0 && c >= xo1 && c < xo1 + nx1);
-        // w_last = b' Lxx + l_{k+1,x}   (dgead, :276)  -> m_last += W w_last
+        for (int r = 0; r < 4; r++) part += (xc ? S[r] : 0.0) * brow[r];
+        const double pb = xrow_sum(part);
+        gst(Pb, k * V16 + (c - xo1), pb, compute_Pb && live && g == 0 && xc && c < xo1 + nx1);
+        // m_last += BAbt_k (P b + p_{k+1})
+        const double wc = xc ? pb + ml_prev : 0.0;
+        double wrow[4];
+        col2row(sm, wc, wrow);
         double mp = 0.0;
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const double w = (g + 4 * r >= xo1) ? vrow[r] + lr_prev[r] : 0.0;
-            mp += acc[r] * w;
-        }
+        for (int r = 0; r < 4; r++) mp += cur.bop[r] * wrow[r];
         if (live) ml += xrow_sum(mp);
     }
     HK_STAMP(2, k);
     double invd, kg = 0.0;
-    stage_chol<AUG, SH::fixed>(M, ml, invd, sh.nu, sh.nx, sh.xo, &kg, k);
+    // stage 0 of a generic problem keeps the full factor; every other stage is factorised in P form
+    const bool full = !SH::fixed && k == 0;
+    stage_chol<AUG, SH::fixed>(M, ml, invd, sh.nu, sh.nx, sh.xo, full, !SH::fixed, &kg, k);
     kg_prev = kg;
     HK_STAMP(3, k);
-    if (AUG) col2row(sm, ml, lr_prev);  // l in row layout, for the next stage's w_last
 #pragma unroll
     for (int r = 0; r < 4; r++) S[r] = M[r];
     ml_prev = ml;
@@ -825,7 +830,6 @@ template <bool AUG, int BM, class FX>
 __device__ void ric_backward(const RicIO& io, Scratch* sm, int update_b, const double* bsrc, int update_q,
                              const double* qsrc, const BoxCtx& bc, int compute_Pb, double* Pb) {
     d4 S = {0.0, 0.0, 0.0, 0.0};
-    double lr_prev[4] = {0.0, 0.0, 0.0, 0.0};
     double ml_prev = 0.0, invd_prev = 0.0, kg_prev = 0.0;
     StageInfo si = load_stage(io.st, io.N);
     BwdFrag cur;
@@ -845,7 +849,7 @@ __device__ void ric_backward(const RicIO& io, Scratch* sm, int update_b, const d
         asm volatile("" ::: "memory");  // keep those stores here, ahead of this stage's math
         HK_STAMP(1, k);
         with_shape<FX>(si, [&](const auto& sh) {
-            bwd_step<AUG, BM>(io, sm, sh, k, cur, bc, compute_Pb, Pb, S, lr_prev, ml_prev, invd_prev, kg_prev);
+            bwd_step<AUG, BM>(io, sm, sh, k, cur, bc, compute_Pb, Pb, S, ml_prev, invd_prev, kg_prev);
         });
         if constexpr (BM == BX_P2R)
             with_shape<FX>(sn, [&](const auto& sh) { bwd_residual(io, sm, sh, kn, bc, nxt, k > 0); });
@@ -914,22 +918,14 @@ __device__ __forceinline__ double solve_ln(const SH& sh, const d4& S, double inv
     return h;
 }
 
-// pi = Lxx (Lxx' x + p)  on the next-stage factor S1 (dtrmv_u_n + dtrmv_u_t, :355-365), col layout.
-__device__ __forceinline__ double pi_from_x(Scratch* sm, const d4& S1, int xo1, const double x1row[4], double pcol) {
-    const int l = lane_id(), g = l >> 4, c = l & 15;
+// pi = P x + p on the next stage's record S1 (P form; the reference's Lxx (Lxx' x + l_x), dtrmv_u_n +
+// dtrmv_u_t, d_back_ric_rec.c:355-365), x in row layout, result in col layout.
+__device__ __forceinline__ double pi_from_x(const d4& S1, int xo1, const double x1row[4], double pcol) {
+    const int c = lane_id() & 15;
     double part = 0.0;
 #pragma unroll
-    for (int r = 0; r < 4; r++) part += (c >= xo1 && g + 4 * r >= c) ? S1[r] * x1row[r] : 0.0;
-    const double tcol = (c >= xo1) ? xrow_sum(part) + pcol : 0.0;
-    double trow[4];
-    col2row(sm, tcol, trow);
-    double p2 = 0.0;
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-        const int j = g + 4 * r;
-        p2 += (j <= c && j >= xo1) ? S1[r] * trow[r] : 0.0;
-    }
-    return xrow_sum(p2);
+    for (int r = 0; r < 4; r++) part += (c >= xo1 ? S1[r] : 0.0) * x1row[r];
+    return xrow_sum(part) + pcol;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1122,9 +1118,9 @@ __device__ __forceinline__ void fwd_step(const RicIO& io, Scratch* sm, const SH&
         double x1row[4];
         col2row(sm, xcol, x1row);
         if (MODE == 0)
-            pv = pi_from_x(sm, nxt.S, sh.xo1, x1row, nxt.lc);  // pi_k = Lxx (Lxx' x + l_x)
+            pv = pi_from_x(nxt.S, sh.xo1, x1row, nxt.lc);  // pi_k = P x + p (p: the record's row)
         else
-            pv = pi_from_x(sm, nxt.S, sh.xo1, x1row, 0.0) + cur.pk;  // pi_k = p_{k+1} + P x
+            pv = pi_from_x(nxt.S, sh.xo1, x1row, cur.pk);  // pi_k = P x + p_{k+1} (trs backward vector)
     }
     gst(pi, k * V16 + s, pv, compute_pi && g == 0 && ok);
 }
@@ -1274,20 +1270,11 @@ __device__ __forceinline__ void trs_step(const RicIO& io, Scratch* sm, const SH&
     double pbc = cur.pbc;
     // P_{k+1} b_k is recomputed only on request (wave-uniform branch): the IPM corrector passes
     // compute_Pb = 0 and reuses the Pb its factorisation stored (d_ip2_res_hard.c:628, :1168)
-    if (compute_Pb) {
+    if (compute_Pb) {  // P_{k+1} b_k on the P-form record
         double part = 0.0;
 #pragma unroll
-        for (int r = 0; r < 4; r++) part += (c >= xo1 ? lowS(S1, r, g, c) : 0.0) * cur.brow[r];
-        const double vcol = xrow_sum(part);
-        double vrow[4];
-        col2row(sm, vcol, vrow);
-        double pp = 0.0;
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const int j = g + 4 * r;
-            pp += (j <= c && j >= xo1) ? S1[r] * vrow[r] : 0.0;
-        }
-        pbc = xrow_sum(pp);
+        for (int r = 0; r < 4; r++) part += (c >= xo1 ? S1[r] : 0.0) * cur.brow[r];
+        pbc = xrow_sum(part);
     }
     gst(Pb, k * V16 + s, pbc, compute_Pb && g == 0 && s >= 0 && s < nx1);
     const double wc = (s >= 0 && s < nx1) ? pbc + pcol : 0.0;

@@ -336,17 +336,21 @@ def compare_ipm(case_like_qp, a, b, tol=TOL_IPM, allow_divergent=False):
 
     A primal-dual divergence (the oracle stops on alpha_min, ret 2, with |lam| > 1e12: an infeasible QP whose
     lam runs to 1e33) amplifies last-bit differences without bound -- the oracle and the reference build itself
-    differ by O(1) there -- so only kk and ret are comparable.  That escape is taken only where the caller
+    differ by O(1) there -- so only ret (and kk to +-2) are comparable.  That escape is taken only where the caller
     allows it (allow_divergent, for deliberately sampled non-converged problems), and every use is recorded in
     DIVERGENT_SKIPS; a converged problem (ret 0) can never take it."""
     qp = case_like_qp
-    assert a["kk"] == b["kk"] and a["ret"] == b["ret"], (a["kk"], b["kk"], a["ret"], b["ret"])
+    assert a["ret"] == b["ret"], (a["kk"], b["kk"], a["ret"], b["ret"])
     if b["ret"] == 2:
         lam_max = max(float(np.max(np.abs(x))) for x in b["lam"])
         if lam_max > 1e12:
             assert allow_divergent, f"oracle diverged (ret 2, |lam| = {lam_max:.1e}) on a case that must compare"
+            # the iteration at which the step length of a divergence (lam growing ~10x per iteration) falls
+            # below alpha_min is itself set by amplified last bits: +-2 iterations, same exit code
+            assert abs(a["kk"] - b["kk"]) <= 2, (a["kk"], b["kk"])
             DIVERGENT_SKIPS.append((int(b["kk"]), lam_max))
             return 0.0
+    assert a["kk"] == b["kk"], (a["kk"], b["kk"], a["ret"], b["ret"])
     e = 0.0
     for k in range(qp.N + 1):
         n = qp.nux(k)
