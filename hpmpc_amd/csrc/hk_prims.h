@@ -49,13 +49,12 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
 __device__ __forceinline__ double mk(int hi, int lo) { return __hiloint2double(hi, lo); }
 
-// DPP move of a double (two v_mov_b32_dpp); CTRL is the DPP control word.
+// DPP move of a double; CTRL is the DPP control word.  row_newbcast (0x150 + lane) is one v_mov_b64_dpp
+// on gfx950 (DPP64); the other controls split into two v_mov_b32_dpp.
 template <int CTRL>
 __device__ __forceinline__ double dpp_mov(double x) {
-    int lo = __double2loint(x), hi = __double2hiint(x);
-    lo = __builtin_amdgcn_mov_dpp(lo, CTRL, 0xf, 0xf, true);
-    hi = __builtin_amdgcn_mov_dpp(hi, CTRL, 0xf, 0xf, true);
-    return mk(hi, lo);
+    const long v = __builtin_bit_cast(long, x);
+    return __builtin_bit_cast(double, (long)__builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, true));
 }
 
 // broadcast lane P of every 16-lane row to the whole row (DPP row_newbcast, gfx90a+)

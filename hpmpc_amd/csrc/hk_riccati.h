@@ -837,11 +837,12 @@ __device__ void ric_backward(const RicIO& io, Scratch* sm, int update_b, const d
         bwd_fetch<AUG, BM>(io, sh, io.N, update_b, bsrc, update_q, qsrc, bc, cur);
         if constexpr (BM == BX_P2R) bwd_residual(io, sm, sh, io.N, bc, cur, true);
     });
-    for (int k = io.N; k >= 0; k--) {
+    // One stage: prefetch stage kn into `nxt` while stage k runs on `cur`.  The loop is unrolled by two
+    // with the fragments swapping roles, so no stage pays a register copy of the prefetched fragment.
+    auto stage = [&](int k, const BwdFrag& cur, BwdFrag& nxt) __attribute__((always_inline)) {
         HK_STAMP(0, k);
         const int kn = k > 0 ? k - 1 : 0;  // unconditional prefetch (stage 0 re-read on the last pass)
         const StageInfo sn = load_stage(io.st, kn);
-        BwdFrag nxt;
         with_shape<FX>(sn, [&](const auto& sh) { bwd_fetch<AUG, BM>(io, sh, kn, update_b, bsrc, update_q, qsrc, bc, nxt); });
         // factor of stage k+1 (still in registers): stored one stage late, behind the prefetch, so
         // that no s_waitcnt of this stage has to wait for the store acknowledgements
@@ -855,7 +856,13 @@ __device__ void ric_backward(const RicIO& io, Scratch* sm, int update_b, const d
             with_shape<FX>(sn, [&](const auto& sh) { bwd_residual(io, sm, sh, kn, bc, nxt, k > 0); });
         HK_STAMP(4, k);
         si = sn;
-        cur = nxt;
+    };
+    BwdFrag alt;
+    for (int k = io.N;;) {
+        stage(k, cur, alt);
+        if (--k < 0) break;
+        stage(k, alt, cur);
+        if (--k < 0) break;
     }
     store_factor(io.F, S, AUG ? ml_prev : 0.0, invd_prev, kg_prev);
 }
@@ -1133,25 +1140,35 @@ __device__ void ric_forward(const RicIO& io, Scratch* sm, const double* bsrc, in
                             int compute_pi, double* pi, const BoxCtx& bc, double& al) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
     double xcol = 0.0;  // x_k in col layout (stage-k tile coords)
-    FwdFrag cur, nxt;
-    fwd_fetch_k<MODE, FM, FX>(io, 0, bsrc, use_bsrc, ux, compute_pi, bc, cur);
-    fwd_fetch_k<MODE, FM, FX>(io, 1, bsrc, use_bsrc, ux, compute_pi, bc, nxt);
-    for (int k = 0; k < io.N; k++) {
+    // Stage k runs on fa (its record) and fb (stage k+1's, for pi) while stage k+2 is fetched into fc; the
+    // loop is unrolled by three with the fragments rotating roles (no register copies between stages).
+    FwdFrag f0, f1, f2;
+    fwd_fetch_k<MODE, FM, FX>(io, 0, bsrc, use_bsrc, ux, compute_pi, bc, f0);
+    fwd_fetch_k<MODE, FM, FX>(io, 1, bsrc, use_bsrc, ux, compute_pi, bc, f1);
+    auto stage = [&](int k, const FwdFrag& fa, const FwdFrag& fb, FwdFrag& fc) __attribute__((always_inline)) {
         HK_STAMP(8, k);
-        FwdFrag nn;
-        fwd_fetch_k<MODE, FM, FX>(io, k + 2 <= io.N ? k + 2 : io.N, bsrc, use_bsrc, ux, compute_pi, bc, nn);
+        fwd_fetch_k<MODE, FM, FX>(io, k + 2 <= io.N ? k + 2 : io.N, bsrc, use_bsrc, ux, compute_pi, bc, fc);
         const StageInfo si = load_stage(io.st, k);
         with_shape<FX>(si, [&](const auto& sh) {
-            fwd_step<MODE, FM>(io, sm, sh, k, cur, nxt, xcol, ux, compute_pi, pi, bc, al);
+            fwd_step<MODE, FM>(io, sm, sh, k, fa, fb, xcol, ux, compute_pi, pi, bc, al);
         });
         HK_STAMP(12, k);
-        cur = nxt;
-        nxt = nn;
-    }
+    };
     const StageInfo sN = load_stage(io.st, io.N);
-    const int v = tile_var(c, sN.nu, sN.nx, sN.xo);
-    gst(ux, io.N * V16 + v, xcol, g == 0 && v >= 0);
-    box_alpha<FM>(bc, cur, xcol, al);  // stage N: nu = 0, every tile is a state
+    auto finish = [&](const FwdFrag& fN) __attribute__((always_inline)) {  // stage N: nu = 0, every tile a state
+        const int v = tile_var(c, sN.nu, sN.nx, sN.xo);
+        gst(ux, io.N * V16 + v, xcol, g == 0 && v >= 0);
+        box_alpha<FM>(bc, fN, xcol, al);
+    };
+    for (int k = 0;;) {
+        if (k >= io.N) { finish(f0); break; }
+        stage(k, f0, f1, f2);
+        if (++k >= io.N) { finish(f1); break; }
+        stage(k, f1, f2, f0);
+        if (++k >= io.N) { finish(f2); break; }
+        stage(k, f2, f0, f1);
+        ++k;
+    }
     if (FM != BX_NONE && sN.ng > 0) gen_alpha<FM>(io, DynSh(sN), io.N, bc, xcol, al);
 }
 
@@ -1319,14 +1336,21 @@ __device__ void ric_trs(const RicIO& io, Scratch* sm, const double* hb, const do
         const StageInfo s1 = load_stage(io.st, io.N - 1);
         with_shape<FX>(s1, [&](const auto& sh) { trs_fetch<TM>(io, sh, io.N - 1, hb, hq, bc, compute_Pb, Pb, nxt); });
     }
-    for (int k = io.N - 1; k >= 0; k--) {
-        cur = nxt;
+    // stage k on fa while stage k-1 is fetched into fb; unrolled by two, the fragments swap roles
+    auto stage = [&](int k, const TrsFrag& fa, TrsFrag& fb) __attribute__((always_inline)) {
         const int kn = k > 0 ? k - 1 : 0;
         const StageInfo sn = load_stage(io.st, kn);
-        with_shape<FX>(sn, [&](const auto& sh) { trs_fetch<TM>(io, sh, kn, hb, hq, bc, compute_Pb, Pb, nxt); });
+        with_shape<FX>(sn, [&](const auto& sh) { trs_fetch<TM>(io, sh, kn, hb, hq, bc, compute_Pb, Pb, fb); });
         asm volatile("" ::: "memory");
         const StageInfo si = load_stage(io.st, k);
-        with_shape<FX>(si, [&](const auto& sh) { trs_step<TM>(io, sm, sh, k, cur, bc, ux, compute_Pb, Pb, S1, pcol); });
+        with_shape<FX>(si, [&](const auto& sh) { trs_step<TM>(io, sm, sh, k, fa, bc, ux, compute_Pb, Pb, S1, pcol); });
+    };
+    for (int k = io.N - 1;;) {
+        if (k < 0) break;
+        stage(k, nxt, cur);
+        if (--k < 0) break;
+        stage(k, cur, nxt);
+        --k;
     }
     __syncthreads();  // hux_k written by row group 0 is re-read by every lane below
     // ---- forward
