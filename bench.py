@@ -264,7 +264,73 @@ def bench_pcond(args, torch, red, rank, world, barrier):
         kern[n]["traffic_bytes_per_launch"] = pcond_traffic(n, B)
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_pcond_baseline(qp, N2, args.cpu_seconds * 0.5, args.cpu_threads)
+    out["ipm"] = bench_pcond_ipm(args, torch, red, rank, world, barrier)
     return out
+
+
+def bench_pcond_ipm(args, torch, red, rank, world, barrier):
+    """configs[4] with box constraints: d_part_cond (inner state boxes become the condensed problem's general
+    constraints, ng2 = 108 per block) -> d_ip2_res_mpc_hard_tv on the condensed N2=20 system (nu2=60 nx2=24,
+    the batched wide-stage IPM: one 256-thread workgroup per problem, one launch) -> d_part_expand_solution, on
+    the same 512-problem batch shape.  value = IP iterations per second of the condensed IPMs."""
+    from hpmpc_amd.pcond import PcondSolver
+    from hpmpc_amd.shard import make_shard
+
+    B, N, nx, nu, N2 = args.pcond_batch, 200, 24, 6, 20
+    k_max = 50
+    qp = make_shard(N, nx, nu, rank, world, B, boxes=True)
+    s = PcondSolver(qp, N2)
+    s.solve_ipm(k_max=k_max)  # warmup (plans, workspaces)
+    stream = torch.cuda.current_stream()
+    K = max(1, min(args.steps, 3))
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(K)]
+    iters = 0.0
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(K):
+        ev[i][0].record(stream)
+        s.condense()
+        ev[i][1].record(stream)
+        s.ipm(k_max=k_max)
+        ev[i][2].record(stream)
+        s.expand()
+        ev[i][3].record(stream)
+    barrier()
+    dt = red.max(time.perf_counter() - t0)
+    kk = s.kk2.cpu().numpy()
+    ret = s.ret2.cpu().numpy()
+    iters = red.sum(float(kk.sum()) * K)
+    ms = np.array([[e[j].elapsed_time(e[j + 1]) for j in range(3)] for e in ev]).mean(axis=0)
+    out = {"workload": f"pcond_ipm_N{N}_nx{nx}_nu{nu}_N2_{N2}_boxes_batch{B}", "value": iters / dt,
+           "unit": "IP-iter/s", "solves_per_s": B * world * K / dt, "ms_per_step": dt / K * 1e3, "steps": K,
+           "k_max": k_max, "condensed": {"N2": N2, "nu2": nu * (N // N2), "nx2": nx,
+                                         "ng2": int(sum(int(qp.nb[k]) - nu for k in range(1, N // N2)))},
+           "ms": {"hk_pcond": float(ms[0]), "hk_wide_ipm": float(ms[1]), "hk_pexpand": float(ms[2])},
+           "sum_kk_per_step": float(kk.sum()),
+           "ret_counts": {str(int(v)): int((ret == v).sum()) for v in np.unique(ret)}}
+    if rank == 0 and world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_pcond_ipm_baseline(qp, N2, k_max, args.cpu_seconds * 0.25)
+    return out
+
+
+def cpu_pcond_ipm_baseline(qp, N2, k_max, seconds):
+    """The oracle's d_part_cond -> d_ip2_res_mpc_hard_tv -> d_part_expand_solution, one host thread, over the
+    first problems of the batch until `seconds` have elapsed (the reference's own c99 condensing cannot serve:
+    it is numerically wrong for nu > 4)."""
+    from hpmpc_amd.cabi import HpmpcAPI, load
+
+    api = HpmpcAPI(load(os.path.join(ROOT, "oracle", "liboracle.so")), "orc_")
+    n, it, t0 = 0, 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds and n < qp.batch:
+        one = qp.problem(n)
+        c, _ = api.part_cond(one.copy(), N2)
+        r = api.ipm(c, k_max=k_max)
+        api.part_expand(one, c, r["ux"], r["pi"], r["lam"], r["t"])
+        it += r["kk"]
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": it / dt, "unit": "IP-iter/s", "cores": 1, "kind": "port",
+            "sample": f"first {n} problems of the batch, oracle (clean-room C) pipeline, {dt:.1f} s"}
 
 
 def bench_single_qp(args, torch, stream):
