@@ -45,6 +45,8 @@ def main(root, out):
         if "SQ_VALU_MFMA_BUSY_CYCLES" in m and "GRBM_GUI_ACTIVE" in m and m["GRBM_GUI_ACTIVE"]:
             simd_cycles = m["GRBM_GUI_ACTIVE"] / 8.0 * 256 * 4
             d["mfma_busy_frac_of_simd_cycles"] = m["SQ_VALU_MFMA_BUSY_CYCLES"] / simd_cycles
+        if "TA_TA_BUSY_sum" in m and "GRBM_GUI_ACTIVE" in m and m["GRBM_GUI_ACTIVE"]:
+            d["ta_busy_frac_of_cu_cycles"] = m["TA_TA_BUSY_sum"] / (m["GRBM_GUI_ACTIVE"] / 8.0 * 256)
         res["kernels"][k] = d
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
