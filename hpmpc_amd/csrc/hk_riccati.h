@@ -843,7 +843,9 @@ __device__ void ric_backward(const RicIO& io, Scratch* sm, int update_b, const d
         HK_STAMP(0, k);
         const int kn = k > 0 ? k - 1 : 0;  // unconditional prefetch (stage 0 re-read on the last pass)
         const StageInfo sn = load_stage(io.st, kn);
+        HK_STAMP(5, k);
         with_shape<FX>(sn, [&](const auto& sh) { bwd_fetch<AUG, BM>(io, sh, kn, update_b, bsrc, update_q, qsrc, bc, nxt); });
+        HK_STAMP(6, k);
         // factor of stage k+1 (still in registers): stored one stage late, behind the prefetch, so
         // that no s_waitcnt of this stage has to wait for the store acknowledgements
         store_factor(io.F + (long)(k + 1) * FSTRIDE, S, AUG ? ml_prev : 0.0, invd_prev, kg_prev, k < io.N);
