@@ -772,7 +772,8 @@ __device__ __forceinline__ void bwd_step(const RicIO& io, Scratch* sm, const SH&
 #pragma unroll
         for (int kc = 0; kc < 4; kc++) {
             if (4 * kc + 3 < xo1 || 4 * kc >= xo1 + nx1) continue;  // uniform
-            const double aop = xc ? S[kc] : 0.0;
+            // lanes c < xo1 (u rows of stage k+1) only produce rows of T' that the second chain skips: no mask
+            const double aop = S[kc];
             if (kc & 1)
                 a1 = mfma(aop, cur.bop[kc], a1);
             else
@@ -796,7 +797,7 @@ __device__ __forceinline__ void bwd_step(const RicIO& io, Scratch* sm, const SH&
         // never skipped: the row update below needs it anyway
         double part = 0.0;
 #pragma unroll
-        for (int r = 0; r < 4; r++) part += (xc ? S[r] : 0.0) * brow[r];
+        for (int r = 0; r < 4; r++) part += S[r] * brow[r];  // columns c < xo1: unused (masked below)
         const double pb = xrow_sum(part);
         gst(Pb, k * V16 + (c - xo1), pb, compute_Pb && live && g == 0 && xc && c < xo1 + nx1);
         // m_last += BAbt_k (P b + p_{k+1})
@@ -933,7 +934,7 @@ __device__ __forceinline__ double pi_from_x(const d4& S1, int xo1, const double 
     const int c = lane_id() & 15;
     double part = 0.0;
 #pragma unroll
-    for (int r = 0; r < 4; r++) part += (c >= xo1 ? S1[r] : 0.0) * x1row[r];
+    for (int r = 0; r < 4; r++) part += S1[r] * x1row[r];  // columns c < xo1 are never stored
     return xrow_sum(part) + pcol;
 }
 
@@ -1292,7 +1293,7 @@ __device__ __forceinline__ void trs_step(const RicIO& io, Scratch* sm, const SH&
     if (compute_Pb) {  // P_{k+1} b_k on the P-form record
         double part = 0.0;
 #pragma unroll
-        for (int r = 0; r < 4; r++) part += (c >= xo1 ? S1[r] : 0.0) * cur.brow[r];
+        for (int r = 0; r < 4; r++) part += S1[r] * cur.brow[r];  // columns c < xo1: masked at use
         pbc = xrow_sum(part);
     }
     gst(Pb, k * V16 + s, pbc, compute_Pb && g == 0 && s >= 0 && s < nx1);
