@@ -70,6 +70,22 @@ __device__ __forceinline__ void col2row(Scratch* sm, double vc, double vr[4]) {
     __builtin_amdgcn_wave_barrier();
 }
 
+// two col-layout values -> row layout in one LDS round trip
+__device__ __forceinline__ void col2row2(Scratch* sm, double ac, double bc, double ar[4], double br[4]) {
+    const int l = lane_id(), g = l >> 4, c = l & 15;
+    sm->v[c] = ac;
+    sm->v[16 + c] = bc;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        ar[r] = sm->v[g + 4 * r];
+        br[r] = sm->v[16 + g + 4 * r];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
 // row layout (reg r holds v[g+4r], replicated over the columns) -> col layout (lane (g,c) holds v[c])
 __device__ __forceinline__ double row2col(Scratch* sm, const double vr[4]) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
@@ -589,7 +605,7 @@ struct BwdFrag {
     BoxLane bl;
     // BX_P2R residual inputs: ux_k (col c / rows g+4r), pi_k (rows), pi_{k-1} (col), BAbt_k' (col
     // c-xo1 over rows g+4r), x_{k+1} (col)
-    double uc, ur[4], pr[4], pim1, bt[4], x1;
+    double uc, pc, pim1, bt[4], x1;
 };
 
 template <bool AUG, int BM, class SH>
@@ -649,14 +665,13 @@ __device__ __forceinline__ void bwd_fetch(const RicIO& io, const SH& sh, int k, 
         static_assert(BM != BX_P2R || AUG, "residual right-hand sides need the augmented row");
         const int sc = c - sh.xo1;
         const bool oks = live && sc >= 0 && sc < sh.nx1;
+        // ux_k and pi_k in col layout (the residual turns them into row layout through LDS: two loads
+        // instead of eight row-layout loads with four distinct addresses each)
         f.uc = ldsel(bc.ux, k * V16 + vc, vc >= 0);
+        f.pc = ldsel(bc.pi, k * V16 + sc, oks);
 #pragma unroll
         for (int r = 0; r < 4; r++) {
             const int vi = tile_var(g + 4 * r, sh.nu, sh.nx, sh.xo);
-            const int sr = 4 * r + g - sh.xo1;
-            const bool okr = live && sr >= 0 && sr < sh.nx1;
-            f.ur[r] = ldsel(bc.ux, k * V16 + vi, vi >= 0);
-            f.pr[r] = ldsel(bc.pi, k * V16 + sr, okr);
             f.bt[r] = ldsel(Bk, lib4_idx(sh.sdB, vi, sc), oks && vi >= 0);
         }
         f.pim1 = ldsel(bc.pi, (k - 1) * V16 + (vc - sh.nu), k > 0 && vc >= sh.nu);
@@ -714,14 +729,16 @@ __device__ __forceinline__ void bwd_residual(const RicIO& io, Scratch* sm, const
     double h = f.mlq;
     if (k > 0 && vc >= sh.nu) h -= f.pim1;
     if (f.bl.ok) h += -f.bx[0] + f.bx[1];
+    double ur[4], pr[4];  // ux_k (tile rows g+4r) and pi_k (stage-(k+1) tile rows g+4r) in row layout
+    col2row2(sm, f.uc, f.pc, ur, pr);
     double part = 0.0, p2 = 0.0, p3 = 0.0;
 #pragma unroll
-    for (int r = 0; r < 4; r++) part += f.Mi[r] * f.ur[r];
+    for (int r = 0; r < 4; r++) part += f.Mi[r] * ur[r];
     h += xrow_sum(part);
 #pragma unroll
     for (int r = 0; r < 4; r++) {
-        p2 += f.bop[r] * f.pr[r];
-        p3 += f.bt[r] * f.ur[r];
+        p2 += f.bop[r] * pr[r];
+        p3 += f.bt[r] * ur[r];
     }
     const double bpi = xrow_sum(p2);
     const double atu = xrow_sum(p3);
