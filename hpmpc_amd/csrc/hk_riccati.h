@@ -605,7 +605,7 @@ struct BwdFrag {
     BoxLane bl;
     // BX_P2R residual inputs: ux_k (col c / rows g+4r), pi_k (rows), pi_{k-1} (col), BAbt_k' (col
     // c-xo1 over rows g+4r), x_{k+1} (col)
-    double uc, pc, pim1, bt[4], x1;
+    double uc, pc, pim1, bt[4];
 };
 
 template <bool AUG, int BM, class SH>
@@ -675,7 +675,6 @@ __device__ __forceinline__ void bwd_fetch(const RicIO& io, const SH& sh, int k, 
             f.bt[r] = ldsel(Bk, lib4_idx(sh.sdB, vi, sc), oks && vi >= 0);
         }
         f.pim1 = ldsel(bc.pi, (k - 1) * V16 + (vc - sh.nu), k > 0 && vc >= sh.nu);
-        f.x1 = ldsel(bc.ux, (k + 1) * V16 + sh.nu1 + sc, oks);
         f.brow[0] = ldsel(Bk, lib4_idx(sh.sdB, nux, sc), oks);
     }
 }
@@ -719,8 +718,9 @@ __device__ __forceinline__ void box_hessian(const BoxCtx& bc, const BwdFrag& f, 
 //   r_q = q - [0; pi_{k-1}] + (lam_up - lam_lo) + RSQ ux + BAbt pi,   r_b = b - x_{k+1} + BAbt' ux
 // The factorisation's rows become (mlq, brow) = (r_q, r_b) (res_rhs) or the data's own (q, b).
 template <class SH>
+// x1c: x_{k+1} in col layout over stage-(k+1) tiles -- the ux_{k+1} the previous stage's fragment holds.
 __device__ __forceinline__ void bwd_residual(const RicIO& io, Scratch* sm, const SH& sh, int k, const BoxCtx& bc,
-                                             BwdFrag& f, bool store) {
+                                             BwdFrag& f, double x1c, bool store) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
     const bool live = SH::fixed || k < io.N;
     const int vc = tile_var(c, sh.nu, sh.nx, sh.xo);
@@ -746,7 +746,7 @@ __device__ __forceinline__ void bwd_residual(const RicIO& io, Scratch* sm, const
     if constexpr (!SH::fixed) {
         if (sh.ng > 0) h += gen_rq(io, sh, k, bc.lam);
     }
-    const double rb = f.brow[0] - f.x1 + atu;
+    const double rb = f.brow[0] - (oks ? x1c : 0.0) + atu;
     gst(bc.res_q, k * V16 + vc, h, store && g == 0 && vc >= 0);
     gst(bc.res_b, k * V16 + sc, rb, store && g == 0 && oks);
     f.mlq = bc.res_rhs ? h : f.mlq;
@@ -853,7 +853,7 @@ __device__ void ric_backward(const RicIO& io, Scratch* sm, int update_b, const d
     BwdFrag cur;
     with_shape<FX>(si, [&](const auto& sh) {
         bwd_fetch<AUG, BM>(io, sh, io.N, update_b, bsrc, update_q, qsrc, bc, cur);
-        if constexpr (BM == BX_P2R) bwd_residual(io, sm, sh, io.N, bc, cur, true);
+        if constexpr (BM == BX_P2R) bwd_residual(io, sm, sh, io.N, bc, cur, 0.0, true);
     });
     // One stage: prefetch stage kn into `nxt` while stage k runs on `cur`.  The loop is unrolled by two
     // with the fragments swapping roles, so no stage pays a register copy of the prefetched fragment.
@@ -873,7 +873,7 @@ __device__ void ric_backward(const RicIO& io, Scratch* sm, int update_b, const d
             bwd_step<AUG, BM>(io, sm, sh, k, cur, bc, compute_Pb, Pb, S, ml_prev, invd_prev, kg_prev);
         });
         if constexpr (BM == BX_P2R)
-            with_shape<FX>(sn, [&](const auto& sh) { bwd_residual(io, sm, sh, kn, bc, nxt, k > 0); });
+            with_shape<FX>(sn, [&](const auto& sh) { bwd_residual(io, sm, sh, kn, bc, nxt, cur.uc, k > 0); });
         HK_STAMP(4, k);
         si = sn;
     };
