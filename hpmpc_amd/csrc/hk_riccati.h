@@ -985,9 +985,9 @@ __device__ __forceinline__ void fwd_fetch(const RicIO& io, const SH& sh, int k, 
     // S[0] (tile rows 0..3) holds the u block's columns of L: a fixed-shape stage (nu <= 4, xo = 4) solves
     // its u block in gain form, and pi_from_x reads rows >= xo only, so S[0] is never needed there
 #pragma unroll
-    for (int r = 0; r < 4; r++) f.S[r] = gld(Fk, r * 64 + l, needS && (r > 0 || !SH::fixed));
+    for (int r = 0; r < 4; r++) f.S[r] = (SH::fixed && r == 0) ? 0.0 : gld(Fk, r * 64 + l, needS);
     f.lc = gld(Fk, 256 + c, MODE == 0);
-    f.invd = gld(Fk, 272 + c, !SH::fixed);
+    f.invd = SH::fixed ? 0.0 : gld(Fk, 272 + c);
     f.kg = gld(Fk, 288 + l);
     const int kk = k < io.N ? k : io.N - 1;  // stage N has no BAbt block: loads clamped, values masked
     const bool live = k < io.N;
@@ -1214,15 +1214,19 @@ struct TrsFrag {
     BoxLane bl;
 };
 
-template <int TM, class SH>
+// RPB = false: the caller never recomputes P b (the IPM corrector reuses the stored Pb), so the loads that
+// only serve that product are not issued at all.
+template <int TM, bool RPB, class SH>
 __device__ __forceinline__ void trs_fetch(const RicIO& io, const SH& sh, int k, const double* hb, const double* hq,
-                                          const BoxCtx& bc, int compute_Pb, const double* Pb, TrsFrag& f) {
+                                          const BoxCtx& bc, int compute_Pb_, const double* Pb, TrsFrag& f) {
+    const int compute_Pb = RPB ? compute_Pb_ : 0;
     const int l = lane_id(), g = l >> 4, c = l & 15;
     const double* Fk = io.F + (long)k * FSTRIDE;
     // the n-form solve of a fixed-shape stage runs over its u pivots (< 4), i.e. reads S[0] only; rows
     // 4..15 are needed by the generic solve and by P_{k} b_{k-1} (compute_Pb, the KKT re-solve)
 #pragma unroll
-    for (int r = 0; r < 4; r++) f.S[r] = gld(Fk, r * 64 + l, r == 0 || !SH::fixed || compute_Pb);
+    for (int r = 0; r < 4; r++)
+        f.S[r] = (SH::fixed && !RPB && r > 0) ? 0.0 : gld(Fk, r * 64 + l, r == 0 || !SH::fixed || compute_Pb);
     f.invd = gld(Fk, 272 + c);
     const int nux = sh.nu + sh.nx;
     const int vc = tile_var(c, sh.nu, sh.nx, sh.xo);
@@ -1264,7 +1268,7 @@ __device__ __forceinline__ void trs_fetch(const RicIO& io, const SH& sh, int k, 
         const int sr = g + 4 * r - sh.xo1;
         const bool ok = live && sr >= 0 && sr < sh.nx1;
         f.bop[r] = ldsel(Bk, lib4_idx(sh.sdB, vc, sr), ok && vc >= 0);
-        f.brow[r] = ldsel(bp, hb ? sr : lib4_idx(sh.sdB, nux, sr), ok && compute_Pb);
+        f.brow[r] = RPB ? ldsel(bp, hb ? sr : lib4_idx(sh.sdB, nux, sr), ok && compute_Pb) : 0.0;
     }
     const int s = c - sh.xo1;
     f.pbc = ldsel(Pb + k * V16, s, !compute_Pb && live && s >= 0 && s < sh.nx1);
@@ -1296,10 +1300,11 @@ __device__ __forceinline__ double box_gradient(const BoxCtx& bc, const TrsFrag& 
 }
 
 // One backward trs stage k < N: hux_k = q_k + box + BAbt_k (P_{k+1} b_k + p_{k+1}), then the solve.
-template <int TM, class SH>
+template <int TM, bool RPB, class SH>
 __device__ __forceinline__ void trs_step(const RicIO& io, Scratch* sm, const SH& sh, int k, const TrsFrag& cur,
-                                         const BoxCtx& bc, double* ux, int compute_Pb, double* Pb, d4& S1,
+                                         const BoxCtx& bc, double* ux, int compute_Pb_, double* Pb, d4& S1,
                                          double& pcol) {
+    const int compute_Pb = RPB ? compute_Pb_ : 0;
     const int l = lane_id(), g = l >> 4, c = l & 15;
     const int xo1 = sh.xo1, nx1 = sh.nx1;
     const int vc = tile_var(c, sh.nu, sh.nx, sh.xo);
@@ -1335,14 +1340,14 @@ __device__ __forceinline__ void trs_step(const RicIO& io, Scratch* sm, const SH&
 // hb: state order, hq: variable order (null: the BAbt / RSQrq augmented rows), TM: box gradient term;
 // ux (variable order) doubles as the backward work vector exactly like hux in the reference.
 // FM != BX_NONE: box steps + step-length candidate `al` in the forward substitution.
-template <int TM, int FM, class FX>
+template <int TM, int FM, class FX, bool RPB = true>
 __device__ void ric_trs(const RicIO& io, Scratch* sm, const double* hb, const double* hq, const BoxCtx& bc,
                         double* ux, int compute_pi, double* pi, int compute_Pb, double* Pb, double& al) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
     // ---- backward
     TrsFrag cur;
     const StageInfo sN = load_stage(io.st, io.N);
-    with_shape<FX>(sN, [&](const auto& sh) { trs_fetch<TM>(io, sh, io.N, hb, hq, bc, compute_Pb, Pb, cur); });
+    with_shape<FX>(sN, [&](const auto& sh) { trs_fetch<TM, RPB>(io, sh, io.N, hb, hq, bc, compute_Pb, Pb, cur); });
     double hN = cur.h0 + box_gradient<TM>(bc, cur);
     if (sN.ng > 0) hN += gen_gradient<TM>(io, DynSh(sN), io.N, bc);
     {
@@ -1354,16 +1359,16 @@ __device__ void ric_trs(const RicIO& io, Scratch* sm, const double* hb, const do
     TrsFrag nxt;
     {
         const StageInfo s1 = load_stage(io.st, io.N - 1);
-        with_shape<FX>(s1, [&](const auto& sh) { trs_fetch<TM>(io, sh, io.N - 1, hb, hq, bc, compute_Pb, Pb, nxt); });
+        with_shape<FX>(s1, [&](const auto& sh) { trs_fetch<TM, RPB>(io, sh, io.N - 1, hb, hq, bc, compute_Pb, Pb, nxt); });
     }
     // stage k on fa while stage k-1 is fetched into fb; unrolled by two, the fragments swap roles
     auto stage = [&](int k, const TrsFrag& fa, TrsFrag& fb) __attribute__((always_inline)) {
         const int kn = k > 0 ? k - 1 : 0;
         const StageInfo sn = load_stage(io.st, kn);
-        with_shape<FX>(sn, [&](const auto& sh) { trs_fetch<TM>(io, sh, kn, hb, hq, bc, compute_Pb, Pb, fb); });
+        with_shape<FX>(sn, [&](const auto& sh) { trs_fetch<TM, RPB>(io, sh, kn, hb, hq, bc, compute_Pb, Pb, fb); });
         asm volatile("" ::: "memory");
         const StageInfo si = load_stage(io.st, k);
-        with_shape<FX>(si, [&](const auto& sh) { trs_step<TM>(io, sm, sh, k, fa, bc, ux, compute_Pb, Pb, S1, pcol); });
+        with_shape<FX>(si, [&](const auto& sh) { trs_step<TM, RPB>(io, sm, sh, k, fa, bc, ux, compute_Pb, Pb, S1, pcol); });
     };
     for (int k = io.N - 1;;) {
         if (k < 0) break;

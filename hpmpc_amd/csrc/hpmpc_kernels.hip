@@ -641,10 +641,11 @@ __global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_corr(KArgs a) {
     v.bc.smu = st[S_SMU];
     double al = 1.0;
     if (phase == 1)
-        ric_trs<BX_P1, BX_P1, FX>(v.io, &sm, nullptr, nullptr, v.bc, v.w.dux, a.compute_mult, v.w.dpi, 0, v.w.Pb, al);
+        ric_trs<BX_P1, BX_P1, FX, false>(v.io, &sm, nullptr, nullptr, v.bc, v.w.dux, a.compute_mult, v.w.dpi, 0, v.w.Pb,
+                                         al);
     else
-        ric_trs<BX_P2, BX_P2, FX>(v.io, &sm, v.w.res_b, v.w.res_q, v.bc, v.w.dux, a.compute_mult, v.w.dpi, 0, v.w.Pb,
-                              al);
+        ric_trs<BX_P2, BX_P2, FX, false>(v.io, &sm, v.w.res_b, v.w.res_q, v.bc, v.w.dux, a.compute_mult, v.w.dpi, 0,
+                                         v.w.Pb, al);
     al = wave_min(al);
     if (v.l == 0) {
         v.stat[5 * kk] = st[S_SIGMA];
