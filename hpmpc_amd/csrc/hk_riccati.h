@@ -972,10 +972,12 @@ struct FwdFrag {
 
 // Fetch of stage k (sh: shape of stage min(k, N-1), whose BAbt block the pass reads; pnbk: pnb of k).
 // mode 0: sv (b from update_b source or the BAbt row); mode 1: trs (b from hb or the BAbt row, plus hc/pk)
-template <int MODE, int FM, class SH>
+// RPI = false: the caller never asks for pi (the IPM predictor), so the record rows pi would read are not loaded.
+template <int MODE, int FM, bool RPI, class SH>
 __device__ __forceinline__ void fwd_fetch(const RicIO& io, const SH& sh, int k, int pnbk, const double* bsrc,
-                                          int use_bsrc, const double* ux, int compute_pi, const BoxCtx& bc,
+                                          int use_bsrc, const double* ux, int compute_pi_, const BoxCtx& bc,
                                           FwdFrag& f) {
+    const int compute_pi = RPI ? compute_pi_ : 0;
     const int l = lane_id(), g = l >> 4, c = l & 15;
     const double* Fk = io.F + (long)k * FSTRIDE;
     // The factor tile is read by the u-block solve of generic stages and by pi (compute_pi) only, inv_diag by
@@ -985,8 +987,8 @@ __device__ __forceinline__ void fwd_fetch(const RicIO& io, const SH& sh, int k, 
     // S[0] (tile rows 0..3) holds the u block's columns of L: a fixed-shape stage (nu <= 4, xo = 4) solves
     // its u block in gain form, and pi_from_x reads rows >= xo only, so S[0] is never needed there
 #pragma unroll
-    for (int r = 0; r < 4; r++) f.S[r] = (SH::fixed && r == 0) ? 0.0 : gld(Fk, r * 64 + l, needS);
-    f.lc = gld(Fk, 256 + c, MODE == 0);
+    for (int r = 0; r < 4; r++) f.S[r] = ((SH::fixed && (r == 0 || !RPI))) ? 0.0 : gld(Fk, r * 64 + l, needS);
+    f.lc = MODE == 0 ? gld(Fk, 256 + c) : 0.0;
     f.invd = SH::fixed ? 0.0 : gld(Fk, 272 + c);
     f.kg = gld(Fk, 288 + l);
     const int kk = k < io.N ? k : io.N - 1;  // stage N has no BAbt block: loads clamped, values masked
@@ -1038,14 +1040,14 @@ __device__ __forceinline__ void fwd_fetch(const RicIO& io, const SH& sh, int k, 
     }
 }
 
-template <int MODE, int FM, class FX>
+template <int MODE, int FM, class FX, bool RPI>
 __device__ __forceinline__ void fwd_fetch_k(const RicIO& io, int k, const double* bsrc, int use_bsrc,
                                             const double* ux, int compute_pi, const BoxCtx& bc, FwdFrag& f) {
     const int kk = k < io.N ? k : io.N - 1;
     const StageInfo sk = load_stage(io.st, kk);
     const int pnbk = k < io.N ? sk.pnb : load_stage(io.st, k).pnb;
     with_shape<FX>(sk, [&](const auto& sh) {
-        fwd_fetch<MODE, FM>(io, sh, k, pnbk, bsrc, use_bsrc, ux, compute_pi, bc, f);
+        fwd_fetch<MODE, FM, RPI>(io, sh, k, pnbk, bsrc, use_bsrc, ux, compute_pi, bc, f);
     });
 }
 
@@ -1155,7 +1157,7 @@ __device__ __forceinline__ void fwd_step(const RicIO& io, Scratch* sm, const SH&
 // Shared forward substitution (sv: rhs = -l_k ; trs: rhs = -hux_k), d_back_ric_rec.c:339-397 / :704-790.
 // ux: variable order; pi: state order.  FM != BX_NONE also computes the box steps of every stage and
 // the per-lane step-length candidate `al` (caller reduces it with wave_min).
-template <int MODE, int FM, class FX>
+template <int MODE, int FM, class FX, bool RPI = true>
 __device__ void ric_forward(const RicIO& io, Scratch* sm, const double* bsrc, int use_bsrc, double* ux,
                             int compute_pi, double* pi, const BoxCtx& bc, double& al) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
@@ -1163,11 +1165,11 @@ __device__ void ric_forward(const RicIO& io, Scratch* sm, const double* bsrc, in
     // Stage k runs on fa (its record) and fb (stage k+1's, for pi) while stage k+2 is fetched into fc; the
     // loop is unrolled by three with the fragments rotating roles (no register copies between stages).
     FwdFrag f0, f1, f2;
-    fwd_fetch_k<MODE, FM, FX>(io, 0, bsrc, use_bsrc, ux, compute_pi, bc, f0);
-    fwd_fetch_k<MODE, FM, FX>(io, 1, bsrc, use_bsrc, ux, compute_pi, bc, f1);
+    fwd_fetch_k<MODE, FM, FX, RPI>(io, 0, bsrc, use_bsrc, ux, compute_pi, bc, f0);
+    fwd_fetch_k<MODE, FM, FX, RPI>(io, 1, bsrc, use_bsrc, ux, compute_pi, bc, f1);
     auto stage = [&](int k, const FwdFrag& fa, const FwdFrag& fb, FwdFrag& fc) __attribute__((always_inline)) {
         HK_STAMP(8, k);
-        fwd_fetch_k<MODE, FM, FX>(io, k + 2 <= io.N ? k + 2 : io.N, bsrc, use_bsrc, ux, compute_pi, bc, fc);
+        fwd_fetch_k<MODE, FM, FX, RPI>(io, k + 2 <= io.N ? k + 2 : io.N, bsrc, use_bsrc, ux, compute_pi, bc, fc);
         const StageInfo si = load_stage(io.st, k);
         with_shape<FX>(si, [&](const auto& sh) {
             fwd_step<MODE, FM>(io, sm, sh, k, fa, fb, xcol, ux, compute_pi, pi, bc, al);
