@@ -646,8 +646,12 @@ __device__ __forceinline__ void bwd_fetch(const RicIO& io, const SH& sh, int k, 
         f.bx[1] = ldsel(bc.lam, b.up, b.ok);
         f.bx[2] = ldsel(bc.t, b.lo, b.ok);
         f.bx[3] = ldsel(bc.t, b.up, b.ok);
-        f.bx[4] = ldsel(bc.res_m, b.lo, b.ok);
-        f.bx[5] = ldsel(bc.res_m, b.up, b.ok);
+        // BX_P2R: r_m of the current iterate is lam * t, exactly the product the update pass stored
+        // (update_p2_pass), so it is formed at use instead of loaded
+        if (BM == BX_P2) {
+            f.bx[4] = ldsel(bc.res_m, b.lo, b.ok);
+            f.bx[5] = ldsel(bc.res_m, b.up, b.ok);
+        }
         f.bx[6] = ldsel(bc.res_d, b.lo, b.ok);
         f.bx[7] = ldsel(bc.res_d, b.up, b.ok);
     }
@@ -704,7 +708,9 @@ __device__ __forceinline__ void box_hessian(const BoxCtx& bc, const BwdFrag& f, 
         qxv = (AUG && b.ok) ? q : 0.0;
     } else if (BM == BX_P2 || BM == BX_P2R) {  // d_update_hessian_gradient_res_mpc_hard_tv
         const double til = rcp_nr(f.bx[2]), tiu = rcp_nr(f.bx[3]);
-        const double q = til * (f.bx[4] - f.bx[0] * f.bx[6]) - tiu * (f.bx[5] + f.bx[1] * f.bx[7]);
+        const double rml = BM == BX_P2R ? f.bx[0] * f.bx[2] : f.bx[4];
+        const double rmu = BM == BX_P2R ? f.bx[1] * f.bx[3] : f.bx[5];
+        const double q = til * (rml - f.bx[0] * f.bx[6]) - tiu * (rmu + f.bx[1] * f.bx[7]);
         gst(bc.t_inv, b.lo, til, st);
         gst(bc.t_inv, b.up, tiu, st);
         dq = b.ok ? til * f.bx[0] + tiu * f.bx[1] : 0.0;
