@@ -605,7 +605,7 @@ struct BwdFrag {
     BoxLane bl;
     // BX_P2R residual inputs: ux_k (col c / rows g+4r), pi_k (rows), pi_{k-1} (col), BAbt_k' (col
     // c-xo1 over rows g+4r), x_{k+1} (col)
-    double uc, pc, pim1, bt[4];
+    double uc, pc, pim1;
 };
 
 template <bool AUG, int BM, class SH>
@@ -673,11 +673,6 @@ __device__ __forceinline__ void bwd_fetch(const RicIO& io, const SH& sh, int k, 
         // instead of eight row-layout loads with four distinct addresses each)
         f.uc = ldsel(bc.ux, k * V16 + vc, vc >= 0);
         f.pc = ldsel(bc.pi, k * V16 + sc, oks);
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const int vi = tile_var(g + 4 * r, sh.nu, sh.nx, sh.xo);
-            f.bt[r] = ldsel(Bk, lib4_idx(sh.sdB, vi, sc), oks && vi >= 0);
-        }
         f.pim1 = ldsel(bc.pi, (k - 1) * V16 + (vc - sh.nu), k > 0 && vc >= sh.nu);
         f.brow[0] = ldsel(Bk, lib4_idx(sh.sdB, nux, sc), oks);
     }
@@ -737,6 +732,14 @@ __device__ __forceinline__ void bwd_residual(const RicIO& io, Scratch* sm, const
     if (f.bl.ok) h += -f.bx[0] + f.bx[1];
     double ur[4], pr[4];  // ux_k (tile rows g+4r) and pi_k (stage-(k+1) tile rows g+4r) in row layout
     col2row2(sm, f.uc, f.pc, ur, pr);
+    // BAbt_k' as a tile (reg r: BAbt_k[var(g+4r)][c - xo1]) is the transpose of the fragment's BAbt operand
+    // tile: identity MFMAs (exact) on the otherwise idle matrix unit instead of four more loads
+    d4 bt = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        if (4 * r + 3 < sh.xo1 || 4 * r >= sh.xo1 + sh.nx1) continue;  // uniform: chunk without a state
+        bt = mfma(f.bop[r], (c == 4 * r + g) ? 1.0 : 0.0, bt);
+    }
     double part = 0.0, p2 = 0.0, p3 = 0.0;
 #pragma unroll
     for (int r = 0; r < 4; r++) part += f.Mi[r] * ur[r];
@@ -744,7 +747,7 @@ __device__ __forceinline__ void bwd_residual(const RicIO& io, Scratch* sm, const
 #pragma unroll
     for (int r = 0; r < 4; r++) {
         p2 += f.bop[r] * pr[r];
-        p3 += f.bt[r] * ur[r];
+        p3 += bt[r] * ur[r];
     }
     const double bpi = xrow_sum(p2);
     const double atu = xrow_sum(p3);
