@@ -342,8 +342,7 @@ __device__ __forceinline__ void store_factor(double* Fk, const d4& S, double lc,
     const int l = lane_id(), g = l >> 4, c = l & 15;
 #pragma unroll
     for (int r = 0; r < 4; r++) gst(Fk, r * 64 + l, S[r], ok);
-    gst(Fk, 256 + c, lc, ok && g == 0);
-    gst(Fk, 272 + c, invd, ok && g == 0);
+    gst(Fk, 256 + 16 * g + c, g == 0 ? lc : invd, ok && g < 2);  // l (row group 0) and inv_diag (row group 1)
     gst(Fk, 288 + l, kg, ok);
 }
 
@@ -706,8 +705,7 @@ __device__ __forceinline__ void box_hessian(const BoxCtx& bc, const BwdFrag& f, 
         const double rml = BM == BX_P2R ? f.bx[0] * f.bx[2] : f.bx[4];
         const double rmu = BM == BX_P2R ? f.bx[1] * f.bx[3] : f.bx[5];
         const double q = til * (rml - f.bx[0] * f.bx[6]) - tiu * (rmu + f.bx[1] * f.bx[7]);
-        gst(bc.t_inv, b.lo, til, st);
-        gst(bc.t_inv, b.up, tiu, st);
+        gst(bc.t_inv, g == 0 ? b.lo : b.up, g == 0 ? til : tiu, b.ok && g < 2);  // lower / upper: one store
         dq = b.ok ? til * f.bx[0] + tiu * f.bx[1] : 0.0;
         qxv = (AUG && b.ok) ? q : 0.0;
     }
@@ -756,8 +754,11 @@ __device__ __forceinline__ void bwd_residual(const RicIO& io, Scratch* sm, const
         if (sh.ng > 0) h += gen_rq(io, sh, k, bc.lam);
     }
     const double rb = f.brow[0] - (oks ? x1c : 0.0) + atu;
-    gst(bc.res_q, k * V16 + vc, h, store && g == 0 && vc >= 0);
-    gst(bc.res_b, k * V16 + sc, rb, store && g == 0 && oks);
+    // r_q (row group 0) and r_b (row group 1) in one store: both live in the IPM workspace carve (hpmpc_kernels.hip
+    // carve: res_b = res_q + (N+1)*16), so r_b is a positive offset from r_q's base
+    const int db = (int)(bc.res_b - bc.res_q);
+    gst(bc.res_q, g == 0 ? k * V16 + vc : db + k * V16 + sc, g == 0 ? h : rb,
+        store && ((g == 0 && vc >= 0) || (g == 1 && oks)));
     f.mlq = bc.res_rhs ? h : f.mlq;
     double bcol = bc.res_rhs ? rb : f.brow[0];
     bcol = oks ? bcol : 0.0;
@@ -957,7 +958,7 @@ __device__ __forceinline__ double solve_ln(const SH& sh, const d4& S, double inv
 // pi = P x + p on the next stage's record S1 (P form; the reference's Lxx (Lxx' x + l_x), dtrmv_u_n +
 // dtrmv_u_t, d_back_ric_rec.c:355-365), x in row layout, result in col layout.
 __device__ __forceinline__ double pi_from_x(const d4& S1, int xo1, const double x1row[4], double pcol) {
-    const int c = lane_id() & 15;
+    (void)xo1;
     double part = 0.0;
 #pragma unroll
     for (int r = 0; r < 4; r++) part += S1[r] * x1row[r];  // columns c < xo1 are never stored
