@@ -982,12 +982,14 @@ struct FwdFrag {
 
 // Fetch of stage k (sh: shape of stage min(k, N-1), whose BAbt block the pass reads; pnbk: pnb of k).
 // mode 0: sv (b from update_b source or the BAbt row); mode 1: trs (b from hb or the BAbt row, plus hc/pk)
-// RPI = false: the caller never asks for pi (the IPM predictor), so the record rows pi would read are not loaded.
-template <int MODE, int FM, bool RPI, class SH>
+// PRED: the IPM predictor sweep.  It never asks for pi (the record rows pi would read are not loaded), and its
+// r_m is still lam * t as the update pass stored it (formed at use instead of loaded).  The step rule's 1/t is
+// recomputed from t in every sweep (bitwise the factorisation's stored t^-1: the same rcp_nr of the same t).
+template <int MODE, int FM, bool PRED, class SH>
 __device__ __forceinline__ void fwd_fetch(const RicIO& io, const SH& sh, int k, int pnbk, const double* bsrc,
                                           int use_bsrc, const double* ux, int compute_pi_, const BoxCtx& bc,
                                           FwdFrag& f) {
-    const int compute_pi = RPI ? compute_pi_ : 0;
+    const int compute_pi = PRED ? 0 : compute_pi_;
     const int l = lane_id(), g = l >> 4, c = l & 15;
     const double* Fk = io.F + (long)k * FSTRIDE;
     // The factor tile is read by the u-block solve of generic stages and by pi (compute_pi) only, inv_diag by
@@ -997,7 +999,7 @@ __device__ __forceinline__ void fwd_fetch(const RicIO& io, const SH& sh, int k, 
     // S[0] (tile rows 0..3) holds the u block's columns of L: a fixed-shape stage (nu <= 4, xo = 4) solves
     // its u block in gain form, and pi_from_x reads rows >= xo only, so S[0] is never needed there
 #pragma unroll
-    for (int r = 0; r < 4; r++) f.S[r] = ((SH::fixed && (r == 0 || !RPI))) ? 0.0 : gld(Fk, r * 64 + l, needS);
+    for (int r = 0; r < 4; r++) f.S[r] = ((SH::fixed && (r == 0 || PRED))) ? 0.0 : gld(Fk, r * 64 + l, needS);
     f.lc = MODE == 0 ? gld(Fk, 256 + c) : 0.0;
     f.invd = SH::fixed ? 0.0 : gld(Fk, 272 + c);
     f.kg = gld(Fk, 288 + l);
@@ -1035,35 +1037,35 @@ __device__ __forceinline__ void fwd_fetch(const RicIO& io, const SH& sh, int k, 
             f.bx[7] = ldsel(bc.lam, b.up, b.ok);
             f.bx[8] = ldsel(bc.dlam, b.lo, b.ok && !bc.pred);
             f.bx[9] = ldsel(bc.dlam, b.up, b.ok && !bc.pred);
-        } else if (FM == BX_P2) {
+        } else if (FM == BX_P2) {  // [2..3] (1/t) and, in the predictor, [6..7] (r_m) are formed at use
             f.bx[0] = ldsel(bc.res_d, b.lo, b.ok);
             f.bx[1] = ldsel(bc.res_d, b.up, b.ok);
-            f.bx[2] = ldsel(bc.t_inv, b.lo, b.ok);
-            f.bx[3] = ldsel(bc.t_inv, b.up, b.ok);
             f.bx[4] = ldsel(bc.lam, b.lo, b.ok);
             f.bx[5] = ldsel(bc.lam, b.up, b.ok);
-            f.bx[6] = ldsel(bc.res_m, b.lo, b.ok);
-            f.bx[7] = ldsel(bc.res_m, b.up, b.ok);
+            if (!PRED) {
+                f.bx[6] = ldsel(bc.res_m, b.lo, b.ok);
+                f.bx[7] = ldsel(bc.res_m, b.up, b.ok);
+            }
             f.bx[8] = ldsel(bc.t, b.lo, b.ok);
             f.bx[9] = ldsel(bc.t, b.up, b.ok);
         }
     }
 }
 
-template <int MODE, int FM, class FX, bool RPI>
+template <int MODE, int FM, class FX, bool PRED>
 __device__ __forceinline__ void fwd_fetch_k(const RicIO& io, int k, const double* bsrc, int use_bsrc,
                                             const double* ux, int compute_pi, const BoxCtx& bc, FwdFrag& f) {
     const int kk = k < io.N ? k : io.N - 1;
     const StageInfo sk = load_stage(io.st, kk);
     const int pnbk = k < io.N ? sk.pnb : load_stage(io.st, k).pnb;
     with_shape<FX>(sk, [&](const auto& sh) {
-        fwd_fetch<MODE, FM, RPI>(io, sh, k, pnbk, bsrc, use_bsrc, ux, compute_pi, bc, f);
+        fwd_fetch<MODE, FM, PRED>(io, sh, k, pnbk, bsrc, use_bsrc, ux, compute_pi, bc, f);
     });
 }
 
 // Step of the box slacks / multipliers of tile c given the primal step x = dux_k[var(c)] (col layout)
 // and the per-lane step-length candidate (d_compute_alpha_mpc_hard_tv :489-614 / _res_ :1180-1313).
-template <int FM>
+template <int FM, bool PRED>
 __device__ __forceinline__ void box_alpha(const BoxCtx& bc, const FwdFrag& f, double x, double& al) {
     if (FM == BX_NONE) return;
     const int g = lane_id() >> 4;
@@ -1080,10 +1082,13 @@ __device__ __forceinline__ void box_alpha(const BoxCtx& bc, const FwdFrag& f, do
         tl = f.bx[2];
         tu = f.bx[3];
     } else {
+        const double til = rcp_nr(f.bx[8]), tiu = rcp_nr(f.bx[9]);
+        const double rml = PRED ? __dmul_rn(f.bx[4], f.bx[8]) : f.bx[6];
+        const double rmu = PRED ? __dmul_rn(f.bx[5], f.bx[9]) : f.bx[7];
         dtl = x - f.bx[0];
         dtu = -x + f.bx[1];
-        dll = -f.bx[2] * (f.bx[4] * dtl + f.bx[6]);
-        dlu = -f.bx[3] * (f.bx[5] * dtu + f.bx[7]);
+        dll = -til * (f.bx[4] * dtl + rml);
+        dlu = -tiu * (f.bx[5] * dtu + rmu);
         lml = f.bx[4];
         lmu = f.bx[5];
         tl = f.bx[8];
@@ -1102,7 +1107,7 @@ __device__ __forceinline__ void box_alpha(const BoxCtx& bc, const FwdFrag& f, do
 }
 
 // One forward stage k < N: u_k from the factor, x_{k+1} = b + BAbt' ux, pi_k, box steps.
-template <int MODE, int FM, class SH>
+template <int MODE, int FM, bool PRED, class SH>
 __device__ __forceinline__ void fwd_step(const RicIO& io, Scratch* sm, const SH& sh, int k, const FwdFrag& cur,
                                          const FwdFrag& nxt, double& xcol, double* ux, int compute_pi, double* pi,
                                          const BoxCtx& bc, double& al) {
@@ -1139,7 +1144,7 @@ __device__ __forceinline__ void fwd_step(const RicIO& io, Scratch* sm, const SH&
     const double ucol = row2col(sm, ur);
     const int vcs = tile_var(c, sh.nu, sh.nx, sh.xo);
     gst(ux, k * V16 + vcs, ucol, g == 0 && vcs >= 0);
-    box_alpha<FM>(bc, cur, ucol, al);
+    box_alpha<FM, PRED>(bc, cur, ucol, al);
     if constexpr (!SH::fixed && FM != BX_NONE) {
         if (sh.ng > 0) gen_alpha<FM>(io, sh, k, bc, ucol, al);
     }
@@ -1167,7 +1172,7 @@ __device__ __forceinline__ void fwd_step(const RicIO& io, Scratch* sm, const SH&
 // Shared forward substitution (sv: rhs = -l_k ; trs: rhs = -hux_k), d_back_ric_rec.c:339-397 / :704-790.
 // ux: variable order; pi: state order.  FM != BX_NONE also computes the box steps of every stage and
 // the per-lane step-length candidate `al` (caller reduces it with wave_min).
-template <int MODE, int FM, class FX, bool RPI = true>
+template <int MODE, int FM, class FX, bool PRED = false>
 __device__ void ric_forward(const RicIO& io, Scratch* sm, const double* bsrc, int use_bsrc, double* ux,
                             int compute_pi, double* pi, const BoxCtx& bc, double& al) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
@@ -1175,14 +1180,14 @@ __device__ void ric_forward(const RicIO& io, Scratch* sm, const double* bsrc, in
     // Stage k runs on fa (its record) and fb (stage k+1's, for pi) while stage k+2 is fetched into fc; the
     // loop is unrolled by three with the fragments rotating roles (no register copies between stages).
     FwdFrag f0, f1, f2;
-    fwd_fetch_k<MODE, FM, FX, RPI>(io, 0, bsrc, use_bsrc, ux, compute_pi, bc, f0);
-    fwd_fetch_k<MODE, FM, FX, RPI>(io, 1, bsrc, use_bsrc, ux, compute_pi, bc, f1);
+    fwd_fetch_k<MODE, FM, FX, PRED>(io, 0, bsrc, use_bsrc, ux, compute_pi, bc, f0);
+    fwd_fetch_k<MODE, FM, FX, PRED>(io, 1, bsrc, use_bsrc, ux, compute_pi, bc, f1);
     auto stage = [&](int k, const FwdFrag& fa, const FwdFrag& fb, FwdFrag& fc) __attribute__((always_inline)) {
         HK_STAMP(8, k);
-        fwd_fetch_k<MODE, FM, FX, RPI>(io, k + 2 <= io.N ? k + 2 : io.N, bsrc, use_bsrc, ux, compute_pi, bc, fc);
+        fwd_fetch_k<MODE, FM, FX, PRED>(io, k + 2 <= io.N ? k + 2 : io.N, bsrc, use_bsrc, ux, compute_pi, bc, fc);
         const StageInfo si = load_stage(io.st, k);
         with_shape<FX>(si, [&](const auto& sh) {
-            fwd_step<MODE, FM>(io, sm, sh, k, fa, fb, xcol, ux, compute_pi, pi, bc, al);
+            fwd_step<MODE, FM, PRED>(io, sm, sh, k, fa, fb, xcol, ux, compute_pi, pi, bc, al);
         });
         HK_STAMP(12, k);
     };
@@ -1190,7 +1195,7 @@ __device__ void ric_forward(const RicIO& io, Scratch* sm, const double* bsrc, in
     auto finish = [&](const FwdFrag& fN) __attribute__((always_inline)) {  // stage N: nu = 0, every tile a state
         const int v = tile_var(c, sN.nu, sN.nx, sN.xo);
         gst(ux, io.N * V16 + v, xcol, g == 0 && v >= 0);
-        box_alpha<FM>(bc, fN, xcol, al);
+        box_alpha<FM, PRED>(bc, fN, xcol, al);
     };
     for (int k = 0;;) {
         if (k >= io.N) { finish(f0); break; }
@@ -1258,15 +1263,13 @@ __device__ __forceinline__ void trs_fetch(const RicIO& io, const SH& sh, int k, 
         f.bx[4] = ldsel(bc.dt, b.lo, b.ok);
         f.bx[5] = ldsel(bc.dt, b.up, b.ok);
         f.bx[6] = ldsel(bc.qxs, b.s16, b.ok);
-    } else if (TM == BX_P2) {
-        f.bx[0] = ldsel(bc.res_m, b.lo, b.ok);
-        f.bx[1] = ldsel(bc.res_m, b.up, b.ok);
+    } else if (TM == BX_P2) {  // [0..1]: t (r_m = lam t and 1/t are formed at use, bitwise the stored ones)
+        f.bx[0] = ldsel(bc.t, b.lo, b.ok);
+        f.bx[1] = ldsel(bc.t, b.up, b.ok);
         f.bx[2] = ldsel(bc.dt, b.lo, b.ok);
         f.bx[3] = ldsel(bc.dt, b.up, b.ok);
         f.bx[4] = ldsel(bc.dlam, b.lo, b.ok);
         f.bx[5] = ldsel(bc.dlam, b.up, b.ok);
-        f.bx[6] = ldsel(bc.t_inv, b.lo, b.ok);
-        f.bx[7] = ldsel(bc.t_inv, b.up, b.ok);
         f.bx[8] = ldsel(bc.lam, b.lo, b.ok);
         f.bx[9] = ldsel(bc.lam, b.up, b.ok);
         f.bx[10] = ldsel(bc.res_d, b.lo, b.ok);
@@ -1302,11 +1305,14 @@ __device__ __forceinline__ double box_gradient(const BoxCtx& bc, const TrsFrag& 
         return b.ok ? f.bx[6] + (dlu - dll) : 0.0;
     }
     if (TM == BX_P2) {
-        const double rml = f.bx[0] + (f.bx[2] * f.bx[4] - bc.smu);
-        const double rmu = f.bx[1] + (f.bx[3] * f.bx[5] - bc.smu);
+        // r_m of the current iterate = lam t (the update pass's rounded product), 1/t = rcp_nr(t) (the
+        // factorisation's stored t^-1): formed here instead of loaded
+        const double til = rcp_nr(f.bx[0]), tiu = rcp_nr(f.bx[1]);
+        const double rml = __dmul_rn(f.bx[8], f.bx[0]) + (f.bx[2] * f.bx[4] - bc.smu);
+        const double rmu = __dmul_rn(f.bx[9], f.bx[1]) + (f.bx[3] * f.bx[5] - bc.smu);
         gst(bc.res_m, b.lo, rml, st);
         gst(bc.res_m, b.up, rmu, st);
-        return b.ok ? f.bx[6] * (rml - f.bx[8] * f.bx[10]) - f.bx[7] * (rmu + f.bx[9] * f.bx[11]) : 0.0;
+        return b.ok ? til * (rml - f.bx[8] * f.bx[10]) - tiu * (rmu + f.bx[9] * f.bx[11]) : 0.0;
     }
     return 0.0;
 }

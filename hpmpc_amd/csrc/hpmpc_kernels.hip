@@ -604,9 +604,9 @@ __global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_pred(KArgs a) {
     // update uses it (d_ip2_res_hard.c:527 vs :628 and :948 vs :1168), so the predictor skips them.
     if (phase == 1) {
         v.bc.pred = 1;
-        ric_forward<0, BX_P1, FX, false>(v.io, &sm, nullptr, 0, v.w.dux, 0, v.w.dpi, v.bc, al);
+        ric_forward<0, BX_P1, FX, true>(v.io, &sm, nullptr, 0, v.w.dux, 0, v.w.dpi, v.bc, al);
     } else {
-        ric_forward<0, BX_P2, FX, false>(v.io, &sm, v.w.res_b, !sn, v.w.dux, 0, v.w.dpi, v.bc, al);
+        ric_forward<0, BX_P2, FX, true>(v.io, &sm, v.w.res_b, !sn, v.w.dux, 0, v.w.dpi, v.bc, al);
     }
     al = wave_min(al);
     wsync();
