@@ -1019,7 +1019,8 @@ __device__ __forceinline__ void fwd_fetch(const RicIO& io, const SH& sh, int k, 
     if (MODE == 1) {
         const int vc = tile_var(c, sh.nu, sh.nx, sh.xo);
         f.hc = ldsel(ux + kk * V16, vc, live && vc >= 0);
-        f.pk = ldsel(ux + (kk + 1) * V16, sh.nu1 + s, compute_pi && ok);
+        // p_{k+1}: on fixed stages it is the next fragment's hux_{k+1} (fwd_step), not loaded twice
+        f.pk = SH::fixed ? 0.0 : ldsel(ux + (kk + 1) * V16, sh.nu1 + s, compute_pi && ok);
     }
 #pragma unroll
     for (int i = 0; i < 10; i++) f.bx[i] = 0.0;
@@ -1164,7 +1165,9 @@ __device__ __forceinline__ void fwd_step(const RicIO& io, Scratch* sm, const SH&
         if (MODE == 0)
             pv = pi_from_x(nxt.S, sh.xo1, x1row, nxt.lc);  // pi_k = P x + p (p: the record's row)
         else
-            pv = pi_from_x(nxt.S, sh.xo1, x1row, cur.pk);  // pi_k = P x + p_{k+1} (trs backward vector)
+            // pi_k = P x + p_{k+1} (trs backward vector; fixed stages: the x tiles of stage k+1's hux, which the
+            // next fragment holds in col layout over the same tile coordinates)
+            pv = pi_from_x(nxt.S, sh.xo1, x1row, SH::fixed ? (ok ? nxt.hc : 0.0) : cur.pk);
     }
     gst(pi, k * V16 + s, pv, compute_pi && g == 0 && ok);
 }
