@@ -1144,7 +1144,9 @@ __device__ __forceinline__ void fwd_step(const RicIO& io, Scratch* sm, const SH&
     // ux_k, col layout (tile c): one coalesced store from row group 0, and the box steps
     const double ucol = row2col(sm, ur);
     const int vcs = tile_var(c, sh.nu, sh.nx, sh.xo);
-    gst(ux, k * V16 + vcs, ucol, g == 0 && vcs >= 0);
+    // the predictor's step is never read (the corrector's trs overwrites dux before reading it, and mu_aff
+    // needs dt / dlam only): it is not stored
+    if (!PRED) gst(ux, k * V16 + vcs, ucol, g == 0 && vcs >= 0);
     box_alpha<FM, PRED>(bc, cur, ucol, al);
     if constexpr (!SH::fixed && FM != BX_NONE) {
         if (sh.ng > 0) gen_alpha<FM>(io, sh, k, bc, ucol, al);
@@ -1197,7 +1199,7 @@ __device__ void ric_forward(const RicIO& io, Scratch* sm, const double* bsrc, in
     const StageInfo sN = load_stage(io.st, io.N);
     auto finish = [&](const FwdFrag& fN) __attribute__((always_inline)) {  // stage N: nu = 0, every tile a state
         const int v = tile_var(c, sN.nu, sN.nx, sN.xo);
-        gst(ux, io.N * V16 + v, xcol, g == 0 && v >= 0);
+        if (!PRED) gst(ux, io.N * V16 + v, xcol, g == 0 && v >= 0);
         box_alpha<FM, PRED>(bc, fN, xcol, al);
     };
     for (int k = 0;;) {
