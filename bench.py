@@ -465,7 +465,10 @@ def main():
 
         if world > 1:
             cdist.init_process_group("gloo")
-        print(json.dumps({"rank": rank, "world": cdist.get_world_size() if world > 1 else 1}), flush=True)
+        # one write() per line: the ranks share the launcher's stdout pipe, and print() may split the text
+        # and its newline into two writes that interleave with the other rank's
+        sys.stdout.flush()
+        os.write(1, (json.dumps({"rank": rank, "world": cdist.get_world_size() if world > 1 else 1}) + "\n").encode())
         if world > 1:
             cdist.destroy_process_group()
         return
@@ -479,7 +482,7 @@ def main():
         dist.init_process_group("nccl")
     print(f"bench.py: rank {rank} of world {world} on cuda:{local}", file=sys.stderr, flush=True)
 
-    from hpmpc_amd.batch import (BatchSolver, algorithmic_bytes_per_fact, algorithmic_bytes_per_ip_iter,
+    from hpmpc_amd.batch import (BatchSolver, algorithmic_bytes_per_ip_iter, algorithmic_bytes_per_pass,
                                  algorithmic_bytes_per_sv, flops_ip_iter, flops_sv)
     from hpmpc_amd.shard import Reducer, make_shard
 
@@ -530,13 +533,20 @@ def main():
     iters_total = sum_over_ranks(iters_rank)
     value = iters_total / dt
     names = ["hk_ipm_init", "hk_ipm_fact", "hk_ipm_pred", "hk_ipm_corr", "hk_ipm_update"]
-    dom = int(np.argmax(pass_ms))
-    bytes_fact = algorithmic_bytes_per_fact(qp)  # per problem-iteration of the factorisation pass
-    # per launch of the factorisation kernel: the problem-iterations it processes (sum kk / launches)
-    # x their algorithmic bytes, over its average launch duration (both from this timed run)
-    launch_ms = pass_ms[1] / ticks
+    # roofline of the dominant pass kernel (largest device time per step): each pass runs one launch per
+    # tick; per launch, the problem-iterations it processes (sum kk / ticks) x that pass's algorithmic bytes
+    # (algorithmic_bytes_per_pass), over its average launch duration (both from this timed run)
+    dom = 1 + int(np.argmax(pass_ms[1:]))
+    bytes_pass = algorithmic_bytes_per_pass(qp)
     probs_per_launch = iters_rank / ticks
-    achieved = probs_per_launch * bytes_fact / (launch_ms * 1e-3) / 1e9
+    per_pass = {}
+    for i in range(1, len(names)):
+        lm = pass_ms[i] / ticks
+        per_pass[names[i]] = {"launch_ms": float(lm), "algorithmic_bytes_per_problem_iter": bytes_pass[names[i]],
+                              "achieved_GBps": probs_per_launch * bytes_pass[names[i]] / (lm * 1e-3) / 1e9}
+    launch_ms = per_pass[names[dom]]["launch_ms"]
+    bytes_dom = bytes_pass[names[dom]]
+    achieved = per_pass[names[dom]]["achieved_GBps"]
     bytes_iter = algorithmic_bytes_per_ip_iter(qp)
     ipm_ms = float(pass_ms.sum())
     fl_iter = flops_ip_iter(N, nx, nu)
@@ -614,8 +624,17 @@ def main():
             with open(pmc) as f:
                 pm = json.load(f)
             if pm.get("workload") == f"ipm_queue_N{N}_nx{nx}_nu{nu}_batch{B}_slots{slots}":
-                # measured HBM bytes per problem-iteration of hk_ipm_fact x this run's problems per launch
-                traffic = pm["fact_hbm_bytes_per_problem_iter"] * probs_per_launch
+                # measured HBM bytes per problem-iteration of each pass (the PMC run's bytes per launch x its
+                # launches / its sum kk; two passes of the same run are averaged) x this run's problems per launch
+                for n, pp in per_pass.items():
+                    kp = pm["kernels"].get(n)
+                    if kp:
+                        nl = len(kp["raw_fetch"]) / 2
+                        per_it = kp["hbm_bytes_per_launch"] * nl / pm["kk_sum_per_solve"]
+                        pp["traffic_bytes_per_problem_iter"] = per_it
+                        pp["traffic_over_algorithmic"] = per_it / pp["algorithmic_bytes_per_problem_iter"]
+                t_dom = per_pass[names[dom]].get("traffic_bytes_per_problem_iter")
+                traffic = None if t_dom is None else t_dom * probs_per_launch
         except Exception:
             traffic = None
 
@@ -660,7 +679,8 @@ def main():
                          "frac": achieved / PEAK_HBM_GBS, "traffic": traffic, "kernel": names[dom],
                          "launch_ms": launch_ms, "launches": int(ticks),
                          "problem_iters_per_launch": probs_per_launch,
-                         "algorithmic_bytes_per_problem_iter": bytes_fact,
+                         "algorithmic_bytes_per_problem_iter": bytes_dom,
+                         "per_pass": per_pass,
                          "pass_ms_per_step": {n: float(v / args.steps) for n, v in zip(names, pass_ms)},
                          "ipm_whole_solve": {"achieved_GBps": iters_rank * bytes_iter / (ipm_ms * 1e-3) / 1e9,
                                              "algorithmic_bytes_per_ip_iter": bytes_iter,

@@ -288,6 +288,32 @@ def algorithmic_bytes_per_fact(qp: OCPQP) -> float:
     return 8.0 * tot
 
 
+def algorithmic_bytes_per_pass(qp: OCPQP) -> dict:
+    """Algorithmic HBM bytes of one problem-iteration through each IPM pass kernel (phase 2), each datum
+    counted once per pass, T = nux(nux+1)/2, per box pair (lower + upper):
+    - hk_ipm_fact: algorithmic_bytes_per_fact;
+    - hk_ipm_pred: factor L (T + 2 nux), BAbt with r_b in place of its b row; boxes r_d, lam, t read and
+      dt, dlam written (10); the step itself is not stored;
+    - hk_ipm_corr (trs + forward): L, BAbt + r_b, r_q (nux), stored P b (nx'), ux (nux) and pi (nx')
+      written; boxes t, dt, dlam, lam, r_d read, r_m, dt, dlam written (16);
+    - hk_ipm_update: ux, dux read, ux and its backup written (4 nux), the same for pi (4 nx'); boxes
+      lam, t, dlam, dt, d read, lam, t, their backups, r_d, r_m written (22)."""
+    out = {"hk_ipm_fact": algorithmic_bytes_per_fact(qp), "hk_ipm_pred": 0.0, "hk_ipm_corr": 0.0,
+           "hk_ipm_update": 0.0}
+    N = qp.N
+    for k in range(N + 1):
+        nux = qp.nux(k)
+        nx1 = int(qp.nx[k + 1]) if k < N else 0
+        nb = int(qp.nb[k])
+        T = nux * (nux + 1) // 2
+        L = T + 2 * nux
+        babt = (nux + 1) * nx1
+        out["hk_ipm_pred"] += 8.0 * (L + babt + 10 * nb)
+        out["hk_ipm_corr"] += 8.0 * (L + babt + nux + nx1 + nux + nx1 + 16 * nb)
+        out["hk_ipm_update"] += 8.0 * (4 * nux + 4 * nx1 + 22 * nb)
+    return out
+
+
 def algorithmic_bytes_per_sv(qp: OCPQP) -> float:
     """8 N [(nux+1)nx' + (T+nux) + (T+2nux) + nux + nx'] (sum over stages)."""
     tot = 0

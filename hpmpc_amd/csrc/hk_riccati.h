@@ -391,6 +391,45 @@ __device__ __forceinline__ BoxLane box_lane(const signed char* tileslot, int pnb
     return b;
 }
 
+// A box pair's lower and upper value with ONE load: row groups 0/2 read the lower slot, 1/3 the upper one,
+// and one v_permlane16_swap per dword gives every lane both (after the swap, [0] holds the even row's dword
+// and [1] the odd row's, in all lanes -- the order rowgroup_gather relies on).  Rows g and g^1 have the same
+// c, so the same box and mask; a masked lane reads 0 like ldsel.
+__device__ __forceinline__ void ld_lu(const double* p, const BoxLane& b, double& vlo, double& vup) {
+    const bool odd = (lane_id() & 16) != 0;
+    // the slot by a bit mask: a select between the two fields was lowered to a stack round trip
+    const int m = -(int)odd;
+    const double x = gld(p, (b.up & m) | (b.lo & ~m), b.ok);
+    const int xl = __double2loint(x), xh = __double2hiint(x);
+    const auto cl = __builtin_amdgcn_permlane16_swap(xl, xl, false, false);
+    const auto ch = __builtin_amdgcn_permlane16_swap(xh, xh, false, false);
+    vlo = mk((int)ch[0], (int)cl[0]);
+    vup = mk((int)ch[1], (int)cl[1]);
+}
+
+// The same paired load with the exchange deferred to the use (lu_split): a prefetched fragment would
+// otherwise wait for its own load right after issuing it.
+__device__ __forceinline__ double ld_lu_raw(const double* p, const BoxLane& b) {
+    const bool odd = (lane_id() & 16) != 0;
+    const int m = -(int)odd;
+    return gld(p, (b.up & m) | (b.lo & ~m), b.ok);
+}
+__device__ __forceinline__ void lu_split(double x, double& vlo, double& vup) {
+    const int xl = __double2loint(x), xh = __double2hiint(x);
+    const auto cl = __builtin_amdgcn_permlane16_swap(xl, xl, false, false);
+    const auto ch = __builtin_amdgcn_permlane16_swap(xh, xh, false, false);
+    vlo = mk((int)ch[0], (int)cl[0]);
+    vup = mk((int)ch[1], (int)cl[1]);
+}
+
+// A box pair's lower and upper value with ONE store: row group 0 writes the lower slot, row group 1 the
+// upper one (every lane holds both values; rows 2/3 are masked off).
+__device__ __forceinline__ void st_lu(double* p, const BoxLane& b, double vlo, double vup, bool ok) {
+    const bool odd = (lane_id() & 16) != 0;
+    const int m = -(int)odd;
+    gst(p, (b.up & m) | (b.lo & ~m), odd ? vup : vlo, ok && lane_id() < 32);
+}
+
 // sequential step-length rule of d_compute_alpha_* (d_aux_ip_hard_lib4.c:541-565), per lane
 __device__ __forceinline__ void alpha_rule(double& al, double v, double dv) {
     const double cand = -v * rcp_nr(dv);
@@ -641,18 +680,12 @@ __device__ __forceinline__ void bwd_fetch(const RicIO& io, const SH& sh, int k, 
         f.bx[4] = ldsel(bc.d, b.lo, b.ok);
         f.bx[5] = ldsel(bc.d, b.up, b.ok);
     } else if (BM == BX_P2 || BM == BX_P2R) {
-        f.bx[0] = ldsel(bc.lam, b.lo, b.ok);
-        f.bx[1] = ldsel(bc.lam, b.up, b.ok);
-        f.bx[2] = ldsel(bc.t, b.lo, b.ok);
-        f.bx[3] = ldsel(bc.t, b.up, b.ok);
+        ld_lu(bc.lam, b, f.bx[0], f.bx[1]);
+        ld_lu(bc.t, b, f.bx[2], f.bx[3]);
         // BX_P2R: r_m of the current iterate is lam * t, exactly the product the update pass stored
         // (update_p2_pass), so it is formed at use instead of loaded
-        if (BM == BX_P2) {
-            f.bx[4] = ldsel(bc.res_m, b.lo, b.ok);
-            f.bx[5] = ldsel(bc.res_m, b.up, b.ok);
-        }
-        f.bx[6] = ldsel(bc.res_d, b.lo, b.ok);
-        f.bx[7] = ldsel(bc.res_d, b.up, b.ok);
+        if (BM == BX_P2) ld_lu(bc.res_m, b, f.bx[4], f.bx[5]);
+        ld_lu(bc.res_d, b, f.bx[6], f.bx[7]);
     }
     const bool live = SH::fixed || k < io.N;
     const double* Bk = io.BAbt + sh.oB;
@@ -1039,16 +1072,11 @@ __device__ __forceinline__ void fwd_fetch(const RicIO& io, const SH& sh, int k, 
             f.bx[8] = ldsel(bc.dlam, b.lo, b.ok && !bc.pred);
             f.bx[9] = ldsel(bc.dlam, b.up, b.ok && !bc.pred);
         } else if (FM == BX_P2) {  // [2..3] (1/t) and, in the predictor, [6..7] (r_m) are formed at use
-            f.bx[0] = ldsel(bc.res_d, b.lo, b.ok);
-            f.bx[1] = ldsel(bc.res_d, b.up, b.ok);
-            f.bx[4] = ldsel(bc.lam, b.lo, b.ok);
-            f.bx[5] = ldsel(bc.lam, b.up, b.ok);
-            if (!PRED) {
-                f.bx[6] = ldsel(bc.res_m, b.lo, b.ok);
-                f.bx[7] = ldsel(bc.res_m, b.up, b.ok);
-            }
-            f.bx[8] = ldsel(bc.t, b.lo, b.ok);
-            f.bx[9] = ldsel(bc.t, b.up, b.ok);
+            // lower / upper pairs in one load each (even slot: the raw value, split at use by box_alpha)
+            f.bx[0] = ld_lu_raw(bc.res_d, b);
+            f.bx[4] = ld_lu_raw(bc.lam, b);
+            if (!PRED) f.bx[6] = ld_lu_raw(bc.res_m, b);
+            f.bx[8] = ld_lu_raw(bc.t, b);
         }
     }
 }
@@ -1069,9 +1097,7 @@ __device__ __forceinline__ void fwd_fetch_k(const RicIO& io, int k, const double
 template <int FM, bool PRED>
 __device__ __forceinline__ void box_alpha(const BoxCtx& bc, const FwdFrag& f, double x, double& al) {
     if (FM == BX_NONE) return;
-    const int g = lane_id() >> 4;
     const BoxLane& b = f.bl;
-    const bool st = b.ok && g == 0;
     double dtl, dtu, dll, dlu, lml, lmu, tl, tu;
     if (FM == BX_P1) {
         dtl = x - f.bx[0] - f.bx[2];
@@ -1083,22 +1109,25 @@ __device__ __forceinline__ void box_alpha(const BoxCtx& bc, const FwdFrag& f, do
         tl = f.bx[2];
         tu = f.bx[3];
     } else {
-        const double til = rcp_nr(f.bx[8]), tiu = rcp_nr(f.bx[9]);
-        const double rml = PRED ? __dmul_rn(f.bx[4], f.bx[8]) : f.bx[6];
-        const double rmu = PRED ? __dmul_rn(f.bx[5], f.bx[9]) : f.bx[7];
-        dtl = x - f.bx[0];
-        dtu = -x + f.bx[1];
-        dll = -til * (f.bx[4] * dtl + rml);
-        dlu = -tiu * (f.bx[5] * dtu + rmu);
-        lml = f.bx[4];
-        lmu = f.bx[5];
-        tl = f.bx[8];
-        tu = f.bx[9];
+        double bx[10];
+        lu_split(f.bx[0], bx[0], bx[1]);
+        lu_split(f.bx[4], bx[4], bx[5]);
+        if (!PRED) lu_split(f.bx[6], bx[6], bx[7]);
+        lu_split(f.bx[8], bx[8], bx[9]);
+        const double til = rcp_nr(bx[8]), tiu = rcp_nr(bx[9]);
+        const double rml = PRED ? __dmul_rn(bx[4], bx[8]) : bx[6];
+        const double rmu = PRED ? __dmul_rn(bx[5], bx[9]) : bx[7];
+        dtl = x - bx[0];
+        dtu = -x + bx[1];
+        dll = -til * (bx[4] * dtl + rml);
+        dlu = -tiu * (bx[5] * dtu + rmu);
+        lml = bx[4];
+        lmu = bx[5];
+        tl = bx[8];
+        tu = bx[9];
     }
-    gst(bc.dt, b.lo, dtl, st);
-    gst(bc.dt, b.up, dtu, st);
-    gst(bc.dlam, b.lo, dll, st);
-    gst(bc.dlam, b.up, dlu, st);
+    st_lu(bc.dt, b, dtl, dtu, b.ok);
+    st_lu(bc.dlam, b, dll, dlu, b.ok);
     if (b.ok) {
         alpha_rule(al, lml, dll);
         alpha_rule(al, lmu, dlu);
@@ -1269,16 +1298,12 @@ __device__ __forceinline__ void trs_fetch(const RicIO& io, const SH& sh, int k, 
         f.bx[5] = ldsel(bc.dt, b.up, b.ok);
         f.bx[6] = ldsel(bc.qxs, b.s16, b.ok);
     } else if (TM == BX_P2) {  // [0..1]: t (r_m = lam t and 1/t are formed at use, bitwise the stored ones)
-        f.bx[0] = ldsel(bc.t, b.lo, b.ok);
-        f.bx[1] = ldsel(bc.t, b.up, b.ok);
-        f.bx[2] = ldsel(bc.dt, b.lo, b.ok);
-        f.bx[3] = ldsel(bc.dt, b.up, b.ok);
-        f.bx[4] = ldsel(bc.dlam, b.lo, b.ok);
-        f.bx[5] = ldsel(bc.dlam, b.up, b.ok);
-        f.bx[8] = ldsel(bc.lam, b.lo, b.ok);
-        f.bx[9] = ldsel(bc.lam, b.up, b.ok);
-        f.bx[10] = ldsel(bc.res_d, b.lo, b.ok);
-        f.bx[11] = ldsel(bc.res_d, b.up, b.ok);
+        // lower / upper pairs in one load each (even slot: the raw value, split at use by box_gradient)
+        f.bx[0] = ld_lu_raw(bc.t, b);
+        f.bx[2] = ld_lu_raw(bc.dt, b);
+        f.bx[4] = ld_lu_raw(bc.dlam, b);
+        f.bx[8] = ld_lu_raw(bc.lam, b);
+        f.bx[10] = ld_lu_raw(bc.res_d, b);
     }
     const bool live = SH::fixed || k < io.N;
     const double* Bk = io.BAbt + sh.oB;
@@ -1312,12 +1337,17 @@ __device__ __forceinline__ double box_gradient(const BoxCtx& bc, const TrsFrag& 
     if (TM == BX_P2) {
         // r_m of the current iterate = lam t (the update pass's rounded product), 1/t = rcp_nr(t) (the
         // factorisation's stored t^-1): formed here instead of loaded
-        const double til = rcp_nr(f.bx[0]), tiu = rcp_nr(f.bx[1]);
-        const double rml = __dmul_rn(f.bx[8], f.bx[0]) + (f.bx[2] * f.bx[4] - bc.smu);
-        const double rmu = __dmul_rn(f.bx[9], f.bx[1]) + (f.bx[3] * f.bx[5] - bc.smu);
-        gst(bc.res_m, b.lo, rml, st);
-        gst(bc.res_m, b.up, rmu, st);
-        return b.ok ? til * (rml - f.bx[8] * f.bx[10]) - tiu * (rmu + f.bx[9] * f.bx[11]) : 0.0;
+        double bx[12];
+        lu_split(f.bx[0], bx[0], bx[1]);
+        lu_split(f.bx[2], bx[2], bx[3]);
+        lu_split(f.bx[4], bx[4], bx[5]);
+        lu_split(f.bx[8], bx[8], bx[9]);
+        lu_split(f.bx[10], bx[10], bx[11]);
+        const double til = rcp_nr(bx[0]), tiu = rcp_nr(bx[1]);
+        const double rml = __dmul_rn(bx[8], bx[0]) + (bx[2] * bx[4] - bc.smu);
+        const double rmu = __dmul_rn(bx[9], bx[1]) + (bx[3] * bx[5] - bc.smu);
+        st_lu(bc.res_m, b, rml, rmu, b.ok);
+        return b.ok ? til * (rml - bx[8] * bx[10]) - tiu * (rmu + bx[9] * bx[11]) : 0.0;
     }
     return 0.0;
 }
