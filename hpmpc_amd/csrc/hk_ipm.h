@@ -172,7 +172,9 @@ __device__ double update_p1_pass(const RicIO& io, const BoxCtx& bc, double alpha
 // iterate (phase-2 start).  r_q and r_b, the residuals that need the stage matrices, are computed by
 // the next factorisation pass (BX_P2R).  The box variable's x is recomputed from (ux, dux) in the
 // slot lane with the same arithmetic as in its own lane.
-template <int CH, bool UPD>
+// BKP = false (the public queue API, whose per-slot workspace never feeds a KKT re-solve): the iterate
+// backups that only hk_kkt_new_rhs reads are not written.
+template <int CH, bool UPD, bool BKP = true>
 __device__ double update_p2_pass(const RicIO& io, const BoxCtx& bc, const signed char* slotvar, double alpha,
                                  double mu_scal, double* ux, double* pi, const double* dux, const double* dpi,
                                  double* ux_bkp, double* pi_bkp, double* lam_bkp, double* t_bkp, double* res_d,
@@ -218,14 +220,16 @@ __device__ double update_p2_pass(const RicIO& io, const BoxCtx& bc, const signed
         for (int j = 0; j < CH; j++) {
             const QuadLane& b = bl[j];
             if (UPD) {
-                gst(ux_bkp, i16[j], v[j][0], oku[j]);
+                if (BKP) gst(ux_bkp, i16[j], v[j][0], oku[j]);
                 gst(ux, i16[j], v[j][0] + alpha * v[j][1], oku[j]);
-                gst(pi_bkp, i16[j], v[j][2], okp[j]);
+                if (BKP) gst(pi_bkp, i16[j], v[j][2], okp[j]);
                 gst(pi, i16[j], v[j][2] + alpha * v[j][3], okp[j]);
-                gst(lam_bkp, b.lo, v[j][4], b.ok);
-                gst(lam_bkp, b.up, v[j][8], b.ok);
-                gst(t_bkp, b.lo, v[j][6], b.ok);
-                gst(t_bkp, b.up, v[j][10], b.ok);
+                if (BKP) {
+                    gst(lam_bkp, b.lo, v[j][4], b.ok);
+                    gst(lam_bkp, b.up, v[j][8], b.ok);
+                    gst(t_bkp, b.lo, v[j][6], b.ok);
+                    gst(t_bkp, b.up, v[j][10], b.ok);
+                }
             }
             const double ll = UPD ? v[j][4] + alpha * v[j][5] : v[j][4];
             const double lu = UPD ? v[j][8] + alpha * v[j][9] : v[j][8];

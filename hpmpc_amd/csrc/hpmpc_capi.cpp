@@ -547,6 +547,7 @@ extern "C" int hpmpc_mi355x_ipm_queue(const hpmpc_mi355x_plan* plan, const hpmpc
     a.kk = kk;
     a.ret = ret;
     a.stat = stat;
+    a.no_bkp = 1;  // slots are reused and no KKT re-solve follows a queue solve (header): backups are dead stores
     return queue_run<8>(a, nq, n_slots, qctl, k_max, pass_ms, n_ticks, (hipStream_t)stream);
 }
 

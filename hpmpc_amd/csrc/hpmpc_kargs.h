@@ -42,6 +42,7 @@ struct KArgs {
                 // [2 + nslots + p] length of active-slot list p, [4 + nslots + p nslots ..] list p (p = 0, 1)
     unsigned long long* dbg;  // diagnostic stamp buffer (HK_STAMPS builds only)
     int nslots;  // queue slots
+    int no_bkp;  // public queue API: the update pass writes no iterate backups (only the KKT re-solve reads them)
     int qpar;    // queue tick parity: workgroup i of an iteration kernel runs slot list[qpar][i]; the update
                  // pass lists the slots that iterate again in list qpar ^ 1 (hk_ipm_init fills list qpar)
 };

@@ -671,8 +671,13 @@ __global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_update(KArgs a) {
         mu = update_p1_pass<4>(v.io, v.bc, alpha, st[S_MUSCAL], v.ux, v.pi, v.w.dux, v.w.dpi, v.w.ux_bkp,
                                v.w.pi_bkp, v.w.lam_bkp, v.w.t_bkp);
     } else {
-        mu = update_p2_pass<4, true>(v.io, v.bc, v.bt.slotvar, alpha, st[S_MUSCAL], v.ux, v.pi, v.w.dux, v.w.dpi,
-                                     v.w.ux_bkp, v.w.pi_bkp, v.w.lam_bkp, v.w.t_bkp, v.w.res_d, v.w.res_m);
+        if (a.no_bkp)  // wave-uniform: the public queue API keeps no backups (nothing re-solves its slots)
+            mu = update_p2_pass<4, true, false>(v.io, v.bc, v.bt.slotvar, alpha, st[S_MUSCAL], v.ux, v.pi, v.w.dux,
+                                                v.w.dpi, v.w.ux_bkp, v.w.pi_bkp, v.w.lam_bkp, v.w.t_bkp, v.w.res_d,
+                                                v.w.res_m);
+        else
+            mu = update_p2_pass<4, true>(v.io, v.bc, v.bt.slotvar, alpha, st[S_MUSCAL], v.ux, v.pi, v.w.dux, v.w.dpi,
+                                         v.w.ux_bkp, v.w.pi_bkp, v.w.lam_bkp, v.w.t_bkp, v.w.res_d, v.w.res_m);
     }
     wsync();
     if (v.l == 0) v.stat[5 * kk + 4] = mu;
