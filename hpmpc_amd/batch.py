@@ -296,8 +296,9 @@ def algorithmic_bytes_per_pass(qp: OCPQP) -> dict:
       dt, dlam written (10); the step itself is not stored;
     - hk_ipm_corr (trs + forward): L, BAbt + r_b, r_q (nux), stored P b (nx'), ux (nux) and pi (nx')
       written; boxes t, dt, dlam, lam, r_d read, r_m, dt, dlam written (16);
-    - hk_ipm_update: ux, dux read, ux and its backup written (4 nux), the same for pi (4 nx'); boxes
-      lam, t, dlam, dt, d read, lam, t, their backups, r_d, r_m written (22)."""
+    - hk_ipm_update (queue API: no backups, no r_m store -- nothing in a queue solve reads them): ux, dux
+      read, ux written (3 nux), the same for pi (3 nx'); boxes lam, t, dlam, dt, d read, lam, t, r_d
+      written (16)."""
     out = {"hk_ipm_fact": algorithmic_bytes_per_fact(qp), "hk_ipm_pred": 0.0, "hk_ipm_corr": 0.0,
            "hk_ipm_update": 0.0}
     N = qp.N
@@ -310,7 +311,7 @@ def algorithmic_bytes_per_pass(qp: OCPQP) -> dict:
         babt = (nux + 1) * nx1
         out["hk_ipm_pred"] += 8.0 * (L + babt + 10 * nb)
         out["hk_ipm_corr"] += 8.0 * (L + babt + nux + nx1 + nux + nx1 + 16 * nb)
-        out["hk_ipm_update"] += 8.0 * (4 * nux + 4 * nx1 + 22 * nb)
+        out["hk_ipm_update"] += 8.0 * (3 * nux + 3 * nx1 + 16 * nb)
     return out
 
 

@@ -173,7 +173,7 @@ __device__ double update_p1_pass(const RicIO& io, const BoxCtx& bc, double alpha
 // the next factorisation pass (BX_P2R).  The box variable's x is recomputed from (ux, dux) in the
 // slot lane with the same arithmetic as in its own lane.
 // BKP = false (the public queue API, whose per-slot workspace never feeds a KKT re-solve): the iterate
-// backups that only hk_kkt_new_rhs reads are not written.
+// backups and r_m, which only hk_kkt_new_rhs (and general constraints) read, are not written.
 template <int CH, bool UPD, bool BKP = true>
 __device__ double update_p2_pass(const RicIO& io, const BoxCtx& bc, const signed char* slotvar, double alpha,
                                  double mu_scal, double* ux, double* pi, const double* dux, const double* dpi,
@@ -246,8 +246,13 @@ __device__ double update_p2_pass(const RicIO& io, const BoxCtx& bc, const signed
             // r_d of the general pairs needs D x: the next factorisation forms it (gen_hessian)
             gst(res_d, b.lo, v[j][14] - x + tl, b.ok && b.box);
             gst(res_d, b.up, v[j][15] - x - tu, b.ok && b.box);
-            gst(res_m, b.lo, rml, b.ok);
-            gst(res_m, b.up, rmu, b.ok);
+            // r_m = lam t is re-formed at use by every phase-2 pass (and the corrector stores its own centred
+            // r_m before its forward reads it): only the KKT re-solve and the general-constraint halves load
+            // this store, and the queue API has neither (BKP = false; layout_apply refuses ng > 0)
+            if (BKP) {
+                gst(res_m, b.lo, rml, b.ok);
+                gst(res_m, b.up, rmu, b.ok);
+            }
             ms += b.ok ? rml + rmu : 0.0;
         }
     }
