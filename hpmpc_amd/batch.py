@@ -24,7 +24,9 @@ import numpy as np
 from .ocp import OCPQP
 
 _LIB = None
-LIBPATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libhpmpc_mi355x.so")
+# HPMPC_MI355X_LIB: another build of the same library (A/B timing of two builds on one box, tools/gpu_ab.sh)
+LIBPATH = os.environ.get("HPMPC_MI355X_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib",
+                                                             "libhpmpc_mi355x.so")
 
 
 def lib() -> C.CDLL:

@@ -373,6 +373,9 @@ struct BoxCtx {
     const double *ux, *pi;
     double *res_q, *res_b;
     int res_rhs;
+    // BX_P2 / BX_P2R: the factorisation skips its t^-1 store (queue API: the solves re-form 1/t from t, and
+    // only the KKT re-solve and the general-constraint halves load it; wave-uniform)
+    int no_tinv;
 };
 
 struct BoxLane {
@@ -738,7 +741,7 @@ __device__ __forceinline__ void box_hessian(const BoxCtx& bc, const BwdFrag& f, 
         const double rml = BM == BX_P2R ? f.bx[0] * f.bx[2] : f.bx[4];
         const double rmu = BM == BX_P2R ? f.bx[1] * f.bx[3] : f.bx[5];
         const double q = til * (rml - f.bx[0] * f.bx[6]) - tiu * (rmu + f.bx[1] * f.bx[7]);
-        gst(bc.t_inv, g == 0 ? b.lo : b.up, g == 0 ? til : tiu, b.ok && g < 2);  // lower / upper: one store
+        if (!bc.no_tinv) st_lu(bc.t_inv, b, til, tiu, b.ok);  // lower / upper: one store
         dq = b.ok ? til * f.bx[0] + tiu * f.bx[1] : 0.0;
         qxv = (AUG && b.ok) ? q : 0.0;
     }

@@ -581,6 +581,7 @@ __global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_fact(KArgs a) {
         ric_backward<true, BX_P1, FX>(v.io, &sm, 0, nullptr, 0, nullptr, v.bc, 1, v.w.Pb);
     else {  // the single-Newton variant factorises with the data's own b/q rows (d_ip2_res_hard.c:1700-1760)
         v.bc.res_rhs = !sn;
+        v.bc.no_tinv = a.no_bkp;
         ric_backward<true, BX_P2R, FX>(v.io, &sm, 0, nullptr, 0, nullptr, v.bc, 1, v.w.Pb);
     }
 }

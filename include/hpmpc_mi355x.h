@@ -226,7 +226,8 @@ int hpmpc_mi355x_ipm_batch_profiled(const hpmpc_mi355x_plan *plan, const hpmpc_m
  * keeps one slot per SIMD).  A slot whose problem has finished takes
  * the next entry at the following iteration, so the GPU is not left idle behind the slowest problem
  * of a batch.  Results are those of hpmpc_mi355x_ipm_batch on each entry (the per-slot workspace is
- * reused, so a queue solve leaves no factor behind for d_kkt_solve_new_rhs_res_mpc_hard_tv).
+ * reused, so a queue solve leaves no factor behind for d_kkt_solve_new_rhs_res_mpc_hard_tv; for the same
+ * reason its update pass writes neither the iterate backups nor r_m, which only that re-solve reads).
  * Synchronises with the device once per chunk of iterations (it polls the finished counter); on
  * return the last chunk may still be running on `stream`.  pass_ms (nullable): device time of
  * [init, fact, pred, corr, update] summed over the run; n_ticks (nullable): iterations enqueued. */
