@@ -425,6 +425,30 @@ __device__ __forceinline__ void lu_split(double x, double& vlo, double& vup) {
     vup = mk((int)ch[1], (int)cl[1]);
 }
 
+// Box pairs in the solves' prefetched fragments: HK_SOLVE_PAIRS = 1 loads a pair with one ld_lu_raw into the
+// even slot and splits it at the use; 0 (default) keeps two loads into slots (e0, e1).  A same-box A/B
+// (tools/gpu_ab.sh, profiles/ab_solve_pairs/) measured the paired form 0.5-1 % slower in pred and corr: the
+// saved load does not pay for the exchange on their chains.  The factorisation keeps ld_lu (fact 2.87 -> 2.75).
+#ifndef HK_SOLVE_PAIRS
+#define HK_SOLVE_PAIRS 0
+#endif
+__device__ __forceinline__ void fetch_pair(const double* p, const BoxLane& b, double& e0, double& e1) {
+    if (HK_SOLVE_PAIRS) {
+        e0 = ld_lu_raw(p, b);
+    } else {
+        e0 = gld(p, b.lo, b.ok);
+        e1 = gld(p, b.up, b.ok);
+    }
+}
+__device__ __forceinline__ void use_pair(double e0, double e1, double& vlo, double& vup) {
+    if (HK_SOLVE_PAIRS) {
+        lu_split(e0, vlo, vup);
+    } else {
+        vlo = e0;
+        vup = e1;
+    }
+}
+
 // A box pair's lower and upper value with ONE store: row group 0 writes the lower slot, row group 1 the
 // upper one (every lane holds both values; rows 2/3 are masked off).
 __device__ __forceinline__ void st_lu(double* p, const BoxLane& b, double vlo, double vup, bool ok) {
@@ -1076,10 +1100,10 @@ __device__ __forceinline__ void fwd_fetch(const RicIO& io, const SH& sh, int k, 
             f.bx[9] = ldsel(bc.dlam, b.up, b.ok && !bc.pred);
         } else if (FM == BX_P2) {  // [2..3] (1/t) and, in the predictor, [6..7] (r_m) are formed at use
             // lower / upper pairs in one load each (even slot: the raw value, split at use by box_alpha)
-            f.bx[0] = ld_lu_raw(bc.res_d, b);
-            f.bx[4] = ld_lu_raw(bc.lam, b);
-            if (!PRED) f.bx[6] = ld_lu_raw(bc.res_m, b);
-            f.bx[8] = ld_lu_raw(bc.t, b);
+            fetch_pair(bc.res_d, b, f.bx[0], f.bx[1]);
+            fetch_pair(bc.lam, b, f.bx[4], f.bx[5]);
+            if (!PRED) fetch_pair(bc.res_m, b, f.bx[6], f.bx[7]);
+            fetch_pair(bc.t, b, f.bx[8], f.bx[9]);
         }
     }
 }
@@ -1113,10 +1137,10 @@ __device__ __forceinline__ void box_alpha(const BoxCtx& bc, const FwdFrag& f, do
         tu = f.bx[3];
     } else {
         double bx[10];
-        lu_split(f.bx[0], bx[0], bx[1]);
-        lu_split(f.bx[4], bx[4], bx[5]);
-        if (!PRED) lu_split(f.bx[6], bx[6], bx[7]);
-        lu_split(f.bx[8], bx[8], bx[9]);
+        use_pair(f.bx[0], f.bx[1], bx[0], bx[1]);
+        use_pair(f.bx[4], f.bx[5], bx[4], bx[5]);
+        if (!PRED) use_pair(f.bx[6], f.bx[7], bx[6], bx[7]);
+        use_pair(f.bx[8], f.bx[9], bx[8], bx[9]);
         const double til = rcp_nr(bx[8]), tiu = rcp_nr(bx[9]);
         const double rml = PRED ? __dmul_rn(bx[4], bx[8]) : bx[6];
         const double rmu = PRED ? __dmul_rn(bx[5], bx[9]) : bx[7];
@@ -1302,11 +1326,11 @@ __device__ __forceinline__ void trs_fetch(const RicIO& io, const SH& sh, int k, 
         f.bx[6] = ldsel(bc.qxs, b.s16, b.ok);
     } else if (TM == BX_P2) {  // [0..1]: t (r_m = lam t and 1/t are formed at use, bitwise the stored ones)
         // lower / upper pairs in one load each (even slot: the raw value, split at use by box_gradient)
-        f.bx[0] = ld_lu_raw(bc.t, b);
-        f.bx[2] = ld_lu_raw(bc.dt, b);
-        f.bx[4] = ld_lu_raw(bc.dlam, b);
-        f.bx[8] = ld_lu_raw(bc.lam, b);
-        f.bx[10] = ld_lu_raw(bc.res_d, b);
+        fetch_pair(bc.t, b, f.bx[0], f.bx[1]);
+        fetch_pair(bc.dt, b, f.bx[2], f.bx[3]);
+        fetch_pair(bc.dlam, b, f.bx[4], f.bx[5]);
+        fetch_pair(bc.lam, b, f.bx[8], f.bx[9]);
+        fetch_pair(bc.res_d, b, f.bx[10], f.bx[11]);
     }
     const bool live = SH::fixed || k < io.N;
     const double* Bk = io.BAbt + sh.oB;
@@ -1341,11 +1365,11 @@ __device__ __forceinline__ double box_gradient(const BoxCtx& bc, const TrsFrag& 
         // r_m of the current iterate = lam t (the update pass's rounded product), 1/t = rcp_nr(t) (the
         // factorisation's stored t^-1): formed here instead of loaded
         double bx[12];
-        lu_split(f.bx[0], bx[0], bx[1]);
-        lu_split(f.bx[2], bx[2], bx[3]);
-        lu_split(f.bx[4], bx[4], bx[5]);
-        lu_split(f.bx[8], bx[8], bx[9]);
-        lu_split(f.bx[10], bx[10], bx[11]);
+        use_pair(f.bx[0], f.bx[1], bx[0], bx[1]);
+        use_pair(f.bx[2], f.bx[3], bx[2], bx[3]);
+        use_pair(f.bx[4], f.bx[5], bx[4], bx[5]);
+        use_pair(f.bx[8], f.bx[9], bx[8], bx[9]);
+        use_pair(f.bx[10], f.bx[11], bx[10], bx[11]);
         const double til = rcp_nr(bx[0]), tiu = rcp_nr(bx[1]);
         const double rml = __dmul_rn(bx[8], bx[0]) + (bx[2] * bx[4] - bc.smu);
         const double rmu = __dmul_rn(bx[9], bx[1]) + (bx[3] * bx[5] - bc.smu);
