@@ -20,6 +20,10 @@ HEADERS = ["hk_prims.h", "hk_riccati.h", "hk_ipm.h", "hpmpc_kargs.h", "hk_wide_a
 # MFMA accumulators stay in ordinary VGPRs: the stage tile is read and written by VALU code between
 # MFMAs, and the AGPR form costs 8 v_accvgpr moves each way per MFMA group.
 KFLAGS = ["-mllvm", "-amdgpu-mfma-vgpr-form"] + os.environ.get("HK_EXTRA_FLAGS", "").split()
+# Per-source flags.  The narrow IPM / Riccati passes use the memory-clause machine scheduler: a same-box A/B
+# (tools/gpu_ab.sh, profiles/ab_sched_max_memory_clause/) measured hk_ipm_corr 3.161 -> 3.125 ms per step with
+# the other passes unchanged (max-ilp instead slowed the factorisation by 8 %).
+SRC_FLAGS = {"hpmpc_kernels.hip": ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"]}
 
 
 def _newer(out, deps):
@@ -43,7 +47,7 @@ def build_hip(force: bool = False, verbose: bool = False) -> str:
         obj = os.path.join(objdir, src + ".o")
         objs.append(obj)
         if force or not _newer(obj, [os.path.join(CSRC, src)] + hdrs):
-            cmd = common + ["-c", os.path.join(CSRC, src), "-o", obj]
+            cmd = common + SRC_FLAGS.get(src, []) + ["-c", os.path.join(CSRC, src), "-o", obj]
             if verbose:
                 print(" ".join(cmd), flush=True)
             procs.append((src, subprocess.Popen(cmd)))
