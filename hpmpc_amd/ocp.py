@@ -138,13 +138,13 @@ def default_x0(nx: int) -> np.ndarray:
     return x0
 
 
-def batch_x0(nx: int, batch: int, seed_base: int = 20261015) -> np.ndarray:
-    """Per-problem initial states: problem 0 uses the driver's x0, problem p>0 ~ U(-2.5, 2.5) from
-    PCG64(seed_base + p)."""
+def batch_x0(nx: int, batch: int, seed_base: int = 20261015, start: int = 0) -> np.ndarray:
+    """Initial states of global problems start .. start+batch-1: problem 0 uses the driver's x0, problem
+    p>0 ~ U(-2.5, 2.5) from PCG64(seed_base + p)."""
     X = np.empty((batch, nx))
-    X[0] = default_x0(nx)
-    for p in range(1, batch):
-        X[p] = np.random.Generator(np.random.PCG64(seed_base + p)).uniform(-2.5, 2.5, nx)
+    for i, p in enumerate(range(start, start + batch)):
+        X[i] = default_x0(nx) if p == 0 else \
+            np.random.Generator(np.random.PCG64(seed_base + p)).uniform(-2.5, 2.5, nx)
     return X
 
 
@@ -159,13 +159,35 @@ def pack_lib4_batch(M: np.ndarray) -> np.ndarray:
     return np.ascontiguousarray(np.swapaxes(P, -1, -2)).reshape(lead + (pm * sd,))
 
 
+def _perturbations(N: int, nx: int, nu: int, problem_ids, seed: int):
+    """Per-problem stage perturbations drawn from a stream of the problem's own: PCG64([seed, p]) for global
+    problem p.  Returns dA (B, N, nx, nx), dB (B, N, nx, nu) and G (B, N, nx, nx) (G[:, k-1] perturbs Q_k,
+    k = 1..N), all already scaled by 1e-3.  A problem's data are then a function of (seed, p) alone, so a
+    shard of the global batch is bitwise the same block whatever the world size."""
+    ids = np.asarray(problem_ids, dtype=np.int64)
+    dA = np.empty((ids.size, N, nx, nx))
+    dB = np.empty((ids.size, N, nx, nu))
+    G = np.empty((ids.size, N, nx, nx))
+    for i, p in enumerate(ids):
+        rng = np.random.Generator(np.random.PCG64([int(seed), int(p)]))
+        dA[i] = rng.standard_normal((N, nx, nx))
+        dB[i] = rng.standard_normal((N, nx, nu))
+        G[i] = rng.standard_normal((N, nx, nx))
+    return 1e-3 * dA, 1e-3 * dB, 1e-3 * G
+
+
 def mass_spring_qp(N: int, nx: int, nu: int, *, boxes: bool = True, x0=None, batch: int | None = None,
-                   time_variant: bool = False, seed: int = 0) -> OCPQP:
+                   time_variant: bool = False, seed: int = 0, problem_ids=None) -> OCPQP:
     """The reference drivers' mass-spring MPC QP (nx[0] = 0, nu[N] = 0).
 
     ``batch`` stacks ``batch`` problems that differ in x0 (problem 0 = the drivers' x0) and, with
     ``time_variant``, in a seeded perturbation of every stage's A, B (1e-3 N(0,1)) and Q (+ G G',
     G ~ 1e-3 N(0,1)) so that no two stage buffers alias (SURVEY.md §8d roofline accounting).
+
+    With ``problem_ids`` (the global indices of the batch's problems) each problem's perturbations come from
+    its own stream ``PCG64([seed, p])`` (`_perturbations`), so the data of global problem p do not depend on
+    which batch or rank it is generated in.  Without it the perturbations come from one stream over the whole
+    batch (``PCG64(seed)``, the layout the committed goldens were generated with).
     """
     A, B = mass_spring_dynamics(nx, nu)
     b = np.full(nx, 0.1)
@@ -180,6 +202,10 @@ def mass_spring_qp(N: int, nx: int, nu: int, *, boxes: bool = True, x0=None, bat
         X0 = np.atleast_2d(np.asarray(x0, dtype=np.float64))
         assert X0.shape == (Bn, nx)
     rng = np.random.Generator(np.random.PCG64(seed))
+    per_problem = None
+    if time_variant and problem_ids is not None:
+        assert len(problem_ids) == Bn, (len(problem_ids), Bn)
+        per_problem = _perturbations(N, nx, nu, problem_ids, seed)
 
     nxv = np.array([0] + [nx] * N, dtype=np.int32)
     nuv = np.array([nu] * N + [0], dtype=np.int32)
@@ -197,7 +223,10 @@ def mass_spring_qp(N: int, nx: int, nu: int, *, boxes: bool = True, x0=None, bat
             nx1 = int(nxv[k + 1])
             Ak = np.broadcast_to(A, (Bn, nx, nx))
             Bk = np.broadcast_to(B, (Bn, nx, nu))
-            if time_variant:
+            if per_problem is not None:
+                Ak = A + per_problem[0][:, k]
+                Bk = B + per_problem[1][:, k]
+            elif time_variant:
                 Ak = A + 1e-3 * rng.standard_normal((Bn, nx, nx))
                 Bk = B + 1e-3 * rng.standard_normal((Bn, nx, nu))
             M = np.zeros((Bn, nux + 1, nx1))
@@ -211,7 +240,10 @@ def mass_spring_qp(N: int, nx: int, nu: int, *, boxes: bool = True, x0=None, bat
         M = np.zeros((Bn, nux + 1, nux))
         M[:, :nuk, :nuk] = R[:nuk, :nuk]
         Qk = np.broadcast_to(Q[:nxk, :nxk], (Bn, nxk, nxk))
-        if time_variant and nxk > 0:
+        if per_problem is not None and nxk > 0:
+            G = per_problem[2][:, k - 1]
+            Qk = Q[:nxk, :nxk] + G @ np.swapaxes(G, 1, 2)
+        elif time_variant and nxk > 0:
             G = 1e-3 * rng.standard_normal((Bn, nxk, nxk))
             Qk = Q[:nxk, :nxk] + G @ np.swapaxes(G, 1, 2)
         M[:, nuk:nux, nuk:nux] = Qk

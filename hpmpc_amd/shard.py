@@ -15,6 +15,8 @@ counts).  The same code runs over RCCL (backend "nccl", device tensors) on the G
 """
 from __future__ import annotations
 
+import numpy as np
+
 from .ocp import OCPQP, batch_x0, mass_spring_qp
 
 
@@ -71,15 +73,26 @@ def shard_range(rank: int, world: int, per_rank: int) -> tuple[int, int]:
     return rank * per_rank, (rank + 1) * per_rank
 
 
+SHARD_SEED = 1
+
+
 def make_shard(N: int, nx: int, nu: int, rank: int, world: int, per_rank: int, *, boxes: bool = True,
                time_variant: bool = True) -> OCPQP:
-    """The rank's block of the benchmark workload.  x0 of global problem p comes from PCG64(20261015+p)
-    (problem 0 = the reference drivers' x0); the time-variant stage perturbations of a block come
-    from PCG64(1 + rank)."""
+    """The rank's block of the benchmark workload, a function of the global problem indices only: x0 of
+    global problem p comes from PCG64(20261015+p) (problem 0 = the reference drivers' x0) and its
+    time-variant stage perturbations from PCG64([SHARD_SEED, p]).  So global problem p is bitwise the same QP
+    whether it is solved in a world-1 batch or in rank r's block of an 8-GPU split (configs[3]), and a
+    strong-scaling curve compares identical inputs (BASELINE.json north_star)."""
     start, stop = shard_range(rank, world, per_rank)
-    X0 = batch_x0(nx, stop)[start:stop]
-    return mass_spring_qp(N, nx, nu, boxes=boxes, batch=per_rank, x0=X0, time_variant=time_variant,
-                          seed=1 + rank)
+    return global_block(N, nx, nu, start, stop, boxes=boxes, time_variant=time_variant)
+
+
+def global_block(N: int, nx: int, nu: int, start: int, stop: int, *, boxes: bool = True,
+                 time_variant: bool = True) -> OCPQP:
+    """Global problems [start, stop) of the benchmark workload (see make_shard)."""
+    X0 = batch_x0(nx, stop - start, start=start)
+    return mass_spring_qp(N, nx, nu, boxes=boxes, batch=stop - start, x0=X0, time_variant=time_variant,
+                          seed=SHARD_SEED, problem_ids=np.arange(start, stop))
 
 
 class Reducer:

@@ -51,6 +51,22 @@ def test_shard_ranges_partition_the_batch():
     assert got == [(0, 5), (5, 10), (10, 15), (15, 20)]
 
 
+def test_shard_data_depend_on_global_index_only():
+    """Global problem p is bitwise the same QP in a world-1 batch and in any rank's block of any split
+    (configs[3]: 4096 over 8 ranks is the same problem set as 4096 on one GPU)."""
+    from hpmpc_amd.batch import pack_batch
+
+    whole = pack_batch(make_shard(8, 12, 4, 0, 1, 16))
+    for world in (2, 4, 8):
+        per = 16 // world
+        for r in range(world):
+            blk = pack_batch(make_shard(8, 12, 4, r, world, per))
+            for a, b in zip(whole, blk):
+                np.testing.assert_array_equal(a[r * per:(r + 1) * per], b)
+    # and the problems of a batch differ from one another
+    assert not np.array_equal(whole[0][1], whole[0][2])
+
+
 def test_gloo_world2_matches_single_process():
     if not os.path.exists(os.path.join(ROOT, "oracle", "liboracle.so")):
         pytest.skip("oracle not built")
