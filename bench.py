@@ -10,9 +10,9 @@ A "step" is one batch of 1024 problems (default K = 40 steps).  The K timed step
 (hpmpc_mi355x_ipm_queue): 2 x 1024 resident solver slots, each taking the next problem as soon as its
 own has converged (iterations are ticks of the pass kernels hk_ipm_fact, hk_ipm_pred, hk_ipm_corr,
 hk_ipm_update over all slots).  value = IP iterations per second over all ranks (sum of per-problem
-iteration counts / max-over-ranks time).  The roofline object is for the dominant kernel (the
-factorisation pass, hk_ipm_fact), timed with hipEvents at every kernel boundary inside the timed
-region.  An isolated single-batch solve is reported beside it.
+iteration counts / max-over-ranks time).  The roofline object is for the dominant kernel (the pass
+with the largest device time per step, priced with that pass's own algorithmic bytes; `per_pass` lists
+all four), timed with hipEvents at every kernel boundary inside the timed region.  An isolated single-batch solve is reported beside it.
 The Riccati factorisation rate (d_back_ric_rec_sv_tv_res, nb = 0, compute_pi = 1) of the same
 batch is reported in the same JSON line, and so is configs[4] ("pcond": 512 x N=200 nx=24 nu=6 condensed into
 20 blocks, the condensed Riccati and the expansion, with its own roofline and CPU baseline).

@@ -16,7 +16,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("HPMPC_ARCH", "gfx950")
 SOURCES = ["hpmpc_kernels.hip", "hk_wide.hip", "hk_wide_ipm.hip", "hk_soft.hip", "hpmpc_capi.cpp", "hpmpc_capi_wide.cpp",
            "hpmpc_capi_wide_ipm.cpp", "hpmpc_capi_iface.cpp"]
-HEADERS = ["hk_prims.h", "hk_riccati.h", "hk_ipm.h", "hpmpc_kargs.h", "hk_wide_args.h", "hk_wide_core.h", "hk_wide_host.h", "hk_soft_args.h"]
+HEADERS = ["hpmpc_api.h", "hk_prims.h", "hk_riccati.h", "hk_ipm.h", "hpmpc_kargs.h", "hk_wide_args.h", "hk_wide_core.h", "hk_wide_host.h", "hk_soft_args.h"]
 # MFMA accumulators stay in ordinary VGPRs: the stage tile is read and written by VALU code between
 # MFMAs, and the AGPR form costs 8 v_accvgpr moves each way per MFMA group.
 KFLAGS = ["-mllvm", "-amdgpu-mfma-vgpr-form"] + os.environ.get("HK_EXTRA_FLAGS", "").split()
@@ -24,6 +24,9 @@ KFLAGS = ["-mllvm", "-amdgpu-mfma-vgpr-form"] + os.environ.get("HK_EXTRA_FLAGS",
 # (tools/gpu_ab.sh, profiles/ab_sched_max_memory_clause/) measured hk_ipm_corr 3.161 -> 3.125 ms per step with
 # the other passes unchanged (max-ilp instead slowed the factorisation by 8 %).
 SRC_FLAGS = {"hpmpc_kernels.hip": ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"]}
+
+
+EXPORTS = os.path.join(CSRC, "exports.map")
 
 
 def _newer(out, deps):
@@ -41,7 +44,9 @@ def build_hip(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(objdir, exist_ok=True)
     out = os.path.join(LIBDIR, "libhpmpc_mi355x.so")
     hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, "include", "hpmpc_mi355x.h")]
-    common = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function"] + KFLAGS
+    # -fvisibility=hidden: only include/hpmpc_mi355x.h's functions are exported (csrc/hpmpc_api.h)
+    common = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall",
+              "-Wno-unused-function"] + KFLAGS
     objs, procs = [], []
     for src in SOURCES:
         obj = os.path.join(objdir, src + ".o")
@@ -54,8 +59,9 @@ def build_hip(force: bool = False, verbose: bool = False) -> str:
     for src, pr in procs:
         if pr.wait() != 0:
             raise subprocess.CalledProcessError(pr.returncode, src)
-    if procs or force or not _newer(out, objs):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC"] + objs + ["-o", out]
+    if procs or force or not _newer(out, objs + [EXPORTS]):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", f"-Wl,--version-script={EXPORTS}"] + objs + \
+              ["-o", out]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
@@ -94,6 +100,8 @@ def build_oracle(force: bool = False) -> None:
     if os.path.isdir(os.environ.get("HPMPC_REF", "/root/reference")):
         targets.append("ref")
     subprocess.run(["make", "-s", "-C", odir] + (["-B"] if force else []) + targets, check=True)
+    if "ref" in targets:  # the reference's own test_d_ric_mpc.c, unchanged, relinked against the product
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tools", "relink"), "drivers"], check=True)
 
 
 def build_all(force: bool = False, verbose: bool = False) -> None:

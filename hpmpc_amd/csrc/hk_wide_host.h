@@ -10,7 +10,7 @@
 #include <cstring>
 #include <vector>
 
-#include "../../include/hpmpc_mi355x.h"
+#include "hpmpc_api.h"
 #include "hk_wide_args.h"
 
 extern "C" int hk_wide_launch(int which, const void* args, int count, int lds_doubles, hipStream_t stream);

@@ -17,10 +17,11 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <vector>
 
-#include "../../include/hpmpc_mi355x.h"
+#include "hpmpc_api.h"
 #include "hpmpc_kargs.h"
 #include "hk_wide_args.h"
 
@@ -260,9 +261,14 @@ extern "C" long long hpmpc_mi355x_ws_doubles(const hpmpc_mi355x_plan* P) { retur
 
 extern "C" int hpmpc_mi355x_last_error(void) { return g_err; }
 
-// Diagnostic builds (-DHK_STAMPS) record s_memtime stamps of problem 0 into this device buffer.
+// Diagnostic builds (-DHK_STAMPS, build.py build_stamps) record s_memtime stamps of problem 0 into this device
+// buffer; only that build exports the setter (tools/stamps*.py load it through HPMPC_MI355X_LIB).
 static unsigned long long* g_dbg_buf = nullptr;
-extern "C" void hpmpc_mi355x_debug_buffer(void* dev_ptr) { g_dbg_buf = (unsigned long long*)dev_ptr; }
+#ifdef HK_STAMPS
+extern "C" __attribute__((visibility("default"))) void hpmpc_mi355x_debug_buffer(void* dev_ptr) {
+    g_dbg_buf = (unsigned long long*)dev_ptr;
+}
+#endif
 
 extern "C" const char* hpmpc_mi355x_version(void) {
     return "hpmpc_mi355x 0.1 gfx950 (wave-per-problem, f64 MFMA 16x16x4 stage contractions)";
@@ -343,11 +349,9 @@ int ipm_launch(const hpmpc_mi355x_plan* plan, const hpmpc_mi355x_layout* lay, in
     return g_err = 0;
 }
 
-// hipEvents (and optionally a small pinned host buffer) owned by one API call.  The destructor first
-// waits for every event recorded on them, so no queued copy or record can outlive its storage.
+// hipEvents owned by one API call.  The destructor first waits for every event recorded on them.
 struct CallEvents {
     std::vector<hipEvent_t> e;
-    int* hint = nullptr;
     bool create(int n) {
         e.reserve(n);
         for (int i = 0; i < n; i++) {
@@ -357,18 +361,12 @@ struct CallEvents {
         }
         return true;
     }
-    bool host_ints(int n) {
-        if (!hip_ok(hipHostMalloc((void**)&hint, n * sizeof(int), hipHostMallocDefault), "host alloc")) return false;
-        for (int i = 0; i < n; i++) hint[i] = 0;
-        return true;
-    }
     hipEvent_t& operator[](size_t i) { return e[i]; }
     ~CallEvents() {
         for (hipEvent_t x : e) {
             (void)hipEventSynchronize(x);
             (void)hipEventDestroy(x);
         }
-        if (hint) (void)hipHostFree(hint);
     }
 };
 
@@ -428,11 +426,54 @@ extern "C" int hpmpc_mi355x_ipm_pass(const hpmpc_mi355x_plan* plan, const hpmpc_
 // problem of a batch finishes.  The host enqueues ticks (fact, pred, corr, update) in chunks and stops
 // once the device-side finished counter reaches nq, checking a chunk behind so the stream never drains.
 namespace {
+// Polling state of the queue driver (hipEvents + a pinned copy of the device's finished counter), pooled per
+// host thread and (device, stream).  A call does not wait for the chunk it enqueued last: the next call that
+// reuses the same entry is on the same in-order stream, so its own records and counter copies land after every
+// copy the earlier call left queued, and it reads a counter only after waiting on its own event.  Calls on other
+// streams (or devices) use other entries and never see each other's counts.  Entries live as long as the thread.
+struct PollState {
+    int dev = -1;
+    hipStream_t stream = nullptr;
+    std::vector<hipEvent_t> e;
+    int* hint = nullptr;
+    ~PollState() {
+        for (hipEvent_t x : e) {
+            (void)hipEventSynchronize(x);
+            (void)hipEventDestroy(x);
+        }
+        if (hint) (void)hipHostFree(hint);
+    }
+};
+
+constexpr int kPollEvents = 2 * (8 * 4 + 1) + 2;  // enough for queue_run<R> with R <= 8
+
+PollState* poll_state(hipStream_t st) {
+    thread_local std::vector<std::unique_ptr<PollState>> pool;
+    int dev = 0;
+    if (!hip_ok(hipGetDevice(&dev), "get device")) return nullptr;
+    for (auto& p : pool)
+        if (p->dev == dev && p->stream == st) return p.get();
+    auto p = std::make_unique<PollState>();
+    p->dev = dev;
+    p->stream = st;
+    p->e.reserve(kPollEvents);
+    for (int i = 0; i < kPollEvents; i++) {
+        hipEvent_t x;
+        if (!hip_ok(hipEventCreate(&x), "event create")) return nullptr;
+        p->e.push_back(x);
+    }
+    if (!hip_ok(hipHostMalloc((void**)&p->hint, 2 * sizeof(int), hipHostMallocDefault), "host alloc")) return nullptr;
+    p->hint[0] = p->hint[1] = 0;
+    pool.push_back(std::move(p));
+    return pool.back().get();
+}
+
 // The queue driver shared by hpmpc_mi355x_ipm_queue and the single-problem entry points (which run their one
 // problem as a queue of one entry in one slot, so no pass is enqueued after it has converged).  `a` carries the
 // problem data and solver parameters; R ticks per chunk.
 template <int R>
 int queue_run(KArgs a, int nq, int n_slots, int* qctl, int k_max, double* pass_ms, int* n_ticks, hipStream_t st) {
+    static_assert(2 * (R * 4 + 1) + 2 <= kPollEvents, "poll pool sized for R <= 8");
     if (n_ticks) *n_ticks = 0;
     if (pass_ms)
         for (int i = 0; i < 5; i++) pass_ms[i] = 0.0;
@@ -441,14 +482,13 @@ int queue_run(KArgs a, int nq, int n_slots, int* qctl, int k_max, double* pass_m
     a.qctl = qctl;
     a.nslots = n_slots;
     a.qpar = 0;  // hk_ipm_init fills active list 0; iteration t runs list t & 1
-    // Per-call polling state: 2 chunk parities x (R*4 + 1) kernel boundaries + 2 "finished count copied"
-    // events, and the pinned host copy of the device's finished counter.  Nothing is shared between calls
-    // (so a later call on another stream or device can never read a stale count of this one); the
-    // destructor waits for the copies this call left queued before it frees their target.
+    // 2 chunk parities x (R*4 + 1) kernel boundaries + 2 "finished count copied" events, and the pinned host copy
+    // of the finished counter, from the (device, stream) pool above
     const int nev = R * 4 + 1;
-    CallEvents ev;
-    if (!ev.create(2 * nev + 2) || !ev.host_ints(2)) return g_err;
-    int* hdone = ev.hint;
+    PollState* ps = poll_state(st);
+    if (!ps) return g_err;
+    hipEvent_t* ev = ps->e.data();
+    int* hdone = ps->hint;
     hipEvent_t* done_ev = &ev[2 * nev];
     auto launch = [&](int which) {
         if (hk_launch(which, &a, n_slots, st)) {

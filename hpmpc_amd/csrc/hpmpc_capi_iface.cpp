@@ -18,7 +18,7 @@
 #include <cstring>
 #include <vector>
 
-#include "../../include/hpmpc_mi355x.h"
+#include "hpmpc_api.h"
 
 extern "C" void hk_set_error(int code, const char* what);
 

@@ -769,6 +769,26 @@ extern "C" hpmpc_mi355x_pcond_plan* hpmpc_mi355x_pcond_plan_create(int N, const 
         for (int k = 0; k <= N2; k++) i2[k] = q->P.idxb2.data() + P.cond.st[k].oI;
         q->wide = hpmpc_mi355x_wide_plan_create(N2, P.nx2.data(), P.nu2.data(), P.nb2.data(), i2.data(),
                                                 P.ng2.data());
+        // the wide IPM indexes BAbt2 / RSQrq2 / DCt2 / d2 / ux2 / pi2 with its own layout: it must be exactly the
+        // condensing kernels' carve (same per-problem sizes, same stage offsets), or it would read other blocks
+        if (q->wide) {
+            long long ws[8];
+            std::vector<long long> wo(6 * (size_t)(N2 + 1));
+            bool same = hpmpc_mi355x_wide_sizes(q->wide, ws) == 0 && hpmpc_mi355x_wide_offsets(q->wide, wo.data()) == 0;
+            same = same && ws[0] == P.cond.nB && ws[1] == P.cond.nR && ws[2] == P.nG2 && ws[3] == P.cond.nD &&
+                   ws[4] == P.cond.nU && ws[5] == P.cond.nP;
+            for (int k = 0; same && k <= N2; k++) {
+                const WideStage& s2 = P.cond.st[k];
+                const long long* o = wo.data() + 6 * k;  // oB, oR, oG, oD, oU, oP
+                same = o[0] == s2.oB && o[1] == s2.oR && o[3] == s2.oD && o[4] == s2.oU && o[5] == s2.oP &&
+                       (k == N2 || P.ng2[k] == 0 || o[2] == P.blk[k].oG2);
+            }
+            if (!same) {
+                fprintf(stderr, "hpmpc_mi355x: condensed wide IPM layout differs from the condensing carve\n");
+                hpmpc_mi355x_wide_plan_destroy(q->wide);
+                q->wide = nullptr;
+            }
+        }
     }
     hk_set_error(0, nullptr);  // a condensed problem beyond the wide IPM keeps the condense / Riccati pipeline
     return q;

@@ -487,6 +487,12 @@ extern "C" int hpmpc_mi355x_wide_ipm_batch(const hpmpc_mi355x_wide_plan* q, int 
         return HPMPC_MI355X_EUNSUPPORTED;
     const WIpm& W = q->W;
     const WLayout& L = W.L;
+    // every array the kernel dereferences unconditionally (DCt only when a stage has general constraints; stat is
+    // nullable): a null one is a caller error, reported instead of faulting on the device
+    if (!BAbt || !RSQrq || !d || !ux || !pi || !lam || !t || !work || !kk || !ret || (L.any_ng && !DCt)) {
+        hk_set_error(HPMPC_MI355X_EUNSUPPORTED, "hpmpc_mi355x_wide_ipm_batch: null array");
+        return HPMPC_MI355X_EUNSUPPORTED;
+    }
     WideIpmArgs a;
     memset(&a, 0, sizeof a);
     a.w.N = q->N;

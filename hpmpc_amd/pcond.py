@@ -45,6 +45,7 @@ def _bind():
     L.hpmpc_mi355x_pcond_wide_plan.restype = vp
     L.hpmpc_mi355x_pcond_wide_plan.argtypes = [vp]
     L.hpmpc_mi355x_wide_sizes.argtypes = [vp, vp]
+    L.hpmpc_mi355x_wide_offsets.argtypes = [vp, vp]
     L.hpmpc_mi355x_wide_ipm_batch.restype = i
     d = C.c_double
     L.hpmpc_mi355x_wide_ipm_batch.argtypes = [vp, i, i, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, i, d, d, d, i, i, vp,
@@ -169,7 +170,14 @@ class PcondSolver:
             ws = (C.c_longlong * 8)()
             L.hpmpc_mi355x_wide_sizes(self.wplan, ws)
             self.wsizes = [int(v) for v in ws]
-            assert self.wsizes[3] == self.sizes[8] and self.wsizes[4] == self.sizes[9], (self.wsizes, self.sizes)
+            # the wide IPM indexes the condensed arrays with its own layout: it must be the condensing carve's
+            # (the library also checks every stage offset when it creates the plan)
+            s = self.sizes
+            assert self.wsizes[:6] == [s[5], s[6], s[7], s[8], s[9], s[10]], (self.wsizes, self.sizes)
+            wo = (C.c_longlong * (6 * (self.N2 + 1)))()
+            L.hpmpc_mi355x_wide_offsets(self.wplan, wo)
+            wo = np.array(wo[:], dtype=np.int64).reshape(self.N2 + 1, 6)  # oB oR oG oD oU oP
+            assert np.array_equal(wo[:, [0, 1, 3, 4, 5]], self.off2[:, [0, 1, 2, 3, 4]]), (wo, self.off2)
         P = self.nprob
         if getattr(self, "_kmax", None) != k_max:
             self.work2 = torch.zeros((P, self.wsizes[6]), dtype=torch.float64, device=self.dev)

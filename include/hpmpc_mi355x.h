@@ -299,8 +299,9 @@ void hpmpc_mi355x_wide_plan_destroy(hpmpc_mi355x_wide_plan *plan);
 int hpmpc_mi355x_wide_sizes(const hpmpc_mi355x_wide_plan *plan, long long *out);
 /* out[6*(N+1)]: oB, oR, oG, oD, oU, oP per stage */
 int hpmpc_mi355x_wide_offsets(const hpmpc_mi355x_wide_plan *plan, long long *out);
-/* problems [p0, p0+count) of the batch; kk / ret per problem, stat 5*k_max per problem, work: each problem's work
- * image (factor, iterate backup).  Asynchronous on `stream` (a hipStream_t, or null). */
+/* problems [p0, p0+count) of the batch; kk / ret per problem, stat 5*k_max per problem (nullable), work: each
+ * problem's work image (factor, iterate backup).  Every other array is required (DCt only when some stage has
+ * ng > 0): a null one returns HPMPC_MI355X_EUNSUPPORTED.  Asynchronous on `stream` (a hipStream_t, or null). */
 int hpmpc_mi355x_wide_ipm_batch(const hpmpc_mi355x_wide_plan *plan, int nprob, int p0, int count, const double *BAbt,
                                 const double *RSQrq, const double *DCt, const double *d, double *ux, double *pi,
                                 double *lam, double *t, double *work, int k_max, double mu0, double mu_tol,

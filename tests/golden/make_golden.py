@@ -219,6 +219,8 @@ def main():
     pcond(ref, out)
     iface(ref, out)
     wide(ref, ref_avx_api(), out)
+    divergent(ref, out)
+    driver(out)
     total = sum(os.path.getsize(p) for p in out)
     print(f"wrote {len(out)} cases, {total / 1e6:.2f} MB")
 
@@ -400,6 +402,63 @@ def wide(ref, refa, out):
                              outs, extra=IO.to_flat(P)))
 
 
+def parse_ric_driver(text):
+    """ux / pi rows printed by test_problems/test_d_ric_mpc.c (d_print_mat, "%9.5f")."""
+    blocks = {"ux": [], "pi": []}
+    cur = None
+    for line in text.splitlines():
+        w = line.split()
+        if w in (["ux"], ["pi"]):
+            cur = w[0]
+            continue
+        if cur and w:
+            try:
+                blocks[cur].append([float(x) for x in w])
+            except ValueError:
+                cur = None
+    return blocks
+
+
+def driver(out):
+    """The reference's own driver test_problems/test_d_ric_mpc.c, compiled unchanged and linked against the full
+    reference (tools/relink/Makefile), run on the host: its printed ux / pi (N=10 nx=8 nu=3, after 1000 sv, trf and
+    trs calls) pin tests/test_gpu_ref_driver.py, which runs the same driver relinked against libhpmpc_mi355x.so."""
+    import subprocess
+    import tempfile
+
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tools", "relink"), "drivers"], check=True)
+    exe = os.path.join(ROOT, "oracle", "_ref", "relink", "test_d_ric_mpc_ref")
+    with tempfile.TemporaryDirectory() as d:
+        os.makedirs(os.path.join(d, "test_problems", "results"))
+        text = subprocess.run([exe], cwd=d, check=True, capture_output=True, text=True, timeout=300).stdout
+    b = parse_ric_driver(text)
+    path = os.path.join(HERE, "drivers", "test_d_ric_mpc.npz")
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    ux = np.concatenate([np.asarray(r) for r in b["ux"]])
+    uxn = np.array([len(r) for r in b["ux"]], dtype=np.int32)
+    np.savez_compressed(path, ux=ux, ux_len=uxn, pi=np.asarray(b["pi"]))
+    out.append(path)
+
+
+def divergent(ref, out):
+    """Infeasible draws of the benchmark workload (hpmpc_amd.shard.make_shard(100, 12, 4, 0, 1, 1024), global
+    problems 841 and 920): the primal-dual iterates diverge (lam -> 1e17..1e19) until the step length falls below
+    alpha_min (ret 2).  The exit iteration is set by amplified last bits: the oracle (a second c99 build of the
+    same algorithm) exits 2 iterations earlier than the reference on both (28 vs 30, 38 vs 40; over the whole
+    1024-problem batch the two builds differ by 1-2 iterations on 30 of its 91 divergent problems).  These pin
+    the divergence gate of tests/helpers.py compare_ipm (same ret, kk within 2)."""
+    from hpmpc_amd.shard import make_shard
+
+    qp = make_shard(100, 12, 4, 0, 1, 1024)
+    args = dict(k_max=50, mu0=2.0, mu_tol=1e-12, alpha_min=1e-8)
+    for p in (841, 920):
+        one = qp.problem(p)
+        r = ref.ipm(one.copy(), **args)
+        out.append(save_case(f"ipm_div_p{p}_N100_nx12_nu4", "ipm_div", one, args,
+                             dict(ux=r["ux"], pi=r["pi"], lam=r["lam"], t=r["t"], stat=r["stat"], kk=r["kk"],
+                                  ret=r["ret"])))
+
+
 def soft(ref, out):
     """Soft-constraint IPM d_ip2_mpc_soft_tv (mpc_solvers/d_ip2_soft.c:83): the reference driver's problem
     (test_d_ip_soft.c: Q = 0, Z = 0, z = 100, mu0 = 100) at three sizes, stopped at mu_tol = 1e-5 -- below that its
@@ -443,6 +502,14 @@ if __name__ == "__main__":
         o = []
         wide(ref_api(), ref_avx_api(), o)
         print(f"wrote {len(o)} wide cases, {sum(os.path.getsize(p) for p in o) / 1e6:.2f} MB")
+    elif len(sys.argv) > 1 and sys.argv[1] == "driver":
+        o = []
+        driver(o)
+        print(f"wrote {o}")
+    elif len(sys.argv) > 1 and sys.argv[1] == "divergent":
+        o = []
+        divergent(ref_api(), o)
+        print(f"wrote {len(o)} divergent cases, {sum(os.path.getsize(p) for p in o) / 1e6:.2f} MB")
     elif len(sys.argv) > 1 and sys.argv[1] == "pcond":
         o = []
         pcond(ref_api(), o)

@@ -33,7 +33,7 @@ def run_case(api, case):
         mem = api.ric_trf(qp, bd=inp["bd"], Qx=inp["Qx"])
         ux, pi, Pb = api.ric_trs(qp, mem, b=inp["b"], q=inp["q"], qx=inp["qx"], compute_pi=1, compute_Pb=1)
         return dict(ux=ux, pi=pi, Pb=Pb)
-    if case.kind == "ipm":
+    if case.kind in ("ipm", "ipm_div"):
         kw = dict(k_max=int(a["k_max"]), mu0=a["mu0"], mu_tol=a["mu_tol"], alpha_min=a["alpha_min"])
         if a.get("warm_start"):
             kw.update(warm_start=1, ux=inp["ux0"])
@@ -64,6 +64,13 @@ def run_case(api, case):
         c, _ = api.part_cond(qp, int(a["N2"]))
         e = api.part_expand(qp, c, inp["u2"], inp["p2"], inp["lam2"], inp["t2"])
         return dict(cqp=c, ux=e["ux"], pi=e["pi"], lam=e["lam"], t=e["t"])
+    if case.kind == "ipm_div":
+        # a diverging infeasible problem: only ret and kk to +-2 are comparable (the reference and a second c99
+        # build of it differ by 2 iterations on these very cases, make_golden.py divergent())
+        out = case.out
+        assert int(got["ret"]) == int(out["ret"]) == 2, (case.name, got["ret"], out["ret"])
+        assert abs(int(got["kk"]) - int(out["kk"])) <= 2, (case.name, got["kk"], out["kk"])
+        return
     if case.kind == "pcond_sv":
         return pcond_sv(api, qp, int(a["N2"]))
     if case.kind in ("iface", "iface_kkt"):
@@ -247,6 +254,13 @@ def check_case(case, got):
         return check_pcond(case, got)
     if case.kind in ("iface", "iface_kkt"):
         return check_iface(case, got)
+    if case.kind == "ipm_div":
+        # a diverging infeasible problem: only ret and kk to +-2 are comparable (the reference and a second c99
+        # build of it differ by 2 iterations on these very cases, make_golden.py divergent())
+        out = case.out
+        assert int(got["ret"]) == int(out["ret"]) == 2, (case.name, got["ret"], out["ret"])
+        assert abs(int(got["kk"]) - int(out["kk"])) <= 2, (case.name, got["kk"], out["kk"])
+        return
     if case.kind == "pcond_sv":
         for key in ("ux", "pi"):
             e = max_err(case, key, got[key], case.out[key])
@@ -346,7 +360,8 @@ def compare_ipm(case_like_qp, a, b, tol=TOL_IPM, allow_divergent=False):
         if lam_max > 1e12:
             assert allow_divergent, f"oracle diverged (ret 2, |lam| = {lam_max:.1e}) on a case that must compare"
             # the iteration at which the step length of a divergence (lam growing ~10x per iteration) falls
-            # below alpha_min is itself set by amplified last bits: +-2 iterations, same exit code
+            # below alpha_min is itself set by amplified last bits: +-2 iterations, same exit code -- the
+            # reference build and the oracle differ by exactly that on the ipm_div goldens (make_golden.py)
             assert abs(a["kk"] - b["kk"]) <= 2, (a["kk"], b["kk"])
             DIVERGENT_SKIPS.append((int(b["kk"]), lam_max))
             return 0.0

@@ -57,6 +57,20 @@ def test_library_exports_every_declared_symbol(hiplib):
     assert not missing, missing
 
 
+def test_library_exports_nothing_else(hiplib):
+    """A shim linked beside the reference archive must not leak internal symbols into the caller's namespace:
+    the dynamic symbol table is exactly the header's functions (build: -fvisibility=hidden + exports.map)."""
+    import shutil
+    import subprocess
+
+    if shutil.which("nm") is None:
+        pytest.skip("nm not available")
+    out = subprocess.run(["nm", "-D", "--defined-only", batch.LIBPATH], check=True, capture_output=True,
+                         text=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if len(ln.split()) >= 3}
+    assert exported == set(header_functions()), sorted(exported ^ set(header_functions()))
+
+
 def test_every_reference_citation_resolves():
     """Each prototype cites the reference declaration it replaces; the cited headers exist in the
     reference layout (checked by name only: the reference tree is not needed at run time)."""

@@ -168,8 +168,10 @@ def test_batch_ipm_vs_oracle(oracle, small_batch):
                    t=[t[p, k] for k in range(31)])
         # infeasible draws of x0 diverge (ret 2, lam -> 1e33) in the oracle and on the GPU alike: kk/ret only
         compare_ipm(one, got, r, allow_divergent=True)
+    # this seeded batch has exactly one infeasible (diverging) problem, p = 59 (oracle and reference: kk 16,
+    # ret 2, lam -> 3e33); nothing else may take the divergence escape
     n_div = len(DIVERGENT_SKIPS) - skips0
-    assert n_div <= int((ret == 2).sum()) and n_div <= qp.batch // 8, n_div
+    assert n_div <= 1, n_div
 
 
 def test_batch_riccati_vs_oracle(oracle):

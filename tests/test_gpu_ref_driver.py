@@ -1,0 +1,38 @@
+"""The reference's own driver, unchanged, on the MI355X.
+
+test_problems/test_d_ric_mpc.c (with test_problems/tools.c) is compiled unchanged from the reference sources and
+linked against the reference archive minus the files libhpmpc_mi355x.so replaces plus -lhpmpc_mi355x
+(tools/relink/Makefile, in the build container; the binary travels to the GPU box as oracle/_ref/drivers/).  Run
+here, its 1000 sv + 1000 trf + 1000 trs calls go through the drop-in boundary to the GPU, and the ux / pi it
+prints (d_print_mat, "%9.5f") must be what the same driver linked against the whole reference prints on the
+host (tests/golden/drivers/test_d_ric_mpc.npz, make_golden.py driver()).
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DRV = os.path.join(ROOT, "oracle", "_ref", "drivers", "test_d_ric_mpc")
+
+
+def test_unchanged_reference_driver_on_gpu(tmp_path):
+    assert os.path.exists(DRV), "relinked reference driver not built (tools/relink/Makefile drivers)"
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from make_golden import parse_ric_driver
+
+    (tmp_path / "test_problems" / "results").mkdir(parents=True)
+    r = subprocess.run([DRV], cwd=tmp_path, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "hpmpc_mi355x" not in r.stderr, r.stderr[-2000:]  # no error line from the shim
+    b = parse_ric_driver(r.stdout)
+    z = np.load(os.path.join(ROOT, "tests", "golden", "drivers", "test_d_ric_mpc.npz"))
+    ux = np.concatenate([np.asarray(x) for x in b["ux"]])
+    assert ux.shape == z["ux"].shape and np.asarray(b["pi"]).shape == z["pi"].shape
+    # same numbers at the printed precision (one unit of the 5th decimal covers a rounding-boundary flip)
+    np.testing.assert_allclose(ux, z["ux"], rtol=0, atol=1.01e-5)
+    np.testing.assert_allclose(np.asarray(b["pi"]), z["pi"], rtol=0, atol=1.01e-5)
+    print(r.stdout.strip().splitlines()[-1])  # the driver's own timing line (sv / trf / trs through the GPU)

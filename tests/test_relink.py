@@ -81,3 +81,49 @@ def test_reference_auxiliaries_still_come_from_the_reference(relinked):
 def test_driver_needs_the_shim_library(relinked):
     r = subprocess.run(["readelf", "-d", relinked], check=True, capture_output=True, text=True).stdout
     assert "libhpmpc_mi355x.so" in r
+
+
+# ------------------------------------------------------------------ the reference's own driver, unchanged
+DRV = os.path.join(ROOT, "oracle", "_ref", "drivers", "test_d_ric_mpc")
+RIC_SYMS = ["d_back_ric_rec_sv_tv_res", "d_back_ric_rec_trf_tv_res", "d_back_ric_rec_trs_tv_res",
+            "d_back_ric_rec_sv_tv_work_space_size_bytes", "d_back_ric_rec_sv_tv_memory_space_size_bytes"]
+
+
+@pytest.fixture(scope="module")
+def drivers():
+    r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tools", "relink"), f"REF={REF}", "drivers"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return DRV
+
+
+def test_unchanged_reference_driver_relinks(drivers):
+    """test_problems/test_d_ric_mpc.c and tools.c compile unchanged (gcc -DTARGET_C99_4X4) and link against the
+    reference archive minus the replaced objects plus -lhpmpc_mi355x: every Riccati entry point it calls is
+    undefined in its object, defined by the shim, and bound dynamically by the executable."""
+    drv_undef = _syms(_nm(os.path.join(OUT, "drv", "test_d_ric_mpc.o")), {"U"})
+    shim_def = _syms(_nm("-D", "--defined-only", LIB), {"T"})
+    exe_undef = _syms(_nm("-D", "--undefined-only", drivers), {"U"})
+    for s in RIC_SYMS:
+        assert s in drv_undef and s in shim_def and s in exe_undef, s
+
+
+def test_reference_driver_output_is_the_golden(drivers):
+    """The same unchanged driver linked against the whole reference, run here on the host, prints exactly the
+    ux / pi that tests/golden/drivers/test_d_ric_mpc.npz holds (what the GPU-relinked run is compared with)."""
+    import sys
+    import tempfile
+
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from make_golden import parse_ric_driver
+
+    with tempfile.TemporaryDirectory() as d:
+        os.makedirs(os.path.join(d, "test_problems", "results"))
+        text = subprocess.run([os.path.join(OUT, "test_d_ric_mpc_ref")], cwd=d, check=True, capture_output=True,
+                              text=True, timeout=300).stdout
+    b = parse_ric_driver(text)
+    z = np.load(os.path.join(ROOT, "tests", "golden", "drivers", "test_d_ric_mpc.npz"))
+    np.testing.assert_array_equal(np.concatenate([np.asarray(r) for r in b["ux"]]), z["ux"])
+    np.testing.assert_array_equal(np.asarray(b["pi"]), z["pi"])
