@@ -177,18 +177,52 @@ def test_pcond_ipm_batch_pipeline(oracle, N, nx, nu, N2, B):
     hk_pexpand, against the oracle's d_part_cond -> d_ip2_res_mpc_hard_tv -> d_part_expand_solution problem by
     problem: identical iteration counts and return codes, the expanded point close to the oracle's and meeting the
     original problem's KKT conditions as tightly."""
-    from hpmpc_amd.cabi import bq_from_qp
     from hpmpc_amd.ocp import mass_spring_qp
+
+    _pcond_ipm_vs_oracle(oracle, mass_spring_qp(N, nx, nu, boxes=True, batch=B, time_variant=True, seed=N), N2,
+                         range(B))
+
+
+def test_pcond_ipm_full_size(oracle):
+    """configs[4] with boxes at its full size: 512 x N=200 nx=24 nu=6 condensed into 20 blocks (ng2 = 108 general
+    constraints per inner block), the whole batch in one wide-IPM launch; split launches are bitwise the whole
+    batch's, and sampled problems -- converged ones and non-converged ones -- match the oracle's pipeline."""
+    import torch
+
+    from hpmpc_amd.shard import global_block
+
+    bq = global_block(200, 24, 6, 0, 512)
+    s = _pcond_ipm_vs_oracle(oracle, bq, 20, [])
+    ux1, kk1, ret1 = s.ux.clone(), s.kk2.clone(), s.ret2.clone()
+    s.ux.zero_()
+    s.condense(0, 200)
+    s.condense(200, 312)
+    s.ipm(k_max=60, p0=0, count=300)
+    s.ipm(k_max=60, p0=300, count=212)
+    s.expand()
+    torch.cuda.synchronize()
+    assert torch.equal(s.ux, ux1) and torch.equal(s.kk2, kk1) and torch.equal(s.ret2, ret1)
+    ret = ret1.cpu().numpy()
+    conv, bad = np.nonzero(ret == 0)[0], np.nonzero(ret != 0)[0]
+    assert conv.size > 0
+    sample = sorted({int(conv[0]), int(conv[-1]), int(conv[conv.size // 2])} | {int(p) for p in bad[:2]})
+    _pcond_ipm_vs_oracle(oracle, bq, 20, sample, solver=s)
+
+
+def _pcond_ipm_vs_oracle(oracle, bq, N2, problems, solver=None):
+    from hpmpc_amd.cabi import bq_from_qp
     from hpmpc_amd.pcond import PcondSolver
 
-    bq = mass_spring_qp(N, nx, nu, boxes=True, batch=B, time_variant=True, seed=N)
-    s = PcondSolver(bq, N2)
-    s.solve_ipm(k_max=60)
+    N, nx = bq.N, int(bq.nx[1])
+    s = solver
+    if s is None:
+        s = PcondSolver(bq, N2)
+        s.solve_ipm(k_max=60)
     import torch
 
     torch.cuda.synchronize()
     kk, ret = s.kk2.cpu().numpy(), s.ret2.cpu().numpy()
-    for p in range(B):
+    for p in problems:
         qp = bq.problem(p)
         c, _ = oracle.part_cond(qp.copy(), N2)
         r = oracle.ipm(c.copy(), k_max=60)
@@ -224,3 +258,4 @@ def test_pcond_ipm_batch_pipeline(oracle, N, nx, nu, N2, B):
             got = max(float(np.max(np.abs(x), initial=0)) for x in rg[key])
             ref = max(float(np.max(np.abs(x), initial=0)) for x in ro[key])
             assert got <= max(10 * ref, 1e-9), (p, key, got, ref)
+    return s
