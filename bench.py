@@ -335,9 +335,9 @@ def cpu_pcond_ipm_baseline(qp, N2, k_max, seconds):
 
 def bench_single_qp(args, torch, stream):
     """configs[1]: one QP (the drivers' x0, test_d_ip_hard.c:306-322) solved alone on the GPU: the device time of
-    a one-entry problem queue (data resident in HBM; the same run as the drop-in's), of the batched API with a
-    batch of one, and the drop-in d_ip2_res_mpc_hard_tv call on host lib4 buffers (PCIe staging included).
-    Latency-bound: one wavefront walks the N stages serially."""
+    the latency path (hpmpc_mi355x_ipm_solo, data resident in HBM; the kernel the drop-in runs), of a one-entry
+    problem queue, of the batched API with a batch of one, and the drop-in d_ip2_res_mpc_hard_tv call on host lib4
+    buffers (PCIe staging included).  Latency-bound: one wavefront walks the N stages serially."""
     from hpmpc_amd.batch import LIBPATH, BatchSolver
     from hpmpc_amd.cabi import HpmpcAPI, load
     from hpmpc_amd.ocp import mass_spring_qp
@@ -345,20 +345,28 @@ def bench_single_qp(args, torch, stream):
     one = mass_spring_qp(args.N, args.nx, args.nu, batch=1)
     s = BatchSolver(one, k_max=args.k_max)
     reps = max(min(args.steps, 20), 5)
-    # a queue of one entry in one slot: the passes stop a chunk after convergence (the batched solve
-    # hpmpc_mi355x_ipm_batch enqueues k_max x 4 pass launches; its time is reported beside)
+    # the latency path (hpmpc_mi355x_ipm_solo, what the drop-in calls): the whole solve in one launch; beside it a
+    # queue of one entry in one slot (pass kernels, chunks of 8 iterations) and the batched solve
+    # (hpmpc_mi355x_ipm_batch: k_max x 4 pass launches)
     Q = s.queue(1, 1)
     for _ in range(2):
         Q.run()
         s.ipm()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
-    for a, b in ev:
-        a.record(stream)
-        Q.run()
-        b.record(stream)
-    torch.cuda.synchronize()
-    ms = float(np.median([a.elapsed_time(b) for a, b in ev]))
-    kk = int(Q.kk[0].item())
+        s.ipm_solo()
+
+    def timed(fn):
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+        for a, b in ev:
+            a.record(stream)
+            fn()
+            b.record(stream)
+        torch.cuda.synchronize()
+        return float(np.median([a.elapsed_time(b) for a, b in ev]))
+
+    ms = timed(s.ipm_solo)
+    kk = int(s.kk[0].item())
+    ms_queue = timed(Q.run)
+    assert int(Q.kk[0].item()) == kk
     evb = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
     for a, b in evb:
         a.record(stream)
@@ -374,7 +382,8 @@ def bench_single_qp(args, torch, stream):
         call()
     host_ms = (time.perf_counter() - t0) / reps * 1e3
     return {"workload": f"single_qp_N{args.N}_nx{args.nx}_nu{args.nu}", "kk": kk, "device_ms_per_solve": ms,
-            "device_us_per_ip_iter": ms * 1e3 / max(kk, 1), "batch_api_ms_per_solve": ms_batch,
+            "device_us_per_ip_iter": ms * 1e3 / max(kk, 1), "path": "hpmpc_mi355x_ipm_solo (one launch per solve)",
+            "queue1_ms_per_solve": ms_queue, "batch_api_ms_per_solve": ms_batch,
             "dropin_ms_per_solve": host_ms, "dropin_kk": int(kkc.value)}
 
 

@@ -42,6 +42,9 @@ def lib() -> C.CDLL:
         L.hpmpc_mi355x_plan_destroy.argtypes = [vp]
         L.hpmpc_mi355x_ws_doubles.restype = ll
         L.hpmpc_mi355x_ws_doubles.argtypes = [vp]
+        L.hpmpc_mi355x_ipm_solo.restype = i
+        L.hpmpc_mi355x_ipm_solo.argtypes = [vp, vp, i, i, i, vp, vp, vp, vp, vp, vp, vp, vp, i, d, d, d, i, i, vp,
+                                            vp, vp, vp]
         L.hpmpc_mi355x_ipm_batch.restype = i
         L.hpmpc_mi355x_ipm_batch.argtypes = [vp, vp, i, i, i, vp, vp, vp, vp, vp, vp, vp, vp, i, d, d, d, i, i, vp,
                                              vp, vp, vp]
@@ -193,6 +196,17 @@ class BatchSolver:
             self.ret.data_ptr(), self.stat.data_ptr(), self._stream())
         if rc != 0:
             raise RuntimeError(f"hpmpc_mi355x_ipm_batch failed ({rc})")
+
+    def ipm_solo(self, *, mu0=2.0, mu_tol=1e-12, alpha_min=1e-8, warm_start=0, compute_mult=1, p0=0, count=None):
+        """ipm() as the latency path: each problem's whole solve in one launch (hpmpc_mi355x_ipm_solo)."""
+        count = self.nprob - p0 if count is None else count
+        rc = lib().hpmpc_mi355x_ipm_solo(
+            self.plan, C.byref(self.layout), self.nprob, p0, count, self.BAbt.data_ptr(), self.RSQrq.data_ptr(),
+            self.d.data_ptr(), self.ux.data_ptr(), self.pi.data_ptr(), self.lam.data_ptr(), self.t.data_ptr(),
+            self.ws.data_ptr(), self.k_max, mu0, mu_tol, alpha_min, warm_start, compute_mult, self.kk.data_ptr(),
+            self.ret.data_ptr(), self.stat.data_ptr(), self._stream())
+        if rc != 0:
+            raise RuntimeError(f"hpmpc_mi355x_ipm_solo failed ({rc})")
 
     def ipm_pass(self, pss, *, mu0=2.0, mu_tol=1e-12, alpha_min=1e-8, warm_start=0, compute_mult=1, p0=0,
                  count=None):

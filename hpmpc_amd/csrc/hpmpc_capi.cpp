@@ -54,7 +54,7 @@ extern "C" void hk_wide_trs_entry(int N, int* nx, int* nu, int* nb, int** idxb, 
 
 namespace {
 
-enum { K_SV = 0, K_TRF = 1, K_TRS = 2, K_RES = 3, K_IPM = 4, K_KKT = 5, K_KKT_P1 = 6 };
+enum { K_SV = 0, K_TRF = 1, K_TRS = 2, K_RES = 3, K_IPM = 4, K_KKT = 5, K_KKT_P1 = 6, K_SOLO = 15 };
 constexpr int FSTRIDE = 352, V16 = 16, V32 = 32, BS = 4, NCL = 2;
 
 struct StageInfoH {  // mirror of hk::StageInfo
@@ -215,7 +215,9 @@ extern "C" hpmpc_mi355x_plan* hpmpc_mi355x_plan_create(int N, const int* nx, con
         }
         P->offR[k] = P->packR;
         P->packR += (long long)rup(nux + 1, BS) * s.sdR;
-        P->idxb[k].assign(idxb[k], idxb[k] + nb[k]);
+        // idxb[k] is read only for a stage with boxes: callers without boxes may pass idxb = NULL (the reference's
+        // test_d_ric_mpc.c does), exactly as the reference never touches it there
+        if (nb[k] > 0) P->idxb[k].assign(idxb[k], idxb[k] + nb[k]);
         P->nbt += nb[k];
         for (int l = 0; l < nb[k]; l++) {
             const int v = idxb[k][l];
@@ -379,6 +381,15 @@ extern "C" int hpmpc_mi355x_ipm_batch(const hpmpc_mi355x_plan* plan, const hpmpc
                                       int* kk, int* ret, double* stat, void* stream) {
     return ipm_launch(plan, lay, nprob, p0, count, BAbt, RSQrq, d, ux, pi, lam, t, ws, k_max, mu0, mu_tol, alpha_min,
                       warm_start, compute_mult, kk, ret, stat, K_IPM, stream);
+}
+
+extern "C" int hpmpc_mi355x_ipm_solo(const hpmpc_mi355x_plan* plan, const hpmpc_mi355x_layout* lay, int nprob, int p0,
+                                     int count, const double* BAbt, const double* RSQrq, const double* d, double* ux,
+                                     double* pi, double* lam, double* t, double* ws, int k_max, double mu0,
+                                     double mu_tol, double alpha_min, int warm_start, int compute_mult, int* kk,
+                                     int* ret, double* stat, void* stream) {
+    return ipm_launch(plan, lay, nprob, p0, count, BAbt, RSQrq, d, ux, pi, lam, t, ws, k_max, mu0, mu_tol, alpha_min,
+                      warm_start, compute_mult, kk, ret, stat, K_SOLO, stream);
 }
 
 extern "C" int hpmpc_mi355x_ipm_batch_profiled(const hpmpc_mi355x_plan* plan, const hpmpc_mi355x_layout* lay,
@@ -1065,11 +1076,13 @@ int ipm_entry(int single_newton, int phase1_only, int* kk, int k_max, double mu0
     a.compute_mult = compute_mult;
     a.single_newton = single_newton;
     a.phase1_only = phase1_only;
-    // the solve runs as a queue of one entry in one slot: passes are enqueued in chunks of 4 iterations and
-    // stop one chunk after the problem has finished, instead of k_max x 4 launches
+    // the whole solve in one launch (hk_ipm_solo): one workgroup runs init and every iteration's passes back to
+    // back, its stage data and factor records resident in one XCD's L2
     if (!up(A)) return g_err;
-    if (queue_run<4>(a, 1, 1, reinterpret_cast<int*>(g_ctx.dev + A.qctl), k_max, nullptr, nullptr, g_ctx.stream))
+    if (hk_launch(K_SOLO, &a, 1, g_ctx.stream)) {
+        set_err(HPMPC_MI355X_EHIP, "hk_ipm_solo launch failed");
         return g_err;
+    }
     if (!down(A)) return g_err;
     const int* iv = reinterpret_cast<const int*>(H + A.ints);
     *kk = iv[0];

@@ -564,18 +564,16 @@ __global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_init(KArgs a) {
     ipm_start<FX, 7, true>(a, T, v);
 }
 
+// The bodies of the four iteration passes.  Each runs one pass of one problem (its IpmView) and reads / writes
+// the problem's control state in its workspace; the pass kernels run one body over a batch or queue, the solo
+// kernel runs them all in sequence for one problem per workgroup.
+namespace {
+
 // Factorisation of the iteration's KKT system, Hessian / gradient box terms fused into the fetch.
 template <class FX>
-__global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_fact(KArgs a) {
-    // queue: empty the list this iteration's update pass fills (nothing reads it before then)
-    if (a.nq && blockIdx.x == 0 && lane_id() == 0) *qcount(a, a.qpar ^ 1) = 0;
-    Who who;
-    if (!who_am_i(a, who) || !slot_active(a, who)) return;  // idle slots leave before staging the tables
-    const LdsTabs T = lds_tables(a);
+__device__ __forceinline__ void fact_body(const KArgs& a, const LdsTabs& T, IpmView& v) {
     Scratch& sm = *T.sm;
-    IpmView v = ipm_view(a, T, who);
     const double* st = v.w.state;
-    if (st[S_ACTIVE] == 0.0) return;
     const bool sn = a.single_newton != 0;
     if (st[S_PHASE] == 1.0)
         ric_backward<true, BX_P1, FX>(v.io, &sm, 0, nullptr, 0, nullptr, v.bc, 1, v.w.Pb);
@@ -588,14 +586,9 @@ __global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_fact(KArgs a) {
 
 // Predictor solve with the box steps and step length fused in, then mu_aff and the centering target.
 template <class FX>
-__global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_pred(KArgs a) {
-    Who who;
-    if (!who_am_i(a, who) || !slot_active(a, who)) return;  // idle slots leave before staging the tables
-    const LdsTabs T = lds_tables(a);
+__device__ __forceinline__ void pred_body(const KArgs& a, const LdsTabs& T, IpmView& v) {
     Scratch& sm = *T.sm;
-    IpmView v = ipm_view(a, T, who);
     double* st = v.w.state;
-    if (st[S_ACTIVE] == 0.0) return;
     const bool sn = a.single_newton != 0;
     const int phase = (int)st[S_PHASE], kk = (int)st[S_KK];
     const double mu = st[S_MU];
@@ -630,14 +623,9 @@ __global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_pred(KArgs a) {
 
 // Corrector: centering / gradient update fused into the trs backward, box steps + alpha into its forward.
 template <class FX>
-__global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_corr(KArgs a) {
-    Who who;
-    if (!who_am_i(a, who) || !slot_active(a, who)) return;  // idle slots leave before staging the tables
-    const LdsTabs T = lds_tables(a);
+__device__ __forceinline__ void corr_body(const KArgs& a, const LdsTabs& T, IpmView& v) {
     Scratch& sm = *T.sm;
-    IpmView v = ipm_view(a, T, who);
     double* st = v.w.state;
-    if (st[S_ACTIVE] == 0.0) return;
     const int phase = (int)st[S_PHASE], kk = (int)st[S_KK];
     v.bc.smu = st[S_SMU];
     double al = 1.0;
@@ -655,40 +643,127 @@ __global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_corr(KArgs a) {
     }
 }
 
-// Update of the iterate (with backups) and, in phase 2, the residuals of the new iterate; loop control.
+// Update of the iterate (with backups) and, in phase 2, the residuals of the new iterate; loop control.  Returns
+// whether the problem iterates again (CI: stages per chunk of the element-wise passes).
+template <class FX, int CI>
+__device__ __forceinline__ bool update_body(const KArgs& a, IpmView& v) {
+    double* st = v.w.state;
+    const int phase = (int)st[S_PHASE];
+    int kk = (int)st[S_KK];
+    const double alpha = st[S_ALPHA];
+    double mu;
+    if (phase == 1) {
+        mu = update_p1_pass<CI>(v.io, v.bc, alpha, st[S_MUSCAL], v.ux, v.pi, v.w.dux, v.w.dpi, v.w.ux_bkp,
+                                v.w.pi_bkp, v.w.lam_bkp, v.w.t_bkp);
+    } else {
+        if (a.no_bkp)  // wave-uniform: the public queue API keeps no backups (nothing re-solves its slots)
+            mu = update_p2_pass<CI, true, false>(v.io, v.bc, v.bt.slotvar, alpha, st[S_MUSCAL], v.ux, v.pi, v.w.dux,
+                                                 v.w.dpi, v.w.ux_bkp, v.w.pi_bkp, v.w.lam_bkp, v.w.t_bkp, v.w.res_d,
+                                                 v.w.res_m);
+        else
+            mu = update_p2_pass<CI, true>(v.io, v.bc, v.bt.slotvar, alpha, st[S_MUSCAL], v.ux, v.pi, v.w.dux, v.w.dpi,
+                                          v.w.ux_bkp, v.w.pi_bkp, v.w.lam_bkp, v.w.t_bkp, v.w.res_d, v.w.res_m);
+    }
+    wsync();
+    if (v.l == 0) v.stat[5 * kk + 4] = mu;
+    kk++;
+    return ipm_continue<FX, CI>(a, v, kk, mu, alpha, st[S_SIGMA], phase);
+}
+
+}  // namespace
+
+template <class FX>
+__global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_fact(KArgs a) {
+    // queue: empty the list this iteration's update pass fills (nothing reads it before then)
+    if (a.nq && blockIdx.x == 0 && lane_id() == 0) *qcount(a, a.qpar ^ 1) = 0;
+    Who who;
+    if (!who_am_i(a, who) || !slot_active(a, who)) return;  // idle slots leave before staging the tables
+    const LdsTabs T = lds_tables(a);
+    IpmView v = ipm_view(a, T, who);
+    if (v.w.state[S_ACTIVE] == 0.0) return;
+    fact_body<FX>(a, T, v);
+}
+
+template <class FX>
+__global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_pred(KArgs a) {
+    Who who;
+    if (!who_am_i(a, who) || !slot_active(a, who)) return;  // idle slots leave before staging the tables
+    const LdsTabs T = lds_tables(a);
+    IpmView v = ipm_view(a, T, who);
+    if (v.w.state[S_ACTIVE] == 0.0) return;
+    pred_body<FX>(a, T, v);
+}
+
+template <class FX>
+__global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_corr(KArgs a) {
+    Who who;
+    if (!who_am_i(a, who) || !slot_active(a, who)) return;  // idle slots leave before staging the tables
+    const LdsTabs T = lds_tables(a);
+    IpmView v = ipm_view(a, T, who);
+    if (v.w.state[S_ACTIVE] == 0.0) return;
+    corr_body<FX>(a, T, v);
+}
+
 template <class FX>
 __global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_update(KArgs a) {
     Who who;
     if (!who_am_i(a, who) || !slot_active(a, who)) return;  // idle slots leave before staging the tables
     const LdsTabs T = lds_tables(a);
     IpmView v = ipm_view(a, T, who);
-    double* st = v.w.state;
-    if (st[S_ACTIVE] == 0.0) return;
-    const int phase = (int)st[S_PHASE];
-    int kk = (int)st[S_KK];
-    const double alpha = st[S_ALPHA];
-    double mu;
-    if (phase == 1) {
-        mu = update_p1_pass<4>(v.io, v.bc, alpha, st[S_MUSCAL], v.ux, v.pi, v.w.dux, v.w.dpi, v.w.ux_bkp,
-                               v.w.pi_bkp, v.w.lam_bkp, v.w.t_bkp);
-    } else {
-        if (a.no_bkp)  // wave-uniform: the public queue API keeps no backups (nothing re-solves its slots)
-            mu = update_p2_pass<4, true, false>(v.io, v.bc, v.bt.slotvar, alpha, st[S_MUSCAL], v.ux, v.pi, v.w.dux,
-                                                v.w.dpi, v.w.ux_bkp, v.w.pi_bkp, v.w.lam_bkp, v.w.t_bkp, v.w.res_d,
-                                                v.w.res_m);
-        else
-            mu = update_p2_pass<4, true>(v.io, v.bc, v.bt.slotvar, alpha, st[S_MUSCAL], v.ux, v.pi, v.w.dux, v.w.dpi,
-                                         v.w.ux_bkp, v.w.pi_bkp, v.w.lam_bkp, v.w.t_bkp, v.w.res_d, v.w.res_m);
-    }
-    wsync();
-    if (v.l == 0) v.stat[5 * kk + 4] = mu;
-    kk++;
-    bool again = ipm_continue<FX, 4>(a, v, kk, mu, alpha, st[S_SIGMA], phase);
+    if (v.w.state[S_ACTIVE] == 0.0) return;
+    bool again = update_body<FX, 4>(a, v);
     if (!again && a.nq) {
         if (v.l == 0) atomicAdd(&a.qctl[1], 1);
         again = ipm_refill<FX, 4, false>(a, T, who.s);  // queue mode: the slot takes the next entry
     }
     if (a.nq && again) qlist_push(a, a.qpar ^ 1, who.s);
+}
+
+// One problem per workgroup, the whole solve in ONE launch (configs[1]: a lone QP).  A pass kernel per iteration
+// lands its single workgroup on whichever XCD the dispatcher picks, so every pass of a lone problem starts from a
+// cold L2; here the same workgroup runs init and every iteration's four passes back to back on one CU, its ~1 MB
+// of stage data and factor records stay in that XCD's L2, and no launch or host poll separates the passes.
+template <class FX>
+__global__ __launch_bounds__(64) void hk_ipm_solo(KArgs a) {
+    const LdsTabs T = lds_tables(a);
+    const int p = blockIdx.x + a.p0;
+    if (p >= a.nprob) return;
+    const Who who{p, p, p};
+    {
+        IpmView v = ipm_view(a, T, who);
+        if (!ipm_start<FX, 7, true>(a, T, v)) return;
+    }
+    // every body gets a fresh view (its pointers are re-derived from the kernel arguments), so no register of one
+    // pass is live across the next: each body keeps the allocation it has in its own pass kernel
+    // (the problem index is made opaque before each view, so that nothing derived from it is hoisted out of the
+    // loop and kept live across the bodies)
+    auto view = [&]() __attribute__((always_inline)) {
+        int q = p;
+        asm volatile("" : "+v"(q));
+        q = __builtin_amdgcn_readfirstlane(q);
+        const Who w{q, q, q};
+        return ipm_view(a, T, w);
+    };
+    for (int it = 0; it < a.k_max; it++) {  // ipm_continue ends the loop; k_max bounds it regardless
+        wsync();
+        {
+            IpmView v = view();
+            fact_body<FX>(a, T, v);
+        }
+        wsync();
+        {
+            IpmView v = view();
+            pred_body<FX>(a, T, v);
+        }
+        wsync();
+        {
+            IpmView v = view();
+            corr_body<FX>(a, T, v);
+        }
+        wsync();
+        IpmView v = view();
+        if (!update_body<FX, 4>(a, v)) break;
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -882,6 +957,8 @@ static int launch_t(int which, const KArgs* a, int count, hipStream_t stream) {
         case 12: hipLaunchKernelGGL(hk_ipm_pred<FX>, grid, block, lds, stream, *a); break;
         case 13: hipLaunchKernelGGL(hk_ipm_corr<FX>, grid, block, lds, stream, *a); break;
         case 14: hipLaunchKernelGGL(hk_ipm_update<FX>, grid, block, lds, stream, *a); break;
+        // the whole IPM per problem in one launch (hk_ipm_solo)
+        case 15: hipLaunchKernelGGL(hk_ipm_solo<FX>, grid, block, lds, stream, *a); break;
         default: return -1;
     }
     return (int)hipGetLastError();

@@ -201,6 +201,15 @@ int hpmpc_mi355x_ipm_batch(const hpmpc_mi355x_plan *plan, const hpmpc_mi355x_lay
                            double *lam, double *t, double *ws, int k_max, double mu0, double mu_tol, double alpha_min,
                            int warm_start, int compute_mult, int *kk, int *ret, double *stat, void *stream);
 
+/* Latency path: hpmpc_mi355x_ipm_batch with each problem's WHOLE solve in one launch -- one workgroup per problem
+ * runs init and every iteration's passes back to back on one CU, so its stage data and factor stay in that XCD's L2
+ * and no launch or host poll separates the passes.  For a lone problem or a handful (configs[1]); for throughput
+ * over many problems use hpmpc_mi355x_ipm_queue.  Same arguments and results as hpmpc_mi355x_ipm_batch. */
+int hpmpc_mi355x_ipm_solo(const hpmpc_mi355x_plan *plan, const hpmpc_mi355x_layout *lay, int nprob, int p0, int count,
+                          const double *BAbt, const double *RSQrq, const double *d, double *ux, double *pi,
+                          double *lam, double *t, double *ws, int k_max, double mu0, double mu_tol, double alpha_min,
+                          int warm_start, int compute_mult, int *kk, int *ret, double *stat, void *stream);
+
 /* One pass of the batched IPM, for callers that interleave their own work or timing: the batched
  * solve above is pass 0 (init) followed by k_max rounds of passes 1 (factorisation), 2 (predictor
  * solve + step length + mu_aff), 3 (corrector solve + step length), 4 (update + residuals); problems

@@ -71,4 +71,5 @@ def test_configs3_rank_block(oracle, rank):
         got = dict(kk=int(kk[p]), ret=int(ret[p]), ux=[ux[p, k] for k in range(N + 1)],
                    pi=[pi[p, k] for k in range(N)], lam=[lam[p, k] for k in range(N + 1)],
                    t=[t[p, k] for k in range(N + 1)])
-        compare_ipm(one, got, r, tol=TOL_IPM, allow_divergent=p in bad and ret[p] == 2)
+        # a diverging infeasible draw (ret 2, lam -> 1e30) compares by ret and kk only (helpers.compare_ipm)
+        compare_ipm(one, got, r, tol=TOL_IPM, allow_divergent=bool(ret[p] == 2))

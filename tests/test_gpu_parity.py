@@ -319,6 +319,37 @@ def test_queue_back_to_back_on_two_streams(small_batch):
     _queue_equals_batch(s, Q2, 131)
 
 
+@pytest.mark.parametrize("shape", ["ms_N30", "tv_N100", "random"])
+def test_solo_matches_batch(shape):
+    """The latency path (hpmpc_mi355x_ipm_solo: each problem's whole solve in one launch) is bitwise the batched
+    solve: same kernels' bodies, same order of operations (fixed-shape classes and the generic kernels)."""
+    import torch
+
+    from hpmpc_amd.batch import BatchSolver
+    from hpmpc_amd.shard import make_shard
+
+    if shape == "ms_N30":
+        qp = mass_spring_qp(30, 8, 3, batch=16, time_variant=True, seed=9)
+    elif shape == "tv_N100":
+        qp = make_shard(100, 12, 4, 0, 1, 8)
+    else:
+        from hpmpc_amd.ocp import OCPQP
+
+        one = random_qp(9, [0] + [7] * 9, [3] * 9 + [0], [2] + [5] * 8 + [3], seed=5)
+        qp = OCPQP(one.N, one.nx, one.nu, one.nb, one.ng, one.idxb, [a[None].repeat(3, 0) for a in one.BAbt],
+                   [a[None].repeat(3, 0) for a in one.RSQrq], [a[None].repeat(3, 0) for a in one.d], [], 3)
+    s = BatchSolver(qp, k_max=50)
+    s.ipm()
+    torch.cuda.synchronize()
+    ref = {n: getattr(s, n).clone() for n in ("ux", "pi", "lam", "t", "kk", "ret", "stat")}
+    for n in ("ux", "pi", "lam", "t"):
+        getattr(s, n).zero_()
+    s.ipm_solo()
+    torch.cuda.synchronize()
+    for n, v in ref.items():
+        assert torch.equal(getattr(s, n), v), n
+
+
 def test_queue_unconstrained_entries_finish_at_init():
     """nb = 0 problems are solved by one sv inside the refill (kk = 0): the queue drains without
     any iteration doing work."""
