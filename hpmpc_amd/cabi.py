@@ -476,6 +476,35 @@ class HpmpcAPI:
                     pi=[pi[k][:nxv[k + 1]] for k in range(N)],
                     lam=[lam[k][:2 * P["nb"][k] + 2 * P["ng"][k]] for k in range(N + 1)], work0=work0)
 
+    def newton_ocp(self, P, ux0, pi0, lam0, t0, *, k_max=1, mu0=0.1, mu_tol=1e-12):
+        """fortran_order_d_ip_ocp_hard_tv_single_newton_step (include/c_interface.h:66)."""
+        N = P["N"]
+        nx, nu, nb, ng = iv(P["nx"]), iv(P["nu"]), iv(P["nb"]), iv(P["ng"])
+        idx = [np.ascontiguousarray(i, dtype=np.int32) for i in P["hidxb"]]
+        a = self._iface_args(P, "F")
+        x = [np.zeros(P["nx"][k] + 4) for k in range(N + 1)]
+        u = [np.zeros(P["nu"][k] + 4) for k in range(N + 1)]
+        pi = [np.zeros(P["nx"][k + 1] + 4) for k in range(N)]
+        lam = [np.zeros(2 * P["nb"][k] + 2 * P["ng"][k] + 4) for k in range(N + 1)]
+        t = [np.zeros(2 * P["nb"][k] + 2 * P["ng"][k] + 4) for k in range(N + 1)]
+        inf = np.zeros(4)
+        stat = np.zeros(5 * k_max + 5)
+        wsz = self.fn("hpmpc_d_ip_ocp_hard_tv_work_space_size_bytes")(C.c_int(N), nx, nu, nb, ipp(idx), ng, C.c_int(N))
+        work0 = np.zeros(wsz // 8 + 16)
+        kk = C.c_int(0)
+        ret = self.fn("fortran_order_d_ip_ocp_hard_tv_single_newton_step")(
+            C.byref(kk), C.c_int(k_max), C.c_double(mu0), C.c_double(mu_tol), C.c_int(N), nx, nu, nb, ipp(idx), ng,
+            C.c_int(N), C.c_int(0), dpp(a["A"]), dpp(a["B"]), dpp(a["b"]), dpp(a["Q"]), dpp(a["S"]), dpp(a["R"]),
+            dpp(a["q"]), dpp(a["r"]), dpp(a["lb"]), dpp(a["ub"]), dpp(a["C"]), dpp(a["D"]), dpp(a["lg"]),
+            dpp(a["ug"]), dpp(x), dpp(u), dpp(pi), dpp(lam), dpp(t), _dptr(inf), _dptr(work0), _dptr(stat),
+            dpp(ux0), dpp(pi0), dpp(lam0), dpp(t0))
+        nxv, nuv = P["nx"], P["nu"]
+        n = [2 * P["nb"][k] + 2 * P["ng"][k] for k in range(N + 1)]
+        return dict(status=ret, kk=kk.value, stat=stat[:5 * kk.value].copy(), inf_norm_res=inf,
+                    u=[u[k][:nuv[k]] for k in range(N)], x=[x[k][:nxv[k]] for k in range(N + 1)],
+                    pi=[pi[k][:nxv[k + 1]] for k in range(N)], lam=[lam[k][:n[k]] for k in range(N + 1)],
+                    t=[t[k][:n[k]] for k in range(N + 1)])
+
     def kkt_ocp(self, P, work0, *, order="F"):
         """fortran_order_d_solve_kkt_new_rhs_ocp_hard_tv / c_order_ twin (include/c_interface.h:63,67): new b, q,
         r and bounds of P on the factor ip_ocp left in work0 (full-space solve)."""

@@ -215,7 +215,7 @@ void pack_problem(Carve& C, int* nx, int* nb, int** hidxb, int* ng, bool rowmajo
 
 // Outputs shared by both wrappers (:590-686): u, x, the equality-box fix, residual infinity norms, pi, lam.
 void outputs(Carve& C, int* nx, int* nb, int** hidxb, int* ng, double** lb, double** ub, double** x, double** u,
-             double** pi, double** lam, double* inf_norm_res) {
+             double** pi, double** lam, double* inf_norm_res, double** t = nullptr) {
     const int N = C.N;
     const auto& nu = C.nu;
     for (int k = 0; k < N; k++)
@@ -261,6 +261,17 @@ void outputs(Carve& C, int* nx, int* nb, int** hidxb, int* ng, double** lb, doub
         for (int j = 0; j < ng[k]; j++) {
             lam[k][2 * nb[k] + j] = C.lam[k][2 * C.pnb[k] + j];
             lam[k][2 * nb[k] + j + ng[k]] = C.lam[k][2 * C.pnb[k] + j + C.png[k]];
+        }
+    }
+    if (!t) return;
+    for (int k = 0; k <= N; k++) {  // the single-Newton wrapper's t, compact like lam (:1057-1075)
+        for (int j = 0; j < nb[k]; j++) {
+            t[k][j] = C.t[k][j];
+            t[k][j + nb[k]] = C.t[k][j + C.pnb[k]];
+        }
+        for (int j = 0; j < ng[k]; j++) {
+            t[k][2 * nb[k] + j] = C.t[k][2 * C.pnb[k] + j];
+            t[k][2 * nb[k] + j + ng[k]] = C.t[k][2 * C.pnb[k] + j + C.png[k]];
         }
     }
 }
@@ -373,6 +384,56 @@ void kkt_ocp(bool rowmajor, int N, int* nx, int* nu, int* nb, int** hidxb, int* 
 }
 
 }  // namespace
+
+// include/c_interface.h:66 (interfaces/c/fortran_order_interface.c:690-1080): k_max Newton steps of the residual IPM
+// from the caller's (ux0, pi0, lam0, t0) with the fixed centering target mu0 (d_ip2_res_mpc_hard_tv_single_newton_step),
+// always on the full space (the reference computes N2 but never condenses here), then the common outputs plus t.
+extern "C" int fortran_order_d_ip_ocp_hard_tv_single_newton_step(
+    int* kk, int k_max, double mu0, double mu_tol, int N, int* nx, int* nu_N, int* nb, int** hidxb, int* ng, int N2,
+    int warm_start, double** A, double** B, double** b, double** Q, double** S, double** R, double** q, double** r,
+    double** lb, double** ub, double** Cm, double** D, double** lg, double** ug, double** x, double** u, double** pi,
+    double** lam, double** t, double* inf_norm_res, void* work0, double* stat, double** ux0, double** pi0,
+    double** lam0, double** t0) {
+    (void)N2;
+    hk_set_error(0, nullptr);
+    if (!check_sizes(N, nx, nu_N, nb)) return HPMPC_MI355X_EUNSUPPORTED;
+    char* base = aligned(work0);
+    Carve C;
+    carve(C, base, N, nx, nu_N, nb, hidxb, ng, N);
+    pack_problem(C, nx, nb, hidxb, ng, false, A, B, b, Q, S, R, q, r, lb, ub, Cm, D, lg, ug, true);
+    reinterpret_cast<double*>(base)[0] = N;
+    const double alpha_min = 1e-8;
+    const int status = d_ip2_res_mpc_hard_tv_single_newton_step(
+        kk, k_max, mu0, mu_tol, alpha_min, warm_start, stat, N, nx, C.nu.data(), nb, hidxb, ng, C.BAbt.data(),
+        C.RSQ.data(), C.DCt.data(), C.d.data(), C.ux.data(), 1, C.pi.data(), C.lam.data(), C.t.data(), C.ws, ux0, pi0,
+        lam0, t0);
+    if (status <= HPMPC_MI355X_EUNSUPPORTED) return status;
+    outputs(C, nx, nb, hidxb, ng, lb, ub, x, u, pi, lam, inf_norm_res, t);
+    return status;
+}
+
+// include/c_interface.h:60.  The reference defines it only in its BLASFEO interface
+// (interfaces/c/fortran_order_interface_libstr.c:110): the work space of hpmpc_d_ip_ocp_hard_tv_work_space_size_bytes
+// for a problem whose boxes are given by count -- nbu[k] boxed inputs and nbx[k] boxed states per stage -- instead
+// of by index.  This library's carve depends on the box positions only through how many are input / state boxes
+// (partial condensing turns inner state boxes into general constraints, d_part_cond.c:716-731), so the size is that
+// of the canonical index set [0, nbu[k]) u [nu[k], nu[k] + nbx[k]).
+extern "C" int hpmpc_d_ip_ocp_hard_tv_work_space_size_bytes_noidxb(int N, int* nx, int* nu, int* nb, int* nbx, int* nbu,
+                                                                   int* ng, int N2) {
+    std::vector<std::vector<int>> idx(N + 1);
+    std::vector<int*> hidxb(N + 1);
+    std::vector<int> nbk(N + 1);
+    for (int k = 0; k <= N; k++) {
+        const int u = k < N ? nu[k] : 0;
+        const int bu = nbu[k] < u ? nbu[k] : u, bx = nbx[k] < nx[k] ? nbx[k] : nx[k];
+        for (int j = 0; j < bu; j++) idx[k].push_back(j);
+        for (int j = 0; j < bx; j++) idx[k].push_back(u + j);
+        nbk[k] = nb[k] > bu + bx ? nb[k] : bu + bx;
+        while ((int)idx[k].size() < nbk[k]) idx[k].push_back((int)idx[k].size());  // nb beyond nbu + nbx (sizes only)
+        hidxb[k] = idx[k].data();
+    }
+    return hpmpc_d_ip_ocp_hard_tv_work_space_size_bytes(N, nx, nu, nbk.data(), hidxb.data(), ng, N2);
+}
 
 // include/c_interface.h:59 (interfaces/c/c_interface_work_space.c:70)
 extern "C" int hpmpc_d_ip_ocp_hard_tv_work_space_size_bytes(int N, int* nx, int* nu, int* nb, int** hidxb, int* ng,

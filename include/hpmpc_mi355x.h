@@ -143,6 +143,12 @@ void d_part_expand_solution(int N, int *nx, int *nu, int *nb, int **hidxb, int *
  * re-use the factor the IPM wrapper left in work0 (full-space solves only). */
 /* include/c_interface.h:59 (interfaces/c/c_interface_work_space.c:70) */
 int hpmpc_d_ip_ocp_hard_tv_work_space_size_bytes(int N, int *nx, int *nu, int *nb, int **hidxb, int *ng, int N2);
+/* include/c_interface.h:60 (defined by the reference only in interfaces/c/fortran_order_interface_libstr.c:110): the
+ * same size for boxes given by count, nbu[k] inputs and nbx[k] states */
+int hpmpc_d_ip_ocp_hard_tv_work_space_size_bytes_noidxb(int N, int *nx, int *nu, int *nb, int *nbx, int *nbu, int *ng, int N2);
+/* include/c_interface.h:66 (interfaces/c/fortran_order_interface.c:690) -- k_max Newton steps from (ux0, pi0, lam0,
+ * t0) with centering target mu0 on the full space; lam and t returned compact like the IPM wrapper's lam */
+int fortran_order_d_ip_ocp_hard_tv_single_newton_step(int *kk, int k_max, double mu0, double mu_tol, int N, int *nx, int *nu_N, int *nb, int **hidxb, int *ng, int N2, int warm_start, double **A, double **B, double **b, double **Q, double **S, double **R, double **q, double **r, double **lb, double **ub, double **C, double **D, double **lg, double **ug, double **x, double **u, double **pi, double **lam, double **t, double *inf_norm_res, void *work0, double *stat, double **ux0, double **pi0, double **lam0, double **t0);
 /* include/c_interface.h:62 (interfaces/c/c_order_interface.c:53) */
 int c_order_d_ip_ocp_hard_tv(int *kk, int k_max, double mu0, double mu_tol, int N, int *nx, int *nu, int *nb,
                              int **hidxb, int *ng, int N2, int warm_start, double **A, double **B, double **b,

@@ -169,6 +169,24 @@ def finish(api, P, qp, ux, pi, lam, t):
                 inf_norm_res=np.array([n0, n1, n2, res["mu"]]))
 
 
+def newton_ocp(api, P, ux0, pi0, lam0, t0, k_max=1, mu0=0.1, mu_tol=1e-12):
+    """fortran_order_d_ip_ocp_hard_tv_single_newton_step (interfaces/c/fortran_order_interface.c:690-1080): the same
+    packing, always the full space (its N2 is computed and never used), d_ip2_res_mpc_hard_tv_single_newton_step from
+    the caller's (ux0, pi0, lam0, t0) with the fixed centering target mu0 (no cost-based mu0), then the outputs of the
+    IPM wrapper plus t, compact like lam (:1057-1075)."""
+    N, nb, ng = P["N"], P["nb"], P["ng"]
+    qp = to_qp(P)
+    r = api.single_newton(qp.copy(), ux0, pi0, lam0, t0, k_max=k_max, mu0=mu0, mu_tol=mu_tol)
+    out = finish(api, P, qp, r["ux"], r["pi"], r["lam"], r["t"])
+    t_c = []
+    for k in range(N + 1):
+        pnb, png = rup(nb[k], 4), rup(ng[k], 4)
+        t = r["t"][k]
+        t_c.append(np.r_[t[:nb[k]], t[pnb:pnb + nb[k]], t[2 * pnb:2 * pnb + ng[k]], t[2 * pnb + png:2 * pnb + png + ng[k]]])
+    out.update(t=t_c, status=r["ret"], kk=r["kk"], stat=r["stat"])
+    return out
+
+
 def kkt_ocp(api, P, P2, k_max=50, mu0=2.0, mu_tol=1e-10):
     """fortran_order_d_ip_ocp_hard_tv on P (full space), then fortran_order_d_solve_kkt_new_rhs_ocp_hard_tv with
     the right-hand sides of P2 (b, q, r, bounds; same matrices): d_kkt_solve_new_rhs_res_mpc_hard_tv on the IPM's

@@ -308,6 +308,22 @@ def iface(ref, out):
                     ret=r["status"], stat=r["stat"])
         out.append(save_case(f"iface_{name}", "iface", qp, dict(N2=N2, mu0=mu0, mu_tol=1e-10, k_max=50), outs,
                              extra=IO.to_flat(P)))
+    # fortran_order_d_ip_ocp_hard_tv_single_newton_step: two Newton steps from an interior point near the solution
+    # (ux0, pi0 at 0.9 x the IPM's, lam0 / t0 as [lower(nb) | upper(nb)] away from 0)
+    P = IO.random_iface_problem(10, [0] + [4] * 10, [2] * 10, 2, 2, None, seed=7)
+    qp = IO.to_qp(P)
+    r = ref.ipm(qp.copy(), k_max=50, mu0=2.0, mu_tol=1e-10)
+    nrng = np.random.default_rng(8)
+    ux0 = [0.9 * x for x in r["ux"]]
+    pi0 = [0.9 * x for x in r["pi"]]
+    lam0 = [np.r_[1.0 + 0.1 * nrng.random(2 * P["nb"][k]), np.zeros(4)] for k in range(P["N"] + 1)]
+    t0 = [np.r_[0.5 + 0.1 * nrng.random(2 * P["nb"][k]), np.zeros(4)] for k in range(P["N"] + 1)]
+    n = IO.newton_ocp(ref, P, ux0, pi0, lam0, t0, k_max=2, mu0=0.1, mu_tol=1e-12)
+    extra = IO.to_flat(P)
+    extra.update(ux0=ux0, pi0=pi0, lam0=lam0, t0=t0)
+    out.append(save_case("iface_newton_N10_nx4_nu2", "iface_newton", qp, dict(mu0=0.1, mu_tol=1e-12, k_max=2),
+                         dict(u=n["u"], x=n["x"], pi=n["pi"], lam=n["lam"], t=n["t"], inf_norm_res=n["inf_norm_res"],
+                              kk=n["kk"], ret=n["status"], stat=n["stat"]), extra=extra))
     P = IO.random_iface_problem(10, [0] + [4] * 10, [2] * 10, 2, 2, None, seed=5)
     P2 = IO.new_rhs(P, seed=6)
     k = IO.kkt_ocp(ref, P, P2, mu_tol=1e-10)

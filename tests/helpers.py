@@ -73,7 +73,7 @@ def run_case(api, case):
         return
     if case.kind == "pcond_sv":
         return pcond_sv(api, qp, int(a["N2"]))
-    if case.kind in ("iface", "iface_kkt"):
+    if case.kind in ("iface", "iface_kkt", "iface_newton"):
         return run_iface(api, case)
     if case.kind == "soft":
         from hpmpc_amd.soft import SoftQP
@@ -107,6 +107,16 @@ def run_iface(api, case, order="F"):
         out = {k: r[k] for k in ("u", "x", "pi", "lam", "inf_norm_res", "kk", "stat")}
         out["ret"] = r["status"]
         return out
+    if case.kind == "iface_newton":
+        kw = dict(k_max=int(a["k_max"]), mu0=a["mu0"], mu_tol=a["mu_tol"])
+        st = [case.inp[k] for k in ("ux0", "pi0", "lam0", "t0")]
+        if hasattr(api.lib, api.p + "fortran_order_d_ip_ocp_hard_tv_single_newton_step"):
+            r = api.newton_ocp(P, *st, **kw)
+        else:
+            r = IO.newton_ocp(api, P, *st, **kw)
+        out = {k: r[k] for k in ("u", "x", "pi", "lam", "t", "inf_norm_res", "kk", "stat")}
+        out["ret"] = r["status"]
+        return out
     P2 = IO.from_flat(qp.N, qp.nx, qp.nu, qp.nb, qp.ng, {k[1:]: v for k, v in case.inp.items() if k.startswith("NP_")})
     if has:
         r = api.ip_ocp(P, qp.N, order=order, **kw)
@@ -121,7 +131,9 @@ def check_iface(case, got):
     if "kk" in out:
         assert int(got["kk"]) == int(out["kk"]) and int(got["ret"]) == int(out["ret"]), (case.name, got["kk"], out["kk"])
         np.testing.assert_allclose(got["stat"], out["stat"], rtol=TOL_STAT, atol=1e-14, err_msg=case.name)
-    for key in ("u", "x", "pi", "lam"):
+    for key in ("u", "x", "pi", "lam", "t"):
+        if key not in out:
+            continue
         for k, (g, r) in enumerate(zip(got[key], out[key])):
             g, r = np.asarray(g), np.asarray(r)
             if r.size:
@@ -252,7 +264,7 @@ def check_case(case, got):
         return check_soft(case, got)
     if case.kind == "pcond":
         return check_pcond(case, got)
-    if case.kind in ("iface", "iface_kkt"):
+    if case.kind in ("iface", "iface_kkt", "iface_newton"):
         return check_iface(case, got)
     if case.kind == "ipm_div":
         # a diverging infeasible problem: only ret and kk to +-2 are comparable (the reference and a second c99

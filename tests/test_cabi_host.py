@@ -190,3 +190,30 @@ def test_batch_solver_refuses_without_gpu():
         pytest.skip("GPU present")
     with pytest.raises(RuntimeError):
         batch.BatchSolver(mass_spring_qp(5, 4, 1, batch=2))
+
+
+def test_noidxb_size_matches_idxb_size(hiplib):
+    """hpmpc_d_ip_ocp_hard_tv_work_space_size_bytes_noidxb (c_interface.h:60): boxes given by count (nbu inputs, nbx
+    states) need the work space of any index set with those counts, full space and partially condensed (host only)."""
+    N = 12
+    nx = np.array([0] + [6] * N, dtype=np.int32)
+    nu = np.array([2] * N + [0], dtype=np.int32)
+    nbu = np.array([2] * N + [0], dtype=np.int32)
+    nbx = np.array([0] + [3] * N, dtype=np.int32)
+    nb = (nbu + nbx).astype(np.int32)
+    ng = np.zeros(N + 1, dtype=np.int32)
+    rng = np.random.default_rng(0)
+    idx = []
+    for k in range(N + 1):
+        u = rng.permutation(int(nu[k]))[: nbu[k]] if nu[k] else np.zeros(0, int)
+        x = int(nu[k]) + rng.permutation(int(nx[k]))[: nbx[k]] if nx[k] else np.zeros(0, int)
+        idx.append(np.ascontiguousarray(np.r_[u, x], dtype=np.int32))
+    P = C.POINTER(C.c_int)
+    idxp = (P * (N + 1))(*[a.ctypes.data_as(P) for a in idx])
+    f = hiplib.hpmpc_d_ip_ocp_hard_tv_work_space_size_bytes
+    g = hiplib.hpmpc_d_ip_ocp_hard_tv_work_space_size_bytes_noidxb
+    ip = lambda a: a.ctypes.data_as(P)
+    for N2 in (N, 4, 3):
+        a = f(N, ip(nx), ip(nu), ip(nb), idxp, ip(ng), N2)
+        b = g(N, ip(nx), ip(nu), ip(nb), ip(nbx), ip(nbu), ip(ng), N2)
+        assert a == b > 0, (N2, a, b)
