@@ -14,6 +14,8 @@
 // so that the state block always starts on an MFMA K-chunk boundary.  Tile indices in [nu, xo) and
 // beyond xo+nx are zero padding (their pivots clamp to 0 and contribute nothing).
 #pragma once
+#include <type_traits>
+
 #include "hk_prims.h"
 
 namespace hk {
@@ -344,6 +346,51 @@ __device__ __forceinline__ void store_factor(double* Fk, const d4& S, double lc,
     for (int r = 0; r < 4; r++) gst(Fk, r * 64 + l, S[r], ok);
     gst(Fk, 256 + 16 * g + c, g == 0 ? lc : invd, ok && g < 2);  // l (row group 0) and inv_diag (row group 1)
     gst(Fk, 288 + l, kg, ok);
+}
+
+// Packed record of a compiled-class stage (nu <= 4, so the u block is tile block 0 and the state block starts at
+// tile index xo = 4).  What the solves read of it, and nothing else:
+//   [0, 64)    S0: tile register 0 = the u columns of L in upper storage (trs: the n-form u solve)
+//   [64, 80)   l = [l_u; p_k] (the sv forward's right-hand side; pi's p_{k+1})
+//   [80, 96)   the u pivots' inverse diagonal (trs)
+//   [96, 160)  the gain block KG (4 x 16, the forward's u = KG [rhs_u; x])
+//   [160, ..)  P_k, the state block, packed lower by rows (NX (NX+1) / 2 doubles; symmetric, so the tile's upper
+//              half is not stored): 1 392 B against the 2 816 B of the full record at nx = 12 (S1..S3 are 1 536 B
+//              of which 1 152 B hold P in both triangles)
+constexpr int FXR_L = 64, FXR_INVD = 80, FXR_KG = 96, FXR_P = 160;
+
+// element (i, j) of the packed-lower P block (either triangle)
+__device__ __forceinline__ int fxr_pidx(int i, int j) {
+    const int a = i > j ? i : j, b = i > j ? j : i;
+    return FXR_P + (a * (a + 1) >> 1) + b;
+}
+
+// Store of a packed record (same six stores as store_factor: the vector-memory count per stage stays fixed).
+template <int NX>
+__device__ __forceinline__ void store_factor_fixed(double* Fk, const d4& S, double lc, double invd, double kg,
+                                                   bool ok) {
+    const int l = lane_id(), g = l >> 4, c = l & 15;
+    gst(Fk, l, S[0], ok);
+    gst(Fk, FXR_L + 16 * g + c, g == 0 ? lc : invd, ok && g < 2);
+    gst(Fk, FXR_KG + l, kg, ok);
+    const int j = c - 4;
+#pragma unroll
+    for (int r = 1; r < 4; r++) {  // lane (g, c) of tile register r holds P[g + 4r - 4][c - 4] (c >= 4)
+        const int i = g + 4 * r - 4;
+        gst(Fk, fxr_pidx(i, j), S[r], ok && j >= 0 && j <= i && i < NX);
+    }
+}
+
+// Tile registers 1..3 (the state rows) of a packed record: P in the tile layout (lanes c < 4 read 0).
+template <int NX>
+__device__ __forceinline__ void load_p_fixed(const double* Fk, d4& S, bool ok) {
+    const int l = lane_id(), g = l >> 4, c = l & 15;
+    const int j = c - 4;
+#pragma unroll
+    for (int r = 1; r < 4; r++) {
+        const int i = g + 4 * r - 4;
+        S[r] = gld(Fk, fxr_pidx(i, j), ok && j >= 0 && i < NX && j < NX);
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -927,6 +974,7 @@ __device__ void ric_backward(const RicIO& io, Scratch* sm, int update_b, const d
     });
     // One stage: prefetch stage kn into `nxt` while stage k runs on `cur`.  The loop is unrolled by two
     // with the fragments swapping roles, so no stage pays a register copy of the prefetched fragment.
+    bool rec_fixed = false;  // the record in registers (stage k+1's) belongs to the compiled class: packed format
     auto stage = [&](int k, const BwdFrag& cur, BwdFrag& nxt) __attribute__((always_inline)) {
         HK_STAMP(0, k);
         const int kn = k > 0 ? k - 1 : 0;  // unconditional prefetch (stage 0 re-read on the last pass)
@@ -936,11 +984,20 @@ __device__ void ric_backward(const RicIO& io, Scratch* sm, int update_b, const d
         HK_STAMP(6, k);
         // factor of stage k+1 (still in registers): stored one stage late, behind the prefetch, so
         // that no s_waitcnt of this stage has to wait for the store acknowledgements
-        store_factor(io.F + (long)(k + 1) * FSTRIDE, S, AUG ? ml_prev : 0.0, invd_prev, kg_prev, k < io.N);
+        double* Fk1 = io.F + (long)(k + 1) * FSTRIDE;
+        if constexpr (FX::enabled) {
+            if (rec_fixed)
+                store_factor_fixed<FX::nx>(Fk1, S, AUG ? ml_prev : 0.0, invd_prev, kg_prev, k < io.N);
+            else
+                store_factor(Fk1, S, AUG ? ml_prev : 0.0, invd_prev, kg_prev, k < io.N);
+        } else {
+            store_factor(Fk1, S, AUG ? ml_prev : 0.0, invd_prev, kg_prev, k < io.N);
+        }
         asm volatile("" ::: "memory");  // keep those stores here, ahead of this stage's math
         HK_STAMP(1, k);
         with_shape<FX>(si, [&](const auto& sh) {
             bwd_step<AUG, BM>(io, sm, sh, k, cur, bc, compute_Pb, Pb, S, ml_prev, invd_prev, kg_prev);
+            rec_fixed = std::remove_reference_t<decltype(sh)>::fixed;
         });
         if constexpr (BM == BX_P2R)
             with_shape<FX>(sn, [&](const auto& sh) { bwd_residual(io, sm, sh, kn, bc, nxt, cur.uc, k > 0); });
@@ -1058,11 +1115,23 @@ __device__ __forceinline__ void fwd_fetch(const RicIO& io, const SH& sh, int k, 
     const bool needS = !SH::fixed || compute_pi;
     // S[0] (tile rows 0..3) holds the u block's columns of L: a fixed-shape stage (nu <= 4, xo = 4) solves
     // its u block in gain form, and pi_from_x reads rows >= xo only, so S[0] is never needed there
+    if constexpr (SH::fixed) {  // packed record (store_factor_fixed): P only, and only for pi
+        f.S[0] = 0.0;
+        if (PRED) {
+            f.S[1] = f.S[2] = f.S[3] = 0.0;
+        } else {
+            load_p_fixed<SH::nx>(Fk, f.S, needS);
+        }
+        f.lc = MODE == 0 ? gld(Fk, FXR_L + c) : 0.0;
+        f.invd = 0.0;
+        f.kg = gld(Fk, FXR_KG + l);
+    } else {
 #pragma unroll
-    for (int r = 0; r < 4; r++) f.S[r] = ((SH::fixed && (r == 0 || PRED))) ? 0.0 : gld(Fk, r * 64 + l, needS);
-    f.lc = MODE == 0 ? gld(Fk, 256 + c) : 0.0;
-    f.invd = SH::fixed ? 0.0 : gld(Fk, 272 + c);
-    f.kg = gld(Fk, 288 + l);
+        for (int r = 0; r < 4; r++) f.S[r] = gld(Fk, r * 64 + l, needS);
+        f.lc = MODE == 0 ? gld(Fk, 256 + c) : 0.0;
+        f.invd = gld(Fk, 272 + c);
+        f.kg = gld(Fk, 288 + l);
+    }
     const int kk = k < io.N ? k : io.N - 1;  // stage N has no BAbt block: loads clamped, values masked
     const bool live = k < io.N;
     const double* Bk = io.BAbt + sh.oB;
@@ -1302,10 +1371,19 @@ __device__ __forceinline__ void trs_fetch(const RicIO& io, const SH& sh, int k, 
     const double* Fk = io.F + (long)k * FSTRIDE;
     // the n-form solve of a fixed-shape stage runs over its u pivots (< 4), i.e. reads S[0] only; rows
     // 4..15 are needed by the generic solve and by P_{k} b_{k-1} (compute_Pb, the KKT re-solve)
+    if constexpr (SH::fixed) {  // packed record: S0 (the u columns), the u pivots, P only for a P b recompute
+        f.S[0] = gld(Fk, l);
+        if (RPB) {
+            load_p_fixed<SH::nx>(Fk, f.S, compute_Pb);
+        } else {
+            f.S[1] = f.S[2] = f.S[3] = 0.0;
+        }
+        f.invd = gld(Fk, FXR_INVD + c);
+    } else {
 #pragma unroll
-    for (int r = 0; r < 4; r++)
-        f.S[r] = (SH::fixed && !RPB && r > 0) ? 0.0 : gld(Fk, r * 64 + l, r == 0 || !SH::fixed || compute_Pb);
-    f.invd = gld(Fk, 272 + c);
+        for (int r = 0; r < 4; r++) f.S[r] = gld(Fk, r * 64 + l);
+        f.invd = gld(Fk, 272 + c);
+    }
     const int nux = sh.nu + sh.nx;
     const int vc = tile_var(c, sh.nu, sh.nx, sh.xo);
     const double* R = io.RSQ + sh.oR;

@@ -719,20 +719,17 @@ __global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_update(KArgs a) {
     if (a.nq && again) qlist_push(a, a.qpar ^ 1, who.s);
 }
 
-// One problem per workgroup, the whole solve in ONE launch (configs[1]: a lone QP).  A pass kernel per iteration
-// lands its single workgroup on whichever XCD the dispatcher picks, so every pass of a lone problem starts from a
-// cold L2; here the same workgroup runs init and every iteration's four passes back to back on one CU, its ~1 MB
-// of stage data and factor records stay in that XCD's L2, and no launch or host poll separates the passes.
+// One problem per workgroup, every iteration in ONE launch after hk_ipm_init (configs[1]: a lone QP): the same
+// workgroup runs each iteration's four passes back to back on one CU, so no launch or host poll separates them and
+// the problem's ~1 MB of stage data and factor records stay in that XCD's L2.
 template <class FX>
 __global__ __launch_bounds__(64) void hk_ipm_solo(KArgs a) {
     const LdsTabs T = lds_tables(a);
     const int p = blockIdx.x + a.p0;
     if (p >= a.nprob) return;
-    const Who who{p, p, p};
-    {
-        IpmView v = ipm_view(a, T, who);
-        if (!ipm_start<FX, 7, true>(a, T, v)) return;
-    }
+    // init is its own launch (hk_ipm_init, right before this one): inlined here it pushed the kernel into scratch
+    // spills (852 B per lane) on top of the four iteration bodies
+    if (carve(a.ws + (long)p * a.sW, a.N).state[S_ACTIVE] == 0.0) return;
     // every body gets a fresh view (its pointers are re-derived from the kernel arguments), so no register of one
     // pass is live across the next: each body keeps the allocation it has in its own pass kernel
     // (the problem index is made opaque before each view, so that nothing derived from it is hoisted out of the
@@ -958,7 +955,10 @@ static int launch_t(int which, const KArgs* a, int count, hipStream_t stream) {
         case 13: hipLaunchKernelGGL(hk_ipm_corr<FX>, grid, block, lds, stream, *a); break;
         case 14: hipLaunchKernelGGL(hk_ipm_update<FX>, grid, block, lds, stream, *a); break;
         // the whole IPM per problem in one launch (hk_ipm_solo)
-        case 15: hipLaunchKernelGGL(hk_ipm_solo<FX>, grid, block, lds, stream, *a); break;
+        case 15:
+            hipLaunchKernelGGL(hk_ipm_init<FX>, grid, block, lds, stream, *a);
+            hipLaunchKernelGGL(hk_ipm_solo<FX>, grid, block, lds, stream, *a);
+            break;
         default: return -1;
     }
     return (int)hipGetLastError();

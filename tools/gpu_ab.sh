@@ -17,7 +17,7 @@ import json, sys
 l = [x for x in open(f"gpurun_out/ab/{sys.argv[1]}.log") if x.startswith("{")][-1]
 d = json.loads(l)
 p = d["roofline"]["pass_ms_per_step"]
-print(sys.argv[1], round(d["value"]), {k[7:]: round(v, 3) for k, v in p.items()})
+print(sys.argv[1], round(d["value"]), {k[7:]: round(v, 3) for k, v in p.items()}, "ric", round(d["riccati"]["value"]))
 PY
   done
 done

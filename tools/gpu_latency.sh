@@ -1,3 +1,4 @@
+# lone-QP latency probe (tools/latency_probe.py), after the GPU parity suite
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -5,5 +6,4 @@ timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeou
 tail -3 gpurun_out/tests.log
 [ $rc -ne 0 ] && { grep -E "Error|assert|FAILED" gpurun_out/tests.log | head -30; exit $rc; }
 timeout -k 10 300 python3 tools/latency_probe.py > gpurun_out/latency.log 2>&1 || { tail -20 gpurun_out/latency.log; exit 1; }
-cat gpurun_out/latency.log | grep -v amdgpu.ids
-timeout -k 10 120 python3 tools/stamps.py 1 > gpurun_out/stamps1.log 2>&1 && timeout -k 10 120 python3 tools/stamps.py 1024 > gpurun_out/stamps1024.log 2>&1; cat gpurun_out/stamps1.log gpurun_out/stamps1024.log | grep -v amdgpu.ids
+grep -v amdgpu.ids gpurun_out/latency.log
