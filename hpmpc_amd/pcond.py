@@ -193,6 +193,30 @@ class PcondSolver:
                                                   p(self.kk2), p(self.ret2), p(self.stat2), self._stream()),
                     "condensed IPM")
 
+    def cond_sizes(self):
+        """Stage sizes of the condensed problem (lists of N2+1): nx, nu, nb, ng."""
+        N, N2, qp = self.N, self.N2, self.qp
+        nx = [int(v) for v in qp.nx]
+        nu = [int(v) for v in qp.nu]
+        nb = [int(v) for v in qp.nb]
+        ng = [int(v) for v in qp.ng]
+        blocks = _blocks(N, N2)
+        c = dict(nx=[], nu=[], nb=[], ng=[])
+        s = 0
+        for T in blocks:  # d_part_cond_compute_problem_size (d_part_cond.c:694-741)
+            c["nx"].append(nx[s])
+            c["nu"].append(sum(nu[s + j] for j in range(T)))
+            inner_u = sum(sum(1 for v in qp.idxb[s + j] if v < nu[s + j]) for j in range(1, T))
+            inner_x = sum(sum(1 for v in qp.idxb[s + j] if v >= nu[s + j]) for j in range(1, T))
+            c["nb"].append(nb[s] + inner_u)
+            c["ng"].append(sum(ng[s + j] for j in range(T)) + inner_x)
+            s += T
+        c["nx"].append(nx[N])
+        c["nu"].append(0)
+        c["nb"].append(nb[N])
+        c["ng"].append(ng[N])
+        return c
+
     def solve_ipm(self, **kw):
         """condense -> IPM on the condensed problems -> expand (solution and multipliers), asynchronous."""
         self.condense()
@@ -251,6 +275,27 @@ def pcond_algorithmic_bytes(qp: OCPQP, N2: int):
     sv = 8.0 * (b2B + b2R + fac + u2 + p2)
     expand = 8.0 * (bB + bR + u2 + p2 + sum(nux) + sum(nx[1:]))
     return cond, sv, expand
+
+
+def wide_ipm_algorithmic_bytes(nx, nu, nb, ng):
+    """Bytes of ONE IP iteration of the wide-stage IPM (hk_wide_ipm) on a problem with stage sizes nx, nu, nb, ng
+    (lists of N+1; the condensed problem at configs[4]), SURVEY.md §8d's rule -- each datum once per pass -- applied to
+    the passes of an iteration: the factorisation (BAbt, lower RSQrq + row and DCt in; packed L + row + 1/diag out),
+    the predictor and corrector solves (L, BAbt and DCt in; ux, pi out), the residuals (lower RSQrq, BAbt, DCt, ux,
+    pi in; r_q, r_b out) and 24 doubles per constraint pair (the element-wise IPM vectors, as the narrow IPM's
+    accounting)."""
+    N = len(nx) - 1
+    nux = [int(nu[k]) + int(nx[k]) for k in range(N + 1)]
+    B = sum((nux[k] + 1) * int(nx[k + 1]) for k in range(N))
+    R = sum(_tri(n) + n for n in nux)
+    L = sum(_tri(n) + 2 * n for n in nux)
+    D = sum(nux[k] * int(ng[k]) for k in range(N + 1))
+    u, p = sum(nux), sum(int(nx[k + 1]) for k in range(N))
+    fact = B + R + D + L
+    solve = L + B + D + u + p
+    res = R + B + D + 2 * (u + p)
+    vec = 24 * sum(int(nb[k]) + int(ng[k]) for k in range(N + 1))
+    return 8.0 * (fact + 2 * solve + res + vec)
 
 
 def _blocks(N, N2):
