@@ -357,6 +357,60 @@ class HpmpcAPI:
         cqp = OCPQP(N2, nx2, nu2, nb2, ng2, idx2, BAbt2, RSQ2, d2, DCt2 if ng2.any() else [], None)
         return cqp, memory
 
+    # the building blocks of one condensing block (d_part_cond.c:214-689): qp's N stages are the block
+    @staticmethod
+    def gamma_shapes(qp: OCPQP):
+        """(rows, cols, lib4 size) of Gamma_j, j < N: rows sum_{i<=j} nu_i + nx_0 + 1, cols nx_{j+1}."""
+        out, r = [], int(qp.nx[0]) + 1
+        for j in range(qp.N):
+            r += int(qp.nu[j])
+            c = int(qp.nx[j + 1])
+            out.append((r, c, rup(r, 4) * rup(c, 2)))
+        return out
+
+    def _cond_work(self, qp: OCPQP):
+        nzM = max(int(qp.nu[k] + qp.nx[k]) + 1 for k in range(qp.N + 1))
+        g = sum(2 * s for (_, _, s) in self.gamma_shapes(qp))
+        return np.zeros(g + 8 * (rup(nzM, 4) + 4) ** 2 + 4096)
+
+    def cond_BAbt(self, qp: OCPQP, fill: float = 0.0):
+        """d_cond_BAbt (d_part_cond.c:214): Gamma_0..Gamma_{N-1} (lib4) and BAbt2; outputs pre-filled with fill."""
+        N = qp.N
+        G = [np.full(s + 8, fill) for (_, _, s) in self.gamma_shapes(qp)]
+        r, c, s = self.gamma_shapes(qp)[-1]
+        B2 = np.full(s + 8, fill)
+        self.fn("d_cond_BAbt")(C.c_int(N), iv(qp.nx), iv(qp.nu), self._pp(qp.BAbt), self._p(self._cond_work(qp)),
+                               self._pp(G), self._p(B2))
+        self._sync()
+        return G, B2
+
+    def cond_RSQrq(self, qp: OCPQP, G, fill: float = 0.0):
+        """d_cond_RSQrq (d_part_cond.c:312): the condensed Hessian from the Gammas G; output pre-filled with fill."""
+        N = qp.N
+        nv = int(np.sum(qp.nu[:N])) + int(qp.nx[0])
+        R2 = np.full(rup(nv + 1, 4) * rup(nv, 2) + 8, fill)
+        G = [np.ascontiguousarray(g, dtype=np.float64) for g in G] + [np.zeros(8)]
+        self.fn("d_cond_RSQrq")(C.c_int(N), iv(qp.nx), iv(qp.nu), self._pp(qp.BAbt), self._pp(qp.RSQrq),
+                                self._pp(G), self._p(self._cond_work(qp)), self._p(R2))
+        self._sync()
+        return R2
+
+    def cond_DCtd(self, qp: OCPQP, G, fill: float = 0.0):
+        """d_cond_DCtd (d_part_cond.c:579): DCt2, d2, idxb2 of the block; outputs pre-filled with fill (idxb2: -7)."""
+        N = qp.N
+        nv = int(np.sum(qp.nu[:N])) + int(qp.nx[0])
+        nbb = int(qp.nb[0]) + sum(int(np.sum(qp.idxb[k] < qp.nu[k])) for k in range(1, N))
+        nbg = sum(int(np.sum(qp.idxb[k] >= qp.nu[k])) for k in range(1, N))
+        DCt2 = np.full(rup(nv, 4) * rup(nbg, 2) + 8, fill)
+        d2 = np.full(2 * rup(nbb, 4) + 2 * rup(nbg, 4) + 8, fill)
+        idxb2 = np.full(nbb + 4, -7, dtype=np.int32)
+        idxb = [np.ascontiguousarray(i, dtype=np.int32) for i in qp.idxb]
+        G = [np.ascontiguousarray(g, dtype=np.float64) for g in G] + [np.zeros(8)]
+        self.fn("d_cond_DCtd")(C.c_int(N), iv(qp.nx), iv(qp.nu), iv(qp.nb), ipp(idxb), self._pp(qp.d), self._pp(G),
+                               self._p(DCt2), self._p(d2), idxb2.ctypes.data_as(IP))
+        self._sync()
+        return DCt2, d2, idxb2[:nbb], (nbb, nbg)
+
     def part_expand(self, qp: OCPQP, cqp: OCPQP, ux2, pi2, lam2, t2):
         """d_part_expand_solution (d_part_cond.c:1103): the full-space solution of qp from the condensed one."""
         N, N2 = qp.N, cqp.N

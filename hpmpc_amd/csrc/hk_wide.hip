@@ -66,6 +66,8 @@ __global__ __launch_bounds__(WT) void hk_pcond(PcArgs a) {
     // ---- d_cond_BAbt: Gamma_{j-1} stays in LDS (GA); Gamma_j = [B_j; Gamma_{j-1} A_j] comes from MFMA tiles
     // held in registers, then overwrites GA and streams to HBM ----
     double* GA = sm + a.offGA;
+    const int ph = a.ph;
+    if (ph & PC_BABT) {
     {
         const WideStage s = st[0];
         const int r0 = s.nu + s.nx + 1;
@@ -106,10 +108,13 @@ __global__ __launch_bounds__(WT) void hk_pcond(PcArgs a) {
             *P4w(B2, sd, i, c) = GA[i + c * rT];
         }
     }
+    }  // PC_BABT
+    bar();  // Gamma scratch complete (written by this block's threads) before the later phases read it
 
     // ---- d_cond_RSQrq ----
     const int cnux2 = (nv + 1) / 2 * 2;
-    {
+    if (ph & PC_RSQ) {
+    if (!(ph & PC_PART)) {
         const int n = ((nv + 1 + 3) / 4 * 4) * cnux2;
         for (int e = tid; e < n; e += WT) R2[e] = 0.0;
     }
@@ -219,53 +224,100 @@ __global__ __launch_bounds__(WT) void hk_pcond(PcArgs a) {
             bar();
         }
     }
+    }  // PC_RSQ
 
-    // ---- d_cond_DCtd: input boxes stay boxes, state boxes of stages 1..T-1 become general constraints ----
-    {
+    // ---- d_cond_DCtd: input boxes stay boxes, state boxes of stages 1..T-1 become general constraints.  The
+    // reference walks the stages backwards assigning box / general slots in order (:637-678); here each wave
+    // takes whole stages and ranks its entries with ballots, after a per-stage count and a prefix over stages
+    // (the LDS tiles are free by now and hold the integer bookkeeping), then the general constraints' Gamma
+    // rows are copied one column per wave ----
+    if (ph & PC_DCTD) {
         const int nbb = blk.nb2, nbg = blk.ng2, pnbb = (nbb + 3) / 4 * 4, pnbg = (nbg + 3) / 4 * 4;
         const int cnbg = (nbg + 1) / 2 * 2, pnv = (nv + 3) / 4 * 4;
-        for (int e = tid; e < pnv * cnbg; e += WT) G2[e] = 0.0;
-        for (int e = tid; e < 2 * pnbb + 2 * pnbg; e += WT) d2[e] = 0.0;
+        const int wv = tid >> 6, ln = tid & 63;
+        const unsigned long long below = (1ull << ln) - 1ull;
+        int* I = reinterpret_cast<int*>(sm);
+        int *cU = I, *cX = I + T, *iob = I + 2 * T, *iog = I + 3 * T, *ntmp = I + 4 * T, *igb = I + 5 * T;
+        int* gd = I + 6 * T;  // general constraint ig: (stage << 16) | state index g
+        bar();                // the RSQ phase's last LDS reads are done
+        if (!(ph & PC_PART)) {
+            for (int e = tid; e < pnv * cnbg; e += WT) G2[e] = 0.0;
+            for (int e = tid; e < 2 * pnbb + 2 * pnbg; e += WT) d2[e] = 0.0;
+        }
+        for (int sI = wv; sI < T; sI += WT / 64) {  // input / state box counts of each stage
+            const WideStage s = st[sI];
+            int nU = 0, nX = 0;
+            for (int j0 = 0; j0 < s.nb; j0 += 64) {
+                const int jj = j0 + ln;
+                const int vv = jj < s.nb ? idxb[s.oI + jj] : -1;
+                const unsigned long long mu = __ballot(jj < s.nb && vv < s.nu), mx = __ballot(jj < s.nb && vv >= s.nu);
+                nU += __popcll(mu);
+                nX += __popcll(mx);
+            }
+            if (ln == 0) {
+                cU[sI] = nU;
+                cX[sI] = nX;
+            }
+        }
         bar();
-        if (tid == 0) {
-            int* i2 = p == 0 ? a.idxb2 + blk.oI2 : nullptr;
-            int ib = 0, ig = 0, nu_tmp = 0, idx_gammab = nx0;
-            for (int j = 0; j < T - 1; j++) idx_gammab += st[j].nu;
+        if (tid == 0) {  // slots in the reference's order: stages T-1 .. 1, then all of stage 0's boxes
+            int ib = 0, ig = 0, nt = 0;
             for (int sI = T - 1; sI >= 1; sI--) {
-                const WideStage s = st[sI];
-                nu_tmp += s.nu;
-                const int r0 = rows(sI - 1);
-                const double* Gp = G + goff(sI - 1);
-                for (int jj = 0; jj < s.nb; jj++) {
-                    const int vv = idxb[s.oI + jj];
-                    if (vv < s.nu) {
-                        d2[ib] = dv[s.oD + jj];
-                        d2[pnbb + ib] = dv[s.oD + s.pnb + jj];
-                        if (i2) i2[ib] = nu_tmp - s.nu + vv;
-                        ib++;
-                    } else {
-                        const int g = vv - s.nu;
-                        const double c0 = Gp[idx_gammab + g * r0];
-                        d2[2 * pnbb + ig] = dv[s.oD + jj] - c0;
-                        d2[2 * pnbb + pnbg + ig] = dv[s.oD + s.pnb + jj] - c0;
-                        for (int i = 0; i < idx_gammab; i++) *P4w(G2, cnbg, nu_tmp + i, ig) = Gp[i + g * r0];
-                        ig++;
-                    }
+                nt += st[sI].nu;
+                iob[sI] = ib;
+                iog[sI] = ig;
+                ntmp[sI] = nt;
+                ib += cU[sI];
+                ig += cX[sI];
+            }
+            iob[0] = ib;
+            iog[0] = ig;
+            ntmp[0] = nt + st[0].nu;
+            int acc = nx0;  // idx_gammab of stage s: nx0 + sum_{j<s} nu_j (= rows(s-1) - 1)
+            for (int sI = 0; sI < T; sI++) {
+                igb[sI] = acc;
+                acc += st[sI].nu;
+            }
+        }
+        bar();
+        int* i2 = p == 0 ? a.idxb2 + blk.oI2 : nullptr;
+        for (int sI = wv; sI < T; sI += WT / 64) {
+            const WideStage s = st[sI];
+            const int r0 = sI > 0 ? igb[sI] + 1 : 0, gb = igb[sI];
+            const double* Gp = sI > 0 ? G + goff(sI - 1) : nullptr;
+            int rU = iob[sI], rX = iog[sI];
+            for (int j0 = 0; j0 < s.nb; j0 += 64) {
+                const int jj = j0 + ln;
+                const bool in = jj < s.nb;
+                const int vv = in ? idxb[s.oI + jj] : -1;
+                const bool isb = in && (sI == 0 || vv < s.nu), isg = in && !isb;
+                const unsigned long long mb = __ballot(isb), mg = __ballot(isg);
+                if (isb) {
+                    const int ib = rU + __popcll(mb & below);
+                    d2[ib] = dv[s.oD + jj];
+                    d2[pnbb + ib] = dv[s.oD + s.pnb + jj];
+                    if (i2) i2[ib] = ntmp[sI] - s.nu + vv;
                 }
-                idx_gammab -= st[sI - 1].nu;
+                if (isg) {
+                    const int ig = rX + __popcll(mg & below), g = vv - s.nu;
+                    const double c0 = Gp[gb + g * r0];
+                    d2[2 * pnbb + ig] = dv[s.oD + jj] - c0;
+                    d2[2 * pnbb + pnbg + ig] = dv[s.oD + s.pnb + jj] - c0;
+                    gd[ig] = (sI << 16) | g;
+                }
+                rU += __popcll(mb);
+                rX += __popcll(mg);
             }
-            const WideStage s = st[0];
-            nu_tmp += s.nu;
-            for (int jj = 0; jj < s.nb; jj++) {
-                d2[ib] = dv[s.oD + jj];
-                d2[pnbb + ib] = dv[s.oD + s.pnb + jj];
-                if (i2) i2[ib] = nu_tmp - s.nu + idxb[s.oI + jj];
-                ib++;
-            }
+        }
+        bar();
+        for (int ig = wv; ig < nbg; ig += WT / 64) {  // DCt2 column ig: rows nu_tmp + i <- Gamma_{s-1}(i, g)
+            const int sI = gd[ig] >> 16, g = gd[ig] & 0xffff, rowsI = igb[sI], r0 = rowsI + 1, nt = ntmp[sI];
+            const double* Gp = G + goff(sI - 1);
+            for (int i = ln; i < rowsI; i += 64) *P4w(G2, cnbg, nt + i, ig) = Gp[i + g * r0];
         }
     }
     // the terminal condensed stage is the original's (d_part_cond.c:1052-1056): block N2-1 copies it
-    if (ii == a.N2 - 1) {
+    if (ii == a.N2 - 1 && !(ph & PC_PART)) {
         const WideStage sN = a.st[a.N];
         const int n = (a.nzN + 3) / 4 * 4 * a.sdRN;
         double* RN = a.RSQ2 + (long)p * a.sR2 + a.oR2N;

@@ -78,7 +78,12 @@ struct PcArgs {
     int offGA, offGB;                                // Gamma_{j-1} / Gamma_j tiles (and stage scratch)
     int skip;  // profiling only (HK_PCOND_SKIP): bit 0 Gamma, 1 RSQ phase, 2 its Cholesky, 3 M product, 4 W/syrk
     int oD2N, nDN;  // terminal stage: its bounds d_N (original offset st[N].oD, nDN doubles) -> d2 at oD2N
+    // phases (d_part_cond: PC_ALL).  Without PC_BABT the Gammas are inputs, already in the scratch G; PC_PART runs
+    // one building block alone (d_cond_BAbt / _RSQrq / _DCtd): outputs are not cleared first (the caller's
+    // contents stay where the reference writes nothing) and the terminal stage is not copied
+    int ph;
 };
+enum { PC_BABT = 1, PC_RSQ = 2, PC_DCTD = 4, PC_ALL = 7, PC_PART = 8 };
 
 // Expansion (d_part_expand_solution): one workgroup per (block, problem).
 struct PxArgs {

@@ -419,6 +419,11 @@ bool pc_plan(PcPlan& P, int N, const int* nx, const int* nu_in, const int* nb, c
     P.xoW = P.xoV + nzM;
     P.xoQ = P.xoW + nzM;
     P.px_lds = P.xoQ + std::max(nzM, nxM);
+    for (int ii = 0; ii < N2; ii++)  // hk_pcond's d_cond_DCtd bookkeeping: 6 ints per stage + 1 per general row
+        if (6 * P.blk[ii].T + P.ng2[ii] > 2 * P.pc_lds) {
+            hk_set_error(HPMPC_MI355X_EUNSUPPORTED, "condensing block with more state boxes than the LDS tiles hold");
+            return false;
+        }
     if (P.pc_lds > LDS_MAX_DOUBLES || P.px_lds > LDS_MAX_DOUBLES) {
         hk_set_error(HPMPC_MI355X_EUNSUPPORTED, "condensing stage tiles beyond the 64 KiB LDS budget");
         return false;
@@ -453,6 +458,7 @@ void fill_pc_args(const PcPlan& P, PcArgs& a) {
     a.ldB = P.ldB;
     a.offGA = P.offGA;
     a.offGB = P.offGB;
+    a.ph = PC_ALL;
 }
 
 void fill_px_args(const PcPlan& P, PxArgs& a) {
@@ -618,6 +624,152 @@ extern "C" void d_part_cond(int N, int* nx, int* nu, int* nb, int** hidxb, int* 
     hpDCt2[N2] = hpDCt[N];
     hd2[N2] = hd[N];
     hidxb2[N2] = hidxb[N];
+}
+
+// ------------------------------------------------------------------------------------------------
+// The building blocks of one condensing block (d_cond_BAbt / d_cond_RSQrq / d_cond_DCtd, d_part_cond.c:214-688):
+// the block is a horizon-N problem condensed with N2 = 1 by hk_pcond restricted to one phase (PC_PART).  Gammas
+// move between the caller's lib4 matrices and the kernel's dense column-major scratch on the host; the outputs
+// the reference writes only in part are uploaded first, so what it leaves alone comes back unchanged.
+// ------------------------------------------------------------------------------------------------
+namespace {
+inline long long l4(int sd, int i, int j) { return (long long)(i / BS) * BS * sd + i % BS + BS * j; }
+
+void cond_part(int ph, int N, const int* nx, const int* nu, const int* nb, int* const* hidxb, double* const* hpBAbt,
+               double* const* hpRSQrq, double* const* hd, double** hpGamma, double* pBAbt2, double* pRSQrq2,
+               double* pDCt2, double* d2, int* idxb2) {
+    hk_set_error(0, nullptr);
+    if (N < 1) return;  // the reference returns early (d_part_cond.c:315, :583)
+    std::vector<int> nxv(nx, nx + N + 1), nuv(nu, nu + N), nbv(N + 1, 0), ngv(N + 1, 0);
+    nuv.push_back(0);
+    std::vector<const int*> idx(N + 1, nullptr);
+    if (ph == PC_DCTD)
+        for (int k = 0; k < N; k++) {
+            nbv[k] = nb[k];
+            idx[k] = hidxb[k];
+        }
+    PcPlan P;
+    if (!pc_plan(P, N, nxv.data(), nuv.data(), nbv.data(), idx.data(), ngv.data(), 1)) return;
+    const WLayout& O = P.orig;
+    const PcBlock& b0 = P.blk[0];
+    const int nv = b0.nut + b0.nx0, nbb = b0.nb2, nbg = b0.ng2;
+    const int pnbb = rup(nbb, BS), pnbg = rup(nbg, BS), cnbg = rup(nbg, NCL), cnux2 = rup(nv, NCL);
+    // Gamma_j: rows r_j, dense at go[j] in the scratch
+    std::vector<int> rj(N);
+    std::vector<long long> go(N + 1, 0);
+    for (int j = 0, acc = b0.nx0 + 1; j < N; j++) {
+        acc += nuv[j];
+        rj[j] = acc;
+        go[j + 1] = go[j] + (long long)acc * nxv[j + 1];
+    }
+    // extents the reference touches in the partly-written outputs (last element + 1)
+    long long nR2 = l4(cnux2, nv, nv - 1) + 1, nG2 = 0, nD2 = nbg > 0 ? 2 * pnbb + pnbg + nbg : (nbb > 0 ? pnbb + nbb : 0);
+    if (ph == PC_DCTD) {  // d_part_cond.c:637-668: the column of general constraint ig spans rows nu_tmp .. +idx_gammab
+        int ig = 0, nu_tmp = 0, idx_gammab = b0.nx0;
+        for (int j = 0; j < N - 1; j++) idx_gammab += nuv[j];
+        for (int s = N - 1; s >= 1; s--) {
+            nu_tmp += nuv[s];
+            for (int jj = 0; jj < nb[s]; jj++)
+                if (hidxb[s][jj] >= nuv[s]) {
+                    if (idx_gammab > 0) nG2 = std::max(nG2, l4(cnbg, nu_tmp + idx_gammab - 1, ig) + 1);
+                    ig++;
+                }
+            idx_gammab -= nuv[s - 1];
+        }
+    }
+    const long long nB2 = (long long)rup(nv + 1, BS) * rup(nxv[N], NCL);
+    Carve c;
+    const size_t oSt = c.take(sizeof(WideStage) * (N + 1)), oBlk = c.take(sizeof(PcBlock)), oIdx = c.take(4 * O.nI + 4),
+                 oB = c.take(8 * O.nB), oR = c.take(8 * O.nR), oD = c.take(8 * O.nD + 8), oG = c.take(8 * P.nG),
+                 oB2 = c.take(8 * nB2), oR2 = c.take(8 * nR2), oG2 = c.take(8 * nG2 + 8), oD2 = c.take(8 * nD2 + 8),
+                 oI2 = c.take(4 * nbb + 4);
+    if (!g_w.ensure(c.o)) return;
+    char* H = g_w.host;
+    memset(H, 0, c.o);
+    memcpy(H + oSt, O.st.data(), sizeof(WideStage) * (N + 1));
+    PcBlock blk = b0;
+    blk.oB2 = blk.oR2 = blk.oG2 = blk.oD2 = blk.oI2 = 0;
+    memcpy(H + oBlk, &blk, sizeof blk);
+    memcpy(H + oIdx, P.idxb.data(), 4 * O.nI);
+    double* HB = reinterpret_cast<double*>(H + oB);
+    double* HR = reinterpret_cast<double*>(H + oR);
+    double* HD = reinterpret_cast<double*>(H + oD);
+    double* HG = reinterpret_cast<double*>(H + oG);
+    for (int k = 0; k < N; k++) {
+        const WideStage& s = O.st[k];
+        const int nz = s.nu + s.nx + 1;
+        if (ph != PC_DCTD) memcpy(HB + s.oB, hpBAbt[k], (size_t)rup(nz, BS) * s.sdB * sizeof(double));
+        if (ph == PC_RSQ) memcpy(HR + s.oR, hpRSQrq[k], (size_t)rup(nz, BS) * s.sdR * sizeof(double));
+        if (ph == PC_DCTD && nb[k] > 0) memcpy(HD + s.oD, hd[k], (size_t)2 * s.pnb * sizeof(double));
+    }
+    if (ph != PC_BABT)  // the given Gammas (RSQrq reads Gamma_0..N-2, DCtd those of stages with state boxes)
+        for (int j = 0; j + 1 < N; j++) {
+            const int sd = rup(nxv[j + 1], NCL);
+            for (int cc = 0; cc < nxv[j + 1]; cc++)
+                for (int i = 0; i < rj[j]; i++) HG[go[j] + i + (long long)cc * rj[j]] = hpGamma[j][l4(sd, i, cc)];
+        }
+    if (ph == PC_RSQ) memcpy(H + oR2, pRSQrq2, 8 * nR2);
+    if (ph == PC_DCTD) {
+        if (nG2) memcpy(H + oG2, pDCt2, 8 * nG2);
+        if (nD2) memcpy(H + oD2, d2, 8 * nD2);
+    }
+    char* D = g_w.dev;
+    PcArgs a;
+    fill_pc_args(P, a);
+    a.ph = ph | PC_PART;
+    a.nprob = 1;
+    a.st = reinterpret_cast<const WideStage*>(D + oSt);
+    a.blk = reinterpret_cast<const PcBlock*>(D + oBlk);
+    a.idxb = reinterpret_cast<const int*>(D + oIdx);
+    a.BAbt = reinterpret_cast<const double*>(D + oB);
+    a.RSQ = reinterpret_cast<const double*>(D + oR);
+    a.d = reinterpret_cast<const double*>(D + oD);
+    a.G = reinterpret_cast<double*>(D + oG);
+    a.BAbt2 = reinterpret_cast<double*>(D + oB2);
+    a.RSQ2 = reinterpret_cast<double*>(D + oR2);
+    a.DCt2 = reinterpret_cast<double*>(D + oG2);
+    a.d2 = reinterpret_cast<double*>(D + oD2);
+    a.idxb2 = reinterpret_cast<int*>(D + oI2);
+    if (!g_w.up(c.o) || !launch(1, &a, 1, P.pc_lds, g_w.stream, "hk_pcond") || !g_w.down(c.o)) return;
+    if (ph == PC_BABT) {  // d_part_cond.c:262-303: Gamma_j (r_j x nx_{j+1}) and BAbt2 = Gamma_{N-1}
+        const double* B2 = reinterpret_cast<const double*>(H + oB2);
+        for (int j = 0; j < N; j++) {
+            const int sd = rup(nxv[j + 1], NCL);
+            for (int cc = 0; cc < nxv[j + 1]; cc++)
+                for (int i = 0; i < rj[j]; i++) hpGamma[j][l4(sd, i, cc)] = HG[go[j] + i + (long long)cc * rj[j]];
+        }
+        const int sd = rup(nxv[N], NCL);
+        for (int cc = 0; cc < nxv[N]; cc++)
+            for (int i = 0; i < rj[N - 1]; i++) pBAbt2[l4(sd, i, cc)] = B2[l4(sd, i, cc)];
+    } else if (ph == PC_RSQ) {
+        memcpy(pRSQrq2, H + oR2, 8 * nR2);
+    } else {
+        if (nG2) memcpy(pDCt2, H + oG2, 8 * nG2);
+        if (nD2) memcpy(d2, H + oD2, 8 * nD2);
+        if (nbb) memcpy(idxb2, H + oI2, 4 * nbb);
+    }
+}
+}  // namespace
+
+// d_part_cond.c:214-308
+extern "C" void d_cond_BAbt(int N, int* nx, int* nu, double** hpBAbt, double* work, double** hpGamma, double* pBAbt2) {
+    (void)work;
+    cond_part(PC_BABT, N, nx, nu, nullptr, nullptr, hpBAbt, nullptr, nullptr, hpGamma, pBAbt2, nullptr, nullptr,
+              nullptr, nullptr);
+}
+
+// d_part_cond.c:312-574
+extern "C" void d_cond_RSQrq(int N, int* nx, int* nu, double** hpBAbt, double** hpRSQrq, double** hpGamma,
+                             double* work, double* pRSQrq2) {
+    (void)work;
+    cond_part(PC_RSQ, N, nx, nu, nullptr, nullptr, hpBAbt, hpRSQrq, nullptr, hpGamma, nullptr, pRSQrq2, nullptr,
+              nullptr, nullptr);
+}
+
+// d_part_cond.c:579-689
+extern "C" void d_cond_DCtd(int N, int* nx, int* nu, int* nb, int** hidxb, double** hd, double** hpGamma,
+                            double* pDCt2, double* d2, int* idxb2) {
+    cond_part(PC_DCTD, N, nx, nu, nb, hidxb, nullptr, nullptr, hd, hpGamma, nullptr, nullptr, pDCt2, d2, idxb2);
 }
 
 extern "C" int d_part_expand_work_space_size_bytes(int N, int* nx, int* nu, int* nb, int* ng) { return 64; }

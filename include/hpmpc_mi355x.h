@@ -114,6 +114,23 @@ void d_res_mpc_hard_tv(int N, int *nx, int *nu, int *nb, int **idxb, int *ng, do
  * arrays hpBAbt2 .. hidxb2 are set into it, and the terminal stage aliases the caller's (d_part_cond.c:1052-1056).
  * Stages with nu+nx > 16 (e.g. the condensed nu2+nx2 = 84 of configs[4]) are solved by
  * d_back_ric_rec_sv_tv_res on the wide-stage path. */
+/* The three building blocks of one condensing block (horizon N, condensed variable [u_{N-1}; ..; u_0; x_0]), each
+ * one hk_pcond launch.  Gamma_j = hpGamma[j] is lib4 with (sum_{i<=j} nu_i + nx_0 + 1) rows, nx_{j+1} columns,
+ * panel stride round_up(nx_{j+1}, 2); work is not used (every temporary is on the device).  Only the elements the
+ * reference writes are written, except the strict upper triangle of pRSQrq2 (of each u_s x u_s diagonal block
+ * and of the first stage's square), which the reference copies from its work matrix: it is left as the caller
+ * had it (every consumer reads the lower triangle).  Limits as for d_part_cond (nx <= 63, Gamma rows x nx <= 3072): else no output and
+ * hpmpc_mi355x_last_error() = HPMPC_MI355X_EUNSUPPORTED. */
+/* include/lqcp_solvers.h:80 (lqcp_solvers/d_part_cond.c:214) -- Gamma_0..Gamma_{N-1} and pBAbt2 = Gamma_{N-1} */
+void d_cond_BAbt(int N, int *nx, int *nu, double **hpBAbt, double *work, double **hpGamma, double *pBAbt2);
+/* include/lqcp_solvers.h:82 (d_part_cond.c:312) -- the condensed Hessian from the given Gamma_0..Gamma_{N-2} */
+void d_cond_RSQrq(int N, int *nx, int *nu, double **hpBAbt, double **hpRSQrq, double **hpGamma, double *work,
+                  double *pRSQrq2);
+/* include/lqcp_solvers.h:84 (d_part_cond.c:579) -- boxes of stage 0 and input boxes stay boxes (d2 lower/upper
+ * at 0 / round_up(nbb,4), idxb2), state boxes of stages 1..N-1 become rows of pDCt2 with bounds at
+ * 2 round_up(nbb,4) / + round_up(nbg,4) */
+void d_cond_DCtd(int N, int *nx, int *nu, int *nb, int **hidxb, double **hd, double **hpGamma, double *pDCt2,
+                 double *d2, int *idxb2);
 /* include/lqcp_solvers.h:86 (lqcp_solvers/d_part_cond.c:694) */
 void d_part_cond_compute_problem_size(int N, int *nx, int *nu, int *nb, int **hidxb, int *ng, int N2, int *nx2,
                                       int *nu2, int *nb2, int *ng2);

@@ -71,6 +71,11 @@ void orc_d_res_mpc_hard_tv(int N, int *nx, int *nu, int *nb, int **idxb, int *ng
                            double **hlam, double **ht, double **hrq, double **hrb, double **hrd, double *mu);
 
 /* partial condensing (lqcp_solvers/d_part_cond.c) */
+void orc_d_cond_BAbt(int N, int *nx, int *nu, double **hpBAbt, double *work, double **hpGamma, double *pBAbt2);
+void orc_d_cond_RSQrq(int N, int *nx, int *nu, double **hpBAbt, double **hpRSQrq, double **hpGamma, double *work,
+                      double *pRSQrq2);
+void orc_d_cond_DCtd(int N, int *nx, int *nu, int *nb, int **hidxb, double **hd, double **hpGamma, double *pDCt2,
+                     double *d2, int *idxb2);
 void orc_d_part_cond_compute_problem_size(int N, int *nx, int *nu, int *nb, int **hidxb, int *ng, int N2, int *nx2,
                                           int *nu2, int *nb2, int *ng2);
 int orc_d_part_cond_work_space_size_bytes(int N, int *nx, int *nu, int *nb, int **hidxb, int *ng, int N2, int *nx2,

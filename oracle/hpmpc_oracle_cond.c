@@ -10,7 +10,8 @@
  *   problem size         d_part_cond.c:694-738
  *   work / memory sizes  :743-924 (memory carve and sizes reproduced: callers read the condensed
  *                        data through the pointer arrays d_part_cond fills, :1013-1041)
- *   condensing           :926-1062 -> d_cond_BAbt :214-303, d_cond_RSQrq :307-574, d_cond_DCtd :579-688
+ *   condensing           :926-1062 -> d_cond_BAbt :214-308, d_cond_RSQrq :312-574, d_cond_DCtd :579-689
+ *                        (each also exported alone, orc_d_cond_*, with the reference prototypes)
  *   expansion            :1103-1308
  */
 #include <math.h>
@@ -64,7 +65,7 @@ void orc_d_part_cond_compute_problem_size(int N, int *nx, int *nu, int *nb, int 
     ng2[N2] = ng[N];
 }
 
-/* oracle-private: the dense Gamma matrices of the largest block plus the stage temporaries */
+/* oracle-private: the lib4 and dense Gamma matrices of the largest block plus the stage temporaries */
 int orc_d_part_cond_work_space_size_bytes(int N, int *nx, int *nu, int *nb, int **hidxb, int *ng, int N2, int *nx2,
                                           int *nu2, int *nb2, int *ng2) {
     long best = 0;
@@ -75,7 +76,8 @@ int orc_d_part_cond_work_space_size_bytes(int N, int *nx, int *nu, int *nb, int 
         for (int jj = 0; jj < T1; jj++) {
             int st = N_tmp + jj;
             nut += nu[st];
-            s += (nut + nx[N_tmp] + 1) * (long)nx[st + 1];
+            s += (nut + nx[N_tmp] + 1) * (long)nx[st + 1] +
+                 (long)rup(nut + nx[N_tmp] + 1, BS) * rup(nx[st + 1], NCL);
             if (nu[st] + nx[st] + 1 > nzM) nzM = nu[st] + nx[st] + 1;
         }
         s += 4 * nzM * nzM + 4 * (nut + nx[N_tmp] + 1) * (nut + nx[N_tmp] + 1);
@@ -104,121 +106,151 @@ static void unpack(double *pA, int sd, int m, int n, double *A, int lda) {
         for (int i = 0; i < m; i++) A[i + j * lda] = *P4(pA, sd, i, j);
 }
 
-/* Condense one block of T stages (d_cond_BAbt / d_cond_RSQrq / d_cond_DCtd).  Inputs are the block's
- * stage arrays; outputs are lib4 (BAbt2 sd cnx2', RSQ2 sd cnux2, DCt2 sd cng2) and the padded d2/idxb2. */
-static void cond_block(int T, int *nx, int *nu, int *nb, int **hidxb, double **hpBAbt, double **hpRSQrq, double **hd,
-                       double *pBAbt2, double *pRSQ2, double *pDCt2, double *d2, int *idxb2, double *work) {
-    const int nx0 = nx[0];
-    int nut = 0;
-    for (int j = 0; j < T; j++) nut += nu[j];
-    const int nv = nut + nx0; /* condensed stage variables [u_{T-1} .. u_0, x_0] */
-    /* rows of Gamma_j: [u_j .. u_0, x_0, 1] */
-    int rj[T], off[T + 1];
-    double *G[T];
-    double *p = work;
-    int acc = 0;
-    for (int j = 0; j < T; j++) {
-        acc += nu[j];
-        rj[j] = acc + nx0 + 1;
-        G[j] = p;
-        p += (long)rj[j] * nx[j + 1];
-    }
-    /* off[s]: column of u_s in the condensed variables = sum_{r > s} nu_r (nu3 in d_cond_RSQrq) */
-    off[T] = 0;
-    for (int s = T - 1; s >= 0; s--) off[s] = (s == T - 1 ? 0 : off[s + 1] + nu[s + 1]);
+static void pack(const double *A, int lda, int m, int n, double *pA, int sd) {
+    for (int j = 0; j < n; j++)
+        for (int i = 0; i < m; i++) *P4(pA, sd, i, j) = A[i + j * lda];
+}
 
-    /* ---- d_cond_BAbt (:214-303): Gamma_0 = BAbt_0, Gamma_j = [B_j ; Gamma_{j-1} A_j] + b_j e_last ---- */
+/* rows of Gamma_j: [u_j .. u_0, x_0, 1] -> r_j = sum_{i<=j} nu_i + nx_0 + 1 */
+static int gamma_rows(int j, int *nx, int *nu) {
+    int r = nx[0] + 1;
+    for (int i = 0; i <= j; i++) r += nu[i];
+    return r;
+}
+
+/* the dense copies of hpGamma[0..n) laid end to end in work; returns the first double past them */
+static double *gamma_dense(int n, int *nx, int *nu, double **hpGamma, double *work, double **G) {
+    double *p = work;
+    for (int j = 0; j < n; j++) {
+        const int r = gamma_rows(j, nx, nu);
+        G[j] = p;
+        unpack(hpGamma[j], rup(nx[j + 1], NCL), r, nx[j + 1], G[j], r);
+        p += (long)r * nx[j + 1];
+    }
+    return p;
+}
+
+/* d_part_cond.c:214-308: Gamma_0 = BAbt_0, Gamma_j = [B_j ; Gamma_{j-1} A_j] + b_j e_last (lib4, rows r_j, panel
+ * stride cnx_{j+1}); pBAbt2 = Gamma_{N-1}.  Dense column-major temporaries in work. */
+void orc_d_cond_BAbt(int N, int *nx, int *nu, double **hpBAbt, double *work, double **hpGamma, double *pBAbt2) {
+    if (N < 1) return;
+    double *G[N];
+    double *p = work;
+    for (int j = 0; j < N; j++) {
+        G[j] = p;
+        p += (long)gamma_rows(j, nx, nu) * nx[j + 1];
+    }
     {
         const int nux = nu[0] + nx[0], cnx1 = rup(nx[1], NCL);
-        unpack(hpBAbt[0], cnx1, nux + 1, nx[1], G[0], rj[0]);
+        unpack(hpBAbt[0], cnx1, nux + 1, nx[1], G[0], gamma_rows(0, nx, nu));
     }
-    for (int j = 1; j < T; j++) {
-        const int nuj = nu[j], nxj = nx[j], nx1 = nx[j + 1], cnx1 = rup(nx1, NCL), r0 = rj[j - 1];
+    for (int j = 1; j < N; j++) {
+        const int nuj = nu[j], nxj = nx[j], nx1 = nx[j + 1], cnx1 = rup(nx1, NCL), r0 = gamma_rows(j - 1, nx, nu),
+                  rj = r0 + nuj;
         double *Gj = G[j], *Gp = G[j - 1];
         for (int c = 0; c < nx1; c++) {
-            for (int i = 0; i < nuj; i++) Gj[i + c * rj[j]] = *P4(hpBAbt[j], cnx1, i, c);
+            for (int i = 0; i < nuj; i++) Gj[i + c * rj] = *P4(hpBAbt[j], cnx1, i, c);
             for (int i = 0; i < r0; i++) {
                 double a = 0.0;
                 for (int l = 0; l < nxj; l++) a += Gp[i + l * r0] * *P4(hpBAbt[j], cnx1, nuj + l, c);
-                Gj[nuj + i + c * rj[j]] = a;
+                Gj[nuj + i + c * rj] = a;
             }
-            Gj[rj[j] - 1 + c * rj[j]] += *P4(hpBAbt[j], cnx1, nuj + nxj, c);
+            Gj[rj - 1 + c * rj] += *P4(hpBAbt[j], cnx1, nuj + nxj, c);
         }
     }
-    {
-        const int cnxT = rup(nx[T], NCL);
-        for (int c = 0; c < nx[T]; c++)
-            for (int i = 0; i < nv + 1; i++) *P4(pBAbt2, cnxT, i, c) = G[T - 1][i + c * rj[T - 1]];
+    for (int j = 0; j < N; j++) {
+        const int r = gamma_rows(j, nx, nu);
+        pack(G[j], r, r, nx[j + 1], hpGamma[j], rup(nx[j + 1], NCL));
     }
+    pack(G[N - 1], gamma_rows(N - 1, nx, nu), gamma_rows(N - 1, nx, nu), nx[N], pBAbt2, rup(nx[N], NCL));
+}
 
-    /* ---- d_cond_RSQrq (:307-574) ---- */
-    const int cnux2 = rup(nv, NCL);
-    for (int i = 0; i < rup(nv + 1, BS) * cnux2; i++) pRSQ2[i] = 0.0;
+/* d_part_cond.c:312-574: the condensed Hessian [D M'; M P] with its gradient row, from the given Gammas.  Writes
+ * the lower triangle of every column block the reference writes (the reference also copies the strict upper
+ * triangle of the u_s x u_s blocks from its work matrix; not part of the result). */
+void orc_d_cond_RSQrq(int N, int *nx, int *nu, double **hpBAbt, double **hpRSQrq, double **hpGamma, double *work,
+                      double *pRSQ2) {
+    if (N < 1) return;
+    const int T = N, nx0 = nx[0];
+    int nut = 0;
+    for (int j = 0; j < T; j++) nut += nu[j];
+    const int nv = nut + nx0, cnux2 = rup(nv, NCL);
     if (T == 1) {
         const int nux = nu[0] + nx[0], cnux = rup(nux, NCL);
         for (int c = 0; c < nux; c++)
             for (int i = c; i <= nux; i++) *P4(pRSQ2, cnux2, i, c) = *P4(hpRSQrq[0], cnux, i, c);
-    } else {
-        /* pL: dense (nux_s+1) x nux_s accumulated Hessian of stage s (lower triangle + last row) */
-        int nzM = 0;
-        for (int j = 0; j < T; j++)
-            if (nu[j] + nx[j] + 1 > nzM) nzM = nu[j] + nx[j] + 1;
-        double *pL = p, *Lx = pL + nzM * nzM, *W = Lx + nzM * nzM, *tmp = W + nzM * nzM, *dLx = tmp + nzM * nzM;
-        int s = T - 1;
-        {
-            const int nux = nu[s] + nx[s], cnux = rup(nux, NCL);
-            for (int c = 0; c < nux; c++)
-                for (int i = c; i <= nux; i++) pL[i + c * (nux + 1)] = *P4(hpRSQrq[s], cnux, i, c);
-        }
-        for (;;) {
-            const int nus = nu[s], nxs = nx[s], nux = nus + nxs, ld = nux + 1;
-            if (s == 0) {
-                /* D, M, m, P, p of the first stage: the whole pL at (off_0, off_0) */
-                for (int c = 0; c < nux; c++)
-                    for (int i = c; i <= nux; i++) *P4(pRSQ2, cnux2, off[0] + i, off[0] + c) = pL[i + c * ld];
-                break;
-            }
-            /* D: the u_s x u_s block */
-            for (int c = 0; c < nus; c++)
-                for (int i = c; i < nus; i++) *P4(pRSQ2, cnux2, off[s] + i, off[s] + c) = pL[i + c * ld];
-            /* M: Gamma_{s-1} (rows [u_{s-1}..u_0, x_0, 1]) times the x_s x u_s block; its last row is the
-             * gradient row, to which m (the r row of pL) is added */
-            const int r0 = rj[s - 1];
-            for (int c = 0; c < nus; c++) {
-                for (int i = 0; i < r0; i++) {
-                    double a = 0.0;
-                    for (int l = 0; l < nxs; l++) a += G[s - 1][i + l * r0] * pL[nus + l + c * ld];
-                    *P4(pRSQ2, cnux2, off[s] + nus + i, off[s] + c) = a;
-                }
-                *P4(pRSQ2, cnux2, nv, off[s] + c) += pL[nux + c * ld];
-            }
-            /* state cost-to-go of x_s: Lx = chol_aug(pL[x, x] with its gradient row) */
-            const int ldx = nxs + 1;
-            for (int c = 0; c < nxs; c++)
-                for (int i = c; i <= nxs; i++) tmp[i + c * ldx] = pL[nus + i + (nus + c) * ld];
-            orc__chol_aug(nxs + 1, nxs, tmp, ldx, Lx, ldx, dLx);
-            /* W = BAbt_{s-1} Lx (dtrmm_nt_u), last row += l (dgead), pL = RSQ_{s-1} + W W' (dsyrk_nt) */
-            const int sp = s - 1, nuxp = nu[sp] + nx[sp], ldp = nuxp + 1, cnx1 = rup(nxs, NCL),
-                      cnuxp = rup(nuxp, NCL);
-            for (int c = 0; c < nxs; c++)
-                for (int i = 0; i <= nuxp; i++) {
-                    double a = 0.0;
-                    for (int l = c; l < nxs; l++) a += *P4(hpBAbt[sp], cnx1, i, l) * Lx[l + c * ldx];
-                    W[i + c * ldp] = a;
-                }
-            for (int c = 0; c < nxs; c++) W[nuxp + c * ldp] += Lx[nxs + c * ldx];
-            for (int c = 0; c < nuxp; c++)
-                for (int i = c; i <= nuxp; i++) {
-                    double a = 0.0;
-                    for (int l = 0; l < nxs; l++) a += W[i + l * ldp] * W[c + l * ldp];
-                    pL[i + c * ldp] = *P4(hpRSQrq[sp], cnuxp, i, c) + a;
-                }
-            s = sp;
-        }
+        return;
     }
+    double *G[T];
+    double *p = gamma_dense(T - 1, nx, nu, hpGamma, work, G);
+    /* off[s]: column of u_s in the condensed variables = sum_{r > s} nu_r (nu3 in d_cond_RSQrq) */
+    int off[T + 1];
+    off[T] = 0;
+    for (int s = T - 1; s >= 0; s--) off[s] = (s == T - 1 ? 0 : off[s + 1] + nu[s + 1]);
+    /* pL: dense (nux_s+1) x nux_s accumulated Hessian of stage s (lower triangle + last row) */
+    int nzM = 0;
+    for (int j = 0; j < T; j++)
+        if (nu[j] + nx[j] + 1 > nzM) nzM = nu[j] + nx[j] + 1;
+    double *pL = p, *Lx = pL + nzM * nzM, *W = Lx + nzM * nzM, *tmp = W + nzM * nzM, *dLx = tmp + nzM * nzM;
+    int s = T - 1;
+    {
+        const int nux = nu[s] + nx[s], cnux = rup(nux, NCL);
+        for (int c = 0; c < nux; c++)
+            for (int i = c; i <= nux; i++) pL[i + c * (nux + 1)] = *P4(hpRSQrq[s], cnux, i, c);
+    }
+    for (;;) {
+        const int nus = nu[s], nxs = nx[s], nux = nus + nxs, ld = nux + 1;
+        if (s == 0) {
+            /* D, M, m, P, p of the first stage: the whole pL at (off_0, off_0) */
+            for (int c = 0; c < nux; c++)
+                for (int i = c; i <= nux; i++) *P4(pRSQ2, cnux2, off[0] + i, off[0] + c) = pL[i + c * ld];
+            break;
+        }
+        /* D: the u_s x u_s block */
+        for (int c = 0; c < nus; c++)
+            for (int i = c; i < nus; i++) *P4(pRSQ2, cnux2, off[s] + i, off[s] + c) = pL[i + c * ld];
+        /* M: Gamma_{s-1} (rows [u_{s-1}..u_0, x_0, 1]) times the x_s x u_s block; its last row is the
+         * gradient row, to which m (the r row of pL) is added */
+        const int r0 = gamma_rows(s - 1, nx, nu);
+        for (int c = 0; c < nus; c++) {
+            for (int i = 0; i < r0; i++) {
+                double a = 0.0;
+                for (int l = 0; l < nxs; l++) a += G[s - 1][i + l * r0] * pL[nus + l + c * ld];
+                if (i == r0 - 1) a += pL[nux + c * ld];
+                *P4(pRSQ2, cnux2, off[s] + nus + i, off[s] + c) = a;
+            }
+        }
+        /* state cost-to-go of x_s: Lx = chol_aug(pL[x, x] with its gradient row) */
+        const int ldx = nxs + 1;
+        for (int c = 0; c < nxs; c++)
+            for (int i = c; i <= nxs; i++) tmp[i + c * ldx] = pL[nus + i + (nus + c) * ld];
+        orc__chol_aug(nxs + 1, nxs, tmp, ldx, Lx, ldx, dLx);
+        /* W = BAbt_{s-1} Lx (dtrmm_nt_u), last row += l (dgead), pL = RSQ_{s-1} + W W' (dsyrk_nt) */
+        const int sp = s - 1, nuxp = nu[sp] + nx[sp], ldp = nuxp + 1, cnx1 = rup(nxs, NCL), cnuxp = rup(nuxp, NCL);
+        for (int c = 0; c < nxs; c++)
+            for (int i = 0; i <= nuxp; i++) {
+                double a = 0.0;
+                for (int l = c; l < nxs; l++) a += *P4(hpBAbt[sp], cnx1, i, l) * Lx[l + c * ldx];
+                W[i + c * ldp] = a;
+            }
+        for (int c = 0; c < nxs; c++) W[nuxp + c * ldp] += Lx[nxs + c * ldx];
+        for (int c = 0; c < nuxp; c++)
+            for (int i = c; i <= nuxp; i++) {
+                double a = 0.0;
+                for (int l = 0; l < nxs; l++) a += W[i + l * ldp] * W[c + l * ldp];
+                pL[i + c * ldp] = *P4(hpRSQrq[sp], cnuxp, i, c) + a;
+            }
+        s = sp;
+    }
+}
 
-    /* ---- d_cond_DCtd (:579-688): input boxes stay boxes, state boxes of stages 1..T-1 become general
-     * constraints on [u_{s-1} .. u_0, x_0] through Gamma_{s-1}; stage 0's boxes all stay boxes ---- */
+/* d_part_cond.c:579-689: input boxes stay boxes, state boxes of stages 1..N-1 become general constraints on
+ * [u_{s-1} .. u_0, x_0] through Gamma_{s-1}; stage 0's boxes all stay boxes.  Only the slots the reference
+ * assigns are written. */
+void orc_d_cond_DCtd(int N, int *nx, int *nu, int *nb, int **hidxb, double **hd, double **hpGamma, double *pDCt2,
+                     double *d2, int *idxb2) {
+    if (N < 1) return;
+    const int T = N;
     int nbb = nb[0], nbg = 0;
     for (int s = 1; s < T; s++)
         for (int jj = 0; jj < nb[s]; jj++) {
@@ -228,13 +260,11 @@ static void cond_block(int T, int *nx, int *nu, int *nb, int **hidxb, double **h
                 nbg++;
         }
     const int pnbb = rup(nbb, BS), pnbg = rup(nbg, BS), cnbg = rup(nbg, NCL);
-    for (int i = 0; i < rup(nv, BS) * cnbg; i++) pDCt2[i] = 0.0;
-    for (int i = 0; i < 2 * pnbb + 2 * pnbg; i++) d2[i] = 0.0;
-    int ib = 0, ig = 0, nu_tmp = 0, idx_gammab = nx0;
+    int ib = 0, ig = 0, nu_tmp = 0, idx_gammab = nx[0];
     for (int j = 0; j < T - 1; j++) idx_gammab += nu[j];
     for (int s = T - 1; s >= 1; s--) {
         nu_tmp += nu[s];
-        const int pnbs = rup(nb[s], BS);
+        const int pnbs = rup(nb[s], BS), sdg = rup(nx[s], NCL);
         for (int jj = 0; jj < nb[s]; jj++) {
             const int v = hidxb[s][jj];
             if (v < nu[s]) {
@@ -243,26 +273,54 @@ static void cond_block(int T, int *nx, int *nu, int *nb, int **hidxb, double **h
                 idxb2[ib] = nu_tmp - nu[s] + v;
                 ib++;
             } else {
-                const int g = v - nu[s], r0 = rj[s - 1];
-                const double c0 = G[s - 1][idx_gammab + g * r0];
+                const int g = v - nu[s];
+                const double c0 = *P4(hpGamma[s - 1], sdg, idx_gammab, g);
                 d2[2 * pnbb + ig] = hd[s][jj] - c0;
                 d2[2 * pnbb + pnbg + ig] = hd[s][pnbs + jj] - c0;
-                for (int i = 0; i < idx_gammab; i++) *P4(pDCt2, cnbg, nu_tmp + i, ig) = G[s - 1][i + g * r0];
+                for (int i = 0; i < idx_gammab; i++) *P4(pDCt2, cnbg, nu_tmp + i, ig) = *P4(hpGamma[s - 1], sdg, i, g);
                 ig++;
             }
         }
         idx_gammab -= nu[s - 1];
     }
     nu_tmp += nu[0];
-    {
-        const int pnb0 = rup(nb[0], BS);
-        for (int jj = 0; jj < nb[0]; jj++) {
-            d2[ib] = hd[0][jj];
-            d2[pnbb + ib] = hd[0][pnb0 + jj];
-            idxb2[ib] = nu_tmp - nu[0] + hidxb[0][jj];
-            ib++;
-        }
+    const int pnb0 = rup(nb[0], BS);
+    for (int jj = 0; jj < nb[0]; jj++) {
+        d2[ib] = hd[0][jj];
+        d2[pnbb + ib] = hd[0][pnb0 + jj];
+        idxb2[ib] = nu_tmp - nu[0] + hidxb[0][jj];
+        ib++;
     }
+}
+
+/* Condense one block of T stages: the three building blocks on cleared outputs (the condensed arrays of
+ * d_part_cond), the Gammas as lib4 matrices at the start of work.  Outputs are lib4 (BAbt2 sd cnx2',
+ * RSQ2 sd cnux2, DCt2 sd cng2) and the padded d2/idxb2. */
+static void cond_block(int T, int *nx, int *nu, int *nb, int **hidxb, double **hpBAbt, double **hpRSQrq, double **hd,
+                       double *pBAbt2, double *pRSQ2, double *pDCt2, double *d2, int *idxb2, double *work) {
+    int nut = 0;
+    for (int j = 0; j < T; j++) nut += nu[j];
+    const int nv = nut + nx[0];
+    double *hpGamma[T];
+    double *p = work;
+    for (int j = 0; j < T; j++) {
+        hpGamma[j] = p;
+        p += (long)rup(gamma_rows(j, nx, nu), BS) * rup(nx[j + 1], NCL);
+    }
+    int nbb = nb[0], nbg = 0;
+    for (int s = 1; s < T; s++)
+        for (int jj = 0; jj < nb[s]; jj++) {
+            if (hidxb[s][jj] < nu[s])
+                nbb++;
+            else
+                nbg++;
+        }
+    for (int i = 0; i < rup(nv + 1, BS) * rup(nv, NCL); i++) pRSQ2[i] = 0.0;
+    for (int i = 0; i < rup(nv, BS) * rup(nbg, NCL); i++) pDCt2[i] = 0.0;
+    for (int i = 0; i < 2 * rup(nbb, BS) + 2 * rup(nbg, BS); i++) d2[i] = 0.0;
+    orc_d_cond_BAbt(T, nx, nu, hpBAbt, p, hpGamma, pBAbt2);
+    orc_d_cond_RSQrq(T, nx, nu, hpBAbt, hpRSQrq, hpGamma, p, pRSQ2);
+    orc_d_cond_DCtd(T, nx, nu, nb, hidxb, hd, hpGamma, pDCt2, d2, idxb2);
 }
 
 /* d_part_cond.c:926-1062 */

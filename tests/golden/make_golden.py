@@ -25,6 +25,9 @@ from hpmpc_amd.golden import save_case  # noqa: E402
 from hpmpc_amd.ocp import (BS, OCPQP, lib4_size, mass_spring_qp, pack_lib4, rup,  # noqa: E402
                            unpack_lib4)
 
+sys.path.insert(0, os.path.dirname(HERE))
+from helpers import COND_FILL, sub_block  # noqa: E402
+
 
 def ref_api():
     path = os.path.join(ROOT, "oracle", "_ref", "libhpmpc_ref.so")
@@ -217,6 +220,7 @@ def main():
     # ---------------- alternate IPM: d_ip2_mpc_hard_tv, d_kkt_solve_new_rhs_mpc_hard_tv, d_res_mpc_hard_tv ----
     alt(ref, ref_avx_api(), rng, out)
     pcond(ref, out)
+    cond_parts(ref, out)
     iface(ref, out)
     wide(ref, ref_avx_api(), out)
     divergent(ref, out)
@@ -286,6 +290,23 @@ def pcond(ref, out):
         qp = mass_spring_qp(N, nx, nu, boxes=False)
         ux, pi, _, _ = ref.ric_sv(qp.copy(), compute_pi=1, compute_Pb=0)
         out.append(save_case(f"pcond_sv_N{N}_nx{nx}_nu{nu}_N2_{N2}", "pcond_sv", qp, dict(N2=N2), dict(ux=ux, pi=pi)))
+
+
+def cond_parts(ref, out):
+    """The building blocks of one condensing block alone (d_part_cond.c:214-689): d_cond_BAbt, then d_cond_RSQrq
+    and d_cond_DCtd on the reference's own Gammas, outputs pre-filled with COND_FILL.  Blocks cut from
+    time-variant boxed mass-spring problems, first block (nx_0 = 0) and inner ones, T = 1 .. 10, nu <= 4 (the c99
+    build's RSQrq is wrong for nu > 4)."""
+    for (N, nx, nu, s0, T) in [(12, 8, 3, 3, 5), (8, 12, 4, 0, 4), (6, 6, 2, 2, 1), (24, 24, 4, 10, 10),
+                               (6, 4, 1, 1, 3), (9, 8, 3, 0, 9)]:
+        qp = mass_spring_qp(N, nx, nu, boxes=True, batch=1, time_variant=True, seed=100 + N).problem(0)
+        b = sub_block(qp, s0, T)
+        G, B2 = ref.cond_BAbt(b.copy(), fill=COND_FILL)
+        R2 = ref.cond_RSQrq(b.copy(), G, fill=COND_FILL)
+        DCt2, d2, idxb2, (nbb, nbg) = ref.cond_DCtd(b.copy(), G, fill=COND_FILL)
+        outs = dict(Gamma=G, BAbt2=B2, RSQrq2=R2, DCt2=DCt2, d2=d2, idxb2=idxb2.astype(np.float64), nbb=nbb, nbg=nbg)
+        out.append(save_case(f"cond_parts_N{N}_s{s0}_T{T}_nx{nx}_nu{nu}", "cond_parts", b, dict(fill=COND_FILL),
+                             outs))
 
 
 def iface(ref, out):
@@ -526,6 +547,10 @@ if __name__ == "__main__":
         o = []
         divergent(ref_api(), o)
         print(f"wrote {len(o)} divergent cases, {sum(os.path.getsize(p) for p in o) / 1e6:.2f} MB")
+    elif len(sys.argv) > 1 and sys.argv[1] == "cond_parts":
+        o = []
+        cond_parts(ref_api(), o)
+        print(f"wrote {len(o)} cond_parts cases, {sum(os.path.getsize(p) for p in o) / 1e6:.2f} MB")
     elif len(sys.argv) > 1 and sys.argv[1] == "pcond":
         o = []
         pcond(ref_api(), o)

@@ -64,15 +64,15 @@ def run_case(api, case):
         c, _ = api.part_cond(qp, int(a["N2"]))
         e = api.part_expand(qp, c, inp["u2"], inp["p2"], inp["lam2"], inp["t2"])
         return dict(cqp=c, ux=e["ux"], pi=e["pi"], lam=e["lam"], t=e["t"])
-    if case.kind == "ipm_div":
-        # a diverging infeasible problem: only ret and kk to +-2 are comparable (the reference and a second c99
-        # build of it differ by 2 iterations on these very cases, make_golden.py divergent())
-        out = case.out
-        assert int(got["ret"]) == int(out["ret"]) == 2, (case.name, got["ret"], out["ret"])
-        assert abs(int(got["kk"]) - int(out["kk"])) <= 2, (case.name, got["kk"], out["kk"])
-        return
     if case.kind == "pcond_sv":
         return pcond_sv(api, qp, int(a["N2"]))
+    if case.kind == "cond_parts":
+        # each building block alone; RSQrq and DCtd on the reference's own Gammas
+        f = a["fill"]
+        G, B2 = api.cond_BAbt(qp.copy(), fill=f)
+        R2 = api.cond_RSQrq(qp.copy(), case.out["Gamma"], fill=f)
+        DCt2, d2, idxb2, _ = api.cond_DCtd(qp.copy(), case.out["Gamma"], fill=f)
+        return dict(Gamma=G, BAbt2=B2, RSQrq2=R2, DCt2=DCt2, d2=d2, idxb2=idxb2)
     if case.kind in ("iface", "iface_kkt", "iface_newton"):
         return run_iface(api, case)
     if case.kind == "soft":
@@ -258,8 +258,60 @@ def check_soft(case, got):
         assert e <= TOL_SOFT[key], f"{case.name}: {key} err {e:.3e} > {TOL_SOFT[key]:.0e}"
 
 
+def sub_block(qp, s0: int, T: int):
+    """Stages s0 .. s0+T of qp as a horizon-T problem: one condensing block (its stage T only sizes nx_T)."""
+    from hpmpc_amd.ocp import OCPQP
+
+    sl = slice(s0, s0 + T + 1)
+    return OCPQP(T, qp.nx[sl].copy(), qp.nu[sl].copy(), qp.nb[sl].copy(), np.zeros(T + 1, np.int32),
+                 [i.copy() for i in qp.idxb[sl]], [b.copy() for b in qp.BAbt[s0:s0 + T]],
+                 [r.copy() for r in qp.RSQrq[sl]], [d.copy() for d in qp.d[sl]], [], None)
+
+
+COND_FILL = 7.25  # sentinel pre-filled into every output: what the reference leaves alone stays 7.25
+
+
+def _check_written(name, got, ref, fill, tol):
+    """Same elements written (the rest still holds the pre-filled sentinel), written values within tol."""
+    got, ref = np.asarray(got)[: len(ref)], np.asarray(ref)
+    w = ref != fill
+    np.testing.assert_array_equal(got == fill, ~w, err_msg=name + " (written elements)")
+    if w.any():
+        e = float(np.max(np.abs(got[w] - ref[w]) / np.maximum(1.0, np.abs(ref[w]))))
+        assert e <= tol, f"{name}: err {e:.3e}"
+
+
+def check_cond_parts(case, got):
+    """d_cond_BAbt / d_cond_RSQrq / d_cond_DCtd: every element the reference writes and nothing else, except the
+    strict upper triangle of pRSQrq2, which the reference fills for the u_s x u_s blocks and the first stage's
+    square from its work matrix and no consumer reads: there only the lower triangle is compared (and an element
+    the reference leaves alone must stay untouched)."""
+    from hpmpc_amd.ocp import rup, unpack_lib4
+
+    out, f, qp = case.out, case.args["fill"], case.qp
+    for j, (g, r) in enumerate(zip(got["Gamma"], out["Gamma"])):
+        _check_written(f"{case.name} Gamma[{j}]", g, r, f, TOL_RIC)
+    for key in ("BAbt2", "DCt2", "d2"):
+        _check_written(f"{case.name} {key}", got[key], out[key], f, TOL_RIC)
+    np.testing.assert_array_equal(np.asarray(got["idxb2"]), out["idxb2"].astype(np.int32), err_msg=case.name)
+    nv = int(np.sum(qp.nu[: qp.N])) + int(qp.nx[0])
+    n = rup(nv + 1, 4) * rup(nv, 2)
+    A, B = unpack_lib4(np.asarray(got["RSQrq2"])[:n], nv + 1, nv), unpack_lib4(out["RSQrq2"][:n], nv + 1, nv)
+    lo = np.tril(np.ones((nv + 1, nv), dtype=bool))
+    assert np.all(A[lo] != f) and np.all(B[lo] != f), case.name
+    e = float(np.max(np.abs(A[lo] - B[lo]) / np.maximum(1.0, np.abs(B[lo]))))
+    assert e <= TOL_RIC, f"{case.name}: RSQrq2 lower err {e:.3e}"
+    assert np.all(A[B == f] == f), case.name + " RSQrq2 wrote where the reference does not"
+    flat_g, flat_r = np.asarray(got["RSQrq2"]), out["RSQrq2"]
+    pad = np.ones(flat_r.size, dtype=bool)  # lib4 padding rows / columns outside the matrix
+    pad[:n] = False
+    assert np.all(flat_g[: flat_r.size][pad & (flat_r == f)] == f), case.name
+
+
 def check_case(case, got):
     """Assert parity of `got` against the golden outputs of `case`."""
+    if case.kind == "cond_parts":
+        return check_cond_parts(case, got)
     if case.kind == "soft":
         return check_soft(case, got)
     if case.kind == "pcond":

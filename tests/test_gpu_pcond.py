@@ -126,6 +126,39 @@ def test_pcond_entry_points_vs_oracle(product, oracle, case):
     check_pcond(case_like, dict(cqp=gc, ux=ge["ux"], pi=ge["pi"], lam=ge["lam"], t=ge["t"]))
 
 
+COND_PARTS = [
+    # N, nx, nu, s0, T: blocks of time-variant boxed mass-spring problems
+    (200, 24, 6, 40, 10),   # a configs[4] block (nu > 4: the oracle is the checker)
+    (30, 12, 5, 0, 6),      # first block (nx_0 = 0)
+    (12, 18, 7, 4, 2),
+    (20, 30, 3, 5, 7),      # nx > 16
+]
+
+
+@pytest.mark.parametrize("case", COND_PARTS, ids=[f"N{c[0]}_nx{c[1]}_nu{c[2]}_T{c[4]}" for c in COND_PARTS])
+def test_cond_parts_vs_oracle(product, oracle, case):
+    """d_cond_BAbt / d_cond_RSQrq / d_cond_DCtd alone (one hk_pcond phase each) against the oracle's restatement
+    of the same building blocks, on shapes the c99 reference build gets wrong (nu > 4) or the goldens lack; the
+    checks are the goldens' (check_cond_parts): same elements written, values to 1e-12."""
+    from hpmpc_amd.golden import Case
+    from hpmpc_amd.ocp import mass_spring_qp
+    from helpers import COND_FILL, check_cond_parts, sub_block
+
+    N, nx, nu, s0, T = case
+    qp = mass_spring_qp(N, nx, nu, boxes=True, batch=1, time_variant=True, seed=N + T).problem(0)
+    b = sub_block(qp, s0, T)
+    G, B2 = oracle.cond_BAbt(b.copy(), fill=COND_FILL)
+    R2 = oracle.cond_RSQrq(b.copy(), G, fill=COND_FILL)
+    DCt2, d2, idxb2, _ = oracle.cond_DCtd(b.copy(), G, fill=COND_FILL)
+    like = Case.__new__(Case)
+    like.name, like.qp, like.args = f"cond_parts_{case}", b, dict(fill=COND_FILL)
+    like.out = dict(Gamma=G, BAbt2=B2, RSQrq2=R2, DCt2=DCt2, d2=d2, idxb2=idxb2.astype(np.float64))
+    pG, pB2 = product.cond_BAbt(b.copy(), fill=COND_FILL)
+    pR2 = product.cond_RSQrq(b.copy(), G, fill=COND_FILL)
+    pD, pd2, pidx, _ = product.cond_DCtd(b.copy(), G, fill=COND_FILL)
+    check_cond_parts(like, dict(Gamma=pG, BAbt2=pB2, RSQrq2=pR2, DCt2=pD, d2=pd2, idxb2=pidx))
+
+
 def test_pcond_sv_pipeline_nu6(product, oracle):
     """condense -> wide sv -> expand through the C ABI == the oracle's direct Riccati (nu = 6)."""
     from hpmpc_amd.ocp import mass_spring_qp

@@ -13,7 +13,7 @@ CASES = load_all()
 
 def test_goldens_present():
     kinds = {c.kind for c in CASES}
-    assert {"sv", "trf_trs", "ipm", "kkt", "res", "newton", "ipm2", "kkt2", "res2", "pcond", "pcond_sv", "iface", "iface_kkt", "soft"} <= kinds, kinds
+    assert {"sv", "trf_trs", "ipm", "kkt", "res", "newton", "ipm2", "kkt2", "res2", "pcond", "pcond_sv", "cond_parts", "iface", "iface_kkt", "soft"} <= kinds, kinds
     assert len(CASES) >= 20
 
 
