@@ -207,6 +207,25 @@ class HpmpcAPI:
         self._sync()
         return dict(ret=ret, kk=kk.value, stat=stat[: 5 * max(kk.value, 0)].copy(), ux=ux_, pi=pi, lam=lam, t=t)
 
+    def residuals_soft(self, sq, q, ux, pi, lam, t):
+        """d_res_mpc_soft_tv (mpc_solvers/d_res_ip_soft.c:38) at an iterate of a SoftQP (general constraints
+        allowed: sq.ng / sq.DCt).  Returns rq, rb, rd, rz, mu."""
+        N = sq.N
+        pns = [rup(int(sq.ns[k]), 4) for k in range(N + 1)]
+        rq = [np.zeros(sq.nux(k) + 8) for k in range(N + 1)]
+        rb = [np.zeros(int(sq.nx[k + 1]) + 8) for k in range(N)] + [np.zeros(8)]
+        rd = [np.zeros(2 * rup(int(sq.nb[k]), 4) + 2 * rup(int(sq.ng[k]), 4) + 2 * pns[k] + 8) for k in range(N + 1)]
+        rz = [np.zeros(2 * pns[k] + 8) for k in range(N + 1)]
+        mu = C.c_double(0.0)
+        dct = sq.DCt if sq.DCt else [np.zeros(8)] * (N + 1)
+        self.fn("d_res_mpc_soft_tv")(
+            C.c_int(N), iv(sq.nx), iv(sq.nu), iv(sq.nb), ipp(sq.idxb), iv(sq.ng), iv(sq.ns), self._pp(sq.BAbt),
+            self._pp(sq.RSQrq), self._pp(q), self._pp(sq.Z), self._pp(sq.z), self._pp(ux), self._pp(dct),
+            self._pp(sq.d), self._pp(pi), self._pp(lam), self._pp(t), self._pp(rq), self._pp(rb), self._pp(rd),
+            self._pp(rz), C.byref(mu))
+        self._sync()
+        return dict(rq=rq, rb=rb[:N], rd=rd, rz=rz, mu=mu.value)
+
     def prepare_ipm(self, qp: OCPQP, *, k_max=50, mu0=2.0, mu_tol=1e-12, alpha_min=1e-8):
         """Pre-marshalled d_ip2_res_mpc_hard_tv call: returns (call, kk) where call() runs one cold-start
         solve on private buffers and returns the status; kk.value holds the iteration count.  Used to
@@ -529,6 +548,41 @@ class HpmpcAPI:
                     u=[u[k][:nuv[k]] for k in range(N)], x=[x[k][:nxv[k]] for k in range(N + 1)],
                     pi=[pi[k][:nxv[k + 1]] for k in range(N)],
                     lam=[lam[k][:2 * P["nb"][k] + 2 * P["ng"][k]] for k in range(N + 1)], work0=work0)
+
+    def ip_ocp_soft(self, P, *, k_max=50, mu0=100.0, mu_tol=1e-8, warm=None):
+        """fortran_order_d_ip_ocp_soft_tv (include/c_interface.h:71) on an interface-form problem with ns / Z / z
+        (oracle/iface_oracle.py random_soft_iface_problem)."""
+        N = P["N"]
+        nx, nu, nb, ng, ns = iv(P["nx"]), iv(P["nu"]), iv(P["nb"]), iv(P["ng"]), iv(P["ns"])
+        idx = [np.ascontiguousarray(i, dtype=np.int32) for i in P["hidxb"]]
+        a = self._iface_args(P, "F")
+        Z = [np.concatenate([np.asarray(v, dtype=np.float64), np.zeros(4)]) for v in P["Z"]]
+        z = [np.concatenate([np.asarray(v, dtype=np.float64), np.zeros(4)]) for v in P["z"]]
+        x = [np.zeros(P["nx"][k] + 4) for k in range(N + 1)]
+        u = [np.zeros(P["nu"][k] + 4) for k in range(N + 1)]
+        if warm is not None:
+            for k in range(N + 1):
+                x[k][:P["nx"][k]] = warm["x"][k]
+                if k < N:
+                    u[k][:P["nu"][k]] = warm["u"][k]
+        pi = [np.zeros(P["nx"][k + 1] + 4) for k in range(N)]
+        nl = [2 * P["nb"][k] + 2 * P["ng"][k] + 4 * P["ns"][k] for k in range(N + 1)]
+        lam = [np.zeros(n + 4) for n in nl]
+        inf = np.zeros(4)
+        stat = np.zeros(5 * k_max + 5)
+        wsz = self.fn("hpmpc_d_ip_ocp_soft_tv_work_space_size_bytes")(C.c_int(N), nx, nu, nb, ipp(idx), ng, ns)
+        work0 = np.zeros(wsz // 8 + 16)
+        kk = C.c_int(0)
+        ret = self.fn("fortran_order_d_ip_ocp_soft_tv")(
+            C.byref(kk), C.c_int(k_max), C.c_double(mu0), C.c_double(mu_tol), C.c_int(N), nx, nu, nb, ipp(idx), ng, ns,
+            C.c_int(1 if warm is not None else 0), dpp(a["A"]), dpp(a["B"]), dpp(a["b"]), dpp(a["Q"]), dpp(a["S"]),
+            dpp(a["R"]), dpp(a["q"]), dpp(a["r"]), dpp(Z), dpp(z), dpp(a["lb"]), dpp(a["ub"]), dpp(a["C"]),
+            dpp(a["D"]), dpp(a["lg"]), dpp(a["ug"]), dpp(x), dpp(u), dpp(pi), dpp(lam), _dptr(inf), _dptr(work0),
+            _dptr(stat))
+        nxv, nuv = P["nx"], P["nu"]
+        return dict(status=ret, kk=kk.value, stat=stat[:5 * max(kk.value, 0)].copy(), inf_norm_res=inf,
+                    u=[u[k][:nuv[k]] for k in range(N)], x=[x[k][:nxv[k]] for k in range(N + 1)],
+                    pi=[pi[k][:nxv[k + 1]] for k in range(N)], lam=[lam[k][:nl[k]] for k in range(N + 1)])
 
     def newton_ocp(self, P, ux0, pi0, lam0, t0, *, k_max=1, mu0=0.1, mu_tol=1e-12):
         """fortran_order_d_ip_ocp_hard_tv_single_newton_step (include/c_interface.h:66)."""

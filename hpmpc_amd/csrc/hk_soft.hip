@@ -423,3 +423,123 @@ extern "C" int hk_soft_launch(int which, const SoftArgs* a, int count, hipStream
     hipLaunchKernelGGL(hk_soft_pass, dim3(count), dim3(64), 0, stream, *a, which);
     return hipGetLastError() == hipSuccess ? 0 : 1;
 }
+
+// ------------------------------------------------------------------------------------------------
+// d_res_mpc_soft_tv (mpc_solvers/d_res_ip_soft.c:38-268), one workgroup of RT threads per call: the stages in
+// order, a thread per row of r_q / r_b and per constraint of r_d / r_z, signs as the reference leaves them (r_q,
+// r_b, r_d negated at the end, r_z not).  The reference's layout quirks are kept (soft residual): the
+// soft constraint i of stage k acts on ux[idxb[k][nu_k + i]]; its multipliers enter r_q as lam_0 - lam_1 on
+// k < N and as -lam_2 + lam_3 on k = N; on stage N, r_q starts from pi_{N-1} - q on the state rows (the input
+// rows keep the caller's values) and its symv covers the leading nx_N x nx_N block; mu averages lam t over
+// 2 (nb + ng + ns).
+// ------------------------------------------------------------------------------------------------
+namespace {
+constexpr int RT = 256;
+__device__ __forceinline__ double q4(const double* A, int sd, int i, int j) {
+    return A[(i >> 2) * 4 * sd + (i & 3) + 4 * j];
+}
+}  // namespace
+
+__global__ __launch_bounds__(RT) void hk_soft_res(SoftResArgs a) {
+    __shared__ double red[RT];
+    double* B = a.buf;
+    const int tid = threadIdx.x;
+    double musum = 0.0;
+    long ntot = 0;
+    for (int k = 0; k <= a.N; k++) {
+        const SoftResStage s = a.st[k];
+        const int nux = s.nu + s.nx, og = 2 * s.pnb, os = 2 * s.pnb + 2 * s.png, pns = s.pns;
+        const bool last = k == a.N;
+        const int* ib = a.idxb + s.oI;
+        const double *ux = B + s.oux, *lam = B + s.olam, *t = B + s.ot, *d = B + s.od;
+        ntot += s.nb + s.ng + s.ns;
+        // mu partial sums
+        for (int j = tid; j < s.nb; j += RT) musum += lam[j] * t[j] + lam[s.pnb + j] * t[s.pnb + j];
+        for (int j = tid; j < s.ng; j += RT) musum += lam[og + j] * t[og + j] + lam[og + s.png + j] * t[og + s.png + j];
+        for (int j = tid; j < s.ns; j += RT)
+            musum += lam[os + j] * t[os + j] + lam[os + pns + j] * t[os + pns + j] + lam[os + 2 * pns + j] * t[os + 2 * pns + j] +
+                     lam[os + 3 * pns + j] * t[os + 3 * pns + j];
+        // r_d (negated) and r_z
+        double* rd = B + s.ord;
+        for (int j = tid; j < s.nb; j += RT) {
+            const double x = ux[ib[j]];
+            rd[j] = -(x - d[j] - t[j]);
+            rd[s.pnb + j] = -(-x + d[s.pnb + j] - t[s.pnb + j]);
+        }
+        for (int j = tid; j < s.ng; j += RT) {
+            const double* G = B + s.oG;
+            double g = 0.0;
+            for (int i = 0; i < nux; i++) g += q4(G, s.sdG, i, j) * ux[i];
+            rd[og + j] = -(g - d[og + j] - t[og + j]);
+            rd[og + s.png + j] = -(-g + d[og + s.png + j] - t[og + s.png + j]);
+        }
+        for (int j = tid; j < s.ns; j += RT) {
+            const double x = ux[ib[s.nu + j]];
+            rd[os + j] = -(t[os + 2 * pns + j] + x - d[os + j] - t[os + j]);
+            rd[os + pns + j] = -(t[os + 3 * pns + j] - x + d[os + pns + j] - t[os + pns + j]);
+            const double *Z = B + s.oZ, *z = B + s.oz;
+            double* rz = B + s.orz;
+            rz[j] = z[j] + Z[j] * t[os + 2 * pns + j] - lam[os + j] - lam[os + 2 * pns + j];
+            rz[pns + j] = z[pns + j] + Z[pns + j] * t[os + 3 * pns + j] - lam[os + pns + j] - lam[os + 3 * pns + j];
+        }
+        // r_q (negated): row i by one thread
+        double* rq = B + s.orq;
+        const double* q = B + s.oq;
+        const int nsym = last ? s.nx : nux;
+        for (int i = tid; i < nux; i += RT) {
+            double v;
+            if (i < s.nu)
+                v = last ? rq[i] : -q[i];  // stage N input rows: the caller's values (:199-200 writes only x rows)
+            else
+                v = -q[i] + (s.opim1 >= 0 ? B[s.opim1 + i - s.nu] : 0.0);
+            if (i < nsym) {
+                const double* Q = B + s.oQ;
+                double acc = 0.0;
+                for (int j = 0; j < nsym; j++) acc += (i >= j ? q4(Q, s.sdQ, i, j) : q4(Q, s.sdQ, j, i)) * ux[j];
+                v -= acc;
+            }
+            for (int j = 0; j < s.nb; j++)
+                if (ib[j] == i) v += lam[j] - lam[s.pnb + j];
+            if (s.ng > 0) {
+                const double* G = B + s.oG;
+                double acc = 0.0;
+                for (int j = 0; j < s.ng; j++) acc += q4(G, s.sdG, i, j) * (lam[og + j] - lam[og + s.png + j]);
+                v += acc;
+            }
+            for (int j = 0; j < s.ns; j++)
+                if (ib[s.nu + j] == i)
+                    v += last ? -lam[os + 2 * pns + j] + lam[os + 3 * pns + j] : lam[os + j] - lam[os + pns + j];
+            if (!last) {
+                const double* Bt = B + s.oB;
+                const double* pi = B + s.opi;
+                double acc = 0.0;
+                for (int j = 0; j < s.nx1; j++) acc += q4(Bt, s.sdB, i, j) * pi[j];
+                v -= acc;
+            }
+            rq[i] = -v;
+        }
+        // r_b (negated): x_{k+1} - A x - B u - b
+        if (!last) {
+            const double* Bt = B + s.oB;
+            const double* ux1 = B + s.oux1;
+            double* rb = B + s.orb;
+            for (int j = tid; j < s.nx1; j += RT) {
+                double acc = 0.0;
+                for (int i = 0; i < nux; i++) acc += q4(Bt, s.sdB, i, j) * ux[i];
+                rb[j] = -(ux1[s.nu1 + j] - q4(Bt, s.sdB, nux, j) - acc);
+            }
+        }
+    }
+    red[tid] = musum;
+    __syncthreads();
+    for (int w = RT / 2; w > 0; w >>= 1) {
+        if (tid < w) red[tid] += red[tid + w];
+        __syncthreads();
+    }
+    if (tid == 0) B[a.omu] = ntot != 0 ? red[0] / (2.0 * ntot) : 0.0;
+}
+
+extern "C" int hk_soft_res_launch(const SoftResArgs* a, hipStream_t stream) {
+    hipLaunchKernelGGL(hk_soft_res, dim3(1), dim3(RT), 0, stream, *a);
+    return (int)hipGetLastError();
+}

@@ -43,3 +43,20 @@ struct SoftArgs {
     double* stat;  // per problem, 5 k_max
     long long sS;
 };
+
+// d_res_mpc_soft_tv (mpc_solvers/d_res_ip_soft.c:38-268): one 256-thread workgroup walks the stages of one
+// problem.  Every input and output array of the call is copied into one buffer; SoftResStage holds each stage's
+// sizes and offsets (doubles, -1 = absent).
+struct SoftResStage {
+    int nu, nx, nb, ng, ns, nx1, nu1;
+    int pnb, png, pns, sdB, sdQ, sdG;
+    int oB, oQ, oq, oZ, oz, oux, oux1, oG, od, opi, opim1, olam, ot, orq, orb, ord, orz, oI;
+};
+
+struct SoftResArgs {
+    int N;
+    const SoftResStage* st;
+    const int* idxb;  // the caller's idxb rows, packed (oI)
+    double* buf;      // inputs and outputs
+    int omu;          // mu
+};

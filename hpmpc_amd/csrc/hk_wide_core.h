@@ -181,7 +181,13 @@ __device__ __forceinline__ WideProb wide_prob(const WideArgs& a, int p) {
 // Forward (:339-397): ux_k = -L_k^{-T}(l_k ...) over the u block (the whole block at k = 0),
 //   x_{k+1} = b_k + BAbt_k' ux_k (dgemv_t), pi_k = Lxx_{k+1}(Lxx_{k+1}' x_{k+1} + l_{k+1,x}).
 // ------------------------------------------------------------------------------------------------
-__device__ void wide_sv_body(const WideArgs& a, const WideProb& q) {
+// HK_WIDE_NOINLINE (probe builds only, tools/wide_noinline.sh): the two bodies as real calls
+#ifdef HK_WIDE_NOINLINE
+#define HK_WIDE_BODY __attribute__((noinline))
+#else
+#define HK_WIDE_BODY
+#endif
+__device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) {
     extern __shared__ double sm[];
     const int tid = threadIdx.x;
     double* M = sm;
@@ -491,7 +497,7 @@ __device__ void wide_sv_body(const WideArgs& a, const WideProb& q) {
 // stage 0) with the rectangular update of the later rows.  Forward as the sv forward,
 // pi_k = Lxx(Lxx' x_{k+1}) + v_{k+1,x}.  The processed v_k are parked in ux (the forward overwrites them).
 // ------------------------------------------------------------------------------------------------
-__device__ void wide_trs_body(const WideArgs& a, const WideProb& q) {
+__device__ HK_WIDE_BODY void wide_trs_body(const WideArgs& a, const WideProb& q) {
     extern __shared__ double sm[];
     const int tid = threadIdx.x, lane = tid & 63;
     double* M = sm;

@@ -1539,3 +1539,128 @@ extern "C" int d_ip2_mpc_soft_tv(int* kk, int k_max, double mu0, double mu_tol, 
     }
     return hist[2];
 }
+
+// ------------------------------------------------------------------------------------------------
+// d_res_mpc_soft_tv (mpc_solvers/d_res_ip_soft.c:38-268, include/mpc_solvers.h:71): hk_soft_res on a copy of
+// every array of the call.  The output vectors are uploaded first, so the entries the reference does not write
+// (padding, and stage N's input rows of r_q, :199-200) come back as the caller left them.  General constraints
+// are supported (the residual has no soft-gradient quirk); stage 0's pi_{-1} (nx_0 > 0) reads as zero.
+// ------------------------------------------------------------------------------------------------
+extern "C" int hk_soft_res_launch(const SoftResArgs* a, hipStream_t stream);
+
+extern "C" void d_res_mpc_soft_tv(int N, int* nx, int* nu, int* nb, int** idxb, int* ng, int* ns, double** hpBAbt,
+                                  double** hpQ, double** hq, double** hZ, double** hz, double** hux, double** hpDCt,
+                                  double** hd, double** hpi, double** hlam, double** ht, double** hrq, double** hrb,
+                                  double** hrd, double** hrz, double* mu) {
+    g_err = 0;
+    if (N < 0) {
+        set_err(HPMPC_MI355X_EUNSUPPORTED, "d_res_mpc_soft_tv: N < 0");
+        return;
+    }
+    std::vector<SoftResStage> st(N + 1);
+    std::vector<int> ints;
+    size_t o = 0;
+    auto take = [&](size_t n) {
+        size_t r = o;
+        o += (n + 7) / 8 * 8;
+        return (int)r;
+    };
+    for (int k = 0; k <= N; k++) {
+        SoftResStage& s = st[k];
+        s.nu = nu[k];
+        s.nx = nx[k];
+        s.nb = nb[k];
+        s.ng = ng[k];
+        s.ns = ns[k];
+        s.nx1 = k < N ? nx[k + 1] : 0;
+        s.nu1 = k < N ? nu[k + 1] : 0;
+        s.pnb = rup(nb[k], BS);
+        s.png = rup(ng[k], BS);
+        s.pns = rup(ns[k], BS);
+        const int nux = s.nu + s.nx, ncv = 2 * s.pnb + 2 * s.png + 4 * s.pns, nrd = 2 * s.pnb + 2 * s.png + 2 * s.pns;
+        s.sdB = rup(s.nx1, NCL);
+        s.sdQ = rup(nux, NCL);
+        s.sdG = rup(ng[k], NCL);
+        s.oB = k < N ? take((size_t)rup(nux + 1, BS) * s.sdB) : -1;
+        s.oQ = take((size_t)rup(nux + 1, BS) * s.sdQ);
+        s.oq = take(nux);
+        s.oZ = take(2 * s.pns);
+        s.oz = take(2 * s.pns);
+        s.oux = take(nux);
+        s.oG = ng[k] > 0 ? take((size_t)rup(nux, BS) * s.sdG) : -1;
+        s.od = take(nrd);
+        s.opi = k < N ? take(s.nx1) : -1;
+        s.olam = take(ncv);
+        s.ot = take(ncv);
+        s.orq = take(nux);
+        s.orb = k < N ? take(s.nx1) : -1;
+        s.ord = take(nrd);
+        s.orz = take(2 * s.pns);
+        s.oI = (int)ints.size();
+        // the soft constraints read idxb[k][nu_k + i] (:107), so the row is copied that far
+        const int nI = std::max(nb[k], ns[k] > 0 ? nu[k] + ns[k] : 0);
+        for (int j = 0; j < nI; j++) ints.push_back(idxb[k][j]);
+    }
+    for (int k = 0; k <= N; k++) {
+        st[k].oux1 = k < N ? st[k + 1].oux : -1;
+        st[k].opim1 = k > 0 ? st[k - 1].opi : -1;
+    }
+    const int omu = take(1);
+    const size_t oSt = take((sizeof(SoftResStage) * (N + 1) + 7) / 8), oIdx = take((4 * ints.size() + 7) / 8 + 1);
+    Arena A{};
+    A.total = o;
+    if (!g_ctx.ensure(A.total)) return;
+    double* H = g_ctx.host;
+    memset(H, 0, A.total * sizeof(double));
+    auto cp = [&](int off, const double* src, size_t n) {
+        if (off >= 0 && n > 0) memcpy(H + off, src, n * sizeof(double));
+    };
+    for (int k = 0; k <= N; k++) {
+        const SoftResStage& s = st[k];
+        const int nux = s.nu + s.nx, ncv = 2 * s.pnb + 2 * s.png + 4 * s.pns, nrd = 2 * s.pnb + 2 * s.png + 2 * s.pns;
+        if (k < N) cp(s.oB, hpBAbt[k], (size_t)rup(nux + 1, BS) * s.sdB);
+        cp(s.oQ, hpQ[k], (size_t)rup(nux + 1, BS) * s.sdQ);
+        cp(s.oq, hq[k], nux);
+        if (ns[k] > 0) {
+            cp(s.oZ, hZ[k], 2 * s.pns);
+            cp(s.oz, hz[k], 2 * s.pns);
+            cp(s.orz, hrz[k], 2 * s.pns);
+        }
+        cp(s.oux, hux[k], nux);
+        if (ng[k] > 0) cp(s.oG, hpDCt[k], (size_t)rup(nux, BS) * s.sdG);
+        if (nrd > 0) {
+            cp(s.od, hd[k], nrd);
+            cp(s.ord, hrd[k], nrd);
+            cp(s.olam, hlam[k], ncv);
+            cp(s.ot, ht[k], ncv);
+        }
+        if (k < N) {
+            cp(s.opi, hpi[k], s.nx1);
+            cp(s.orb, hrb[k], s.nx1);
+        }
+        cp(s.orq, hrq[k], nux);
+    }
+    memcpy(H + oSt, st.data(), sizeof(SoftResStage) * (N + 1));
+    if (!ints.empty()) memcpy(H + oIdx, ints.data(), 4 * ints.size());
+    SoftResArgs a;
+    a.N = N;
+    a.st = reinterpret_cast<const SoftResStage*>(g_ctx.dev + oSt);
+    a.idxb = reinterpret_cast<const int*>(g_ctx.dev + oIdx);
+    a.buf = g_ctx.dev;
+    a.omu = omu;
+    if (!up(A)) return;
+    if (hk_soft_res_launch(&a, g_ctx.stream)) {
+        set_err(HPMPC_MI355X_EHIP, "hk_soft_res launch failed");
+        return;
+    }
+    if (!down(A)) return;
+    for (int k = 0; k <= N; k++) {
+        const SoftResStage& s = st[k];
+        const int nux = s.nu + s.nx, nrd = 2 * s.pnb + 2 * s.png + 2 * s.pns;
+        memcpy(hrq[k], H + s.orq, nux * sizeof(double));
+        if (k < N && s.nx1 > 0) memcpy(hrb[k], H + s.orb, s.nx1 * sizeof(double));
+        if (nrd > 0) memcpy(hrd[k], H + s.ord, nrd * sizeof(double));
+        if (ns[k] > 0) memcpy(hrz[k], H + s.orz, 2 * s.pns * sizeof(double));
+    }
+    *mu = H[omu];
+}

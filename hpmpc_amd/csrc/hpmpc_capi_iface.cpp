@@ -487,3 +487,185 @@ extern "C" void c_order_d_solve_kkt_new_rhs_ocp_hard_tv(int N, int* nx, int* nu,
     kkt_ocp(true, N, nx, nu, nb, hidxb, ng, A, B, b, Q, S, R, q, r, lb, ub, C, D, lg, ug, x, u, pi, lam, inf_norm_res,
             work0);
 }
+
+// ------------------------------------------------------------------------------------------------
+// Soft constraints: fortran_order_d_ip_ocp_soft_tv (interfaces/c/fortran_order_interface.c:1442-1971) and its
+// work-space size (interfaces/c/c_interface_work_space.c:177-236).  Packing on the host into private buffers (work0
+// is not used), then this library's d_ip2_mpc_soft_tv and d_res_mpc_soft_tv -- both on the GPU.  As the reference:
+// no partial condensing; idxb = the nb hard boxes then the ns soft ones, lb / ub hold nb + ns bounds; Z[k] =
+// [lower (ns) | upper (ns)]; mu0 <= 0 -> the largest entry (not absolute value) of R, S, Q, r, q, Z, z.  Two
+// reference defects are handled as follows (soft constraints):
+//   * the reference never copies z into the IPM's hz (:1712-1719 fill hZ only), so its IPM sees the contents of
+//     work0 there -- zeros for a zeroed work0; the linear slack penalty passed to the IPM here is zero;
+//   * its residual call passes the arguments shifted by one (an extra hb after hpBAbt and no hrz, :1880 against
+//     mpc_solvers.h:71), so its inf_norm_res comes from scrambled inputs; here d_res_mpc_soft_tv is called as
+//     declared (r_q / r_b / r_d of the returned iterate, with the same zero z).
+// ------------------------------------------------------------------------------------------------
+extern "C" int hpmpc_d_ip_ocp_soft_tv_work_space_size_bytes(int N, int* nx, int* nu, int* nb, int** hidxb, int* ng,
+                                                             int* ns) {
+    (void)hidxb;
+    long long d_size = BS;
+    for (int k = 0; k <= N; k++) {
+        const int u = k < N ? nu[k] : 0;
+        const int pnx = rup(nx[k], BS), pnz = rup(u + nx[k] + 1, BS), pnb = rup(nb[k], BS), png = rup(ng[k], BS),
+                  pns = rup(ns[k], BS), cnx1 = k < N ? rup(nx[k + 1], NCL) : 0, cnux = rup(u + nx[k], NCL),
+                  cng = rup(ng[k], NCL);
+        d_size += (long long)pnz * cnx1 + (long long)pnz * cng + (long long)pnz * cnux + 3 * pnx + 3 * pnz + 8 * pnb +
+                  8 * png + 16 * pns;
+    }
+    std::vector<int> nuv(nu, nu + N + 1);
+    nuv[N] = 0;
+    long long size = 2 * 64 + d_ip2_mpc_soft_tv_work_space_size_bytes(N, nx, nuv.data(), nb, ng, ns) + d_size * 8;
+    return (int)((size + 63) / 64 * 64);
+}
+
+// include/c_interface.h:71 (interfaces/c/fortran_order_interface.c:1442)
+extern "C" int fortran_order_d_ip_ocp_soft_tv(int* kk, int k_max, double mu0, double mu_tol, int N, int* nx, int* nu_N,
+                                              int* nb, int** hidxb, int* ng, int* ns, int warm_start, double** A,
+                                              double** B, double** b, double** Q, double** S, double** R, double** q,
+                                              double** r, double** Z, double** z, double** lb, double** ub, double** C,
+                                              double** D, double** lg, double** ug, double** x, double** u,
+                                              double** pi, double** lam, double* inf_norm_res, void* work0,
+                                              double* stat) {
+    (void)work0;
+    hk_set_error(0, nullptr);
+    std::vector<int> nu(nu_N, nu_N + N + 1);
+    nu[N] = 0;
+    if (!check_sizes(N, nx, nu.data(), nb)) return HPMPC_MI355X_EUNSUPPORTED;
+    const int n1 = N + 1;
+    std::vector<std::vector<double>> vBAbt(N), vDCt(n1), vRSQ(n1), vrq(n1), vZ(n1), vz(n1), vd(n1), vux(n1),
+        vpi(N), vlam(n1), vt(n1), vrb(N), vrrq(n1), vrd(n1), vrz(n1);
+    std::vector<double*> pBAbt(N), pDCt(n1), pRSQ(n1), prq(n1), pZ(n1), pz(n1), pd(n1), pux(n1), ppi(N), plam(n1),
+        pt(n1), prb(N), prrq(n1), prd(n1), prz(n1);
+    std::vector<int> pnb(n1), png(n1), pns(n1);
+    for (int k = 0; k <= N; k++) {
+        const int nuk = nu[k], nxk = nx[k], nux = nuk + nxk, pnz = rup(nux + 1, BS), cnux = rup(nux, NCL);
+        pnb[k] = rup(nb[k], BS);
+        png[k] = rup(ng[k], BS);
+        pns[k] = rup(ns[k], BS);
+        const int ncv = 2 * pnb[k] + 2 * png[k] + 4 * pns[k], nd = 2 * pnb[k] + 2 * png[k] + 2 * pns[k];
+        auto mk = [](std::vector<double>& v, size_t n, std::vector<double*>& p, int k) {
+            v.assign(n + 8, 0.0);
+            p[k] = v.data();
+        };
+        if (k < N) {
+            const int nx1 = nx[k + 1], cnx1 = rup(nx1, NCL);
+            mk(vBAbt[k], (size_t)pnz * cnx1, pBAbt, k);
+            mk(vpi[k], rup(nx1, BS), ppi, k);
+            mk(vrb[k], rup(nx1, BS), prb, k);
+            double* M = pBAbt[k];
+            pack(B[k], nx1, nuk, nx1, true, M, cnx1, 0);
+            pack(A[k], nx1, nxk, nx1, true, M, cnx1, nuk);
+            for (int j = 0; j < nx1; j++) P4(M, cnx1, nux, j) = b[k][j];
+        }
+        mk(vDCt[k], (size_t)pnz * rup(ng[k], NCL), pDCt, k);
+        if (ng[k] > 0) {
+            const int cng = rup(ng[k], NCL);
+            if (k < N) pack(D[k], ng[k], nuk, ng[k], true, pDCt[k], cng, 0);
+            pack(C[k], ng[k], nxk, ng[k], true, pDCt[k], cng, nuk);
+        }
+        mk(vRSQ[k], (size_t)pnz * cnux, pRSQ, k);
+        mk(vrq[k], pnz, prq, k);
+        double* M = pRSQ[k];
+        if (k < N) {
+            pack(R[k], nuk, nuk, nuk, false, M, cnux, 0);
+            pack(S[k], nuk, nxk, nuk, true, M, cnux, nuk);  // S' below R
+        }
+        for (int j = 0; j < nxk; j++)  // Q at (nu, nu)
+            for (int i = 0; i < nxk; i++) P4(M, cnux, nuk + i, nuk + j) = Q[k][i + j * nxk];
+        for (int j = 0; j < nuk; j++) P4(M, cnux, nux, j) = prq[k][j] = r[k][j];
+        for (int j = 0; j < nxk; j++) P4(M, cnux, nux, nuk + j) = prq[k][nuk + j] = q[k][j];
+        mk(vZ[k], 2 * pns[k], pZ, k);
+        mk(vz[k], 2 * pns[k], pz, k);  // never filled by the reference wrapper (see above)
+        for (int j = 0; j < ns[k]; j++) {
+            pZ[k][j] = Z[k][j];
+            pZ[k][pns[k] + j] = Z[k][ns[k] + j];
+        }
+        mk(vd[k], nd, pd, k);
+        for (int j = 0; j < nb[k]; j++) {
+            pd[k][j] = lb[k][j];
+            pd[k][pnb[k] + j] = ub[k][j];
+        }
+        for (int j = 0; j < ns[k]; j++) {
+            pd[k][2 * pnb[k] + 2 * png[k] + j] = lb[k][nb[k] + j];
+            pd[k][2 * pnb[k] + 2 * png[k] + pns[k] + j] = ub[k][nb[k] + j];
+        }
+        for (int j = 0; j < ng[k]; j++) {
+            pd[k][2 * pnb[k] + j] = lg[k][j];
+            pd[k][2 * pnb[k] + png[k] + j] = ug[k][j];
+        }
+        mk(vux[k], pnz, pux, k);
+        mk(vlam[k], ncv, plam, k);
+        mk(vt[k], ncv, pt, k);
+        mk(vrrq[k], pnz, prrq, k);
+        mk(vrd[k], nd, prd, k);
+        mk(vrz[k], 2 * pns[k], prz, k);
+        if (warm_start) {
+            for (int j = 0; j < nuk; j++) pux[k][j] = u[k][j];
+            for (int j = 0; j < nxk; j++) pux[k][nuk + j] = x[k][j];
+        }
+    }
+    if (mu0 <= 0) {  // :1723-1740 (no absolute value)
+        for (int k = 0; k <= N; k++) {
+            const int nuk = nu[k], nxk = nx[k];
+            if (k < N) {
+                for (int i = 0; i < nuk * nuk; i++) mu0 = fmax(mu0, R[k][i]);
+                for (int i = 0; i < nxk * nuk; i++) mu0 = fmax(mu0, S[k][i]);
+                for (int i = 0; i < nuk; i++) mu0 = fmax(mu0, r[k][i]);
+            }
+            for (int i = 0; i < nxk * nxk; i++) mu0 = fmax(mu0, Q[k][i]);
+            for (int i = 0; i < nxk; i++) mu0 = fmax(mu0, q[k][i]);
+            for (int i = 0; i < 2 * ns[k]; i++) mu0 = fmax(mu0, Z[k][i]);
+            for (int i = 0; i < 2 * ns[k]; i++) mu0 = fmax(mu0, z[k][i]);
+        }
+    }
+    std::vector<double> work(8);
+    const int status = d_ip2_mpc_soft_tv(kk, k_max, mu0, mu_tol, 1e-8, warm_start, stat, N, nx, nu.data(), nb, hidxb,
+                                         ng, ns, pBAbt.data(), pRSQ.data(), pZ.data(), pz.data(), pDCt.data(),
+                                         pd.data(), pux.data(), 1, ppi.data(), plam.data(), pt.data(), work.data());
+    if (hpmpc_mi355x_last_error() != 0) return status;
+    for (int k = 0; k < N; k++)
+        for (int j = 0; j < nu[k]; j++) u[k][j] = pux[k][j];
+    for (int k = 0; k <= N; k++)
+        for (int j = 0; j < nx[k]; j++) x[k][j] = pux[k][nu[k] + j];
+    double mu = 0.0;
+    d_res_mpc_soft_tv(N, nx, nu.data(), nb, hidxb, ng, ns, pBAbt.data(), pRSQ.data(), prq.data(), pZ.data(), pz.data(),
+                      pux.data(), pDCt.data(), pd.data(), ppi.data(), plam.data(), pt.data(), prrq.data(), prb.data(),
+                      prd.data(), prz.data(), &mu);
+    if (hpmpc_mi355x_last_error() != 0) return status;
+    double tq = fabs(prrq[0][0]);
+    for (int k = 0; k < N; k++)
+        for (int j = 0; j < nu[k] + nx[k]; j++) tq = fmax(tq, fabs(prrq[k][j]));
+    for (int j = 0; j < nx[N]; j++) tq = fmax(tq, fabs(prrq[N][j]));
+    double tb = N > 0 ? fabs(prb[0][0]) : 0.0;
+    for (int k = 0; k < N; k++)
+        for (int j = 0; j < nx[k + 1]; j++) tb = fmax(tb, fabs(prb[k][j]));
+    double td = fabs(prd[0][0]);
+    for (int k = 0; k <= N; k++) {
+        const int os = 2 * pnb[k] + 2 * png[k];
+        for (int j = 0; j < nb[k]; j++) td = fmax(td, fmax(fabs(prd[k][j]), fabs(prd[k][pnb[k] + j])));
+        for (int j = 0; j < ng[k]; j++)
+            td = fmax(td, fmax(fabs(prd[k][2 * pnb[k] + j]), fabs(prd[k][2 * pnb[k] + png[k] + j])));
+        for (int j = 0; j < ns[k]; j++) td = fmax(td, fmax(fabs(prd[k][os + j]), fabs(prd[k][os + pns[k] + j])));
+    }
+    inf_norm_res[0] = tq;
+    inf_norm_res[1] = tb;
+    inf_norm_res[2] = td;
+    inf_norm_res[3] = mu;
+    for (int k = 0; k < N; k++)
+        for (int j = 0; j < nx[k + 1]; j++) pi[k][j] = ppi[k][j];
+    for (int k = 0; k <= N; k++) {  // compact lam: [lo nb | up nb | lg ng | ug ng | 4 soft blocks of ns]
+        const int os = 2 * pnb[k] + 2 * png[k];
+        for (int j = 0; j < nb[k]; j++) {
+            lam[k][j] = plam[k][j];
+            lam[k][nb[k] + j] = plam[k][pnb[k] + j];
+        }
+        for (int j = 0; j < ng[k]; j++) {
+            lam[k][2 * nb[k] + j] = plam[k][2 * pnb[k] + j];
+            lam[k][2 * nb[k] + ng[k] + j] = plam[k][2 * pnb[k] + png[k] + j];
+        }
+        for (int s = 0; s < 4; s++)
+            for (int j = 0; j < ns[k]; j++) lam[k][2 * nb[k] + 2 * ng[k] + s * ns[k] + j] = plam[k][os + s * pns[k] + j];
+    }
+    return status;
+}

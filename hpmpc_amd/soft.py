@@ -40,13 +40,13 @@ class SoftQP:
         return int(self.nu[k] + self.nx[k])
 
     def ncv(self, k: int) -> int:
-        """length of lam[k] / t[k]"""
-        return 2 * rup(int(self.nb[k]), 4) + 4 * rup(int(self.ns[k]), 4)
+        """length of lam[k] / t[k]: [lower, upper (pnb) | general lower, upper (png) | 4 soft blocks (pns)]"""
+        return 2 * rup(int(self.nb[k]), 4) + 2 * rup(int(self.ng[k]), 4) + 4 * rup(int(self.ns[k]), 4)
 
     def copy(self) -> "SoftQP":
         cp = lambda L: [np.array(a, copy=True) for a in L]
         return SoftQP(self.N, self.nx.copy(), self.nu.copy(), self.nb.copy(), self.ns.copy(), cp(self.idxb),
-                      cp(self.BAbt), cp(self.RSQrq), cp(self.d), cp(self.Z), cp(self.z), self.ng.copy())
+                      cp(self.BAbt), cp(self.RSQrq), cp(self.d), cp(self.Z), cp(self.z), self.ng.copy(), cp(self.DCt))
 
     @staticmethod
     def from_case(case) -> "SoftQP":
@@ -55,7 +55,8 @@ class SoftQP:
         ns = np.asarray(case.inp["ns"][0], dtype=np.float64).astype(np.int32)
         return SoftQP(q.N, q.nx.copy(), q.nu.copy(), q.nb.copy(), ns, [a.copy() for a in q.idxb],
                       [a.copy() for a in q.BAbt], [a.copy() for a in q.RSQrq], [a.copy() for a in q.d],
-                      [a.copy() for a in case.inp["Z"]], [a.copy() for a in case.inp["z"]])
+                      [a.copy() for a in case.inp["Z"]], [a.copy() for a in case.inp["z"]], q.ng.copy(),
+                      [a.copy() for a in q.DCt])
 
     def alloc_solution(self):
         N = self.N

@@ -104,6 +104,13 @@ int d_ip2_mpc_soft_tv(int *kk, int k_max, double mu0, double mu_tol, double alph
                       int N, int *nx, int *nu, int *nb, int **idxb, int *ng, int *ns, double **pBAbt, double **pQ,
                       double **Z, double **z, double **pDCt, double **d, double **ux, int compute_mult, double **pi,
                       double **lam, double **t, double *double_work_memory);
+/* include/mpc_solvers.h:71 (mpc_solvers/d_res_ip_soft.c:38) -- r_q, r_b, r_d (hard | general | 2 soft blocks),
+ * r_z and mu of a soft-constraint iterate, with the reference's indexing (soft constraint i of stage k on
+ * ux[idxb[k][nu_k + i]]) and signs; general constraints allowed.  Entries the reference does not write keep the
+ * caller's values. */
+void d_res_mpc_soft_tv(int N, int *nx, int *nu, int *nb, int **idxb, int *ng, int *ns, double **hpBAbt, double **hpQ,
+                       double **hq, double **hZ, double **hz, double **hux, double **hpDCt, double **hd, double **hpi,
+                       double **hlam, double **ht, double **hrq, double **hrb, double **hrd, double **hrz, double *mu);
 /* include/mpc_solvers.h:36 (mpc_solvers/d_res_ip_hard.c:38) -- r_q, r_b, r_d and mu (no r_m) */
 void d_res_mpc_hard_tv(int N, int *nx, int *nu, int *nb, int **idxb, int *ng, double **hpBAbt, double **hb,
                        double **hpQ, double **hq, double **hux, double **hpDCt, double **hd, double **hpi,
@@ -166,6 +173,20 @@ int hpmpc_d_ip_ocp_hard_tv_work_space_size_bytes_noidxb(int N, int *nx, int *nu,
 /* include/c_interface.h:66 (interfaces/c/fortran_order_interface.c:690) -- k_max Newton steps from (ux0, pi0, lam0,
  * t0) with centering target mu0 on the full space; lam and t returned compact like the IPM wrapper's lam */
 int fortran_order_d_ip_ocp_hard_tv_single_newton_step(int *kk, int k_max, double mu0, double mu_tol, int N, int *nx, int *nu_N, int *nb, int **hidxb, int *ng, int N2, int warm_start, double **A, double **B, double **b, double **Q, double **S, double **R, double **q, double **r, double **lb, double **ub, double **C, double **D, double **lg, double **ug, double **x, double **u, double **pi, double **lam, double **t, double *inf_norm_res, void *work0, double *stat, double **ux0, double **pi0, double **lam0, double **t0);
+/* include/c_interface.h:70 (interfaces/c/c_interface_work_space.c:177) -- the reference's formula over this library's
+ * d_ip2_mpc_soft_tv work space */
+int hpmpc_d_ip_ocp_soft_tv_work_space_size_bytes(int N, int *nx, int *nu, int *nb, int **hidxb, int *ng, int *ns);
+/* include/c_interface.h:71 (interfaces/c/fortran_order_interface.c:1442) -- soft-constraint IPM wrapper: idxb / lb /
+ * ub list the nb hard boxes then the ns soft ones, Z / z = [lower (ns) | upper (ns)]; full space; lam returned as
+ * [lo nb | up nb | lg ng | ug ng | 4 soft blocks of ns].  As the reference's IPM sees it, z is not used (the
+ * reference never copies it, :1712-1719); inf_norm_res comes from d_res_mpc_soft_tv called as declared (the
+ * reference's call is shifted by one argument, :1880).  Limits of d_ip2_mpc_soft_tv apply. */
+int fortran_order_d_ip_ocp_soft_tv(int *kk, int k_max, double mu0, double mu_tol, int N, int *nx, int *nu_N, int *nb,
+                                   int **hidxb, int *ng, int *ns, int warm_start, double **A, double **B, double **b,
+                                   double **Q, double **S, double **R, double **q, double **r, double **Z, double **z,
+                                   double **lb, double **ub, double **C, double **D, double **lg, double **ug,
+                                   double **x, double **u, double **pi, double **lam, double *inf_norm_res,
+                                   void *work0, double *stat);
 /* include/c_interface.h:62 (interfaces/c/c_order_interface.c:53) */
 int c_order_d_ip_ocp_hard_tv(int *kk, int k_max, double mu0, double mu_tol, int N, int *nx, int *nu, int *nb,
                              int **hidxb, int *ng, int N2, int warm_start, double **A, double **B, double **b,

@@ -93,6 +93,10 @@ void orc_d_part_expand_solution(int N, int *nx, int *nu, int *nb, int **hidxb, i
 
 /* soft-constraint IPM (hpmpc_oracle_soft.c; mpc_solvers/d_ip2_soft.c:42-547) */
 int orc_soft_supported(int N, int *nx, int *nu, int *ng);
+void orc_d_res_mpc_soft_tv(int N, int *nx, int *nu, int *nb, int **idxb, int *ng, int *ns, double **hpBAbt,
+                           double **hpQ, double **hq, double **hZ, double **hz, double **hux, double **hpDCt,
+                           double **hd, double **hpi, double **hlam, double **ht, double **hrq, double **hrb,
+                           double **hrd, double **hrz, double *mu);
 int orc_d_ip2_mpc_soft_tv_work_space_size_bytes(int N, int *nx, int *nu, int *nb, int *ng, int *ns);
 int orc_d_ip2_mpc_soft_tv(int *kk, int k_max, double mu0, double mu_tol, double alpha_min, int warm_start,
                           double *stat, int N, int *nx, int *nu, int *nb, int **idxb, int *ng, int *ns,

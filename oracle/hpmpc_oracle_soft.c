@@ -415,3 +415,109 @@ int orc_d_ip2_mpc_soft_tv(int *kk, int k_max, double mu0, double mu_tol, double 
     if (alpha < alpha_min) return 2;
     return -1;
 }
+
+/* d_res_mpc_soft_tv (mpc_solvers/d_res_ip_soft.c:38-268): residuals r_q, r_b, r_d, r_z and mu of a soft-constraint
+ * iterate, restated with the reference's layout and quirks:
+ *   - soft constraint i of stage k acts on ux[idxb[k][nu_k + i]] (the reference indexes idxb past the nu_k
+ *     inputs, not past the nb_k hard boxes: :107-108, :134);
+ *   - its multipliers enter r_q as lam_0 - lam_1 on stages k < N (:134) but as -lam_2 + lam_3 on stage N (:220);
+ *   - on stage N r_q starts from pi_{N-1} - q on the state rows only (:199-200; the input rows, empty when
+ *     nu_N = 0, keep what the caller's vector holds) and its symv covers the leading nx_N x nx_N block (:204-207);
+ *   - mu = sum(lam t) over the hard, general and all four soft blocks / (2 (nb + ng + ns)) (:51-84, :231);
+ *   - r_q, r_b and r_d (hard, general and the first two soft blocks) change sign at the end (:237-264), r_z
+ *     does not.
+ * pi_{-1} (stage 0 with nx_0 > 0) is read as zero (the reference reads before hpi[0]). */
+void orc_d_res_mpc_soft_tv(int N, int *nx, int *nu, int *nb, int **idxb, int *ng, int *ns, double **hpBAbt,
+                           double **hpQ, double **hq, double **hZ, double **hz, double **hux, double **hpDCt,
+                           double **hd, double **hpi, double **hlam, double **ht, double **hrq, double **hrb,
+                           double **hrd, double **hrz, double *mu) {
+    double m = 0.0;
+    long ntot = 0;
+    for (int k = 0; k <= N; k++) {
+        const int nu0 = nu[k], nx0 = nx[k], nux = nu0 + nx0, cnux = rup(nux, NCL);
+        const int pnb = rup(nb[k], BS), png = rup(ng[k], BS), pns = rup(ns[k], BS), cng = rup(ng[k], NCL);
+        const int ob = 0, og = 2 * pnb, os = 2 * pnb + 2 * png;
+        const double *lam = hlam[k], *t = ht[k], *ux = hux[k], *d = hd[k];
+        double *rq = hrq[k], *rd = hrd[k];
+        ntot += nb[k] + ng[k] + ns[k];
+        for (int j = 0; j < nb[k]; j++) m += lam[ob + j] * t[ob + j] + lam[ob + pnb + j] * t[ob + pnb + j];
+        for (int j = 0; j < ng[k]; j++) m += lam[og + j] * t[og + j] + lam[og + png + j] * t[og + png + j];
+        for (int j = 0; j < ns[k]; j++)
+            for (int b = 0; b < 4; b++) m += lam[os + b * pns + j] * t[os + b * pns + j];
+        /* r_d */
+        for (int j = 0; j < nb[k]; j++) {
+            const double x = ux[idxb[k][j]];
+            rd[j] = x - d[j] - t[j];
+            rd[pnb + j] = -x + d[pnb + j] - t[pnb + j];
+        }
+        for (int j = 0; j < ng[k]; j++) {
+            double g = 0.0;
+            for (int i = 0; i < nux; i++) g += *P4(hpDCt[k], cng, i, j) * ux[i];
+            rd[og + j] = g - d[og + j] - t[og + j];
+            rd[og + png + j] = -g + d[og + png + j] - t[og + png + j];
+        }
+        for (int j = 0; j < ns[k]; j++) {
+            const double x = ux[idxb[k][nu0 + j]];
+            rd[os + j] = t[os + 2 * pns + j] + x - d[os + j] - t[os + j];
+            rd[os + pns + j] = t[os + 3 * pns + j] - x + d[os + pns + j] - t[os + pns + j];
+        }
+        /* r_q */
+        const int nsym = k < N ? nux : nx0;
+        if (k < N)
+            for (int i = 0; i < nu0; i++) rq[i] = -hq[k][i];
+        for (int i = 0; i < nx0; i++) rq[nu0 + i] = -hq[k][nu0 + i] + (k > 0 ? hpi[k - 1][i] : 0.0);
+        if (k == N)
+            for (int j = 0; j < nb[k]; j++) rq[idxb[k][j]] += lam[j] - lam[pnb + j];
+        for (int i = 0; i < nsym; i++) {
+            double s = 0.0;
+            for (int j = 0; j < nsym; j++) s += (i >= j ? *P4(hpQ[k], cnux, i, j) : *P4(hpQ[k], cnux, j, i)) * ux[j];
+            rq[i] -= s;
+        }
+        if (k < N)
+            for (int j = 0; j < nb[k]; j++) rq[idxb[k][j]] += lam[j] - lam[pnb + j];
+        for (int i = 0; i < nux; i++) {
+            double s = 0.0;
+            for (int j = 0; j < ng[k]; j++) s += *P4(hpDCt[k], cng, i, j) * (lam[og + j] - lam[og + png + j]);
+            rq[i] += s;
+        }
+        for (int j = 0; j < ns[k]; j++)
+            rq[idxb[k][nu0 + j]] += k < N ? lam[os + j] - lam[os + pns + j] : -lam[os + 2 * pns + j] + lam[os + 3 * pns + j];
+        if (k < N) {
+            const int nx1 = nx[k + 1], nu1 = nu[k + 1], cnx1 = rup(nx1, NCL);
+            for (int j = 0; j < nx1; j++) {
+                double s = 0.0;
+                for (int i = 0; i < nux; i++) s += *P4(hpBAbt[k], cnx1, i, j) * ux[i];
+                hrb[k][j] = hux[k + 1][nu1 + j] - *P4(hpBAbt[k], cnx1, nux, j) - s;
+            }
+            for (int i = 0; i < nux; i++) {
+                double s = 0.0;
+                for (int j = 0; j < nx1; j++) s += *P4(hpBAbt[k], cnx1, i, j) * hpi[k][j];
+                rq[i] -= s;
+            }
+        }
+        /* r_z */
+        for (int j = 0; j < ns[k]; j++) {
+            hrz[k][j] = hz[k][j] + hZ[k][j] * t[os + 2 * pns + j] - lam[os + j] - lam[os + 2 * pns + j];
+            hrz[k][pns + j] = hz[k][pns + j] + hZ[k][pns + j] * t[os + 3 * pns + j] - lam[os + pns + j] - lam[os + 3 * pns + j];
+        }
+    }
+    *mu = ntot != 0 ? m / (2.0 * ntot) : 0.0;
+    for (int k = 0; k <= N; k++) {
+        const int pnb = rup(nb[k], BS), png = rup(ng[k], BS), pns = rup(ns[k], BS), os = 2 * pnb + 2 * png;
+        for (int i = 0; i < nu[k] + nx[k]; i++) hrq[k][i] = -hrq[k][i];
+        if (k < N)
+            for (int j = 0; j < nx[k + 1]; j++) hrb[k][j] = -hrb[k][j];
+        for (int j = 0; j < nb[k]; j++) {
+            hrd[k][j] = -hrd[k][j];
+            hrd[k][pnb + j] = -hrd[k][pnb + j];
+        }
+        for (int j = 0; j < ng[k]; j++) {
+            hrd[k][2 * pnb + j] = -hrd[k][2 * pnb + j];
+            hrd[k][2 * pnb + png + j] = -hrd[k][2 * pnb + png + j];
+        }
+        for (int j = 0; j < ns[k]; j++) {
+            hrd[k][os + j] = -hrd[k][os + j];
+            hrd[k][os + pns + j] = -hrd[k][os + pns + j];
+        }
+    }
+}

@@ -224,6 +224,10 @@ def to_flat(P):
     for key in ("A", "B", "Q", "S", "R", "C", "D", "b", "q", "r", "lb", "ub", "lg", "ug"):
         out["P_" + key] = [np.asarray(M, dtype=np.float64).reshape(-1) for M in P[key]]
     out["P_hidxb"] = [np.asarray(i, dtype=np.float64) for i in P["hidxb"]]
+    if "ns" in P:  # soft constraints
+        out["P_Z"] = [np.asarray(v, dtype=np.float64) for v in P["Z"]]
+        out["P_z"] = [np.asarray(v, dtype=np.float64) for v in P["z"]]
+        out["P_ns"] = [np.asarray(P["ns"], dtype=np.float64)]
     return out
 
 
@@ -235,4 +239,124 @@ def from_flat(N, nx, nu, nb, ng, inp):
     P["hidxb"] = [np.array(v).astype(np.int32) for v in inp["P_hidxb"]]
     for key, shp in SHAPES.items():
         P[key] = [np.array(v).reshape(shp(P, k)) for k, v in enumerate(inp["P_" + key])]
+    if "P_ns" in inp:
+        P["ns"] = [int(v) for v in inp["P_ns"][0]]
+        P["Z"] = [np.array(v) for v in inp["P_Z"]]
+        P["z"] = [np.array(v) for v in inp["P_z"]]
     return P
+
+
+# ------------------------------------------------------------------------------------------------- soft constraints
+def random_soft_iface_problem(N, nx, nu, seed=0, Zq=0.5, zl=10.0):
+    """Random soft-constrained OCP in interface form, in the reference driver's shape (test_d_ip_soft.c): hard
+    boxes on every input of stages 0..N-1 (nb = nu), soft boxes on every state of stages 1..N (ns = nx), penalties
+    Z = Zq, z = zl; x0 is stage 0's affine term (nx[0] = 0)."""
+    rng = np.random.default_rng(seed)
+    nxv = [0] + [nx] * N
+    nuv = [nu] * N + [0]
+    P = dict(N=N, nx=nxv, nu=nuv, ng=[0] * (N + 1), A=[], B=[], b=[], Q=[], S=[], R=[], q=[], r=[], lb=[], ub=[],
+             hidxb=[], nb=[], ns=[], Z=[], z=[], C=[], D=[], lg=[], ug=[])
+    x0 = 2.0 * rng.standard_normal(nx)
+    for k in range(N + 1):
+        nxk, nuk = nxv[k], nuv[k]
+        if k < N:
+            A = np.eye(nx) + 0.1 * rng.standard_normal((nx, nx)) / np.sqrt(nx)
+            B = rng.standard_normal((nx, nuk)) / np.sqrt(max(nuk, 1))
+            P["A"].append(A[:, :nxk].copy())
+            P["B"].append(B)
+            P["b"].append(A @ x0 if k == 0 else 0.05 * rng.standard_normal(nx))
+        G = rng.standard_normal((nxk + nuk, nxk + nuk))
+        H = 0.5 * G @ G.T / max(nxk + nuk, 1) + 0.5 * np.eye(nxk + nuk)
+        P["R"].append(H[:nuk, :nuk].copy())
+        P["S"].append(H[:nuk, nuk:].copy())
+        P["Q"].append(H[nuk:, nuk:].copy())
+        P["r"].append(0.2 * rng.standard_normal(nuk))
+        P["q"].append(0.2 * rng.standard_normal(nxk))
+        nbk, nsk = nuk, (nxk if k > 0 else 0)
+        P["hidxb"].append(np.r_[np.arange(nbk), nuk + np.arange(nsk)].astype(np.int32))
+        P["nb"].append(nbk)
+        P["ns"].append(nsk)
+        P["lb"].append(np.r_[-(0.5 + rng.random(nbk)), -(0.8 + 0.4 * rng.random(nsk))])
+        P["ub"].append(np.r_[0.5 + rng.random(nbk), 0.8 + 0.4 * rng.random(nsk)])
+        P["Z"].append(np.full(2 * nsk, Zq))
+        P["z"].append(np.full(2 * nsk, zl))
+        P["C"].append(np.zeros((0, nxk)))
+        P["D"].append(np.zeros((0, nuk)))
+        P["lg"].append(np.zeros(0))
+        P["ug"].append(np.zeros(0))
+    return P
+
+
+def to_soft_qp(P):
+    """Interface form -> the SoftQP fortran_order_d_ip_ocp_soft_tv packs (interfaces/c/fortran_order_interface.c:
+    1653-1799): the hard OCP blocks as to_qp, Z[k] = [lower | upper] padded to pns, d = [lb | ub | lg | ug | ls | us]
+    with the soft bounds read at lb[k][nb + i] / ub[k][nb + i].  z is NOT packed: the reference wrapper never copies
+    z into its hz (:1712-1719 fill hZ only), so the IPM sees the zeros of a zeroed work0."""
+    from hpmpc_amd.soft import SoftQP
+
+    N = P["N"]
+    hard = dict(P, lb=[P["lb"][k][:P["nb"][k]] for k in range(N + 1)], ub=[P["ub"][k][:P["nb"][k]] for k in range(N + 1)],
+                hidxb=[P["hidxb"][k][:P["nb"][k]] for k in range(N + 1)])
+    qp = to_qp(hard)
+    Z, z, d = [], [], []
+    for k in range(N + 1):
+        nb, ng, ns = P["nb"][k], P["ng"][k], P["ns"][k]
+        pnb, png, pns = rup(nb, 4), rup(ng, 4), rup(ns, 4)
+        Zk = np.zeros(2 * pns + 4)
+        Zk[:ns] = P["Z"][k][:ns]
+        Zk[pns:pns + ns] = P["Z"][k][ns:2 * ns]
+        Z.append(Zk)
+        z.append(np.zeros(2 * pns + 4))
+        dk = np.zeros(2 * pnb + 2 * png + 2 * pns + 4)
+        dk[:2 * pnb + 2 * png] = qp.d[k][:2 * pnb + 2 * png]
+        dk[2 * pnb + 2 * png:2 * pnb + 2 * png + ns] = P["lb"][k][nb:nb + ns]
+        dk[2 * pnb + 2 * png + pns:2 * pnb + 2 * png + pns + ns] = P["ub"][k][nb:nb + ns]
+        d.append(dk)
+    idxb = [np.ascontiguousarray(i, dtype=np.int32) for i in P["hidxb"]]
+    return SoftQP(N, qp.nx.copy(), qp.nu.copy(), qp.nb.copy(), np.array(P["ns"], np.int32), idxb, qp.BAbt,
+                  qp.RSQrq, d, Z, z, qp.ng.copy(), qp.DCt)
+
+
+def ip_ocp_soft(api, P, k_max=50, mu0=100.0, mu_tol=1e-8, warm=None):
+    """fortran_order_d_ip_ocp_soft_tv (interfaces/c/fortran_order_interface.c:1442-1971): pack (to_soft_qp), mu0 <= 0
+    -> the largest entry of R, S, Q, r, q, Z, z (:1723-1740, no absolute value), d_ip2_mpc_soft_tv on the full
+    space, then the residuals d_res_mpc_soft_tv and their infinity norms (:1876-1924) and the compact outputs
+    (u, x, pi, lam = [lo nb | up nb | lg ng | ug ng | 4 soft blocks of ns]).  The reference wrapper passes its
+    residual call's arguments shifted by one (an extra hb after hpBAbt, no hrz: :1880 vs mpc_solvers.h:71), so
+    its inf_norm_res is computed on scrambled inputs; this composition (and the product) calls it as declared."""
+    N, nx, nu, nb, ng, ns = P["N"], P["nx"], P["nu"], P["nb"], P["ng"], P["ns"]
+    sq = to_soft_qp(P)
+    if mu0 <= 0:
+        m = 0.0
+        for k in range(N + 1):
+            keys = ("R", "S", "Q", "r", "q", "Z", "z") if k < N else ("Q", "q", "Z", "z")
+            for key in keys:
+                a = np.asarray(P[key][k])
+                if a.size:
+                    m = max(m, float(a.max()))
+        mu0 = m
+    kw = {}
+    if warm is not None:
+        kw = dict(warm_start=1, ux=[np.r_[warm["u"][k] if k < N else [], warm["x"][k]] for k in range(N + 1)])
+    r = api.ipm_soft(sq.copy(), k_max=k_max, mu0=mu0, mu_tol=mu_tol, alpha_min=1e-8, work_extra=1 << 16, **kw)
+    ux, pi, lam, t = r["ux"], r["pi"], r["lam"], r["t"]
+    q = [np.r_[P["r"][k] if k < N else [], P["q"][k], np.zeros(8)] for k in range(N + 1)]
+    res = api.residuals_soft(sq, q, ux, pi, lam, t)
+    n0 = max(abs(res["rq"][0][0]), max(float(np.max(np.abs(res["rq"][k][:nu[k] + nx[k]]), initial=0)) for k in range(N)),
+             float(np.max(np.abs(res["rq"][N][:nx[N]]), initial=0)))
+    n1 = max(abs(res["rb"][0][0]), max(float(np.max(np.abs(res["rb"][k][:nx[k + 1]]), initial=0)) for k in range(N)))
+    n2 = abs(res["rd"][0][0])
+    lam_c = []
+    for k in range(N + 1):
+        pnb, png, pns = rup(nb[k], 4), rup(ng[k], 4), rup(ns[k], 4)
+        o = 2 * pnb + 2 * png
+        idx = np.r_[0:nb[k], pnb:pnb + nb[k], 2 * pnb:2 * pnb + ng[k], 2 * pnb + png:2 * pnb + png + ng[k],
+                    o:o + ns[k], o + pns:o + pns + ns[k]].astype(int)
+        if idx.size:
+            n2 = max(n2, float(np.max(np.abs(res["rd"][k][idx]))))
+        lam_c.append(np.concatenate([lam[k][:nb[k]], lam[k][pnb:pnb + nb[k]], lam[k][2 * pnb:2 * pnb + ng[k]],
+                                     lam[k][2 * pnb + png:2 * pnb + png + ng[k]]] +
+                                    [lam[k][o + s * pns:o + s * pns + ns[k]] for s in range(4)]))
+    return dict(u=[np.array(ux[k][:nu[k]]) for k in range(N)], x=[np.array(ux[k][nu[k]:nu[k] + nx[k]]) for k in range(N + 1)],
+                pi=[np.array(pi[k][:nx[k + 1]]) for k in range(N)], lam=lam_c,
+                inf_norm_res=np.array([n0, n1, n2, res["mu"]]), status=r["ret"], kk=r["kk"], stat=r["stat"])

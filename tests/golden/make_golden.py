@@ -26,7 +26,7 @@ from hpmpc_amd.ocp import (BS, OCPQP, lib4_size, mass_spring_qp, pack_lib4, rup,
                            unpack_lib4)
 
 sys.path.insert(0, os.path.dirname(HERE))
-from helpers import COND_FILL, sub_block  # noqa: E402
+from helpers import COND_FILL, sub_block, xclamp_qp  # noqa: E402
 
 
 def ref_api():
@@ -221,7 +221,10 @@ def main():
     alt(ref, ref_avx_api(), rng, out)
     pcond(ref, out)
     cond_parts(ref, out)
+    xclamp(ref, out)
+    soft_res(ref, out)
     iface(ref, out)
+    iface_soft(ref, out)
     wide(ref, ref_avx_api(), out)
     divergent(ref, out)
     driver(out)
@@ -309,6 +312,60 @@ def cond_parts(ref, out):
                              outs))
 
 
+def xclamp(ref, out):
+    """The reference clamping an inner-stage x pivot (kernel_dpotrf_c99_lib4.c:555-640): helpers.xclamp_qp puts
+    an exact pivot d <= 1e-15 with nonzero cross terms on state 0 of every stage k >= 1.  The clamp zeroes that
+    column of Lxx, so the cost-to-go the reference carries loses the pivot's rank-one term (entries d and `off`:
+    solution change ~off) and, through l_x, the gradient along it (change ~r).  The P form carries the cost-to-go
+    itself and solves the QP exactly; these pin what the reference does instead (kind sv_xclamp)."""
+    for name, kw in (("r0", dict(d=1e-16, off=1e-9, r=0.0)), ("r05", dict(d=1e-16, off=1e-9, r=0.5))):
+        qp = xclamp_qp(**kw)
+        ux, pi, Pb, _ = ref.ric_sv(qp.copy(), compute_pi=1, compute_Pb=1)
+        out.append(save_case(f"sv_xclamp_{name}_N10_nx8_nu3", "sv_xclamp", qp, dict(compute_pi=1, compute_Pb=1, **kw),
+                             dict(ux=ux, pi=pi, Pb=Pb)))
+
+
+def soft_res(ref, out):
+    """d_res_mpc_soft_tv (mpc_solvers/d_res_ip_soft.c:38) at random iterates (t, lam > 0) of soft problems: the
+    driver's shape (nb = nu: the soft index idxb[nu + i] is the soft box), hard boxes at stage N (nu_N = 0: the
+    soft index reads the hard entries, as the reference does), and general constraints on the inner stages."""
+    from hpmpc_amd.soft import mass_spring_soft
+
+    rng = np.random.default_rng(20261017)
+
+    def with_general(sq, ng=2):
+        sq.ng = np.array([0] + [ng] * (sq.N - 1) + [0], dtype=np.int32)
+        sq.DCt = [np.zeros(8)] * (sq.N + 1)
+        for k in range(1, sq.N):
+            nb, ns, pnb, pns, png = int(sq.nb[k]), int(sq.ns[k]), rup(int(sq.nb[k]), 4), rup(int(sq.ns[k]), 4), rup(ng, 4)
+            sq.DCt[k] = pack_lib4(rng.standard_normal((sq.nux(k), ng)))
+            d = np.zeros(2 * pnb + 2 * png + 2 * pns + 4)
+            d[:2 * pnb] = sq.d[k][:2 * pnb]
+            d[2 * pnb:2 * pnb + ng] = -1.0
+            d[2 * pnb + png:2 * pnb + png + ng] = 1.0
+            d[2 * pnb + 2 * png:2 * pnb + 2 * png + 2 * pns] = sq.d[k][2 * pnb:2 * pnb + 2 * pns]
+            sq.d[k] = d
+        return sq
+
+    cases = [("ms_N10_nx8_nu3", mass_spring_soft(10, 8, 3, Q_diag=1.0, Zq=0.5)),
+             ("hardN_N12_nx8_nu2", mass_spring_soft(12, 8, 2, hard_last=2, time_variant=True, seed=3)),
+             ("ng_N8_nx6_nu2", with_general(mass_spring_soft(8, 6, 2, Q_diag=0.5)))]
+    for name, sq in cases:
+        N = sq.N
+        ux, pi, lam, t = sq.alloc_solution()
+        for k in range(N + 1):
+            ux[k][:sq.nux(k)] = rng.standard_normal(sq.nux(k))
+            lam[k][:sq.ncv(k)] = 0.1 + rng.random(sq.ncv(k))
+            t[k][:sq.ncv(k)] = 0.1 + rng.random(sq.ncv(k))
+            if k < N:
+                pi[k][:int(sq.nx[k + 1])] = rng.standard_normal(int(sq.nx[k + 1]))
+        q = [np.concatenate([rng.standard_normal(sq.nux(k)), np.zeros(8)]) for k in range(N + 1)]
+        r = ref.residuals_soft(sq.copy(), q, ux, pi, lam, t)
+        out.append(save_case(f"softres_{name}", "soft_res", sq, {}, dict(rq=r["rq"], rb=r["rb"], rd=r["rd"],
+                             rz=r["rz"], mu=r["mu"]), extra=dict(ns=[sq.ns.astype(np.float64)], Z=sq.Z, z=sq.z, q=q,
+                                                                  ux=ux, pi=pi, lam=lam, t=t)))
+
+
 def iface(ref, out):
     """High-level wrappers of include/c_interface.h, restated by oracle/iface_oracle.py over the reference's own
     low-level entry points (the reference wrapper sources need the generated include/target.h and are
@@ -353,6 +410,24 @@ def iface(ref, out):
     out.append(save_case("iface_kkt_N10_nx4_nu2", "iface_kkt", IO.to_qp(P), dict(mu0=2.0, mu_tol=1e-10, k_max=50),
                          dict(u=k["u"], x=k["x"], pi=k["pi"], lam=k["lam"], inf_norm_res=k["inf_norm_res"]),
                          extra=extra))
+
+
+def iface_soft(ref, out):
+    """fortran_order_d_ip_ocp_soft_tv (interfaces/c/fortran_order_interface.c:1442) restated by
+    oracle/iface_oracle.py ip_ocp_soft over the reference's d_ip2_mpc_soft_tv and d_res_mpc_soft_tv: the driver's
+    shape (hard input boxes, soft state boxes), a fixed and the cost-based mu0, stopped at mu_tol 1e-6 (the soft end
+    game is rounding-sensitive, DESIGN.md)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import iface_oracle as IO
+
+    for name, (N, nx, nu, seed), mu0 in (("N12_nx8_nu3", (12, 8, 3, 12), 100.0), ("automu0_N10_nx4_nu1", (10, 4, 1, 10), -1.0),
+                                         ("N8_nx12_nu4", (8, 12, 4, 8), 50.0)):
+        P = IO.random_soft_iface_problem(N, nx, nu, seed=seed)
+        r = IO.ip_ocp_soft(ref, P, k_max=50, mu0=mu0, mu_tol=1e-6)
+        outs = dict(u=r["u"], x=r["x"], pi=r["pi"], lam=r["lam"], inf_norm_res=r["inf_norm_res"], kk=r["kk"],
+                    ret=r["status"], stat=r["stat"])
+        out.append(save_case(f"iface_soft_{name}", "iface_soft", IO.to_soft_qp(P), dict(mu0=mu0, mu_tol=1e-6, k_max=50),
+                             outs, extra=IO.to_flat(P)))
 
 
 def wide(ref, refa, out):
@@ -547,6 +622,18 @@ if __name__ == "__main__":
         o = []
         divergent(ref_api(), o)
         print(f"wrote {len(o)} divergent cases, {sum(os.path.getsize(p) for p in o) / 1e6:.2f} MB")
+    elif len(sys.argv) > 1 and sys.argv[1] == "iface_soft":
+        o = []
+        iface_soft(ref_api(), o)
+        print(f"wrote {len(o)} iface_soft cases")
+    elif len(sys.argv) > 1 and sys.argv[1] == "soft_res":
+        o = []
+        soft_res(ref_api(), o)
+        print(f"wrote {len(o)} soft_res cases")
+    elif len(sys.argv) > 1 and sys.argv[1] == "xclamp":
+        o = []
+        xclamp(ref_api(), o)
+        print(f"wrote {len(o)} xclamp cases")
     elif len(sys.argv) > 1 and sys.argv[1] == "cond_parts":
         o = []
         cond_parts(ref_api(), o)

@@ -20,7 +20,7 @@ def run_case(api, case):
     qp = case.fresh_qp()
     a = case.args
     inp = case.inp
-    if case.kind == "sv":
+    if case.kind in ("sv", "sv_xclamp"):
         kw = {}
         if a.get("update_b"):
             kw.update(update_b=1, b=inp["b"], update_q=1, q=inp["q"], bd=inp["bd"], Qx=inp["Qx"], qx=inp["qx"])
@@ -66,6 +66,10 @@ def run_case(api, case):
         return dict(cqp=c, ux=e["ux"], pi=e["pi"], lam=e["lam"], t=e["t"])
     if case.kind == "pcond_sv":
         return pcond_sv(api, qp, int(a["N2"]))
+    if case.kind == "soft_res":
+        from hpmpc_amd.soft import SoftQP
+
+        return api.residuals_soft(SoftQP.from_case(case), inp["q"], inp["ux"], inp["pi"], inp["lam"], inp["t"])
     if case.kind == "cond_parts":
         # each building block alone; RSQrq and DCtd on the reference's own Gammas
         f = a["fill"]
@@ -73,7 +77,7 @@ def run_case(api, case):
         R2 = api.cond_RSQrq(qp.copy(), case.out["Gamma"], fill=f)
         DCt2, d2, idxb2, _ = api.cond_DCtd(qp.copy(), case.out["Gamma"], fill=f)
         return dict(Gamma=G, BAbt2=B2, RSQrq2=R2, DCt2=DCt2, d2=d2, idxb2=idxb2)
-    if case.kind in ("iface", "iface_kkt", "iface_newton"):
+    if case.kind in ("iface", "iface_kkt", "iface_newton", "iface_soft"):
         return run_iface(api, case)
     if case.kind == "soft":
         from hpmpc_amd.soft import SoftQP
@@ -101,6 +105,12 @@ def run_iface(api, case, order="F"):
     qp, a = case.qp, case.args
     P = IO.from_flat(qp.N, qp.nx, qp.nu, qp.nb, qp.ng, case.inp)
     kw = dict(k_max=int(a["k_max"]), mu0=a["mu0"], mu_tol=a["mu_tol"])
+    if case.kind == "iface_soft":
+        r = api.ip_ocp_soft(P, **kw) if hasattr(api.lib, api.p + "fortran_order_d_ip_ocp_soft_tv") else \
+            IO.ip_ocp_soft(api, P, **kw)
+        out = {k: r[k] for k in ("u", "x", "pi", "lam", "inf_norm_res", "kk", "stat")}
+        out["ret"] = r["status"]
+        return out
     has = hasattr(api.lib, api.p + "fortran_order_d_ip_ocp_hard_tv")
     if case.kind == "iface":
         r = api.ip_ocp(P, int(a["N2"]), order=order, **kw) if has else IO.ip_ocp(api, P, int(a["N2"]), **kw)
@@ -128,6 +138,17 @@ def run_iface(api, case, order="F"):
 
 def check_iface(case, got):
     out = case.out
+    if case.kind == "iface_soft":  # the soft IPM's gates (TOL_SOFT); residual norms at its mu_tol 1e-6
+        assert int(got["kk"]) == int(out["kk"]) and int(got["ret"]) == int(out["ret"]), (case.name, got["kk"], out["kk"])
+        np.testing.assert_allclose(got["stat"], out["stat"], rtol=TOL_SOFT["stat"], atol=1e-14, err_msg=case.name)
+        for key, tol in (("u", TOL_SOFT["ux"]), ("x", TOL_SOFT["ux"]), ("pi", TOL_SOFT["pi"]), ("lam", TOL_SOFT["lam"])):
+            for k, (g, r) in enumerate(zip(got[key], out[key])):
+                g, r = np.asarray(g), np.asarray(r)
+                if r.size:
+                    e = float(np.max(np.abs(g - r) / np.maximum(1.0, np.abs(r))))
+                    assert e <= tol, f"{case.name}: {key}[{k}] err {e:.3e}"
+        np.testing.assert_allclose(got["inf_norm_res"], out["inf_norm_res"], rtol=0, atol=1e-7, err_msg=case.name)
+        return
     if "kk" in out:
         assert int(got["kk"]) == int(out["kk"]) and int(got["ret"]) == int(out["ret"]), (case.name, got["kk"], out["kk"])
         np.testing.assert_allclose(got["stat"], out["stat"], rtol=TOL_STAT, atol=1e-14, err_msg=case.name)
@@ -271,6 +292,68 @@ def sub_block(qp, s0: int, T: int):
 COND_FILL = 7.25  # sentinel pre-filled into every output: what the reference leaves alone stays 7.25
 
 
+def dense_kkt(qp):
+    """The exact solution of an OCP QP without inequality constraints from its dense KKT system (numpy LU):
+    ux_k and pi_k with the reference's sign (pi_k = the gradient of the cost-to-go at x_{k+1})."""
+    from hpmpc_amd.ocp import unpack_lib4
+
+    N = qp.N
+    sizes = [qp.nux(k) for k in range(N + 1)]
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(int)
+    n = int(off[-1])
+    H, g = np.zeros((n, n)), np.zeros(n)
+    for k in range(N + 1):
+        m = sizes[k]
+        M = unpack_lib4(qp.RSQrq[k], m + 1, m)
+        L = np.tril(M[:m])
+        H[off[k]:off[k + 1], off[k]:off[k + 1]] = L + np.tril(L, -1).T
+        g[off[k]:off[k + 1]] = M[m]
+    ncon = sum(int(qp.nx[k + 1]) for k in range(N))
+    Cm, c, r0 = np.zeros((ncon, n)), np.zeros(ncon), 0
+    for k in range(N):
+        m, nx1, nu1 = sizes[k], int(qp.nx[k + 1]), int(qp.nu[k + 1])
+        Bt = unpack_lib4(qp.BAbt[k], m + 1, nx1)
+        Cm[r0:r0 + nx1, off[k]:off[k + 1]] = -Bt[:m].T
+        Cm[r0:r0 + nx1, off[k + 1] + nu1:off[k + 1] + nu1 + nx1] = np.eye(nx1)
+        c[r0:r0 + nx1] = Bt[m]
+        r0 += nx1
+    K = np.block([[H, Cm.T], [Cm, np.zeros((ncon, ncon))]])
+    sol = np.linalg.solve(K, np.concatenate([-g, c]))
+    z, lam = sol[:n], sol[n:]
+    ux = [z[off[k]:off[k + 1]] for k in range(N + 1)]
+    pi, r0 = [], 0
+    for k in range(N):
+        nx1 = int(qp.nx[k + 1])
+        pi.append(-lam[r0:r0 + nx1])
+        r0 += nx1
+    return ux, pi
+
+
+def xclamp_qp(N=10, nx=8, nu=3, d=1e-16, off=1e-9, r=0.0):
+    """State 0 of every stage k >= 1 has Hessian diagonal d <= 1e-15, cross terms `off` with the other states,
+    gradient r and no effect on the next state (its A' row is zero), so the first x pivot of the reference's
+    stage Cholesky is exactly d and is clamped (kernel_dpotrf_c99_lib4.c:555-640) while the stage Hessian stays
+    positive semidefinite (off^2 <= d Q_ll)."""
+    from hpmpc_amd.ocp import mass_spring_qp, pack_lib4, unpack_lib4
+
+    qp = mass_spring_qp(N, nx, nu, boxes=False)
+    for k in range(1, N + 1):
+        nuk, nux = int(qp.nu[k]), qp.nux(k)
+        M = unpack_lib4(qp.RSQrq[k], nux + 1, nux).copy()
+        j = nuk
+        M[j, :] = 0.0
+        M[:, j] = 0.0
+        M[j, j] = d
+        M[j + 1:nux, j] = off
+        M[nux, j] = r
+        qp.RSQrq[k] = pack_lib4(M)
+        if k < N:
+            Bt = unpack_lib4(qp.BAbt[k], nux + 1, int(qp.nx[k + 1])).copy()
+            Bt[j, :] = 0.0
+            qp.BAbt[k] = pack_lib4(Bt)
+    return qp
+
+
 def _check_written(name, got, ref, fill, tol):
     """Same elements written (the rest still holds the pre-filled sentinel), written values within tol."""
     got, ref = np.asarray(got)[: len(ref)], np.asarray(ref)
@@ -308,15 +391,41 @@ def check_cond_parts(case, got):
     assert np.all(flat_g[: flat_r.size][pad & (flat_r == f)] == f), case.name
 
 
+def check_soft_res(case, got):
+    """d_res_mpc_soft_tv: r_q / r_b on the stage sizes, r_d on its hard, general and first two soft blocks,
+    r_z on its two soft blocks, mu; 1e-12 relative to max(1, |ref|) (residuals)."""
+    from hpmpc_amd.soft import SoftQP
+
+    sq, out = SoftQP.from_case(case), case.out
+    rel = lambda g, r: float(np.max(np.abs(np.asarray(g) - r) / np.maximum(1.0, np.abs(r)), initial=0.0))
+    for k in range(sq.N + 1):
+        n = sq.nux(k)
+        assert rel(got["rq"][k][:n], out["rq"][k][:n]) <= TOL_RIC, (case.name, "rq", k)
+        if k < sq.N:
+            m = int(sq.nx[k + 1])
+            assert rel(got["rb"][k][:m], out["rb"][k][:m]) <= TOL_RIC, (case.name, "rb", k)
+        nb, ng, ns = int(sq.nb[k]), int(sq.ng[k]), int(sq.ns[k])
+        pnb, png, pns = (nb + 3) // 4 * 4, (ng + 3) // 4 * 4, (ns + 3) // 4 * 4
+        os_ = 2 * pnb + 2 * png
+        idx = np.r_[0:nb, pnb:pnb + nb, 2 * pnb:2 * pnb + ng, 2 * pnb + png:2 * pnb + png + ng, os_:os_ + ns,
+                    os_ + pns:os_ + pns + ns].astype(int)
+        assert rel(np.asarray(got["rd"][k])[idx], out["rd"][k][idx]) <= TOL_RIC, (case.name, "rd", k)
+        iz = np.r_[0:ns, pns:pns + ns].astype(int)
+        assert rel(np.asarray(got["rz"][k])[iz], out["rz"][k][iz]) <= TOL_RIC, (case.name, "rz", k)
+    assert abs(got["mu"] - float(out["mu"])) <= TOL_RIC * max(1.0, abs(float(out["mu"]))), case.name
+
+
 def check_case(case, got):
     """Assert parity of `got` against the golden outputs of `case`."""
+    if case.kind == "soft_res":
+        return check_soft_res(case, got)
     if case.kind == "cond_parts":
         return check_cond_parts(case, got)
     if case.kind == "soft":
         return check_soft(case, got)
     if case.kind == "pcond":
         return check_pcond(case, got)
-    if case.kind in ("iface", "iface_kkt", "iface_newton"):
+    if case.kind in ("iface", "iface_kkt", "iface_newton", "iface_soft"):
         return check_iface(case, got)
     if case.kind == "ipm_div":
         # a diverging infeasible problem: only ret and kk to +-2 are comparable (the reference and a second c99
@@ -334,7 +443,7 @@ def check_case(case, got):
     if "kk" in out:
         assert int(got["kk"]) == int(out["kk"]), (case.name, got["kk"], out["kk"])
         assert int(got["ret"]) == int(out["ret"]), (case.name, got["ret"], out["ret"])
-    tol = TOL_RIC if case.kind in ("sv", "trf_trs", "res", "res2") else TOL_IPM
+    tol = TOL_RIC if case.kind in ("sv", "sv_xclamp", "trf_trs", "res", "res2") else TOL_IPM
     per_key = {}
     if case.kind == "ipm2":
         per_key = TOL_IPM2_TIGHT if case.args["mu_tol"] < 1e-8 and int(out["kk"]) < case.args["k_max"] else TOL_IPM2
