@@ -17,6 +17,8 @@
 // restatement is oracle/hpmpc_oracle.c ipm_core); each pass below names the reference routine it restates.
 #include <hip/hip_runtime.h>
 
+#include "hk_launch_guard.h"
+
 #include "hk_wide_core.h"
 
 namespace {
@@ -641,6 +643,9 @@ __global__ __launch_bounds__(WT) void hk_wide_ipm(WideIpmArgs A) {
 
 extern "C" int hk_wide_ipm_launch(const WideIpmArgs* a, int count, int lds_doubles, hipStream_t stream) {
     if (count <= 0) return 0;
+    // scratch / LDS need against what the device reserves (round-2 noinline-build fault)
+    static const HkKernelLimits lim(reinterpret_cast<const void*>(&hk_wide_ipm));
+    if (const int g = lim.check((size_t)lds_doubles * sizeof(double), WT)) return g;
     hipLaunchKernelGGL(hk_wide_ipm, dim3(count), dim3(WT), (size_t)lds_doubles * sizeof(double), stream, *a);
     return (int)hipGetLastError();
 }

@@ -235,8 +235,8 @@ bool run(const WIpm& W, const Stage& S, const WideIpmArgs& a) {
     const int e = hk_wide_ipm_launch(&a, 1, W.L.lds + 8, g_w.stream);
     if (e) {
         char msg[96];
-        snprintf(msg, sizeof msg, "hk_wide_ipm launch failed (%d)", e);
-        hk_set_error(HPMPC_MI355X_EHIP, msg);
+        snprintf(msg, sizeof msg, "hk_wide_ipm launch %s (%d)", e == -2 ? "refused: scratch / LDS beyond the limits" : "failed", e);
+        hk_set_error(e == -2 ? HPMPC_MI355X_EUNSUPPORTED : HPMPC_MI355X_EHIP, msg);
         return false;
     }
     return g_w.down(S.total);
@@ -555,9 +555,10 @@ extern "C" int hpmpc_mi355x_wide_ipm_batch(const hpmpc_mi355x_wide_plan* q, int 
     const int e = hk_wide_ipm_launch(&a, count, L.lds + 8, (hipStream_t)stream);
     if (e) {
         char msg[96];
-        snprintf(msg, sizeof msg, "hk_wide_ipm launch failed (%d)", e);
-        hk_set_error(HPMPC_MI355X_EHIP, msg);
-        return HPMPC_MI355X_EHIP;
+        snprintf(msg, sizeof msg, "hk_wide_ipm launch %s (%d)", e == -2 ? "refused: scratch / LDS beyond the limits" : "failed", e);
+        const int code = e == -2 ? HPMPC_MI355X_EUNSUPPORTED : HPMPC_MI355X_EHIP;
+        hk_set_error(code, msg);
+        return code;
     }
     return 0;
 }
