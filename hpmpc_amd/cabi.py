@@ -636,6 +636,88 @@ class HpmpcAPI:
                     lam=[lam[k][:2 * P["nb"][k] + 2 * P["ng"][k]] for k in range(N + 1)])
 
 
+    # --------------------------------------------------------------------------------- legacy c_interface.h wrappers
+    @staticmethod
+    def _mpc_args(M, order):
+        """Legacy flat problem (oracle/iface_oracle.py random_mpc_problem, column-major stage blocks) -> the wrappers'
+        double* arguments; each stage block row-major for order 'C' (c_order_*)."""
+        nx, nu, ng, ngN = M["nx"], M["nu"], M["ng"], M["ngN"]
+        shapes = {"A": (nx, nx), "B": (nx, nu), "Q": (nx, nx), "S": (nu, nx), "R": (nu, nu), "C": (ng, nx),
+                  "D": (ng, nu), "Qf": (nx, nx), "Cf": (ngN, nx)}
+        a = {}
+        for key in ("A", "B", "b", "Q", "Qf", "S", "R", "q", "qf", "r", "lb", "ub", "C", "D", "lg", "ug", "Cf", "lgf",
+                    "ugf"):
+            v = np.asarray(M[key], dtype=np.float64).reshape(-1)
+            if order == "C" and key in shapes and shapes[key][0] * shapes[key][1] > 0:
+                m, n = shapes[key]
+                nblk = v.size // (m * n)
+                v = np.concatenate([v[i * m * n:(i + 1) * m * n].reshape((m, n), order="F").reshape(-1)
+                                    for i in range(nblk)] + [v[nblk * m * n:]])
+            a[key] = np.concatenate([v, np.zeros(8)])
+        return a
+
+    @staticmethod
+    def mpc_lam_size(M):
+        """Length of the legacy wrappers' lam / t outputs (the largest index they write, +1)."""
+        N, nu, nb, ng, ngN = (M[k] for k in ("N", "nu", "nb", "ng", "ngN"))
+        s = 2 * nb + 2 * ng
+        return N * s + max(s, nu + max(nb - nu, 0) + nb + ngN, 2 * nb + 2 * ngN)
+
+    def _mpc_outs(self, M, x, u, pi, lam, t, inf):
+        N, nx, nu = M["N"], M["nx"], M["nu"]
+        L = self.mpc_lam_size(M)
+        return dict(u=u[:N * nu].copy(), x=x[:(N + 1) * nx].copy(), pi=pi[:N * nx].copy(), lam=lam[:L].copy(),
+                    t=t[:L].copy(), inf_norm_res=inf.copy())
+
+    def ip_mpc(self, M, *, order="F", k_max=50, mu0=2.0, mu_tol=1e-10, warm=None, work0=None):
+        """fortran_order_d_ip_mpc_hard_tv / c_order_d_ip_mpc_hard_tv (include/c_interface.h:45,52)."""
+        N, nx, nu, nb, ng, ngN = (int(M[k]) for k in ("N", "nx", "nu", "nb", "ng", "ngN"))
+        a = self._mpc_args(M, order)
+        x = np.zeros((N + 1) * nx + 8)
+        x[:nx] = M["x0"]
+        u = np.zeros(N * nu + 8)
+        if warm is not None:
+            x[nx:(N + 1) * nx] = warm["x"][nx:(N + 1) * nx]
+            u[:N * nu] = warm["u"][:N * nu]
+        pi = np.zeros(N * nx + 8)
+        L = self.mpc_lam_size(M) + 8
+        lam, t = np.zeros(L), np.zeros(L)
+        inf = np.zeros(4)
+        stat = np.zeros(5 * k_max + 5)
+        if work0 is None:
+            work0 = np.zeros(self.fn("hpmpc_d_ip_mpc_hard_tv_work_space_size_doubles")(
+                C.c_int(N), C.c_int(nx), C.c_int(nu), C.c_int(nb), C.c_int(ng), C.c_int(ngN)) + 16)
+        kk = C.c_int(0)
+        f = self.fn("fortran_order_d_ip_mpc_hard_tv" if order == "F" else "c_order_d_ip_mpc_hard_tv")
+        ret = f(C.byref(kk), C.c_int(k_max), C.c_double(mu0), C.c_double(mu_tol), C.c_int(N), C.c_int(nx), C.c_int(nu),
+                C.c_int(nb), C.c_int(ng), C.c_int(ngN), C.c_int(int(M["ti"])), C.c_int(0),
+                C.c_int(1 if warm is not None else 0), *[_dptr(a[k]) for k in (
+                    "A", "B", "b", "Q", "Qf", "S", "R", "q", "qf", "r", "lb", "ub", "C", "D", "lg", "ug", "Cf", "lgf",
+                    "ugf")], _dptr(x), _dptr(u), _dptr(pi), _dptr(lam), _dptr(t), _dptr(inf), _dptr(work0), _dptr(stat))
+        out = self._mpc_outs(M, x, u, pi, lam, t, inf)
+        out.update(status=ret, kk=kk.value, stat=stat[:5 * max(kk.value, 0)].copy(), work0=work0)
+        return out
+
+    def kkt_mpc(self, M2, work0, *, order="F"):
+        """fortran_order_d_solve_kkt_new_rhs_mpc_hard_tv / c_order_ twin (include/c_interface.h:46,53): the new
+        x0, b, r, q, qf and bounds of M2 on the factor ip_mpc left in work0."""
+        N, nx, nu, nb, ng, ngN = (int(M2[k]) for k in ("N", "nx", "nu", "nb", "ng", "ngN"))
+        a = self._mpc_args(M2, order)
+        x = np.zeros((N + 1) * nx + 8)
+        x[:nx] = M2["x0"]
+        u = np.zeros(N * nu + 8)
+        pi = np.zeros(N * nx + 8)
+        L = self.mpc_lam_size(M2) + 8
+        lam, t = np.zeros(L), np.zeros(L)
+        inf = np.zeros(4)
+        f = self.fn("fortran_order_d_solve_kkt_new_rhs_mpc_hard_tv" if order == "F"
+                    else "c_order_d_solve_kkt_new_rhs_mpc_hard_tv")
+        f(C.c_int(N), C.c_int(nx), C.c_int(nu), C.c_int(nb), C.c_int(ng), C.c_int(ngN), C.c_int(int(M2["ti"])),
+          C.c_int(0), *[_dptr(a[k]) for k in ("A", "B", "b", "Q", "Qf", "S", "R", "q", "qf", "r", "lb", "ub", "C", "D",
+                                              "lg", "ug", "Cf", "lgf", "ugf")],
+          _dptr(x), _dptr(u), _dptr(pi), _dptr(lam), _dptr(t), _dptr(inf), _dptr(work0))
+        return self._mpc_outs(M2, x, u, pi, lam, t, inf)
+
 def bq_from_qp(qp: OCPQP):
     """b[k] and q[k] vectors extracted from the augmented rows (as the IPM does, d_ip2_res_hard.c:202-220)."""
     from .ocp import unpack_lib4

@@ -214,6 +214,46 @@ void fortran_order_d_solve_kkt_new_rhs_ocp_hard_tv(int N, int *nx, int *nu, int 
                                                    double **u, double **pi, double **lam, double *inf_norm_res,
                                                    double *work0);
 
+/* Legacy uniform-size wrappers (include/c_interface.h:40-53; interfaces/c/fortran_order_interface.c:1975,3017,
+ * c_order_interface.c:1052,2083): N stages of nx states / nu inputs in flat arrays (time_invariant: one copy of each
+ * stage array; lg / ug are read per stage either way), x0 = x[0..nx) folded into stage 0, nb boxes per stage
+ * ([inputs | states]; nb - nu state boxes on stage N), ng general constraints per stage and ngN on stage N; the
+ * alternate IPM d_ip2_mpc_hard_tv, then d_res_mpc_hard_tv for inf_norm_res.  u (N nu), x (stages 1..N), pi (N nx),
+ * lam / t with stage stride 2 nb + 2 ng.  The KKT twins re-solve on the factor the IPM wrapper left in work0 with
+ * new x0, b, r, q, qf and bounds.  The reference's quirks and the reads it makes of unwritten memory are listed in
+ * hpmpc_amd/csrc/hpmpc_capi_mpc.cpp. */
+/* include/c_interface.h:40 -- declared, never defined by the reference: the doubles of work0 these wrappers use */
+int hpmpc_d_ip_mpc_hard_tv_work_space_size_doubles(int N, int nx, int nu, int nb, int ng, int ngN);
+/* include/c_interface.h:45 (interfaces/c/c_order_interface.c:1052) */
+int c_order_d_ip_mpc_hard_tv(int *kk, int k_max, double mu0, double mu_tol, int N, int nx, int nu, int nb, int ng,
+                             int ngN, int time_invariant, int free_x0, int warm_start, double *A, double *B,
+                             double *b, double *Q, double *Qf, double *S, double *R, double *q, double *qf, double *r,
+                             double *lb, double *ub, double *C, double *D, double *lg, double *ug, double *Cf,
+                             double *lgf, double *ugf, double *x, double *u, double *pi, double *lam, double *t,
+                             double *inf_norm_res, double *work0, double *stat);
+/* include/c_interface.h:46 (interfaces/c/c_order_interface.c:2083) */
+void c_order_d_solve_kkt_new_rhs_mpc_hard_tv(int N, int nx, int nu, int nb, int ng, int ngN, int time_invariant,
+                                             int free_x0, double *A, double *B, double *b, double *Q, double *Qf,
+                                             double *S, double *R, double *q, double *qf, double *r, double *lb,
+                                             double *ub, double *C, double *D, double *lg, double *ug, double *Cf,
+                                             double *lgf, double *ugf, double *x, double *u, double *pi, double *lam,
+                                             double *t, double *inf_norm_res, double *work0);
+/* include/c_interface.h:52 (interfaces/c/fortran_order_interface.c:1975) */
+int fortran_order_d_ip_mpc_hard_tv(int *kk, int k_max, double mu0, double mu_tol, int N, int nx, int nu, int nb,
+                                   int ng, int ngN, int time_invariant, int free_x0, int warm_start, double *A,
+                                   double *B, double *b, double *Q, double *Qf, double *S, double *R, double *q,
+                                   double *qf, double *r, double *lb, double *ub, double *C, double *D, double *lg,
+                                   double *ug, double *Cf, double *lgf, double *ugf, double *x, double *u, double *pi,
+                                   double *lam, double *t, double *inf_norm_res, double *work0, double *stat);
+/* include/c_interface.h:53 (interfaces/c/fortran_order_interface.c:3017) */
+void fortran_order_d_solve_kkt_new_rhs_mpc_hard_tv(int N, int nx, int nu, int nb, int ng, int ngN, int time_invariant,
+                                                   int free_x0, double *A, double *B, double *b, double *Q, double *Qf,
+                                                   double *S, double *R, double *q, double *qf, double *r, double *lb,
+                                                   double *ub, double *C, double *D, double *lg, double *ug,
+                                                   double *Cf, double *lgf, double *ugf, double *x, double *u,
+                                                   double *pi, double *lam, double *t, double *inf_norm_res,
+                                                   double *work0);
+
 /* ================================ Part 2: batched device API ==================================== */
 
 /* Opaque plan: stage sizes, box indices and device tables shared by every problem of a batch. */

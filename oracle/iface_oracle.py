@@ -360,3 +360,372 @@ def ip_ocp_soft(api, P, k_max=50, mu0=100.0, mu_tol=1e-8, warm=None):
     return dict(u=[np.array(ux[k][:nu[k]]) for k in range(N)], x=[np.array(ux[k][nu[k]:nu[k] + nx[k]]) for k in range(N + 1)],
                 pi=[np.array(pi[k][:nx[k + 1]]) for k in range(N)], lam=lam_c,
                 inf_norm_res=np.array([n0, n1, n2, res["mu"]]), status=r["ret"], kk=r["kk"], stat=r["stat"])
+
+
+# ------------------------------------------------------------------------------------------------- legacy MPC wrappers
+# fortran_order_d_ip_mpc_hard_tv / c_order_d_ip_mpc_hard_tv (interfaces/c/fortran_order_interface.c:1975-3013,
+# c_order_interface.c:1052-2082) and their KKT re-solves (fortran_order_interface.c:3017-3779,
+# c_order_interface.c:2083-2848): uniform stage sizes, flat arrays, a time_invariant flag, x0 folded into stage 0
+# (nx[0] = 0) and the alternate IPM d_ip2_mpc_hard_tv.  Restated step by step, including the reference's
+# deterministic quirks; where the reference reads memory it never wrote or reads past an array, the evident intent
+# is taken instead (each case is listed in DESIGN.md §3c and in hpmpc_capi_mpc.cpp).
+MPC_KEYS = ("A", "B", "b", "Q", "Qf", "S", "R", "q", "qf", "r", "lb", "ub", "C", "D", "lg", "ug", "Cf", "lgf", "ugf",
+            "x0")
+MPC_SHAPES = {"A": lambda M: (M["nx"], M["nx"]), "B": lambda M: (M["nx"], M["nu"]), "Q": lambda M: (M["nx"], M["nx"]),
+              "S": lambda M: (M["nu"], M["nx"]), "R": lambda M: (M["nu"], M["nu"]), "C": lambda M: (M["ng"], M["nx"]),
+              "D": lambda M: (M["ng"], M["nu"])}
+
+
+def _li(sd, i, j):
+    """lib4 index of element (i, j) of a panel-major matrix with panel stride sd."""
+    return (i // 4) * 4 * sd + i % 4 + 4 * j
+
+
+def random_mpc_problem(N, nx, nu, nb, ng, ngN, ti, seed=0, eq=()):
+    """Random problem in the legacy flat column-major format.  Time-invariant: one copy of each stage array (lg / ug
+    still per stage: the wrapper indexes them by stage either way); time-variant: N copies.  lb / ub hold nb bounds
+    per stage ([inputs (nu) | states]), (N + 1) blocks when time-variant (stage N's state bounds at nb N + nu).
+    eq: input indices whose bounds are made equal (lb == ub) on every stage."""
+    rng = np.random.default_rng(seed)
+    S_ = 1 if ti else N
+    M = dict(N=N, nx=nx, nu=nu, nb=nb, ng=ng, ngN=ngN, ti=int(ti))
+    A, B, b, Q, S, R, q, r, C, D = [], [], [], [], [], [], [], [], [], []
+    for _ in range(S_):
+        A.append(np.eye(nx) + 0.2 * rng.standard_normal((nx, nx)) / np.sqrt(nx))
+        B.append(rng.standard_normal((nx, nu)) / np.sqrt(nu))
+        b.append(0.1 * rng.standard_normal(nx))
+        G = rng.standard_normal((nx + nu, nx + nu))
+        H = G @ G.T / (nx + nu) + np.eye(nx + nu)
+        R.append(H[:nu, :nu])
+        S.append(H[:nu, nu:])
+        Q.append(H[nu:, nu:])
+        r.append(0.2 * rng.standard_normal(nu))
+        q.append(0.2 * rng.standard_normal(nx))
+        C.append(rng.standard_normal((ng, nx)) / np.sqrt(nx))
+        D.append(rng.standard_normal((ng, nu)) / np.sqrt(nu))
+    G = rng.standard_normal((nx, nx))
+    flatF = lambda L: np.concatenate([np.asarray(m, dtype=np.float64).reshape(-1, order="F") for m in L])
+    M.update(A=flatF(A), B=flatF(B), b=flatF(b), Q=flatF(Q), S=flatF(S), R=flatF(R), q=flatF(q), r=flatF(r),
+             C=flatF(C) if ng else np.zeros(1), D=flatF(D) if ng else np.zeros(1))
+    M["Qf"] = flatF([G @ G.T / nx + np.eye(nx)])
+    M["qf"] = 0.2 * rng.standard_normal(nx)
+    nlb = nb if ti else nb * (N + 1)
+    M["lb"] = -(1.0 + rng.random(nlb))
+    M["ub"] = 1.0 + rng.random(nlb)
+    for blk in range(1 if ti else N + 1):
+        for i in eq:
+            if i < min(nb, nu):
+                M["ub"][blk * nb + i] = M["lb"][blk * nb + i]
+    M["lg"] = -(0.5 + rng.random(max(N * ng, 1)))
+    M["ug"] = 0.5 + rng.random(max(N * ng, 1))
+    M["Cf"] = rng.standard_normal((ngN, nx)).reshape(-1, order="F") / np.sqrt(nx) if ngN else np.zeros(1)
+    M["lgf"] = -(0.5 + rng.random(max(ngN, 1)))
+    M["ugf"] = 0.5 + rng.random(max(ngN, 1))
+    M["x0"] = 0.5 * rng.standard_normal(nx)
+    return M
+
+
+def mpc_new_rhs(M, seed=1):
+    """M with perturbed x0, b, r, q, qf and bounds (what the legacy KKT wrapper re-packs; same matrices)."""
+    rng = np.random.default_rng(seed)
+    M2 = {k: (np.array(v, copy=True) if isinstance(v, np.ndarray) else v) for k, v in M.items()}
+    for key in ("x0", "b", "r", "q", "qf"):
+        M2[key] = M[key] + 0.05 * rng.standard_normal(M[key].shape)
+    for key in ("lb", "lg", "lgf"):
+        M2[key] = M[key] - 0.05 * rng.random(M[key].shape)
+    for key in ("ub", "ug", "ugf"):
+        M2[key] = M[key] + 0.05 * rng.random(M[key].shape)
+    return M2
+
+
+def mpc_to_flat(M):
+    """Legacy problem -> golden extras (lists of flat float arrays) and args."""
+    return {k: [np.asarray(M[k], dtype=np.float64)] for k in MPC_KEYS}
+
+
+def mpc_from_flat(args, inp):
+    M = {k: int(args[k]) for k in ("N", "nx", "nu", "nb", "ng", "ngN", "ti")}
+    for k in MPC_KEYS:
+        M[k] = np.asarray(inp[k][0])
+    return M
+
+
+def mpc_sizes(M):
+    """Stage sizes the wrapper builds (:2029-2062): x0 folded into stage 0, nbu = min(nb, nu) input boxes on stage 0,
+    nb on the middle stages, nb - nu state boxes on stage N, idxb[k] = 0..nbb[k]-1."""
+    N, nx, nu, nb, ng, ngN = (M[k] for k in ("N", "nx", "nu", "nb", "ng", "ngN"))
+    nbu = min(nb, nu)
+    nxx = [0] + [nx] * N
+    nuu = [nu] * N + [0]
+    nbb = [nbu] + [nb] * (N - 1) + [max(nb - nu, 0)]
+    ngg = [ng] * N + [ngN]
+    return nbu, nxx, nuu, nbb, ngg
+
+
+def _mpc_mat(M, key, k):
+    """Dense stage-k matrix `key` (time-invariant: the single copy)."""
+    m, n = MPC_SHAPES[key](M)
+    o = 0 if M["ti"] else k * m * n
+    return M[key][o:o + m * n].reshape((m, n), order="F")
+
+
+def _mpc_vec(M, key, k, n):
+    o = 0 if M["ti"] else k * n
+    return M[key][o:o + n]
+
+
+def mpc_pack(M, kkt=False, base=None):
+    """The wrapper's lib4 problem (IPM wrapper :2213-2757) or, with kkt=True, the KKT wrapper's re-pack of the
+    right-hand sides on top of `base` (the IPM wrapper's packed data, :3248-3366 / time-variant :3480-3560).
+    Returns an OCPQP (stage blocks, bounds d) plus hb, hrq (the separate b / q vectors)."""
+    N, nx, nu, nb, ng, ngN, ti = (M[k] for k in ("N", "nx", "nu", "nb", "ng", "ngN", "ti"))
+    nbu, nxx, nuu, nbb, ngg = mpc_sizes(M)
+    pnz, pnx, pnb, png, pngN = rup(nx + nu + 1, 4), rup(nx, 4), rup(nb, 4), rup(ng, 4), rup(ngN, 4)
+    cnux, cnu, cnx, cng, cngN = rup(nu + nx, 2), rup(nu, 2), rup(nx, 2), rup(ng, 2), rup(ngN, 2)
+    x0 = M["x0"]
+    if base is None:
+        BAbt = [np.zeros(pnz * cnx + 8) for _ in range(N)]
+        RSQ = [np.zeros(pnz * cnux + 8) for _ in range(N + 1)]
+        DCt = [np.zeros(pnz * max(cng, cngN, 2) + 8) for _ in range(N + 1)]
+    else:
+        BAbt, RSQ, DCt = [a.copy() for a in base.BAbt], [a.copy() for a in base.RSQrq], [a.copy() for a in base.DCt]
+    hb = [np.zeros(pnx + 4) for _ in range(N)]
+    hrq = [np.zeros(pnz + 4) for _ in range(N + 1)]
+    d = [np.zeros(2 * pnb + 2 * (png if k < N else pngN) + 4) for k in range(N + 1)]
+    # stage 0: b0 = A0 x0 + b0 (:2561-2572), r0 = r0 + S0 x0 (:2628-2639)
+    A0, B0 = _mpc_mat(M, "A", 0), _mpc_mat(M, "B", 0)
+    hb[0][:nx] = A0 @ x0 + _mpc_vec(M, "b", 0, nx)
+    r0 = _mpc_vec(M, "r", 0, nu) + _mpc_mat(M, "S", 0) @ x0
+    for i in range(nu):  # B0' into rows 0..nu-1 (the KKT wrapper restores it, :3264)
+        for j in range(nx):
+            BAbt[0][_li(cnx, i, j)] = B0[j, i]
+    if kkt:
+        hrq[0][:nu] = r0
+    else:
+        for j in range(nx):
+            BAbt[0][_li(cnx, nu, j)] = hb[0][j]
+        R0 = _mpc_mat(M, "R", 0)
+        for i in range(nu):
+            for j in range(nu):
+                RSQ[0][_li(cnu, i, j)] = R0[i, j]
+            RSQ[0][_li(cnu, nu, i)] = r0[i]
+    for k in range(1, N):
+        bk = _mpc_vec(M, "b", k, nx)
+        hb[k][:nx] = bk
+        rk, qk = _mpc_vec(M, "r", k, nu), _mpc_vec(M, "q", k, nx)
+        if kkt:
+            hrq[k][:nu], hrq[k][nu:nu + nx] = rk, qk
+            continue
+        Ak, Bk = _mpc_mat(M, "A", k), _mpc_mat(M, "B", k)
+        Rk, Sk, Qk = _mpc_mat(M, "R", k), _mpc_mat(M, "S", k), _mpc_mat(M, "Q", k)
+        for j in range(nx):
+            for i in range(nu):
+                BAbt[k][_li(cnx, i, j)] = Bk[j, i]
+            for i in range(nx):
+                BAbt[k][_li(cnx, nu + i, j)] = Ak[j, i]
+            BAbt[k][_li(cnx, nu + nx, j)] = bk[j]
+        for i in range(nu):
+            for j in range(nu):
+                RSQ[k][_li(cnux, i, j)] = Rk[i, j]
+            RSQ[k][_li(cnux, nu + nx, i)] = rk[i]
+        for i in range(nx):
+            for j in range(nu):
+                RSQ[k][_li(cnux, nu + i, j)] = Sk[j, i]
+            for j in range(nx):
+                RSQ[k][_li(cnux, nu + i, nu + j)] = Qk[i, j]
+            RSQ[k][_li(cnux, nu + nx, nu + i)] = qk[i]
+    Qf = M["Qf"][:nx * nx].reshape((nx, nx), order="F")
+    if kkt:
+        hrq[N][:nx] = M["qf"][:nx]
+    else:
+        for i in range(nx):
+            for j in range(nx):
+                RSQ[N][_li(cnx, i, j)] = Qf[i, j]
+            RSQ[N][_li(cnx, nx, i)] = M["qf"][i]
+        if ng > 0:  # general constraints (:2592-2603): [D'; C'] (stage 0: D' only)
+            for k in range(N):
+                Dk = _mpc_mat(M, "D", k)
+                for i in range(nu):
+                    for j in range(ng):
+                        DCt[k][_li(cng, i, j)] = Dk[j, i]
+                if k > 0:
+                    Ck = _mpc_mat(M, "C", k)
+                    for i in range(nx):
+                        for j in range(ng):
+                            DCt[k][_li(cng, nu + i, j)] = Ck[j, i]
+        if ngN > 0:
+            Cf = M["Cf"][:ngN * nx].reshape((ngN, nx), order="F")
+            for i in range(nx):
+                for j in range(ngN):
+                    DCt[N][_li(cngN, i, j)] = Cf[j, i]
+    # bounds (:2683-2753).  lb / ub of stage k start at nb k (time-variant) or 0; stage N's state bounds at
+    # nb N + nu (the loop index the wrapper leaves at N) or nu.
+    lb, ub = M["lb"], M["ub"]
+    blk = lambda k: 0 if ti else nb * k
+    for k in range(N):
+        p0 = rup(nbb[k], 4)
+        for i in range(nbu):
+            lo, up = lb[i + blk(k)], ub[i + blk(k)]
+            if kkt or lo != up:  # the KKT wrapper copies the bounds as they are (:3300-3316)
+                d[k][i], d[k][i + p0] = lo, up
+            else:  # input equality constraint: folded into b (:2695-2705)
+                for ll in range(nx):
+                    # the b row is addressed with panel (nxx + nuu) / 4 but in-panel row (nx + nu) % 4 (:2698)
+                    BAbt[k][((nxx[k] + nuu[k]) // 4) * cnx * 4 + (nx + nu) % 4 + ll * 4] += BAbt[k][_li(cnx, i, ll)] * lo
+                    BAbt[k][_li(cnx, i, ll)] = 0.0
+                d[k][i], d[k][i + p0] = lo + 1e3, up - 1e3
+    for k in range(1, N):
+        p0 = rup(nbb[k], 4)
+        for i in range(nu, nbb[k]):
+            d[k][i], d[k][i + p0] = lb[i + blk(k)], ub[i + blk(k)]
+    p0 = rup(nbb[N], 4)
+    for i in range(nbb[N]):
+        d[N][i], d[N][i + p0] = lb[nu + i + blk(N)], ub[nu + i + blk(N)]
+    if ng > 0:
+        for k in range(N):
+            p0, g0 = rup(nbb[k], 4), rup(ngg[k], 4)
+            # time-invariant: the middle stages share one bound vector, so the last stage's bounds win (:2425-2433)
+            kk_ = N - 1 if (ti and k > 0) else k
+            for i in range(ng):
+                d[k][2 * p0 + i], d[k][2 * p0 + g0 + i] = M["lg"][i + ng * kk_], M["ug"][i + ng * kk_]
+    if ngN > 0:
+        p0, g0 = rup(nbb[N], 4), rup(ngN, 4)
+        for i in range(ngN):
+            d[N][2 * p0 + i], d[N][2 * p0 + g0 + i] = M["lgf"][i], M["ugf"][i]
+    # the residual's right-hand sides (:2846-2867): b as packed, q = the data's r, q (stage 0: r without S x0)
+    if not kkt:
+        for k in range(N):
+            hrq[k][:nu] = _mpc_vec(M, "r", k, nu)
+            if k > 0:
+                hrq[k][nu:nu + nx] = _mpc_vec(M, "q", k, nx)
+        hrq[N][:nx] = M["qf"][:nx]
+    idxb = [np.arange(nbb[k], dtype=np.int32) for k in range(N + 1)]
+    qp = OCPQP(N, np.array(nxx, np.int32), np.array(nuu, np.int32), np.array(nbb, np.int32), np.array(ngg, np.int32),
+               idxb, BAbt, RSQ, d, DCt, None)
+    return qp, hb, hrq
+
+
+def mpc_mu0(M):
+    """mu0 <= 0 (:2320-2340 time-invariant with absolute values, :2659-2675 time-variant without).  The reference
+    reads qf[nx] (one past qf) in both, and in the time-invariant case the stage-1 slots R + nu^2, S + nu nx, ... of
+    single-stage arrays; here qf[0..nx) and the single stage are read."""
+    N, nx, nu, ti = M["N"], M["nx"], M["nu"], M["ti"]
+    f = (lambda a: np.abs(a)) if ti else (lambda a: a)
+    m = 0.0
+    parts = [_mpc_mat(M, "R", 0), _mpc_vec(M, "r", 0, nu)]
+    for k in range(1, 2 if ti else N):
+        if k < N:
+            parts += [_mpc_mat(M, "R", k), _mpc_mat(M, "S", k), _mpc_mat(M, "Q", k), _mpc_vec(M, "r", k, nu),
+                      _mpc_vec(M, "q", k, nx)]
+    parts += [M["Qf"][:nx * nx], M["qf"][:nx]]
+    for p in parts:
+        if np.size(p):
+            m = max(m, float(np.max(f(np.asarray(p)))))
+    return m
+
+
+def mpc_outputs(M, qp, hb, hrq, ux, pi, lam, t, res, eqfix, gen_norm=True):
+    """Outputs (:2802-3007): u, x (stages 1..N), the input-equality fix, inf_norm_res, pi, lam / t in the wrapper's
+    layout (stage stride 2 nb + 2 ng; box lower at 0, upper at nb + ng; general lower at nb, upper at 2 nb + ng;
+    stage N's boxes at nu + j, upper offset nb + ngN).  The stage-N box term of inf_norm_res[2] reads r_d of stage N
+    (the reference reads r_q of stage N there, :2920-2925, partly memory it never wrote).  gen_norm=False: the
+    c_order KKT wrapper, whose norm skips the general constraints of stages 0..N-1."""
+    N, nx, nu, nb, ng, ngN = (M[k] for k in ("N", "nx", "nu", "nb", "ng", "ngN"))
+    nbu, nxx, nuu, nbb, ngg = mpc_sizes(M)
+    blk = lambda k: 0 if M["ti"] else nb * k
+    u = np.zeros(N * nu)
+    x = np.zeros((N + 1) * nx)
+    x[:nx] = M["x0"]
+    for k in range(N):
+        u[k * nu:(k + 1) * nu] = ux[k][:nu]
+    for k in range(1, N + 1):
+        x[k * nx:(k + 1) * nx] = ux[k][nuu[k]:nuu[k] + nx]
+    if eqfix:
+        for k in range(N):
+            for i in range(nbu):
+                if M["lb"][i + blk(k)] == M["ub"][i + blk(k)]:
+                    u[i + nu * k] = M["lb"][i + blk(k)]
+    rq, rb, rd = res["rq"], res["rb"], res["rd"]
+    n0 = max([abs(rq[0][0])] + [abs(v) for v in rq[0][:nu]] +
+             [abs(v) for k in range(1, N) for v in rq[k][:nu + nx]] + [abs(v) for v in rq[N][:nx]])
+    n1 = max([abs(rb[0][0])] + [abs(v) for k in range(N) for v in rb[k][:nx]])
+    n2 = abs(rd[0][0])
+    for k in range(N + 1):
+        p0 = rup(nbb[k], 4)
+        cnt = nbu if k == 0 else (nb if k < N else nbb[N])
+        for j in range(cnt):
+            n2 = max(n2, abs(rd[k][j]), abs(rd[k][p0 + j]))
+    for k in range(N + 1):
+        if k < N and not gen_norm:
+            continue
+        p0, g0 = rup(nbb[k], 4), rup(ngg[k], 4)
+        for j in range(2 * p0, 2 * p0 + ngg[k]):
+            n2 = max(n2, abs(rd[k][j]), abs(rd[k][g0 + j]))
+    pi_o = np.zeros(N * nx)
+    for k in range(N):
+        pi_o[k * nx:(k + 1) * nx] = pi[k][:nx]
+    L = mpc_lam_size(M)
+    lam_o, t_o = np.zeros(L), np.zeros(L)
+    s = 2 * nb + 2 * ng
+    for src, dst in ((lam, lam_o), (t, t_o)):
+        for k in range(N):
+            p0 = rup(nbb[k], 4)
+            for j in range(nbu if k == 0 else nb):
+                dst[j + k * s] = src[k][j]
+                dst[j + k * s + nb + ng] = src[k][p0 + j]
+        p0 = rup(nbb[N], 4)
+        for j in range(nbb[N]):
+            dst[nu + j + N * s] = src[N][j]
+            dst[nu + j + N * s + nb + ngN] = src[N][p0 + j]
+        for k in range(N):
+            p0, g0 = rup(nbb[k], 4), rup(ngg[k], 4)
+            for j in range(ng):
+                dst[j + k * s + nb] = src[k][2 * p0 + j]
+                dst[j + k * s + nb + ng + nb] = src[k][2 * p0 + g0 + j]
+        p0, g0 = rup(nbb[N], 4), rup(ngN, 4)
+        for j in range(ngN):
+            dst[j + N * s + nb] = src[N][2 * p0 + j]
+            dst[j + N * s + nb + ngN + nb] = src[N][2 * p0 + g0 + j]
+    return dict(u=u, x=x, pi=pi_o, lam=lam_o, t=t_o, inf_norm_res=np.array([n0, n1, n2, res["mu"]]))
+
+
+def mpc_lam_size(M):
+    """Length of the wrappers' lam / t outputs (the largest index they write, +1)."""
+    N, nu, nb, ng, ngN = (M[k] for k in ("N", "nu", "nb", "ng", "ngN"))
+    nbN = max(nb - nu, 0)
+    s = 2 * nb + 2 * ng
+    return N * s + max(s, nu + nbN + nb + ngN, 2 * nb + 2 * ngN)
+
+
+def ip_mpc(api, M, k_max=50, mu0=2.0, mu_tol=1e-10, warm=None):
+    """fortran_order_d_ip_mpc_hard_tv restated over `api`: pack, mu0, warm start (u, x of stages 0..N-1 / 1..N),
+    d_ip2_mpc_hard_tv, then the residuals d_res_mpc_hard_tv and the outputs.  Returns the outputs plus the IPM's
+    work (for kkt_mpc) and the packed problem."""
+    N, nx, nu = M["N"], M["nx"], M["nu"]
+    qp, hb, hrq = mpc_pack(M)
+    if mu0 <= 0:
+        mu0 = mpc_mu0(M)
+    kw = {}
+    if warm is not None:
+        ux0 = [np.r_[warm["u"][k * nu:(k + 1) * nu] if k < N else [], warm["x"][k * nx:(k + 1) * nx] if k > 0 else []]
+               for k in range(N + 1)]
+        kw = dict(warm_start=1, ux=ux0)
+    r = api.ipm(qp.copy(), k_max=k_max, mu0=mu0, mu_tol=mu_tol, alpha_min=1e-8, res=False, **kw)
+    res = api.residuals_plain(qp, hb, hrq, r["ux"], r["pi"], r["lam"], r["t"])
+    out = mpc_outputs(M, qp, hb, hrq, r["ux"], r["pi"], r["lam"], r["t"], res, eqfix=True)
+    out.update(status=r["ret"], kk=r["kk"], stat=r["stat"], work=r["work"], qp=qp, ux=r["ux"])
+    return out
+
+
+def kkt_mpc(api, M, M2, k_max=50, mu0=2.0, mu_tol=1e-10, order="F"):
+    """fortran_order_d_ip_mpc_hard_tv on M, then fortran_order_d_solve_kkt_new_rhs_mpc_hard_tv with the
+    right-hand sides of M2 (x0, b, r, q, bounds; same matrices): d_kkt_solve_new_rhs_mpc_hard_tv on the IPM's
+    work, with stage 0's B' re-packed over the IPM's data and the bounds copied as they are, then the residuals
+    and outputs (no input-equality fix; the c_order twin's norm skips the general constraints of stages < N)."""
+    ip = ip_mpc(api, M, k_max=k_max, mu0=mu0, mu_tol=mu_tol)
+    qp2, hb2, hrq2 = mpc_pack(M2, kkt=True, base=ip["qp"])
+    k = api.kkt_new_rhs_plain(qp2, ip["work"], hb2, hrq2, qp2.d, ip["ux"])
+    _, _, hrq_res = mpc_pack(M2)
+    res = api.residuals_plain(qp2, hb2, hrq_res, k["ux"], k["pi"], k["lam"], k["t"])
+    return mpc_outputs(M2, qp2, hb2, hrq_res, k["ux"], k["pi"], k["lam"], k["t"], res, eqfix=False,
+                       gen_norm=(order == "F"))

@@ -225,6 +225,7 @@ def main():
     soft_res(ref, out)
     iface(ref, out)
     iface_soft(ref, out)
+    iface_mpc(ref, ref_avx_api(), out)
     wide(ref, ref_avx_api(), out)
     divergent(ref, out)
     driver(out)
@@ -410,6 +411,61 @@ def iface(ref, out):
     out.append(save_case("iface_kkt_N10_nx4_nu2", "iface_kkt", IO.to_qp(P), dict(mu0=2.0, mu_tol=1e-10, k_max=50),
                          dict(u=k["u"], x=k["x"], pi=k["pi"], lam=k["lam"], inf_norm_res=k["inf_norm_res"]),
                          extra=extra))
+
+
+MPC_CASES = [  # name, (N, nx, nu, nb, ng, ngN, ti, seed, eq), mu0, warm
+    ("tv_N10_nx4_nu2", (10, 4, 2, 6, 0, 0, 0, 21, ()), 2.0, False),
+    ("ti_ng_N12_nx3_nu2", (12, 3, 2, 4, 2, 1, 1, 22, ()), 2.0, False),
+    ("tv_ng_automu0_N8_nx5_nu2", (8, 5, 2, 5, 2, 2, 0, 23, ()), -1.0, False),
+    ("ti_automu0_N9_nx4_nu3", (9, 4, 3, 5, 0, 0, 1, 25, ()), -1.0, False),
+    ("tv_nbltnu_N6_nx3_nu3", (6, 3, 3, 2, 0, 0, 0, 25, ()), 2.0, False),
+    ("tv_N1_nx3_nu2", (1, 3, 2, 5, 0, 1, 0, 26, ()), 2.0, False),
+    ("tv_warm_N10_nx4_nu2", (10, 4, 2, 6, 0, 0, 0, 28, ()), 2.0, True),
+]
+
+
+def iface_mpc(ref, refa, out):
+    """The legacy uniform-size wrappers fortran_order_d_ip_mpc_hard_tv / c_order_ twin and their KKT re-solves
+    (include/c_interface.h:45-53), restated by oracle/iface_oracle.py ip_mpc / kkt_mpc over the reference's own
+    d_ip2_mpc_hard_tv, d_kkt_solve_new_rhs_mpc_hard_tv and d_res_mpc_hard_tv (the wrapper sources need the
+    generated include/target.h): time-variant and time-invariant data, general constraints (time-invariant: the
+    shared-bounds quirk), the cost-based mu0, fewer boxes than inputs, N = 1, a warm start, and the KKT re-solve."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import iface_oracle as IO
+
+    for name, (N, nx, nu, nb, ng, ngN, ti, seed, eq), mu0, warm in MPC_CASES:
+        M = IO.random_mpc_problem(N, nx, nu, nb, ng, ngN, ti, seed=seed, eq=eq)
+        w = None
+        if warm:
+            r0 = IO.ip_mpc(ref, M, k_max=50, mu0=mu0, mu_tol=1e-8)
+            w = dict(u=0.9 * r0["u"], x=0.9 * r0["x"])
+        # mu_tol 1e-8: below it these small random problems reach the end game where the reference's own c99 and avx
+        # builds already differ in the step length of the last iteration (~1e-6 relative)
+        r = IO.ip_mpc(ref, M, k_max=50, mu0=mu0, mu_tol=1e-8, warm=w)
+        args = dict(N=N, nx=nx, nu=nu, nb=nb, ng=ng, ngN=ngN, ti=ti, mu0=mu0, mu_tol=1e-8, k_max=50,
+                    warm=int(warm))
+        extra = IO.mpc_to_flat(M)
+        if warm:
+            extra.update(warm_u=[w["u"]], warm_x=[w["x"]])
+        outs = dict(u=[r["u"]], x=[r["x"]], pi=[r["pi"]], lam=[r["lam"]], t=[r["t"]], inf_norm_res=r["inf_norm_res"],
+                    kk=r["kk"], ret=r["status"], stat=r["stat"])
+        out.append(save_case(f"iface_mpc_{name}", "iface_mpc", r["qp"], args, outs, extra=extra))
+    for name, (N, nx, nu, nb, ng, ngN, ti, seed), order in (("tv_N10_nx4_nu2", (10, 4, 2, 6, 0, 0, 0, 31), "F"),
+                                                            ("ti_ng_N12_nx3_nu2", (12, 3, 2, 4, 2, 1, 1, 32), "F"),
+                                                            ("ti_ng_N12_nx3_nu2_c", (12, 3, 2, 4, 2, 1, 1, 32), "C")):
+        M = IO.random_mpc_problem(N, nx, nu, nb, ng, ngN, ti, seed=seed)
+        M2 = IO.mpc_new_rhs(M, seed=seed + 100)  # same matrices, perturbed right-hand sides
+        # the KKT re-solve's goldens come from the reference's default-target (avx) build of the alternate IPM, whose
+        # d_kkt_solve_new_rhs_mpc_hard_tv binds its gradient helper with the right arity (oracle/Makefile ref_avx)
+        k = IO.kkt_mpc(refa, M, M2, k_max=50, mu0=2.0, mu_tol=1e-8, order=order)
+        args = dict(N=N, nx=nx, nu=nu, nb=nb, ng=ng, ngN=ngN, ti=ti, mu0=2.0, mu_tol=1e-8, k_max=50,
+                    order=0 if order == "F" else 1)
+        extra = IO.mpc_to_flat(M)
+        extra.update({"N" + key: v for key, v in IO.mpc_to_flat(M2).items()})
+        qp, _, _ = IO.mpc_pack(M)
+        out.append(save_case(f"iface_mpc_kkt_{name}", "iface_mpc_kkt", qp, args,
+                             dict(u=[k["u"]], x=[k["x"]], pi=[k["pi"]], lam=[k["lam"]], t=[k["t"]],
+                                  inf_norm_res=k["inf_norm_res"]), extra=extra))
 
 
 def iface_soft(ref, out):
@@ -622,6 +678,10 @@ if __name__ == "__main__":
         o = []
         divergent(ref_api(), o)
         print(f"wrote {len(o)} divergent cases, {sum(os.path.getsize(p) for p in o) / 1e6:.2f} MB")
+    elif len(sys.argv) > 1 and sys.argv[1] == "iface_mpc":
+        o = []
+        iface_mpc(ref_api(), ref_avx_api(), o)
+        print(f"wrote {len(o)} iface_mpc cases")
     elif len(sys.argv) > 1 and sys.argv[1] == "iface_soft":
         o = []
         iface_soft(ref_api(), o)

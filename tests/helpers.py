@@ -79,6 +79,8 @@ def run_case(api, case):
         return dict(Gamma=G, BAbt2=B2, RSQrq2=R2, DCt2=DCt2, d2=d2, idxb2=idxb2)
     if case.kind in ("iface", "iface_kkt", "iface_newton", "iface_soft"):
         return run_iface(api, case)
+    if case.kind in ("iface_mpc", "iface_mpc_kkt"):
+        return run_iface_mpc(api, case)
     if case.kind == "soft":
         from hpmpc_amd.soft import SoftQP
 
@@ -134,6 +136,34 @@ def run_iface(api, case, order="F"):
     else:
         k = IO.kkt_ocp(api, P, P2, **kw)
     return {key: k[key] for key in ("u", "x", "pi", "lam", "inf_norm_res")}
+
+
+def run_iface_mpc(api, case, order=None):
+    """The legacy uniform-size wrappers (include/c_interface.h:45-53): through the library's own symbols when it has
+    them (the product), else oracle/iface_oracle.py ip_mpc / kkt_mpc over its low-level entry points."""
+    IO = _iface_oracle()
+    a = case.args
+    M = IO.mpc_from_flat(a, case.inp)
+    kw = dict(k_max=int(a["k_max"]), mu0=a["mu0"], mu_tol=a["mu_tol"])
+    has = hasattr(api.lib, api.p + "fortran_order_d_ip_mpc_hard_tv")
+    keys = ("u", "x", "pi", "lam", "t", "inf_norm_res")
+    if case.kind == "iface_mpc":
+        order = order or "F"
+        w = dict(u=case.inp["warm_u"][0], x=case.inp["warm_x"][0]) if int(a.get("warm", 0)) else None
+        r = api.ip_mpc(M, order=order, warm=w, **kw) if has else IO.ip_mpc(api, M, warm=w, **kw)
+        out = {k: [r[k]] for k in keys[:-1]}
+        out.update(inf_norm_res=r["inf_norm_res"], kk=r["kk"], ret=r["status"], stat=r["stat"])
+        return out
+    order = "C" if int(a["order"]) else "F"
+    M2 = IO.mpc_from_flat(a, {k[1:]: v for k, v in case.inp.items() if k.startswith("N")})
+    if has:
+        r = api.ip_mpc(M, order=order, **kw)
+        k = api.kkt_mpc(M2, r["work0"], order=order)
+    else:
+        k = IO.kkt_mpc(api, M, M2, order=order, **kw)
+    out = {key: [k[key]] for key in keys[:-1]}
+    out["inf_norm_res"] = k["inf_norm_res"]
+    return out
 
 
 def check_iface(case, got):
@@ -425,7 +455,7 @@ def check_case(case, got):
         return check_soft(case, got)
     if case.kind == "pcond":
         return check_pcond(case, got)
-    if case.kind in ("iface", "iface_kkt", "iface_newton", "iface_soft"):
+    if case.kind in ("iface", "iface_kkt", "iface_newton", "iface_soft", "iface_mpc", "iface_mpc_kkt"):
         return check_iface(case, got)
     if case.kind == "ipm_div":
         # a diverging infeasible problem: only ret and kk to +-2 are comparable (the reference and a second c99
