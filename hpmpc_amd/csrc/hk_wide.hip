@@ -26,7 +26,7 @@ __global__ __launch_bounds__(WT) void hk_wide_sv(WideArgs a) {
 // Condensed stage variables: [u_{T-1}; ...; u_0; x_0].  Gamma_j (rows [u_j..u_0, x_0, 1] x nx_{j+1},
 // dense column-major) lives in the problem's scratch; the stage tiles (pL, Lx, BAbt, W) in LDS.
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(WT) void hk_pcond(PcArgs a) {
+__global__ __launch_bounds__(WT, 4) void hk_pcond(PcArgs a) {  // 4 waves per SIMD: four workgroups per CU (the LDS fits four)
     extern __shared__ double sm[];
     const int ii = blockIdx.x, p = blockIdx.y + a.p0;
     if (p >= a.nprob || ii >= a.N2) return;
@@ -75,13 +75,29 @@ __global__ __launch_bounds__(WT) void hk_pcond(PcArgs a) {
         bar();
         for (int e = tid; e < r0 * s.nx1; e += WT) G[e] = GA[e];
     }
+    // BAbt_{j+1} is loaded into registers while Gamma_j is formed (Staged), and stored into LDS at the top of the
+    // next step: one memory round trip per block instead of one per stage
+    Staged<4> nb;
+    bool staged = false;
     for (int j = 1; j < ((a.skip & 1) ? 1 : T); j++) {
         const WideStage s = st[j];
         const int nuj = s.nu, nxj = s.nx, nx1 = s.nx1, nzj = nuj + nxj + 1;
         const int rp = rows(j - 1), rj = rp + nuj, n = rj * nx1;
         double* Gj = G + goff(j);
-        load_dense<8>(Bt, ldB, BAbt + s.oB, s.sdB, nzj, nx1);
+        if (staged)
+            put_dense(nb, Bt, ldB);
+        else
+            load_dense<8>(Bt, ldB, BAbt + s.oB, s.sdB, nzj, nx1);
         bar();
+        staged = false;
+        if (j + 1 < ((a.skip & 1) ? 1 : T)) {
+            const WideStage sn = st[j + 1];
+            const int nzn = sn.nu + sn.nx + 1;
+            if (nzn * sn.nx1 <= 4 * WT) {  // uniform
+                pre_dense(nb, BAbt + sn.oB, sn.sdB, nzn, sn.nx1);
+                staged = true;
+            }
+        }
         // rows nuj.. : Gamma_{j-1} A_j (+ b_j on the last row) on MFMA; rows ..nuj: B_j.  The results overwrite
         // GA (leading dimension rp -> rj) after mfma_gemm's barrier, when every operand read is done.
         mfma_gemm(
@@ -147,6 +163,16 @@ __global__ __launch_bounds__(WT) void hk_pcond(PcArgs a) {
             // D: the u_s x u_s block
             for (int j = tid >> 6; j < nus; j += WT / 64)
                 for (int i = j + (tid & 63); i < nus; i += 64) *P4w(R2, cnux2, os + i, os + j) = Pl[i + j * ldP];
+            // BAbt_{s-1} / RSQrq_{s-1} (needed after the Cholesky) are loaded into registers now, so their memory
+            // round trip overlaps Gamma_{s-1}'s and the work below; they go to LDS once Bt / pL are free
+            const WideStage sp = st[sI - 1];
+            const int nuxp = sp.nu + sp.nx, nzp = nuxp + 1;
+            const bool stg = nzp * nxs <= 4 * WT && nzp * nuxp <= 4 * WT;  // uniform
+            Staged<4> pb, pr;
+            if (stg) {
+                pre_dense(pb, BAbt + sp.oB, sp.sdB, nzp, nxs);
+                pre_dense(pr, RSQ + sp.oR, sp.sdR, nzp, nuxp);
+            }
             // Gamma_{s-1} into GA; the state block of pL (with its gradient row) into X
             const int r0 = rows(sI - 1);
             load_flat<8>(GA, G + goff(sI - 1), r0 * nxs);
@@ -199,10 +225,13 @@ __global__ __launch_bounds__(WT) void hk_pcond(PcArgs a) {
             }
             bar();
             // W = BAbt_{s-1} Lx (in place in Bt, row i by one thread), last row += l; pL = RSQ_{s-1} + W W'
-            const WideStage sp = st[sI - 1];
-            const int nuxp = sp.nu + sp.nx, nzp = nuxp + 1;
-            load_dense<8>(Bt, ldB, BAbt + sp.oB, sp.sdB, nzp, nxs);
-            load_dense<8>(Pl, ldP, RSQ + sp.oR, sp.sdR, nzp, nuxp);
+            if (stg) {
+                put_dense(pb, Bt, ldB);
+                put_dense(pr, Pl, ldP);
+            } else {
+                load_dense<8>(Bt, ldB, BAbt + sp.oB, sp.sdB, nzp, nxs);
+                load_dense<8>(Pl, ldP, RSQ + sp.oR, sp.sdR, nzp, nuxp);
+            }
             bar();
             if (!(a.skip & 16)) {
                 // W = BAbt_{s-1} Lx (+ l on the last row) in place over Bt, then pL += W W' (lower), both on MFMA

@@ -64,6 +64,33 @@ __device__ void load_dense(double* D, int ld, const double* src, int sd, int nr,
         }
     }
 }
+// The same copy split in two: pre_dense issues the loads of a block of at most CH * WT elements into registers,
+// put_dense stores them into LDS later, so their memory latency overlaps whatever work runs in between.
+template <int CH>
+struct Staged {
+    double r[CH];
+    int nr, nc;
+};
+template <int CH>
+__device__ __forceinline__ void pre_dense(Staged<CH>& S, const double* src, int sd, int nr, int nc) {
+    const int tid = threadIdx.x, n = nr * nc;
+    S.nr = nr;
+    S.nc = nc;
+#pragma unroll
+    for (int u = 0; u < CH; u++) {
+        const int e = u * WT + tid, i = e % nr, c = e / nr;
+        S.r[u] = gld(src, p4i(i, c, sd), e < n);
+    }
+}
+template <int CH>
+__device__ __forceinline__ void put_dense(const Staged<CH>& S, double* D, int ld) {
+    const int tid = threadIdx.x, nr = S.nr, n = S.nr * S.nc;
+#pragma unroll
+    for (int u = 0; u < CH; u++) {
+        const int e = u * WT + tid, i = e % nr, c = e / nr;
+        if (e < n) D[i + c * ld] = S.r[u];
+    }
+}
 // lib4 lower trapezoid rows [j, nz) of cols [0, nc) -> packed lower columns (nz <= 128: two rows per lane)
 template <int CU>
 __device__ void load_lower(double* M, const double* src, int sd, int nz, int nc) {
@@ -136,6 +163,26 @@ __device__ __forceinline__ void mfma_gemm(int m, int n, int K, FA a, FB b, FO ou
             }
         }
     }
+}
+
+// sum_{j < n} a(j) b(j), accumulated in the order j = 0, 1, .. exactly as the plain loop (so bitwise the same
+// result), with the operands of 8 terms loaded before their multiply-adds: a global-memory dot product then costs
+// one memory latency per 8 terms instead of one per term.  a(j, ok) / b(j, ok) load term j (0 when !ok).
+template <class FA, class FB>
+__device__ __forceinline__ double bdot(int n, FA a, FB b, double acc = 0.0) {
+    for (int j0 = 0; j0 < n; j0 += 8) {
+        double x[8], y[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const bool ok = j0 + u < n;
+            x[u] = a(j0 + u, ok);
+            y[u] = b(j0 + u, ok);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+            if (j0 + u < n) acc += x[u] * y[u];
+    }
+    return acc;
 }
 
 // Per-problem pointers of one wide Riccati call (already offset to the problem).
@@ -315,14 +362,23 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
                 const int J = t - I * (I + 1) / 2;
                 const int ra = 16 * I + c16, rb = 16 * J + c16;
                 hk::d4 acc = {0.0, 0.0, 0.0, 0.0};
-                for (int kc = 0; kc < nK; kc++) {
-                    const int kk = 4 * kc + g4;
-                    const bool kok = kk < ng;
-                    const double dq = gld(Qg, kk, kok);
-                    double av = gld(D, p4i(ra, kk, sdG), kok && ra < nux) * dq;
-                    if (ra == nux) av = a.trf ? 0.0 : gld(qg, kk, kok);
-                    const double bv = gld(D, p4i(rb, kk, sdG), kok && rb < nux);
-                    acc = hk::mfma(av, bv, acc);
+                // K chunks in batches of 8: every operand of a batch is loaded before its MFMAs (the MFMA chain
+                // keeps the chunk order, so the sum is the same as one chunk at a time)
+                for (int kc0 = 0; kc0 < nK; kc0 += 8) {
+                    double avs[8], bvs[8];
+#pragma unroll
+                    for (int u = 0; u < 8; u++) {
+                        const int kk = 4 * (kc0 + u) + g4;
+                        const bool kok = kk < ng;
+                        const double dq = gld(Qg, kk, kok);
+                        double av = gld(D, p4i(ra, kk, sdG), kok && ra < nux) * dq;
+                        if (ra == nux) av = a.trf ? 0.0 : gld(qg, kk, kok);
+                        avs[u] = av;
+                        bvs[u] = gld(D, p4i(rb, kk, sdG), kok && rb < nux);
+                    }
+#pragma unroll
+                    for (int u = 0; u < 8; u++)
+                        if (kc0 + u < nK) acc = hk::mfma(avs[u], bvs[u], acc);
                 }
                 const int col = 16 * J + c16;
 #pragma unroll
@@ -532,8 +588,10 @@ __device__ HK_WIDE_BODY void wide_trs_body(const WideArgs& a, const WideProb& q)
         if (q.DCt && s.ng > 0) {  // + DCt qx_g (dgemv_n_lib, d_back_ric_rec.c:620-633)
             if (tid < nux) {
                 const double* D = q.DCt + s.oG;
-                double c = 0.0;
-                for (int g = 0; g < s.ng; g++) c += P4(D, s.sdG, tid, g) * qx[s.oD + s.pnb + g];
+                const double* qg = qx + s.oD + s.pnb;
+                const double c = bdot(
+                    s.ng, [&](int g, bool ok) { return gld(D, p4i(tid, g, s.sdG), ok); },
+                    [&](int g, bool ok) { return gld(qg, g, ok); });
                 v[tid] += c;
             }
             bar();

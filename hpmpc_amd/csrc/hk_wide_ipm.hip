@@ -94,11 +94,10 @@ __device__ __forceinline__ void alpha_rule(double& al, double v, double dv) {
 __device__ __forceinline__ double cval(const WideIpmArgs& A, const IP& P, const double* x, const WideCSlot& c) {
     if (c.var >= 0) return x[c.var];
     const WideStage s = A.w.st[-1 - c.var];
-    const double* D = P.DCt + s.oG;
-    const int nux = s.nu + s.nx;
-    double acc = 0.0;
-    for (int i = 0; i < nux; i++) acc += P4(D, s.sdG, i, c.g) * x[s.oU + i];
-    return acc;
+    // the slots of one wave may sit on different stages: the problem's (wave-uniform) bases, per-lane offsets
+    return bdot(
+        s.nu + s.nx, [&](int i, bool ok) { return hk::gld(P.DCt, s.oG + p4i(i, c.g, s.sdG), ok); },
+        [&](int i, bool ok) { return hk::gld(x, s.oU + i, ok); });
 }
 
 // ---- d_init_var_mpc_hard_tv (d_aux_ip_hard_lib4.c:43-149) ----
@@ -350,25 +349,38 @@ __device__ __forceinline__ void update_var_res(const WideIpmArgs& A, const IP& P
 // b_k / q_k come from vb / vq when given, else from the augmented rows.  Returns mu (unchanged without
 // constraints for the res variant, 0 for the plain one).
 __device__ __forceinline__ double residuals(const WideIpmArgs& A, const IP& P, bool plain, double mu_in, double* red) {
+    using hk::gld;
     const int tid = threadIdx.x, N = A.w.N;
-    for (int k = 0; k <= N; k++) {
+    // the rows of every stage (nux r_q rows, then nx1 r_b rows) form one flat range that all threads share, so a
+    // stage's ~100 rows do not leave most of the workgroup idle; each row's dot products load 8 terms at a time
+    // from the problem's (wave-uniform) bases.  Every row sums in the reference's order, as before.
+    int k = 0, rbase = 0;
+    for (int rr = tid;; rr += WT) {
+        while (k <= N && rr >= rbase + A.w.st[k].nu + A.w.st[k].nx + A.w.st[k].nx1) {
+            rbase += A.w.st[k].nu + A.w.st[k].nx + A.w.st[k].nx1;
+            k++;
+        }
+        if (k > N) break;
+        const int r = rr - rbase;
         const WideStage s = A.w.st[k];
-        const int nux = s.nu + s.nx, nx1 = s.nx1;
+        const int nux = s.nu + s.nx;
         const double* R = P.RSQ + s.oR;
         const double* B = P.BAbt + s.oB;
-        const double* D = P.DCt ? P.DCt + s.oG : nullptr;
-        const double* ux = P.ux + s.oU;
-        const double* pik = P.pi + s.oP;
         const int pnb = s.pnb, png = (s.ng + 3) & ~3;
-        const double* lg = P.lam + s.oD + 2 * pnb;
-        for (int r = tid; r < nux + nx1; r += WT) {
+        const int olg = s.oD + 2 * pnb;  // general multipliers: lam[olg + g] (lower), lam[olg + png + g] (upper)
+        {
             if (r < nux) {
                 const int i = r;
                 const double q = P.vq ? P.vq[s.oU + i] : P4(R, s.sdR, nux, i);
-                double sy = 0.0;
-                for (int j = 0; j < nux; j++) sy += (i >= j ? P4(R, s.sdR, i, j) : P4(R, s.sdR, j, i)) * ux[j];
-                double bp = 0.0;
-                for (int j = 0; j < nx1; j++) bp += P4(B, s.sdB, i, j) * pik[j];
+                const double sy = bdot(
+                    nux,
+                    [&](int j, bool ok) {
+                        return gld(P.RSQ, s.oR + (i >= j ? p4i(i, j, s.sdR) : p4i(j, i, s.sdR)), ok);
+                    },
+                    [&](int j, bool ok) { return gld(P.ux, s.oU + j, ok); });
+                const double bp = bdot(
+                    s.nx1, [&](int j, bool ok) { return gld(P.BAbt, s.oB + p4i(i, j, s.sdB), ok); },
+                    [&](int j, bool ok) { return gld(P.pi, s.oP + j, ok); });
                 const int lo = A.vbox[s.oU + i];
                 double v;
                 if (!plain) {
@@ -377,20 +389,20 @@ __device__ __forceinline__ double residuals(const WideIpmArgs& A, const IP& P, b
                     if (lo >= 0) v += -P.lam[lo] + P.lam[lo + pnb];
                     v += sy;
                     if (k < N) v += bp;
-                    if (s.ng > 0) {
-                        double c = 0.0;
-                        for (int g = 0; g < s.ng; g++) c += P4(D, s.sdG, i, g) * (lg[png + g] - lg[g]);
-                        v += c;
-                    }
+                    if (s.ng > 0)
+                        v += bdot(
+                            s.ng, [&](int g, bool ok) { return gld(P.DCt, s.oG + p4i(i, g, s.sdG), ok); },
+                            [&](int g, bool ok) { return gld(P.lam, olg + png + g, ok) - gld(P.lam, olg + g, ok); });
                 } else {
                     v = -q;
                     if (k > 0 && i >= s.nu) v = -q + P.pi[A.w.st[k - 1].oP + i - s.nu];
                     if (lo >= 0) v += P.lam[lo] - P.lam[lo + pnb];
                     v -= sy;
                     if (s.ng > 0) {
-                        double ca = 0.0, cb = 0.0;
-                        for (int g = 0; g < s.ng; g++) ca += P4(D, s.sdG, i, g) * lg[g];
-                        for (int g = 0; g < s.ng; g++) cb += P4(D, s.sdG, i, g) * lg[png + g];
+                        auto dg = [&](int g, bool ok) { return gld(P.DCt, s.oG + p4i(i, g, s.sdG), ok); };
+                        const double ca = bdot(s.ng, dg, [&](int g, bool ok) { return gld(P.lam, olg + g, ok); });
+                        const double cb =
+                            bdot(s.ng, dg, [&](int g, bool ok) { return gld(P.lam, olg + png + g, ok); });
                         v += ca;
                         v -= cb;
                     }
@@ -403,12 +415,14 @@ __device__ __forceinline__ double residuals(const WideIpmArgs& A, const IP& P, b
                 const WideStage s1 = A.w.st[k + 1];
                 const double b = P.vb ? P.vb[s.oP + j] : P4(B, s.sdB, nux, j);
                 const double x1 = P.ux[s1.oU + s1.nu + j];
-                double c = 0.0;
-                for (int i = 0; i < nux; i++) c += P4(B, s.sdB, i, j) * ux[i];
+                const double c = bdot(
+                    nux, [&](int i, bool ok) { return gld(P.BAbt, s.oB + p4i(i, j, s.sdB), ok); },
+                    [&](int i, bool ok) { return gld(P.ux, s.oU + i, ok); });
                 P.rb[s.oP + j] = plain ? -((x1 - b) - c) : (b - x1) + c;
             }
         }
     }
+    bar();  // r_q / r_b complete before anything reads them
     double s2 = 0.0;
     for (int e = tid; e < A.ncs; e += WT) {
         const WideCSlot c = A.cs[e];
@@ -491,7 +505,34 @@ __device__ __forceinline__ void ric_trs(const WideIpmArgs& A, const IP& P, const
 
 }  // namespace
 
+#ifdef HK_STAMPS
+// Diagnostic build only: per-phase s_memtime cycle totals of workgroup 0 (tools/wide_phases.py)
+__device__ unsigned long long* g_wdbg;
+extern "C" __attribute__((visibility("default"))) int hk_wide_ipm_debug(void* dev_ptr) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_wdbg), &dev_ptr, sizeof(void*));
+}
+#define WPH(i)                                                                              \
+    do {                                                                                    \
+        unsigned long long t_;                                                              \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");           \
+        if (g_wdbg && blockIdx.x == 0 && threadIdx.x == 0) {                                \
+            if (ph_ >= 0) g_wdbg[ph_] += t_ - t0_;                                          \
+            g_wdbg[31] += 1;                                                                \
+        }                                                                                   \
+        t0_ = t_;                                                                           \
+        ph_ = (i);                                                                          \
+    } while (0)
+#else
+#define WPH(i) \
+    do {       \
+    } while (0)
+#endif
+
 __global__ __launch_bounds__(WT) void hk_wide_ipm(WideIpmArgs A) {
+#ifdef HK_STAMPS
+    unsigned long long t0_ = 0;
+    int ph_ = -1;
+#endif
     extern __shared__ double sm[];
     const int p = blockIdx.x + A.w.p0;
     if (p >= A.w.nprob) return;
@@ -607,12 +648,16 @@ __global__ __launch_bounds__(WT) void hk_wide_ipm(WideIpmArgs A) {
     bar();
     // phase 2: residual-based Mehrotra (d_ip2_res_hard.c:783-1273); single Newton step: :1640-1905
     while (kk < A.k_max && (newton || (mu > A.mu_tol && alpha >= A.alpha_min))) {
+        WPH(0);
         update_hessian_gradient_res(A, P);
+        WPH(1);
         if (!newton)
             ric_sv(A, P, P.rb, P.rq, true, P.dux, P.dpi);
         else  // the single-Newton step factorises with the data's own b / q rows
             ric_sv(A, P, nullptr, nullptr, true, P.dux, P.dpi);
+        WPH(2);
         alpha = dt_dlam_res(A, P, true, red);
+        WPH(3);
         put_stat(kk, 0, sigma);
         put_stat(kk, 1, alpha);
         alpha *= 0.995;
@@ -625,18 +670,25 @@ __global__ __launch_bounds__(WT) void hk_wide_ipm(WideIpmArgs A) {
         } else {
             centering_correction(A, P, A.mu0);
         }
+        WPH(4);
         update_gradient_res(A, P);
+        WPH(5);
         ric_trs(A, P, P.rb, P.rq, 0, P.dux, P.dpi);
+        WPH(6);
         alpha = dt_dlam_res(A, P, true, red);
         put_stat(kk, 0, sigma);
         put_stat(kk, 3, alpha);
         alpha *= 0.995;
+        WPH(7);
         update_var_res(A, P, alpha, true);
+        WPH(8);
         mu = residuals(A, P, false, mu, red);
         bar();
         put_stat(kk, 4, mu);
         kk++;
+        WPH(9);
     }
+    WPH(10);
     const int ret = (!newton && mu <= A.mu_tol) ? 0 : kk >= A.k_max ? 1 : alpha < A.alpha_min ? 2 : -1;
     finish(kk, ret, mu);
 }
