@@ -16,6 +16,7 @@ using hk::gld;
 
 constexpr int WT = 256;  // threads per workgroup
 constexpr int WS_TILES = 8;  // W = BAbt Lxx output tiles per wave (nz <= 128, nx <= 64: <= 32 tiles, host-checked)
+constexpr int DT_TILES = 6;  // DCt diag DCt' lower tiles per wave on the LDS-staged path (nz <= 96; larger stages read HBM directly)
 constexpr int BS = 4;
 
 __device__ __forceinline__ int p4i(int i, int j, int sd) { return (i / BS) * BS * sd + i % BS + BS * j; }
@@ -127,6 +128,40 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
+// In-register triangular solves for wave 0 on a packed-lower factor M (poff columns, nz rows) with inverse diagonal
+// dL: v[0..n) sits in registers, two entries per lane (v[l], v[l + 64], n <= 128), each pivot is broadcast by
+// readlane.  Every entry sees the same operations in the same order as the column loops over LDS they replace
+// (one LDS round trip and wave barrier per pivot), so the results are the same.
+// L' y = v on the first ns unknowns, descending (dtrsv_t over the u block): v[j] -= L[i][j] y_i for j < i.
+__device__ __forceinline__ void wave_solve_lt(double* v, const double* M, const double* dL, int nz, int ns) {
+    const int l = threadIdx.x & 63;
+    double v0 = l < ns ? v[l] : 0.0, v1 = l + 64 < ns ? v[l + 64] : 0.0;
+    for (int i = ns - 1; i >= 0; i--) {
+        const double y = rdlane(i < 64 ? v0 : v1, i & 63) * dL[i];
+        if (l < i) v0 -= M[poff(l, nz) + i - l] * y;
+        if (l + 64 < i) v1 -= M[poff(l + 64, nz) + i - l - 64] * y;
+        if (l == i) v0 = y;
+        if (l + 64 == i) v1 = y;
+    }
+    if (l < ns) v[l] = v0;
+    if (l + 64 < ns) v[l + 64] = v1;
+}
+// L y = v on the first ns columns with the rectangular update of rows up to n (dtrsv_n): v[i] -= L[i][j] y_j.
+__device__ __forceinline__ void wave_solve_ln(double* v, const double* M, const double* dL, int nz, int ns, int n) {
+    const int l = threadIdx.x & 63;
+    double v0 = l < n ? v[l] : 0.0, v1 = l + 64 < n ? v[l + 64] : 0.0;
+    for (int j = 0; j < ns; j++) {
+        const double y = rdlane(j < 64 ? v0 : v1, j & 63) * dL[j];
+        const int cj = poff(j, nz) - j;
+        if (l > j && l < n) v0 -= M[cj + l] * y;
+        if (l + 64 > j && l + 64 < n) v1 -= M[cj + l + 64] * y;
+        if (l == j) v0 = y;
+        if (l + 64 == j) v1 = y;
+    }
+    if (l < n) v[l] = v0;
+    if (l + 64 < n) v[l + 64] = v1;
+}
+
 // C (m x n) = A (m x K) B (K x n) on v_mfma_f64_16x16x4: wave w takes output tiles w, w+4, ..; a(i, k) / b(k, j)
 // read the operands (0 outside), out(i, j, v) stores a result after a workgroup barrier, so C may overwrite
 // an operand.  All threads of the workgroup must call it.  At most 4 * GM_TILES output tiles.
@@ -234,6 +269,11 @@ __device__ __forceinline__ WideProb wide_prob(const WideArgs& a, int p) {
 #else
 #define HK_WIDE_BODY
 #endif
+#ifndef WSUB
+#define WSUB(i) \
+    do {        \
+    } while (0)
+#endif
 __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) {
     extern __shared__ double sm[];
     const int tid = threadIdx.x;
@@ -253,6 +293,7 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
     for (int k = a.N; k >= 0; k--) {
         const WideStage s = a.st[k];
         const int nu = s.nu, nux = s.nu + s.nx, nz = nux + 1, nx1 = s.nx1;
+        WSUB(0);
         load_lower<4>(M, RSQ + s.oR, s.sdR, nz, nux);
         if (q.vq || q.dev_box) {  // device-side q_k row and box terms (d_back_ric_rec.c:197-209, :249-291): the
             bar();           // staged RSQrq is the caller's original, so diag[idxb] = bd + Qx is a += Qx
@@ -267,8 +308,10 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
                 }
         }
         if (k < a.N && !(a.skip & 4)) {
+            WSUB(1);
             load_dense<8>(W, ldW, BAbt + s.oB, s.sdB, nz, nx1);
             bar();
+            WSUB(2);
             if (a.trf) {  // trf factorises without the augmented row: the b row and the gradient row read as 0
                 for (int j = tid; j < nux + nx1; j += WT) {
                     if (j < nx1) W[nux + j * ldW] = 0.0;
@@ -313,6 +356,7 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
                 }
             }
             bar();
+            WSUB(3);
             if (q.compute_Pb && tid < nx1) {  // Pb_k = Lxx (Lxx' b_k) from W's last row before + l
                 double acc = 0.0;
                 for (int j = 0; j <= tid; j++) acc += X[tid + j * ldX] * W[nux + j * ldW];
@@ -321,6 +365,7 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
             bar();
             if (tid < nx1) W[nux + tid * ldW] += X[nx1 + tid * ldX];
             bar();
+            WSUB(4);
             // M += W W' (dsyrk) on MFMA over the lower 16x16 tiles
             {
                 const int nI = (nz + 15) >> 4, nK = (nx1 + 3) >> 2, nT = nI * (nI + 1) / 2;
@@ -348,14 +393,85 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
             bar();
             for (int j = tid; j < nux; j += WT) M[poff(j, nz) + nux - j] = 0.0;
         }
+        WSUB(5);
         if (q.DCt && s.ng > 0) {
             // general constraints: M += [DCt diag(Qx_g) ; qx_g'] DCt' over the lower tiles on MFMA, K = ng
             // (d_back_ric_rec.c:210-231, :292-317); DCt is read from HBM (nux x ng may exceed LDS)
             bar();
+            WSUB(6);
             const double* D = q.DCt + s.oG;
             const double* Qg = q.Qx + s.oD + s.pnb;
             const double* qg = q.qx + s.oD + s.pnb;
             const int ng = s.ng, sdG = s.sdG, nI = (nz + 15) >> 4, nK = (ng + 3) >> 2, nT = nI * (nI + 1) / 2;
+            const int ldS = 16 * nI;
+            if (nT <= 4 * DT_TILES && 16 * ldS + 32 <= a.offV - a.offW) {  // uniform
+                // K blocks of 16 constraints staged in LDS (W and X are free between the syrk and the Cholesky):
+                // the block's DCt columns (zero beyond nux / ng), diag(Qx_g) and the qx_g entries, one memory round
+                // trip per block for the whole workgroup.  Each wave keeps its output tiles in registers across
+                // the blocks; the MFMA chain of a tile runs over the same K chunks in the same order as the direct
+                // loop below, so M gets the same sums.
+                double* Ds = W;
+                double* dqs = W + 16 * ldS;
+                double* qrs = dqs + 16;
+                hk::d4 acc[DT_TILES];
+#pragma unroll
+                for (int u = 0; u < DT_TILES; u++) acc[u] = hk::d4{0.0, 0.0, 0.0, 0.0};
+                for (int kb = 0; kb < ng; kb += 16) {
+                    double r[8];
+#pragma unroll
+                    for (int u = 0; u < 8; u++) {
+                        const int e = u * WT + tid, i = e % ldS, kk = e / ldS;
+                        r[u] = gld(D, p4i(i, kb + kk, sdG), e < 16 * ldS && i < nux && kb + kk < ng);
+                    }
+                    const double dq = gld(Qg, kb + (tid & 15), tid < 16 && kb + tid < ng);
+                    const double qq = gld(qg, kb + (tid & 15), tid < 16 && kb + tid < ng);
+                    bar();  // the previous block's operands are read
+#pragma unroll
+                    for (int u = 0; u < 8; u++) {
+                        const int e = u * WT + tid;
+                        if (e < 16 * ldS) Ds[e] = r[u];  // Ds[i + kk ldS]
+                    }
+                    if (tid < 16) {
+                        dqs[tid] = dq;
+                        qrs[tid] = qq;
+                    }
+                    bar();
+#pragma unroll
+                    for (int u = 0; u < DT_TILES; u++) {
+                        const int t = wv + 4 * u;
+                        if (t < nT) {
+                            int I = 0;
+                            while ((I + 1) * (I + 2) / 2 <= t) I++;
+                            const int J = t - I * (I + 1) / 2;
+                            const int ra = 16 * I + c16, rb = 16 * J + c16;
+#pragma unroll
+                            for (int kc = 0; kc < 4; kc++) {
+                                if (kb + 4 * kc >= ng) break;  // the direct loop's chunk count, nK
+                                const int kk = 4 * kc + g4;
+                                double av = Ds[ra + kk * ldS] * dqs[kk];
+                                if (ra == nux) av = a.trf ? 0.0 : qrs[kk];
+                                const double bv = Ds[rb + kk * ldS];
+                                acc[u] = hk::mfma(av, bv, acc[u]);
+                            }
+                        }
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < DT_TILES; u++) {
+                    const int t = wv + 4 * u;
+                    if (t < nT) {
+                        int I = 0;
+                        while ((I + 1) * (I + 2) / 2 <= t) I++;
+                        const int J = t - I * (I + 1) / 2;
+                        const int col = 16 * J + c16;
+#pragma unroll
+                        for (int rr = 0; rr < 4; rr++) {
+                            const int row = 16 * I + g4 + 4 * rr;
+                            if (row < nz && col < nux && row >= col) M[poff(col, nz) + row - col] += acc[u][rr];
+                        }
+                    }
+                }
+            } else
             for (int t = wv; t < nT; t += 4) {
                 int I = 0;
                 while ((I + 1) * (I + 2) / 2 <= t) I++;
@@ -389,6 +505,7 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
             }
         }
         bar();
+        WSUB(7);
         // Cholesky with the augmented row, blocked by 16-column panels: wave 0 factors the panel (row i on
         // lanes i - j0 and i - j0 + 64, shuffles for the pivot row, no workgroup barrier), then all waves
         // apply the panel's rank-16 update to the trailing lower tiles on MFMA
@@ -443,6 +560,7 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
                 }
             }
             bar();
+            WSUB(8);
             if (pe < nux) {  // trailing update: M[i, jj] -= sum_{k in panel} L[i, k] L[jj, k], tiles from pe
                 const int T0 = pe >> 4, nI = (nz + 15) >> 4, nTI = nI - T0;
                 const int nT = nTI * (nTI + 1) / 2, nK = (pe - p0 + 3) >> 2;
@@ -468,6 +586,7 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
                 }
                 bar();
             }
+            WSUB(9);
         }
         // the factor (packed columns + 1/diag) to HBM in one coalesced sweep
         for (int e = tid; e < poff(nux, nz) + nux; e += WT) Lk[e] = M[e];
@@ -478,6 +597,7 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
             if (i < cc) X[i + cc * ldX] = 0.0;
         }
         bar();
+        WSUB(10);
     }
 
     // forward substitution: L_k (packed + 1/diag) and BAbt_k are staged into LDS (M, W) per stage
@@ -503,14 +623,7 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
         }
         bar();
         // back substitution with L[0:ns, 0:ns]' (inv_diag multiply), column-oriented inside wave 0
-        if (tid < 64) {
-            for (int i = ns - 1; i >= 0; i--) {
-                const double y = v[i] * dL[i];
-                for (int j = tid; j < i; j += 64) v[j] -= M[poff(j, nz) + i - j] * y;
-                if (tid == 0) v[i] = y;
-                wave_sync();
-            }
-        }
+        if (tid < 64) wave_solve_lt(v, M, dL, nz, ns);
         bar();
         for (int j = tid; j < nux; j += WT) ux[s.oU + j] = v[j];
         // x_{k+1} = b_k + BAbt_k' ux_k
@@ -544,6 +657,7 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
             bar();
         }
     }
+    WSUB(11);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -605,15 +719,7 @@ __device__ HK_WIDE_BODY void wide_trs_body(const WideArgs& a, const WideProb& q)
             bar();
             // n-form solve on the first ns columns with the rectangular update (column-oriented, one wave)
             const double* dL = M + poff(nux, nz);
-            if (tid < 64) {
-                for (int j = 0; j < ns; j++) {
-                    const double y = v[j] * dL[j];
-                    const int cj = poff(j, nz) - j;
-                    for (int i = j + 1 + lane; i < nux; i += 64) v[i] -= M[cj + i] * y;
-                    if (lane == 0) v[j] = y;
-                    wave_sync();
-                }
-            }
+            if (tid < 64) wave_solve_ln(v, M, dL, nz, ns, nux);
             bar();
         }
         for (int i = tid; i < nux; i += WT) ux[s.oU + i] = v[i];
@@ -664,14 +770,7 @@ __device__ HK_WIDE_BODY void wide_trs_body(const WideArgs& a, const WideProb& q)
         bar();
         if (tid < ns) v[tid] = r;
         bar();
-        if (tid < 64) {
-            for (int i = ns - 1; i >= 0; i--) {
-                const double y = v[i] * dL[i];
-                for (int j = tid; j < i; j += 64) v[j] -= M[poff(j, nz) + i - j] * y;
-                if (tid == 0) v[i] = y;
-                wave_sync();
-            }
-        }
+        if (tid < 64) wave_solve_lt(v, M, dL, nz, ns);
         bar();
         for (int j = tid; j < nux; j += WT) ux[s.oU + j] = v[j];
         double xn = 0.0;

@@ -19,6 +19,21 @@
 
 #include "hk_launch_guard.h"
 
+#ifdef HK_STAMPS
+// Diagnostic build only: per-phase s_memtime cycle totals of workgroup 0 (tools/wide_phases.py); WSUB marks the
+// sub-phases of the Riccati bodies (hk_wide_core.h)
+__device__ unsigned long long* g_wdbg;
+__device__ unsigned long long g_wsub_t0;
+#define WSUB(i)                                                                             \
+    do {                                                                                    \
+        unsigned long long t_;                                                              \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");           \
+        if (g_wdbg && blockIdx.x == 0 && threadIdx.x == 0) {                                \
+            if ((i) > 0) g_wdbg[11 + (i)] += t_ - g_wsub_t0;                                \
+            g_wsub_t0 = t_;                                                                 \
+        }                                                                                   \
+    } while (0)
+#endif
 #include "hk_wide_core.h"
 
 namespace {
@@ -506,8 +521,6 @@ __device__ __forceinline__ void ric_trs(const WideIpmArgs& A, const IP& P, const
 }  // namespace
 
 #ifdef HK_STAMPS
-// Diagnostic build only: per-phase s_memtime cycle totals of workgroup 0 (tools/wide_phases.py)
-__device__ unsigned long long* g_wdbg;
 extern "C" __attribute__((visibility("default"))) int hk_wide_ipm_debug(void* dev_ptr) {
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_wdbg), &dev_ptr, sizeof(void*));
 }

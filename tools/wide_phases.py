@@ -31,3 +31,10 @@ tot = t[:10].sum()
 print(f"batch {B}: problem 0, {t[31]} stamps, {tot} cycles in the phase-2 loop")
 for i, n in enumerate(names):
     print(f"  {n:20s} {t[i]:12d}  {100.0 * t[i] / max(tot, 1):5.1f} %")
+sub = ["stage top -> W load", "W load (lib4 -> LDS)", "W = BAbt Lxx (MFMA)", "Pb, row", "syrk W W' (MFMA)",
+       "-> general terms", "DCt diag DCt' (MFMA)", "panel factor (wave 0)", "trailing update (MFMA)",
+       "factor store, Lxx copy", "forward substitution"]
+st = t[12:23]
+print(f"  inside every ric_sv of the solve (phase 1 included), {st.sum()} cycles:")
+for i, n in enumerate(sub):
+    print(f"    {n:26s} {st[i]:12d}  {100.0 * st[i] / max(st.sum(), 1):5.1f} %")
