@@ -13,6 +13,28 @@
 
 #include "hk_wide_core.h"
 
+#ifdef HK_STAMPS
+// Diagnostic build only: per-phase s_memtime cycle totals of hk_pcond workgroup (0, 0) (tools/pcond_phases.py)
+__device__ unsigned long long* g_pdbg;
+__device__ unsigned long long g_pst_t0;
+extern "C" __attribute__((visibility("default"))) int hk_pcond_debug(void* dev_ptr) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_pdbg), &dev_ptr, sizeof(void*));
+}
+#define PST(i)                                                                                  \
+    do {                                                                                        \
+        unsigned long long t_;                                                                  \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");               \
+        if (g_pdbg && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {                 \
+            if ((i) > 0) g_pdbg[i] += t_ - g_pst_t0;                                            \
+            g_pst_t0 = t_;                                                                      \
+        }                                                                                       \
+    } while (0)
+#else
+#define PST(i) \
+    do {       \
+    } while (0)
+#endif
+
 
 // d_back_ric_rec_sv_tv_res / _trf_tv_res on wide stages (wide_sv_body, hk_wide_core.h)
 __global__ __launch_bounds__(WT) void hk_wide_sv(WideArgs a) {
@@ -67,6 +89,7 @@ __global__ __launch_bounds__(WT, 4) void hk_pcond(PcArgs a) {  // 4 waves per SI
     // held in registers, then overwrites GA and streams to HBM ----
     double* GA = sm + a.offGA;
     const int ph = a.ph;
+    PST(0);
     if (ph & PC_BABT) {
     {
         const WideStage s = st[0];
@@ -84,11 +107,13 @@ __global__ __launch_bounds__(WT, 4) void hk_pcond(PcArgs a) {  // 4 waves per SI
         const int nuj = s.nu, nxj = s.nx, nx1 = s.nx1, nzj = nuj + nxj + 1;
         const int rp = rows(j - 1), rj = rp + nuj, n = rj * nx1;
         double* Gj = G + goff(j);
+        PST(1);
         if (staged)
             put_dense(nb, Bt, ldB);
         else
             load_dense<8>(Bt, ldB, BAbt + s.oB, s.sdB, nzj, nx1);
         bar();
+        PST(2);
         staged = false;
         if (j + 1 < ((a.skip & 1) ? 1 : T)) {
             const WideStage sn = st[j + 1];
@@ -115,6 +140,7 @@ __global__ __launch_bounds__(WT, 4) void hk_pcond(PcArgs a) {  // 4 waves per SI
         }
         (void)n;
         bar();
+        PST(3);
     }
     {
         const int rT = rows(T - 1), nxT = st[T - 1].nx1;
@@ -126,6 +152,7 @@ __global__ __launch_bounds__(WT, 4) void hk_pcond(PcArgs a) {  // 4 waves per SI
     }
     }  // PC_BABT
     bar();  // Gamma scratch complete (written by this block's threads) before the later phases read it
+    PST(4);
 
     // ---- d_cond_RSQrq ----
     const int cnux2 = (nv + 1) / 2 * 2;
@@ -179,6 +206,7 @@ __global__ __launch_bounds__(WT, 4) void hk_pcond(PcArgs a) {  // 4 waves per SI
             for (int j = tid >> 6; j < nxs; j += WT / 64)
                 for (int i = j + (tid & 63); i <= nxs; i += 64) X[i + j * ldX] = Pl[nus + i + (nus + j) * ldP];
             bar();
+            PST(5);
             // M: Gamma_{s-1} times the x_s x u_s block of pL; m: + the r row on the gradient row
             for (int e = tid; e < ((a.skip & 8) ? 0 : r0 * nus); e += WT) {
                 const int i = e % r0, c = e / r0;
@@ -187,6 +215,7 @@ __global__ __launch_bounds__(WT, 4) void hk_pcond(PcArgs a) {  // 4 waves per SI
                 if (i == r0 - 1) acc += Pl[nux + c * ldP];
                 *P4w(R2, cnux2, os + nus + i, os + c) = acc;
             }
+            PST(6);
             // Lx = chol_aug(X) inside wave 0 (row i on lane i, nxs + 1 <= 64 rows): 16-column panels factored in
             // registers (pivot values broadcast by readlane), each followed by its update of the later columns
             if (tid < 64 && !(a.skip & 4)) {
@@ -224,6 +253,7 @@ __global__ __launch_bounds__(WT, 4) void hk_pcond(PcArgs a) {  // 4 waves per SI
                 }
             }
             bar();
+            PST(7);
             // W = BAbt_{s-1} Lx (in place in Bt, row i by one thread), last row += l; pL = RSQ_{s-1} + W W'
             if (stg) {
                 put_dense(pb, Bt, ldB);
@@ -233,6 +263,7 @@ __global__ __launch_bounds__(WT, 4) void hk_pcond(PcArgs a) {  // 4 waves per SI
                 load_dense<8>(Pl, ldP, RSQ + sp.oR, sp.sdR, nzp, nuxp);
             }
             bar();
+            PST(8);
             if (!(a.skip & 16)) {
                 // W = BAbt_{s-1} Lx (+ l on the last row) in place over Bt, then pL += W W' (lower), both on MFMA
                 mfma_gemm(
@@ -251,6 +282,7 @@ __global__ __launch_bounds__(WT, 4) void hk_pcond(PcArgs a) {  // 4 waves per SI
                     });
             }
             bar();
+            PST(9);
         }
     }
     }  // PC_RSQ
@@ -345,6 +377,7 @@ __global__ __launch_bounds__(WT, 4) void hk_pcond(PcArgs a) {  // 4 waves per SI
             for (int i = ln; i < rowsI; i += 64) *P4w(G2, cnbg, nt + i, ig) = Gp[i + g * r0];
         }
     }
+    PST(10);
     // the terminal condensed stage is the original's (d_part_cond.c:1052-1056): block N2-1 copies it
     if (ii == a.N2 - 1 && !(ph & PC_PART)) {
         const WideStage sN = a.st[a.N];
