@@ -12,6 +12,8 @@ step tests timeout -k 10 900 python3 -u -m pytest tests -m gpu -q -x --timeout 3
 step smoke timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()"
 step pmc bash tools/pmc_mix.sh
 cp gpurun_out/pmc_hk_ipm.json profiles/pmc_hk_ipm.json && cp gpurun_out/pmc_mix.json gpurun_out/${R}_pmc_mix.json
+step hbmbw timeout -k 10 120 python3 tools/hbm_bw.py
+grep '^{' gpurun_out/hbmbw.log | tail -1 > gpurun_out/${R}_hbm_bw.json
 step bench timeout -k 10 600 python3 bench.py
 grep '^{' gpurun_out/bench.log | tail -1 > gpurun_out/${R}_bench.json
 # kernel stats of the timed region only: no warmup queue, no isolated batch, so every hk_ipm_* launch
