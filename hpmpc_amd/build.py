@@ -16,7 +16,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("HPMPC_ARCH", "gfx950")
 SOURCES = ["hpmpc_kernels.hip", "hk_wide.hip", "hk_wide_ipm.hip", "hk_soft.hip", "hpmpc_capi.cpp", "hpmpc_capi_wide.cpp",
            "hpmpc_capi_wide_ipm.cpp", "hpmpc_capi_iface.cpp", "hpmpc_capi_mpc.cpp"]
-HEADERS = ["hpmpc_api.h", "hk_prims.h", "hk_riccati.h", "hk_ipm.h", "hpmpc_kargs.h", "hk_wide_args.h", "hk_wide_core.h", "hk_wide_host.h", "hk_soft_args.h", "hk_launch_guard.h"]
+HEADERS = ["hpmpc_api.h", "hk_prims.h", "hk_riccati.h", "hk_ipm.h", "hk_mw.h", "hpmpc_kargs.h", "hk_wide_args.h", "hk_wide_core.h", "hk_wide_host.h", "hk_soft_args.h", "hk_launch_guard.h"]
 # MFMA accumulators stay in ordinary VGPRs: the stage tile is read and written by VALU code between
 # MFMAs, and the AGPR form costs 8 v_accvgpr moves each way per MFMA group.
 KFLAGS = ["-mllvm", "-amdgpu-mfma-vgpr-form"] + os.environ.get("HK_EXTRA_FLAGS", "").split()
@@ -36,6 +36,26 @@ def _newer(out, deps):
     return all(os.path.getmtime(d) <= t for d in deps)
 
 
+def _deps(src, hdrs_all):
+    """The headers a source reaches through its quoted #include lines (transitively, within csrc/ and include/)."""
+    import re
+    seen, todo = set(), [os.path.join(CSRC, src)]
+    while todo:
+        path = todo.pop()
+        try:
+            text = open(path).read()
+        except OSError:
+            continue
+        for name in re.findall(r'^\s*#\s*include\s+"([^"]+)"', text, re.M):
+            for cand in (os.path.join(os.path.dirname(path), name), os.path.join(CSRC, name),
+                         os.path.join(ROOT, "include", os.path.basename(name))):
+                if os.path.exists(cand) and cand not in seen:
+                    seen.add(cand)
+                    todo.append(cand)
+                    break
+    return sorted(seen | {h for h in hdrs_all if os.path.basename(h) == "hpmpc_mi355x.h"})
+
+
 def build_hip(force: bool = False, verbose: bool = False) -> str:
     """Each source compiles to its own object under build/ (rebuilt when it or a header is newer), then one
     link; a one-file change recompiles one translation unit."""
@@ -43,7 +63,7 @@ def build_hip(force: bool = False, verbose: bool = False) -> str:
     objdir = os.path.join(ROOT, "build", "obj")
     os.makedirs(objdir, exist_ok=True)
     out = os.path.join(LIBDIR, "libhpmpc_mi355x.so")
-    hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, "include", "hpmpc_mi355x.h")]
+    hdrs_all = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, "include", "hpmpc_mi355x.h")]
     # -fvisibility=hidden: only include/hpmpc_mi355x.h's functions are exported (csrc/hpmpc_api.h)
     common = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall",
               "-Wno-unused-function"] + KFLAGS
@@ -51,7 +71,7 @@ def build_hip(force: bool = False, verbose: bool = False) -> str:
     for src in SOURCES:
         obj = os.path.join(objdir, src + ".o")
         objs.append(obj)
-        if force or not _newer(obj, [os.path.join(CSRC, src)] + hdrs):
+        if force or not _newer(obj, [os.path.join(CSRC, src)] + _deps(src, hdrs_all)):
             cmd = common + SRC_FLAGS.get(src, []) + ["-c", os.path.join(CSRC, src), "-o", obj]
             if verbose:
                 print(" ".join(cmd), flush=True)

@@ -78,6 +78,30 @@ __device__ __forceinline__ QuadLane quad_lane(const RicIO& io, int q) {
     return b;
 }
 
+// Multi-wave split of the element-wise update passes (the one-problem-per-workgroup solo kernel, hk_mw.h): wave w
+// of NW takes the quad chunks w, w + NW, ...; each quad's per-lane r_m contribution goes to red[q * 64 + lane] and
+// every wave then sums all of them in quad order -- the single-wave loop's order, so mu is bitwise the same.
+typedef __attribute__((address_space(3))) double lds_f64;  // an LDS pointer that stays one through memory
+
+struct MwSplit {
+    int w;
+    lds_f64* red;  // round_up(nq, CH) x 64 doubles
+};
+
+template <int NW>
+__device__ __forceinline__ double mw_quad_sum(const MwSplit& ms, int nq_pad, double ms_local) {
+    if constexpr (NW == 1) {
+        return ms_local;
+    } else {
+        const int l = lane_id();
+        __syncthreads();
+        double m = 0.0;
+        for (int q = 0; q < nq_pad; q++) m += ms.red[q * 64 + l];
+        __syncthreads();  // red is written again by the next pass
+        return m;
+    }
+}
+
 // d_compute_mu_[res_]mpc_hard_tv: mu_aff = sum (lam + alpha dlam)(t + alpha dt) * mu_scal
 template <int CH>
 __device__ double mu_aff_pass(const RicIO& io, const BoxCtx& bc, double alpha, double mu_scal) {
@@ -107,14 +131,14 @@ __device__ double mu_aff_pass(const RicIO& io, const BoxCtx& bc, double alpha, d
 
 // Phase-1 update (d_update_var_mpc_hard_tv :618-711 with the backups of :721-732): the phase-1 dux/dpi
 // are full iterates, so ux += alpha (dux - ux).  Returns mu = sum lam t * mu_scal of the new iterate.
-template <int CH>
+template <int CH, int NW = 1>
 __device__ double update_p1_pass(const RicIO& io, const BoxCtx& bc, double alpha, double mu_scal, double* ux,
                                  double* pi, const double* dux, const double* dpi, double* ux_bkp, double* pi_bkp,
-                                 double* lam_bkp, double* t_bkp) {
+                                 double* lam_bkp, double* t_bkp, const MwSplit& mws = MwSplit{0, nullptr}) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
     const int nq = (io.N + 4) / 4;
     double ms = 0.0;
-    for (int q0 = 0; q0 < nq; q0 += CH) {
+    for (int q0 = NW > 1 ? mws.w * CH : 0; q0 < nq; q0 += NW * CH) {
         double v[CH][12];
         int i16[CH];
         bool oku[CH], okp[CH];
@@ -160,9 +184,14 @@ __device__ double update_p1_pass(const RicIO& io, const BoxCtx& bc, double alpha
             gst(bc.lam, b.up, lu, b.ok);
             gst(bc.t, b.lo, tl, b.ok);
             gst(bc.t, b.up, tu, b.ok);
-            ms += b.ok ? ll * tl + lu * tu : 0.0;
+            const double mc = b.ok ? ll * tl + lu * tu : 0.0;
+            if constexpr (NW > 1)
+                mws.red[(q0 + j) * 64 + l] = mc;
+            else
+                ms += mc;
         }
     }
+    ms = mw_quad_sum<NW>(mws, (nq + CH - 1) / CH * CH, ms);
     return wave_sum(ms) * mu_scal;
 }
 
@@ -174,15 +203,15 @@ __device__ double update_p1_pass(const RicIO& io, const BoxCtx& bc, double alpha
 // slot lane with the same arithmetic as in its own lane.
 // BKP = false (the public queue API, whose per-slot workspace never feeds a KKT re-solve): the iterate
 // backups and r_m, which only hk_kkt_new_rhs (and general constraints) read, are not written.
-template <int CH, bool UPD, bool BKP = true>
+template <int CH, bool UPD, bool BKP = true, int NW = 1>
 __device__ double update_p2_pass(const RicIO& io, const BoxCtx& bc, const signed char* slotvar, double alpha,
                                  double mu_scal, double* ux, double* pi, const double* dux, const double* dpi,
                                  double* ux_bkp, double* pi_bkp, double* lam_bkp, double* t_bkp, double* res_d,
-                                 double* res_m) {
+                                 double* res_m, const MwSplit& mws = MwSplit{0, nullptr}) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
     const int nq = (io.N + 4) / 4;
     double ms = 0.0;
-    for (int q0 = 0; q0 < nq; q0 += CH) {
+    for (int q0 = NW > 1 ? mws.w * CH : 0; q0 < nq; q0 += NW * CH) {
         double v[CH][16];
         int i16[CH], iv[CH];
         bool oku[CH], okp[CH];
@@ -253,9 +282,14 @@ __device__ double update_p2_pass(const RicIO& io, const BoxCtx& bc, const signed
                 gst(res_m, b.lo, rml, b.ok);
                 gst(res_m, b.up, rmu, b.ok);
             }
-            ms += b.ok ? rml + rmu : 0.0;
+            const double mc = b.ok ? rml + rmu : 0.0;
+            if constexpr (NW > 1)
+                mws.red[(q0 + j) * 64 + l] = mc;
+            else
+                ms += mc;
         }
     }
+    ms = mw_quad_sum<NW>(mws, (nq + CH - 1) / CH * CH, ms);
     return wave_sum(ms) * mu_scal;
 }
 

@@ -875,27 +875,31 @@ __device__ __forceinline__ void bwd_residual(const RicIO& io, Scratch* sm, const
     for (int r = 0; r < 4; r++) f.brow[r] = br[r];
 }
 
-// One backward stage: M = RSQ + BAbt P BAbt' (+ box terms), then the stage factorisation (P form on
-// stages k >= 1, see stage_chol).  S (in: record of stage k+1, whose x block is P_{k+1}; out: record of
-// stage k), ml/invd/kg likewise.  The reference forms the same M as RSQ + W W' with W = BAbt Lxx
-// (dtrmm_nt_u + dsyrk, d_back_ric_rec.c:262-264, :325) and the same row as W (Lxx' b + l_x) (:266-276).
+// First half of a backward stage: the stage tile and augmented row with the box (and general) Hessian /
+// gradient terms added -- everything that does not depend on the recursion (the multi-wave solo kernel runs it
+// on a helper wave, hk_mw.h).
 template <bool AUG, int BM, class SH>
-__device__ __forceinline__ void bwd_step(const RicIO& io, Scratch* sm, const SH& sh, int k, const BwdFrag& cur,
-                                         const BoxCtx& bc, int compute_Pb, double* Pb, d4& S, double& ml_prev,
-                                         double& invd_prev, double& kg_prev) {
+__device__ __forceinline__ void bwd_pre(const RicIO& io, const SH& sh, int k, const BwdFrag& cur, const BoxCtx& bc,
+                                        d4& M, double& ml) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
-    const bool live = SH::fixed || k < io.N;
     double dq, qxv;
     box_hessian<AUG, BM>(bc, cur, dq, qxv);
-    const double mlq = cur.mlq;
-    const d4 brow = cur.brow;
-    d4 M = cur.Mi;
-    double ml = mlq + qxv;  // update_q row (or RSQrq row) + drowad qx
+    M = cur.Mi;
+    ml = cur.mlq + qxv;  // update_q row (or RSQrq row) + drowad qx
 #pragma unroll
     for (int r = 0; r < 4; r++) M[r] += (g + 4 * r == c) ? dq : 0.0;  // ddiaadin: diag = bd + Qx
     if constexpr (!SH::fixed && BM != BX_NONE) {
         if (sh.ng > 0) gen_hessian<BM>(io, sh, k, bc, BM == BX_P2R ? cur.uc : 0.0, M, ml, AUG);
     }
+}
+
+// Second half: M += BAbt P BAbt', the row update and the stage factorisation (the recursion's chain).
+template <bool AUG, class SH>
+__device__ __forceinline__ void bwd_core(const RicIO& io, Scratch* sm, const SH& sh, int k, const d4& bop,
+                                         const d4& brow, d4 M, double ml, int compute_Pb, double* Pb, d4& S,
+                                         double& ml_prev, double& invd_prev, double& kg_prev) {
+    const int l = lane_id(), g = l >> 4, c = l & 15;
+    const bool live = SH::fixed || k < io.N;
     const int nx1 = sh.nx1, xo1 = sh.xo1;
     const bool xc = c >= xo1;  // tile column c is a state of stage k+1 (padding beyond xo1+nx1 is zero)
     if (live) {
@@ -909,9 +913,9 @@ __device__ __forceinline__ void bwd_step(const RicIO& io, Scratch* sm, const SH&
             // lanes c < xo1 (u rows of stage k+1) only produce rows of T' that the second chain skips: no mask
             const double aop = S[kc];
             if (kc & 1)
-                a1 = mfma(aop, cur.bop[kc], a1);
+                a1 = mfma(aop, bop[kc], a1);
             else
-                a0 = mfma(aop, cur.bop[kc], a0);
+                a0 = mfma(aop, bop[kc], a0);
         }
         const d4 acc = a0 + a1;
         // M += BAbt_k T'  (A fragment of chunk r = the BAbt operand already in registers), two chains
@@ -920,9 +924,9 @@ __device__ __forceinline__ void bwd_step(const RicIO& io, Scratch* sm, const SH&
         for (int r = 0; r < 4; r++) {
             if (4 * r + 3 < xo1 || 4 * r >= xo1 + nx1) continue;
             if (r & 1)
-                m1 = mfma(cur.bop[r], acc[r], m1);
+                m1 = mfma(bop[r], acc[r], m1);
             else
-                M = mfma(cur.bop[r], acc[r], M);
+                M = mfma(bop[r], acc[r], M);
         }
         M = M + m1;
     }
@@ -940,7 +944,7 @@ __device__ __forceinline__ void bwd_step(const RicIO& io, Scratch* sm, const SH&
         col2row(sm, wc, wrow);
         double mp = 0.0;
 #pragma unroll
-        for (int r = 0; r < 4; r++) mp += cur.bop[r] * wrow[r];
+        for (int r = 0; r < 4; r++) mp += bop[r] * wrow[r];
         if (live) ml += xrow_sum(mp);
     }
     HK_STAMP(2, k);
@@ -954,6 +958,20 @@ __device__ __forceinline__ void bwd_step(const RicIO& io, Scratch* sm, const SH&
     for (int r = 0; r < 4; r++) S[r] = M[r];
     ml_prev = ml;
     invd_prev = invd;
+}
+
+// One backward stage: M = RSQ + BAbt P BAbt' (+ box terms), then the stage factorisation (P form on
+// stages k >= 1, see stage_chol).  S (in: record of stage k+1, whose x block is P_{k+1}; out: record of
+// stage k), ml/invd/kg likewise.  The reference forms the same M as RSQ + W W' with W = BAbt Lxx
+// (dtrmm_nt_u + dsyrk, d_back_ric_rec.c:262-264, :325) and the same row as W (Lxx' b + l_x) (:266-276).
+template <bool AUG, int BM, class SH>
+__device__ __forceinline__ void bwd_step(const RicIO& io, Scratch* sm, const SH& sh, int k, const BwdFrag& cur,
+                                         const BoxCtx& bc, int compute_Pb, double* Pb, d4& S, double& ml_prev,
+                                         double& invd_prev, double& kg_prev) {
+    d4 M;
+    double ml;
+    bwd_pre<AUG, BM>(io, sh, k, cur, bc, M, ml);
+    bwd_core<AUG>(io, sm, sh, k, cur.bop, cur.brow, M, ml, compute_Pb, Pb, S, ml_prev, invd_prev, kg_prev);
 }
 
 // Backward Riccati recursion (sv when AUG, trf otherwise), d_back_ric_rec.c:186-335 / :447-558.

@@ -6,7 +6,9 @@
 // All IPM control flow (iteration count, step length, mu) is per wave, so problems that converge
 // early simply retire their wave.
 #include "hk_ipm.h"
+#include "hk_mw.h"
 #include "hpmpc_kargs.h"
+#include <cstdlib>
 
 using namespace hk;
 
@@ -415,19 +417,20 @@ __device__ __forceinline__ ResIO res_io(const IpmView& v) {
 // Phase-2 start residuals: r_d, r_m and mu here; r_q, r_b in the first phase-2 factorisation.  CI: stages
 // per chunk of the element-wise passes (7 in hk_ipm_init; 2 inside hk_ipm_update, where the problem-start and
 // phase-switch paths run once per problem and must not raise the update loop's register allocation).
-template <class FX, int CI>
-__device__ double p2_start(const KArgs& a, IpmView& v) {
-    const double mu = update_p2_pass<CI, false>(v.io, v.bc, v.bt.slotvar, 0.0, 1.0 / (2.0 * a.nbt), v.ux, v.pi,
-                                               nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, v.w.res_d,
-                                               v.w.res_m);
+template <class FX, int CI, int NW = 1>
+__device__ double p2_start(const KArgs& a, IpmView& v, const MwSplit& mws = MwSplit{0, nullptr}) {
+    const double mu = update_p2_pass<CI, false, true, NW>(v.io, v.bc, v.bt.slotvar, 0.0, 1.0 / (2.0 * a.nbt), v.ux,
+                                                          v.pi, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                                          v.w.res_d, v.w.res_m, mws);
     wsync();
     return mu;
 }
 
 // End of an iteration (or of init): decide whether the problem continues, switching from phase 1 to
 // phase 2 (with the phase-2 start residuals) when phase 1's loop condition fails.
-template <class FX, int CI>
-__device__ bool ipm_continue(const KArgs& a, IpmView& v, int kk, double mu, double alpha, double sigma, int phase) {
+template <class FX, int CI, int NW = 1>
+__device__ bool ipm_continue(const KArgs& a, IpmView& v, int kk, double mu, double alpha, double sigma, int phase,
+                             const MwSplit& mws = MwSplit{0, nullptr}) {
     const bool sn = a.single_newton != 0;
     bool active;
     if (a.phase1_only) {  // d_ip2_mpc_hard_tv: the phase-1 loop run to mu_tol (d_ip2_hard.c:329-520)
@@ -436,7 +439,7 @@ __device__ bool ipm_continue(const KArgs& a, IpmView& v, int kk, double mu, doub
         if (phase == 1) {
             const double mu_tol_low = a.mu_tol < 1e-5 ? 1e-5 : a.mu_tol;
             if (!(kk < a.k_max && mu > mu_tol_low && alpha >= a.alpha_min)) {
-                mu = p2_start<FX, CI>(a, v);  // phase-2 start (d_ip2_res_hard.c:756-781)
+                mu = p2_start<FX, CI, NW>(a, v, mws);  // phase-2 start (d_ip2_res_hard.c:756-781)
                 phase = 2;
             }
         }
@@ -764,6 +767,198 @@ __global__ __launch_bounds__(64) void hk_ipm_solo(KArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// The same solve with one problem per 256-thread workgroup (hk_mw.h): wave 0 runs each sweep's recursion, waves
+// 1..3 everything off it, and the element-wise update is split over the four waves.  Every body keeps the
+// single-wave body's arithmetic (same routines, same operands, mu summed in the same order), so the iterates are
+// bitwise hk_ipm_solo's.  All four waves run every body, so that they meet the same barriers in the same order;
+// the loop-control state is read by all and written by thread 0 (IpmView.l = threadIdx.x here).
+// ------------------------------------------------------------------------------------------------
+namespace {
+
+template <class FX>
+__device__ __forceinline__ void fact_body_mw(const KArgs& a, IpmView& v, int& tb, int w) {
+    const double* st = v.w.state;
+    const bool sn = a.single_newton != 0;
+    if (st[S_PHASE] == 1.0)
+        tb = ric_backward_mw<true, BX_P1, FX>(v.io, tb, w, 0, nullptr, 0, nullptr, v.bc, 1, v.w.Pb);
+    else {
+        v.bc.res_rhs = !sn;
+        v.bc.no_tinv = a.no_bkp;
+        tb = ric_backward_mw<true, BX_P2R, FX>(v.io, tb, w, 0, nullptr, 0, nullptr, v.bc, 1, v.w.Pb);
+    }
+}
+
+template <class FX>
+__device__ __forceinline__ void pred_body_mw(const KArgs& a, IpmView& v, int& tb, int w) {
+    double* st = v.w.state;
+    const bool sn = a.single_newton != 0;
+    const int phase = (int)st[S_PHASE], kk = (int)st[S_KK];
+    const double mu = st[S_MU];
+    double sigma = st[S_SIGMA];
+    double al = 1.0;
+    if (phase == 1) {
+        v.bc.pred = 1;
+        tb = ric_forward_mw<0, BX_P1, FX, true>(v.io, tb, w, nullptr, 0, v.w.dux, 0, v.w.dpi, v.bc, al);
+    } else {
+        tb = ric_forward_mw<0, BX_P2, FX, true>(v.io, tb, w, v.w.res_b, !sn, v.w.dux, 0, v.w.dpi, v.bc, al);
+    }
+    // al is the workgroup minimum in every wave, and the helpers' dt / dlam stores are visible (the sweep ends with
+    // a barrier): every wave forms the same mu_aff and sigma
+    const double alpha = al * 0.995;
+    double mu_aff;
+    {  // callees that may stay out of line get their own copies, so that the view itself never escapes to memory
+        const RicIO io = v.io;
+        const BoxCtx bc = v.bc;
+        mu_aff = mu_aff_pass<7>(io, bc, alpha, st[S_MUSCAL]);
+    }
+    double smu = a.mu0;
+    if (!sn) {
+        sigma = mu_aff / mu;
+        sigma = sigma * sigma * sigma;
+        smu = sigma * mu;
+    }
+    __syncthreads();  // every wave has read the state before thread 0 rewrites it
+    if (v.l == 0) {
+        v.stat[5 * kk] = st[S_SIGMA];
+        v.stat[5 * kk + 1] = al;
+        v.stat[5 * kk + 2] = mu_aff;
+        st[S_SIGMA] = sigma;
+        st[S_SMU] = smu;
+    }
+}
+
+template <class FX>
+__device__ __forceinline__ void corr_body_mw(const KArgs& a, IpmView& v, int& tb, int w) {
+    double* st = v.w.state;
+    const int phase = (int)st[S_PHASE], kk = (int)st[S_KK];
+    v.bc.smu = st[S_SMU];
+    double al = 1.0;
+    if (phase == 1)
+        tb = ric_trs_mw<BX_P1, BX_P1, FX>(v.io, tb, w, nullptr, nullptr, v.bc, v.w.dux, a.compute_mult, v.w.dpi,
+                                     v.w.Pb, al);
+    else
+        tb = ric_trs_mw<BX_P2, BX_P2, FX>(v.io, tb, w, v.w.res_b, v.w.res_q, v.bc, v.w.dux, a.compute_mult, v.w.dpi,
+                                     v.w.Pb, al);
+    if (v.l == 0) {
+        v.stat[5 * kk] = st[S_SIGMA];
+        v.stat[5 * kk + 3] = al;
+        st[S_ALPHA] = al * 0.995;
+    }
+}
+
+template <class FX, int CI>
+__device__ __forceinline__ bool update_body_mw(const KArgs& a, const IpmView& v0, const MwSplit& mws0) {
+    IpmView v = v0;  // a copy: the out-of-line passes below take it by reference
+    const MwSplit mws = mws0;
+    double* st = v.w.state;
+    const int phase = (int)st[S_PHASE];
+    int kk = (int)st[S_KK];
+    const double alpha = st[S_ALPHA];
+    const double sigma = st[S_SIGMA];
+    double mu;
+    if (phase == 1) {
+        mu = update_p1_pass<CI, MW_WAVES>(v.io, v.bc, alpha, st[S_MUSCAL], v.ux, v.pi, v.w.dux, v.w.dpi, v.w.ux_bkp,
+                                          v.w.pi_bkp, v.w.lam_bkp, v.w.t_bkp, mws);
+    } else {
+        if (a.no_bkp)
+            mu = update_p2_pass<CI, true, false, MW_WAVES>(v.io, v.bc, v.bt.slotvar, alpha, st[S_MUSCAL], v.ux, v.pi,
+                                                           v.w.dux, v.w.dpi, v.w.ux_bkp, v.w.pi_bkp, v.w.lam_bkp,
+                                                           v.w.t_bkp, v.w.res_d, v.w.res_m, mws);
+        else
+            mu = update_p2_pass<CI, true, true, MW_WAVES>(v.io, v.bc, v.bt.slotvar, alpha, st[S_MUSCAL], v.ux, v.pi,
+                                                          v.w.dux, v.w.dpi, v.w.ux_bkp, v.w.pi_bkp, v.w.lam_bkp,
+                                                          v.w.t_bkp, v.w.res_d, v.w.res_m, mws);
+    }
+    wsync();
+    if (v.l == 0) v.stat[5 * kk + 4] = mu;
+    kk++;
+    return ipm_continue<FX, CI, MW_WAVES>(a, v, kk, mu, alpha, sigma, phase, mws);
+}
+
+// LDS of the multi-wave kernel: the stage tables (lds_tables, dynamic) beside the static hk_mw object
+__host__ __device__ constexpr size_t mw_lds_bytes(int N) {
+    return sizeof(Scratch) + (size_t)(N + 1) * (sizeof(StageInfo) + 32);
+}
+
+}  // namespace
+
+template <class FX>
+__global__ __launch_bounds__(256) void hk_ipm_solo_mw(KArgs a) {
+    const LdsTabs T = lds_tables(a);
+    const int p = blockIdx.x + a.p0;
+    if (p >= a.nprob) return;
+    if (carve(a.ws + (long)p * a.sW, a.N).state[S_ACTIVE] == 0.0) return;
+    const int w = threadIdx.x >> 6;
+    if (threadIdx.x < MW_D) {
+        hk_mw.full[threadIdx.x] = 0;
+        hk_mw.freed[threadIdx.x] = 0;
+    }
+    if (threadIdx.x == 0) hk_mw.err = 0;
+    __syncthreads();
+    int tb = 0;
+    const MwSplit mws{w, (lds_f64*)&hk_mw.red[0][0]};
+    const Who who{p, p, p};
+#ifdef HK_STAMPS
+    // diagnostic build: cycles per body (summed over the iterations) and per wave in hand-over waits, problem 0
+    unsigned long long tph[4] = {0, 0, 0, 0}, tm = 0;
+    if (threadIdx.x < MW_WAVES) hk_mw.wait_cyc[threadIdx.x] = 0;
+#define HK_MW_PHASE(i)                            \
+    do {                                          \
+        const unsigned long long t_ = mw_clock(); \
+        if (i >= 0) tph[i] += t_ - tm;            \
+        tm = t_;                                  \
+    } while (0)
+#else
+#define HK_MW_PHASE(i) \
+    do {               \
+    } while (0)
+#endif
+    for (int it = 0; it < a.k_max; it++) {
+        __syncthreads();
+        HK_MW_PHASE(-1);
+        {
+            IpmView v = ipm_view(a, T, who);
+            v.l = threadIdx.x;  // thread 0 alone writes the control state and the statistics
+            fact_body_mw<FX>(a, v, tb, w);
+        }
+        __syncthreads();
+        HK_MW_PHASE(0);
+        {
+            IpmView v = ipm_view(a, T, who);
+            v.l = threadIdx.x;
+            pred_body_mw<FX>(a, v, tb, w);
+        }
+        __syncthreads();
+        HK_MW_PHASE(1);
+        {
+            IpmView v = ipm_view(a, T, who);
+            v.l = threadIdx.x;
+            corr_body_mw<FX>(a, v, tb, w);
+        }
+        __syncthreads();
+        HK_MW_PHASE(2);
+        IpmView v = ipm_view(a, T, who);
+        v.l = threadIdx.x;
+        const bool again = update_body_mw<FX, 4>(a, v, mws);
+        __syncthreads();
+        HK_MW_PHASE(3);
+        // an expired hand-over wait (a bug, never a data condition) ends the solve with HK_MW_ERR
+        if (!again || __atomic_load_n(&hk_mw.err, __ATOMIC_RELAXED)) break;
+    }
+#ifdef HK_STAMPS
+    if (a.dbg && p == 0 && threadIdx.x == 0) {
+        for (int i = 0; i < 4; i++) a.dbg[32 + i] = tph[i];
+        for (int i = 0; i < MW_WAVES; i++) a.dbg[40 + i] = hk_mw.wait_cyc[i];
+    }
+#endif
+#undef HK_MW_PHASE
+    if (threadIdx.x == 0 && hk_mw.err) {
+        a.ret[p] = HK_MW_ERR;
+        for (int i = 0; i < 4; i++) a.stat[(long)p * 5 * a.k_max + i] = hk_mw.dbg[i];
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // d_kkt_solve_new_rhs_res_mpc_hard_tv: re-solve with the factor + iterate persisted in ws.
 // vb/vq hold the new b (state order) / q (variable order).
 // ------------------------------------------------------------------------------------------------
@@ -956,9 +1151,26 @@ static int launch_t(int which, const KArgs* a, int count, hipStream_t stream) {
         case 14: hipLaunchKernelGGL(hk_ipm_update<FX>, grid, block, lds, stream, *a); break;
         // the whole IPM per problem in one launch (hk_ipm_solo)
         case 15:
+        case 16: {
+            // one problem per 256-thread workgroup (hk_ipm_solo_mw) unless its LDS carve does not fit or
+            // HPMPC_MI355X_SOLO=1 asks for the single-wave kernel; which == 16 forces the single-wave one
+            static int lds_max = -1;
+            if (lds_max < 0) {
+                int dev = 0, v = 0;
+                (void)hipGetDevice(&dev);
+                (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, dev);
+                lds_max = v;
+            }
+            const char* env = getenv("HPMPC_MI355X_SOLO");
+            const bool single = which == 16 || (env && env[0] == '1');
+            const size_t lds_mw = mw_lds_bytes(a->N);
             hipLaunchKernelGGL(hk_ipm_init<FX>, grid, block, lds, stream, *a);
-            hipLaunchKernelGGL(hk_ipm_solo<FX>, grid, block, lds, stream, *a);
+            if (!single && a->N <= MW_NMAX && lds_mw + sizeof(MwShared) <= (size_t)lds_max)
+                hipLaunchKernelGGL(hk_ipm_solo_mw<FX>, grid, dim3(256), lds_mw, stream, *a);
+            else
+                hipLaunchKernelGGL(hk_ipm_solo<FX>, grid, block, lds, stream, *a);
             break;
+        }
         default: return -1;
     }
     return (int)hipGetLastError();

@@ -10,6 +10,8 @@
 Tolerances: Riccati outputs 1e-12, IPM iterates 1e-10 relative to max(1,|ref|), with
 identical iteration counts and return codes.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -349,9 +351,17 @@ def test_queue_back_to_back_on_two_streams(small_batch):
 
 
 @pytest.mark.parametrize("shape", ["ms_N30", "tv_N100", "random"])
-def test_solo_matches_batch(shape):
-    """The latency path (hpmpc_mi355x_ipm_solo: each problem's whole solve in one launch) is bitwise the batched
-    solve: same kernels' bodies, same order of operations (fixed-shape classes and the generic kernels)."""
+def test_solo_matches_batch(oracle, shape):
+    """The latency path (hpmpc_mi355x_ipm_solo: each problem's whole solve in one launch).
+    * HPMPC_MI355X_SOLO=1, the single-wave solo kernel: the batched passes' bodies in one launch, bitwise the batched
+      solve (fixed-shape classes and the generic kernels);
+    * the default, one problem per four-wave workgroup (hk_ipm_solo_mw): the same routines on the same operands, but
+      hipcc contracts a * b + c into FMAs differently once the bodies are split over waves (built with
+      -ffp-contract=on the two are bitwise equal, measured), and at mu_tol = 1e-12 the last Newton systems
+      (lam / t ~ 1 / mu) lift a last-bit difference to ~1e-9 in pi: identical iteration counts and return codes as
+      the batched solve, and every problem held to the CPU oracle at the IPM gate (helpers.compare_ipm) -- or, for a
+      problem that the batched solve itself only meets at a looser distance (tv_N100 problem 5, kk 15: batch 4.2e-9,
+      multi-wave 6.5e-9 from the oracle, tools/mw_oracle.py), at twice the batched solve's distance."""
     import torch
 
     from hpmpc_amd.batch import BatchSolver
@@ -371,12 +381,42 @@ def test_solo_matches_batch(shape):
     s.ipm()
     torch.cuda.synchronize()
     ref = {n: getattr(s, n).clone() for n in ("ux", "pi", "lam", "t", "kk", "ret", "stat")}
-    for n in ("ux", "pi", "lam", "t"):
-        getattr(s, n).zero_()
-    s.ipm_solo()
-    torch.cuda.synchronize()
-    for n, v in ref.items():
-        assert torch.equal(getattr(s, n), v), n
+    old = os.environ.get("HPMPC_MI355X_SOLO")
+    try:
+        os.environ["HPMPC_MI355X_SOLO"] = "1"
+        for n in ("ux", "pi", "lam", "t"):
+            getattr(s, n).zero_()
+        s.ipm_solo()
+        torch.cuda.synchronize()
+        for n, v in ref.items():
+            assert torch.equal(getattr(s, n), v), n
+        os.environ["HPMPC_MI355X_SOLO"] = "0"
+        for n in ("ux", "pi", "lam", "t"):
+            getattr(s, n).zero_()
+        s.ipm_solo()
+        torch.cuda.synchronize()
+    finally:
+        if old is None:
+            os.environ.pop("HPMPC_MI355X_SOLO", None)
+        else:
+            os.environ["HPMPC_MI355X_SOLO"] = old
+    assert torch.equal(s.kk, ref["kk"]) and torch.equal(s.ret, ref["ret"])
+    N = qp.N
+
+    def view(src, p):
+        g = {n: (src[n].cpu().numpy() if hasattr(src[n], "cpu") else src[n]) for n in ("ux", "pi", "lam", "t", "kk",
+                                                                                         "ret")}
+        return dict(kk=int(g["kk"][p]), ret=int(g["ret"][p]), ux=[g["ux"][p, k] for k in range(N + 1)],
+                    pi=[g["pi"][p, k] for k in range(N)], lam=[g["lam"][p, k] for k in range(N + 1)],
+                    t=[g["t"][p, k] for k in range(N + 1)])
+
+    mw = {n: getattr(s, n) for n in ("ux", "pi", "lam", "t", "kk", "ret")}
+    for p in range(qp.batch):
+        one = qp.problem(p)
+        r = oracle.ipm(one, k_max=50)
+        div = bool(int(ref["ret"][p]) == 2)
+        e_batch = compare_ipm(one, view(ref, p), r, tol=1.0, allow_divergent=div)
+        compare_ipm(one, view(mw, p), r, tol=max(TOL_IPM, 2 * e_batch), allow_divergent=div)
 
 
 def test_queue_unconstrained_entries_finish_at_init():
