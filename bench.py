@@ -352,7 +352,9 @@ def bench_single_qp(args, torch, stream):
     """configs[1]: one QP (the drivers' x0, test_d_ip_hard.c:306-322) solved alone on the GPU: the device time of
     the latency path (hpmpc_mi355x_ipm_solo, data resident in HBM; the kernel the drop-in runs), of a one-entry
     problem queue, of the batched API with a batch of one, and the drop-in d_ip2_res_mpc_hard_tv call on host lib4
-    buffers (PCIe staging included).  Latency-bound: one wavefront walks the N stages serially."""
+    buffers (PCIe staging included).  Latency-bound: the stages are walked serially; the solo kernel gives one problem
+    a 256-thread workgroup (hk_ipm_solo_mw: wave 0 runs the recursion, waves 1..3 everything off it), and the line also
+    reports the single-wave solo kernel (HPMPC_MI355X_SOLO=1) beside it."""
     from hpmpc_amd.batch import LIBPATH, BatchSolver
     from hpmpc_amd.cabi import HpmpcAPI, load
     from hpmpc_amd.ocp import mass_spring_qp
@@ -380,6 +382,13 @@ def bench_single_qp(args, torch, stream):
 
     ms = timed(s.ipm_solo)
     kk = int(s.kk[0].item())
+    os.environ["HPMPC_MI355X_SOLO"] = "1"  # read at each launch: the single-wave solo kernel
+    try:
+        s.ipm_solo()
+        ms_single = timed(s.ipm_solo)
+        assert int(s.kk[0].item()) == kk
+    finally:
+        os.environ.pop("HPMPC_MI355X_SOLO", None)
     ms_queue = timed(Q.run)
     assert int(Q.kk[0].item()) == kk
     evb = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
@@ -397,7 +406,9 @@ def bench_single_qp(args, torch, stream):
         call()
     host_ms = (time.perf_counter() - t0) / reps * 1e3
     return {"workload": f"single_qp_N{args.N}_nx{args.nx}_nu{args.nu}", "kk": kk, "device_ms_per_solve": ms,
-            "device_us_per_ip_iter": ms * 1e3 / max(kk, 1), "path": "hpmpc_mi355x_ipm_solo (one launch per solve)",
+            "device_us_per_ip_iter": ms * 1e3 / max(kk, 1),
+            "path": "hpmpc_mi355x_ipm_solo (one launch per solve, one problem per 4-wave workgroup: hk_ipm_solo_mw)",
+            "single_wave_ms_per_solve": ms_single, "single_wave_us_per_ip_iter": ms_single * 1e3 / max(kk, 1),
             "queue1_ms_per_solve": ms_queue, "batch_api_ms_per_solve": ms_batch,
             "dropin_ms_per_solve": host_ms, "dropin_kk": int(kkc.value)}
 
