@@ -28,6 +28,7 @@ namespace hk {
 constexpr int MW_WAVES = 4, MW_HELP = 3;
 constexpr int MW_D = 6;      // ring slots
 constexpr int MW_SLOT = 16;  // doubles per lane per slot
+constexpr int MW_DP = 6;     // tile wave -> row wave ring (backward sweep)
 constexpr int MW_NMAX = 300;  // horizon limit of the multi-wave kernel (the update's reduction rows live in LDS)
 constexpr int MW_RED = ((MW_NMAX + 4) / 4 + 3) / 4 * 4;
 constexpr int HK_MW_ERR = -20;
@@ -38,6 +39,10 @@ struct MwShared {
     Scratch sm[MW_WAVES];
     double al[MW_WAVES];
     int full[MW_D], freed[MW_D];
+    // backward sweep: the row wave's own free flags of the helpers' ring, and the tile wave -> row wave ring
+    int freedB[MW_D];
+    double ringP[MW_DP][5][64];  // [stage record tile (4) | inverse diagonal]
+    int fullP[MW_DP], freedP[MW_DP];
     int err;
     int dbg[4];  // the first expired wait: flag index (full: slot, freed: MW_D + slot), expected, found, wave
 #ifdef HK_STAMPS
@@ -53,15 +58,15 @@ __device__ __forceinline__ void mw_lds_wait() { asm volatile("s_waitcnt lgkmcnt(
 
 __device__ __forceinline__ int mw_flag(const int* f) { return __atomic_load_n(f, __ATOMIC_RELAXED); }
 
-// wait until the flag (full[i] for i < MW_D, freed[i - MW_D] otherwise) reaches v
 __device__ __forceinline__ unsigned long long mw_clock() {
     unsigned long long t;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
     return t;
 }
 
-__device__ __forceinline__ void mw_wait(int i, int v) {
-    const int* f = i < MW_D ? &hk_mw.full[i] : &hk_mw.freed[i - MW_D];
+// wait until flag *f (one of hk_mw's; always inlined, so it stays an LDS access) reaches v; i names the flag in the
+// diagnostics
+__device__ __forceinline__ void mw_wait_at(const int* f, int v, int i) {
 #ifdef HK_STAMPS
     const unsigned long long t0 = mw_clock();
     struct Acc {
@@ -88,12 +93,21 @@ __device__ __forceinline__ void mw_wait(int i, int v) {
     asm volatile("" ::: "memory");
 }
 
-// publish flag i = v after this wave's earlier LDS accesses (the slot data) have completed
-__device__ __forceinline__ void mw_post(int i, int v) {
+// wait until the flag (full[i] for i < MW_D, freed[i - MW_D] otherwise) reaches v
+__device__ __forceinline__ void mw_wait(int i, int v) {
+    mw_wait_at(i < MW_D ? &hk_mw.full[i] : &hk_mw.freed[i - MW_D], v, i);
+}
+
+// publish *f = v after this wave's earlier LDS accesses (the slot data) have completed
+__device__ __forceinline__ void mw_post_at(int* f, int v) {
     mw_lds_wait();
-    int* f = i < MW_D ? &hk_mw.full[i] : &hk_mw.freed[i - MW_D];
     if (lane_id() == 0) __atomic_store_n(f, v, __ATOMIC_RELAXED);
     asm volatile("" ::: "memory");
+}
+
+// publish flag i (full[i] for i < MW_D, freed[i - MW_D] otherwise) = v
+__device__ __forceinline__ void mw_post(int i, int v) {
+    mw_post_at(i < MW_D ? &hk_mw.full[i] : &hk_mw.freed[i - MW_D], v);
 }
 
 // producer side of step j: wait for the slot's previous occupant (step j - MW_D of this sweep) to be consumed
@@ -105,16 +119,26 @@ __device__ __forceinline__ void mw_put(int j, int i, double v) { hk_mw.ring[j % 
 __device__ __forceinline__ double mw_get(int j, int i) { return hk_mw.ring[j % MW_D][i][lane_id()]; }
 
 // ------------------------------------------------------------------------------------------------
-// Backward factorisation (ric_backward): slot = [M (4) | ml | bop (4) | brow (4)].
+// Backward factorisation (ric_backward), split over two recursions:
+//   wave 0 (tile): M += BAbt P_{k+1} BAbt' and the tile half of the stage Cholesky -> P_k (bwd_tile_update,
+//                  stage_chol without the row), handed to wave 1 through ringP = [record tile (4) | inv diag];
+//   wave 1 (row):  P_{k+1} b, the row update ml += BAbt (P b + p_{k+1}), the row half of each Cholesky block, the
+//                  gain block (stage_chol_row) and the stage record -- a second recursion (p_{k+1} -> p_k) that
+//                  needs the tile wave's factor but never feeds it, so it runs one stage behind;
+//   waves 2, 3 (helpers, every other stage): fetch, residuals, box terms -> ring = [M (4) | ml | bop (4) | brow (4)],
+//                  read by both recursions (its slot is free once both have read it).
 // ------------------------------------------------------------------------------------------------
+constexpr int MW_BHELP = 2;
+
 template <bool AUG, int BM, class FX>
 __device__ __forceinline__ int ric_backward_mw(const RicIO& io, int tb, int w, int update_b, const double* bsrc,
-                                int update_q, const double* qsrc, const BoxCtx& bc, int compute_Pb, double* Pb) {
+                                               int update_q, const double* qsrc, const BoxCtx& bc, int compute_Pb,
+                                               double* Pb) {
     const int N = io.N, l = lane_id(), c = l & 15;
     Scratch* sm = &hk_mw.sm[w];
-    if (w > 0) {
-        // each helper walks its stages with one-step register prefetch: step j + MW_HELP is fetched before step j
-        // is computed (the unrolled pair swaps the fragments' roles)
+    if (w >= 2) {
+        // each helper walks its stages with one-step register prefetch: step j + MW_BHELP is fetched before step
+        // j is computed (the unrolled pair swaps the fragments' roles)
         auto fetch = [&](int j, BwdFrag& f, double& x1c) __attribute__((always_inline)) {
             const int k = N - j;
             const StageInfo si = load_stage(io.st, k);
@@ -141,7 +165,10 @@ __device__ __forceinline__ int ric_backward_mw(const RicIO& io, int tb, int w, i
                 if constexpr (BM == BX_P2R) bwd_residual(io, sm, sh, k, bc, f, x1c, true);
                 bwd_pre<AUG, BM>(io, sh, k, f, bc, M, ml);
             });
-            mw_acquire(tb, j);
+            if (j >= MW_D) {  // the slot's previous occupant read by both recursions
+                mw_wait_at(&hk_mw.freed[j % MW_D], tb + j - MW_D + 1, MW_D + j % MW_D);
+                mw_wait_at(&hk_mw.freedB[j % MW_D], tb + j - MW_D + 1, 2 * MW_D + j % MW_D);
+            }
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 mw_put(j, r, M[r]);
@@ -153,56 +180,93 @@ __device__ __forceinline__ int ric_backward_mw(const RicIO& io, int tb, int w, i
         };
         BwdFrag fa, fb;
         double xa = 0.0, xb = 0.0;
-        int j = w - 1;
+        int j = w - 2;
         if (j <= N) fetch(j, fa, xa);
         for (;;) {
             if (j > N) break;
-            if (j + MW_HELP <= N) fetch(j + MW_HELP, fb, xb);
+            if (j + MW_BHELP <= N) fetch(j + MW_BHELP, fb, xb);
             work(j, fa, xa);
-            j += MW_HELP;
+            j += MW_BHELP;
             if (j > N) break;
-            if (j + MW_HELP <= N) fetch(j + MW_HELP, fa, xa);
+            if (j + MW_BHELP <= N) fetch(j + MW_BHELP, fa, xa);
             work(j, fb, xb);
-            j += MW_HELP;
+            j += MW_BHELP;
         }
-    } else {
-        d4 P = {0.0, 0.0, 0.0, 0.0};
-        double ml_prev = 0.0, invd_prev = 0.0, kg_prev = 0.0;
-        bool rec_fixed = false;
+    } else if (w == 0) {
+        d4 P = {0.0, 0.0, 0.0, 0.0};  // record tile of stage k+1 (its x block is P_{k+1})
         for (int j = 0; j <= N; j++) {
             const int k = N - j;
             HK_STAMP(0, k);
             const StageInfo si = load_stage(io.st, k);
             mw_wait(j % MW_D, tb + j + 1);
             HK_STAMP(5, k);
-            d4 M, bop, brow;
+            d4 M, bop;
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 M[r] = mw_get(j, r);
                 bop[r] = mw_get(j, 5 + r);
-                brow[r] = mw_get(j, 9 + r);
             }
-            const double ml = mw_get(j, 4);
             mw_post(MW_D + j % MW_D, tb + j + 1);
             HK_STAMP(6, k);
-            if (k < N) {  // record of stage k+1, in the format of its shape class (as ric_backward)
-                double* Fk1 = io.F + (long)(k + 1) * FSTRIDE;
-                if constexpr (FX::enabled) {
-                    if (rec_fixed)
-                        store_factor_fixed<FX::nx>(Fk1, P, AUG ? ml_prev : 0.0, invd_prev, kg_prev, true);
-                    else
-                        store_factor(Fk1, P, AUG ? ml_prev : 0.0, invd_prev, kg_prev, true);
-                } else {
-                    store_factor(Fk1, P, AUG ? ml_prev : 0.0, invd_prev, kg_prev, true);
-                }
-            }
-            HK_STAMP(1, k);
+            double invd;
             with_shape<FX>(si, [&](const auto& sh) {
-                bwd_core<AUG>(io, sm, sh, k, bop, brow, M, ml, compute_Pb, Pb, P, ml_prev, invd_prev, kg_prev);
-                rec_fixed = std::remove_reference_t<decltype(sh)>::fixed;
+                using SHT = std::remove_reference_t<decltype(sh)>;
+                const bool live = SHT::fixed || k < N;
+                bwd_tile_update(sh, live, bop, P, M);
+                HK_STAMP(2, k);
+                double mld = 0.0;
+                stage_chol<false, false>(M, mld, invd, sh.nu, sh.nx, sh.xo, !SHT::fixed && k == 0, !SHT::fixed,
+                                         nullptr, k);
+                HK_STAMP(3, k);
             });
+            P = M;
+            if (j >= MW_DP) mw_wait_at(&hk_mw.freedP[j % MW_DP], tb + j - MW_DP + 1, 3 * MW_D + j % MW_DP);
+#pragma unroll
+            for (int r = 0; r < 4; r++) hk_mw.ringP[j % MW_DP][r][l] = P[r];
+            hk_mw.ringP[j % MW_DP][4][l] = invd;
+            mw_post_at(&hk_mw.fullP[j % MW_DP], tb + j + 1);
         }
-        store_factor(io.F, P, AUG ? ml_prev : 0.0, invd_prev, kg_prev);
+    } else {
+        d4 P1 = {0.0, 0.0, 0.0, 0.0};  // record tile of stage k+1
+        double ml_prev = 0.0;           // its row [l_u; p_{k+1}]
+        for (int j = 0; j <= N; j++) {
+            const int k = N - j;
+            const StageInfo si = load_stage(io.st, k);
+            mw_wait(j % MW_D, tb + j + 1);
+            d4 bop, brow;
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                bop[r] = mw_get(j, 5 + r);
+                brow[r] = mw_get(j, 9 + r);
+            }
+            double ml = mw_get(j, 4);
+            mw_post_at(&hk_mw.freedB[j % MW_D], tb + j + 1);
+            // the row update needs only P_{k+1} (held from the previous step): it runs while the tile wave
+            // factorises stage k
+            with_shape<FX>(si, [&](const auto& sh) {
+                using SHT = std::remove_reference_t<decltype(sh)>;
+                if (AUG) bwd_row_update(io, sm, sh, k, SHT::fixed || k < N, bop, brow, P1, ml_prev, compute_Pb, Pb, ml);
+            });
+            mw_wait_at(&hk_mw.fullP[j % MW_DP], tb + j + 1, 4 * MW_D + j % MW_DP);
+            d4 S;
+#pragma unroll
+            for (int r = 0; r < 4; r++) S[r] = hk_mw.ringP[j % MW_DP][r][l];
+            const double invd = hk_mw.ringP[j % MW_DP][4][l];
+            mw_post_at(&hk_mw.freedP[j % MW_DP], tb + j + 1);
+            double kg = 0.0;
+            with_shape<FX>(si, [&](const auto& sh) {
+                using SHT = std::remove_reference_t<decltype(sh)>;
+                stage_chol_row<AUG, SHT::fixed>(S, invd, ml, sh.nu, sh.nx, sh.xo, !SHT::fixed && k == 0, &kg);
+                // the stage record, in the format of the stage's shape class (as ric_backward)
+                double* Fk = io.F + (long)k * FSTRIDE;
+                if constexpr (SHT::fixed)
+                    store_factor_fixed<SHT::nx>(Fk, S, AUG ? ml : 0.0, invd, kg, true);
+                else
+                    store_factor(Fk, S, AUG ? ml : 0.0, invd, kg);
+            });
+            P1 = S;
+            ml_prev = ml;
+        }
     }
     return tb + N + 2;
 }

@@ -198,6 +198,56 @@ __device__ __forceinline__ void chol_block(d4& M, double& ml, double& invd, doub
 #undef HK_BSTAMP
 }
 
+// The augmented row's terms (AUG) and the gain block (KGEN) of chol_block<B>, formed after the fact from the
+// block's final factor S[B] (upper storage: lane c of row group j holds y_j = L[c][4B+j]) and the pivots' inverse
+// diagonal (lane 4B+j holds i_j): the same operations on the same operands as chol_block, so ml and kg are bitwise
+// chol_block's.  The multi-wave solo kernel runs the tile half of the factorisation on one wave and this row half
+// one stage behind on another (hk_mw.h).
+template <int B, bool AUG, bool KGEN>
+__device__ __forceinline__ void chol_block_row(const d4& S, double invd, double& ml, double* kg) {
+    const int l = lane_id(), c = l & 15;
+    double y[4];
+    rowgroup_gather(S[B], y);
+    const double i0 = row_bcast<4 * B + 0>(invd), i1 = row_bcast<4 * B + 1>(invd);
+    const double i2 = row_bcast<4 * B + 2>(invd), i3 = row_bcast<4 * B + 3>(invd);
+    const double l10 = row_bcast<4 * B + 1>(y[0]), l20 = row_bcast<4 * B + 2>(y[0]), l30 = row_bcast<4 * B + 3>(y[0]);
+    const double l21 = row_bcast<4 * B + 2>(y[1]), l31 = row_bcast<4 * B + 3>(y[1]);
+    const double l32 = row_bcast<4 * B + 3>(y[2]);
+    if (KGEN && B == 0) {
+        const bool ut = c < 4;
+        const double e0 = ut ? (c == 0 ? 1.0 : 0.0) : y[0], e1 = ut ? (c == 1 ? 1.0 : 0.0) : y[1];
+        const double e2 = ut ? (c == 2 ? 1.0 : 0.0) : y[2], e3 = ut ? (c == 3 ? 1.0 : 0.0) : y[3];
+        const double z3 = e3 * i3;
+        const double z2 = fma(-l32, z3, e2) * i2;
+        const double z1 = fma(-l31, z3, fma(-l21, z2, e1)) * i1;
+        const double z0 = fma(-l30, z3, fma(-l20, z2, fma(-l10, z1, e0))) * i0;
+        *kg = -sel_g(z0, z1, z2, z3);
+    }
+    if (AUG) {
+        const double m0 = row_bcast<4 * B + 0>(ml), m1 = row_bcast<4 * B + 1>(ml);
+        const double m2 = row_bcast<4 * B + 2>(ml), m3 = row_bcast<4 * B + 3>(ml);
+        const double p0 = m0 * i0;
+        const double p1 = fma(-p0, l10, m1) * i1;
+        const double p2 = fma(-p1, l21, fma(-p0, l20, m2)) * i2;
+        const double p3 = fma(-p2, l32, fma(-p1, l31, fma(-p0, l30, m3))) * i3;
+        const bool inb = (c >> 2) == B, below = c > 4 * B + 3;
+        const double mt = fma(-p3, y[3], fma(-p2, y[2], fma(-p1, y[1], fma(-p0, y[0], ml))));
+        const double mb = sel_q(p0, p1, p2, p3);
+        ml = below ? mt : (inb ? mb : ml);
+    }
+}
+
+// stage_chol's row half over the blocks it factorised (same block conditions)
+template <bool AUG, bool KGEN>
+__device__ __forceinline__ void stage_chol_row(const d4& S, double invd, double& ml, int nu, int nx, int xo, bool full,
+                                               double* kg) {
+    const int hi = full ? xo + nx : nu;
+    if (0 < nu || (full && 3 >= xo && 0 < hi)) chol_block_row<0, AUG, KGEN>(S, invd, ml, kg);
+    if (4 < nu || (full && 7 >= xo && 4 < hi)) chol_block_row<1, AUG, false>(S, invd, ml, nullptr);
+    if (8 < nu || (full && 11 >= xo && 8 < hi)) chol_block_row<2, AUG, false>(S, invd, ml, nullptr);
+    if (12 < nu || (full && 15 >= xo && 12 < hi)) chol_block_row<3, AUG, false>(S, invd, ml, nullptr);
+}
+
 // Stage factorisation with the augmented row.
 // In : M (tile, full symmetric), ml (aug row, col layout).
 // full == true : the whole stage Cholesky (d_back_ric_rec.c:325, dsyrk_dpotrf_lib), M = S = lower(L) +
@@ -893,15 +943,10 @@ __device__ __forceinline__ void bwd_pre(const RicIO& io, const SH& sh, int k, co
     }
 }
 
-// Second half: M += BAbt P BAbt', the row update and the stage factorisation (the recursion's chain).
-template <bool AUG, class SH>
-__device__ __forceinline__ void bwd_core(const RicIO& io, Scratch* sm, const SH& sh, int k, const d4& bop,
-                                         const d4& brow, d4 M, double ml, int compute_Pb, double* Pb, d4& S,
-                                         double& ml_prev, double& invd_prev, double& kg_prev) {
-    const int l = lane_id(), g = l >> 4, c = l & 15;
-    const bool live = SH::fixed || k < io.N;
+// M += BAbt_k P_{k+1} BAbt_k' (the tile half of the recursion; P form, see stage_chol).
+template <class SH>
+__device__ __forceinline__ void bwd_tile_update(const SH& sh, bool live, const d4& bop, const d4& S, d4& M) {
     const int nx1 = sh.nx1, xo1 = sh.xo1;
-    const bool xc = c >= xo1;  // tile column c is a state of stage k+1 (padding beyond xo1+nx1 is zero)
     if (live) {
         // T' = P_{k+1} BAbt_k'  (rows in stage-(k+1) tile coords): the A fragment of K-chunk kc is P's
         // register kc itself (P symmetric: lane (g,c) holds P[4kc+g][c] = P[c][4kc+g]), its u columns masked;
@@ -930,23 +975,42 @@ __device__ __forceinline__ void bwd_core(const RicIO& io, Scratch* sm, const SH&
         }
         M = M + m1;
     }
-    if (AUG) {
-        // Pb_k = P_{k+1} b_k (col layout, stage-(k+1) tile); zero at k = N (S = 0, b = 0).  Stored masked,
-        // never skipped: the row update below needs it anyway
-        double part = 0.0;
+}
+
+// The augmented row's update before the stage factorisation: Pb_k = P_{k+1} b_k (stored when compute_Pb) and
+// ml += BAbt_k (P b + p_{k+1}) (the row half of the recursion).
+template <class SH>
+__device__ __forceinline__ void bwd_row_update(const RicIO& io, Scratch* sm, const SH& sh, int k, bool live,
+                                               const d4& bop, const d4& brow, const d4& S, double ml_prev,
+                                               int compute_Pb, double* Pb, double& ml) {
+    const int l = lane_id(), g = l >> 4, c = l & 15;
+    const int nx1 = sh.nx1, xo1 = sh.xo1;
+    const bool xc = c >= xo1;  // tile column c is a state of stage k+1 (padding beyond xo1+nx1 is zero)
+    // Pb_k = P_{k+1} b_k (col layout, stage-(k+1) tile); zero at k = N (S = 0, b = 0).  Stored masked,
+    // never skipped: the row update below needs it anyway
+    double part = 0.0;
 #pragma unroll
-        for (int r = 0; r < 4; r++) part += S[r] * brow[r];  // columns c < xo1: unused (masked below)
-        const double pb = xrow_sum(part);
-        gst(Pb, k * V16 + (c - xo1), pb, compute_Pb && live && g == 0 && xc && c < xo1 + nx1);
-        // m_last += BAbt_k (P b + p_{k+1})
-        const double wc = xc ? pb + ml_prev : 0.0;
-        double wrow[4];
-        col2row(sm, wc, wrow);
-        double mp = 0.0;
+    for (int r = 0; r < 4; r++) part += S[r] * brow[r];  // columns c < xo1: unused (masked below)
+    const double pb = xrow_sum(part);
+    gst(Pb, k * V16 + (c - xo1), pb, compute_Pb && live && g == 0 && xc && c < xo1 + nx1);
+    // m_last += BAbt_k (P b + p_{k+1})
+    const double wc = xc ? pb + ml_prev : 0.0;
+    double wrow[4];
+    col2row(sm, wc, wrow);
+    double mp = 0.0;
 #pragma unroll
-        for (int r = 0; r < 4; r++) mp += bop[r] * wrow[r];
-        if (live) ml += xrow_sum(mp);
-    }
+    for (int r = 0; r < 4; r++) mp += bop[r] * wrow[r];
+    if (live) ml += xrow_sum(mp);
+}
+
+// Second half: M += BAbt P BAbt', the row update and the stage factorisation (the recursion's chain).
+template <bool AUG, class SH>
+__device__ __forceinline__ void bwd_core(const RicIO& io, Scratch* sm, const SH& sh, int k, const d4& bop,
+                                         const d4& brow, d4 M, double ml, int compute_Pb, double* Pb, d4& S,
+                                         double& ml_prev, double& invd_prev, double& kg_prev) {
+    const bool live = SH::fixed || k < io.N;
+    bwd_tile_update(sh, live, bop, S, M);
+    if (AUG) bwd_row_update(io, sm, sh, k, live, bop, brow, S, ml_prev, compute_Pb, Pb, ml);
     HK_STAMP(2, k);
     double invd, kg = 0.0;
     // stage 0 of a generic problem keeps the full factor; every other stage is factorised in P form

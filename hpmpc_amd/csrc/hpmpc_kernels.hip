@@ -892,6 +892,11 @@ __global__ __launch_bounds__(256) void hk_ipm_solo_mw(KArgs a) {
     if (threadIdx.x < MW_D) {
         hk_mw.full[threadIdx.x] = 0;
         hk_mw.freed[threadIdx.x] = 0;
+        hk_mw.freedB[threadIdx.x] = 0;
+    }
+    if (threadIdx.x < MW_DP) {
+        hk_mw.fullP[threadIdx.x] = 0;
+        hk_mw.freedP[threadIdx.x] = 0;
     }
     if (threadIdx.x == 0) hk_mw.err = 0;
     __syncthreads();
