@@ -193,20 +193,30 @@ __device__ __forceinline__ int ric_backward_mw(const RicIO& io, int tb, int w, i
             j += MW_BHELP;
         }
     } else if (w == 0) {
+        // the next step's slot is read while this step computes (its LDS latency off the recursion); the slot is
+        // released once this step is done, by which time those reads have long completed
         d4 P = {0.0, 0.0, 0.0, 0.0};  // record tile of stage k+1 (its x block is P_{k+1})
+        d4 Mn, bopn;
+        auto take = [&](int j) __attribute__((always_inline)) {
+            mw_wait(j % MW_D, tb + j + 1);
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                Mn[r] = mw_get(j, r);
+                bopn[r] = mw_get(j, 5 + r);
+            }
+        };
+        take(0);
+        StageInfo sn = load_stage(io.st, N);
         for (int j = 0; j <= N; j++) {
             const int k = N - j;
             HK_STAMP(0, k);
-            const StageInfo si = load_stage(io.st, k);
-            mw_wait(j % MW_D, tb + j + 1);
-            HK_STAMP(5, k);
-            d4 M, bop;
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                M[r] = mw_get(j, r);
-                bop[r] = mw_get(j, 5 + r);
+            const StageInfo si = sn;
+            d4 M = Mn;
+            const d4 bop = bopn;
+            if (j < N) {
+                take(j + 1);
+                sn = load_stage(io.st, k - 1);
             }
-            mw_post(MW_D + j % MW_D, tb + j + 1);
             HK_STAMP(6, k);
             double invd;
             with_shape<FX>(si, [&](const auto& sh) {
@@ -220,6 +230,7 @@ __device__ __forceinline__ int ric_backward_mw(const RicIO& io, int tb, int w, i
                 HK_STAMP(3, k);
             });
             P = M;
+            mw_post(MW_D + j % MW_D, tb + j + 1);  // step j's slot (read one step ago)
             if (j >= MW_DP) mw_wait_at(&hk_mw.freedP[j % MW_DP], tb + j - MW_DP + 1, 3 * MW_D + j % MW_DP);
 #pragma unroll
             for (int r = 0; r < 4; r++) hk_mw.ringP[j % MW_DP][r][l] = P[r];
@@ -511,43 +522,56 @@ __device__ __forceinline__ int ric_trs_mw(const RicIO& io, int tb, int w, const 
             j += MW_HELP;
         }
     } else {
+        // as the factorisation's tile wave: the next step's slot is read while this step computes
         double pcol = 0.0;
-        for (int j = 0; j <= N; j++) {
-            const int k = N - j;
-            const StageInfo si = load_stage(io.st, k);
+        double hn, invdn, pbcn;
+        d4 bopn, Sn;
+        auto take = [&](int j) __attribute__((always_inline)) {
             mw_wait(j % MW_D, tb + j + 1);
-            const double hpre = mw_get(j, 0);
-            d4 bop, Sk;
+            hn = mw_get(j, 0);
 #pragma unroll
             for (int r = 0; r < 4; r++) {
-                bop[r] = mw_get(j, 1 + r);
-                Sk[r] = mw_get(j, 5 + r);
+                bopn[r] = mw_get(j, 1 + r);
+                Sn[r] = mw_get(j, 5 + r);
             }
-            const double invd = mw_get(j, 9), pbc = mw_get(j, 10);
-            mw_post(MW_D + j % MW_D, tb + j + 1);
+            invdn = mw_get(j, 9);
+            pbcn = mw_get(j, 10);
+        };
+        take(0);
+        StageInfo sn = load_stage(io.st, N);
+        for (int j = 0; j <= N; j++) {
+            const int k = N - j;
+            const StageInfo si = sn;
+            const double hpre = hn, invd = invdn, pbc = pbcn;
+            const d4 bop = bopn, Sk = Sn;
+            if (j < N) {
+                take(j + 1);
+                sn = load_stage(io.st, k - 1);
+            }
             if (k == N) {  // stage N: hux_N = q_N + box (+ general) gradient, no u block
                 const int v = tile_var(c, si.nu, si.nx, si.xo);
                 gst(ux, N * V16 + v, hpre, g == 0 && v >= 0);
                 pcol = hpre;
-                continue;
-            }
-            with_shape<FX>(si, [&](const auto& sh) {
-                using SHT = std::remove_reference_t<decltype(sh)>;
-                const int xo1 = sh.xo1, nx1 = sh.nx1;
-                const int vc = tile_var(c, sh.nu, sh.nx, sh.xo);
-                const int s = c - xo1;
-                const double wc = (s >= 0 && s < nx1) ? pbc + pcol : 0.0;
-                double wrow[4];
-                col2row(sm, wc, wrow);
-                double part = 0.0;
+            } else {
+                with_shape<FX>(si, [&](const auto& sh) {
+                    using SHT = std::remove_reference_t<decltype(sh)>;
+                    const int xo1 = sh.xo1, nx1 = sh.nx1;
+                    const int vc = tile_var(c, sh.nu, sh.nx, sh.xo);
+                    const int s = c - xo1;
+                    const double wc = (s >= 0 && s < nx1) ? pbc + pcol : 0.0;
+                    double wrow[4];
+                    col2row(sm, wc, wrow);
+                    double part = 0.0;
 #pragma unroll
-                for (int r = 0; r < 4; r++) part += bop[r] * wrow[r];
-                double h = hpre;
-                h += xrow_sum(part);
-                h = solve_ln(sh, Sk, invd, h, !SHT::fixed && k == 0);
-                gst(ux, k * V16 + vc, h, g == 0 && vc >= 0);
-                pcol = h;
-            });
+                    for (int r = 0; r < 4; r++) part += bop[r] * wrow[r];
+                    double h = hpre;
+                    h += xrow_sum(part);
+                    h = solve_ln(sh, Sk, invd, h, !SHT::fixed && k == 0);
+                    gst(ux, k * V16 + vc, h, g == 0 && vc >= 0);
+                    pcol = h;
+                });
+            }
+            mw_post(MW_D + j % MW_D, tb + j + 1);
         }
     }
     __syncthreads();  // hux written by wave 0 is read by the forward below

@@ -26,10 +26,10 @@ print(f"kk {kk}; per iteration (s_memtime ticks): " + " ".join(
     f"{n} {t[32 + i] / kk:.0f}" for i, n in enumerate(["fact", "pred", "corr", "update"])) +
     f" | total {tot / kk:.0f}")
 print("hand-over waits per iteration (ticks): " + " ".join(f"w{i} {t[40 + i] / kk:.0f}" for i in range(4)))
-# one backward stage of the recursion wave (stage 50, the solve's last factorisation): stamps 0 (step start),
-# 5 (slot ready), 6 (slot read), 1 (record stored), 2 (M and the row done), 16 (u block factorised), 3 (end)
-st = {i: t[i] for i in (0, 5, 6, 1, 2, 16, 3)}
+# one backward stage of the tile wave (stage 50, the solve's last factorisation): stamps 0 (step start),
+# 5 (slot ready), 6 (slot read), 2 (M += BAbt P BAbt' done), 16 (u block factorised), 3 (end)
+st = {i: t[i] for i in (0, 5, 6, 2, 16, 3)}
 if all(st.values()):
-    seq = [0, 5, 6, 1, 2, 16, 3]
+    seq = [0, 5, 6, 2, 16, 3]
     print("wave-0 backward stage 50 (ticks): " + " ".join(f"{a}->{b} {st[b] - st[a]}" for a, b in zip(seq, seq[1:])) +
           f" | total {st[3] - st[0]}")
