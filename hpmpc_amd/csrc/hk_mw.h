@@ -54,7 +54,6 @@ struct MwShared {
 // could lose its address space): every access is a ds_ op, so a flag poll never waits on the global-memory counter.
 __shared__ MwShared hk_mw;
 
-__device__ __forceinline__ void mw_lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 __device__ __forceinline__ int mw_flag(const int* f) { return __atomic_load_n(f, __ATOMIC_RELAXED); }
 
@@ -98,9 +97,12 @@ __device__ __forceinline__ void mw_wait(int i, int v) {
     mw_wait_at(i < MW_D ? &hk_mw.full[i] : &hk_mw.freed[i - MW_D], v, i);
 }
 
-// publish *f = v after this wave's earlier LDS accesses (the slot data) have completed
+// publish *f = v behind this wave's earlier LDS accesses (the slot data).  The LDS performs one wave's ds_ operations
+// in issue order (lgkmcnt counts them down in order), so a wave that sees the flag sees the data written before it,
+// and a slot's reads are performed before its free flag: only the compiler must not move them (the memory
+// clobbers), the wave itself does not wait for them.
 __device__ __forceinline__ void mw_post_at(int* f, int v) {
-    mw_lds_wait();
+    asm volatile("" ::: "memory");
     if (lane_id() == 0) __atomic_store_n(f, v, __ATOMIC_RELAXED);
     asm volatile("" ::: "memory");
 }
