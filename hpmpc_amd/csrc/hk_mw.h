@@ -47,6 +47,7 @@ struct MwShared {
     int dbg[4];  // the first expired wait: flag index (full: slot, freed: MW_D + slot), expected, found, wave
 #ifdef HK_STAMPS
     unsigned long long wait_cyc[MW_WAVES];  // cycles each wave spent in mw_wait (diagnostic build)
+    unsigned long long seg[4];              // the tile wave's backward step by segment (diagnostic build)
 #endif
 };
 
@@ -209,9 +210,21 @@ __device__ __forceinline__ int ric_backward_mw(const RicIO& io, int tb, int w, i
         };
         take(0);
         StageInfo sn = load_stage(io.st, N);
+#ifdef HK_STAMPS
+        unsigned long long seg[4] = {0, 0, 0, 0}, tq = mw_clock();
+#define MW_SEG(i)                                 \
+    do {                                          \
+        const unsigned long long t_ = mw_clock(); \
+        seg[i] += t_ - tq;                        \
+        tq = t_;                                  \
+    } while (0)
+#else
+#define MW_SEG(i) \
+    do {          \
+    } while (0)
+#endif
         for (int j = 0; j <= N; j++) {
             const int k = N - j;
-            HK_STAMP(0, k);
             const StageInfo si = sn;
             d4 M = Mn;
             const d4 bop = bopn;
@@ -219,17 +232,17 @@ __device__ __forceinline__ int ric_backward_mw(const RicIO& io, int tb, int w, i
                 take(j + 1);
                 sn = load_stage(io.st, k - 1);
             }
-            HK_STAMP(6, k);
+            MW_SEG(0);
             double invd;
             with_shape<FX>(si, [&](const auto& sh) {
                 using SHT = std::remove_reference_t<decltype(sh)>;
                 const bool live = SHT::fixed || k < N;
                 bwd_tile_update(sh, live, bop, P, M);
-                HK_STAMP(2, k);
+                MW_SEG(1);
                 double mld = 0.0;
                 stage_chol<false, false>(M, mld, invd, sh.nu, sh.nx, sh.xo, !SHT::fixed && k == 0, !SHT::fixed,
                                          nullptr, k);
-                HK_STAMP(3, k);
+                MW_SEG(2);
             });
             P = M;
             mw_post(MW_D + j % MW_D, tb + j + 1);  // step j's slot (read one step ago)
@@ -238,7 +251,13 @@ __device__ __forceinline__ int ric_backward_mw(const RicIO& io, int tb, int w, i
             for (int r = 0; r < 4; r++) hk_mw.ringP[j % MW_DP][r][l] = P[r];
             hk_mw.ringP[j % MW_DP][4][l] = invd;
             mw_post_at(&hk_mw.fullP[j % MW_DP], tb + j + 1);
+            MW_SEG(3);
         }
+#ifdef HK_STAMPS
+        if (l == 0)
+            for (int i = 0; i < 4; i++) hk_mw.seg[i] += seg[i];
+#endif
+#undef MW_SEG
     } else {
         d4 P1 = {0.0, 0.0, 0.0, 0.0};  // record tile of stage k+1
         double ml_prev = 0.0;           // its row [l_u; p_{k+1}]

@@ -906,7 +906,7 @@ __global__ __launch_bounds__(256) void hk_ipm_solo_mw(KArgs a) {
 #ifdef HK_STAMPS
     // diagnostic build: cycles per body (summed over the iterations) and per wave in hand-over waits, problem 0
     unsigned long long tph[4] = {0, 0, 0, 0}, tm = 0;
-    if (threadIdx.x < MW_WAVES) hk_mw.wait_cyc[threadIdx.x] = 0;
+    if (threadIdx.x < MW_WAVES) hk_mw.wait_cyc[threadIdx.x] = hk_mw.seg[threadIdx.x] = 0;
 #define HK_MW_PHASE(i)                            \
     do {                                          \
         const unsigned long long t_ = mw_clock(); \
@@ -954,6 +954,7 @@ __global__ __launch_bounds__(256) void hk_ipm_solo_mw(KArgs a) {
     if (a.dbg && p == 0 && threadIdx.x == 0) {
         for (int i = 0; i < 4; i++) a.dbg[32 + i] = tph[i];
         for (int i = 0; i < MW_WAVES; i++) a.dbg[40 + i] = hk_mw.wait_cyc[i];
+        for (int i = 0; i < 4; i++) a.dbg[48 + i] = hk_mw.seg[i];
     }
 #endif
 #undef HK_MW_PHASE

@@ -33,3 +33,10 @@ if all(st.values()):
     seq = [0, 5, 6, 2, 16, 3]
     print("wave-0 backward stage 50 (ticks): " + " ".join(f"{a}->{b} {st[b] - st[a]}" for a, b in zip(seq, seq[1:])) +
           f" | total {st[3] - st[0]}")
+# the tile wave's backward steps by segment, summed over every factorisation of the solve: the hand-over in (slot
+# poll and reads, stage table), M += BAbt P BAbt', the tile Cholesky, the hand-over out
+seg = t[48:52]
+if sum(seg):
+    n = kk * 101
+    print("tile wave per backward step (ticks): " + " ".join(
+        f"{nm} {v / n:.0f}" for nm, v in zip(["handover-in", "mfma", "chol", "handover-out"], seg)))
