@@ -103,6 +103,90 @@ def host_cpu():
             "affinity": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None}
 
 
+def physical_cores():
+    """Physical cores of the host (distinct (package, core) pairs in /proc/cpuinfo), or None."""
+    ids, pkg = set(), None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("physical id"):
+                    pkg = line.split(":", 1)[1].strip()
+                elif line.startswith("core id"):
+                    ids.add((pkg, line.split(":", 1)[1].strip()))
+    except OSError:
+        return None
+    return len(ids) or None
+
+
+def ref_api():
+    """The reference c99 build (oracle/_ref/libhpmpc_ref.so) for the parity samples, or None when absent."""
+    from hpmpc_amd.cabi import HpmpcAPI, load
+
+    path = os.path.join(ROOT, "oracle", "_ref", "libhpmpc_ref.so")
+    return HpmpcAPI(load(path)) if os.path.exists(path) else None
+
+
+def rel_err(a, b):
+    a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
+    return float(np.max(np.abs(a - b) / np.maximum(1.0, np.abs(b)), initial=0.0))
+
+
+def parity_ipm(ref, qp, sol, idx):
+    """SURVEY.md §5 'max parity error' of timed IPM solves: problems `idx` (pairs of (entry in sol, problem of qp))
+    re-solved by the reference c99 build after the timed region; max relative error of ux / pi / lam / t over the
+    valid entries, kk / ret equality.  A problem the reference itself stops on alpha_min with |lam| > 1e12 (an
+    infeasible draw, where last bits grow without bound) contributes only kk / ret."""
+    if ref is None:
+        return None
+    rows_t = sol["ux"].new_tensor([q for q, _ in idx], dtype=sol["kk"].dtype).long()
+    ux, pi, lam, t, kk, ret = (sol[n][rows_t].cpu().numpy() for n in ("ux", "pi", "lam", "t", "kk", "ret"))
+    idx = [(i, p) for i, (_, p) in enumerate(idx)]
+    e, same, div, rows = 0.0, 0, 0, []
+    for q, p in idx:
+        one = qp.problem(int(p))
+        r = ref.ipm(one.copy(), k_max=int(sol["k_max"]))
+        ok = int(kk[q]) == r["kk"] and int(ret[q]) == r["ret"]
+        same += ok
+        if r["ret"] == 2 and max(float(np.max(np.abs(x))) for x in r["lam"]) > 1e12:
+            div += 1
+            rows.append({"problem": int(p), "kk": int(kk[q]), "ret": int(ret[q]), "divergent": True})
+            continue
+        ep = 0.0
+        for k in range(qp.N + 1):
+            ep = max(ep, rel_err(ux[q, k, :qp.nux(k)], r["ux"][k][:qp.nux(k)]))
+            if k < qp.N:
+                ep = max(ep, rel_err(pi[q, k, :int(qp.nx[k + 1])], r["pi"][k][:int(qp.nx[k + 1])]))
+            nb, pnb = int(qp.nb[k]), qp.pnb(k)
+            ib = np.r_[0:nb, pnb:pnb + nb].astype(int)
+            ep = max(ep, rel_err(lam[q, k, ib], r["lam"][k][ib]), rel_err(t[q, k, ib], r["t"][k][ib]))
+        e = max(e, ep)
+        rows.append({"problem": int(p), "kk": int(kk[q]), "ret": int(ret[q]), "max_rel_err": ep})
+    return {"reference": "oracle/_ref c99 build, d_ip2_res_mpc_hard_tv", "problems": len(idx), "max_rel_err": e,
+            "kk_ret_equal": same, "divergent_kk_ret_only": div, "per_problem": rows}
+
+
+def parity_sv(ref, qp, ux_t, pi_t, problems, compute_pi=1):
+    """The same for timed Riccati solves (d_back_ric_rec_sv_tv_res): ux and pi of `problems` against the reference."""
+    if ref is None:
+        return None
+    sel = ux_t.new_tensor(list(problems)).long()
+    ux, pi = ux_t[sel].cpu().numpy(), pi_t[sel].cpu().numpy()
+    e = 0.0
+    for i, p in enumerate(problems):
+        u2, p2, _, _ = ref.ric_sv(qp.problem(int(p)), compute_pi=compute_pi, compute_Pb=0)
+        for k in range(qp.N + 1):
+            e = max(e, rel_err(ux[i, k, :qp.nux(k)], u2[k][:qp.nux(k)]))
+            if k < qp.N and compute_pi:
+                e = max(e, rel_err(pi[i, k, :int(qp.nx[k + 1])], p2[k][:int(qp.nx[k + 1])]))
+    return {"reference": "oracle/_ref c99 build, d_back_ric_rec_sv_tv_res", "problems": [int(p) for p in problems],
+            "max_rel_err": e}
+
+
+def spread(n, total):
+    """n indices spread over [0, total)."""
+    return sorted({int(round(x)) for x in np.linspace(0, total - 1, n)})
+
+
 def cpu_baseline(qp, seconds, k_max, threads):
     """IP iterations/s of the reference c99 build (oracle/_ref, kind 'reference') -- or of the
     clean-room oracle (kind 'port') when the reference build is absent -- on the GPU box's host cores,
@@ -149,11 +233,22 @@ def cpu_baseline(qp, seconds, k_max, threads):
 
     v1, it1, s1, e1 = run(1, seconds * 0.3)
     vn, itn, sn, en = run(threads, seconds * 0.7)
-    return {"value": vn, "unit": "IP-iter/s", "cores": threads, "kind": kind, "host": host_cpu(),
-            "sample": f"first {nprob} problems of the benchmark batch, cold-start d_ip2_res_mpc_hard_tv "
-                      f"(k_max={k_max}) cycled by {threads} host threads for {en:.1f} s ({sn} solves, {itn} IP "
-                      f"iterations); pre-marshalled ctypes calls",
-            "single_core": {"value": v1, "solves": s1, "iters": it1, "seconds": e1}}
+    host = host_cpu()
+    phys = physical_cores()
+    host["physical_cores"] = phys
+    out = {"value": vn, "unit": "IP-iter/s", "cores": threads, "kind": kind, "host": host,
+           "sample": f"first {nprob} problems of the benchmark batch, cold-start d_ip2_res_mpc_hard_tv "
+                     f"(k_max={k_max}) cycled by {threads} host threads for {en:.1f} s ({sn} solves, {itn} IP "
+                     f"iterations); pre-marshalled ctypes calls",
+           "single_core": {"value": v1, "solves": s1, "iters": it1, "seconds": e1}}
+    if phys and phys > threads:
+        # the GPU box is one GPU's share of a shared host (16 CPUs per GPU): the run stays inside that share, and
+        # the all-core figure is the measured per-thread rate at `threads` threads times the physical cores (the
+        # per-thread rate is flat from 1 to `threads` threads: single_core vs value / threads)
+        out["all_cores_estimate"] = {"cores": phys, "value": vn / threads * phys, "unit": "IP-iter/s",
+                                     "basis": f"measured {vn / threads:.0f} IP-iter/s per thread at {threads} threads "
+                                              f"(1 thread: {v1:.0f}) x {phys} physical cores; not measured"}
+    return out
 
 
 def cpu_pcond_baseline(qp, N2, seconds, threads):
@@ -262,6 +357,21 @@ def bench_pcond(args, torch, red, rank, world, barrier):
            "kernels": kern}
     for n in names:
         kern[n]["traffic_bytes_per_launch"] = pcond_traffic(n, B)
+    ref = ref_api() if rank == 0 else None
+    if ref is not None:
+        # the reference's own condensing is wrong for nu > 4: the expanded solution is held to its direct
+        # Riccati solve of the uncondensed problem
+        torch.cuda.synchronize()
+        e = 0.0
+        for p in spread(8, B):
+            U, Pi = s.solution(p)
+            u2, p2, _, _ = ref.ric_sv(qp.problem(p), compute_pi=1, compute_Pb=0)
+            for k in range(N + 1):
+                e = max(e, rel_err(U[k], u2[k][:qp.nux(k)]))
+                if k < N:
+                    e = max(e, rel_err(Pi[k], p2[k][:int(qp.nx[k + 1])]))
+        out["parity"] = {"reference": "oracle/_ref c99 d_back_ric_rec_sv_tv_res on the uncondensed problem",
+                         "problems": spread(8, B), "max_rel_err": e}
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_pcond_baseline(qp, N2, args.cpu_seconds * 0.5, args.cpu_threads)
     out["ipm"] = bench_pcond_ipm(args, torch, red, rank, world, barrier)
@@ -399,6 +509,10 @@ def bench_single_qp(args, torch, stream):
     torch.cuda.synchronize()
     ms_batch = float(np.median([a.elapsed_time(b) for a, b in evb]))
     assert int(s.kk[0].item()) == kk
+    s.ipm_solo()
+    torch.cuda.synchronize()
+    par = parity_ipm(ref_api(), one, dict(ux=s.ux, pi=s.pi, lam=s.lam, t=s.t, kk=s.kk, ret=s.ret, k_max=args.k_max),
+                     [(0, 0)])
     call, kkc = HpmpcAPI(load(LIBPATH)).prepare_ipm(one.problem(0), k_max=args.k_max)
     call()
     t0 = time.perf_counter()
@@ -410,7 +524,7 @@ def bench_single_qp(args, torch, stream):
             "path": "hpmpc_mi355x_ipm_solo (one launch per solve, one problem per 4-wave workgroup: hk_ipm_solo_mw)",
             "single_wave_ms_per_solve": ms_single, "single_wave_us_per_ip_iter": ms_single * 1e3 / max(kk, 1),
             "queue1_ms_per_solve": ms_queue, "batch_api_ms_per_solve": ms_batch,
-            "dropin_ms_per_solve": host_ms, "dropin_kk": int(kkc.value)}
+            "dropin_ms_per_solve": host_ms, "dropin_kk": int(kkc.value), "parity": par}
 
 
 def bench_riccati_small(args, torch, red, rank, world, barrier, stream):
@@ -436,8 +550,9 @@ def bench_riccati_small(args, torch, red, rank, world, barrier, stream):
     ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     by = algorithmic_bytes_per_sv(qp)
     ach = B * by / (ms * 1e-3) / 1e9
+    par = parity_sv(ref_api(), qp, s.ux, s.pi, spread(8, B)) if rank == 0 else None
     return {"workload": f"riccati_N{N}_nx{nx}_nu{nu}_batch{B}", "value": B * world * args.steps / dt, "unit": "fact/s",
-            "launch_ms": ms, "roofline": {"bound": "hbm", "kernel": "hk_ric_sv", "achieved": ach, "peak": PEAK_HBM_GBS,
+            "launch_ms": ms, "parity": par, "roofline": {"bound": "hbm", "kernel": "hk_ric_sv", "achieved": ach, "peak": PEAK_HBM_GBS,
                                           "unit": "GB/s", "frac": ach / PEAK_HBM_GBS, "algorithmic_bytes_per_sv": by}}
 
 
@@ -585,6 +700,11 @@ def main():
     bytes_iter = algorithmic_bytes_per_ip_iter(qp)
     ipm_ms = float(pass_ms.sum())
     fl_iter = flops_ip_iter(N, nx, nu)
+    # parity sample of the timed run (after it): 8 queue entries spread over the K batches against the reference
+    ref = ref_api() if rank == 0 else None
+    nq = args.steps * B
+    par_ipm = parity_ipm(ref, qp, dict(ux=Q.ux, pi=Q.pi, lam=Q.lam, t=Q.t, kk=Q.kk, ret=Q.ret, k_max=args.k_max),
+                         [(q, q % B) for q in spread(8, nq)])
     del Q
 
     # the same K batches through a queue with one resident slot per problem of the batch (B slots: the
@@ -649,6 +769,7 @@ def main():
     rdt = max_over_ranks(r1 - r0)
     fact_total = B * world * args.steps
     sv_ms = float(np.mean([a.elapsed_time(b) for a, b in evr]))
+    par_sv = parity_sv(ref, qp_ric, ric.ux, ric.pi, spread(8, B))
     sv_bytes = algorithmic_bytes_per_sv(qp_ric)
     sv_achieved = B * sv_bytes / (sv_ms * 1e-3) / 1e9
 
@@ -724,7 +845,9 @@ def main():
             "generic_shape": dyn,
             "isolated_batch": iso,
             "scatter": sc,
+            "parity": par_ipm,
             "riccati": {"value": fact_total / rdt, "unit": "fact/s", "kernel": "hk_ric_sv", "launch_ms": sv_ms,
+                        "parity": par_sv,
                         "roofline": {"bound": "hbm", "achieved": sv_achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                                      "frac": sv_achieved / PEAK_HBM_GBS,
                                      "algorithmic_bytes_per_sv": sv_bytes,

@@ -16,8 +16,11 @@
 //     stage k, which stores ux, forms the box steps, the step-length candidates and pi.
 // The hand-over is a ring of MW_D slots in LDS (16 doubles per lane each) with a full / free flag per slot; the
 // flags carry tickets that grow over the whole launch, so no sweep has to reset them.  Every value is computed by
-// the same routine with the same operands as in the single-wave sweeps (hk_riccati.h), so the results are
-// bitwise those of hk_ipm_solo; the step length is the minimum of the helpers' per-lane candidates.
+// the same routine with the same operands as in the single-wave sweeps (hk_riccati.h); the step length is the
+// minimum of the helpers' per-lane candidates.  The results are bitwise those of hk_ipm_solo only when the product
+// terms are contracted into FMAs the same way in both kernels (they are with -ffp-contract=on, measured); under the
+// default contraction hipcc fuses a few a * b + c differently once the bodies are split over waves, and the two
+// agree to rounding (tests/test_gpu_parity.py test_solo_matches_batch).
 // A wait that does not end (a bug, not a data condition) sets MwShared.err after ~2^22 polls and falls through,
 // so every wave still reaches the end of the launch; the kernel then reports ret = HK_MW_ERR.
 #pragma once
@@ -31,7 +34,7 @@ constexpr int MW_SLOT = 16;  // doubles per lane per slot
 constexpr int MW_DP = 6;     // tile wave -> row wave ring (backward sweep)
 constexpr int MW_NMAX = 300;  // horizon limit of the multi-wave kernel (the update's reduction rows live in LDS)
 constexpr int MW_RED = ((MW_NMAX + 4) / 4 + 3) / 4 * 4;
-constexpr int HK_MW_ERR = -20;
+constexpr int HK_MW_ERR = -20;  // HPMPC_MI355X_EMW
 
 struct MwShared {
     double ring[MW_D][MW_SLOT][64];
@@ -41,8 +44,10 @@ struct MwShared {
     int full[MW_D], freed[MW_D];
     // backward sweep: the row wave's own free flags of the helpers' ring, and the tile wave -> row wave ring
     int freedB[MW_D];
-    double ringP[MW_DP][5][64];  // [stage record tile (4) | inverse diagonal]
+    // [stage record tile (4) | inverse diagonal | a clamped stage's x factor (4) and its inverse diagonal]
+    double ringP[MW_DP][10][64];
     int fullP[MW_DP], freedP[MW_DP];
+    int xfacP[MW_DP];  // the stage failed the clamp certificate (stage_chol xfac): rows 5..9 are valid
     int err;
     int dbg[4];  // the first expired wait: flag index (full: slot, freed: MW_D + slot), expected, found, wave
 #ifdef HK_STAMPS
@@ -57,6 +62,30 @@ __shared__ MwShared hk_mw;
 
 
 __device__ __forceinline__ int mw_flag(const int* f) { return __atomic_load_n(f, __ATOMIC_RELAXED); }
+
+// The hand-over's ordering, stated in the memory model: a flag store is a workgroup-scope release of this wave's
+// earlier LDS accesses (the slot data it wrote, or read before freeing the slot), a successful poll is followed by
+// the matching acquire.  Both fences are limited to the LDS address space ("local"): the release is one
+// s_waitcnt lgkmcnt(0) before the flag store, the acquire one after the poll (which has waited already).
+// HK_MW_FENCE=0 builds the earlier form -- compiler barriers only, relying on the LDS performing one wave's ds_
+// operations in issue order -- for an A/B of the cost (tools/gpu_ab.sh).
+#ifndef HK_MW_FENCE
+#define HK_MW_FENCE 1
+#endif
+__device__ __forceinline__ void mw_release_fence() {
+#if HK_MW_FENCE
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+#else
+    asm volatile("" ::: "memory");
+#endif
+}
+__device__ __forceinline__ void mw_acquire_fence() {
+#if HK_MW_FENCE
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+#else
+    asm volatile("" ::: "memory");
+#endif
+}
 
 __device__ __forceinline__ unsigned long long mw_clock() {
     unsigned long long t;
@@ -90,7 +119,7 @@ __device__ __forceinline__ void mw_wait_at(const int* f, int v, int i) {
         }
         if (mw_flag(&hk_mw.err)) break;  // after one expired wait every wait falls through: the launch drains
     }
-    asm volatile("" ::: "memory");
+    mw_acquire_fence();
 }
 
 // wait until the flag (full[i] for i < MW_D, freed[i - MW_D] otherwise) reaches v
@@ -98,12 +127,10 @@ __device__ __forceinline__ void mw_wait(int i, int v) {
     mw_wait_at(i < MW_D ? &hk_mw.full[i] : &hk_mw.freed[i - MW_D], v, i);
 }
 
-// publish *f = v behind this wave's earlier LDS accesses (the slot data).  The LDS performs one wave's ds_ operations
-// in issue order (lgkmcnt counts them down in order), so a wave that sees the flag sees the data written before it,
-// and a slot's reads are performed before its free flag: only the compiler must not move them (the memory
-// clobbers), the wave itself does not wait for them.
+// publish *f = v behind this wave's earlier LDS accesses (the slot data): a release (mw_release_fence) and a relaxed
+// store from one lane.
 __device__ __forceinline__ void mw_post_at(int* f, int v) {
-    asm volatile("" ::: "memory");
+    mw_release_fence();
     if (lane_id() == 0) __atomic_store_n(f, v, __ATOMIC_RELAXED);
     asm volatile("" ::: "memory");
 }
@@ -128,8 +155,11 @@ __device__ __forceinline__ double mw_get(int j, int i) { return hk_mw.ring[j % M
 //   wave 1 (row):  P_{k+1} b, the row update ml += BAbt (P b + p_{k+1}), the row half of each Cholesky block, the
 //                  gain block (stage_chol_row) and the stage record -- a second recursion (p_{k+1} -> p_k) that
 //                  needs the tile wave's factor but never feeds it, so it runs one stage behind;
-//   waves 2, 3 (helpers, every other stage): fetch, residuals, box terms -> ring = [M (4) | ml | bop (4) | brow (4)],
-//                  read by both recursions (its slot is free once both have read it).
+//   waves 2, 3 (helpers, every other stage): fetch, residuals, box terms -> ring = [M (4) | ml | bop (4) | brow (4) |
+//                  dq | T] (dq, T: the box diagonal and the clamp-certificate threshold, cert_ok), read by both
+//                  recursions (its slot is free once both have read it).
+// A stage that fails the clamp certificate is factorised as the reference does (stage_chol xfac): the tile wave
+// carries P_eff on and hands the x factor to the row wave, which adds its row half and p_eff = Lxx l_x.
 // ------------------------------------------------------------------------------------------------
 constexpr int MW_BHELP = 2;
 
@@ -163,10 +193,10 @@ __device__ __forceinline__ int ric_backward_mw(const RicIO& io, int tb, int w, i
             const int k = N - j;
             const StageInfo si = load_stage(io.st, k);
             d4 M;
-            double ml;
+            double ml, dq, T;
             with_shape<FX>(si, [&](const auto& sh) {
                 if constexpr (BM == BX_P2R) bwd_residual(io, sm, sh, k, bc, f, x1c, true);
-                bwd_pre<AUG, BM>(io, sh, k, f, bc, M, ml);
+                bwd_pre<AUG, BM>(io, sh, k, f, bc, M, ml, dq, T);
             });
             if (j >= MW_D) {  // the slot's previous occupant read by both recursions
                 mw_wait_at(&hk_mw.freed[j % MW_D], tb + j - MW_D + 1, MW_D + j % MW_D);
@@ -179,6 +209,8 @@ __device__ __forceinline__ int ric_backward_mw(const RicIO& io, int tb, int w, i
                 mw_put(j, 9 + r, f.brow[r]);
             }
             mw_put(j, 4, ml);
+            mw_put(j, 13, dq);
+            mw_put(j, 14, T);
             mw_post(j % MW_D, tb + j + 1);
         };
         BwdFrag fa, fb;
@@ -200,6 +232,7 @@ __device__ __forceinline__ int ric_backward_mw(const RicIO& io, int tb, int w, i
         // released once this step is done, by which time those reads have long completed
         d4 P = {0.0, 0.0, 0.0, 0.0};  // record tile of stage k+1 (its x block is P_{k+1})
         d4 Mn, bopn;
+        double dqn, Tn;
         auto take = [&](int j) __attribute__((always_inline)) {
             mw_wait(j % MW_D, tb + j + 1);
 #pragma unroll
@@ -207,6 +240,8 @@ __device__ __forceinline__ int ric_backward_mw(const RicIO& io, int tb, int w, i
                 Mn[r] = mw_get(j, r);
                 bopn[r] = mw_get(j, 5 + r);
             }
+            dqn = mw_get(j, 13);
+            Tn = mw_get(j, 14);
         };
         take(0);
         StageInfo sn = load_stage(io.st, N);
@@ -228,20 +263,24 @@ __device__ __forceinline__ int ric_backward_mw(const RicIO& io, int tb, int w, i
             const StageInfo si = sn;
             d4 M = Mn;
             const d4 bop = bopn;
+            const double dq = dqn, T = Tn;
             if (j < N) {
                 take(j + 1);
                 sn = load_stage(io.st, k - 1);
             }
             MW_SEG(0);
             double invd;
+            bool xfac = false;
+            XFac xf;
             with_shape<FX>(si, [&](const auto& sh) {
                 using SHT = std::remove_reference_t<decltype(sh)>;
                 const bool live = SHT::fixed || k < N;
                 bwd_tile_update(sh, live, bop, P, M);
                 MW_SEG(1);
                 double mld = 0.0;
-                stage_chol<false, false>(M, mld, invd, sh.nu, sh.nx, sh.xo, !SHT::fixed && k == 0, !SHT::fixed,
-                                         nullptr, k);
+                const bool full = !SHT::fixed && k == 0;
+                xfac = !full && !cert_ok(M, dq, T);
+                stage_chol<false, false>(M, mld, invd, sh.nu, sh.nx, sh.xo, full, !SHT::fixed, nullptr, k, xfac, &xf);
                 MW_SEG(2);
             });
             P = M;
@@ -250,6 +289,12 @@ __device__ __forceinline__ int ric_backward_mw(const RicIO& io, int tb, int w, i
 #pragma unroll
             for (int r = 0; r < 4; r++) hk_mw.ringP[j % MW_DP][r][l] = P[r];
             hk_mw.ringP[j % MW_DP][4][l] = invd;
+            if (xfac) {  // wave-uniform
+#pragma unroll
+                for (int r = 0; r < 4; r++) hk_mw.ringP[j % MW_DP][5 + r][l] = xf.L[r];
+                hk_mw.ringP[j % MW_DP][9][l] = xf.invd;
+            }
+            if (l == 0) hk_mw.xfacP[j % MW_DP] = xfac ? 1 : 0;
             mw_post_at(&hk_mw.fullP[j % MW_DP], tb + j + 1);
             MW_SEG(3);
         }
@@ -284,11 +329,23 @@ __device__ __forceinline__ int ric_backward_mw(const RicIO& io, int tb, int w, i
 #pragma unroll
             for (int r = 0; r < 4; r++) S[r] = hk_mw.ringP[j % MW_DP][r][l];
             const double invd = hk_mw.ringP[j % MW_DP][4][l];
+            const bool xfac = __builtin_amdgcn_readfirstlane(hk_mw.xfacP[j % MW_DP]) != 0;
+            XFac xf;
+            if (xfac) {
+#pragma unroll
+                for (int r = 0; r < 4; r++) xf.L[r] = hk_mw.ringP[j % MW_DP][5 + r][l];
+                xf.invd = hk_mw.ringP[j % MW_DP][9][l];
+            }
             mw_post_at(&hk_mw.freedP[j % MW_DP], tb + j + 1);
             double kg = 0.0;
             with_shape<FX>(si, [&](const auto& sh) {
                 using SHT = std::remove_reference_t<decltype(sh)>;
                 stage_chol_row<AUG, SHT::fixed>(S, invd, ml, sh.nu, sh.nx, sh.xo, !SHT::fixed && k == 0, &kg);
+                if (AUG && xfac) {  // the clamped x block's row half and p_eff = Lxx l_x (stage_chol xfac)
+                    double lx = ml;
+                    xblocks_chol_row(xf.L, xf.invd, lx, sh.nx, sh.xo);
+                    pform_eff_row(xf.L, lx, sh.nx, sh.xo, ml);
+                }
                 // the stage record, in the format of the stage's shape class (as ric_backward)
                 double* Fk = io.F + (long)k * FSTRIDE;
                 if constexpr (SHT::fixed)

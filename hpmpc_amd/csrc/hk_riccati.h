@@ -248,6 +248,137 @@ __device__ __forceinline__ void stage_chol_row(const d4& S, double invd, double&
     if (12 < nu || (full && 15 >= xo && 12 < hi)) chol_block_row<3, AUG, false>(S, invd, ml, nullptr);
 }
 
+// ------------------------------------------------------------------------------------------------
+// The reference's inner-stage x-pivot clamp on the P form (kernel_dpotrf_c99_lib4.c:555-640, SURVEY.md
+// Appendix C).  The reference factorises every stage completely and clamps a pivot d <= 1e-15 to 0 (its column of
+// L becomes 0), so what it carries to the next stage is not P_k but P_eff = Lxx Lxx' and p_eff = Lxx l_x of the
+// clamped factor.  Without a clamp the two are the same quantity (the P form below); with one they differ by the
+// dropped rank-one term.  A stage therefore keeps the cheap P form only when a certificate shows that none of the
+// reference's x pivots can reach the clamp, and otherwise factorises its x block as the reference does and stores
+// P_eff / p_eff in the record instead of P / p (all consumers of the record read P and p only).
+//
+// The certificate (per stage, per factorisation):
+//   g  = Gershgorin lower bound of the stage's DATA block RSQ_k (min_i M_ii - sum_{j != i} |M_ij| over the active
+//        rows): every later term (box Hessian >= 0, DCt diag(Q) DCt' >= 0, BAbt P_{k+1} BAbt' >= 0 -- the
+//        reference's W W' is an exact Gram product of its own W) only raises the smallest eigenvalue, and every
+//        Cholesky pivot of the full stage matrix -- the x pivots are those of the Schur complement -- is at least
+//        M_ii lambda_min(D^-1/2 M D^-1/2) >= M_ii g / e_max, with e_max = max_i (M_ii - box_i) (the box terms are
+//        diagonal and cancel from that ratio);
+//   the reference's computed pivots are exact pivots of M + dM with |dM_ij| <= c n eps sqrt(M_ii M_jj) (Cholesky's
+//        componentwise backward error; the reference's own M differs from ours by rounding of the same order), so
+//        with 1e-11 >> 16 n eps as the allowance the certificate is  g (g / e_max - 1e-11) > 1e-15, i.e.
+//        e_max < T(g) = min(1e11 g, g^2 / (1e-15 + 1e-11 g))  (T < 0 when g <= 0: no certificate).
+// The threshold T depends on the data only; the e_max test is one compare per diagonal entry and a ballot.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ double cert_T(double g) {
+    return g > 0.0 ? fmin(1e11 * g, g * g / fma(1e-11, g, 1e-15)) : -1.0;
+}
+
+// T of a stage from its data tile Mi (symmetric, zero outside the active rows / columns).  Row sums of |Mi| by MFMA
+// against a ones operand (the A fragment of K-chunk kc is register kc itself: lane (g,c) holds Mi[4kc+g][c] =
+// Mi[c][4kc+g]), the diagonal margin on the lane that holds it, then one wave minimum.
+template <class SH>
+__device__ __forceinline__ double cert_threshold(const d4& Mi, const SH& sh) {
+    const int l = lane_id(), g = l >> 4, c = l & 15;
+    const d4 z = {0.0, 0.0, 0.0, 0.0};
+    d4 r0 = z, r1 = z;
+#pragma unroll
+    for (int kc = 0; kc < 4; kc++) {
+        const bool any = 4 * kc < sh.nu || (4 * kc + 3 >= sh.xo && 4 * kc < sh.xo + sh.nx);
+        if (!any) continue;  // uniform: chunk without an active variable (its rows are zero)
+        if (kc & 1)
+            r1 = mfma(fabs(Mi[kc]), 1.0, r1);
+        else
+            r0 = mfma(fabs(Mi[kc]), 1.0, r0);
+    }
+    const d4 rs = r0 + r1;
+    double m = 1e300;
+    const bool act = tile_active(c, sh.nu, sh.nx, sh.xo);
+#pragma unroll
+    for (int r = 0; r < 4; r++) m = (c == g + 4 * r && act) ? Mi[r] + fabs(Mi[r]) - rs[r] : m;
+    return cert_T(wave_min(m));
+}
+
+// The certificate on the stage matrix M (after the tile update, before the factorisation): every diagonal entry
+// without its box term dq below T.  Wave-uniform (ballot of the failing lanes).
+__device__ __forceinline__ bool cert_ok(const d4& M, double dq, double T) {
+    const int l = lane_id(), g = l >> 4, c = l & 15;
+    // a negative given box term (BX_GIVEN) is not covered by the bound: no certificate
+    bool bad = dq < 0.0;
+#pragma unroll
+    for (int r = 0; r < 4; r++) bad = bad || (c == g + 4 * r && !(M[r] - dq < T));
+    return __builtin_amdgcn_ballot_w64(bad) == 0;
+}
+
+// l[4R + g] (row layout of a col-layout vector over tile block R): the pivot entries of block R
+template <int R>
+__device__ __forceinline__ double lrow_blk(double v) {
+    return sel_g(row_bcast<4 * R + 0>(v), row_bcast<4 * R + 1>(v), row_bcast<4 * R + 2>(v), row_bcast<4 * R + 3>(v));
+}
+
+// The x columns of the factor as MFMA operands: lane (g,c) of block R holds L[c][4R+g] (upper storage, c >= 4R+g)
+// for the x pivots 4R+g >= xo, zero elsewhere.
+__device__ __forceinline__ double xcol_op(const d4& L, int R, int xo) {
+    const int l = lane_id(), g = l >> 4, c = l & 15;
+    const int p = 4 * R + g;
+    return (p >= xo && c >= p) ? L[R] : 0.0;
+}
+
+// P_eff = Lxx Lxx' (one MFMA per x block, A = B = the block's columns of L) written over the x block of M (both
+// triangles).
+__device__ __forceinline__ void pform_eff_tile(const d4& L, int nx, int xo, d4& M) {
+    const int l = lane_id(), g = l >> 4, c = l & 15;
+    const d4 z = {0.0, 0.0, 0.0, 0.0};
+    d4 Pe = z;
+#pragma unroll
+    for (int R = 0; R < 4; R++) {
+        if (4 * R + 3 < xo || 4 * R >= xo + nx) continue;  // uniform
+        const double a = xcol_op(L, R, xo);
+        Pe = mfma(a, a, Pe);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) M[r] = (g + 4 * r >= xo && c >= xo) ? Pe[r] : M[r];
+}
+
+// p_eff = Lxx l_x (col layout) written over the x part of ml; lx holds the clamped factor's row l (x part).
+__device__ __forceinline__ void pform_eff_row(const d4& L, double lx, int nx, int xo, double& ml) {
+    const int c = lane_id() & 15;
+    double part = 0.0;
+    if (4 * 0 + 3 >= xo && 0 < xo + nx) part += xcol_op(L, 0, xo) * lrow_blk<0>(lx);
+    if (4 * 1 + 3 >= xo && 4 < xo + nx) part += xcol_op(L, 1, xo) * lrow_blk<1>(lx);
+    if (4 * 2 + 3 >= xo && 8 < xo + nx) part += xcol_op(L, 2, xo) * lrow_blk<2>(lx);
+    if (4 * 3 + 3 >= xo && 12 < xo + nx) part += xcol_op(L, 3, xo) * lrow_blk<3>(lx);
+    const double pe = xrow_sum(part);
+    ml = c >= xo ? pe : ml;
+}
+
+// The x-block factorisation of a stage whose u pivots are done (the reference's remaining dsyrk_dpotrf pivots,
+// with the same clamp): M (in: u rows factorised, x block = P; out: x rows = upper storage of Lxx), ml (x part: p ->
+// l_x), invd (x pivots' inverse diagonal added).
+template <bool AUG>
+__device__ __forceinline__ void xblocks_chol(d4& M, double& ml, double& invd, int nx, int xo) {
+    const int hi = xo + nx;
+    if (0 >= xo && 0 < hi) chol_block<0, AUG>(M, ml, invd);
+    if (4 >= xo && 4 < hi) chol_block<1, AUG>(M, ml, invd);
+    if (8 >= xo && 8 < hi) chol_block<2, AUG>(M, ml, invd);
+    if (12 >= xo && 12 < hi) chol_block<3, AUG>(M, ml, invd);
+}
+
+// Its row half on another wave (hk_mw.h: the row recursion), from the x factor L and its inverse diagonal.
+__device__ __forceinline__ void xblocks_chol_row(const d4& L, double invd, double& ml, int nx, int xo) {
+    const int hi = xo + nx;
+    if (0 >= xo && 0 < hi) chol_block_row<0, true, false>(L, invd, ml, nullptr);
+    if (4 >= xo && 4 < hi) chol_block_row<1, true, false>(L, invd, ml, nullptr);
+    if (8 >= xo && 8 < hi) chol_block_row<2, true, false>(L, invd, ml, nullptr);
+    if (12 >= xo && 12 < hi) chol_block_row<3, true, false>(L, invd, ml, nullptr);
+}
+
+// What a clamped stage hands the row recursion of the multi-wave kernel: the x factor and its inverse diagonal.
+struct XFac {
+    d4 L;
+    double invd;
+};
+
 // Stage factorisation with the augmented row.
 // In : M (tile, full symmetric), ml (aug row, col layout).
 // full == true : the whole stage Cholesky (d_back_ric_rec.c:325, dsyrk_dpotrf_lib), M = S = lower(L) +
@@ -263,9 +394,13 @@ __device__ __forceinline__ void stage_chol_row(const d4& S, double invd, double&
 //                == column p of L, p < nu), invd holds the u pivots only.
 // Generic shapes restore the lower triangle by an identity-MFMA transpose (L_xu for the generic forward,
 // and P symmetrised); fixed shapes skip it (their consumers read the upper u rows and the P block only).
+// xfac (P form only, wave-uniform): the stage failed the clamp certificate (cert_ok) -- its x block is factorised
+// as the reference does and the record carries P_eff = Lxx Lxx' and p_eff = Lxx l_x (the x factor and its inverse
+// diagonal also go to *xf when given); invd keeps the u pivots only, as in every P-form record.
 template <bool AUG, bool KGEN = false>
 __device__ __forceinline__ void stage_chol(d4& M, double& ml, double& invd, int nu, int nx, int xo, bool full,
-                                           bool transpose, double* kg = nullptr, int kdbg = -1) {
+                                           bool transpose, double* kg = nullptr, int kdbg = -1, bool xfac = false,
+                                           XFac* xf = nullptr) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
     (void)kdbg;
     invd = 0.0;
@@ -279,6 +414,17 @@ __device__ __forceinline__ void stage_chol(d4& M, double& ml, double& invd, int 
     HK_STAMP(20, kdbg);
     if (12 < nu || (full && 15 >= xo && 12 < hi)) chol_block<3, AUG>(M, ml, invd, nullptr, kdbg);
     HK_STAMP(22, kdbg);
+    if (!full && xfac) {
+        d4 L = M;
+        double lx = ml, ivx = invd;
+        xblocks_chol<AUG>(L, lx, ivx, nx, xo);
+        pform_eff_tile(L, nx, xo, M);
+        if (AUG) pform_eff_row(L, lx, nx, xo, ml);
+        if (xf) {
+            xf->L = L;
+            xf->invd = ivx;
+        }
+    }
     if (!transpose) return;
     // lower triangle <- transpose of the upper storage:  T = S' via MFMA with an identity B operand
     // (two accumulator chains: the identity products are exact, so the split does not change T)
@@ -928,12 +1074,15 @@ __device__ __forceinline__ void bwd_residual(const RicIO& io, Scratch* sm, const
 // First half of a backward stage: the stage tile and augmented row with the box (and general) Hessian /
 // gradient terms added -- everything that does not depend on the recursion (the multi-wave solo kernel runs it
 // on a helper wave, hk_mw.h).
+// dq (col layout): the box term on the diagonal; T: the stage's clamp-certificate threshold (cert_threshold,
+// from the data tile; unused on a stage that is fully factorised).
 template <bool AUG, int BM, class SH>
 __device__ __forceinline__ void bwd_pre(const RicIO& io, const SH& sh, int k, const BwdFrag& cur, const BoxCtx& bc,
-                                        d4& M, double& ml) {
+                                        d4& M, double& ml, double& dq, double& T) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
-    double dq, qxv;
+    double qxv;
     box_hessian<AUG, BM>(bc, cur, dq, qxv);
+    T = (SH::fixed || k > 0) ? cert_threshold(cur.Mi, sh) : 0.0;
     M = cur.Mi;
     ml = cur.mlq + qxv;  // update_q row (or RSQrq row) + drowad qx
 #pragma unroll
@@ -1006,16 +1155,18 @@ __device__ __forceinline__ void bwd_row_update(const RicIO& io, Scratch* sm, con
 // Second half: M += BAbt P BAbt', the row update and the stage factorisation (the recursion's chain).
 template <bool AUG, class SH>
 __device__ __forceinline__ void bwd_core(const RicIO& io, Scratch* sm, const SH& sh, int k, const d4& bop,
-                                         const d4& brow, d4 M, double ml, int compute_Pb, double* Pb, d4& S,
-                                         double& ml_prev, double& invd_prev, double& kg_prev) {
+                                         const d4& brow, d4 M, double ml, double dq, double T, int compute_Pb,
+                                         double* Pb, d4& S, double& ml_prev, double& invd_prev, double& kg_prev) {
     const bool live = SH::fixed || k < io.N;
     bwd_tile_update(sh, live, bop, S, M);
+    // stage 0 of a generic problem keeps the full factor; every other stage is factorised in P form, with its x
+    // block factorised as well where the clamp certificate fails (stage_chol)
+    const bool full = !SH::fixed && k == 0;
+    const bool xfac = !full && !cert_ok(M, dq, T);
     if (AUG) bwd_row_update(io, sm, sh, k, live, bop, brow, S, ml_prev, compute_Pb, Pb, ml);
     HK_STAMP(2, k);
     double invd, kg = 0.0;
-    // stage 0 of a generic problem keeps the full factor; every other stage is factorised in P form
-    const bool full = !SH::fixed && k == 0;
-    stage_chol<AUG, SH::fixed>(M, ml, invd, sh.nu, sh.nx, sh.xo, full, !SH::fixed, &kg, k);
+    stage_chol<AUG, SH::fixed>(M, ml, invd, sh.nu, sh.nx, sh.xo, full, !SH::fixed, &kg, k, xfac);
     kg_prev = kg;
     HK_STAMP(3, k);
 #pragma unroll
@@ -1033,9 +1184,9 @@ __device__ __forceinline__ void bwd_step(const RicIO& io, Scratch* sm, const SH&
                                          const BoxCtx& bc, int compute_Pb, double* Pb, d4& S, double& ml_prev,
                                          double& invd_prev, double& kg_prev) {
     d4 M;
-    double ml;
-    bwd_pre<AUG, BM>(io, sh, k, cur, bc, M, ml);
-    bwd_core<AUG>(io, sm, sh, k, cur.bop, cur.brow, M, ml, compute_Pb, Pb, S, ml_prev, invd_prev, kg_prev);
+    double ml, dq, T;
+    bwd_pre<AUG, BM>(io, sh, k, cur, bc, M, ml, dq, T);
+    bwd_core<AUG>(io, sm, sh, k, cur.bop, cur.brow, M, ml, dq, T, compute_Pb, Pb, S, ml_prev, invd_prev, kg_prev);
 }
 
 // Backward Riccati recursion (sv when AUG, trf otherwise), d_back_ric_rec.c:186-335 / :447-558.

@@ -1086,6 +1086,12 @@ int ipm_entry(int single_newton, int phase1_only, int* kk, int k_max, double mu0
     if (!down(A)) return g_err;
     const int* iv = reinterpret_cast<const int*>(H + A.ints);
     *kk = iv[0];
+    if (iv[1] == HPMPC_MI355X_EMW) {
+        // the multi-wave kernel abandoned the solve (an expired hand-over wait: a bug, never a data condition); its
+        // stat holds diagnostics and its iterate is not a solution, so nothing is copied out
+        set_err(HPMPC_MI355X_EMW, "hk_ipm_solo_mw: expired hand-over wait, solve abandoned");
+        return g_err;
+    }
     for (int i = 0; i < 5 * iv[0]; i++) stat[i] = H[A.stat + i];
     // d_ip2_mpc_hard_tv without constraints solves into its workspace only (d_ip2_hard.c:282-291)
     const bool outputs = !(phase1_only && P->nbt == 0);

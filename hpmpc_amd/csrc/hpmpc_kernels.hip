@@ -7,6 +7,7 @@
 // early simply retire their wave.
 #include "hk_ipm.h"
 #include "hk_mw.h"
+#include "hk_launch_guard.h"
 #include "hpmpc_kargs.h"
 #include <cstdlib>
 
@@ -1158,20 +1159,16 @@ static int launch_t(int which, const KArgs* a, int count, hipStream_t stream) {
         // the whole IPM per problem in one launch (hk_ipm_solo)
         case 15:
         case 16: {
-            // one problem per 256-thread workgroup (hk_ipm_solo_mw) unless its LDS carve does not fit or
-            // HPMPC_MI355X_SOLO=1 asks for the single-wave kernel; which == 16 forces the single-wave one
-            static int lds_max = -1;
-            if (lds_max < 0) {
-                int dev = 0, v = 0;
-                (void)hipGetDevice(&dev);
-                (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, dev);
-                lds_max = v;
-            }
+            // one problem per 256-thread workgroup (hk_ipm_solo_mw) unless HPMPC_MI355X_SOLO=1 asks for the
+            // single-wave kernel (which == 16 forces it), the horizon exceeds the kernel's LDS tables, or the
+            // launch guard (static + dynamic LDS, private segment vs the stack limit, launch bound; read once, with
+            // thread-safe static initialisation) refuses it: then the single-wave kernel runs instead
+            static const HkKernelLimits lim_mw(reinterpret_cast<const void*>(&hk_ipm_solo_mw<FX>));
             const char* env = getenv("HPMPC_MI355X_SOLO");
             const bool single = which == 16 || (env && env[0] == '1');
             const size_t lds_mw = mw_lds_bytes(a->N);
             hipLaunchKernelGGL(hk_ipm_init<FX>, grid, block, lds, stream, *a);
-            if (!single && a->N <= MW_NMAX && lds_mw + sizeof(MwShared) <= (size_t)lds_max)
+            if (!single && a->N <= MW_NMAX && lim_mw.check(lds_mw, 256) == 0)
                 hipLaunchKernelGGL(hk_ipm_solo_mw<FX>, grid, dim3(256), lds_mw, stream, *a);
             else
                 hipLaunchKernelGGL(hk_ipm_solo<FX>, grid, block, lds, stream, *a);

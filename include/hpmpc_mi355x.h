@@ -22,8 +22,10 @@
  *   Part 1 serves both; the batched Part 2 takes tile-path plans (plus the partial-condensing pipeline).
  *   Beyond these limits, and for duplicate box indices, calls report HPMPC_MI355X_EUNSUPPORTED.
  * Error reporting: the reference's int entry points keep their codes 0/1/2/-1; this library adds
- *   HPMPC_MI355X_EUNSUPPORTED (-10) and HPMPC_MI355X_EHIP (-11).  void entry points set the
- *   thread-local code returned by hpmpc_mi355x_last_error() and print one line to stderr.
+ *   HPMPC_MI355X_EUNSUPPORTED (-10), HPMPC_MI355X_EHIP (-11) and HPMPC_MI355X_EMW (-20: the one-problem latency
+ *   kernel abandoned a solve after an expired hand-over wait between its waves -- a bug, never a data condition;
+ *   see hpmpc_mi355x_ipm_solo).  void entry points set the thread-local code returned by
+ *   hpmpc_mi355x_last_error() and print one line to stderr; int entry points set it too.
  */
 #ifndef HPMPC_MI355X_H_
 #define HPMPC_MI355X_H_
@@ -34,6 +36,7 @@ extern "C" {
 
 #define HPMPC_MI355X_EUNSUPPORTED (-10)
 #define HPMPC_MI355X_EHIP (-11)
+#define HPMPC_MI355X_EMW (-20)
 
 /* ================================ Part 1: reference entry points ================================ */
 
@@ -288,7 +291,12 @@ int hpmpc_mi355x_ipm_batch(const hpmpc_mi355x_plan *plan, const hpmpc_mi355x_lay
 /* Latency path: hpmpc_mi355x_ipm_batch with each problem's WHOLE solve in one launch -- one workgroup per problem
  * runs init and every iteration's passes back to back on one CU, so its stage data and factor stay in that XCD's L2
  * and no launch or host poll separates the passes.  For a lone problem or a handful (configs[1]); for throughput
- * over many problems use hpmpc_mi355x_ipm_queue.  Same arguments and results as hpmpc_mi355x_ipm_batch. */
+ * over many problems use hpmpc_mi355x_ipm_queue.  Same arguments as hpmpc_mi355x_ipm_batch; the results agree with
+ * it to rounding (the four-wave kernel splits each sweep over waves and hipcc contracts a few products
+ * differently), with the same kk and ret on every tested problem.  One exception: if a hand-over wait between the
+ * kernel's waves expires (~2^22 polls; a bug, never a data condition) the solve stops after that iteration with
+ * ret[p] = HPMPC_MI355X_EMW and stat[5 k_max p + 0..3] = diagnostic integers (flag, expected, found, wave); the
+ * reference-named entry points then return HPMPC_MI355X_EMW, set hpmpc_mi355x_last_error() and copy nothing. */
 int hpmpc_mi355x_ipm_solo(const hpmpc_mi355x_plan *plan, const hpmpc_mi355x_layout *lay, int nprob, int p0, int count,
                           const double *BAbt, const double *RSQrq, const double *d, double *ux, double *pi,
                           double *lam, double *t, double *ws, int k_max, double mu0, double mu_tol, double alpha_min,
