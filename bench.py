@@ -68,6 +68,7 @@ def parse():
     ap.add_argument("--no-scatter", action="store_true", help="skip the rank-0 scatter / gather leg (N > 1)")
     ap.add_argument("--no-queue-batch-slots", action="store_true", help="skip the queue run with one slot per "
                     "problem of the batch")
+    ap.add_argument("--no-aliased", action="store_true", help="skip the time-invariant / aliased leg")
     ap.add_argument("--check-launch", action="store_true", help="start the ranks, join the process group (gloo) "
                     "and print each rank's world size, without touching the GPU (launcher test)")
     return ap.parse_args()
@@ -556,6 +557,43 @@ def bench_riccati_small(args, torch, red, rank, world, barrier, stream):
                                           "unit": "GB/s", "frac": ach / PEAK_HBM_GBS, "algorithmic_bytes_per_sv": by}}
 
 
+def bench_aliased(args, torch, red, rank, world, barrier, slots):
+    """SURVEY.md §8d's aliased "time-invariant" mode, reported beside the headline: the same IPM workload, but every
+    problem shares one A / B / Q / R (time-invariant mass-spring data, the drivers' aliasing, test_d_ip_hard.c:652-662)
+    and the problems differ only in x0, so the batched layout holds one copy of every stage block except stage 0's
+    (hpmpc_mi355x_layout BAbt_shared / RSQrq_shared) and the stage data stay in L2 / the Infinity Cache.  Timed
+    through the same problem queue; beside it the same data in the ordinary per-problem layout."""
+    from hpmpc_amd.batch import BatchSolver
+    from hpmpc_amd.shard import make_shard
+
+    B, N, nx, nu = args.batch, args.N, args.nx, args.nu
+    qa = make_shard(N, nx, nu, rank, world, B, time_variant=False)
+    out = {"workload": f"ipm_N{N}_nx{nx}_nu{nu}_batch{B}_time_invariant_aliased", "unit": "IP-iter/s"}
+    for name, aliased in (("aliased", True), ("per_problem_layout", False)):
+        s = BatchSolver(qa, k_max=args.k_max, aliased=aliased)
+        s.queue(B, slots).run()
+        Q = s.queue(args.steps * B, slots)
+        barrier()
+        t0 = time.perf_counter()
+        pm, ticks = Q.run(profiled=True)
+        barrier()
+        dt = red.max(time.perf_counter() - t0)
+        it = red.sum(float(Q.kk.sum().item()))
+        r = {"value": it / dt, "ms_per_step": dt / args.steps * 1e3,
+             "stage_data_bytes": int((s.BAbt.numel() + s.RSQrq.numel()) * 8),
+             "pass_ms_per_step": {n: float(v) / args.steps for n, v in
+                                  zip(["hk_ipm_init", "hk_ipm_fact", "hk_ipm_pred", "hk_ipm_corr", "hk_ipm_update"], pm)}}
+        if aliased:
+            out.update(r)
+            ref = ref_api() if rank == 0 else None
+            out["parity"] = parity_ipm(ref, qa, dict(ux=Q.ux, pi=Q.pi, lam=Q.lam, t=Q.t, kk=Q.kk, ret=Q.ret,
+                                                     k_max=args.k_max), [(q, q % B) for q in spread(8, args.steps * B)])
+        else:
+            out[name] = r
+        del Q, s
+    return out
+
+
 def bench_scatter(args, torch, dist, rank, world, solver, template, B, barrier):
     """configs[3]'s data path (SURVEY.md §8e scatter mode): rank 0 holds every rank's block in HBM and sends
     it over RCCL point-to-point (xGMI), each rank solves its block through the problem queue, and ux / pi /
@@ -753,6 +791,8 @@ def main():
                "note": "one batch solved alone (hpmpc_mi355x_ipm_batch): every pass runs k_max times, so the "
                        "slowest problem sets the time"}
 
+    ali = None if args.no_aliased else bench_aliased(args, torch, red, rank, world, barrier, slots)
+
     # ---------------- Riccati factorisation + solve ----------------
     for _ in range(args.warmup):
         ric.ric_sv()
@@ -842,6 +882,7 @@ def main():
                                              "algorithmic_bytes_per_ip_iter": bytes_iter,
                                              "fp64_tflops": iters_rank * fl_iter / (ipm_ms * 1e-3) / 1e12}},
             "queue_batch_slots": qb,
+            "aliased": ali,
             "generic_shape": dyn,
             "isolated_batch": iso,
             "scatter": sc,

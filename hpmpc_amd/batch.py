@@ -71,7 +71,35 @@ def lib() -> C.CDLL:
 
 class _Layout(C.Structure):
     _fields_ = [("BAbt_stride", C.c_longlong), ("RSQrq_stride", C.c_longlong),
-                ("BAbt_off", C.POINTER(C.c_longlong)), ("RSQrq_off", C.POINTER(C.c_longlong))]
+                ("BAbt_off", C.POINTER(C.c_longlong)), ("RSQrq_off", C.POINTER(C.c_longlong)),
+                ("BAbt_shared", C.POINTER(C.c_ubyte)), ("RSQrq_shared", C.POINTER(C.c_ubyte))]
+
+
+def aliased_layout(qp: OCPQP):
+    """The time-invariant / aliased device layout of a batch whose problems differ only in stage 0's BAbt block (its b
+    row carries A x0 + b): every other stage block is the same in every problem, and every inner stage the same as
+    stage 1 (the reference drivers' aliasing, test_problems/test_d_ip_hard.c:652-662).  Returns the packed arrays
+    (BAbt: [shared inner block | stage 0 of problem 0 | stage 0 of problem 1 | ...], RSQrq: [stage 0 | inner | N],
+    shared by all problems), the strides, the offsets and the shared flags of hpmpc_mi355x_layout.  Raises
+    ValueError when the data do not alias that way."""
+    N, P = qp.N, qp.batch
+    for k in range(1, N):
+        for a, b in ((qp.BAbt[k], qp.BAbt[1]), (qp.RSQrq[k], qp.RSQrq[1])):
+            if a.shape != b.shape or not np.array_equal(a, b):
+                raise ValueError(f"stage {k} is not stage 1's (time-invariant inner stages needed)")
+    for arr in list(qp.BAbt[1:]) + list(qp.RSQrq):
+        if not (arr == arr[:1]).all():
+            raise ValueError("stage data other than BAbt_0 differ between problems")
+    inner = qp.BAbt[1][0] if N > 1 else np.zeros(0)
+    b0 = qp.BAbt[0]
+    hB = np.concatenate([inner, b0.reshape(-1)])
+    offB = np.array([inner.size] + [0] * (N - 1), dtype=np.int64)
+    shB = np.array([0] + [1] * (N - 1), dtype=np.uint8)
+    r0, r1, rN = qp.RSQrq[0][0], qp.RSQrq[1][0], qp.RSQrq[N][0]
+    hR = np.concatenate([r0, r1, rN])
+    offR = np.array([0] + [r0.size] * (N - 1) + [r0.size + r1.size], dtype=np.int64)
+    shR = np.ones(N + 1, dtype=np.uint8)
+    return hB, hR, int(b0.shape[1]), 0, offB, offR, shB, shR
 
 
 def stage_offsets(qp: OCPQP):
@@ -125,7 +153,7 @@ class BatchSolver:
     idxb); BAbt / RSQrq / d are allocated for ``nprob`` problems and filled by the caller, e.g. by the rank-0
     scatter of hpmpc_amd.shard."""
 
-    def __init__(self, qp: OCPQP, device="cuda", k_max: int = 50, nprob: int | None = None):
+    def __init__(self, qp: OCPQP, device="cuda", k_max: int = 50, nprob: int | None = None, aliased: bool = False):
         import torch
 
         if not torch.cuda.is_available():
@@ -150,13 +178,28 @@ class BatchSolver:
         if not self.plan:
             raise ValueError(f"unsupported problem sizes for the GPU path (code {L.hpmpc_mi355x_last_error()})")
         # problem-major packed inputs
-        offB, offR, packB, packR = stage_offsets(qp)
-        self.offB, self.offR = offB, offR
-        self.layout = _Layout(packB, packR, offB.ctypes.data_as(C.POINTER(C.c_longlong)),
-                              offR.ctypes.data_as(C.POINTER(C.c_longlong)))
         f64 = torch.float64
         P = self.nprob
-        if nprob is None:
+        self.aliased = aliased
+        if aliased:  # one copy of every shared stage block (hpmpc_mi355x_layout BAbt_shared / RSQrq_shared)
+            assert nprob is None
+            hB, hR, sB, sR, offB, offR, shB, shR = aliased_layout(qp)
+            self.offB, self.offR, self._sh = offB, offR, (shB, shR)
+            u8 = C.POINTER(C.c_ubyte)
+            self.layout = _Layout(sB, sR, offB.ctypes.data_as(C.POINTER(C.c_longlong)),
+                                  offR.ctypes.data_as(C.POINTER(C.c_longlong)), shB.ctypes.data_as(u8),
+                                  shR.ctypes.data_as(u8))
+            self.BAbt = torch.from_numpy(hB).to(self.dev)
+            self.RSQrq = torch.from_numpy(hR).to(self.dev)
+            self.d = torch.from_numpy(pack_batch(qp)[2]).to(self.dev)
+        else:
+            offB, offR, packB, packR = stage_offsets(qp)
+            self.offB, self.offR = offB, offR
+            self.layout = _Layout(packB, packR, offB.ctypes.data_as(C.POINTER(C.c_longlong)),
+                                  offR.ctypes.data_as(C.POINTER(C.c_longlong)), None, None)
+        if aliased:
+            pass
+        elif nprob is None:
             hB, hR, hd = pack_batch(qp)
             self.BAbt = torch.from_numpy(hB).to(self.dev)
             self.RSQrq = torch.from_numpy(hR).to(self.dev)

@@ -332,7 +332,7 @@ __device__ __forceinline__ void res_fetch(const RicIO& io, const SH& si, const B
                                           ResFrag<UPD>& f) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
     const int nu = si.nu, nx = si.nx, xo = si.xo, nux = nu + nx;
-    const double* R = io.RSQ + si.oR;
+    const double* R = stage_R(io, si);
     const int vc = tile_var(c, nu, nx, xo);
     const bool live = SH::fixed || k < io.N;
 #pragma unroll
@@ -346,7 +346,7 @@ __device__ __forceinline__ void res_fetch(const RicIO& io, const SH& si, const B
     f.q = ro.qsrc ? ldsel(ro.qsrc, k * V16 + vc, vc >= 0) : ldsel(R, lib4_idx(si.sdR, nux, vc), vc >= 0);
     f.uc = ldsel(ro.ux, k * V16 + vc, vc >= 0);
     f.duc = UPD ? ldsel(ro.dux, k * V16 + vc, vc >= 0) : 0.0;
-    const double* Bk = io.BAbt + si.oB;
+    const double* Bk = stage_B(io, si);
     const int nx1 = si.nx1, xo1 = si.xo1;
     const int s = c - xo1;
     const bool oks = live && s >= 0 && s < nx1;

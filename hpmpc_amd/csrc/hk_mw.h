@@ -381,7 +381,7 @@ __device__ __forceinline__ void fwd_fetch_chain(const RicIO& io, const SH& sh, i
     }
     const int kk = k < io.N ? k : io.N - 1;
     const bool live = k < io.N;
-    const double* Bk = io.BAbt + sh.oB;
+    const double* Bk = stage_B(io, sh);
     const int s = c - sh.xo1;
     const bool ok = live && s >= 0 && s < sh.nx1;
 #pragma unroll

@@ -28,7 +28,9 @@ struct StageInfo {
     int sdB, sdR;       // lib4 panel strides of BAbt_k (cnx_{k+1}) and RSQrq_k (cnux_k)
     int oB, oR, oD;     // offsets (doubles) of BAbt_k / RSQrq_k / d_k inside one problem's arrays
     int pnb;            // round_up(nb, 4)
-    int r0;             // stage belongs to the compiled inner class (constant shapes)
+    int r0;             // flags: bit 0 the stage belongs to the compiled inner class (constant shapes); bits 1 / 2
+                        // its BAbt / RSQrq block is shared by every problem of the batch (no problem stride:
+                        // the time-invariant / aliased layouts, hpmpc_mi355x_layout.BAbt_shared / RSQrq_shared)
     int oG;             // offset (doubles) of DCt_k inside one problem's general-constraint array
 };
 
@@ -447,6 +449,8 @@ struct RicIO {
     const signed char* tileslot;  // (N+1)*16: box slot owning tile t, or -1
     const double* BAbt;           // this problem's BAbt base (stage k block at st[k].oB)
     const double* RSQ;            // this problem's RSQrq base (stage k block at st[k].oR)
+    const double* BAbtS;          // the batch's BAbt / RSQrq base: a stage block shared by every problem (StageInfo
+    const double* RSQS;           // r0 bits 1 / 2) sits at BAbtS + oB / RSQS + oR
     double* F;                    // factor store (N+1)*FSTRIDE (private layout)
     const double* DCt;            // this problem's general-constraint base (stage k block at st[k].oG)
 };
@@ -486,10 +490,10 @@ __device__ __forceinline__ StageInfo load_stage(const StageInfo* st, int k) {
 // ------------------------------------------------------------------------------------------------
 struct DynSh {
     static constexpr bool fixed = false;
-    int nu, nx, xo, nx1, nu1, xo1, sdB, sdR, nb, pnb, oB, oR, ng, oG;
+    int nu, nx, xo, nx1, nu1, xo1, sdB, sdR, nb, pnb, oB, oR, ng, oG, fl;
     __device__ __forceinline__ explicit DynSh(const StageInfo& s)
         : nu(s.nu), nx(s.nx), xo(s.xo), nx1(s.nx1), nu1(s.nu1), xo1(s.xo1), sdB(s.sdB), sdR(s.sdR), nb(s.nb),
-          pnb(s.pnb), oB(s.oB), oR(s.oR), ng(s.ng), oG(s.oG) {}
+          pnb(s.pnb), oB(s.oB), oR(s.oR), ng(s.ng), oG(s.oG), fl(s.r0) {}
 };
 
 template <int NU, int NX>
@@ -497,9 +501,23 @@ struct FixSh {
     static constexpr bool fixed = true, enabled = true;
     static constexpr int nu = NU, nx = NX, xo = (NU + 3) / 4 * 4, nx1 = NX, nu1 = NU, xo1 = xo,
                          sdB = (NX + 1) / 2 * 2, sdR = (NU + NX + 1) / 2 * 2;
-    int nb, pnb, oB, oR;
-    __device__ __forceinline__ explicit FixSh(const StageInfo& s) : nb(s.nb), pnb(s.pnb), oB(s.oB), oR(s.oR) {}
+    int nb, pnb, oB, oR, fl;
+    __device__ __forceinline__ explicit FixSh(const StageInfo& s)
+        : nb(s.nb), pnb(s.pnb), oB(s.oB), oR(s.oR), fl(s.r0) {}
 };
+
+// The stage's data blocks: per problem, or shared by the batch (StageInfo r0 bits 1 / 2; wave-uniform selects).
+__device__ __forceinline__ int stage_flags(const StageInfo& s) { return s.r0; }
+template <class SH>
+__device__ __forceinline__ int stage_flags(const SH& s) { return s.fl; }
+template <class SH>
+__device__ __forceinline__ const double* stage_B(const RicIO& io, const SH& sh) {
+    return ((stage_flags(sh) & 2) ? io.BAbtS : io.BAbt) + sh.oB;
+}
+template <class SH>
+__device__ __forceinline__ const double* stage_R(const RicIO& io, const SH& sh) {
+    return ((stage_flags(sh) & 4) ? io.RSQS : io.RSQ) + sh.oR;
+}
 
 struct NoFix {  // generic kernels: no compile-time stage class
     static constexpr bool enabled = false;
@@ -513,7 +531,7 @@ __device__ __forceinline__ void with_shape(const StageInfo& s, F&& f) {
     if constexpr (FX::enabled) { f(FX(s)); return; }
 #endif
     if constexpr (FX::enabled) {
-        if (s.r0) {
+        if (s.r0 & 1) {
             f(FX(s));
             return;
         }
@@ -619,6 +637,10 @@ struct BoxCtx {
     // BX_P2 / BX_P2R: the factorisation skips its t^-1 store (queue API: the solves re-form 1/t from t, and
     // only the KKT re-solve and the general-constraint halves load it; wave-uniform)
     int no_tinv;
+    // the clamp certificate's per-stage threshold T (cert_threshold, data only): 0 computes it every factorisation,
+    // 1 computes and stores it in cert[k] (an IPM's first factorisation), 2 loads it (the later ones)
+    double* cert;
+    int cert_mode;
 };
 
 struct BoxLane {
@@ -914,6 +936,7 @@ struct BwdFrag {
     // BX_P2R residual inputs: ux_k (col c / rows g+4r), pi_k (rows), pi_{k-1} (col), BAbt_k' (col
     // c-xo1 over rows g+4r), x_{k+1} (col)
     double uc, pc, pim1;
+    double T;  // the stored certificate threshold (BoxCtx cert_mode 2)
 };
 
 template <bool AUG, int BM, class SH>
@@ -921,7 +944,7 @@ __device__ __forceinline__ void bwd_fetch(const RicIO& io, const SH& sh, int k, 
                                           int update_q, const double* qsrc, const BoxCtx& bc, BwdFrag& f) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
     const int nux = sh.nu + sh.nx;
-    const double* R = io.RSQ + sh.oR;
+    const double* R = stage_R(io, sh);
     const int vc = tile_var(c, sh.nu, sh.nx, sh.xo);
 #pragma unroll
     for (int r = 0; r < 4; r++) {
@@ -937,6 +960,7 @@ __device__ __forceinline__ void bwd_fetch(const RicIO& io, const SH& sh, int k, 
     }
     const BoxLane b = box_lane(io.tileslot, sh.pnb, k);
     f.bl = b;
+    f.T = bc.cert_mode == 2 ? gld(bc.cert, k) : 0.0;
 #pragma unroll
     for (int i = 0; i < 8; i++) f.bx[i] = 0.0;
     if (BM == BX_GIVEN) {
@@ -958,7 +982,7 @@ __device__ __forceinline__ void bwd_fetch(const RicIO& io, const SH& sh, int k, 
         ld_lu(bc.res_d, b, f.bx[6], f.bx[7]);
     }
     const bool live = SH::fixed || k < io.N;
-    const double* Bk = io.BAbt + sh.oB;
+    const double* Bk = stage_B(io, sh);
     const double* bp = update_b ? bsrc + k * V16 : Bk;
 #pragma unroll
     for (int r = 0; r < 4; r++) {
@@ -1082,7 +1106,15 @@ __device__ __forceinline__ void bwd_pre(const RicIO& io, const SH& sh, int k, co
     const int l = lane_id(), g = l >> 4, c = l & 15;
     double qxv;
     box_hessian<AUG, BM>(bc, cur, dq, qxv);
-    T = (SH::fixed || k > 0) ? cert_threshold(cur.Mi, sh) : 0.0;
+    T = 0.0;
+    if (SH::fixed || k > 0) {
+        if (bc.cert_mode == 2) {
+            T = cur.T;
+        } else {
+            T = cert_threshold(cur.Mi, sh);
+            if (bc.cert_mode == 1) gst(bc.cert, k, T, l == 0);
+        }
+    }
     M = cur.Mi;
     ml = cur.mlq + qxv;  // update_q row (or RSQrq row) + drowad qx
 #pragma unroll
@@ -1367,7 +1399,7 @@ __device__ __forceinline__ void fwd_fetch(const RicIO& io, const SH& sh, int k, 
     }
     const int kk = k < io.N ? k : io.N - 1;  // stage N has no BAbt block: loads clamped, values masked
     const bool live = k < io.N;
-    const double* Bk = io.BAbt + sh.oB;
+    const double* Bk = stage_B(io, sh);
     const int s = c - sh.xo1;
     const bool ok = live && s >= 0 && s < sh.nx1;
 #pragma unroll
@@ -1619,7 +1651,7 @@ __device__ __forceinline__ void trs_fetch(const RicIO& io, const SH& sh, int k, 
     }
     const int nux = sh.nu + sh.nx;
     const int vc = tile_var(c, sh.nu, sh.nx, sh.xo);
-    const double* R = io.RSQ + sh.oR;
+    const double* R = stage_R(io, sh);
     f.h0 = hq ? ldsel(hq + k * V16, vc, vc >= 0) : ldsel(R, lib4_idx(sh.sdR, nux, vc), vc >= 0);
     const BoxLane b = box_lane(io.tileslot, sh.pnb, k);
     f.bl = b;
@@ -1644,7 +1676,7 @@ __device__ __forceinline__ void trs_fetch(const RicIO& io, const SH& sh, int k, 
         fetch_pair(bc.res_d, b, f.bx[10], f.bx[11]);
     }
     const bool live = SH::fixed || k < io.N;
-    const double* Bk = io.BAbt + sh.oB;
+    const double* Bk = stage_B(io, sh);
     const double* bp = hb ? hb + k * V16 : Bk;
 #pragma unroll
     for (int r = 0; r < 4; r++) {

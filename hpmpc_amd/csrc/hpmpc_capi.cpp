@@ -147,15 +147,22 @@ bool plan_supported(int N, const int* nx, const int* nu, const int* nb, const in
     return true;
 }
 
-bool plan_upload_stages(hpmpc_mi355x_plan* P, const long long* offB, const long long* offR) {
+// Stage offsets (and the shared-block flags, StageInfo r0 bits 1 / 2: the block of stage k sits at the batch's
+// base + offset for every problem) into the device stage table; re-uploaded only when they change.
+bool plan_upload_stages(hpmpc_mi355x_plan* P, const long long* offB, const long long* offR,
+                        const unsigned char* shB = nullptr, const unsigned char* shR = nullptr) {
     const int N = P->N;
+    std::vector<int> fl(N + 1);
+    for (int k = 0; k <= N; k++)
+        fl[k] = (P->st[k].r0 & 1) | ((shB && k < N && shB[k]) ? 2 : 0) | ((shR && shR[k]) ? 4 : 0);
     bool same = !P->dev_offB.empty();
     for (int k = 0; same && k < N; k++) same = P->dev_offB[k] == offB[k];
-    for (int k = 0; same && k <= N; k++) same = P->dev_offR[k] == offR[k];
+    for (int k = 0; same && k <= N; k++) same = P->dev_offR[k] == offR[k] && P->st[k].r0 == fl[k];
     if (same) return true;
     for (int k = 0; k <= N; k++) {
         P->st[k].oB = k < N ? (int)offB[k] : 0;
         P->st[k].oR = (int)offR[k];
+        P->st[k].r0 = fl[k];
     }
     P->dev_offB.assign(offB, offB + N);
     P->dev_offR.assign(offR, offR + N + 1);
@@ -163,7 +170,7 @@ bool plan_upload_stages(hpmpc_mi355x_plan* P, const long long* offB, const long 
                   "plan stage upload");
 }
 
-long long ws_doubles(int N) { return (long long)(N + 1) * (FSTRIDE + 9 * V16 + 8 * V32) + 16; }
+long long ws_doubles(int N) { return (long long)(N + 1) * (FSTRIDE + 9 * V16 + 8 * V32 + 1) + 16; }
 
 }  // namespace
 
@@ -305,7 +312,7 @@ bool layout_apply(hpmpc_mi355x_plan* P, const hpmpc_mi355x_layout* lay, KArgs& a
         return false;
     }
     if (lay && lay->BAbt_off && lay->RSQrq_off) {
-        if (!plan_upload_stages(P, lay->BAbt_off, lay->RSQrq_off)) return false;
+        if (!plan_upload_stages(P, lay->BAbt_off, lay->RSQrq_off, lay->BAbt_shared, lay->RSQrq_shared)) return false;
     } else if (!plan_upload_stages(P, P->offB.data(), P->offR.data())) {
         return false;
     }

@@ -276,6 +276,16 @@ void outputs(Carve& C, int* nx, int* nb, int** hidxb, int* ng, double** lb, doub
     }
 }
 
+// work0's header (the first 64 bytes of the carve): [0] the horizon the IPM ran on (N2), [1] a tag, [2] N -- so that
+// the KKT re-solve can tell a work space the IPM wrapper wrote from one it never saw.
+constexpr double WORK0_TAG = 0x1.48504d5043e5fp+33;
+void mark_work0(char* base, int N2, int N) {
+    double* h = reinterpret_cast<double*>(base);
+    h[0] = N2;
+    h[1] = WORK0_TAG;
+    h[2] = N;
+}
+
 int ip_ocp(bool rowmajor, int* kk, int k_max, double mu0, double mu_tol, int N, int* nx, int* nu_N, int* nb,
            int** hidxb, int* ng, int N2, int warm_start, double** A, double** B, double** b, double** Q, double** S,
            double** R, double** q, double** r, double** lb, double** ub, double** Cm, double** D, double** lg,
@@ -300,7 +310,7 @@ int ip_ocp(bool rowmajor, int* kk, int k_max, double mu0, double mu_tol, int N, 
         for (int j = 0; j < nx[N]; j++) mu0 = fmax(mu0, q[N][j]);
     }
     const double alpha_min = 1e-8;
-    reinterpret_cast<double*>(base)[0] = C.N2;
+    mark_work0(base, C.N2, N);
     int status;
     if (C.N2 < N) {  // partial condensing (:388-545)
         const int N2c = C.N2;
@@ -369,7 +379,16 @@ void kkt_ocp(bool rowmajor, int N, int* nx, int* nu, int* nb, int** hidxb, int* 
     char* base = aligned(work0);
     Carve C;
     carve(C, base, N, nx, nu, nb, hidxb, ng, N);
-    if ((int)reinterpret_cast<double*>(base)[0] != N) {
+    const double* hd = reinterpret_cast<const double*>(base);
+    if (hd[1] != WORK0_TAG || hd[2] != (double)N) {
+        // e.g. test_problems/test_d_ip_hard.c:892 calls the re-solve on a work space no IPM wrapper has written (its
+        // IPM call at :849 is commented out): the reference then reads whatever the buffer holds, this library
+        // refuses instead of solving with an undefined factor
+        hk_set_error(HPMPC_MI355X_EUNSUPPORTED, "KKT re-solve: work0 holds no factor of this problem's IPM wrapper "
+                                                "call (call fortran_order_ / c_order_d_ip_ocp_hard_tv on it first)");
+        return;
+    }
+    if ((int)hd[0] != N) {
         hk_set_error(HPMPC_MI355X_EUNSUPPORTED, "KKT re-solve after a partially condensed IPM (the wrapper keeps "
                                                 "the full-space factor only when N2 == N)");
         return;
@@ -401,7 +420,7 @@ extern "C" int fortran_order_d_ip_ocp_hard_tv_single_newton_step(
     Carve C;
     carve(C, base, N, nx, nu_N, nb, hidxb, ng, N);
     pack_problem(C, nx, nb, hidxb, ng, false, A, B, b, Q, S, R, q, r, lb, ub, Cm, D, lg, ug, true);
-    reinterpret_cast<double*>(base)[0] = N;
+    mark_work0(base, N, N);
     const double alpha_min = 1e-8;
     const int status = d_ip2_res_mpc_hard_tv_single_newton_step(
         kk, k_max, mu0, mu_tol, alpha_min, warm_start, stat, N, nx, C.nu.data(), nb, hidxb, ng, C.BAbt.data(),

@@ -26,6 +26,7 @@ struct Ws {  // per-problem workspace carve (doubles), persistent between an IPM
     double *F, *dux, *dpi, *Pb, *Qx, *qx, *res_q, *res_b, *ux_bkp, *pi_bkp;
     double *dlam, *dt, *t_inv, *lamt, *res_d, *res_m, *t_bkp, *lam_bkp;
     double* state;  // IpmState (16 doubles) carried between the IPM pass kernels
+    double* cert;   // N+1: the clamp certificate's threshold per stage (the first factorisation of a solve)
 };
 
 // Per-problem IPM control state between the pass kernels of one batched solve.
@@ -55,6 +56,7 @@ __device__ __forceinline__ Ws carve(double* W, int N) {
     w.t_bkp = W + 6 * b;
     w.lam_bkp = W + 7 * b;
     w.state = W + 8 * b;
+    w.cert = w.state + 16;
     return w;
 }
 
@@ -102,6 +104,8 @@ __device__ __forceinline__ RicIO make_io(const KArgs& a, const LdsTabs& T, int p
     io.tileslot = T.tileslot;
     io.BAbt = a.BAbt + (long)p * a.sB;
     io.RSQ = a.RSQ + (long)p * a.sR;
+    io.BAbtS = a.BAbt;
+    io.RSQS = a.RSQ;
     io.F = F;
     io.DCt = a.DCt ? a.DCt + (long)p * a.sG : a.RSQ;  // never read when every ng = 0
     return io;
@@ -579,6 +583,9 @@ __device__ __forceinline__ void fact_body(const KArgs& a, const LdsTabs& T, IpmV
     Scratch& sm = *T.sm;
     const double* st = v.w.state;
     const bool sn = a.single_newton != 0;
+    // the certificate thresholds depend on the data only: formed by the solve's first factorisation, then loaded
+    v.bc.cert = v.w.cert;
+    v.bc.cert_mode = st[S_KK] == 0.0 ? 1 : 2;
     if (st[S_PHASE] == 1.0)
         ric_backward<true, BX_P1, FX>(v.io, &sm, 0, nullptr, 0, nullptr, v.bc, 1, v.w.Pb);
     else {  // the single-Newton variant factorises with the data's own b/q rows (d_ip2_res_hard.c:1700-1760)

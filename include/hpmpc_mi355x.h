@@ -268,12 +268,19 @@ hpmpc_mi355x_plan *hpmpc_mi355x_plan_create(int N, const int *nx, const int *nu,
                                             const int *const *idxb, const int *ng);
 void hpmpc_mi355x_plan_destroy(hpmpc_mi355x_plan *plan);
 
-/* Device-array geometry of a problem-major batch (all sizes in doubles). */
+/* Device-array geometry of a problem-major batch (all sizes in doubles).  Stage k of problem p reads its BAbt
+ * block at BAbt + p * BAbt_stride + BAbt_off[k], or -- when BAbt_shared[k] is nonzero -- at BAbt + BAbt_off[k] for
+ * every problem (likewise RSQrq).  Shared blocks give the time-invariant / aliased mode of the reference drivers
+ * (test_problems/test_d_ip_hard.c:652-662: every inner stage points at one block) across a whole batch: e.g. only
+ * stage 0 per problem (its b row carries A x0 + b) and one shared inner block for every other stage.  The offsets
+ * must fit in 32 bits. */
 typedef struct {
     long long BAbt_stride;   /* doubles between problems (0: shared by all problems) */
     long long RSQrq_stride;
     const long long *BAbt_off;   /* host array [N]   : lib4 block of stage k inside one problem */
     const long long *RSQrq_off;  /* host array [N+1] */
+    const unsigned char *BAbt_shared;   /* host array [N] or NULL (no shared block) */
+    const unsigned char *RSQrq_shared;  /* host array [N+1] or NULL */
 } hpmpc_mi355x_layout;
 
 /* Doubles of per-problem device workspace the batched calls need (factor + IPM iterate). */

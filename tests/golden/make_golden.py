@@ -667,6 +667,14 @@ def driver(out):
     uxn = np.array([len(r) for r in b["ux"]], dtype=np.int32)
     np.savez_compressed(path, ux=ux, ux_len=uxn, pi=np.asarray(b["pi"]))
     out.append(path)
+    # tools/relink/relink_driver.c (the low-level call sequence of test_d_ip_hard.c / test_d_ric_mpc.c) linked against
+    # the whole reference: every number it prints, at full precision
+    exe = os.path.join(ROOT, "oracle", "_ref", "relink", "relink_driver_ref")
+    text = subprocess.run([exe], check=True, capture_output=True, text=True, timeout=300).stdout
+    path = os.path.join(HERE, "drivers", "relink_driver.txt")
+    with open(path, "w") as f:
+        f.write(text)
+    out.append(path)
 
 
 def divergent(ref, out):

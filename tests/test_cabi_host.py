@@ -217,3 +217,32 @@ def test_noidxb_size_matches_idxb_size(hiplib):
         a = f(N, ip(nx), ip(nu), ip(nb), idxp, ip(ng), N2)
         b = g(N, ip(nx), ip(nu), ip(nb), ip(nbx), ip(nbu), ip(ng), N2)
         assert a == b > 0, (N2, a, b)
+
+
+@pytest.mark.parametrize("fill", ["zeros", "garbage"])
+def test_kkt_wrapper_refuses_unwritten_work0(fill):
+    """fortran_order_d_solve_kkt_new_rhs_ocp_hard_tv on a work space no IPM wrapper has written -- what
+    test_problems/test_d_ip_hard.c:892 does (its IPM call at :849 is commented out, work1 comes straight from malloc):
+    an error code (HPMPC_MI355X_EUNSUPPORTED via hpmpc_mi355x_last_error) and untouched outputs, decided on the host
+    before any device work."""
+    import sys
+
+    from hpmpc_amd.cabi import HpmpcAPI, load
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import iface_oracle
+
+    P = iface_oracle.random_iface_problem(8, [4] * 9, [2] * 8, [2] * 9, [1] * 9, seed=3)
+    api = HpmpcAPI(load(batch.LIBPATH))
+    wsz = api.fn("hpmpc_d_ip_ocp_hard_tv_work_space_size_bytes")(
+        C.c_int(8), *(np.ascontiguousarray(P[k], dtype=np.int32).ctypes.data_as(C.POINTER(C.c_int))
+                      for k in ("nx", "nu", "nb")),
+        (C.POINTER(C.c_int) * 9)(*[np.ascontiguousarray(i, dtype=np.int32).ctypes.data_as(C.POINTER(C.c_int))
+                                   for i in P["hidxb"]]),
+        np.ascontiguousarray(P["ng"], dtype=np.int32).ctypes.data_as(C.POINTER(C.c_int)), C.c_int(8))
+    work0 = np.zeros(wsz // 8 + 16)
+    if fill == "garbage":
+        work0[:] = np.random.default_rng(1).standard_normal(work0.size) * 1e3
+    r = api.kkt_ocp(P, work0)
+    assert api.lib.hpmpc_mi355x_last_error() == EUNSUPPORTED
+    assert all(not np.any(x) for x in r["x"]) and all(not np.any(u) for u in r["u"])

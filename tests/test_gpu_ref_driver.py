@@ -44,3 +44,46 @@ def test_unchanged_reference_driver_on_gpu(tmp_path):
     np.testing.assert_allclose(ux, z["ux"], rtol=0, atol=1.01e-5)
     np.testing.assert_allclose(np.asarray(b["pi"]), z["pi"], rtol=0, atol=1.01e-5)
     print(r.stdout.strip().splitlines()[-1])  # the driver's own timing line (sv / trf / trs through the GPU)
+
+
+RELINK = os.path.join(ROOT, "oracle", "_ref", "drivers", "relink_driver")
+# gates per printed quantity (tests/helpers.py): Riccati 1e-12; the residual IPM, its KKT re-solve and residuals
+# 1e-10; the alternate IPM (no residual correction, stopped at mu_tol 1e-8) and its re-solve TOL_KKT2
+GATES = {"sv": 1e-12, "trs": 1e-12, "ipm": 1e-10, "kkt": 1e-10, "res": 1e-10, "ipm2": 1e-8, "kkt2": 1e-8,
+         "res2": 1e-8}
+
+
+def _parse_relink(text):
+    vals, heads = {}, []
+    for line in text.splitlines():
+        w = line.split()
+        if not w:
+            continue
+        if w[0] in ("ipm", "ipm2") and w[1] == "status":
+            heads.append((w[0], int(w[2]), int(w[4])))
+        elif "." in w[0]:
+            vals[(w[0], int(w[1]))] = np.array([float(x) for x in w[2:]])
+    return heads, vals
+
+
+def test_relinked_ipm_driver_on_gpu():
+    """tools/relink/relink_driver.c -- the low-level call sequence of test_problems/test_d_ip_hard.c (IPM, KKT re-solve,
+    residuals, the alternate IPM and its re-solve) and test_d_ric_mpc.c (sv, trf, trs) through the reference's own
+    headers and auxiliary objects -- linked against the reference archive minus the replaced files plus
+    -lhpmpc_mi355x, run on the MI355X: every number it prints against the same driver linked against the whole
+    reference (tests/golden/drivers/relink_driver.txt): status and kk identical, values at the gates above."""
+    assert os.path.exists(RELINK), "relinked driver not built (tools/relink/Makefile drivers)"
+    r = subprocess.run([RELINK], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "hpmpc_mi355x" not in r.stderr, r.stderr[-2000:]
+    heads, vals = _parse_relink(r.stdout)
+    rheads, rvals = _parse_relink(open(os.path.join(ROOT, "tests", "golden", "drivers", "relink_driver.txt")).read())
+    assert heads == rheads and len(heads) == 2
+    assert vals.keys() == rvals.keys()
+    for key, ref in rvals.items():
+        tag = key[0].split(".")[0]
+        tol = 1e-9 if key[0] == "ipm.stat" else GATES[tag]
+        got = vals[key]
+        assert got.shape == ref.shape, key
+        e = float(np.max(np.abs(got - ref) / np.maximum(1.0, np.abs(ref)), initial=0.0))
+        assert e <= tol, (key, e)

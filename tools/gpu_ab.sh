@@ -22,14 +22,14 @@ for i in 1 2 3; do
       continue
     fi
     HPMPC_MI355X_LIB=$PWD/hpmpc_amd/lib/ab/lib$v.so timeout -k 10 300 python3 bench.py --no-cpu --no-pcond --no-isolated \
-      --no-queue-batch-slots --steps 20 > gpurun_out/ab/$v$i.log 2>&1 || { tail -20 gpurun_out/ab/$v$i.log; exit 1; }
+      --no-queue-batch-slots --no-aliased --steps 20 > gpurun_out/ab/$v$i.log 2>&1 || { tail -20 gpurun_out/ab/$v$i.log; exit 1; }
     python3 - "$v$i" <<'PY'
 import json, sys
 l = [x for x in open(f"gpurun_out/ab/{sys.argv[1]}.log") if x.startswith("{")][-1]
 d = json.loads(l)
 p = d["roofline"]["pass_ms_per_step"]
 print(sys.argv[1], round(d["value"]), {k[7:]: round(v, 3) for k, v in p.items()}, "ric", round(d["riccati"]["value"]),
-      "N50", round(d.get("riccati_batch_N50", {}).get("value", 0)))
+      "N50", round((d.get("riccati_batch_N50") or {}).get("value", 0)))
 PY
   done
 done
