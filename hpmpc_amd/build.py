@@ -56,17 +56,21 @@ def _deps(src, hdrs_all):
     return sorted(seen | {h for h in hdrs_all if os.path.basename(h) == "hpmpc_mi355x.h"})
 
 
-def build_hip(force: bool = False, verbose: bool = False) -> str:
+def build_hip(force: bool = False, verbose: bool = False, variant: str | None = None, extra=()) -> str:
     """Each source compiles to its own object under build/ (rebuilt when it or a header is newer), then one
-    link; a one-file change recompiles one translation unit."""
+    link; a one-file change recompiles one translation unit.  variant: an A/B build with `extra` compiler flags,
+    objects under build/obj_<variant>, library hpmpc_amd/lib/ab/lib<variant>.so (tools/gpu_ab.sh)."""
     os.makedirs(LIBDIR, exist_ok=True)
-    objdir = os.path.join(ROOT, "build", "obj")
+    objdir = os.path.join(ROOT, "build", "obj" if variant is None else f"obj_{variant}")
     os.makedirs(objdir, exist_ok=True)
     out = os.path.join(LIBDIR, "libhpmpc_mi355x.so")
+    if variant is not None:
+        os.makedirs(os.path.join(LIBDIR, "ab"), exist_ok=True)
+        out = os.path.join(LIBDIR, "ab", f"lib{variant}.so")
     hdrs_all = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, "include", "hpmpc_mi355x.h")]
     # -fvisibility=hidden: only include/hpmpc_mi355x.h's functions are exported (csrc/hpmpc_api.h)
     common = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall",
-              "-Wno-unused-function"] + KFLAGS
+              "-Wno-unused-function"] + KFLAGS + list(extra)
     objs, procs = [], []
     for src in SOURCES:
         obj = os.path.join(objdir, src + ".o")

@@ -669,7 +669,7 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
 // ------------------------------------------------------------------------------------------------
 __device__ HK_WIDE_BODY void wide_trs_body(const WideArgs& a, const WideProb& q) {
     extern __shared__ double sm[];
-    const int tid = threadIdx.x, lane = tid & 63;
+    const int tid = threadIdx.x;
     double* M = sm;
     double* W = sm + a.offW;
     double* X = sm + a.offX;  // w = Pb + v_{k+1,x} (backward) / pi scratch (forward)

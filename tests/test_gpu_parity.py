@@ -596,3 +596,34 @@ def test_aliased_batch_layout(oracle):
     torch.cuda.synchronize()
     for n in ("ux", "pi", "Pb"):
         assert torch.equal(getattr(f2, n), getattr(a2, n)), n
+
+
+@pytest.mark.parametrize("N", [300, 301])
+def test_solo_long_horizons(oracle, N):
+    """The latency path at the multi-wave kernel's horizon limit (MW_NMAX = 300: the update's reduction rows fill its
+    LDS buffer exactly) and one stage beyond it (N = 301: the single-wave solo kernel takes over).  Same kk / ret as the
+    batched solve, bitwise equal to it beyond the limit, and both at the IPM gate of the oracle."""
+    import torch
+
+    from hpmpc_amd.batch import BatchSolver
+
+    qp = mass_spring_qp(N, 8, 3, batch=2, time_variant=True, seed=N)
+    s = BatchSolver(qp, k_max=50)
+    s.ipm()
+    torch.cuda.synchronize()
+    ref = {n: getattr(s, n).clone() for n in ("ux", "pi", "lam", "t", "kk", "ret")}
+    for n in ("ux", "pi", "lam", "t"):
+        getattr(s, n).zero_()
+    s.ipm_solo()
+    torch.cuda.synchronize()
+    assert torch.equal(s.kk, ref["kk"]) and torch.equal(s.ret, ref["ret"])
+    if N > 300:
+        for n, v in ref.items():
+            assert torch.equal(getattr(s, n), v), n
+    for p in range(2):
+        one = qp.problem(p)
+        r = oracle.ipm(one.copy(), k_max=50)
+        got = dict(kk=int(s.kk[p]), ret=int(s.ret[p]), ux=[s.ux[p, k].cpu().numpy() for k in range(N + 1)],
+                   pi=[s.pi[p, k].cpu().numpy() for k in range(N)], lam=[s.lam[p, k].cpu().numpy() for k in range(N + 1)],
+                   t=[s.t[p, k].cpu().numpy() for k in range(N + 1)])
+        compare_ipm(one, got, r, allow_divergent=True)

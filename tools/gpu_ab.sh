@@ -1,7 +1,7 @@
 #!/bin/bash
-# A/B timing of two builds of the library on ONE box: hpmpc_amd/lib/ab/libA.so and libB.so (copies of the
-# in-tree build before / after a change), loaded through HPMPC_MI355X_LIB by alternating runs, so box-to-box
-# variance (+-5-10 % between boxes) does not decide the comparison.  The parity suite runs first, on the in-tree
+# A/B timing of two (or more: AB_VARIANTS="A B C") builds of the library on ONE box: hpmpc_amd/lib/ab/lib<v>.so
+# (copies of the in-tree build before / after a change), loaded through HPMPC_MI355X_LIB by alternating runs, so
+# box-to-box variance (+-5-10 % between boxes) does not decide the comparison.  The parity suite runs first, on the in-tree
 # build (AB_SKIP_TESTS=1 skips it).  Every GPU step has its own time limit; the script stops at the first failure.
 #   tools/gpu_ab.sh            headline queue runs (bench.py, no CPU / configs[4] legs)
 #   tools/gpu_ab.sh latency    lone-QP latency (tools/latency_probe.py)
@@ -14,7 +14,7 @@ if [ "${AB_SKIP_TESTS:-0}" != 1 ]; then
   tail -1 gpurun_out/tests.log
 fi
 for i in 1 2 3; do
-  for v in A B; do
+  for v in ${AB_VARIANTS:-A B}; do
     if [ "$mode" = latency ]; then
       HPMPC_MI355X_LIB=$PWD/hpmpc_amd/lib/ab/lib$v.so timeout -k 10 300 python3 tools/latency_probe.py \
         > gpurun_out/ab/lat_$v$i.log 2>&1 || { tail -20 gpurun_out/ab/lat_$v$i.log; exit 1; }

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round-4 evidence batch (one gpurun call): parity suite, quick bench line, HBM load-width probes, then same-box A/Bs of
+# hpmpc_amd/lib/ab/lib{A,B,C}.so -- A: hand-over without fences (HK_MW_FENCE=0), B: the in-tree build,
+# C: -ffp-contract=on -- on the lone-QP latency and on the headline queue.  Every GPU step has its own limit; the
+# script stops at the first failure.
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+bash tools/gpu_quickbench.sh || exit 1
+timeout -k 10 300 python3 tools/hbm_bw.py > gpurun_out/hbm_bw.json 2> gpurun_out/hbm_bw.err || { tail -5 gpurun_out/hbm_bw.err; exit 1; }
+cat gpurun_out/hbm_bw.json
+AB_SKIP_TESTS=1 AB_VARIANTS="A B C" bash tools/gpu_ab.sh latency || exit 1
+AB_SKIP_TESTS=1 AB_VARIANTS="B C" bash tools/gpu_ab.sh || exit 1
