@@ -92,16 +92,16 @@ def build_hip(force: bool = False, verbose: bool = False, variant: str | None = 
     return out
 
 
-def build_stamps(verbose: bool = False) -> str:
-    """Diagnostic variant with s_memtime stamps (tools/stamps.py); never loaded by the product."""
-    os.makedirs(LIBDIR, exist_ok=True)
-    out = os.path.join(LIBDIR, "libhpmpc_mi355x_stamps.so")
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-DHK_STAMPS",
-           "-Wno-unused-function"] + KFLAGS + [os.path.join(CSRC, s) for s in SOURCES] + ["-o", out]
-    if verbose:
-        print(" ".join(cmd), flush=True)
-    subprocess.run(cmd, check=True)
-    return out
+def build_stamps(verbose: bool = False, force: bool = False) -> str:
+    """Diagnostic variant with s_memtime stamps (tools/stamps.py) and the multi-wave kernel's lost-hand-over hook
+    (tests/test_gpu_parity.py test_multiwave_expired_wait_drains); never loaded by the product."""
+    out = build_hip(force=force, verbose=verbose, variant="stamps", extra=["-DHK_STAMPS"])
+    dst = os.path.join(LIBDIR, "libhpmpc_mi355x_stamps.so")
+    if not _newer(dst, [out]):
+        import shutil
+
+        shutil.copy2(out, dst)
+    return dst
 
 
 def build_calib(verbose: bool = False) -> str:
@@ -130,6 +130,7 @@ def build_oracle(force: bool = False) -> None:
 
 def build_all(force: bool = False, verbose: bool = False) -> None:
     build_hip(force=force, verbose=verbose)
+    build_stamps(verbose=verbose, force=force)
     build_calib(verbose=verbose)
     build_oracle(force=force)
 

@@ -60,6 +60,12 @@ struct MwShared {
 // could lose its address space): every access is a ds_ op, so a flag poll never waits on the global-memory counter.
 __shared__ MwShared hk_mw;
 
+#ifdef HK_STAMPS
+// Diagnostic build only: a helper that "forgets" one hand-over (HPMPC_MI355X_MW_FAULT=1 at launch, hk_launch), so
+// that tests/test_gpu_parity.py can check the expired-wait path: the waits expire, the launch drains, ret = -20.
+__device__ int g_mw_fault;
+#endif
+
 
 __device__ __forceinline__ int mw_flag(const int* f) { return __atomic_load_n(f, __ATOMIC_RELAXED); }
 
@@ -156,7 +162,7 @@ __device__ __forceinline__ double mw_get(int j, int i) { return hk_mw.ring[j % M
 //                  gain block (stage_chol_row) and the stage record -- a second recursion (p_{k+1} -> p_k) that
 //                  needs the tile wave's factor but never feeds it, so it runs one stage behind;
 //   waves 2, 3 (helpers, every other stage): fetch, residuals, box terms -> ring = [M (4) | ml | bop (4) | brow (4) |
-//                  dq | T] (dq, T: the box diagonal and the clamp-certificate threshold, cert_ok), read by both
+//                  dq | g] (dq, g: the box diagonal and the clamp-certificate bound, cert_ok), read by both
 //                  recursions (its slot is free once both have read it).
 // A stage that fails the clamp certificate is factorised as the reference does (stage_chol xfac): the tile wave
 // carries P_eff on and hands the x factor to the row wave, which adds its row half and p_eff = Lxx l_x.
@@ -193,10 +199,10 @@ __device__ __forceinline__ int ric_backward_mw(const RicIO& io, int tb, int w, i
             const int k = N - j;
             const StageInfo si = load_stage(io.st, k);
             d4 M;
-            double ml, dq, T;
+            double ml, dq, gc;
             with_shape<FX>(si, [&](const auto& sh) {
                 if constexpr (BM == BX_P2R) bwd_residual(io, sm, sh, k, bc, f, x1c, true);
-                bwd_pre<AUG, BM>(io, sh, k, f, bc, M, ml, dq, T);
+                bwd_pre<AUG, BM>(io, sh, k, f, bc, M, ml, dq, gc);
             });
             if (j >= MW_D) {  // the slot's previous occupant read by both recursions
                 mw_wait_at(&hk_mw.freed[j % MW_D], tb + j - MW_D + 1, MW_D + j % MW_D);
@@ -210,7 +216,10 @@ __device__ __forceinline__ int ric_backward_mw(const RicIO& io, int tb, int w, i
             }
             mw_put(j, 4, ml);
             mw_put(j, 13, dq);
-            mw_put(j, 14, T);
+            mw_put(j, 14, gc);
+#ifdef HK_STAMPS
+            if (g_mw_fault && j == 3) return;  // the lost hand-over (diagnostic build)
+#endif
             mw_post(j % MW_D, tb + j + 1);
         };
         BwdFrag fa, fb;
@@ -232,7 +241,7 @@ __device__ __forceinline__ int ric_backward_mw(const RicIO& io, int tb, int w, i
         // released once this step is done, by which time those reads have long completed
         d4 P = {0.0, 0.0, 0.0, 0.0};  // record tile of stage k+1 (its x block is P_{k+1})
         d4 Mn, bopn;
-        double dqn, Tn;
+        double dqn, gcn;
         auto take = [&](int j) __attribute__((always_inline)) {
             mw_wait(j % MW_D, tb + j + 1);
 #pragma unroll
@@ -241,7 +250,7 @@ __device__ __forceinline__ int ric_backward_mw(const RicIO& io, int tb, int w, i
                 bopn[r] = mw_get(j, 5 + r);
             }
             dqn = mw_get(j, 13);
-            Tn = mw_get(j, 14);
+            gcn = mw_get(j, 14);
         };
         take(0);
         StageInfo sn = load_stage(io.st, N);
@@ -263,7 +272,7 @@ __device__ __forceinline__ int ric_backward_mw(const RicIO& io, int tb, int w, i
             const StageInfo si = sn;
             d4 M = Mn;
             const d4 bop = bopn;
-            const double dq = dqn, T = Tn;
+            const double dq = dqn, gc = gcn;
             if (j < N) {
                 take(j + 1);
                 sn = load_stage(io.st, k - 1);
@@ -279,7 +288,7 @@ __device__ __forceinline__ int ric_backward_mw(const RicIO& io, int tb, int w, i
                 MW_SEG(1);
                 double mld = 0.0;
                 const bool full = !SHT::fixed && k == 0;
-                xfac = !full && !cert_ok(M, dq, T);
+                xfac = !full && !cert_ok(M, dq, gc);
                 stage_chol<false, false>(M, mld, invd, sh.nu, sh.nx, sh.xo, full, !SHT::fixed, nullptr, k, xfac, &xf);
                 MW_SEG(2);
             });

@@ -269,18 +269,16 @@ __device__ __forceinline__ void stage_chol_row(const d4& S, double invd, double&
 //   the reference's computed pivots are exact pivots of M + dM with |dM_ij| <= c n eps sqrt(M_ii M_jj) (Cholesky's
 //        componentwise backward error; the reference's own M differs from ours by rounding of the same order), so
 //        with 1e-11 >> 16 n eps as the allowance the certificate is  g (g / e_max - 1e-11) > 1e-15, i.e.
-//        e_max < T(g) = min(1e11 g, g^2 / (1e-15 + 1e-11 g))  (T < 0 when g <= 0: no certificate).
-// The threshold T depends on the data only; the e_max test is one compare per diagonal entry and a ballot.
+//        e_max (1e-11 g + 1e-15) < g^2 with g > 0.
+// g depends on the data only: the IPM forms it once per solve (cert_pass, from its init) and its factorisations load
+// it; the Riccati entry points form it per stage (cert_g).  The e_max test is one product and compare per diagonal
+// entry and a ballot.
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ double cert_T(double g) {
-    return g > 0.0 ? fmin(1e11 * g, g * g / fma(1e-11, g, 1e-15)) : -1.0;
-}
-
-// T of a stage from its data tile Mi (symmetric, zero outside the active rows / columns).  Row sums of |Mi| by MFMA
+// g of a stage from its data tile Mi (symmetric, zero outside the active rows / columns): row sums of |Mi| by MFMA
 // against a ones operand (the A fragment of K-chunk kc is register kc itself: lane (g,c) holds Mi[4kc+g][c] =
 // Mi[c][4kc+g]), the diagonal margin on the lane that holds it, then one wave minimum.
 template <class SH>
-__device__ __forceinline__ double cert_threshold(const d4& Mi, const SH& sh) {
+__device__ __forceinline__ double cert_g(const d4& Mi, const SH& sh) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
     const d4 z = {0.0, 0.0, 0.0, 0.0};
     d4 r0 = z, r1 = z;
@@ -298,17 +296,24 @@ __device__ __forceinline__ double cert_threshold(const d4& Mi, const SH& sh) {
     const bool act = tile_active(c, sh.nu, sh.nx, sh.xo);
 #pragma unroll
     for (int r = 0; r < 4; r++) m = (c == g + 4 * r && act) ? Mi[r] + fabs(Mi[r]) - rs[r] : m;
-    return cert_T(wave_min(m));
+    return wave_min(m);
 }
 
-// The certificate on the stage matrix M (after the tile update, before the factorisation): every diagonal entry
-// without its box term dq below T.  Wave-uniform (ballot of the failing lanes).
-__device__ __forceinline__ bool cert_ok(const d4& M, double dq, double T) {
+// The certificate on the stage matrix M (after the tile update, before the factorisation): g > 0 and, on every
+// diagonal entry, (M_ii - dq_i) (1e-11 g + 1e-15) < g^2 -- i.e. g (g / e_max - 1e-11) > 1e-15 without a division.
+// Wave-uniform (ballot of the failing lanes).
+#ifdef HK_STAMPS
+__device__ unsigned long long g_xfac_stat[4];  // P-form stages tested, failed at CERT_ALLOW, at 1e-12, at 1e-13
+#endif
+constexpr double CERT_ALLOW = 1e-11;  // the backward-error allowance (>> 16 n eps, n = 16)
+
+__device__ __forceinline__ bool cert_ok(const d4& M, double dq, double gc, double allow = CERT_ALLOW) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
+    const double cc = fma(allow, gc, 1e-15), g2 = gc * gc;
     // a negative given box term (BX_GIVEN) is not covered by the bound: no certificate
-    bool bad = dq < 0.0;
+    bool bad = !(gc > 0.0) || dq < 0.0;
 #pragma unroll
-    for (int r = 0; r < 4; r++) bad = bad || (c == g + 4 * r && !(M[r] - dq < T));
+    for (int r = 0; r < 4; r++) bad = bad || (c == g + 4 * r && !((M[r] - dq) * cc < g2));
     return __builtin_amdgcn_ballot_w64(bad) == 0;
 }
 
@@ -416,7 +421,13 @@ __device__ __forceinline__ void stage_chol(d4& M, double& ml, double& invd, int 
     HK_STAMP(20, kdbg);
     if (12 < nu || (full && 15 >= xo && 12 < hi)) chol_block<3, AUG>(M, ml, invd, nullptr, kdbg);
     HK_STAMP(22, kdbg);
+#ifdef HK_COUNT_NOFALLBACK  // static instruction counts of the certified path (tools/loop_icount.py): the test stays,
+    // the clamped factorisation is compiled out
+    asm volatile("" ::"s"(__builtin_amdgcn_readfirstlane((int)xfac)));
+    if (false) {
+#else
     if (!full && xfac) {
+#endif
         d4 L = M;
         double lx = ml, ivx = invd;
         xblocks_chol<AUG>(L, lx, ivx, nx, xo);
@@ -621,6 +632,9 @@ __device__ __forceinline__ void load_p_fixed(const double* Fk, d4& S, bool ok) {
 // stored) inside the backward pass instead of by a separate residual pass (backward only).
 enum BoxMode { BX_NONE = 0, BX_GIVEN = 1, BX_P1 = 2, BX_P2 = 3, BX_P2R = 4 };
 
+// the IPM's box modes read the certificate bound g that the solve's init formed (cert_pass); the others form it
+constexpr bool cert_loaded(int bm) { return bm == BX_P1 || bm == BX_P2 || bm == BX_P2R; }
+
 struct BoxCtx {
     const double* d;                                   // bounds [lb (pnb) | ub (pnb)], V32 per stage
     double *lam, *t;                                   // iterate (V32)
@@ -637,10 +651,9 @@ struct BoxCtx {
     // BX_P2 / BX_P2R: the factorisation skips its t^-1 store (queue API: the solves re-form 1/t from t, and
     // only the KKT re-solve and the general-constraint halves load it; wave-uniform)
     int no_tinv;
-    // the clamp certificate's per-stage threshold T (cert_threshold, data only): 0 computes it every factorisation,
-    // 1 computes and stores it in cert[k] (an IPM's first factorisation), 2 loads it (the later ones)
-    double* cert;
-    int cert_mode;
+    // the clamp certificate's data part g per stage (cert_pass): read by the IPM's factorisations (BX_P1 / BX_P2 /
+    // BX_P2R), which never form it themselves
+    const double* cert;
 };
 
 struct BoxLane {
@@ -936,8 +949,41 @@ struct BwdFrag {
     // BX_P2R residual inputs: ux_k (col c / rows g+4r), pi_k (rows), pi_{k-1} (col), BAbt_k' (col
     // c-xo1 over rows g+4r), x_{k+1} (col)
     double uc, pc, pim1;
-    double T;  // the stored certificate threshold (BoxCtx cert_mode 2)
+    double gc;  // the stored certificate bound g (IPM box modes)
 };
+
+// The stage's RSQ block as a full symmetric tile (its lower triangle mirrored), zero outside the active variables.
+template <class SH>
+__device__ __forceinline__ void load_rsq_tile(const double* R, const SH& sh, d4& Mi) {
+    const int l = lane_id(), g = l >> 4, c = l & 15;
+    const int vc = tile_var(c, sh.nu, sh.nx, sh.xo);
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int vi = tile_var(g + 4 * r, sh.nu, sh.nx, sh.xo);
+        const int hi = vi > vc ? vi : vc, lo = vi > vc ? vc : vi;
+        Mi[r] = ldsel(R, lib4_idx(sh.sdR, hi, lo), vi >= 0 && vc >= 0);
+    }
+}
+
+// The certificate's data part g_k of every stage into cert[0..N] (an IPM's init: its factorisations then load it):
+// stages in groups of four, the group's tile loads issued before its math.
+__device__ void cert_pass(const RicIO& io, double* cert) {
+    for (int k0 = 0; k0 <= io.N; k0 += 4) {
+        d4 Mi[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int k = k0 + j <= io.N ? k0 + j : io.N;
+            const DynSh sh(load_stage(io.st, k));
+            load_rsq_tile(stage_R(io, sh), sh, Mi[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int k = k0 + j <= io.N ? k0 + j : io.N;
+            const DynSh sh(load_stage(io.st, k));
+            gst(cert, k0 + j, cert_g(Mi[j], sh), lane_id() == 0 && k0 + j <= io.N);
+        }
+    }
+}
 
 template <bool AUG, int BM, class SH>
 __device__ __forceinline__ void bwd_fetch(const RicIO& io, const SH& sh, int k, int update_b, const double* bsrc,
@@ -946,12 +992,7 @@ __device__ __forceinline__ void bwd_fetch(const RicIO& io, const SH& sh, int k, 
     const int nux = sh.nu + sh.nx;
     const double* R = stage_R(io, sh);
     const int vc = tile_var(c, sh.nu, sh.nx, sh.xo);
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-        const int vi = tile_var(g + 4 * r, sh.nu, sh.nx, sh.xo);
-        const int hi = vi > vc ? vi : vc, lo = vi > vc ? vc : vi;
-        f.Mi[r] = ldsel(R, lib4_idx(sh.sdR, hi, lo), vi >= 0 && vc >= 0);
-    }
+    load_rsq_tile(R, sh, f.Mi);
     f.mlq = 0.0;
     if (AUG) {
         const double* qp = update_q ? qsrc + k * V16 : R;
@@ -960,7 +1001,7 @@ __device__ __forceinline__ void bwd_fetch(const RicIO& io, const SH& sh, int k, 
     }
     const BoxLane b = box_lane(io.tileslot, sh.pnb, k);
     f.bl = b;
-    f.T = bc.cert_mode == 2 ? gld(bc.cert, k) : 0.0;
+    f.gc = cert_loaded(BM) ? gld(bc.cert, k) : 0.0;
 #pragma unroll
     for (int i = 0; i < 8; i++) f.bx[i] = 0.0;
     if (BM == BX_GIVEN) {
@@ -1098,23 +1139,22 @@ __device__ __forceinline__ void bwd_residual(const RicIO& io, Scratch* sm, const
 // First half of a backward stage: the stage tile and augmented row with the box (and general) Hessian /
 // gradient terms added -- everything that does not depend on the recursion (the multi-wave solo kernel runs it
 // on a helper wave, hk_mw.h).
-// dq (col layout): the box term on the diagonal; T: the stage's clamp-certificate threshold (cert_threshold,
-// from the data tile; unused on a stage that is fully factorised).
+// dq (col layout): the box term on the diagonal; gc: the stage's clamp-certificate bound g (cert_g: loaded in the
+// IPM's box modes, formed from the data tile otherwise; unused on a stage that is fully factorised).
 template <bool AUG, int BM, class SH>
 __device__ __forceinline__ void bwd_pre(const RicIO& io, const SH& sh, int k, const BwdFrag& cur, const BoxCtx& bc,
-                                        d4& M, double& ml, double& dq, double& T) {
+                                        d4& M, double& ml, double& dq, double& gc) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
     double qxv;
     box_hessian<AUG, BM>(bc, cur, dq, qxv);
-    T = 0.0;
-    if (SH::fixed || k > 0) {
-        if (bc.cert_mode == 2) {
-            T = cur.T;
-        } else {
-            T = cert_threshold(cur.Mi, sh);
-            if (bc.cert_mode == 1) gst(bc.cert, k, T, l == 0);
-        }
-    }
+#ifdef HK_COUNT_NOCERT
+    gc = 0.0;
+#else
+    if constexpr (cert_loaded(BM))
+        gc = cur.gc;
+    else
+        gc = (SH::fixed || k > 0) ? cert_g(cur.Mi, sh) : 0.0;
+#endif
     M = cur.Mi;
     ml = cur.mlq + qxv;  // update_q row (or RSQrq row) + drowad qx
 #pragma unroll
@@ -1187,14 +1227,31 @@ __device__ __forceinline__ void bwd_row_update(const RicIO& io, Scratch* sm, con
 // Second half: M += BAbt P BAbt', the row update and the stage factorisation (the recursion's chain).
 template <bool AUG, class SH>
 __device__ __forceinline__ void bwd_core(const RicIO& io, Scratch* sm, const SH& sh, int k, const d4& bop,
-                                         const d4& brow, d4 M, double ml, double dq, double T, int compute_Pb,
+                                         const d4& brow, d4 M, double ml, double dq, double gc, int compute_Pb,
                                          double* Pb, d4& S, double& ml_prev, double& invd_prev, double& kg_prev) {
     const bool live = SH::fixed || k < io.N;
     bwd_tile_update(sh, live, bop, S, M);
     // stage 0 of a generic problem keeps the full factor; every other stage is factorised in P form, with its x
     // block factorised as well where the clamp certificate fails (stage_chol)
     const bool full = !SH::fixed && k == 0;
-    const bool xfac = !full && !cert_ok(M, dq, T);
+#ifdef HK_COUNT_NOCERT  // static counts without the clamp certificate (tools/loop_icount.py)
+    const bool xfac = false;
+    (void)dq;
+    (void)gc;
+#else
+    const bool xfac = !full && !cert_ok(M, dq, gc);
+#endif
+#ifdef HK_STAMPS  // diagnostic build: how often the certificate fails, at this allowance and at 10x / 100x smaller ones
+    if (!full) {
+        const bool f12 = !cert_ok(M, dq, gc, 1e-12), f13 = !cert_ok(M, dq, gc, 1e-13);
+        if (lane_id() == 0) {
+            atomicAdd(&g_xfac_stat[0], 1ull);
+            if (xfac) atomicAdd(&g_xfac_stat[1], 1ull);
+            if (f12) atomicAdd(&g_xfac_stat[2], 1ull);
+            if (f13) atomicAdd(&g_xfac_stat[3], 1ull);
+        }
+    }
+#endif
     if (AUG) bwd_row_update(io, sm, sh, k, live, bop, brow, S, ml_prev, compute_Pb, Pb, ml);
     HK_STAMP(2, k);
     double invd, kg = 0.0;
@@ -1216,9 +1273,9 @@ __device__ __forceinline__ void bwd_step(const RicIO& io, Scratch* sm, const SH&
                                          const BoxCtx& bc, int compute_Pb, double* Pb, d4& S, double& ml_prev,
                                          double& invd_prev, double& kg_prev) {
     d4 M;
-    double ml, dq, T;
-    bwd_pre<AUG, BM>(io, sh, k, cur, bc, M, ml, dq, T);
-    bwd_core<AUG>(io, sm, sh, k, cur.bop, cur.brow, M, ml, dq, T, compute_Pb, Pb, S, ml_prev, invd_prev, kg_prev);
+    double ml, dq, gc;
+    bwd_pre<AUG, BM>(io, sh, k, cur, bc, M, ml, dq, gc);
+    bwd_core<AUG>(io, sm, sh, k, cur.bop, cur.brow, M, ml, dq, gc, compute_Pb, Pb, S, ml_prev, invd_prev, kg_prev);
 }
 
 // Backward Riccati recursion (sv when AUG, trf otherwise), d_back_ric_rec.c:186-335 / :447-558.

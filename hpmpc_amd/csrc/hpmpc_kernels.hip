@@ -323,6 +323,7 @@ __device__ __forceinline__ BoxCtx box_ctx(const Ws& w, const double* dv, double*
     bc.qxs = w.qx;
     bc.Qx = w.Qx;
     bc.qx = w.qx;
+    bc.cert = w.cert;
     bc.res_q = w.res_q;
     bc.res_b = w.res_b;
     return bc;
@@ -521,6 +522,8 @@ __device__ bool ipm_start(const KArgs& a, const LdsTabs& T, IpmView& v) {
     // single Newton step (d_ip2_res_hard.c:1348-1919): the caller's ux/pi/lam/t already hold the start
     // iterate (d_init_var_mpc_hard_tv_single_newton is a copy, done by the host), no phase 1.
     const bool sn = a.single_newton != 0;
+    // the clamp certificate's data part of every stage, once per solve (its factorisations load it)
+    cert_pass(v.io, v.w.cert);
     if (!sn) {
         init_var<CI>(v.io, v.dv, v.ux, v.pi, v.w.dpi, v.lam, v.t, a.mu0, a.warm_start);
         if (a.ngt) {
@@ -583,9 +586,6 @@ __device__ __forceinline__ void fact_body(const KArgs& a, const LdsTabs& T, IpmV
     Scratch& sm = *T.sm;
     const double* st = v.w.state;
     const bool sn = a.single_newton != 0;
-    // the certificate thresholds depend on the data only: formed by the solve's first factorisation, then loaded
-    v.bc.cert = v.w.cert;
-    v.bc.cert_mode = st[S_KK] == 0.0 ? 1 : 2;
     if (st[S_PHASE] == 1.0)
         ric_backward<true, BX_P1, FX>(v.io, &sm, 0, nullptr, 0, nullptr, v.bc, 1, v.w.Pb);
     else {  // the single-Newton variant factorises with the data's own b/q rows (d_ip2_res_hard.c:1700-1760)
@@ -1194,6 +1194,18 @@ extern "C" int hk_fixcls(int nu, int nx) {
     return 0;
 }
 
+#ifdef HK_STAMPS
+// Diagnostic build only: the clamp-certificate counters of the tile kernels (g_xfac_stat), read and optionally reset.
+extern "C" __attribute__((visibility("default"))) int hpmpc_mi355x_diag_xfac(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_xfac_stat), 4 * sizeof(unsigned long long)) != hipSuccess) return -11;
+    if (reset) {
+        const unsigned long long z[4] = {0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_xfac_stat), z, sizeof(z)) != hipSuccess) return -11;
+    }
+    return 0;
+}
+#endif
+
 extern "C" int hk_launch(int which, const KArgs* a, int count, hipStream_t stream) {
     if (count <= 0) return 0;
 #ifdef HK_STAMPS
@@ -1202,6 +1214,11 @@ extern "C" int hk_launch(int which, const KArgs* a, int count, hipStream_t strea
         int st = 50;
         (void)hipMemcpyToSymbol(HIP_SYMBOL(g_dbg), &p, sizeof(p));
         (void)hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_stage), &st, sizeof(st));
+    }
+    {
+        const char* f = getenv("HPMPC_MI355X_MW_FAULT");
+        const int fault = (f && f[0] == '1') ? 1 : 0;
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_mw_fault), &fault, sizeof(fault));
     }
 #endif
     switch (a->fixcls) {

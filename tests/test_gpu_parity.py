@@ -627,3 +627,36 @@ def test_solo_long_horizons(oracle, N):
                    pi=[s.pi[p, k].cpu().numpy() for k in range(N)], lam=[s.lam[p, k].cpu().numpy() for k in range(N + 1)],
                    t=[s.t[p, k].cpu().numpy() for k in range(N + 1)])
         compare_ipm(one, got, r, allow_divergent=True)
+
+
+def test_multiwave_expired_wait_drains():
+    """The multi-wave kernel's expired-wait path (hk_mw.h mw_wait_at): in the diagnostic build
+    (libhpmpc_mi355x_stamps.so, -DHK_STAMPS) with HPMPC_MI355X_MW_FAULT=1 a helper drops one hand-over; the waits
+    expire after ~2^22 polls, every later wait falls through, the launch drains and the problem reports
+    ret = -20 (HPMPC_MI355X_EMW), and the drop-in entry point returns -20 with hpmpc_mi355x_last_error() set and its
+    outputs untouched.  Run in a child process (the library path is chosen at import)."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(root, "hpmpc_amd", "lib", "libhpmpc_mi355x_stamps.so")
+    assert os.path.exists(lib), "diagnostic build missing (hpmpc_amd/build.py build_stamps, run by build())"
+    code = r"""
+import numpy as np, torch
+from hpmpc_amd.batch import BatchSolver, LIBPATH
+from hpmpc_amd.cabi import HpmpcAPI, load
+from hpmpc_amd.ocp import mass_spring_qp
+qp = mass_spring_qp(30, 8, 3, batch=2, time_variant=True, seed=3)
+s = BatchSolver(qp, k_max=50)
+s.ipm_solo()
+torch.cuda.synchronize()
+assert s.ret.cpu().tolist() == [-20, -20], s.ret
+api = HpmpcAPI(load(LIBPATH))
+r = api.ipm(qp.problem(0), k_max=50)
+assert r["ret"] == -20 and api.lib.hpmpc_mi355x_last_error() == -20, r["ret"]
+assert all(not np.any(u) for u in r["ux"])
+print("drained")
+"""
+    env = dict(os.environ, HPMPC_MI355X_LIB=lib, HPMPC_MI355X_MW_FAULT="1", PYTHONPATH=root)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=180, env=env, cwd=root)
+    assert r.returncode == 0 and "drained" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]

@@ -9,5 +9,7 @@ export TMPDIR=/tmp
 bash tools/gpu_quickbench.sh || exit 1
 timeout -k 10 300 python3 tools/hbm_bw.py > gpurun_out/hbm_bw.json 2> gpurun_out/hbm_bw.err || { tail -5 gpurun_out/hbm_bw.err; exit 1; }
 cat gpurun_out/hbm_bw.json
+HPMPC_MI355X_LIB=$PWD/hpmpc_amd/lib/libhpmpc_mi355x_stamps.so timeout -k 10 300 python3 tools/xfac_rate.py > gpurun_out/xfac_rate.json 2> gpurun_out/xfac_rate.err || { tail -5 gpurun_out/xfac_rate.err; exit 1; }
+cat gpurun_out/xfac_rate.json
 AB_SKIP_TESTS=1 AB_VARIANTS="A B C" bash tools/gpu_ab.sh latency || exit 1
 AB_SKIP_TESTS=1 AB_VARIANTS="B C" bash tools/gpu_ab.sh || exit 1

@@ -13,8 +13,9 @@ def compile_asm(out="/tmp/hk_kernels.s"):
     sys.path.insert(0, ROOT)
     from hpmpc_amd.build import ARCH, HIPCC, KFLAGS
     src = os.path.join(ROOT, "hpmpc_amd", "csrc", "hpmpc_kernels.hip")
+    extra = os.environ.get("HK_COUNT_FLAGS", "").split()  # e.g. -DHK_COUNT_FIXED -DHK_COUNT_NOFALLBACK
     subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "--cuda-device-only", "-S"] + KFLAGS +
-                   [src, "-o", out], check=True, stderr=subprocess.DEVNULL)
+                   extra + [src, "-o", out], check=True, stderr=subprocess.DEVNULL)
     return out
 
 
