@@ -483,16 +483,16 @@ __device__ bool residual_pass(const RicIO& io, const BoxCtx& bc, const ResIO& ro
     int nbt = 0;
     ResFrag<UPD> cur, nxt;
     {
-        const StageInfo s0 = load_stage(io.st, 0);
+        const StageRef s0{io.st, 0};
         with_shape<FX>(s0, [&](const auto& sh) { res_fetch<UPD>(io, sh, bc, ro, 0, cur); });
     }
     for (int k = 0; k <= io.N; k++) {
         const int kn = k < io.N ? k + 1 : io.N;
-        const StageInfo sn = load_stage(io.st, kn);
+        const StageRef sn{io.st, kn};
         with_shape<FX>(sn, [&](const auto& sh) { res_fetch<UPD>(io, sh, bc, ro, kn, nxt); });
         asm volatile("" ::: "memory");
-        const StageInfo si = load_stage(io.st, k);
-        nbt += si.nb + si.ng;
+        const StageRef si{io.st, k};
+        nbt += srd(si, &StageInfo::nb) + srd(si, &StageInfo::ng);
         with_shape<FX>(si, [&](const auto& sh) { res_step<UPD>(io, sh, k, cur, bc, ro, pim1, ms); });
         cur = nxt;
     }

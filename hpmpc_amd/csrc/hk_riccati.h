@@ -274,12 +274,42 @@ __device__ __forceinline__ void stage_chol_row(const d4& S, double invd, double&
 // it; the Riccati entry points form it per stage (cert_g).  The e_max test is one product and compare per diagonal
 // entry and a ballot.
 // ------------------------------------------------------------------------------------------------
+// The tile's diagonal entry held by this lane: lane (g,c) holds element (g+4r, c) of register r, so it holds the
+// diagonal entry (c, c) iff c % 4 == g, in register c / 4 (callers mask the other lanes with diag_lane()).
+__device__ __forceinline__ double diag_sel(const d4& v) {
+    const int c = lane_id() & 15;
+    const bool b0 = (c & 4) != 0, b1 = (c & 8) != 0;
+    const double lo = b0 ? v[1] : v[0], hi = b0 ? v[3] : v[2];
+    return b1 ? hi : lo;
+}
+__device__ __forceinline__ bool diag_lane() {
+    const int l = lane_id();
+    return (l & 3) == (l >> 4);
+}
+
+// Wave minimum of a double to a conservative f32 bound (<= the exact minimum): one f32 DPP min per row step and two
+// row-group swaps instead of the f64 butterfly; the certificate needs a bound, not the exact value.
+__device__ __forceinline__ double wave_min_lb(double x) {
+    float f = (float)x;  // round to nearest, then step down one ulp-ish so that f <= x
+    f = f - fabsf(f) * 0x1p-22f - 0x1p-126f;
+    f = fminf(f, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, f), 0x128, 0xf, 0xf, true)));
+    f = fminf(f, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, f), 0x124, 0xf, 0xf, true)));
+    f = fminf(f, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, f), 0x122, 0xf, 0xf, true)));
+    f = fminf(f, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, f), 0x121, 0xf, 0xf, true)));
+    int v = __builtin_bit_cast(int, f);
+    const auto a = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    f = fminf(__builtin_bit_cast(float, (int)a[0]), __builtin_bit_cast(float, (int)a[1]));
+    v = __builtin_bit_cast(int, f);
+    const auto b = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return (double)fminf(__builtin_bit_cast(float, (int)b[0]), __builtin_bit_cast(float, (int)b[1]));
+}
+
 // g of a stage from its data tile Mi (symmetric, zero outside the active rows / columns): row sums of |Mi| by MFMA
 // against a ones operand (the A fragment of K-chunk kc is register kc itself: lane (g,c) holds Mi[4kc+g][c] =
-// Mi[c][4kc+g]), the diagonal margin on the lane that holds it, then one wave minimum.
+// Mi[c][4kc+g]), the diagonal margin on the lane that holds it, then a wave minimum (as a conservative f32 bound).
 template <class SH>
 __device__ __forceinline__ double cert_g(const d4& Mi, const SH& sh) {
-    const int l = lane_id(), g = l >> 4, c = l & 15;
+    const int c = lane_id() & 15;
     const d4 z = {0.0, 0.0, 0.0, 0.0};
     d4 r0 = z, r1 = z;
 #pragma unroll
@@ -291,29 +321,23 @@ __device__ __forceinline__ double cert_g(const d4& Mi, const SH& sh) {
         else
             r0 = mfma(fabs(Mi[kc]), 1.0, r0);
     }
-    const d4 rs = r0 + r1;
-    double m = 1e300;
-    const bool act = tile_active(c, sh.nu, sh.nx, sh.xo);
-#pragma unroll
-    for (int r = 0; r < 4; r++) m = (c == g + 4 * r && act) ? Mi[r] + fabs(Mi[r]) - rs[r] : m;
-    return wave_min(m);
+    const double d = diag_sel(Mi), rs = diag_sel(r0 + r1);
+    const double m = (diag_lane() && tile_active(c, sh.nu, sh.nx, sh.xo)) ? d + fabs(d) - rs : 1e300;
+    return wave_min_lb(m);
 }
 
-// The certificate on the stage matrix M (after the tile update, before the factorisation): g > 0 and, on every
-// diagonal entry, (M_ii - dq_i) (1e-11 g + 1e-15) < g^2 -- i.e. g (g / e_max - 1e-11) > 1e-15 without a division.
-// Wave-uniform (ballot of the failing lanes).
 #ifdef HK_STAMPS
 __device__ unsigned long long g_xfac_stat[4];  // P-form stages tested, failed at CERT_ALLOW, at 1e-12, at 1e-13
 #endif
 constexpr double CERT_ALLOW = 1e-11;  // the backward-error allowance (>> 16 n eps, n = 16)
 
+// The certificate on the stage matrix M (after the tile update, before the factorisation): g > 0 and, on every
+// diagonal entry, (M_ii - dq_i) (1e-11 g + 1e-15) < g^2 -- i.e. g (g / e_max - 1e-11) > 1e-15 without a division.
+// Wave-uniform (ballot of the failing lanes).
 __device__ __forceinline__ bool cert_ok(const d4& M, double dq, double gc, double allow = CERT_ALLOW) {
-    const int l = lane_id(), g = l >> 4, c = l & 15;
     const double cc = fma(allow, gc, 1e-15), g2 = gc * gc;
     // a negative given box term (BX_GIVEN) is not covered by the bound: no certificate
-    bool bad = !(gc > 0.0) || dq < 0.0;
-#pragma unroll
-    for (int r = 0; r < 4; r++) bad = bad || (c == g + 4 * r && !((M[r] - dq) * cc < g2));
+    const bool bad = !(gc > 0.0) || dq < 0.0 || (diag_lane() && !((diag_sel(M) - dq) * cc < g2));
     return __builtin_amdgcn_ballot_w64(bad) == 0;
 }
 
@@ -490,6 +514,18 @@ __device__ __forceinline__ StageInfo load_stage(const StageInfo* st, int k) {
     return u;
 }
 
+// A stage of the LDS table by reference: the shape objects below read (readfirstlane) only the fields they use, where
+// they are built, so a stage loop does not hold a whole StageInfo in SGPRs across its body (the compiled-class path
+// needs five fields; the full record would add some thirty live SGPRs per loop, and the stage kernels run at the
+// SGPR limit, spilling to VGPR lanes).
+struct StageRef {
+    const StageInfo* p;
+    int k;
+};
+__device__ __forceinline__ int srd(const StageRef& s, int StageInfo::*m) {
+    return __builtin_amdgcn_readfirstlane(s.p[s.k].*m);
+}
+
 // ------------------------------------------------------------------------------------------------
 // Stage-shape policies.  Every per-stage routine is written once against a shape object `sh`:
 //   DynSh          -- all sizes from the stage table (any problem the plan accepts);
@@ -505,6 +541,12 @@ struct DynSh {
     __device__ __forceinline__ explicit DynSh(const StageInfo& s)
         : nu(s.nu), nx(s.nx), xo(s.xo), nx1(s.nx1), nu1(s.nu1), xo1(s.xo1), sdB(s.sdB), sdR(s.sdR), nb(s.nb),
           pnb(s.pnb), oB(s.oB), oR(s.oR), ng(s.ng), oG(s.oG), fl(s.r0) {}
+    __device__ __forceinline__ explicit DynSh(const StageRef& s)
+        : nu(srd(s, &StageInfo::nu)), nx(srd(s, &StageInfo::nx)), xo(srd(s, &StageInfo::xo)),
+          nx1(srd(s, &StageInfo::nx1)), nu1(srd(s, &StageInfo::nu1)), xo1(srd(s, &StageInfo::xo1)),
+          sdB(srd(s, &StageInfo::sdB)), sdR(srd(s, &StageInfo::sdR)), nb(srd(s, &StageInfo::nb)),
+          pnb(srd(s, &StageInfo::pnb)), oB(srd(s, &StageInfo::oB)), oR(srd(s, &StageInfo::oR)),
+          ng(srd(s, &StageInfo::ng)), oG(srd(s, &StageInfo::oG)), fl(srd(s, &StageInfo::r0)) {}
 };
 
 template <int NU, int NX>
@@ -515,6 +557,9 @@ struct FixSh {
     int nb, pnb, oB, oR, fl;
     __device__ __forceinline__ explicit FixSh(const StageInfo& s)
         : nb(s.nb), pnb(s.pnb), oB(s.oB), oR(s.oR), fl(s.r0) {}
+    __device__ __forceinline__ explicit FixSh(const StageRef& s)
+        : nb(srd(s, &StageInfo::nb)), pnb(srd(s, &StageInfo::pnb)), oB(srd(s, &StageInfo::oB)),
+          oR(srd(s, &StageInfo::oR)), fl(srd(s, &StageInfo::r0)) {}
 };
 
 // The stage's data blocks: per problem, or shared by the batch (StageInfo r0 bits 1 / 2; wave-uniform selects).
@@ -533,6 +578,7 @@ __device__ __forceinline__ const double* stage_R(const RicIO& io, const SH& sh) 
 struct NoFix {  // generic kernels: no compile-time stage class
     static constexpr bool enabled = false;
     __device__ __forceinline__ explicit NoFix(const StageInfo&) {}
+    __device__ __forceinline__ explicit NoFix(const StageRef&) {}
 };
 
 // Run f(sh) with the stage's shape object: the constant one when the stage belongs to FX's class.
@@ -543,6 +589,19 @@ __device__ __forceinline__ void with_shape(const StageInfo& s, F&& f) {
 #endif
     if constexpr (FX::enabled) {
         if (s.r0 & 1) {
+            f(FX(s));
+            return;
+        }
+    }
+    f(DynSh(s));
+}
+template <class FX, class F>
+__device__ __forceinline__ void with_shape(const StageRef& s, F&& f) {
+#ifdef HK_COUNT_FIXED
+    if constexpr (FX::enabled) { f(FX(s)); return; }
+#endif
+    if constexpr (FX::enabled) {
+        if (srd(s, &StageInfo::r0) & 1) {
             f(FX(s));
             return;
         }
@@ -1001,7 +1060,7 @@ __device__ __forceinline__ void bwd_fetch(const RicIO& io, const SH& sh, int k, 
     }
     const BoxLane b = box_lane(io.tileslot, sh.pnb, k);
     f.bl = b;
-    f.gc = cert_loaded(BM) ? gld(bc.cert, k) : 0.0;
+    f.gc = cert_loaded(BM) ? bc.cert[k] : 0.0;  // LDS (fact_body) or the workspace (the multi-wave kernel)
 #pragma unroll
     for (int i = 0; i < 8; i++) f.bx[i] = 0.0;
     if (BM == BX_GIVEN) {
@@ -1288,7 +1347,7 @@ __device__ void ric_backward(const RicIO& io, Scratch* sm, int update_b, const d
                              const double* qsrc, const BoxCtx& bc, int compute_Pb, double* Pb) {
     d4 S = {0.0, 0.0, 0.0, 0.0};
     double ml_prev = 0.0, invd_prev = 0.0, kg_prev = 0.0;
-    StageInfo si = load_stage(io.st, io.N);
+    StageRef si{io.st, io.N};
     BwdFrag cur;
     with_shape<FX>(si, [&](const auto& sh) {
         bwd_fetch<AUG, BM>(io, sh, io.N, update_b, bsrc, update_q, qsrc, bc, cur);
@@ -1300,7 +1359,7 @@ __device__ void ric_backward(const RicIO& io, Scratch* sm, int update_b, const d
     auto stage = [&](int k, const BwdFrag& cur, BwdFrag& nxt) __attribute__((always_inline)) {
         HK_STAMP(0, k);
         const int kn = k > 0 ? k - 1 : 0;  // unconditional prefetch (stage 0 re-read on the last pass)
-        const StageInfo sn = load_stage(io.st, kn);
+        const StageRef sn{io.st, kn};
         HK_STAMP(5, k);
         with_shape<FX>(sn, [&](const auto& sh) { bwd_fetch<AUG, BM>(io, sh, kn, update_b, bsrc, update_q, qsrc, bc, nxt); });
         HK_STAMP(6, k);
@@ -1503,8 +1562,8 @@ template <int MODE, int FM, class FX, bool PRED>
 __device__ __forceinline__ void fwd_fetch_k(const RicIO& io, int k, const double* bsrc, int use_bsrc,
                                             const double* ux, int compute_pi, const BoxCtx& bc, FwdFrag& f) {
     const int kk = k < io.N ? k : io.N - 1;
-    const StageInfo sk = load_stage(io.st, kk);
-    const int pnbk = k < io.N ? sk.pnb : load_stage(io.st, k).pnb;
+    const StageRef sk{io.st, kk};
+    const int pnbk = srd(StageRef{io.st, k}, &StageInfo::pnb);
     with_shape<FX>(sk, [&](const auto& sh) {
         fwd_fetch<MODE, FM, PRED>(io, sh, k, pnbk, bsrc, use_bsrc, ux, compute_pi, bc, f);
     });
@@ -1637,14 +1696,14 @@ __device__ void ric_forward(const RicIO& io, Scratch* sm, const double* bsrc, in
     auto stage = [&](int k, const FwdFrag& fa, const FwdFrag& fb, FwdFrag& fc) __attribute__((always_inline)) {
         HK_STAMP(8, k);
         fwd_fetch_k<MODE, FM, FX, PRED>(io, k + 2 <= io.N ? k + 2 : io.N, bsrc, use_bsrc, ux, compute_pi, bc, fc);
-        const StageInfo si = load_stage(io.st, k);
+        const StageRef si{io.st, k};
         with_shape<FX>(si, [&](const auto& sh) {
             fwd_step<MODE, FM, PRED>(io, sm, sh, k, fa, fb, xcol, ux, compute_pi, pi, bc, al);
         });
         HK_STAMP(12, k);
     };
-    const StageInfo sN = load_stage(io.st, io.N);
     auto finish = [&](const FwdFrag& fN) __attribute__((always_inline)) {  // stage N: nu = 0, every tile a state
+        const DynSh sN(StageRef{io.st, io.N});
         const int v = tile_var(c, sN.nu, sN.nx, sN.xo);
         if (!PRED) gst(ux, io.N * V16 + v, xcol, g == 0 && v >= 0);
         box_alpha<FM, PRED>(bc, fN, xcol, al);
@@ -1658,7 +1717,10 @@ __device__ void ric_forward(const RicIO& io, Scratch* sm, const double* bsrc, in
         stage(k, f2, f0, f1);
         ++k;
     }
-    if (FM != BX_NONE && sN.ng > 0) gen_alpha<FM>(io, DynSh(sN), io.N, bc, xcol, al);
+    if (FM != BX_NONE) {
+        const DynSh sN(StageRef{io.st, io.N});
+        if (sN.ng > 0) gen_alpha<FM>(io, sN, io.N, bc, xcol, al);
+    }
 }
 
 template <class FX>
@@ -1826,11 +1888,11 @@ __device__ void ric_trs(const RicIO& io, Scratch* sm, const double* hb, const do
     const int l = lane_id(), g = l >> 4, c = l & 15;
     // ---- backward
     TrsFrag cur;
-    const StageInfo sN = load_stage(io.st, io.N);
-    with_shape<FX>(sN, [&](const auto& sh) { trs_fetch<TM, RPB>(io, sh, io.N, hb, hq, bc, compute_Pb, Pb, cur); });
+    with_shape<FX>(StageRef{io.st, io.N}, [&](const auto& sh) { trs_fetch<TM, RPB>(io, sh, io.N, hb, hq, bc, compute_Pb, Pb, cur); });
     double hN = cur.h0 + box_gradient<TM>(bc, cur);
-    if (sN.ng > 0) hN += gen_gradient<TM>(io, DynSh(sN), io.N, bc);
     {
+        const DynSh sN(StageRef{io.st, io.N});
+        if (sN.ng > 0) hN += gen_gradient<TM>(io, sN, io.N, bc);
         const int v = tile_var(c, sN.nu, sN.nx, sN.xo);
         gst(ux, io.N * V16 + v, hN, g == 0 && v >= 0);
     }
@@ -1838,16 +1900,14 @@ __device__ void ric_trs(const RicIO& io, Scratch* sm, const double* hb, const do
     d4 S1 = cur.S;
     TrsFrag nxt;
     {
-        const StageInfo s1 = load_stage(io.st, io.N - 1);
-        with_shape<FX>(s1, [&](const auto& sh) { trs_fetch<TM, RPB>(io, sh, io.N - 1, hb, hq, bc, compute_Pb, Pb, nxt); });
+        with_shape<FX>(StageRef{io.st, io.N - 1}, [&](const auto& sh) { trs_fetch<TM, RPB>(io, sh, io.N - 1, hb, hq, bc, compute_Pb, Pb, nxt); });
     }
     // stage k on fa while stage k-1 is fetched into fb; unrolled by two, the fragments swap roles
     auto stage = [&](int k, const TrsFrag& fa, TrsFrag& fb) __attribute__((always_inline)) {
         const int kn = k > 0 ? k - 1 : 0;
-        const StageInfo sn = load_stage(io.st, kn);
-        with_shape<FX>(sn, [&](const auto& sh) { trs_fetch<TM, RPB>(io, sh, kn, hb, hq, bc, compute_Pb, Pb, fb); });
+        with_shape<FX>(StageRef{io.st, kn}, [&](const auto& sh) { trs_fetch<TM, RPB>(io, sh, kn, hb, hq, bc, compute_Pb, Pb, fb); });
         asm volatile("" ::: "memory");
-        const StageInfo si = load_stage(io.st, k);
+        const StageRef si{io.st, k};
         with_shape<FX>(si, [&](const auto& sh) { trs_step<TM, RPB>(io, sm, sh, k, fa, bc, ux, compute_Pb, Pb, S1, pcol); });
     };
     for (int k = io.N - 1;;) {

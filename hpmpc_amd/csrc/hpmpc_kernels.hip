@@ -70,6 +70,7 @@ struct LdsTabs {
     const StageInfo* st;
     const signed char* tileslot;
     const signed char* slotvar;
+    double* gc;  // N+1: the problem's clamp-certificate bounds (filled by the factorisation pass, fact_body)
 };
 
 __device__ __forceinline__ LdsTabs lds_tables(const KArgs& a) {
@@ -94,6 +95,7 @@ __device__ __forceinline__ LdsTabs lds_tables(const KArgs& a) {
     T.st = st;
     T.tileslot = ts;
     T.slotvar = sv;
+    T.gc = reinterpret_cast<double*>(sv + n1 * 16);
     return T;
 }
 
@@ -586,6 +588,11 @@ __device__ __forceinline__ void fact_body(const KArgs& a, const LdsTabs& T, IpmV
     Scratch& sm = *T.sm;
     const double* st = v.w.state;
     const bool sn = a.single_newton != 0;
+    // the certificate bounds of the solve (cert_pass) into LDS: the stage loop reads them with ds_read instead of
+    // holding one more buffer descriptor in SGPRs
+    for (int i = v.l; i <= v.N; i += 64) T.gc[i] = v.w.cert[i];
+    wsync();
+    v.bc.cert = T.gc;
     if (st[S_PHASE] == 1.0)
         ric_backward<true, BX_P1, FX>(v.io, &sm, 0, nullptr, 0, nullptr, v.bc, 1, v.w.Pb);
     else {  // the single-Newton variant factorises with the data's own b/q rows (d_ip2_res_hard.c:1700-1760)
@@ -885,7 +892,7 @@ __device__ __forceinline__ bool update_body_mw(const KArgs& a, const IpmView& v0
 
 // LDS of the multi-wave kernel: the stage tables (lds_tables, dynamic) beside the static hk_mw object
 __host__ __device__ constexpr size_t mw_lds_bytes(int N) {
-    return sizeof(Scratch) + (size_t)(N + 1) * (sizeof(StageInfo) + 32);
+    return sizeof(Scratch) + (size_t)(N + 1) * (sizeof(StageInfo) + 40);
 }
 
 }  // namespace
@@ -1140,7 +1147,7 @@ __global__ __launch_bounds__(64) void hk_kkt_new_rhs_p1(KArgs a) {
 template <class FX>
 static int launch_t(int which, const KArgs* a, int count, hipStream_t stream) {
     dim3 grid(count), block(64);
-    const size_t lds = sizeof(Scratch) + (size_t)(a->N + 1) * (sizeof(StageInfo) + 32);
+    const size_t lds = sizeof(Scratch) + (size_t)(a->N + 1) * (sizeof(StageInfo) + 40);
     switch (which) {
         case 0: hipLaunchKernelGGL(hk_ric_sv<FX>, grid, block, lds, stream, *a); break;
         case 1: hipLaunchKernelGGL(hk_ric_trf<FX>, grid, block, lds, stream, *a); break;

@@ -41,6 +41,10 @@ def test_golden_through_c_abi(product, case):
 # pivot is the difference of two rounding-level terms; the last two variants fail the certificate without a clamp)
 XCLAMP = [(1e-16, 1e-9, 0.0), (1e-16, 1e-9, 0.5), (0.0, 0.0, 0.3), (5e-16, 1e-8, 0.2), (1e-8, 1e-9, 0.1),
           (1e-4, 1e-3, 0.2)]
+# IPM gate of the clamp problems (N=20, boxes): the rule of GATES, max(default, 4 x the spread of the reference's own
+# builds c99 / fma / X64_AVX against c99).  Only (1e-16, 1e-9, 0.5) needs one: it does not converge within k_max=50
+# (ret 1 in every build) and the builds end 2.7e-5 apart; the other five agree to <= 7e-14.
+XCLAMP_IPM_TOL = {(1e-16, 1e-9, 0.5): 4 * 2.7e-5}
 
 
 @pytest.mark.parametrize("d,off,r", XCLAMP, ids=[f"d{x[0]:g}_off{x[1]:g}_r{x[2]:g}" for x in XCLAMP])
@@ -75,8 +79,9 @@ def test_inner_x_pivot_clamp_ipm(product, oracle):
     from helpers import xclamp_qp
 
     qps = [xclamp_qp(N=20, nx=8, nu=3, d=d, off=off, r=r, boxes=True) for d, off, r in XCLAMP]
-    for one in qps:
-        compare_ipm(one, product.ipm(one.copy(), k_max=50), oracle.ipm(one.copy(), k_max=50))
+    tols = [XCLAMP_IPM_TOL.get(v) for v in XCLAMP]
+    for one, tol in zip(qps, tols):
+        compare_ipm(one, product.ipm(one.copy(), k_max=50), oracle.ipm(one.copy(), k_max=50), tol=tol or TOL_IPM)
     q0 = qps[0]
     qp = OCPQP(q0.N, q0.nx, q0.nu, q0.nb, q0.ng, q0.idxb, [np.stack([q.BAbt[k] for q in qps]) for k in range(q0.N)],
                [np.stack([q.RSQrq[k] for q in qps]) for k in range(q0.N + 1)],
@@ -92,11 +97,11 @@ def test_inner_x_pivot_clamp_ipm(product, oracle):
                 s.ipm_solo()
             torch.cuda.synchronize()
             g = {n: getattr(s, n).cpu().numpy() for n in ("ux", "pi", "lam", "t", "kk", "ret")}
-            for p, one in enumerate(qps):
+            for p, (one, tol) in enumerate(zip(qps, tols)):
                 got = dict(kk=int(g["kk"][p]), ret=int(g["ret"][p]), ux=[g["ux"][p, k] for k in range(q0.N + 1)],
                            pi=[g["pi"][p, k] for k in range(q0.N)], lam=[g["lam"][p, k] for k in range(q0.N + 1)],
                            t=[g["t"][p, k] for k in range(q0.N + 1)])
-                compare_ipm(one, got, oracle.ipm(one.copy(), k_max=50))
+                compare_ipm(one, got, oracle.ipm(one.copy(), k_max=50), tol=tol or TOL_IPM)
     finally:
         if old is None:
             os.environ.pop("HPMPC_MI355X_SOLO", None)
