@@ -653,7 +653,7 @@ __device__ __forceinline__ int ric_trs_mw(const RicIO& io, int tb, int w, const 
                     for (int r = 0; r < 4; r++) part += bop[r] * wrow[r];
                     double h = hpre;
                     h += xrow_sum(part);
-                    h = solve_ln(sh, Sk, invd, h, !SHT::fixed && k == 0);
+                    h = trs_usolve(sh, Sk, invd, h, !SHT::fixed && k == 0);
                     gst(ux, k * V16 + vc, h, g == 0 && vc >= 0);
                     pcol = h;
                 });

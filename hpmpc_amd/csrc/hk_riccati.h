@@ -634,9 +634,9 @@ __device__ __forceinline__ void store_factor(double* Fk, const d4& S, double lc,
 
 // Packed record of a compiled-class stage (nu <= 4, so the u block is tile block 0 and the state block starts at
 // tile index xo = 4).  What the solves read of it, and nothing else:
-//   [0, 64)    S0: tile register 0 = the u columns of L in upper storage (trs: the n-form u solve)
+//   [0, 64)    unused (was S0, the u columns of L: the trs u solve now runs in gain form on KG, trs_usolve)
 //   [64, 80)   l = [l_u; p_k] (the sv forward's right-hand side; pi's p_{k+1})
-//   [80, 96)   the u pivots' inverse diagonal (trs)
+//   [80, 96)   the u pivots' inverse diagonal (stored with l by one instruction; no compiled-class solve reads it)
 //   [96, 160)  the gain block KG (4 x 16, the forward's u = KG [rhs_u; x])
 //   [160, ..)  P_k, the state block, packed lower by rows (NX (NX+1) / 2 doubles; symmetric, so the tile's upper
 //              half is not stored): 1 392 B against the 2 816 B of the full record at nx = 12 (S1..S3 are 1 536 B
@@ -654,7 +654,9 @@ template <int NX>
 __device__ __forceinline__ void store_factor_fixed(double* Fk, const d4& S, double lc, double invd, double kg,
                                                    bool ok) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
-    gst(Fk, l, S[0], ok);
+    // S0 is not stored (every solve of a compiled-class stage runs its u block in gain form: fwd_step, trs_usolve);
+    // the masked store keeps the per-stage vector-memory count of store_factor
+    gst(Fk, l, S[0], false);
     gst(Fk, FXR_L + 16 * g + c, g == 0 ? lc : invd, ok && g < 2);
     gst(Fk, FXR_KG + l, kg, ok);
     const int j = c - 4;
@@ -1453,6 +1455,28 @@ __device__ __forceinline__ double solve_ln(const SH& sh, const d4& S, double inv
     return h;
 }
 
+// The trs backward's u solve of stage k (the rectangular dtrsv_n_lib over the nu pivots, d_back_ric_rec.c:687).  A
+// fixed-shape stage (nu <= 4, u block = tile block 0) runs it in gain form on the record's gain block KG, which the
+// trs fetch puts in S[0]: with N = L_uu^-1, the solve is y = N h_u and h_x' = h_x - L_xu N h_u, and KG (stage_chol
+// KGEN: KG[g][c] = -(L_uu^-T e_c)_g on the u tiles, -(L_uu^-T L[c][0..3]')_g on the state tiles) is exactly
+// [-N' | -(L_xu N)'] -- transposes of the substitution's own matrices (also with clamped pivots: the forward and the
+// backward substitution with the same zeroed inverse diagonal are transposes of each other).  So
+//   t[c] = sum_g KG[g][c] h[g],   y[c] = -t[c] (c < 4),   h'[c] = h[c] + t[c] (c >= 4):
+// four row broadcasts, one product and a row-group sum instead of four dependent pivot steps.
+template <class SH>
+__device__ __forceinline__ double trs_usolve(const SH& sh, const d4& S, double invd, double h, bool all) {
+    if constexpr (SH::fixed) {
+        static_assert(SH::xo == 4, "gain form needs the u block in tile block 0");
+        const int c = lane_id() & 15;
+        // h[g] in every lane of row group g (h is in col layout: lane (g, j) holds h[j])
+        const double hg = sel_g(row_bcast<0>(h), row_bcast<1>(h), row_bcast<2>(h), row_bcast<3>(h));
+        const double t = xrow_sum(S[0] * hg);
+        return c < 4 ? -t : h + t;
+    } else {
+        return solve_ln(sh, S, invd, h, all);
+    }
+}
+
 // pi = P x + p on the next stage's record S1 (P form; the reference's Lxx (Lxx' x + l_x), dtrmv_u_n +
 // dtrmv_u_t, d_back_ric_rec.c:355-365), x in row layout, result in col layout.
 __device__ __forceinline__ double pi_from_x(const d4& S1, int xo1, const double x1row[4], double pcol) {
@@ -1753,16 +1777,16 @@ __device__ __forceinline__ void trs_fetch(const RicIO& io, const SH& sh, int k, 
     const int compute_Pb = RPB ? compute_Pb_ : 0;
     const int l = lane_id(), g = l >> 4, c = l & 15;
     const double* Fk = io.F + (long)k * FSTRIDE;
-    // the n-form solve of a fixed-shape stage runs over its u pivots (< 4), i.e. reads S[0] only; rows
-    // 4..15 are needed by the generic solve and by P_{k} b_{k-1} (compute_Pb, the KKT re-solve)
-    if constexpr (SH::fixed) {  // packed record: S0 (the u columns), the u pivots, P only for a P b recompute
-        f.S[0] = gld(Fk, l);
+    // a fixed-shape stage solves its u block in gain form (trs_usolve: KG in S[0], no pivots); rows 4..15 are
+    // needed by the generic solve and by P_{k} b_{k-1} (compute_Pb, the KKT re-solve)
+    if constexpr (SH::fixed) {  // packed record: the gain block KG into S[0] (trs_usolve), P only for a P b recompute
+        f.S[0] = gld(Fk, FXR_KG + l);
         if (RPB) {
             load_p_fixed<SH::nx>(Fk, f.S, compute_Pb);
         } else {
             f.S[1] = f.S[2] = f.S[3] = 0.0;
         }
-        f.invd = gld(Fk, FXR_INVD + c);
+        f.invd = 0.0;
     } else {
 #pragma unroll
         for (int r = 0; r < 4; r++) f.S[r] = gld(Fk, r * 64 + l);
@@ -1872,7 +1896,7 @@ __device__ __forceinline__ void trs_step(const RicIO& io, Scratch* sm, const SH&
         if (sh.ng > 0) h += gen_gradient<TM>(io, sh, k, bc);  // dgemv_n on DCt (:621-633)
     }
     h += xrow_sum(part);
-    h = solve_ln(sh, cur.S, cur.invd, h, !SH::fixed && k == 0);
+    h = trs_usolve(sh, cur.S, cur.invd, h, !SH::fixed && k == 0);
     gst(ux, k * V16 + vc, h, g == 0 && vc >= 0);
     pcol = h;
     S1 = cur.S;

@@ -26,7 +26,7 @@ from hpmpc_amd.ocp import (BS, OCPQP, lib4_size, mass_spring_qp, pack_lib4, rup,
                            unpack_lib4)
 
 sys.path.insert(0, os.path.dirname(HERE))
-from helpers import COND_FILL, sub_block, xclamp_qp  # noqa: E402
+from helpers import COND_FILL, parse_ric_driver, sub_block, xclamp_qp  # noqa: E402
 
 
 def ref_api():
@@ -629,23 +629,6 @@ def wide(ref, refa, out):
                     ret=r["status"], stat=r["stat"])
         out.append(save_case(f"iface_{name}", "iface", IO.to_qp(P), dict(N2=N2, mu0=2.0, mu_tol=1e-10, k_max=50),
                              outs, extra=IO.to_flat(P)))
-
-
-def parse_ric_driver(text):
-    """ux / pi rows printed by test_problems/test_d_ric_mpc.c (d_print_mat, "%9.5f")."""
-    blocks = {"ux": [], "pi": []}
-    cur = None
-    for line in text.splitlines():
-        w = line.split()
-        if w in (["ux"], ["pi"]):
-            cur = w[0]
-            continue
-        if cur and w:
-            try:
-                blocks[cur].append([float(x) for x in w])
-            except ValueError:
-                cur = None
-    return blocks
 
 
 def driver(out):

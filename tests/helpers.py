@@ -602,3 +602,20 @@ def compare_ipm(case_like_qp, a, b, tol=TOL_IPM, allow_divergent=False):
             e = max(e, float(np.max(np.abs(g - r) / np.maximum(1, np.abs(r)), initial=0)))
     assert e <= tol, e
     return e
+
+
+def parse_ric_driver(text):
+    """ux / pi rows printed by test_problems/test_d_ric_mpc.c (d_print_mat, "%9.5f")."""
+    blocks = {"ux": [], "pi": []}
+    cur = None
+    for line in text.splitlines():
+        w = line.split()
+        if w in (["ux"], ["pi"]):
+            cur = w[0]
+            continue
+        if cur and w:
+            try:
+                blocks[cur].append([float(x) for x in w])
+            except ValueError:
+                cur = None
+    return blocks

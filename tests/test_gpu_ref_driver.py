@@ -21,8 +21,7 @@ DRV = os.path.join(ROOT, "oracle", "_ref", "drivers", "test_d_ric_mpc")
 
 def test_unchanged_reference_driver_on_gpu(tmp_path):
     assert os.path.exists(DRV), "relinked reference driver not built (tools/relink/Makefile drivers)"
-    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
-    from make_golden import parse_ric_driver
+    from helpers import parse_ric_driver
 
     (tmp_path / "test_problems" / "results").mkdir(parents=True)
     # The driver allocates hpi[0] with pnx_v[0] = 0 doubles (test_d_ric_mpc.c:498) and every sv / trs call then

@@ -116,8 +116,7 @@ def test_reference_driver_output_is_the_golden(drivers):
 
     import numpy as np
 
-    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
-    from make_golden import parse_ric_driver
+    from helpers import parse_ric_driver
 
     with tempfile.TemporaryDirectory() as d:
         os.makedirs(os.path.join(d, "test_problems", "results"))

@@ -28,8 +28,10 @@ import json, sys
 l = [x for x in open(f"gpurun_out/ab/{sys.argv[1]}.log") if x.startswith("{")][-1]
 d = json.loads(l)
 p = d["roofline"]["pass_ms_per_step"]
+par = d.get("parity") or {}
 print(sys.argv[1], round(d["value"]), {k[7:]: round(v, 3) for k, v in p.items()}, "ric", round(d["riccati"]["value"]),
-      "N50", round((d.get("riccati_batch_N50") or {}).get("value", 0)))
+      "N50", round((d.get("riccati_batch_N50") or {}).get("value", 0)), "parity", par.get("max_rel_err"),
+      par.get("kk_ret_equal"))
 PY
   done
 done
