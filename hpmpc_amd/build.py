@@ -122,7 +122,7 @@ def build_oracle(force: bool = False) -> None:
     odir = os.path.join(ROOT, "oracle")
     targets = ["oracle"]
     if os.path.isdir(os.environ.get("HPMPC_REF", "/root/reference")):
-        targets.append("ref")
+        targets += ["ref", "ref_avx"]  # ref_avx: the alternate IPM's goldens (make_golden.py)
     subprocess.run(["make", "-s", "-C", odir] + (["-B"] if force else []) + targets, check=True)
     if "ref" in targets:  # the reference's own test_d_ric_mpc.c, unchanged, relinked against the product
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tools", "relink"), "drivers"], check=True)

@@ -658,6 +658,55 @@ def driver(out):
     with open(path, "w") as f:
         f.write(text)
     out.append(path)
+    # Its alternate-IPM KKT re-solve (kkt2) from the reference's default-target build instead: the c99 build's
+    # d_kkt_solve_new_rhs_mpc_hard_tv passes 9 arguments to the 8-parameter c99 gradient helper (oracle/Makefile
+    # ref_avx), and on this driver's problem its kkt2 ends 8.3e-8 (ux) / 3.4e-7 (pi) from the X64_AVX / X64_AVX2
+    # builds and the oracle, which agree with each other to 1e-15.  Same problem and call sequence as the driver
+    # (relink_qp; its c99 run reproduces the printed kkt2 lines bitwise).
+    qp, b, q = relink_qp()
+    avx = ref_avx_api()
+    r = avx.ipm(qp.copy(), k_max=50, mu0=2.0, mu_tol=1e-8, alpha_min=1e-8, res=False)
+    kk = avx.kkt_new_rhs_plain(qp.copy(), r["work"], b, q, qp.d, r["ux"])
+    path = os.path.join(HERE, "drivers", "relink_kkt2_avx.npz")
+    arrs = {f"ux_{k}": kk["ux"][k][: qp.nux(k)] for k in range(qp.N + 1)}
+    arrs.update({f"pi_{k}": kk["pi"][k][: int(qp.nx[k + 1])] for k in range(qp.N)})
+    np.savez_compressed(path, **arrs)
+    out.append(path)
+
+
+def relink_qp():
+    """The problem of tools/relink/relink_driver.c:53-100 (N=10, nx = 0 at stage 0 then 8, nu=3, boxes on the first
+    nu + nx/2 variables) and the new right-hand sides b, q of its re-solves (:120-125)."""
+    N, NX, NU = 10, 8, 3
+    nx = np.array([0 if k == 0 else NX for k in range(N + 1)])
+    nu = np.array([NU if k < N else 0 for k in range(N + 1)])
+    nb = nu + nx // 2
+    idxb = [np.arange(nb[k], dtype=np.int32) for k in range(N + 1)]
+    R, Bl, D = [], [], []
+    for k in range(N + 1):
+        nux = int(nu[k] + nx[k])
+        nx1 = int(nx[k + 1]) if k < N else 0
+        M = np.zeros((nux + 1, nux))
+        M[np.arange(nux), np.arange(nux)] = 2.0
+        M[nux, :] = 0.1
+        R.append(pack_lib4(M))
+        if k < N:
+            B = np.zeros((nux + 1, nx1))
+            for i in range(nx1):
+                B[nu[k] + i % (nx[k] if nx[k] > 0 else 1), i] = 1.0
+            for i in range(nx1):
+                B[i % (nu[k] if nu[k] > 0 else 1), i] += 0.1
+            B[nux, :] = 0.05
+            Bl.append(pack_lib4(B))
+        pnb = rup(int(nb[k]), BS)
+        d = np.zeros(2 * pnb + 4)
+        d[: nb[k]] = -1.0
+        d[pnb: pnb + nb[k]] = 1.0
+        D.append(d)
+    qp = OCPQP(N, nx, nu, nb, np.zeros(N + 1, dtype=nx.dtype), idxb, Bl, R, D, [], None)
+    b = [np.array([0.03 * ((i + k) % 3) for i in range(int(nx[k + 1]))] + [0.0] * 4) for k in range(N)]
+    q = [np.array([0.01 * (i + 1) - 0.02 * k for i in range(qp.nux(k))] + [0.0] * 4) for k in range(N + 1)]
+    return qp, b, q
 
 
 def divergent(ref, out):

@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/tests.log 2>&1 || { tail -20 gpurun_out/tests.log; exit 1; }
+timeout -k 10 900 python3 -u -m pytest tests -m gpu --maxfail=5 -q --timeout 300 --timeout-method thread > gpurun_out/tests.log 2>&1 || { tail -20 gpurun_out/tests.log; exit 1; }
 tail -2 gpurun_out/tests.log
 timeout -k 10 300 python3 bench.py --no-cpu --no-pcond "$@" > gpurun_out/qbench.log 2>&1 || { tail -20 gpurun_out/qbench.log; exit 1; }
 python3 - <<'PY'
