@@ -17,10 +17,10 @@
 // The hand-over is a ring of MW_D slots in LDS (16 doubles per lane each) with a full / free flag per slot; the
 // flags carry tickets that grow over the whole launch, so no sweep has to reset them.  Every value is computed by
 // the same routine with the same operands as in the single-wave sweeps (hk_riccati.h); the step length is the
-// minimum of the helpers' per-lane candidates.  The results are bitwise those of hk_ipm_solo only when the product
-// terms are contracted into FMAs the same way in both kernels (they are with -ffp-contract=on, measured); under the
-// default contraction hipcc fuses a few a * b + c differently once the bodies are split over waves, and the two
-// agree to rounding (tests/test_gpu_parity.py test_solo_matches_batch).
+// minimum of the helpers' per-lane candidates.  The two kernels agree to rounding, not bitwise (tests/test_gpu_parity.py
+// test_solo_matches_batch): the single-wave predictor expands mu_aff in alpha during its sweep (MuAcc) while this one
+// forms it element-wise afterwards, and under the default contraction hipcc fuses a few a * b + c differently once
+// the bodies are split over waves.
 // A wait that does not end (a bug, not a data condition) sets MwShared.err after ~2^22 polls and falls through,
 // so every wave still reaches the end of the launch; the kernel then reports ret = HK_MW_ERR.
 #pragma once

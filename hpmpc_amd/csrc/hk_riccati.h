@@ -918,10 +918,30 @@ __device__ double gen_rq(const RicIO& io, const DynSh& sh, int k, const double* 
     return xrow_sum(part);
 }
 
+// The predictor's mu_aff = mu_scal sum_i (lam_i + alpha dlam_i)(t_i + alpha dt_i) (d_compute_mu_mpc_hard_tv,
+// d_aux_ip_hard_lib4.c) needs alpha, which is known only after the whole forward sweep.  Expanded in alpha, it is
+// S0 + alpha S1 + alpha^2 S2 with S0 = sum lam t, S1 = sum (lam dt + dlam t), S2 = sum dlam dt, and the three sums
+// are accumulated per lane while the sweep has lam, t and the fresh steps in registers, so no second pass re-reads
+// them (pred_body).  Each constraint is counted once: in row group 0 of its tile lane (boxes) or in lane (g, 0)
+// (general constraints, gen_alpha).  The expansion rounds differently from the element-wise product; near
+// convergence, where mu_aff << mu, its relative error grows as mu / mu_aff but sigma = (mu_aff / mu)^3 shrinks
+// faster, so the centering term sigma mu moves by far less than the IPM gates.
+struct MuAcc {
+    double s0, s1, s2;
+};
+__device__ __forceinline__ void mu_acc(MuAcc* m, bool on, double ll, double lu, double tl, double tu, double dll,
+                                       double dlu, double dtl, double dtu) {
+    if (m == nullptr) return;
+    m->s0 += on ? ll * tl + lu * tu : 0.0;
+    m->s1 += on ? (ll * dtl + dll * tl) + (lu * dtu + dlu * tu) : 0.0;
+    m->s2 += on ? dll * dtl + dlu * dtu : 0.0;
+}
+
 // Forward: steps of the general slots from the primal step x (col layout) and their step-length
 // candidates (d_compute_alpha_mpc_hard_tv / d_compute_alpha_res_mpc_hard_tv general halves).
 template <int FM>
-__device__ void gen_alpha(const RicIO& io, const DynSh& sh, int k, const BoxCtx& bc, double x, double& al) {
+__device__ void gen_alpha(const RicIO& io, const DynSh& sh, int k, const BoxCtx& bc, double x, double& al,
+                          MuAcc* ma = nullptr) {
     if (FM == BX_NONE) return;
     const int c = lane_id() & 15;
     double dg[4];
@@ -951,6 +971,7 @@ __device__ void gen_alpha(const RicIO& io, const DynSh& sh, int k, const BoxCtx&
         gst(bc.dt, q.up, dtu, st);
         gst(bc.dlam, q.lo, dll, st);
         gst(bc.dlam, q.up, dlu, st);
+        mu_acc(ma, st, lml, lmu, tl, tu, dll, dlu, dtl, dtu);
         if (q.ok) {
             alpha_rule(al, lml, dll);
             alpha_rule(al, lmu, dlu);
@@ -1596,7 +1617,8 @@ __device__ __forceinline__ void fwd_fetch_k(const RicIO& io, int k, const double
 // Step of the box slacks / multipliers of tile c given the primal step x = dux_k[var(c)] (col layout)
 // and the per-lane step-length candidate (d_compute_alpha_mpc_hard_tv :489-614 / _res_ :1180-1313).
 template <int FM, bool PRED>
-__device__ __forceinline__ void box_alpha(const BoxCtx& bc, const FwdFrag& f, double x, double& al) {
+__device__ __forceinline__ void box_alpha(const BoxCtx& bc, const FwdFrag& f, double x, double& al,
+                                          MuAcc* ma = nullptr) {
     if (FM == BX_NONE) return;
     const BoxLane& b = f.bl;
     double dtl, dtu, dll, dlu, lml, lmu, tl, tu;
@@ -1629,6 +1651,7 @@ __device__ __forceinline__ void box_alpha(const BoxCtx& bc, const FwdFrag& f, do
     }
     st_lu(bc.dt, b, dtl, dtu, b.ok);
     st_lu(bc.dlam, b, dll, dlu, b.ok);
+    mu_acc(ma, b.ok && (lane_id() >> 4) == 0, lml, lmu, tl, tu, dll, dlu, dtl, dtu);
     if (b.ok) {
         alpha_rule(al, lml, dll);
         alpha_rule(al, lmu, dlu);
@@ -1641,7 +1664,7 @@ __device__ __forceinline__ void box_alpha(const BoxCtx& bc, const FwdFrag& f, do
 template <int MODE, int FM, bool PRED, class SH>
 __device__ __forceinline__ void fwd_step(const RicIO& io, Scratch* sm, const SH& sh, int k, const FwdFrag& cur,
                                          const FwdFrag& nxt, double& xcol, double* ux, int compute_pi, double* pi,
-                                         const BoxCtx& bc, double& al) {
+                                         const BoxCtx& bc, double& al, MuAcc* ma) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
     const bool all = !SH::fixed && k == 0;
     double xrow[4];
@@ -1677,9 +1700,9 @@ __device__ __forceinline__ void fwd_step(const RicIO& io, Scratch* sm, const SH&
     // the predictor's step is never read (the corrector's trs overwrites dux before reading it, and mu_aff
     // needs dt / dlam only): it is not stored
     if (!PRED) gst(ux, k * V16 + vcs, ucol, g == 0 && vcs >= 0);
-    box_alpha<FM, PRED>(bc, cur, ucol, al);
+    box_alpha<FM, PRED>(bc, cur, ucol, al, ma);
     if constexpr (!SH::fixed && FM != BX_NONE) {
-        if (sh.ng > 0) gen_alpha<FM>(io, sh, k, bc, ucol, al);
+        if (sh.ng > 0) gen_alpha<FM>(io, sh, k, bc, ucol, al, ma);
     }
     // x_{k+1} = b + BAbt_k' ux_k  (dgemv_t_lib alg 1, :347-351), col layout over stage-(k+1) tile
     double gp = 0.0;
@@ -1709,7 +1732,7 @@ __device__ __forceinline__ void fwd_step(const RicIO& io, Scratch* sm, const SH&
 // the per-lane step-length candidate `al` (caller reduces it with wave_min).
 template <int MODE, int FM, class FX, bool PRED = false>
 __device__ void ric_forward(const RicIO& io, Scratch* sm, const double* bsrc, int use_bsrc, double* ux,
-                            int compute_pi, double* pi, const BoxCtx& bc, double& al) {
+                            int compute_pi, double* pi, const BoxCtx& bc, double& al, MuAcc* ma = nullptr) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
     double xcol = 0.0;  // x_k in col layout (stage-k tile coords)
     // Stage k runs on fa (its record) and fb (stage k+1's, for pi) while stage k+2 is fetched into fc; the
@@ -1722,7 +1745,7 @@ __device__ void ric_forward(const RicIO& io, Scratch* sm, const double* bsrc, in
         fwd_fetch_k<MODE, FM, FX, PRED>(io, k + 2 <= io.N ? k + 2 : io.N, bsrc, use_bsrc, ux, compute_pi, bc, fc);
         const StageRef si{io.st, k};
         with_shape<FX>(si, [&](const auto& sh) {
-            fwd_step<MODE, FM, PRED>(io, sm, sh, k, fa, fb, xcol, ux, compute_pi, pi, bc, al);
+            fwd_step<MODE, FM, PRED>(io, sm, sh, k, fa, fb, xcol, ux, compute_pi, pi, bc, al, ma);
         });
         HK_STAMP(12, k);
     };
@@ -1730,7 +1753,7 @@ __device__ void ric_forward(const RicIO& io, Scratch* sm, const double* bsrc, in
         const DynSh sN(StageRef{io.st, io.N});
         const int v = tile_var(c, sN.nu, sN.nx, sN.xo);
         if (!PRED) gst(ux, io.N * V16 + v, xcol, g == 0 && v >= 0);
-        box_alpha<FM, PRED>(bc, fN, xcol, al);
+        box_alpha<FM, PRED>(bc, fN, xcol, al, ma);
     };
     for (int k = 0;;) {
         if (k >= io.N) { finish(f0); break; }
@@ -1743,7 +1766,7 @@ __device__ void ric_forward(const RicIO& io, Scratch* sm, const double* bsrc, in
     }
     if (FM != BX_NONE) {
         const DynSh sN(StageRef{io.st, io.N});
-        if (sN.ng > 0) gen_alpha<FM>(io, sN, io.N, bc, xcol, al);
+        if (sN.ng > 0) gen_alpha<FM>(io, sN, io.N, bc, xcol, al, ma);
     }
 }
 

@@ -658,7 +658,8 @@ def driver(out):
     with open(path, "w") as f:
         f.write(text)
     out.append(path)
-    # Its alternate-IPM KKT re-solve (kkt2) from the reference's default-target build instead: the c99 build's
+    # Its alternate-IPM KKT re-solve (kkt2) and that re-solve's residuals (res2) from the reference's default-target
+    # build instead: the c99 build's
     # d_kkt_solve_new_rhs_mpc_hard_tv passes 9 arguments to the 8-parameter c99 gradient helper (oracle/Makefile
     # ref_avx), and on this driver's problem its kkt2 ends 8.3e-8 (ux) / 3.4e-7 (pi) from the X64_AVX / X64_AVX2
     # builds and the oracle, which agree with each other to 1e-15.  Same problem and call sequence as the driver
@@ -670,6 +671,8 @@ def driver(out):
     path = os.path.join(HERE, "drivers", "relink_kkt2_avx.npz")
     arrs = {f"ux_{k}": kk["ux"][k][: qp.nux(k)] for k in range(qp.N + 1)}
     arrs.update({f"pi_{k}": kk["pi"][k][: int(qp.nx[k + 1])] for k in range(qp.N)})
+    # and the residuals of that re-solve (d_res_mpc_hard_tv on its ux, pi, lam, t: the driver prints res2.mu)
+    arrs["mu_0"] = np.array([avx.residuals_plain(qp, b, q, kk["ux"], kk["pi"], kk["lam"], kk["t"])["mu"]])
     np.savez_compressed(path, **arrs)
     out.append(path)
 

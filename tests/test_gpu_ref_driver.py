@@ -79,13 +79,13 @@ def test_relinked_ipm_driver_on_gpu():
     rheads, rvals = _parse_relink(open(os.path.join(ROOT, "tests", "golden", "drivers", "relink_driver.txt")).read())
     assert heads == rheads and len(heads) == 2
     assert vals.keys() == rvals.keys()
-    # kkt2 against the reference's default-target build (make_golden.py driver(): the c99 build's alternate KKT
-    # re-solve mis-binds its gradient helper and ends 8.3e-8 from every other build on this problem)
+    # kkt2 and its residuals res2 against the reference's default-target build (make_golden.py driver(): the c99
+    # build's alternate KKT re-solve mis-binds its gradient helper and ends 8.3e-8 from every other build here)
     kkt2 = np.load(os.path.join(ROOT, "tests", "golden", "drivers", "relink_kkt2_avx.npz"))
     for key, ref in rvals.items():
         tag = key[0].split(".")[0]
         tol = 1e-9 if key[0] == "ipm.stat" else GATES[tag]
-        if tag == "kkt2":
+        if tag in ("kkt2", "res2"):
             ref = kkt2[f"{key[0].split('.')[1]}_{key[1]}"]
         got = vals[key]
         assert got.shape == ref.shape, key
