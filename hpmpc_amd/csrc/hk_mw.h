@@ -17,10 +17,10 @@
 // The hand-over is a ring of MW_D slots in LDS (16 doubles per lane each) with a full / free flag per slot; the
 // flags carry tickets that grow over the whole launch, so no sweep has to reset them.  Every value is computed by
 // the same routine with the same operands as in the single-wave sweeps (hk_riccati.h); the step length is the
-// minimum of the helpers' per-lane candidates.  The two kernels agree to rounding, not bitwise (tests/test_gpu_parity.py
-// test_solo_matches_batch): the single-wave predictor expands mu_aff in alpha during its sweep (MuAcc) while this one
-// forms it element-wise afterwards, and under the default contraction hipcc fuses a few a * b + c differently once
-// the bodies are split over waves.
+// minimum of the helpers' per-lane candidates.  The results are bitwise those of hk_ipm_solo only when the product
+// terms are contracted into FMAs the same way in both kernels (they are with -ffp-contract=on, measured); under the
+// default contraction hipcc fuses a few a * b + c differently once the bodies are split over waves, and the two
+// agree to rounding (tests/test_gpu_parity.py test_solo_matches_batch).
 // A wait that does not end (a bug, not a data condition) sets MwShared.err after ~2^22 polls and falls through,
 // so every wave still reaches the end of the launch; the kernel then reports ret = HK_MW_ERR.
 #pragma once
@@ -69,14 +69,18 @@ __device__ int g_mw_fault;
 
 __device__ __forceinline__ int mw_flag(const int* f) { return __atomic_load_n(f, __ATOMIC_RELAXED); }
 
-// The hand-over's ordering, stated in the memory model: a flag store is a workgroup-scope release of this wave's
-// earlier LDS accesses (the slot data it wrote, or read before freeing the slot), a successful poll is followed by
-// the matching acquire.  Both fences are limited to the LDS address space ("local"): the release is one
-// s_waitcnt lgkmcnt(0) before the flag store, the acquire one after the poll (which has waited already).
-// HK_MW_FENCE=0 builds the earlier form -- compiler barriers only, relying on the LDS performing one wave's ds_
-// operations in issue order -- for an A/B of the cost (tools/gpu_ab.sh).
+// The hand-over's ordering.  Everything a hand-over moves -- slot data and flags -- is LDS, and the LDS performs one
+// wave's ds_ instructions in issue order (for LDS-only traffic they also complete in order, which is why lgkmcnt
+// can count them): a flag written after the slot data by the same wave cannot become visible before the data, and a
+// consumer issues its slot reads only after the poll that saw the flag has returned.  The compiler keeps that order
+// through the "memory" clobbers below (no LDS access moves across a post or a successful poll).
+// HK_MW_FENCE=1 states the same order in the memory model instead -- a workgroup-scope release (LDS only) before
+// each flag store and the matching acquire after each successful poll -- at the price of an s_waitcnt lgkmcnt(0)
+// before every post, which also waits for the poster's unrelated scalar loads: a same-box A/B measured 350.4 vs
+// 367.1-367.5 us per lone-QP IP iteration (3 pairs, profiles/r04/ab_latency.txt), 4.7 %, above the 2 % the fenced
+// form was allowed, so it is a build option (tools/gpu_ab.sh variants) and not the default.
 #ifndef HK_MW_FENCE
-#define HK_MW_FENCE 1
+#define HK_MW_FENCE 0
 #endif
 __device__ __forceinline__ void mw_release_fence() {
 #if HK_MW_FENCE

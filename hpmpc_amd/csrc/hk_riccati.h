@@ -918,30 +918,10 @@ __device__ double gen_rq(const RicIO& io, const DynSh& sh, int k, const double* 
     return xrow_sum(part);
 }
 
-// The predictor's mu_aff = mu_scal sum_i (lam_i + alpha dlam_i)(t_i + alpha dt_i) (d_compute_mu_mpc_hard_tv,
-// d_aux_ip_hard_lib4.c) needs alpha, which is known only after the whole forward sweep.  Expanded in alpha, it is
-// S0 + alpha S1 + alpha^2 S2 with S0 = sum lam t, S1 = sum (lam dt + dlam t), S2 = sum dlam dt, and the three sums
-// are accumulated per lane while the sweep has lam, t and the fresh steps in registers, so no second pass re-reads
-// them (pred_body).  Each constraint is counted once: in row group 0 of its tile lane (boxes) or in lane (g, 0)
-// (general constraints, gen_alpha).  The expansion rounds differently from the element-wise product; near
-// convergence, where mu_aff << mu, its relative error grows as mu / mu_aff but sigma = (mu_aff / mu)^3 shrinks
-// faster, so the centering term sigma mu moves by far less than the IPM gates.
-struct MuAcc {
-    double s0, s1, s2;
-};
-__device__ __forceinline__ void mu_acc(MuAcc* m, bool on, double ll, double lu, double tl, double tu, double dll,
-                                       double dlu, double dtl, double dtu) {
-    if (m == nullptr) return;
-    m->s0 += on ? ll * tl + lu * tu : 0.0;
-    m->s1 += on ? (ll * dtl + dll * tl) + (lu * dtu + dlu * tu) : 0.0;
-    m->s2 += on ? dll * dtl + dlu * dtu : 0.0;
-}
-
 // Forward: steps of the general slots from the primal step x (col layout) and their step-length
 // candidates (d_compute_alpha_mpc_hard_tv / d_compute_alpha_res_mpc_hard_tv general halves).
 template <int FM>
-__device__ void gen_alpha(const RicIO& io, const DynSh& sh, int k, const BoxCtx& bc, double x, double& al,
-                          MuAcc* ma = nullptr) {
+__device__ void gen_alpha(const RicIO& io, const DynSh& sh, int k, const BoxCtx& bc, double x, double& al) {
     if (FM == BX_NONE) return;
     const int c = lane_id() & 15;
     double dg[4];
@@ -971,7 +951,6 @@ __device__ void gen_alpha(const RicIO& io, const DynSh& sh, int k, const BoxCtx&
         gst(bc.dt, q.up, dtu, st);
         gst(bc.dlam, q.lo, dll, st);
         gst(bc.dlam, q.up, dlu, st);
-        mu_acc(ma, st, lml, lmu, tl, tu, dll, dlu, dtl, dtu);
         if (q.ok) {
             alpha_rule(al, lml, dll);
             alpha_rule(al, lmu, dlu);
@@ -1574,8 +1553,7 @@ __device__ __forceinline__ void fwd_fetch(const RicIO& io, const SH& sh, int k, 
     if (MODE == 1) {
         const int vc = tile_var(c, sh.nu, sh.nx, sh.xo);
         f.hc = ldsel(ux + kk * V16, vc, live && vc >= 0);
-        // p_{k+1}: on fixed stages it is the next fragment's hux_{k+1} (fwd_step), not loaded twice
-        f.pk = SH::fixed ? 0.0 : ldsel(ux + (kk + 1) * V16, sh.nu1 + s, compute_pi && ok);
+        // p_{k+1} for pi_k is not loaded: fwd_step forms pi_{k-1} from its own fragment's hc (= hux_k)
     }
 #pragma unroll
     for (int i = 0; i < 10; i++) f.bx[i] = 0.0;
@@ -1617,8 +1595,7 @@ __device__ __forceinline__ void fwd_fetch_k(const RicIO& io, int k, const double
 // Step of the box slacks / multipliers of tile c given the primal step x = dux_k[var(c)] (col layout)
 // and the per-lane step-length candidate (d_compute_alpha_mpc_hard_tv :489-614 / _res_ :1180-1313).
 template <int FM, bool PRED>
-__device__ __forceinline__ void box_alpha(const BoxCtx& bc, const FwdFrag& f, double x, double& al,
-                                          MuAcc* ma = nullptr) {
+__device__ __forceinline__ void box_alpha(const BoxCtx& bc, const FwdFrag& f, double x, double& al) {
     if (FM == BX_NONE) return;
     const BoxLane& b = f.bl;
     double dtl, dtu, dll, dlu, lml, lmu, tl, tu;
@@ -1651,7 +1628,6 @@ __device__ __forceinline__ void box_alpha(const BoxCtx& bc, const FwdFrag& f, do
     }
     st_lu(bc.dt, b, dtl, dtu, b.ok);
     st_lu(bc.dlam, b, dll, dlu, b.ok);
-    mu_acc(ma, b.ok && (lane_id() >> 4) == 0, lml, lmu, tl, tu, dll, dlu, dtl, dtu);
     if (b.ok) {
         alpha_rule(al, lml, dll);
         alpha_rule(al, lmu, dlu);
@@ -1660,15 +1636,31 @@ __device__ __forceinline__ void box_alpha(const BoxCtx& bc, const FwdFrag& f, do
     }
 }
 
-// One forward stage k < N: u_k from the factor, x_{k+1} = b + BAbt' ux, pi_k, box steps.
+// pi_{k-1} = P_k x_k + p_k (the reference's Lxx (Lxx' x + l_x): dtrmv_u_n + dtrmv_u_t, d_back_ric_rec.c:355-365) from
+// stage k's record S (P_k in its state rows), x_k in row layout and p_k in col layout (the record's l row in the sv,
+// hux_k in the trs), stored over stage k's state tiles.  Formed at the start of stage k, where x_k is in row layout
+// for the u solve anyway, instead of at the end of stage k-1 with a second layout change of the same x_k.
+template <int MODE>
+__device__ __forceinline__ void fwd_pi(int xo, int nx, int k, const d4& S, const double xrow[4], double pc,
+                                       int compute_pi, double* pi) {
+    const int g = lane_id() >> 4, c = lane_id() & 15;
+    const int s = c - xo;
+    const bool okp = s >= 0 && s < nx;
+    double pv = 0.0;
+    if (compute_pi && k > 0) pv = pi_from_x(S, xo, xrow, okp ? pc : 0.0);  // wave-uniform
+    gst(pi, (k - 1) * V16 + s, pv, compute_pi && k > 0 && g == 0 && okp);
+}
+
+// One forward stage k < N: pi_{k-1}, u_k from the factor, x_{k+1} = b + BAbt' ux, box steps.
 template <int MODE, int FM, bool PRED, class SH>
 __device__ __forceinline__ void fwd_step(const RicIO& io, Scratch* sm, const SH& sh, int k, const FwdFrag& cur,
-                                         const FwdFrag& nxt, double& xcol, double* ux, int compute_pi, double* pi,
-                                         const BoxCtx& bc, double& al, MuAcc* ma) {
+                                         double& xcol, double* ux, int compute_pi, double* pi, const BoxCtx& bc,
+                                         double& al) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
     const bool all = !SH::fixed && k == 0;
     double xrow[4];
     col2row(sm, xcol, xrow);
+    if constexpr (!PRED) fwd_pi<MODE>(sh.xo, sh.nx, k, cur.S, xrow, MODE == 0 ? cur.lc : cur.hc, compute_pi, pi);
     const double rhs = (MODE == 0) ? cur.lc : cur.hc;
     double ur[4];
     if constexpr (SH::fixed) {
@@ -1700,9 +1692,9 @@ __device__ __forceinline__ void fwd_step(const RicIO& io, Scratch* sm, const SH&
     // the predictor's step is never read (the corrector's trs overwrites dux before reading it, and mu_aff
     // needs dt / dlam only): it is not stored
     if (!PRED) gst(ux, k * V16 + vcs, ucol, g == 0 && vcs >= 0);
-    box_alpha<FM, PRED>(bc, cur, ucol, al, ma);
+    box_alpha<FM, PRED>(bc, cur, ucol, al);
     if constexpr (!SH::fixed && FM != BX_NONE) {
-        if (sh.ng > 0) gen_alpha<FM>(io, sh, k, bc, ucol, al, ma);
+        if (sh.ng > 0) gen_alpha<FM>(io, sh, k, bc, ucol, al);
     }
     // x_{k+1} = b + BAbt_k' ux_k  (dgemv_t_lib alg 1, :347-351), col layout over stage-(k+1) tile
     double gp = 0.0;
@@ -1713,18 +1705,6 @@ __device__ __forceinline__ void fwd_step(const RicIO& io, Scratch* sm, const SH&
     const double x1 = cur.bval + xrow_sum(gp);
     xcol = ok ? x1 : 0.0;
     HK_STAMP(11, k);
-    double pv = 0.0;
-    if (compute_pi) {
-        double x1row[4];
-        col2row(sm, xcol, x1row);
-        if (MODE == 0)
-            pv = pi_from_x(nxt.S, sh.xo1, x1row, nxt.lc);  // pi_k = P x + p (p: the record's row)
-        else
-            // pi_k = P x + p_{k+1} (trs backward vector; fixed stages: the x tiles of stage k+1's hux, which the
-            // next fragment holds in col layout over the same tile coordinates)
-            pv = pi_from_x(nxt.S, sh.xo1, x1row, SH::fixed ? (ok ? nxt.hc : 0.0) : cur.pk);
-    }
-    gst(pi, k * V16 + s, pv, compute_pi && g == 0 && ok);
 }
 
 // Shared forward substitution (sv: rhs = -l_k ; trs: rhs = -hux_k), d_back_ric_rec.c:339-397 / :704-790.
@@ -1732,28 +1712,37 @@ __device__ __forceinline__ void fwd_step(const RicIO& io, Scratch* sm, const SH&
 // the per-lane step-length candidate `al` (caller reduces it with wave_min).
 template <int MODE, int FM, class FX, bool PRED = false>
 __device__ void ric_forward(const RicIO& io, Scratch* sm, const double* bsrc, int use_bsrc, double* ux,
-                            int compute_pi, double* pi, const BoxCtx& bc, double& al, MuAcc* ma = nullptr) {
+                            int compute_pi, double* pi, const BoxCtx& bc, double& al) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
     double xcol = 0.0;  // x_k in col layout (stage-k tile coords)
-    // Stage k runs on fa (its record) and fb (stage k+1's, for pi) while stage k+2 is fetched into fc; the
+    // Stage k runs on fa (its record) while stage k+2 is fetched into fc (fb, stage k+1's, is in flight); the
     // loop is unrolled by three with the fragments rotating roles (no register copies between stages).
     FwdFrag f0, f1, f2;
     fwd_fetch_k<MODE, FM, FX, PRED>(io, 0, bsrc, use_bsrc, ux, compute_pi, bc, f0);
     fwd_fetch_k<MODE, FM, FX, PRED>(io, 1, bsrc, use_bsrc, ux, compute_pi, bc, f1);
     auto stage = [&](int k, const FwdFrag& fa, const FwdFrag& fb, FwdFrag& fc) __attribute__((always_inline)) {
+        (void)fb;  // stage k+1's fragment stays in flight (the prefetch depth), it is no longer read here
         HK_STAMP(8, k);
         fwd_fetch_k<MODE, FM, FX, PRED>(io, k + 2 <= io.N ? k + 2 : io.N, bsrc, use_bsrc, ux, compute_pi, bc, fc);
         const StageRef si{io.st, k};
         with_shape<FX>(si, [&](const auto& sh) {
-            fwd_step<MODE, FM, PRED>(io, sm, sh, k, fa, fb, xcol, ux, compute_pi, pi, bc, al, ma);
+            fwd_step<MODE, FM, PRED>(io, sm, sh, k, fa, xcol, ux, compute_pi, pi, bc, al);
         });
         HK_STAMP(12, k);
     };
     auto finish = [&](const FwdFrag& fN) __attribute__((always_inline)) {  // stage N: nu = 0, every tile a state
         const DynSh sN(StageRef{io.st, io.N});
         const int v = tile_var(c, sN.nu, sN.nx, sN.xo);
-        if (!PRED) gst(ux, io.N * V16 + v, xcol, g == 0 && v >= 0);
-        box_alpha<FM, PRED>(bc, fN, xcol, al, ma);
+        if constexpr (!PRED) {
+            // pi_{N-1} = P_N x_N + p_N: the fragment of stage N carries the record's l row but not hux_N (it is fetched
+            // with stage N-1's shape), so the trs reads p_N here, before x_N overwrites ux_N
+            double pc = MODE == 0 ? fN.lc : ldsel(ux + io.N * V16, v, compute_pi && v >= 0);
+            double xrow[4] = {0.0, 0.0, 0.0, 0.0};
+            if (compute_pi) col2row(sm, xcol, xrow);
+            fwd_pi<MODE>(sN.xo, sN.nx, io.N, fN.S, xrow, pc, compute_pi, pi);
+            gst(ux, io.N * V16 + v, xcol, g == 0 && v >= 0);
+        }
+        box_alpha<FM, PRED>(bc, fN, xcol, al);
     };
     for (int k = 0;;) {
         if (k >= io.N) { finish(f0); break; }
@@ -1766,7 +1755,7 @@ __device__ void ric_forward(const RicIO& io, Scratch* sm, const double* bsrc, in
     }
     if (FM != BX_NONE) {
         const DynSh sN(StageRef{io.st, io.N});
-        if (sN.ng > 0) gen_alpha<FM>(io, sN, io.N, bc, xcol, al, ma);
+        if (sN.ng > 0) gen_alpha<FM>(io, sN, io.N, bc, xcol, al);
     }
 }
 

@@ -170,7 +170,13 @@ bool plan_upload_stages(hpmpc_mi355x_plan* P, const long long* offB, const long 
                   "plan stage upload");
 }
 
-long long ws_doubles(int N) { return (long long)(N + 1) * (FSTRIDE + 9 * V16 + 8 * V32 + 1) + 16; }
+// Per-problem workspace (device carve in hpmpc_kernels.hip): rounded to 256 B, so that every slot of a batch or queue
+// starts on a cache-line boundary and its 16- / 32-double stage vectors stay line-aligned (the certificate's N+1
+// doubles alone would shift each slot by 8 B per stage: +50 % on the element-wise update pass, measured)
+long long ws_doubles(int N) {
+    const long long n = (long long)(N + 1) * (FSTRIDE + 9 * V16 + 8 * V32 + 1) + 16;
+    return (n + 31) / 32 * 32;
+}
 
 }  // namespace
 
@@ -745,9 +751,9 @@ struct Arena {
 Arena arena(const hpmpc_mi355x_plan* P, int k_max) {
     Arena A;
     size_t o = 0;
-    auto take = [&](size_t n) {
+    auto take = [&](size_t n) {  // 128-B granules: every array starts on a cache line
         size_t r = o;
-        o += (n + 7) / 8 * 8;
+        o += (n + 15) / 16 * 16;
         return r;
     };
     const size_t n1 = P->N + 1;

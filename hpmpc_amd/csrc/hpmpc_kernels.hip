@@ -612,18 +612,18 @@ __device__ __forceinline__ void pred_body(const KArgs& a, const LdsTabs& T, IpmV
     const double mu = st[S_MU];
     double sigma = st[S_SIGMA];
     double al = 1.0;
-    MuAcc ma{0.0, 0.0, 0.0};  // mu_aff's three alpha-free sums, accumulated by the sweep (MuAcc)
     // The predictor's multipliers are never read: the corrector's solve overwrites dpi before the
     // update uses it (d_ip2_res_hard.c:527 vs :628 and :948 vs :1168), so the predictor skips them.
     if (phase == 1) {
         v.bc.pred = 1;
-        ric_forward<0, BX_P1, FX, true>(v.io, &sm, nullptr, 0, v.w.dux, 0, v.w.dpi, v.bc, al, &ma);
+        ric_forward<0, BX_P1, FX, true>(v.io, &sm, nullptr, 0, v.w.dux, 0, v.w.dpi, v.bc, al);
     } else {
-        ric_forward<0, BX_P2, FX, true>(v.io, &sm, v.w.res_b, !sn, v.w.dux, 0, v.w.dpi, v.bc, al, &ma);
+        ric_forward<0, BX_P2, FX, true>(v.io, &sm, v.w.res_b, !sn, v.w.dux, 0, v.w.dpi, v.bc, al);
     }
     al = wave_min(al);
+    wsync();
     const double alpha = al * 0.995;
-    const double mu_aff = wave_sum(ma.s0 + alpha * (ma.s1 + alpha * ma.s2)) * st[S_MUSCAL];
+    const double mu_aff = mu_aff_pass<7>(v.io, v.bc, alpha, st[S_MUSCAL]);
     double smu = a.mu0;  // single Newton: sigma*mu is supplied by the caller as mu0 (:1788-1790)
     if (!sn) {
         sigma = mu_aff / mu;
@@ -784,10 +784,8 @@ __global__ __launch_bounds__(64) void hk_ipm_solo(KArgs a) {
 // ------------------------------------------------------------------------------------------------
 // The same solve with one problem per 256-thread workgroup (hk_mw.h): wave 0 runs each sweep's recursion, waves
 // 1..3 everything off it, and the element-wise update is split over the four waves.  Every body keeps the
-// single-wave body's arithmetic (same routines, same operands, mu summed in the same order) except mu_aff, which
-// this kernel forms element-wise after the sweep (mu_aff_pass; the single-wave bodies expand it in alpha, MuAcc),
-// so the iterates agree with hk_ipm_solo's to rounding.  All four waves run every body, so that they meet the same
-// barriers in the same order;
+// single-wave body's arithmetic (same routines, same operands, mu summed in the same order), so the iterates are
+// bitwise hk_ipm_solo's.  All four waves run every body, so that they meet the same barriers in the same order;
 // the loop-control state is read by all and written by thread 0 (IpmView.l = threadIdx.x here).
 // ------------------------------------------------------------------------------------------------
 namespace {
