@@ -270,8 +270,8 @@ __device__ __forceinline__ void stage_chol_row(const d4& S, double invd, double&
 //        componentwise backward error; the reference's own M differs from ours by rounding of the same order), so
 //        with 1e-11 >> 16 n eps as the allowance the certificate is  g (g / e_max - 1e-11) > 1e-15, i.e.
 //        e_max (1e-11 g + 1e-15) < g^2 with g > 0.
-// g depends on the data only: the IPM forms it once per solve (cert_pass, from its init) and its factorisations load
-// it; the Riccati entry points form it per stage (cert_g).  The e_max test is one product and compare per diagonal
+// g depends on the data only: an IPM solve forms it in its first factorisation (from the data tiles that pass loads
+// anyway) and its later factorisations load it; the Riccati entry points form it per stage (cert_g).  The e_max test is one product and compare per diagonal
 // entry and a ballot.
 // ------------------------------------------------------------------------------------------------
 // The tile's diagonal entry held by this lane: lane (g,c) holds element (g+4r, c) of register r, so it holds the
@@ -410,6 +410,23 @@ struct XFac {
     double invd;
 };
 
+// The clamped x-block factorisation of a stage that failed the certificate (stage_chol's xfac branch: 0.25 % of the
+// headline queue's stages), out of line with HK_FALLBACK_CALL: its registers then stay out of the stage loop's
+// allocation (arguments and result travel in VGPRs; only the call itself saves and restores).
+struct XRes {
+    d4 M;
+    double ml;
+};
+template <bool AUG>
+__device__ __attribute__((noinline)) XRes xfac_fallback(d4 M, double ml, double invd, int nx, int xo) {
+    d4 L = M;
+    double lx = ml, ivx = invd;
+    xblocks_chol<AUG>(L, lx, ivx, nx, xo);
+    pform_eff_tile(L, nx, xo, M);
+    if (AUG) pform_eff_row(L, lx, nx, xo, ml);
+    return XRes{M, ml};
+}
+
 // Stage factorisation with the augmented row.
 // In : M (tile, full symmetric), ml (aug row, col layout).
 // full == true : the whole stage Cholesky (d_back_ric_rec.c:325, dsyrk_dpotrf_lib), M = S = lower(L) +
@@ -452,14 +469,23 @@ __device__ __forceinline__ void stage_chol(d4& M, double& ml, double& invd, int 
 #else
     if (!full && xfac) {
 #endif
-        d4 L = M;
-        double lx = ml, ivx = invd;
-        xblocks_chol<AUG>(L, lx, ivx, nx, xo);
-        pform_eff_tile(L, nx, xo, M);
-        if (AUG) pform_eff_row(L, lx, nx, xo, ml);
-        if (xf) {
-            xf->L = L;
-            xf->invd = ivx;
+#ifdef HK_FALLBACK_CALL
+        if (!xf) {
+            const XRes r = xfac_fallback<AUG>(M, ml, invd, nx, xo);
+            M = r.M;
+            ml = r.ml;
+        } else
+#endif
+        {
+            d4 L = M;
+            double lx = ml, ivx = invd;
+            xblocks_chol<AUG>(L, lx, ivx, nx, xo);
+            pform_eff_tile(L, nx, xo, M);
+            if (AUG) pform_eff_row(L, lx, nx, xo, ml);
+            if (xf) {
+                xf->L = L;
+                xf->invd = ivx;
+            }
         }
     }
     if (!transpose) return;
@@ -712,9 +738,12 @@ struct BoxCtx {
     // BX_P2 / BX_P2R: the factorisation skips its t^-1 store (queue API: the solves re-form 1/t from t, and
     // only the KKT re-solve and the general-constraint halves load it; wave-uniform)
     int no_tinv;
-    // the clamp certificate's data part g per stage (cert_pass): read by the IPM's factorisations (BX_P1 / BX_P2 /
-    // BX_P2R), which never form it themselves
+    // the clamp certificate's data part g per stage, for the IPM's factorisations (BX_P1 / BX_P2 / BX_P2R): the first
+    // factorisation of a solve forms it from the data tiles it loads anyway (cert_new, wave-uniform) and stores it to
+    // cert_out; the later ones read it from cert (staged in LDS by fact_body, the workspace in the multi-wave kernel)
     const double* cert;
+    double* cert_out;
+    int cert_new;
 };
 
 struct BoxLane {
@@ -1026,26 +1055,6 @@ __device__ __forceinline__ void load_rsq_tile(const double* R, const SH& sh, d4&
     }
 }
 
-// The certificate's data part g_k of every stage into cert[0..N] (an IPM's init: its factorisations then load it):
-// stages in groups of four, the group's tile loads issued before its math.
-__device__ void cert_pass(const RicIO& io, double* cert) {
-    for (int k0 = 0; k0 <= io.N; k0 += 4) {
-        d4 Mi[4];
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int k = k0 + j <= io.N ? k0 + j : io.N;
-            const DynSh sh(load_stage(io.st, k));
-            load_rsq_tile(stage_R(io, sh), sh, Mi[j]);
-        }
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int k = k0 + j <= io.N ? k0 + j : io.N;
-            const DynSh sh(load_stage(io.st, k));
-            gst(cert, k0 + j, cert_g(Mi[j], sh), lane_id() == 0 && k0 + j <= io.N);
-        }
-    }
-}
-
 template <bool AUG, int BM, class SH>
 __device__ __forceinline__ void bwd_fetch(const RicIO& io, const SH& sh, int k, int update_b, const double* bsrc,
                                           int update_q, const double* qsrc, const BoxCtx& bc, BwdFrag& f) {
@@ -1062,7 +1071,7 @@ __device__ __forceinline__ void bwd_fetch(const RicIO& io, const SH& sh, int k, 
     }
     const BoxLane b = box_lane(io.tileslot, sh.pnb, k);
     f.bl = b;
-    f.gc = cert_loaded(BM) ? bc.cert[k] : 0.0;  // LDS (fact_body) or the workspace (the multi-wave kernel)
+    f.gc = cert_loaded(BM) ? bc.cert[k] : 0.0;  // LDS (fact_body) or the workspace (multi-wave); unused when cert_new
 #pragma unroll
     for (int i = 0; i < 8; i++) f.bx[i] = 0.0;
     if (BM == BX_GIVEN) {
@@ -1211,10 +1220,14 @@ __device__ __forceinline__ void bwd_pre(const RicIO& io, const SH& sh, int k, co
 #ifdef HK_COUNT_NOCERT
     gc = 0.0;
 #else
-    if constexpr (cert_loaded(BM))
-        gc = cur.gc;
-    else
+    if constexpr (cert_loaded(BM)) {
+        // the solve's first factorisation forms g from the tile (stage 0 too: a later one may be a P-form stage of
+        // another plan shape) and keeps it for the others; masked store otherwise (fixed vector-memory count)
+        gc = bc.cert_new ? cert_g(cur.Mi, sh) : cur.gc;
+        gst(bc.cert_out, k, gc, bc.cert_new && lane_id() == 0);
+    } else {
         gc = (SH::fixed || k > 0) ? cert_g(cur.Mi, sh) : 0.0;
+    }
 #endif
     M = cur.Mi;
     ml = cur.mlq + qxv;  // update_q row (or RSQrq row) + drowad qx

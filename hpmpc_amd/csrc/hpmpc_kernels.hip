@@ -326,6 +326,8 @@ __device__ __forceinline__ BoxCtx box_ctx(const Ws& w, const double* dv, double*
     bc.Qx = w.Qx;
     bc.qx = w.qx;
     bc.cert = w.cert;
+    bc.cert_out = w.cert;
+    bc.cert_new = 0;
     bc.res_q = w.res_q;
     bc.res_b = w.res_b;
     return bc;
@@ -524,8 +526,6 @@ __device__ bool ipm_start(const KArgs& a, const LdsTabs& T, IpmView& v) {
     // single Newton step (d_ip2_res_hard.c:1348-1919): the caller's ux/pi/lam/t already hold the start
     // iterate (d_init_var_mpc_hard_tv_single_newton is a copy, done by the host), no phase 1.
     const bool sn = a.single_newton != 0;
-    // the clamp certificate's data part of every stage, once per solve (its factorisations load it)
-    cert_pass(v.io, v.w.cert);
     if (!sn) {
         init_var<CI>(v.io, v.dv, v.ux, v.pi, v.w.dpi, v.lam, v.t, a.mu0, a.warm_start);
         if (a.ngt) {
@@ -588,9 +588,11 @@ __device__ __forceinline__ void fact_body(const KArgs& a, const LdsTabs& T, IpmV
     Scratch& sm = *T.sm;
     const double* st = v.w.state;
     const bool sn = a.single_newton != 0;
-    // the certificate bounds of the solve (cert_pass) into LDS: the stage loop reads them with ds_read instead of
-    // holding one more buffer descriptor in SGPRs
-    for (int i = v.l; i <= v.N; i += 64) T.gc[i] = v.w.cert[i];
+    // the certificate bounds of the solve into LDS (the stage loop reads them with ds_read instead of holding one more
+    // buffer descriptor in SGPRs), except in the solve's first factorisation, which forms them (BoxCtx.cert_new)
+    v.bc.cert_new = st[S_KK] == 0.0;
+    if (!v.bc.cert_new)
+        for (int i = v.l; i <= v.N; i += 64) T.gc[i] = v.w.cert[i];
     wsync();
     v.bc.cert = T.gc;
     if (st[S_PHASE] == 1.0)
@@ -794,6 +796,7 @@ template <class FX>
 __device__ __forceinline__ void fact_body_mw(const KArgs& a, IpmView& v, int& tb, int w) {
     const double* st = v.w.state;
     const bool sn = a.single_newton != 0;
+    v.bc.cert_new = st[S_KK] == 0.0;  // the helpers form the certificate bounds in the solve's first factorisation
     if (st[S_PHASE] == 1.0)
         tb = ric_backward_mw<true, BX_P1, FX>(v.io, tb, w, 0, nullptr, 0, nullptr, v.bc, 1, v.w.Pb);
     else {
