@@ -327,7 +327,9 @@ __device__ __forceinline__ double cert_g(const d4& Mi, const SH& sh) {
 }
 
 #ifdef HK_STAMPS
-__device__ unsigned long long g_xfac_stat[4];  // P-form stages tested, failed at CERT_ALLOW, at 1e-12, at 1e-13
+// P-form stages tested, failed at CERT_ALLOW, at 1e-12, at 1e-13; backward sweeps, sweeps with a failed stage
+__device__ unsigned long long g_xfac_stat[6];
+__device__ unsigned g_xfac_sweep[1 << 16];  // per workgroup: this sweep has failed a stage (one wave per workgroup)
 #endif
 constexpr double CERT_ALLOW = 1e-11;  // the backward-error allowance (>> 16 n eps, n = 16)
 
@@ -410,23 +412,6 @@ struct XFac {
     double invd;
 };
 
-// The clamped x-block factorisation of a stage that failed the certificate (stage_chol's xfac branch: 0.25 % of the
-// headline queue's stages), out of line with HK_FALLBACK_CALL: its registers then stay out of the stage loop's
-// allocation (arguments and result travel in VGPRs; only the call itself saves and restores).
-struct XRes {
-    d4 M;
-    double ml;
-};
-template <bool AUG>
-__device__ __attribute__((noinline)) XRes xfac_fallback(d4 M, double ml, double invd, int nx, int xo) {
-    d4 L = M;
-    double lx = ml, ivx = invd;
-    xblocks_chol<AUG>(L, lx, ivx, nx, xo);
-    pform_eff_tile(L, nx, xo, M);
-    if (AUG) pform_eff_row(L, lx, nx, xo, ml);
-    return XRes{M, ml};
-}
-
 // Stage factorisation with the augmented row.
 // In : M (tile, full symmetric), ml (aug row, col layout).
 // full == true : the whole stage Cholesky (d_back_ric_rec.c:325, dsyrk_dpotrf_lib), M = S = lower(L) +
@@ -469,23 +454,14 @@ __device__ __forceinline__ void stage_chol(d4& M, double& ml, double& invd, int 
 #else
     if (!full && xfac) {
 #endif
-#ifdef HK_FALLBACK_CALL
-        if (!xf) {
-            const XRes r = xfac_fallback<AUG>(M, ml, invd, nx, xo);
-            M = r.M;
-            ml = r.ml;
-        } else
-#endif
-        {
-            d4 L = M;
-            double lx = ml, ivx = invd;
-            xblocks_chol<AUG>(L, lx, ivx, nx, xo);
-            pform_eff_tile(L, nx, xo, M);
-            if (AUG) pform_eff_row(L, lx, nx, xo, ml);
-            if (xf) {
-                xf->L = L;
-                xf->invd = ivx;
-            }
+        d4 L = M;
+        double lx = ml, ivx = invd;
+        xblocks_chol<AUG>(L, lx, ivx, nx, xo);
+        pform_eff_tile(L, nx, xo, M);
+        if (AUG) pform_eff_row(L, lx, nx, xo, ml);
+        if (xf) {
+            xf->L = L;
+            xf->invd = ivx;
         }
     }
     if (!transpose) return;
@@ -1055,6 +1031,26 @@ __device__ __forceinline__ void load_rsq_tile(const double* R, const SH& sh, d4&
     }
 }
 
+// The certificate's data part g_k of every stage into cert[0..N], as its own pass (stages in groups of eight, the
+// group's tile loads issued before its math): the single-Newton start, whose first factorisation is a phase-2 one.
+__device__ void cert_pass(const RicIO& io, double* cert) {
+    for (int k0 = 0; k0 <= io.N; k0 += 8) {
+        d4 Mi[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int k = k0 + j <= io.N ? k0 + j : io.N;
+            const DynSh sh(StageRef{io.st, k});
+            load_rsq_tile(stage_R(io, sh), sh, Mi[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int k = k0 + j <= io.N ? k0 + j : io.N;
+            const DynSh sh(StageRef{io.st, k});
+            gst(cert, k0 + j, cert_g(Mi[j], sh), lane_id() == 0 && k0 + j <= io.N);
+        }
+    }
+}
+
 template <bool AUG, int BM, class SH>
 __device__ __forceinline__ void bwd_fetch(const RicIO& io, const SH& sh, int k, int update_b, const double* bsrc,
                                           int update_q, const double* qsrc, const BoxCtx& bc, BwdFrag& f) {
@@ -1211,7 +1207,12 @@ __device__ __forceinline__ void bwd_residual(const RicIO& io, Scratch* sm, const
 // on a helper wave, hk_mw.h).
 // dq (col layout): the box term on the diagonal; gc: the stage's clamp-certificate bound g (cert_g: loaded in the
 // IPM's box modes, formed from the data tile otherwise; unused on a stage that is fully factorised).
-template <bool AUG, int BM, class SH>
+// CN (IPM box modes): how the stage's certificate bound g is had -- CERT_LOAD: from bc.cert (a later factorisation
+// of the solve); CERT_FORM: formed from the data tile and stored to bc.cert_out (the solve's first factorisation);
+// CERT_RT: either, by bc.cert_new at run time (the multi-wave kernel's helpers, which have the issue slots to spare).
+// The pass kernels pick CERT_LOAD or CERT_FORM once per launch, so neither stage loop carries the other's code.
+enum CertMode { CERT_LOAD = 0, CERT_FORM = 1, CERT_RT = 2 };
+template <bool AUG, int BM, int CN = CERT_RT, class SH>
 __device__ __forceinline__ void bwd_pre(const RicIO& io, const SH& sh, int k, const BwdFrag& cur, const BoxCtx& bc,
                                         d4& M, double& ml, double& dq, double& gc) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
@@ -1223,8 +1224,15 @@ __device__ __forceinline__ void bwd_pre(const RicIO& io, const SH& sh, int k, co
     if constexpr (cert_loaded(BM)) {
         // the solve's first factorisation forms g from the tile (stage 0 too: a later one may be a P-form stage of
         // another plan shape) and keeps it for the others; masked store otherwise (fixed vector-memory count)
-        gc = bc.cert_new ? cert_g(cur.Mi, sh) : cur.gc;
-        gst(bc.cert_out, k, gc, bc.cert_new && lane_id() == 0);
+        if constexpr (CN == CERT_LOAD) {
+            gc = cur.gc;
+        } else if constexpr (CN == CERT_FORM) {
+            gc = cert_g(cur.Mi, sh);
+            gst(bc.cert_out, k, gc, lane_id() == 0);
+        } else {
+            gc = bc.cert_new ? cert_g(cur.Mi, sh) : cur.gc;
+            gst(bc.cert_out, k, gc, bc.cert_new && lane_id() == 0);
+        }
     } else {
         gc = (SH::fixed || k > 0) ? cert_g(cur.Mi, sh) : 0.0;
     }
@@ -1321,6 +1329,7 @@ __device__ __forceinline__ void bwd_core(const RicIO& io, Scratch* sm, const SH&
         if (lane_id() == 0) {
             atomicAdd(&g_xfac_stat[0], 1ull);
             if (xfac) atomicAdd(&g_xfac_stat[1], 1ull);
+            if (xfac) g_xfac_sweep[blockIdx.x & 0xffff] = 1u;
             if (f12) atomicAdd(&g_xfac_stat[2], 1ull);
             if (f13) atomicAdd(&g_xfac_stat[3], 1ull);
         }
@@ -1342,13 +1351,13 @@ __device__ __forceinline__ void bwd_core(const RicIO& io, Scratch* sm, const SH&
 // stages k >= 1, see stage_chol).  S (in: record of stage k+1, whose x block is P_{k+1}; out: record of
 // stage k), ml/invd/kg likewise.  The reference forms the same M as RSQ + W W' with W = BAbt Lxx
 // (dtrmm_nt_u + dsyrk, d_back_ric_rec.c:262-264, :325) and the same row as W (Lxx' b + l_x) (:266-276).
-template <bool AUG, int BM, class SH>
+template <bool AUG, int BM, int CN, class SH>
 __device__ __forceinline__ void bwd_step(const RicIO& io, Scratch* sm, const SH& sh, int k, const BwdFrag& cur,
                                          const BoxCtx& bc, int compute_Pb, double* Pb, d4& S, double& ml_prev,
                                          double& invd_prev, double& kg_prev) {
     d4 M;
     double ml, dq, gc;
-    bwd_pre<AUG, BM>(io, sh, k, cur, bc, M, ml, dq, gc);
+    bwd_pre<AUG, BM, CN>(io, sh, k, cur, bc, M, ml, dq, gc);
     bwd_core<AUG>(io, sm, sh, k, cur.bop, cur.brow, M, ml, dq, gc, compute_Pb, Pb, S, ml_prev, invd_prev, kg_prev);
 }
 
@@ -1357,11 +1366,14 @@ __device__ __forceinline__ void bwd_step(const RicIO& io, Scratch* sm, const SH&
 //   BM                                    : box Hessian / gradient terms (BoxMode)
 //   Pb (state order)                      : P_{k+1} b_k (compute_Pb, AUG only)
 // Vector arguments use a per-stage stride of V16.
-template <bool AUG, int BM, class FX>
+template <bool AUG, int BM, class FX, int CN = CERT_LOAD>
 __device__ void ric_backward(const RicIO& io, Scratch* sm, int update_b, const double* bsrc, int update_q,
                              const double* qsrc, const BoxCtx& bc, int compute_Pb, double* Pb) {
     d4 S = {0.0, 0.0, 0.0, 0.0};
     double ml_prev = 0.0, invd_prev = 0.0, kg_prev = 0.0;
+#ifdef HK_STAMPS
+    if (lane_id() == 0) g_xfac_sweep[blockIdx.x & 0xffff] = 0u;
+#endif
     StageRef si{io.st, io.N};
     BwdFrag cur;
     with_shape<FX>(si, [&](const auto& sh) {
@@ -1392,7 +1404,7 @@ __device__ void ric_backward(const RicIO& io, Scratch* sm, int update_b, const d
         asm volatile("" ::: "memory");  // keep those stores here, ahead of this stage's math
         HK_STAMP(1, k);
         with_shape<FX>(si, [&](const auto& sh) {
-            bwd_step<AUG, BM>(io, sm, sh, k, cur, bc, compute_Pb, Pb, S, ml_prev, invd_prev, kg_prev);
+            bwd_step<AUG, BM, CN>(io, sm, sh, k, cur, bc, compute_Pb, Pb, S, ml_prev, invd_prev, kg_prev);
             rec_fixed = std::remove_reference_t<decltype(sh)>::fixed;
         });
         if constexpr (BM == BX_P2R)
@@ -1408,6 +1420,12 @@ __device__ void ric_backward(const RicIO& io, Scratch* sm, int update_b, const d
         if (--k < 0) break;
     }
     store_factor(io.F, S, AUG ? ml_prev : 0.0, invd_prev, kg_prev);
+#ifdef HK_STAMPS
+    if (lane_id() == 0) {
+        atomicAdd(&g_xfac_stat[4], 1ull);
+        if (g_xfac_sweep[blockIdx.x & 0xffff]) atomicAdd(&g_xfac_stat[5], 1ull);
+    }
+#endif
 }
 
 // ------------------------------------------------------------------------------------------------

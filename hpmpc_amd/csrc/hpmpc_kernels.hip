@@ -588,19 +588,28 @@ __device__ __forceinline__ void fact_body(const KArgs& a, const LdsTabs& T, IpmV
     Scratch& sm = *T.sm;
     const double* st = v.w.state;
     const bool sn = a.single_newton != 0;
-    // the certificate bounds of the solve into LDS (the stage loop reads them with ds_read instead of holding one more
-    // buffer descriptor in SGPRs), except in the solve's first factorisation, which forms them (BoxCtx.cert_new)
-    v.bc.cert_new = st[S_KK] == 0.0;
-    if (!v.bc.cert_new)
+    // The clamp certificate's bounds: the solve's first factorisation forms them from the data tiles it loads anyway
+    // (CERT_FORM: a phase-1 one, except in the single-Newton variant, which starts in phase 2 and runs the bounds'
+    // own pass first); the later ones read them, staged in LDS (ds_read in the stage loop instead of one more buffer
+    // descriptor in SGPRs).
+    const bool first = st[S_KK] == 0.0;
+    if (first && st[S_PHASE] != 1.0) {
+        cert_pass(v.io, v.w.cert);
+        wsync();
+    }
+    if (!first || st[S_PHASE] != 1.0)
         for (int i = v.l; i <= v.N; i += 64) T.gc[i] = v.w.cert[i];
     wsync();
     v.bc.cert = T.gc;
-    if (st[S_PHASE] == 1.0)
-        ric_backward<true, BX_P1, FX>(v.io, &sm, 0, nullptr, 0, nullptr, v.bc, 1, v.w.Pb);
-    else {  // the single-Newton variant factorises with the data's own b/q rows (d_ip2_res_hard.c:1700-1760)
+    if (st[S_PHASE] == 1.0) {
+        if (first)
+            ric_backward<true, BX_P1, FX, CERT_FORM>(v.io, &sm, 0, nullptr, 0, nullptr, v.bc, 1, v.w.Pb);
+        else
+            ric_backward<true, BX_P1, FX, CERT_LOAD>(v.io, &sm, 0, nullptr, 0, nullptr, v.bc, 1, v.w.Pb);
+    } else {  // the single-Newton variant factorises with the data's own b/q rows (d_ip2_res_hard.c:1700-1760)
         v.bc.res_rhs = !sn;
         v.bc.no_tinv = a.no_bkp;
-        ric_backward<true, BX_P2R, FX>(v.io, &sm, 0, nullptr, 0, nullptr, v.bc, 1, v.w.Pb);
+        ric_backward<true, BX_P2R, FX, CERT_LOAD>(v.io, &sm, 0, nullptr, 0, nullptr, v.bc, 1, v.w.Pb);
     }
 }
 
@@ -1207,9 +1216,9 @@ extern "C" int hk_fixcls(int nu, int nx) {
 #ifdef HK_STAMPS
 // Diagnostic build only: the clamp-certificate counters of the tile kernels (g_xfac_stat), read and optionally reset.
 extern "C" __attribute__((visibility("default"))) int hpmpc_mi355x_diag_xfac(unsigned long long* out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_xfac_stat), 4 * sizeof(unsigned long long)) != hipSuccess) return -11;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_xfac_stat), 6 * sizeof(unsigned long long)) != hipSuccess) return -11;
     if (reset) {
-        const unsigned long long z[4] = {0, 0, 0, 0};
+        const unsigned long long z[6] = {0, 0, 0, 0, 0, 0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_xfac_stat), z, sizeof(z)) != hipSuccess) return -11;
     }
     return 0;

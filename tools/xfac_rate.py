@@ -1,7 +1,8 @@
 """How often the P form's clamp certificate fails (hk_riccati.h cert_ok) on the benchmark workload: the headline
 queue (N=100 nx=12 nu=4, 1024 problems, the IPM end game included) and the Riccati sv, through the diagnostic build
 (libhpmpc_mi355x_stamps.so, HK_STAMPS counters: P-form stages tested / failed at the build's allowance 1e-11 and at
-1e-12, 1e-13).  Run with HPMPC_MI355X_LIB pointing at the stamps build."""
+1e-12, 1e-13; backward sweeps and the sweeps with at least one failed stage).  Run with HPMPC_MI355X_LIB pointing
+at the stamps build."""
 import ctypes as C
 import json
 import os
@@ -16,7 +17,7 @@ from hpmpc_amd.shard import make_shard  # noqa: E402
 lib = C.CDLL(LIBPATH)
 f = lib.hpmpc_mi355x_diag_xfac
 f.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
-buf = (C.c_ulonglong * 4)()
+buf = (C.c_ulonglong * 6)()
 
 
 def stat(reset=True):
@@ -33,10 +34,11 @@ Q = s.queue(4 * 1024, 2048)
 Q.run()
 st = stat()
 out["ipm_queue_4x1024"] = {"stages": st[0], "fail_1e-11": st[1], "fail_1e-12": st[2], "fail_1e-13": st[3],
-                           "sum_kk": int(Q.kk.sum().item())}
+                           "sweeps": st[4], "sweeps_with_fail": st[5], "sum_kk": int(Q.kk.sum().item())}
 qr = make_shard(100, 12, 4, 0, 1, 1024, boxes=False)
 r = BatchSolver(qr, k_max=1)
 r.ric_sv()
 st = stat()
-out["riccati_sv_1024"] = {"stages": st[0], "fail_1e-11": st[1], "fail_1e-12": st[2], "fail_1e-13": st[3]}
+out["riccati_sv_1024"] = {"stages": st[0], "fail_1e-11": st[1], "fail_1e-12": st[2], "fail_1e-13": st[3],
+                          "sweeps": st[4], "sweeps_with_fail": st[5]}
 print(json.dumps(out))
