@@ -177,6 +177,7 @@ template <bool AUG, int BM, class FX>
 __device__ __forceinline__ int ric_backward_mw(const RicIO& io, int tb, int w, int update_b, const double* bsrc,
                                                int update_q, const double* qsrc, const BoxCtx& bc, int compute_Pb,
                                                double* Pb) {
+    static_assert(cert_loaded(BM), "the tile wave tests the certificate in threshold form (the IPM's box modes)");
     const int N = io.N, l = lane_id(), c = l & 15;
     Scratch* sm = &hk_mw.sm[w];
     if (w >= 2) {
@@ -292,7 +293,7 @@ __device__ __forceinline__ int ric_backward_mw(const RicIO& io, int tb, int w, i
                 MW_SEG(1);
                 double mld = 0.0;
                 const bool full = !SHT::fixed && k == 0;
-                xfac = !full && !cert_ok(M, dq, gc);
+                xfac = !full && !cert_ok_thr(M, dq, gc, cert_diag_w());  // gc: the threshold T (IPM modes)
                 stage_chol<false, false>(M, mld, invd, sh.nu, sh.nx, sh.xo, full, !SHT::fixed, nullptr, k, xfac, &xf);
                 MW_SEG(2);
             });

@@ -343,6 +343,28 @@ __device__ __forceinline__ bool cert_ok(const d4& M, double dq, double gc, doubl
     return __builtin_amdgcn_ballot_w64(bad) == 0;
 }
 
+// The same test in threshold form, for the IPM's factorisations, whose bounds are formed once per solve: the stage
+// stores T = g^2 / (1e-11 g + 1e-15) (cert_thr; -inf when g <= 0, rounded down by 2^-40 so that e < T implies the
+// division-free test above), and the test is max_i (M_ii - dq_i) < T.  The diagonal entry comes from per-lane 0/1
+// weights (cert_diag_w, loop-invariant VGPRs) instead of lane-mask selects: no SGPR mask stays live across the
+// stage loop, and lanes without a diagonal entry test -dq_c < T, which holds whenever the stage can pass at all.
+// (dq >= 0 in these modes: it is a sum of lam / t terms.)
+__device__ __forceinline__ double cert_thr(double g) {
+    const double T = (g * g) * rcp_nr(fma(CERT_ALLOW, g, 1e-15)) * (1.0 - 0x1p-40);
+    return g > 0.0 ? T : -__builtin_inf();
+}
+__device__ __forceinline__ d4 cert_diag_w() {
+    const int l = lane_id(), g = l >> 4, c = l & 15;
+    d4 w;
+#pragma unroll
+    for (int r = 0; r < 4; r++) w[r] = (c == g + 4 * r) ? 1.0 : 0.0;
+    return w;
+}
+__device__ __forceinline__ bool cert_ok_thr(const d4& M, double dq, double T, const d4& w) {
+    const double d = w[0] * M[0] + w[1] * M[1] + w[2] * M[2] + w[3] * M[3];
+    return __builtin_amdgcn_ballot_w64(!(d - dq < T)) == 0;
+}
+
 // l[4R + g] (row layout of a col-layout vector over tile block R): the pivot entries of block R
 template <int R>
 __device__ __forceinline__ double lrow_blk(double v) {
@@ -1046,7 +1068,7 @@ __device__ void cert_pass(const RicIO& io, double* cert) {
         for (int j = 0; j < 8; j++) {
             const int k = k0 + j <= io.N ? k0 + j : io.N;
             const DynSh sh(StageRef{io.st, k});
-            gst(cert, k0 + j, cert_g(Mi[j], sh), lane_id() == 0 && k0 + j <= io.N);
+            gst(cert, k0 + j, cert_thr(cert_g(Mi[j], sh)), lane_id() == 0 && k0 + j <= io.N);
         }
     }
 }
@@ -1224,13 +1246,14 @@ __device__ __forceinline__ void bwd_pre(const RicIO& io, const SH& sh, int k, co
     if constexpr (cert_loaded(BM)) {
         // the solve's first factorisation forms g from the tile (stage 0 too: a later one may be a P-form stage of
         // another plan shape) and keeps it for the others; masked store otherwise (fixed vector-memory count)
+        // gc carries the threshold T (cert_thr) in these modes
         if constexpr (CN == CERT_LOAD) {
             gc = cur.gc;
         } else if constexpr (CN == CERT_FORM) {
-            gc = cert_g(cur.Mi, sh);
+            gc = cert_thr(cert_g(cur.Mi, sh));
             gst(bc.cert_out, k, gc, lane_id() == 0);
         } else {
-            gc = bc.cert_new ? cert_g(cur.Mi, sh) : cur.gc;
+            gc = bc.cert_new ? cert_thr(cert_g(cur.Mi, sh)) : cur.gc;
             gst(bc.cert_out, k, gc, bc.cert_new && lane_id() == 0);
         }
     } else {
@@ -1307,7 +1330,8 @@ __device__ __forceinline__ void bwd_row_update(const RicIO& io, Scratch* sm, con
 }
 
 // Second half: M += BAbt P BAbt', the row update and the stage factorisation (the recursion's chain).
-template <bool AUG, class SH>
+// THR: gc is the certificate threshold T of the IPM's modes (cert_ok_thr), else the bound g (cert_ok).
+template <bool AUG, bool THR, class SH>
 __device__ __forceinline__ void bwd_core(const RicIO& io, Scratch* sm, const SH& sh, int k, const d4& bop,
                                          const d4& brow, d4 M, double ml, double dq, double gc, int compute_Pb,
                                          double* Pb, d4& S, double& ml_prev, double& invd_prev, double& kg_prev) {
@@ -1321,11 +1345,16 @@ __device__ __forceinline__ void bwd_core(const RicIO& io, Scratch* sm, const SH&
     (void)dq;
     (void)gc;
 #else
-    const bool xfac = !full && !cert_ok(M, dq, gc);
+    bool xfac;
+    if constexpr (THR)
+        xfac = !full && !cert_ok_thr(M, dq, gc, cert_diag_w());
+    else
+        xfac = !full && !cert_ok(M, dq, gc);
 #endif
-#ifdef HK_STAMPS  // diagnostic build: how often the certificate fails, at this allowance and at 10x / 100x smaller ones
+#ifdef HK_STAMPS  // diagnostic build: how often the certificate fails, at this allowance and (with g) at 10x / 100x
+    // smaller ones -- the threshold form only knows its own allowance, so those two count its failures
     if (!full) {
-        const bool f12 = !cert_ok(M, dq, gc, 1e-12), f13 = !cert_ok(M, dq, gc, 1e-13);
+        const bool f12 = THR ? xfac : !cert_ok(M, dq, gc, 1e-12), f13 = THR ? xfac : !cert_ok(M, dq, gc, 1e-13);
         if (lane_id() == 0) {
             atomicAdd(&g_xfac_stat[0], 1ull);
             if (xfac) atomicAdd(&g_xfac_stat[1], 1ull);
@@ -1358,7 +1387,7 @@ __device__ __forceinline__ void bwd_step(const RicIO& io, Scratch* sm, const SH&
     d4 M;
     double ml, dq, gc;
     bwd_pre<AUG, BM, CN>(io, sh, k, cur, bc, M, ml, dq, gc);
-    bwd_core<AUG>(io, sm, sh, k, cur.bop, cur.brow, M, ml, dq, gc, compute_Pb, Pb, S, ml_prev, invd_prev, kg_prev);
+    bwd_core<AUG, cert_loaded(BM)>(io, sm, sh, k, cur.bop, cur.brow, M, ml, dq, gc, compute_Pb, Pb, S, ml_prev, invd_prev, kg_prev);
 }
 
 // Backward Riccati recursion (sv when AUG, trf otherwise), d_back_ric_rec.c:186-335 / :447-558.
