@@ -79,6 +79,14 @@ __device__ __forceinline__ int mw_flag(const int* f) { return __atomic_load_n(f,
 // before every post, which also waits for the poster's unrelated scalar loads: a same-box A/B measured 350.4 vs
 // 367.1-367.5 us per lone-QP IP iteration (3 pairs, profiles/r04/ab_latency.txt), 4.7 %, above the 2 % the fenced
 // form was allowed, so it is a build option (tools/gpu_ab.sh variants) and not the default.
+// HK_MW_NOINLINE: each sweep of the multi-wave kernel as its own (out-of-line) function, so that the register
+// allocator sees one sweep's roles at a time instead of the whole solve (experiment: SGPR spills of hk_ipm_solo_mw).
+#ifdef HK_MW_NOINLINE
+#define HK_MW_SWEEP __device__ __attribute__((noinline))
+#else
+#define HK_MW_SWEEP __device__ __forceinline__
+#endif
+
 #ifndef HK_MW_FENCE
 #define HK_MW_FENCE 0
 #endif
@@ -174,7 +182,7 @@ __device__ __forceinline__ double mw_get(int j, int i) { return hk_mw.ring[j % M
 constexpr int MW_BHELP = 2;
 
 template <bool AUG, int BM, class FX>
-__device__ __forceinline__ int ric_backward_mw(const RicIO& io, int tb, int w, int update_b, const double* bsrc,
+HK_MW_SWEEP int ric_backward_mw(const RicIO& io, int tb, int w, int update_b, const double* bsrc,
                                                int update_q, const double* qsrc, const BoxCtx& bc, int compute_Pb,
                                                double* Pb) {
     static_assert(cert_loaded(BM), "the tile wave tests the certificate in threshold form (the IPM's box modes)");
@@ -460,7 +468,7 @@ __device__ __forceinline__ void fwd_chain(Scratch* sm, const SH& sh, int k, cons
 }
 
 template <int MODE, int FM, class FX, bool PRED = false>
-__device__ __forceinline__ int ric_forward_mw(const RicIO& io, int tb, int w, const double* bsrc, int use_bsrc,
+HK_MW_SWEEP int ric_forward_mw(const RicIO& io, int tb, int w, const double* bsrc, int use_bsrc,
                                double* ux, int compute_pi_, double* pi, const BoxCtx& bc, double& al_out) {
     const int N = io.N, l = lane_id(), g = l >> 4, c = l & 15;
     const int compute_pi = PRED ? 0 : compute_pi_;
@@ -568,7 +576,7 @@ __device__ __forceinline__ int ric_forward_mw(const RicIO& io, int tb, int w, co
 // slot = [q + box gradient | bop (4) | S (4) | invd | Pb].
 // ------------------------------------------------------------------------------------------------
 template <int TM, int FM, class FX>
-__device__ __forceinline__ int ric_trs_mw(const RicIO& io, int tb, int w, const double* hb, const double* hq,
+HK_MW_SWEEP int ric_trs_mw(const RicIO& io, int tb, int w, const double* hb, const double* hq,
                            const BoxCtx& bc, double* ux, int compute_pi, double* pi, double* Pb, double& al) {
     const int N = io.N, l = lane_id(), g = l >> 4, c = l & 15;
     Scratch* sm = &hk_mw.sm[w];
