@@ -1395,9 +1395,13 @@ __device__ __forceinline__ void bwd_step(const RicIO& io, Scratch* sm, const SH&
 //   BM                                    : box Hessian / gradient terms (BoxMode)
 //   Pb (state order)                      : P_{k+1} b_k (compute_Pb, AUG only)
 // Vector arguments use a per-stage stride of V16.
-template <bool AUG, int BM, class FX, int CN = CERT_LOAD>
+// PD: prefetch depth in stages.  2 (stage k-2's fragment in flight while stage k runs) for the Riccati entry points,
+// which run one wave per SIMD at the benchmark batches and wait on memory for over half of their cycles; the IPM
+// passes (two waves per SIMD, ~200 VGPRs) keep 1 -- a third fragment would push them past 256 VGPRs.
+template <bool AUG, int BM, class FX, int CN = CERT_LOAD, int PD = 1>
 __device__ void ric_backward(const RicIO& io, Scratch* sm, int update_b, const double* bsrc, int update_q,
                              const double* qsrc, const BoxCtx& bc, int compute_Pb, double* Pb) {
+    static_assert(PD == 1 || (PD == 2 && BM != BX_P2R), "depth 2 is for the Riccati entry points");
     d4 S = {0.0, 0.0, 0.0, 0.0};
     double ml_prev = 0.0, invd_prev = 0.0, kg_prev = 0.0;
 #ifdef HK_STAMPS
@@ -1441,12 +1445,52 @@ __device__ void ric_backward(const RicIO& io, Scratch* sm, int update_b, const d
         HK_STAMP(4, k);
         si = sn;
     };
-    BwdFrag alt;
-    for (int k = io.N;;) {
-        stage(k, cur, alt);
-        if (--k < 0) break;
-        stage(k, alt, cur);
-        if (--k < 0) break;
+    if constexpr (PD == 1) {
+        BwdFrag alt;
+        for (int k = io.N;;) {
+            stage(k, cur, alt);
+            if (--k < 0) break;
+            stage(k, alt, cur);
+            if (--k < 0) break;
+        }
+    } else {
+        // depth 2: fragments rotate over three registers sets; stage k runs on fa with stage k-1's fragment (fb)
+        // already in flight and fetches stage k-2 into fc (clamped at 0: the last passes re-read stage 0)
+        auto stage2 = [&](int k, const BwdFrag& fa, BwdFrag& fc) __attribute__((always_inline)) {
+            HK_STAMP(0, k);
+            const int kn = k > 1 ? k - 2 : 0;
+            with_shape<FX>(StageRef{io.st, kn},
+                           [&](const auto& sh) { bwd_fetch<AUG, BM>(io, sh, kn, update_b, bsrc, update_q, qsrc, bc, fc); });
+            double* Fk1 = io.F + (long)(k + 1) * FSTRIDE;
+            if constexpr (FX::enabled) {
+                if (rec_fixed)
+                    store_factor_fixed<FX::nx>(Fk1, S, AUG ? ml_prev : 0.0, invd_prev, kg_prev, k < io.N);
+                else
+                    store_factor(Fk1, S, AUG ? ml_prev : 0.0, invd_prev, kg_prev, k < io.N);
+            } else {
+                store_factor(Fk1, S, AUG ? ml_prev : 0.0, invd_prev, kg_prev, k < io.N);
+            }
+            asm volatile("" ::: "memory");
+            with_shape<FX>(StageRef{io.st, k}, [&](const auto& sh) {
+                bwd_step<AUG, BM, CN>(io, sm, sh, k, fa, bc, compute_Pb, Pb, S, ml_prev, invd_prev, kg_prev);
+                rec_fixed = std::remove_reference_t<decltype(sh)>::fixed;
+            });
+            HK_STAMP(4, k);
+        };
+        BwdFrag f1, f2;
+        {
+            const int k1 = io.N > 0 ? io.N - 1 : 0;
+            with_shape<FX>(StageRef{io.st, k1},
+                           [&](const auto& sh) { bwd_fetch<AUG, BM>(io, sh, k1, update_b, bsrc, update_q, qsrc, bc, f1); });
+        }
+        for (int k = io.N;;) {
+            stage2(k, cur, f2);
+            if (--k < 0) break;
+            stage2(k, f1, cur);
+            if (--k < 0) break;
+            stage2(k, f2, f1);
+            if (--k < 0) break;
+        }
     }
     store_factor(io.F, S, AUG ? ml_prev : 0.0, invd_prev, kg_prev);
 #ifdef HK_STAMPS

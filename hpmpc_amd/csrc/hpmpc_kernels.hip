@@ -120,6 +120,10 @@ __device__ __forceinline__ void wsync() { __syncthreads(); }
 // ------------------------------------------------------------------------------------------------
 // d_back_ric_rec_sv_tv_res / _trf_ / _trs_ over a batch (one problem per workgroup)
 // ------------------------------------------------------------------------------------------------
+// Prefetch depth of the Riccati entry points' backward sweep (ric_backward PD; HK_RIC_PD=1 for an A/B)
+#ifndef HK_RIC_PD
+#define HK_RIC_PD 2
+#endif
 template <class FX>
 __global__ __launch_bounds__(64) void hk_ric_sv(KArgs a) {
     const LdsTabs T = lds_tables(a);
@@ -136,9 +140,9 @@ __global__ __launch_bounds__(64) void hk_ric_sv(KArgs a) {
     bc.qx = a.vqx ? a.vqx + o16 : nullptr;
     double* Pb = a.vPb ? a.vPb + o16 : nullptr;
     if (a.use_box)
-        ric_backward<true, BX_GIVEN, FX>(io, &sm, a.update_b, b, a.update_q, q, bc, a.compute_Pb, Pb);
+        ric_backward<true, BX_GIVEN, FX, CERT_LOAD, HK_RIC_PD>(io, &sm, a.update_b, b, a.update_q, q, bc, a.compute_Pb, Pb);
     else
-        ric_backward<true, BX_NONE, FX>(io, &sm, a.update_b, b, a.update_q, q, bc, a.compute_Pb, Pb);
+        ric_backward<true, BX_NONE, FX, CERT_LOAD, HK_RIC_PD>(io, &sm, a.update_b, b, a.update_q, q, bc, a.compute_Pb, Pb);
     wsync();
     ric_forward_sv<FX>(io, &sm, a.update_b, b, a.ux + o16, a.compute_pi, a.pi + o16);
 }
@@ -155,9 +159,9 @@ __global__ __launch_bounds__(64) void hk_ric_trf(KArgs a) {
     BoxCtx bc{};
     bc.Qx = a.vQx ? a.vQx + o16 : nullptr;
     if (a.use_box)
-        ric_backward<false, BX_GIVEN, FX>(io, &sm, 0, nullptr, 0, nullptr, bc, 0, nullptr);
+        ric_backward<false, BX_GIVEN, FX, CERT_LOAD, HK_RIC_PD>(io, &sm, 0, nullptr, 0, nullptr, bc, 0, nullptr);
     else
-        ric_backward<false, BX_NONE, FX>(io, &sm, 0, nullptr, 0, nullptr, bc, 0, nullptr);
+        ric_backward<false, BX_NONE, FX, CERT_LOAD, HK_RIC_PD>(io, &sm, 0, nullptr, 0, nullptr, bc, 0, nullptr);
 }
 
 template <class FX>

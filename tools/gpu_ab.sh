@@ -5,6 +5,7 @@
 # build (AB_SKIP_TESTS=1 skips it).  Every GPU step has its own time limit; the script stops at the first failure.
 #   tools/gpu_ab.sh            headline queue runs (bench.py, no CPU / configs[4] legs)
 #   tools/gpu_ab.sh latency    lone-QP latency (tools/latency_probe.py)
+#   tools/gpu_ab.sh ric        headline runs with the isolated legs (configs[2] Riccati, the lone QP) included
 set -o pipefail
 mkdir -p gpurun_out/ab
 export TMPDIR=/tmp
@@ -21,7 +22,9 @@ for i in 1 2 3; do
       echo "$v$i $(grep -E 'solo' gpurun_out/ab/lat_$v$i.log)"
       continue
     fi
-    HPMPC_MI355X_LIB=$PWD/hpmpc_amd/lib/ab/lib$v.so timeout -k 10 300 python3 bench.py --no-cpu --no-pcond --no-isolated \
+    iso=--no-isolated
+    [ "$mode" = ric ] && iso=  # the Riccati legs: configs[2] (riccati_batch_N50) runs with the isolated legs
+    HPMPC_MI355X_LIB=$PWD/hpmpc_amd/lib/ab/lib$v.so timeout -k 10 300 python3 bench.py --no-cpu --no-pcond $iso \
       --no-queue-batch-slots --no-aliased --steps 20 > gpurun_out/ab/$v$i.log 2>&1 || { tail -20 gpurun_out/ab/$v$i.log; exit 1; }
     python3 - "$v$i" <<'PY'
 import json, sys
