@@ -79,87 +79,6 @@ __device__ __forceinline__ int mw_flag(const int* f) { return __atomic_load_n(f,
 // before every post, which also waits for the poster's unrelated scalar loads: a same-box A/B measured 350.4 vs
 // 367.1-367.5 us per lone-QP IP iteration (3 pairs, profiles/r04/ab_latency.txt), 4.7 %, above the 2 % the fenced
 // form was allowed, so it is a build option (tools/gpu_ab.sh variants) and not the default.
-// HK_MW_NOINLINE: each sweep of the multi-wave kernel as its own (out-of-line) function, so that the register
-// allocator sees one sweep's roles at a time instead of the whole solve (experiment: SGPR spills of hk_ipm_solo_mw).
-#ifdef HK_MW_NOINLINE
-#define HK_MW_SWEEP __device__ __attribute__((noinline))
-#else
-#define HK_MW_SWEEP __device__ __forceinline__
-#endif
-
-// Out of line, the sweeps receive their pointers through memory (the structs are passed by reference) and the
-// compiler can no longer prove them wave-uniform: every buffer access would sit in a waterfall loop and the stage
-// tables would be read with FLAT loads.  mw_uni re-establishes both facts at entry: readfirstlane for every scalar
-// and pointer, and the LDS address space for the stage tables.
-template <class T>
-__device__ __forceinline__ T* mw_uni(T* p) {
-    const unsigned long long v = (unsigned long long)p;
-    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
-    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
-    return (T*)(((unsigned long long)hi << 32) | lo);
-}
-__device__ __forceinline__ int mw_uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
-__device__ __forceinline__ double mw_uni(double x) {
-    return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(x)), __builtin_amdgcn_readfirstlane(__double2loint(x)));
-}
-template <class T>
-__device__ __forceinline__ const T* mw_lds(const T* p) {
-    return (const T*)(const __attribute__((address_space(3))) T*)p;
-}
-__device__ __forceinline__ RicIO mw_uni(const RicIO& a) {
-#ifdef HK_MW_NOINLINE
-    RicIO r;
-    r.N = mw_uni(a.N);
-    r.st = mw_lds(mw_uni(a.st));
-    r.tileslot = mw_lds(mw_uni(a.tileslot));
-    r.BAbt = mw_uni(a.BAbt);
-    r.RSQ = mw_uni(a.RSQ);
-    r.BAbtS = mw_uni(a.BAbtS);
-    r.RSQS = mw_uni(a.RSQS);
-    r.F = mw_uni(a.F);
-    r.DCt = mw_uni(a.DCt);
-    return r;
-#else
-    return a;
-#endif
-}
-__device__ __forceinline__ BoxCtx mw_uni(const BoxCtx& a) {
-#ifdef HK_MW_NOINLINE
-    BoxCtx r;
-    r.d = mw_uni(a.d);
-    r.lam = mw_uni(a.lam);
-    r.t = mw_uni(a.t);
-    r.dlam = mw_uni(a.dlam);
-    r.dt = mw_uni(a.dt);
-    r.t_inv = mw_uni(a.t_inv);
-    r.lamt = mw_uni(a.lamt);
-    r.res_d = mw_uni(a.res_d);
-    r.res_m = mw_uni(a.res_m);
-    r.qxs = mw_uni(a.qxs);
-    r.Qx = mw_uni(a.Qx);
-    r.qx = mw_uni(a.qx);
-    r.smu = mw_uni(a.smu);
-    r.pred = mw_uni(a.pred);
-    r.ux = mw_uni(a.ux);
-    r.pi = mw_uni(a.pi);
-    r.res_q = mw_uni(a.res_q);
-    r.res_b = mw_uni(a.res_b);
-    r.res_rhs = mw_uni(a.res_rhs);
-    r.no_tinv = mw_uni(a.no_tinv);
-    r.cert = mw_uni(a.cert);
-    r.cert_out = mw_uni(a.cert_out);
-    r.cert_new = mw_uni(a.cert_new);
-    return r;
-#else
-    return a;
-#endif
-}
-#ifdef HK_MW_NOINLINE
-#define MW_UNI(x) mw_uni(x)
-#else
-#define MW_UNI(x) (x)
-#endif
-
 #ifndef HK_MW_FENCE
 #define HK_MW_FENCE 0
 #endif
@@ -255,20 +174,10 @@ __device__ __forceinline__ double mw_get(int j, int i) { return hk_mw.ring[j % M
 constexpr int MW_BHELP = 2;
 
 template <bool AUG, int BM, class FX>
-HK_MW_SWEEP int ric_backward_mw(const RicIO& io_in, int tb, int w, int update_b, const double* bsrc,
-                                               int update_q, const double* qsrc, const BoxCtx& bc_in, int compute_Pb,
+__device__ __forceinline__ int ric_backward_mw(const RicIO& io, int tb, int w, int update_b, const double* bsrc,
+                                               int update_q, const double* qsrc, const BoxCtx& bc, int compute_Pb,
                                                double* Pb) {
     static_assert(cert_loaded(BM), "the tile wave tests the certificate in threshold form (the IPM's box modes)");
-    const RicIO io = mw_uni(io_in);
-    const BoxCtx bc = mw_uni(bc_in);
-    tb = MW_UNI(tb);
-    w = MW_UNI(w);
-    update_b = MW_UNI(update_b);
-    update_q = MW_UNI(update_q);
-    compute_Pb = MW_UNI(compute_Pb);
-    bsrc = MW_UNI(bsrc);
-    qsrc = MW_UNI(qsrc);
-    Pb = MW_UNI(Pb);
     const int N = io.N, l = lane_id(), c = l & 15;
     Scratch* sm = &hk_mw.sm[w];
     if (w >= 2) {
@@ -551,17 +460,8 @@ __device__ __forceinline__ void fwd_chain(Scratch* sm, const SH& sh, int k, cons
 }
 
 template <int MODE, int FM, class FX, bool PRED = false>
-HK_MW_SWEEP int ric_forward_mw(const RicIO& io_in, int tb, int w, const double* bsrc, int use_bsrc,
-                               double* ux, int compute_pi_, double* pi, const BoxCtx& bc_in, double& al_out) {
-    const RicIO io = mw_uni(io_in);
-    const BoxCtx bc = mw_uni(bc_in);
-    tb = MW_UNI(tb);
-    w = MW_UNI(w);
-    use_bsrc = MW_UNI(use_bsrc);
-    compute_pi_ = MW_UNI(compute_pi_);
-    bsrc = MW_UNI(bsrc);
-    ux = MW_UNI(ux);
-    pi = MW_UNI(pi);
+__device__ __forceinline__ int ric_forward_mw(const RicIO& io, int tb, int w, const double* bsrc, int use_bsrc,
+                               double* ux, int compute_pi_, double* pi, const BoxCtx& bc, double& al_out) {
     const int N = io.N, l = lane_id(), g = l >> 4, c = l & 15;
     const int compute_pi = PRED ? 0 : compute_pi_;
     Scratch* sm = &hk_mw.sm[w];
@@ -668,18 +568,8 @@ HK_MW_SWEEP int ric_forward_mw(const RicIO& io_in, int tb, int w, const double* 
 // slot = [q + box gradient | bop (4) | S (4) | invd | Pb].
 // ------------------------------------------------------------------------------------------------
 template <int TM, int FM, class FX>
-HK_MW_SWEEP int ric_trs_mw(const RicIO& io_in, int tb, int w, const double* hb, const double* hq,
-                           const BoxCtx& bc_in, double* ux, int compute_pi, double* pi, double* Pb, double& al) {
-    const RicIO io = mw_uni(io_in);
-    const BoxCtx bc = mw_uni(bc_in);
-    tb = MW_UNI(tb);
-    w = MW_UNI(w);
-    compute_pi = MW_UNI(compute_pi);
-    hb = MW_UNI(hb);
-    hq = MW_UNI(hq);
-    ux = MW_UNI(ux);
-    pi = MW_UNI(pi);
-    Pb = MW_UNI(Pb);
+__device__ __forceinline__ int ric_trs_mw(const RicIO& io, int tb, int w, const double* hb, const double* hq,
+                           const BoxCtx& bc, double* ux, int compute_pi, double* pi, double* Pb, double& al) {
     const int N = io.N, l = lane_id(), g = l >> 4, c = l & 15;
     Scratch* sm = &hk_mw.sm[w];
     if (w > 0) {

@@ -800,7 +800,9 @@ __global__ __launch_bounds__(64) void hk_ipm_solo(KArgs a) {
 // The same solve with one problem per 256-thread workgroup (hk_mw.h): wave 0 runs each sweep's recursion, waves
 // 1..3 everything off it, and the element-wise update is split over the four waves.  Every body keeps the
 // single-wave body's arithmetic (same routines, same operands, mu summed in the same order), so the iterates are
-// bitwise hk_ipm_solo's.  All four waves run every body, so that they meet the same barriers in the same order;
+// bitwise hk_ipm_solo's when both are built with -ffp-contract=on; under the build's default contraction hipcc fuses
+// a few a * b + c differently once the bodies are split over waves and the two agree to rounding (hk_mw.h).  All four
+// waves run every body, so that they meet the same barriers in the same order;
 // the loop-control state is read by all and written by thread 0 (IpmView.l = threadIdx.x here).
 // ------------------------------------------------------------------------------------------------
 namespace {
