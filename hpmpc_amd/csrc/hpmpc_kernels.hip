@@ -737,6 +737,10 @@ __global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_corr(KArgs a) {
     corr_body<FX>(a, T, v);
 }
 
+// Stages per chunk of the update pass (quads loaded before any is used; HK_UPD_CH=6 for an A/B)
+#ifndef HK_UPD_CH
+#define HK_UPD_CH 4
+#endif
 template <class FX>
 __global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_update(KArgs a) {
     Who who;
@@ -744,7 +748,7 @@ __global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_update(KArgs a) {
     const LdsTabs T = lds_tables(a);
     IpmView v = ipm_view(a, T, who);
     if (v.w.state[S_ACTIVE] == 0.0) return;
-    bool again = update_body<FX, 4>(a, v);
+    bool again = update_body<FX, HK_UPD_CH>(a, v);
     if (!again && a.nq) {
         if (v.l == 0) atomicAdd(&a.qctl[1], 1);
         again = ipm_refill<FX, 4, false>(a, T, who.s);  // queue mode: the slot takes the next entry
