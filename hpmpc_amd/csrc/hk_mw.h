@@ -293,9 +293,10 @@ __device__ __forceinline__ int ric_backward_mw(const RicIO& io, int tb, int w, i
                 MW_SEG(1);
                 double mld = 0.0;
                 const bool full = !SHT::fixed && k == 0;
-                // gc: the threshold T (IPM modes); the certificate's ballot is taken after the u blocks
-                xfac = stage_chol<false, false>(M, mld, invd, sh.nu, sh.nx, sh.xo, full, !SHT::fixed, nullptr, k,
-                                                cert_defer_thr(M, dq, gc, cert_diag_w()), &xf);
+                // gc: the threshold T (IPM modes).  Taken before the u blocks: deferring the ballot past them
+                // (CertDefer) measured 329 vs 319 us per lone-QP IP iteration (profiles/r04/ab_latency_OR.txt)
+                xfac = !full && !cert_ok_thr(M, dq, gc, cert_diag_w());
+                stage_chol<false, false>(M, mld, invd, sh.nu, sh.nx, sh.xo, full, !SHT::fixed, nullptr, k, xfac, &xf);
                 MW_SEG(2);
             });
             P = M;

@@ -14,7 +14,6 @@
 // so that the state block always starts on an MFMA K-chunk boundary.  Tile indices in [nu, xo) and
 // beyond xo+nx are zero padding (their pivots clamp to 0 and contribute nothing).
 #pragma once
-#include <type_traits>
 
 #include "hk_prims.h"
 
@@ -365,27 +364,6 @@ __device__ __forceinline__ bool cert_ok_thr(const d4& M, double dq, double T, co
     return __builtin_amdgcn_ballot_w64(!(d - dq < T)) == 0;
 }
 
-// The certificate's per-lane comparison formed before the stage factorisation and its ballot taken after the u
-// blocks, where stage_chol first needs the verdict: the comparison's inputs (the tile diagonal after the update, the
-// box term, the bound) are ready before the u-block chain starts, so its latency hides under that chain instead of
-// sitting between the tile update and the first pivot.  fails() is wave-uniform.
-struct CertDefer {
-    double lhs, rhs;  // the stage fails iff some lane has !(lhs < rhs)
-    __device__ __forceinline__ bool fails() const { return __builtin_amdgcn_ballot_w64(!(lhs < rhs)) != 0; }
-};
-// threshold form (the IPM's modes): lhs = M_ii - dq_i from the 0/1 diagonal weights, rhs = T
-__device__ __forceinline__ CertDefer cert_defer_thr(const d4& M, double dq, double T, const d4& w) {
-    return CertDefer{(w[0] * M[0] + w[1] * M[1] + w[2] * M[2] + w[3] * M[3]) - dq, T};
-}
-// bound form (cert_ok): lhs = (M_ii - dq_i)(allow g + 1e-15) on the diagonal lanes, rhs = g^2; a lane with dq < 0, or
-// g <= 0, fails outright
-__device__ __forceinline__ CertDefer cert_defer_g(const d4& M, double dq, double gc) {
-    const double cc = fma(CERT_ALLOW, gc, 1e-15), g2 = gc * gc;
-    const bool force = !(gc > 0.0) || dq < 0.0;
-    const double lhs = force ? __builtin_inf() : (diag_lane() ? (diag_sel(M) - dq) * cc : -__builtin_inf());
-    return CertDefer{lhs, g2};
-}
-
 // l[4R + g] (row layout of a col-layout vector over tile block R): the pivot entries of block R
 template <int R>
 __device__ __forceinline__ double lrow_blk(double v) {
@@ -473,10 +451,9 @@ struct XFac {
 // xfac (P form only, wave-uniform): the stage failed the clamp certificate (cert_ok) -- its x block is factorised
 // as the reference does and the record carries P_eff = Lxx Lxx' and p_eff = Lxx l_x (the x factor and its inverse
 // diagonal also go to *xf when given); invd keeps the u pivots only, as in every P-form record.
-// xfac: a bool (the verdict, taken before the call) or a CertDefer (its ballot is taken after the u blocks).
-template <bool AUG, bool KGEN = false, class XT = bool>
-__device__ __forceinline__ bool stage_chol(d4& M, double& ml, double& invd, int nu, int nx, int xo, bool full,
-                                           bool transpose, double* kg = nullptr, int kdbg = -1, XT xfac = false,
+template <bool AUG, bool KGEN = false>
+__device__ __forceinline__ void stage_chol(d4& M, double& ml, double& invd, int nu, int nx, int xo, bool full,
+                                           bool transpose, double* kg = nullptr, int kdbg = -1, bool xfac = false,
                                            XFac* xf = nullptr) {
     const int l = lane_id(), g = l >> 4, c = l & 15;
     (void)kdbg;
@@ -491,11 +468,7 @@ __device__ __forceinline__ bool stage_chol(d4& M, double& ml, double& invd, int 
     HK_STAMP(20, kdbg);
     if (12 < nu || (full && 15 >= xo && 12 < hi)) chol_block<3, AUG>(M, ml, invd, nullptr, kdbg);
     HK_STAMP(22, kdbg);
-    bool xf_now;
-    if constexpr (std::is_same<XT, bool>::value)
-        xf_now = xfac;
-    else
-        xf_now = !full && xfac.fails();
+    const bool xf_now = xfac;
 #ifdef HK_COUNT_NOFALLBACK  // static instruction counts of the certified path (tools/loop_icount.py): the test stays,
     // the clamped factorisation is compiled out
     asm volatile("" ::"s"(__builtin_amdgcn_readfirstlane((int)xf_now)));
@@ -513,7 +486,7 @@ __device__ __forceinline__ bool stage_chol(d4& M, double& ml, double& invd, int 
             xf->invd = ivx;
         }
     }
-    if (!transpose) return xf_now;
+    if (!transpose) return;
     // lower triangle <- transpose of the upper storage:  T = S' via MFMA with an identity B operand
     // (two accumulator chains: the identity products are exact, so the split does not change T)
     const d4 z = {0.0, 0.0, 0.0, 0.0};
@@ -524,7 +497,6 @@ __device__ __forceinline__ bool stage_chol(d4& M, double& ml, double& invd, int 
     const d4 T = T0 + T1;
 #pragma unroll
     for (int r = 0; r < 4; r++) M[r] = (g + 4 * r > c) ? T[r] : M[r];
-    return xf_now;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1373,8 +1345,8 @@ __device__ __forceinline__ void bwd_core(const RicIO& io, Scratch* sm, const SH&
     (void)dq;
     (void)gc;
 #else
-    // taken here, before the factorisation: deferring the ballot past the u blocks (CertDefer, as the multi-wave tile
-    // wave does) keeps the comparison live across the chain and cost the pass kernels more spills than it hid
+    // taken here, before the factorisation: deferring the ballot past the u blocks keeps the comparison live across the
+    // chain -- more spills in the pass kernels (static count), slower in the multi-wave tile wave (measured, hk_mw.h)
     const bool xcert = !full && (THR ? !cert_ok_thr(M, dq, gc, cert_diag_w()) : !cert_ok(M, dq, gc));
 #endif
 #ifdef HK_STAMPS  // diagnostic build: how often the certificate fails, at this allowance and (with g) at 10x / 100x

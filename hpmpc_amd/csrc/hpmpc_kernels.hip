@@ -120,9 +120,10 @@ __device__ __forceinline__ void wsync() { __syncthreads(); }
 // ------------------------------------------------------------------------------------------------
 // d_back_ric_rec_sv_tv_res / _trf_ / _trs_ over a batch (one problem per workgroup)
 // ------------------------------------------------------------------------------------------------
-// Prefetch depth of the Riccati entry points' backward sweep (ric_backward PD; HK_RIC_PD=1 for an A/B)
+// Prefetch depth of the Riccati entry points' backward sweep (ric_backward PD).  2 measured no faster than 1 on the
+// 1024-problem sv batches (N=100: 3.48 vs 3.50 M fact/s; configs[2]: 7.14 vs 7.25 M, profiles/r04/ab_ric_LO.txt)
 #ifndef HK_RIC_PD
-#define HK_RIC_PD 2
+#define HK_RIC_PD 1
 #endif
 template <class FX>
 __global__ __launch_bounds__(64) void hk_ric_sv(KArgs a) {
