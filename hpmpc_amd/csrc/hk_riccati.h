@@ -56,6 +56,24 @@ __device__ __forceinline__ int lib4_idx(int sd, int i, int j) { return (i >> 2) 
 // counted s_waitcnt vmcnt(N) instead of draining the whole prefetch queue.
 __device__ __forceinline__ double ldsel(const double* p, int idx, bool ok) { return gld(p, idx, ok); }
 
+// HK_WIDE_BOP (an A/B build): two tile registers of a lib4 operand whose lane (g, c) element is
+// (row c, column j_r) -- the BAbt operand of the compiled (4, 12) class, where tile index = variable -- fetched with
+// one 16-B load per lane instead of two 8-B ones: rows c and c+1 of a column are 16 contiguous bytes (c even), so the
+// even lane of each pair loads column ja's pair, the odd lane column jb's, and they swap the half the other needs
+// (DPP quad_perm [1,0,3,2]).  oka / okb: this lane's elements exist (column in range; rows always are).
+__device__ __forceinline__ void ld_pair16(const double* B, int sd, int c, int ja, int jb, bool oka, bool okb,
+                                          double& va, double& vb) {
+    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+    const bool odd = (c & 1) != 0;
+    const int j = odd ? jb : ja;
+    const int off = (odd ? okb : oka) ? lib4_idx(sd, c & ~1, j) * 8 : (int)0xFFFFFFF0;
+    const u4 q = __builtin_amdgcn_raw_buffer_load_b128(rsrc(B), off, 0, 0);
+    const double d0 = mk((int)q[1], (int)q[0]), d1 = mk((int)q[3], (int)q[2]);
+    const double recv = dpp_mov<0xB1>(odd ? d0 : d1);  // quad_perm [1,0,3,2]: the pair partner's half
+    va = oka ? (odd ? recv : d0) : 0.0;
+    vb = okb ? (odd ? d1 : recv) : 0.0;
+}
+
 // LDS scratch for col->row layout conversion: 16 doubles per wave.
 struct Scratch {
     double v[32];
@@ -585,6 +603,15 @@ struct FixSh {
         : nb(srd(s, &StageInfo::nb)), pnb(srd(s, &StageInfo::pnb)), oB(srd(s, &StageInfo::oB)),
           oR(srd(s, &StageInfo::oR)), fl(srd(s, &StageInfo::r0)) {}
 };
+
+// HK_WIDE_BOP applies to the compiled (4, 12) class only (tile index = variable index, ld_pair16)
+template <class SH>
+constexpr bool wide_bop_shape() {
+    if constexpr (SH::fixed)
+        return SH::nu == 4 && SH::nx == 12;
+    else
+        return false;
+}
 
 // The stage's data blocks: per problem, or shared by the batch (StageInfo r0 bits 1 / 2; wave-uniform selects).
 __device__ __forceinline__ int stage_flags(const StageInfo& s) { return s.r0; }
@@ -1117,6 +1144,17 @@ __device__ __forceinline__ void bwd_fetch(const RicIO& io, const SH& sh, int k, 
     for (int r = 0; r < 4; r++) {
         const int s = 4 * r + g - sh.xo1;
         const bool ok = live && s >= 0 && s < sh.nx1;
+#ifdef HK_WIDE_BOP
+        if constexpr (wide_bop_shape<SH>()) {  // registers 1 and 2 in one 16-B load, 0 is masked
+            if (r == 1) {
+                double b1, b2;
+                ld_pair16(Bk, sh.sdB, c, s, s + 4, ok, live && s + 4 < sh.nx1, b1, b2);
+                f.bop[1] = b1;
+                f.bop[2] = b2;
+            }
+            if (r == 0 || r == 3) f.bop[r] = ldsel(Bk, lib4_idx(sh.sdB, vc, s), ok && vc >= 0);
+        } else
+#endif
         f.bop[r] = ldsel(Bk, lib4_idx(sh.sdB, vc, s), ok && vc >= 0);
         if (BM != BX_P2R) f.brow[r] = AUG ? ldsel(bp, update_b ? s : lib4_idx(sh.sdB, nux, s), ok) : 0.0;
     }
@@ -1940,6 +1978,17 @@ __device__ __forceinline__ void trs_fetch(const RicIO& io, const SH& sh, int k, 
     for (int r = 0; r < 4; r++) {
         const int sr = g + 4 * r - sh.xo1;
         const bool ok = live && sr >= 0 && sr < sh.nx1;
+#ifdef HK_WIDE_BOP
+        if constexpr (wide_bop_shape<SH>()) {  // registers 1 and 2 in one 16-B load, 0 is masked
+            if (r == 1) {
+                double b1, b2;
+                ld_pair16(Bk, sh.sdB, c, sr, sr + 4, ok, live && sr + 4 < sh.nx1, b1, b2);
+                f.bop[1] = b1;
+                f.bop[2] = b2;
+            }
+            if (r == 0 || r == 3) f.bop[r] = ldsel(Bk, lib4_idx(sh.sdB, vc, sr), ok && vc >= 0);
+        } else
+#endif
         f.bop[r] = ldsel(Bk, lib4_idx(sh.sdB, vc, sr), ok && vc >= 0);
         f.brow[r] = RPB ? ldsel(bp, hb ? sr : lib4_idx(sh.sdB, nux, sr), ok && compute_Pb) : 0.0;
     }
