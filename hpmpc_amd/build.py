@@ -120,7 +120,7 @@ def build_calib(verbose: bool = False) -> str:
 
 def build_oracle(force: bool = False) -> None:
     odir = os.path.join(ROOT, "oracle")
-    targets = ["oracle"]
+    targets = ["oracle", "oracle_fma"]  # oracle_fma: the build spread that gates the configs[4] IPM test
     if os.path.isdir(os.environ.get("HPMPC_REF", "/root/reference")):
         targets += ["ref", "ref_avx"]  # ref_avx: the alternate IPM's goldens (make_golden.py)
     subprocess.run(["make", "-s", "-C", odir] + (["-B"] if force else []) + targets, check=True)

@@ -8,8 +8,14 @@ checker -- DESIGN.md), boxes that become general constraints, wide stages of arb
 d_back_ric_rec_sv_tv_res, and the batched device pipeline.  Tolerances: Riccati 1e-12 (SURVEY.md §8c);
 condensed pipeline vs direct solve 1e-11.
 """
+import os
+
 import numpy as np
 import pytest
+
+from hpmpc_amd.cabi import HpmpcAPI, load
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 from helpers import TOL_PCOND_SV, TOL_RIC, check_pcond, pcond_sv, random_qp
 
@@ -255,34 +261,40 @@ def _pcond_ipm_vs_oracle(oracle, bq, N2, problems, solver=None):
 
     torch.cuda.synchronize()
     kk, ret = s.kk2.cpu().numpy(), s.ret2.cpu().numpy()
+    # no reference golden exists at these shapes (the reference's own condensing is wrong at nu > 4), so
+    # the gates come from the build spread of the oracle pipeline itself, per problem and quantity: the same
+    # restatement built with -mfma -ffp-contract=fast (oracle/liboracle_fma.so), gate = max(1e-10, 4 x spread) -- the
+    # rule of test_gpu_parity.py GATES.  Measured (tools/pcond_ipm_err.py): the GPU point sits at the builds' own
+    # spread, 1e-14..1e-13 on well-conditioned problems and up to ~1e-8 where the last Newton systems carry
+    # lam / t ~ 1/mu and the condensed inner-state boxes enter as general constraints.
+    ofma = HpmpcAPI(load(os.path.join(ROOT, "oracle", "liboracle_fma.so")), "orc_")
     for p in problems:
         qp = bq.problem(p)
-        c, _ = oracle.part_cond(qp.copy(), N2)
-        r = oracle.ipm(c.copy(), k_max=60)
-        e = oracle.part_expand(qp, c, r["ux"], r["pi"], r["lam"], r["t"])
+        es = []
+        for o in (oracle, ofma):
+            c, _ = o.part_cond(qp.copy(), N2)
+            r = o.ipm(c.copy(), k_max=60)
+            es.append((r, o.part_expand(qp, c, r["ux"], r["pi"], r["lam"], r["t"])))
+        (r, e), (_, e2) = es
         assert (int(kk[p]), int(ret[p])) == (r["kk"], r["ret"]), (p, kk[p], r["kk"], ret[p], r["ret"])
         if r["ret"] != 0:  # N60_nx24: three of four problems are box-infeasible (ret 1 / 2, |pi| 1e16..1e33): the
             continue  # matching (kk, ret) is the check, the diverged iterates carry no comparable digits
-        # the last Newton systems carry lam/t ~ 1/mu at mu_tol 1e-12 and the condensed inner-state boxes enter them
-        # as general constraints (DCt lam) of a Hessian condensed over N/N2 stages: sums in MFMA order vs the
-        # oracle's loops move the converged point by up to ~1e-8 relative (measured), so the expanded outputs are
-        # gated at 1e-6 and, as the sharper check, the GPU point must satisfy the ORIGINAL problem's KKT
-        # conditions (d_res_mpc_hard_tv) as well as the oracle's own point does
-        # (lam / t: the N60 problems converge with multipliers up to ~1e12 on stage-0 boxes, whose relative spread
-        # between two correct solvers is TOL_KKT2's lam gate 1e-4)
-        tm, tl = 1e-6, 1e-4
         U, Pi = s.solution(p)
         Lm, T = s.multipliers(p)
-        for k in range(N + 1):
-            n = qp.nux(k)
-            assert np.max(np.abs(U[k] - e["ux"][k][:n]) / np.maximum(1, np.abs(e["ux"][k][:n])), initial=0) <= tm, (p, k)
-            if k < N:
-                m = int(qp.nx[k + 1])
-                assert np.max(np.abs(Pi[k] - e["pi"][k][:m]) / np.maximum(1, np.abs(e["pi"][k][:m])), initial=0) <= tm, (p, k)
-            nbk, pnb = int(qp.nb[k]), qp.pnb(k)
-            idx = np.r_[0:nbk, pnb:pnb + nbk].astype(int)
-            for got, ref in ((Lm[k], e["lam"][k]), (T[k], e["t"][k])):
-                assert np.max(np.abs(got[idx] - ref[idx]) / np.maximum(1, np.abs(ref[idx])), initial=0) <= tl, (p, k)
+        box = [np.r_[0:int(qp.nb[k]), qp.pnb(k):qp.pnb(k) + int(qp.nb[k])].astype(int) for k in range(N + 1)]
+        views = {"ux": (U, e["ux"], e2["ux"], [slice(0, qp.nux(k)) for k in range(N + 1)]),
+                 "pi": (Pi, e["pi"], e2["pi"], [slice(0, int(qp.nx[k + 1])) for k in range(N)]),
+                 "lam": (Lm, e["lam"], e2["lam"], box), "t": (T, e["t"], e2["t"], box)}
+        for key, (got, ref, alt, sel) in views.items():
+            err = spread = 0.0
+            for k, ix in enumerate(sel):
+                g_, r_, a_ = np.asarray(got[k])[ix], np.asarray(ref[k])[ix], np.asarray(alt[k])[ix]
+                w = np.maximum(1.0, np.abs(r_))
+                err = max(err, float(np.max(np.abs(g_ - r_) / w, initial=0.0)))
+                spread = max(spread, float(np.max(np.abs(a_ - r_) / w, initial=0.0)))
+            assert err <= max(1e-10, 4.0 * spread), (p, key, err, spread)
+        # and the GPU point satisfies the ORIGINAL problem's KKT conditions (d_res_mpc_hard_tv) as well as the
+        # oracle's own point does
         b, q = bq_from_qp(qp)
         pad = lambda xs: [np.r_[np.asarray(x, dtype=np.float64), np.zeros(8)] for x in xs]
         rg = oracle.residuals_plain(qp, b, q, pad(U), pad(Pi), pad(Lm), pad(T))
