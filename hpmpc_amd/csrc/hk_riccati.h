@@ -491,8 +491,6 @@ __device__ __forceinline__ void stage_chol(d4& M, double& ml, double& invd, int 
     // the clamped factorisation is compiled out
     asm volatile("" ::"s"(__builtin_amdgcn_readfirstlane((int)xf_now)));
     if (false) {
-#elif defined(HK_XFAC_UNLIKELY)
-    if (__builtin_expect(!full && xf_now, 0)) {  // A/B: the clamped fallback laid out as the cold path
 #else
     if (!full && xf_now) {
 #endif
