@@ -69,6 +69,7 @@ def parse():
     ap.add_argument("--no-queue-batch-slots", action="store_true", help="skip the queue run with one slot per "
                     "problem of the batch")
     ap.add_argument("--no-aliased", action="store_true", help="skip the time-invariant / aliased leg")
+    ap.add_argument("--no-coupled", action="store_true", help="skip the coupled-Hessian IPM leg")
     ap.add_argument("--check-launch", action="store_true", help="start the ranks, join the process group (gloo) "
                     "and print each rank's world size, without touching the GPU (launcher test)")
     return ap.parse_args()
@@ -594,6 +595,40 @@ def bench_aliased(args, torch, red, rank, world, barrier, slots):
     return out
 
 
+def bench_coupled(args, torch, red, rank, world, barrier, slots, headline_value):
+    """the headline IPM workload with strongly coupled stage Hessians (hpmpc_amd.shard.coupled_shard:
+    diag(R, Q) + G G' / nux, positive definite but not diagonally dominant, so Gershgorin's bound is negative on every
+    inner stage).  The clamp certificate then rests on the shifted-Cholesky bound (hk_riccati.h cert_g_shift); before
+    it, every stage of every factorisation took the clamped x-block fallback.  Same queue, slots and steps as the
+    headline; the ratio to the headline's rate is reported beside it."""
+    from hpmpc_amd.batch import BatchSolver
+    from hpmpc_amd.shard import coupled_shard
+
+    B, N, nx, nu = args.batch, args.N, args.nx, args.nu
+    qc = coupled_shard(N, nx, nu, rank, world, B)
+    s = BatchSolver(qc, k_max=args.k_max)
+    s.queue(B, slots).run()
+    K = min(args.steps, 20)
+    Q = s.queue(K * B, slots)
+    barrier()
+    t0 = time.perf_counter()
+    pm, ticks = Q.run(profiled=True)
+    barrier()
+    dt = red.max(time.perf_counter() - t0)
+    it = red.sum(float(Q.kk.sum().item()))
+    ret = Q.ret.cpu().numpy()
+    out = {"workload": f"ipm_N{N}_nx{nx}_nu{nu}_batch{B}_coupled_hessians", "value": it / dt, "unit": "IP-iter/s",
+           "steps": K, "ms_per_step": dt / K * 1e3, "vs_headline": (it / dt) / headline_value,
+           "ret_counts": {str(int(r)): int((ret == r).sum()) for r in np.unique(ret)},
+           "pass_ms_per_step": {n: float(v) / K for n, v in
+                                zip(["hk_ipm_init", "hk_ipm_fact", "hk_ipm_pred", "hk_ipm_corr", "hk_ipm_update"], pm)}}
+    ref = ref_api() if rank == 0 else None
+    out["parity"] = parity_ipm(ref, qc, dict(ux=Q.ux, pi=Q.pi, lam=Q.lam, t=Q.t, kk=Q.kk, ret=Q.ret, k_max=args.k_max),
+                               [(q, q % B) for q in spread(8, K * B)])
+    del Q, s
+    return out
+
+
 def bench_scatter(args, torch, dist, rank, world, solver, template, B, barrier):
     """configs[3]'s data path (SURVEY.md §8e scatter mode): rank 0 holds every rank's block in HBM and sends
     it over RCCL point-to-point (xGMI), each rank solves its block through the problem queue, and ux / pi /
@@ -792,6 +827,7 @@ def main():
                        "slowest problem sets the time"}
 
     ali = None if args.no_aliased else bench_aliased(args, torch, red, rank, world, barrier, slots)
+    cpl = None if args.no_coupled else bench_coupled(args, torch, red, rank, world, barrier, slots, value)
 
     # ---------------- Riccati factorisation + solve ----------------
     for _ in range(args.warmup):
@@ -878,11 +914,16 @@ def main():
                          "algorithmic_bytes_per_problem_iter": bytes_dom,
                          "per_pass": per_pass,
                          "pass_ms_per_step": {n: float(v / args.steps) for n, v in zip(names, pass_ms)},
+                         # fixed fields: the two tied passes and the whole iteration, whichever pass 'kernel' names
+                         "frac_fact": per_pass["hk_ipm_fact"]["achieved_GBps"] / PEAK_HBM_GBS,
+                         "frac_corr": per_pass["hk_ipm_corr"]["achieved_GBps"] / PEAK_HBM_GBS,
+                         "frac_whole_iteration": iters_rank * bytes_iter / (ipm_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
                          "ipm_whole_solve": {"achieved_GBps": iters_rank * bytes_iter / (ipm_ms * 1e-3) / 1e9,
                                              "algorithmic_bytes_per_ip_iter": bytes_iter,
                                              "fp64_tflops": iters_rank * fl_iter / (ipm_ms * 1e-3) / 1e12}},
             "queue_batch_slots": qb,
             "aliased": ali,
+            "coupled": cpl,
             "generic_shape": dyn,
             "isolated_batch": iso,
             "scatter": sc,

@@ -14,7 +14,7 @@ CSRC = os.path.join(ROOT, "hpmpc_amd", "csrc")
 LIBDIR = os.path.join(ROOT, "hpmpc_amd", "lib")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("HPMPC_ARCH", "gfx950")
-SOURCES = ["hpmpc_kernels.hip", "hk_wide.hip", "hk_wide_ipm.hip", "hk_soft.hip", "hpmpc_capi.cpp", "hpmpc_capi_wide.cpp",
+SOURCES = ["hpmpc_kernels.hip", "hk_ric2.hip", "hk_wide.hip", "hk_wide_ipm.hip", "hk_soft.hip", "hpmpc_capi.cpp", "hpmpc_capi_wide.cpp",
            "hpmpc_capi_wide_ipm.cpp", "hpmpc_capi_iface.cpp", "hpmpc_capi_mpc.cpp"]
 HEADERS = ["hpmpc_api.h", "hk_prims.h", "hk_riccati.h", "hk_ipm.h", "hk_mw.h", "hpmpc_kargs.h", "hk_wide_args.h", "hk_wide_core.h", "hk_wide_host.h", "hk_soft_args.h", "hk_launch_guard.h"]
 # MFMA accumulators stay in ordinary VGPRs: the stage tile is read and written by VALU code between

@@ -321,11 +321,12 @@ __device__ __forceinline__ double wave_min_lb(double x) {
     return (double)fminf(__builtin_bit_cast(float, (int)b[0]), __builtin_bit_cast(float, (int)b[1]));
 }
 
-// g of a stage from its data tile Mi (symmetric, zero outside the active rows / columns): row sums of |Mi| by MFMA
-// against a ones operand (the A fragment of K-chunk kc is register kc itself: lane (g,c) holds Mi[4kc+g][c] =
+// Gershgorin's g of a stage from its data tile Mi (symmetric, zero outside the active rows / columns): row sums of |Mi|
+// by MFMA against a ones operand (the A fragment of K-chunk kc is register kc itself: lane (g,c) holds Mi[4kc+g][c] =
 // Mi[c][4kc+g]), the diagonal margin on the lane that holds it, then a wave minimum (as a conservative f32 bound).
+// cert_g (after stage_chol below) falls back to a shifted Cholesky where this bound is not positive.
 template <class SH>
-__device__ __forceinline__ double cert_g(const d4& Mi, const SH& sh) {
+__device__ __forceinline__ double cert_g_gersh(const d4& Mi, const SH& sh) {
     const int c = lane_id() & 15;
     const d4 z = {0.0, 0.0, 0.0, 0.0};
     d4 r0 = z, r1 = z;
@@ -515,6 +516,38 @@ __device__ __forceinline__ void stage_chol(d4& M, double& ml, double& invd, int 
     const d4 T = T0 + T1;
 #pragma unroll
     for (int r = 0; r < 4; r++) M[r] = (g + 4 * r > c) ? T[r] : M[r];
+}
+
+// A sharper lower bound on lambda_min of the data block where Gershgorin's is not positive (strongly coupled stage
+// Hessians, e.g. Q = G G' / n + I: every such stage used to fail the certificate and take the clamped x-block
+// factorisation).  tau = 2^-10 max_i Mi_ii; a Cholesky of Mi - tau I that keeps every active pivot
+// above the clamp proves lambda_min(Mi) >= tau - (eps + n gamma_{n+1}) max_i Mi_ii: the computed factor is the exact
+// factor of Mi - tau I + E with |E_ij| <= gamma_{n+1} sqrt(a_ii a_jj) (Cholesky's componentwise backward error), so
+// ||E||_2 <= n gamma_{n+1} max_i a_ii ~ 3e-14 max_i Mi_ii at n = 16; 1e-12 max_i Mi_ii is subtracted.  Any lower bound
+// on lambda_min(RSQ_k) can stand in for Gershgorin's g in the certificate (its derivation only uses that one).
+// Returns -1 (no bound) when the shifted factorisation clamps a pivot.  Wave-uniform.
+template <class SH>
+__device__ __forceinline__ double cert_g_shift(const d4& Mi, const SH& sh) {
+    const int l = lane_id(), g = l >> 4, c = l & 15;
+    const bool act = tile_active(c, sh.nu, sh.nx, sh.xo);
+    const double dm = -wave_min((diag_lane() && act) ? -diag_sel(Mi) : 0.0);  // max_i Mi_ii (exact)
+    const double tau = dm * 0x1p-10;
+    d4 A = Mi;
+#pragma unroll
+    for (int r = 0; r < 4; r++) A[r] -= (g + 4 * r == c && act) ? tau : 0.0;
+    double ml = 0.0, invd = 0.0;
+    stage_chol<false, false>(A, ml, invd, sh.nu, sh.nx, sh.xo, true, false);
+    const bool ok = dm > 0.0 && __builtin_amdgcn_ballot_w64(act && !(invd > 0.0)) == 0;
+    return ok ? tau - 1e-12 * dm : -1.0;
+}
+
+// The certificate's data part: a lower bound g on the smallest eigenvalue of the stage's data block RSQ_k -- Gershgorin's,
+// or where that one is not positive the shifted-Cholesky bound (wave-uniform branch; the benchmark data never take it).
+template <class SH>
+__device__ __forceinline__ double cert_g(const d4& Mi, const SH& sh) {
+    const double g = cert_g_gersh(Mi, sh);
+    if (g > 0.0) return g;
+    return cert_g_shift(Mi, sh);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -26,6 +26,7 @@
 #include "hk_wide_args.h"
 
 extern "C" int hk_launch(int which, const KArgs* a, int count, hipStream_t stream);
+extern "C" int hk_launch_ric2(int which, const KArgs* a, int count, hipStream_t stream);  // hk_ric2.hip
 extern "C" int hk_fixcls(int nu, int nx);
 // wide-stage path (hpmpc_capi_wide.cpp, hpmpc_capi_wide_ipm.cpp)
 extern "C" long long hk_wide_ipm_bytes(int N, const int* nx, const int* nu, const int* nb, const int* ng);
@@ -56,6 +57,20 @@ namespace {
 
 enum { K_SV = 0, K_TRF = 1, K_TRS = 2, K_RES = 3, K_IPM = 4, K_KKT = 5, K_KKT_P1 = 6, K_SOLO = 15 };
 constexpr int FSTRIDE = 352, V16 = 16, V32 = 32, BS = 4, NCL = 2;
+
+// d_back_ric_rec_sv_tv_res runs the two-wave kernel (hk_ric2.hip: the tile recursion on one wave, fetch / row half /
+// stores on the other) unless HPMPC_MI355X_RIC_WAVES=1 asks for the one-wave kernel, or the two-wave launch guard
+// refuses the launch (HK_LAUNCH_REFUSED = -2, hk_launch_guard.h); every other entry point is hk_launch's.
+int launch(int which, const KArgs* a, int count, hipStream_t s) {
+    if (which == K_SV) {
+        const char* e = getenv("HPMPC_MI355X_RIC_WAVES");
+        if (!(e && e[0] == '1')) {
+            const int r = hk_launch_ric2(which, a, count, s);
+            if (r != -2) return r;
+        }
+    }
+    return hk_launch(which, a, count, s);
+}
 
 struct StageInfoH {  // mirror of hk::StageInfo
     int nu, nx, nb, ng, xo, nx1, nu1, xo1, sdB, sdR, oB, oR, oD, pnb, r0, oG;
@@ -100,9 +115,16 @@ struct hpmpc_mi355x_plan {
     std::vector<signed char> tileslot, slotvar;
     std::vector<long long> offB, offR;  // packed default layout
     long long packB = 0, packR = 0;
-    void* d_st = nullptr;
+    void* d_st = nullptr;  // the stage table of the packed default layout (uploaded once, never rewritten)
     signed char *d_tileslot = nullptr, *d_slotvar = nullptr;
-    std::vector<long long> dev_offB, dev_offR;  // offsets currently uploaded into d_st
+    // one device stage table per caller layout (hpmpc_mi355x_layout: offsets and shared-block flags differ), uploaded
+    // the first time a layout is used and never rewritten: a launch still running on another stream keeps reading its
+    // own layout's offsets while the next call uses a different one
+    struct LayoutTable {
+        std::vector<StageInfoH> st;
+        void* d = nullptr;
+    };
+    std::vector<LayoutTable> ltabs;
     int fixcls = 0;                             // compiled inner-stage class (kernel instance)
     int nbt = 0;                                // sum of nb + ng
     int ngt = 0;                                // sum of ng
@@ -114,6 +136,12 @@ namespace {
 
 bool plan_supported(int N, const int* nx, const int* nu, const int* nb, const int* const* idxb, const int* ng,
                     const char** why) {
+    // the tile kernels stage the plan's tables in LDS, 256 B + 104 B per stage (hpmpc_kernels.hip launch_t: Scratch +
+    // StageInfo + tile / slot tables + the certificate bounds), within the 160 KiB one workgroup may use
+    if (256 + 104LL * (N + 1) > 160 * 1024) {
+        *why = "horizon beyond the LDS stage tables of the tile kernels (N <= 1571)";
+        return false;
+    }
     for (int k = 0; k <= N; k++) {
         const int u = k < N ? nu[k] : 0;
         if (ng[k] < 0 || rup(nb[k], 4) + rup(ng[k], 4) > 16) {
@@ -149,25 +177,29 @@ bool plan_supported(int N, const int* nx, const int* nu, const int* nb, const in
 
 // Stage offsets (and the shared-block flags, StageInfo r0 bits 1 / 2: the block of stage k sits at the batch's
 // base + offset for every problem) into the device stage table; re-uploaded only when they change.
-bool plan_upload_stages(hpmpc_mi355x_plan* P, const long long* offB, const long long* offR,
-                        const unsigned char* shB = nullptr, const unsigned char* shR = nullptr) {
+// The device stage table for the given stage offsets and shared-block flags: the plan's default table when they are
+// the packed defaults, else the table of that layout (uploaded on first use, cached for the plan's lifetime).
+const void* plan_stage_table(hpmpc_mi355x_plan* P, const long long* offB, const long long* offR,
+                             const unsigned char* shB = nullptr, const unsigned char* shR = nullptr) {
     const int N = P->N;
-    std::vector<int> fl(N + 1);
-    for (int k = 0; k <= N; k++)
-        fl[k] = (P->st[k].r0 & 1) | ((shB && k < N && shB[k]) ? 2 : 0) | ((shR && shR[k]) ? 4 : 0);
-    bool same = !P->dev_offB.empty();
-    for (int k = 0; same && k < N; k++) same = P->dev_offB[k] == offB[k];
-    for (int k = 0; same && k <= N; k++) same = P->dev_offR[k] == offR[k] && P->st[k].r0 == fl[k];
-    if (same) return true;
+    std::vector<StageInfoH> st = P->st;
     for (int k = 0; k <= N; k++) {
-        P->st[k].oB = k < N ? (int)offB[k] : 0;
-        P->st[k].oR = (int)offR[k];
-        P->st[k].r0 = fl[k];
+        st[k].oB = k < N ? (int)offB[k] : 0;
+        st[k].oR = (int)offR[k];
+        st[k].r0 = (P->st[k].r0 & 1) | ((shB && k < N && shB[k]) ? 2 : 0) | ((shR && shR[k]) ? 4 : 0);
     }
-    P->dev_offB.assign(offB, offB + N);
-    P->dev_offR.assign(offR, offR + N + 1);
-    return hip_ok(hipMemcpy(P->d_st, P->st.data(), sizeof(StageInfoH) * (N + 1), hipMemcpyHostToDevice),
-                  "plan stage upload");
+    const size_t bytes = sizeof(StageInfoH) * (N + 1);
+    if (!memcmp(st.data(), P->st.data(), bytes)) return P->d_st;
+    for (const auto& t : P->ltabs)
+        if (!memcmp(st.data(), t.st.data(), bytes)) return t.d;
+    void* d = nullptr;
+    if (!hip_ok(hipMalloc(&d, bytes), "layout stage table")) return nullptr;
+    if (!hip_ok(hipMemcpy(d, st.data(), bytes, hipMemcpyHostToDevice), "layout stage table")) {
+        (void)hipFree(d);
+        return nullptr;
+    }
+    P->ltabs.push_back({std::move(st), d});
+    return d;
 }
 
 // Per-problem workspace (device carve in hpmpc_kernels.hip): rounded to 256 B, so that every slot of a batch or queue
@@ -250,12 +282,16 @@ extern "C" hpmpc_mi355x_plan* hpmpc_mi355x_plan_create(int N, const int* nx, con
                                   ? 1
                                   : 0;
     }
+    for (int k = 0; k <= N; k++) {  // the packed default layout
+        P->st[k].oB = k < N ? (int)P->offB[k] : 0;
+        P->st[k].oR = (int)P->offR[k];
+    }
     bool ok = hip_ok(hipMalloc(&P->d_st, sizeof(StageInfoH) * (N + 1)), "plan alloc") &&
               hip_ok(hipMalloc((void**)&P->d_tileslot, (N + 1) * 16), "plan alloc") &&
               hip_ok(hipMalloc((void**)&P->d_slotvar, (N + 1) * 16), "plan alloc") &&
               hip_ok(hipMemcpy(P->d_tileslot, P->tileslot.data(), (N + 1) * 16, hipMemcpyHostToDevice), "plan") &&
               hip_ok(hipMemcpy(P->d_slotvar, P->slotvar.data(), (N + 1) * 16, hipMemcpyHostToDevice), "plan") &&
-              plan_upload_stages(P, P->offB.data(), P->offR.data());
+              hip_ok(hipMemcpy(P->d_st, P->st.data(), sizeof(StageInfoH) * (N + 1), hipMemcpyHostToDevice), "plan");
     if (!ok) {
         hpmpc_mi355x_plan_destroy(P);
         return nullptr;
@@ -267,6 +303,7 @@ extern "C" hpmpc_mi355x_plan* hpmpc_mi355x_plan_create(int N, const int* nx, con
 extern "C" void hpmpc_mi355x_plan_destroy(hpmpc_mi355x_plan* P) {
     if (!P) return;
     if (P->d_st) (void)hipFree(P->d_st);
+    for (auto& t : P->ltabs) (void)hipFree(t.d);
     if (P->d_tileslot) (void)hipFree(P->d_tileslot);
     if (P->d_slotvar) (void)hipFree(P->d_slotvar);
     delete P;
@@ -318,9 +355,8 @@ bool layout_apply(hpmpc_mi355x_plan* P, const hpmpc_mi355x_layout* lay, KArgs& a
         return false;
     }
     if (lay && lay->BAbt_off && lay->RSQrq_off) {
-        if (!plan_upload_stages(P, lay->BAbt_off, lay->RSQrq_off, lay->BAbt_shared, lay->RSQrq_shared)) return false;
-    } else if (!plan_upload_stages(P, P->offB.data(), P->offR.data())) {
-        return false;
+        a.st = plan_stage_table(P, lay->BAbt_off, lay->RSQrq_off, lay->BAbt_shared, lay->RSQrq_shared);
+        if (!a.st) return false;
     }
     a.sB = lay ? lay->BAbt_stride : P->packB;
     a.sR = lay ? lay->RSQrq_stride : P->packR;
@@ -631,7 +667,7 @@ extern "C" int hpmpc_mi355x_ric_sv_batch(const hpmpc_mi355x_plan* plan, const hp
     a.compute_pi = compute_pi;
     a.compute_Pb = compute_Pb && Pb;
     a.vPb = Pb;
-    int e = hk_launch(K_SV, &a, count, (hipStream_t)stream);
+    int e = launch(K_SV, &a, count, (hipStream_t)stream);
     if (e) {
         set_err(HPMPC_MI355X_EHIP, "hk_ric_sv launch failed");
         return HPMPC_MI355X_EHIP;
@@ -840,7 +876,7 @@ void stage_gen_q(const hpmpc_mi355x_plan* P, double* H, size_t off, double** v) 
 }
 
 bool run(int which, const KArgs& a, const char* name) {
-    int e = hk_launch(which, &a, 1, g_ctx.stream);
+    int e = launch(which, &a, 1, g_ctx.stream);
     if (e) {
         char msg[128];
         snprintf(msg, sizeof msg, "%s launch failed (%d)", name, e);

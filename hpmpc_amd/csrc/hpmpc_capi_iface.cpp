@@ -279,12 +279,15 @@ void outputs(Carve& C, int* nx, int* nb, int** hidxb, int* ng, double** lb, doub
 // work0's header (the first 64 bytes of the carve): [0] the horizon the IPM ran on (N2), [1] a tag, [2] N -- so that
 // the KKT re-solve can tell a work space the IPM wrapper wrote from one it never saw.
 constexpr double WORK0_TAG = 0x1.48504d5043e5fp+33;
+// Set only after a solve that left its factor in work0; cleared (clear_work0) when a wrapper call starts, so that a
+// call that returns early (size error, condensing error, a device failure) leaves a work space the re-solve refuses.
 void mark_work0(char* base, int N2, int N) {
     double* h = reinterpret_cast<double*>(base);
     h[0] = N2;
     h[1] = WORK0_TAG;
     h[2] = N;
 }
+void clear_work0(char* base) { reinterpret_cast<double*>(base)[1] = 0.0; }
 
 int ip_ocp(bool rowmajor, int* kk, int k_max, double mu0, double mu_tol, int N, int* nx, int* nu_N, int* nb,
            int** hidxb, int* ng, int N2, int warm_start, double** A, double** B, double** b, double** Q, double** S,
@@ -310,7 +313,7 @@ int ip_ocp(bool rowmajor, int* kk, int k_max, double mu0, double mu_tol, int N, 
         for (int j = 0; j < nx[N]; j++) mu0 = fmax(mu0, q[N][j]);
     }
     const double alpha_min = 1e-8;
-    mark_work0(base, C.N2, N);
+    clear_work0(base);
     int status;
     if (C.N2 < N) {  // partial condensing (:388-545)
         const int N2c = C.N2;
@@ -355,6 +358,7 @@ int ip_ocp(bool rowmajor, int* kk, int k_max, double mu0, double mu_tol, int N, 
                                C.rq.data(), C.DCt.data(), C.ux.data(), C.pi.data(), C.lam.data(), C.t.data(), N2c,
                                C.nx2.data(), C.nu2.data(), C.nb2.data(), idxb2.data(), C.ng2.data(), ux2.data(),
                                pi2.data(), lam2.data(), t2.data(), wpx);
+        if (hpmpc_mi355x_last_error()) return hpmpc_mi355x_last_error();
     } else {
         if (warm_start) {
             for (int k = 0; k < N; k++)
@@ -367,6 +371,7 @@ int ip_ocp(bool rowmajor, int* kk, int k_max, double mu0, double mu_tol, int N, 
                                        1, C.pi.data(), C.lam.data(), C.t.data(), C.ws);
         if (status <= HPMPC_MI355X_EUNSUPPORTED) return status;
     }
+    mark_work0(base, C.N2, N);
     outputs(C, nx, nb, hidxb, ng, lb, ub, x, u, pi, lam, inf_norm_res);
     return status;
 }
@@ -420,13 +425,14 @@ extern "C" int fortran_order_d_ip_ocp_hard_tv_single_newton_step(
     Carve C;
     carve(C, base, N, nx, nu_N, nb, hidxb, ng, N);
     pack_problem(C, nx, nb, hidxb, ng, false, A, B, b, Q, S, R, q, r, lb, ub, Cm, D, lg, ug, true);
-    mark_work0(base, N, N);
+    clear_work0(base);
     const double alpha_min = 1e-8;
     const int status = d_ip2_res_mpc_hard_tv_single_newton_step(
         kk, k_max, mu0, mu_tol, alpha_min, warm_start, stat, N, nx, C.nu.data(), nb, hidxb, ng, C.BAbt.data(),
         C.RSQ.data(), C.DCt.data(), C.d.data(), C.ux.data(), 1, C.pi.data(), C.lam.data(), C.t.data(), C.ws, ux0, pi0,
         lam0, t0);
     if (status <= HPMPC_MI355X_EUNSUPPORTED) return status;
+    mark_work0(base, N, N);
     outputs(C, nx, nb, hidxb, ng, lb, ub, x, u, pi, lam, inf_norm_res, t);
     return status;
 }

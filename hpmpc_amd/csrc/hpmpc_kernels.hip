@@ -140,12 +140,25 @@ __global__ __launch_bounds__(64) void hk_ric_sv(KArgs a) {
     bc.Qx = a.vQx ? a.vQx + o16 : nullptr;
     bc.qx = a.vqx ? a.vqx + o16 : nullptr;
     double* Pb = a.vPb ? a.vPb + o16 : nullptr;
+#ifdef HK_STAMPS  // diagnostic build: the two sweeps of problem 0 (cycles), a.dbg[60] backward, [61] forward
+    const unsigned long long t0 = mw_clock();
+#endif
     if (a.use_box)
         ric_backward<true, BX_GIVEN, FX, CERT_LOAD, HK_RIC_PD>(io, &sm, a.update_b, b, a.update_q, q, bc, a.compute_Pb, Pb);
     else
         ric_backward<true, BX_NONE, FX, CERT_LOAD, HK_RIC_PD>(io, &sm, a.update_b, b, a.update_q, q, bc, a.compute_Pb, Pb);
     wsync();
+#ifdef HK_STAMPS
+    const unsigned long long t1 = mw_clock();
+#endif
     ric_forward_sv<FX>(io, &sm, a.update_b, b, a.ux + o16, a.compute_pi, a.pi + o16);
+#ifdef HK_STAMPS
+    const unsigned long long t2 = mw_clock();
+    if (a.dbg && p == 0 && lane_id() == 0) {
+        a.dbg[60] = t1 - t0;
+        a.dbg[61] = t2 - t1;
+    }
+#endif
 }
 
 template <class FX>

@@ -124,3 +124,28 @@ class Reducer:
 
     def sum(self, x: float) -> float:
         return self._all_reduce(x, None if self.dist is None else self.dist.ReduceOp.SUM)
+
+
+COUPLED_SEED = 7
+
+
+def coupled_shard(N: int, nx: int, nu: int, rank: int, world: int, per_rank: int, *, boxes: bool = True) -> OCPQP:
+    """The benchmark block (make_shard) with strongly coupled stage Hessians: every stage's [R S'; S Q] becomes
+    diag(R, Q) + G G' / nux with G ~ N(0, 1) (nux x nux) from PCG64([COUPLED_SEED, p]) for global problem p (the
+    random_qp style of the parity tests).  The blocks stay positive definite (lambda_min >= 1) but are far from
+    diagonally dominant, so Gershgorin's bound on them is negative: the workload of the clamp certificate's
+    shifted-Cholesky bound (hk_riccati.h cert_g_shift; VERDICT r4 item 5, bench.py 'coupled')."""
+    from .ocp import pack_lib4_batch, unpack_lib4
+
+    qp = make_shard(N, nx, nu, rank, world, per_rank, boxes=boxes)
+    start, stop = shard_range(rank, world, per_rank)
+    G = np.empty((stop - start, N + 1, nx + nu, nx + nu))
+    for i, p in enumerate(range(start, stop)):
+        G[i] = np.random.Generator(np.random.PCG64([COUPLED_SEED, p])).standard_normal(G.shape[1:])
+    for k in range(N + 1):
+        nux = qp.nux(k)
+        M = np.stack([unpack_lib4(qp.RSQrq[k][i], nux + 1, nux) for i in range(stop - start)])
+        Gk = G[:, k, :nux, :nux]
+        M[:, :nux, :nux] += Gk @ np.swapaxes(Gk, 1, 2) / max(nux, 1)
+        qp.RSQrq[k] = pack_lib4_batch(M)
+    return qp

@@ -246,3 +246,20 @@ def test_kkt_wrapper_refuses_unwritten_work0(fill):
     r = api.kkt_ocp(P, work0)
     assert api.lib.hpmpc_mi355x_last_error() == EUNSUPPORTED
     assert all(not np.any(x) for x in r["x"]) and all(not np.any(u) for u in r["u"])
+
+
+def test_plan_rejects_horizon_beyond_lds_tables(hiplib):
+    """the tile kernels keep 104 B of stage tables per stage in LDS (+ 256 B); a horizon whose tables exceed
+    the 160 KiB of one workgroup is refused when the plan is created, before any device allocation (N <= 1571)."""
+    L = hiplib
+    L.hpmpc_mi355x_plan_create.restype = C.c_void_p
+    L.hpmpc_mi355x_plan_create.argtypes = [C.c_int] + [C.c_void_p] * 5
+    N = 1572
+    nxv = np.array([0] + [4] * N, dtype=np.int32)
+    nuv = np.array([2] * N + [0], dtype=np.int32)
+    z = np.zeros(N + 1, dtype=np.int32)
+    idx = (C.POINTER(C.c_int) * (N + 1))()
+    p = L.hpmpc_mi355x_plan_create(N, nxv.ctypes.data, nuv.ctypes.data, z.ctypes.data, C.cast(idx, C.c_void_p),
+                                   z.ctypes.data)
+    assert not p
+    assert L.hpmpc_mi355x_last_error() == EUNSUPPORTED

@@ -158,3 +158,33 @@ def test_ip_mpc_goldens_row_major(product):
     assert len(cases) >= 7
     for c in cases:
         check_iface(c, run_iface_mpc(product, c, order="C"))
+
+
+def test_kkt_wrapper_refuses_after_failed_ipm():
+    """the wrapper tags work0 as holding an IPM factor only after a successful solve.  In the diagnostic
+    build (libhpmpc_mi355x_stamps.so) with HPMPC_MI355X_MW_FAULT=1 the multi-wave IPM kernel drops a hand-over and the
+    solve returns -20 (HPMPC_MI355X_EMW) without copying anything out; the KKT re-solve on that work0 must then refuse
+    (HPMPC_MI355X_EUNSUPPORTED) and leave its outputs untouched.  A child process (the library is chosen at import)."""
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(root, "hpmpc_amd", "lib", "libhpmpc_mi355x_stamps.so")
+    assert os.path.exists(lib), "diagnostic build missing (hpmpc_amd/build.py build_stamps, run by build())"
+    code = r"""
+import sys, numpy as np
+sys.path.insert(0, "oracle")
+import iface_oracle as IO
+from hpmpc_amd.batch import LIBPATH
+from hpmpc_amd.cabi import HpmpcAPI, load
+api = HpmpcAPI(load(LIBPATH))
+P = IO.random_iface_problem(10, [0] + [4] * 10, [2] * 10, 2, 2, None, seed=5)
+r = api.ip_ocp(P, 10, mu_tol=1e-10)
+assert r["status"] == -20, r["status"]
+got = api.kkt_ocp(IO.new_rhs(P, seed=6), r["work0"])
+assert api.lib.hpmpc_mi355x_last_error() == -10, api.lib.hpmpc_mi355x_last_error()
+assert all(not np.any(v) for key in ("u", "x", "pi", "lam") for v in got[key])
+print("refused")
+"""
+    env = dict(os.environ, HPMPC_MI355X_LIB=lib, HPMPC_MI355X_MW_FAULT="1", PYTHONPATH=root)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=180, env=env, cwd=root)
+    assert r.returncode == 0 and "refused" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]

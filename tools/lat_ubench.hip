@@ -15,6 +15,19 @@ __device__ __forceinline__ unsigned long long now() {
 #define DPP(a) asm volatile("v_mov_b32_dpp %0, %0 row_newbcast:3 row_mask:0xf bank_mask:0xf" : "+v"(a))
 #define PL16(a, b) asm volatile("v_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b))
 #define FMA32(a, b, c) asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(a) : "v"(b), "v"(c))
+// f64 MFMA 16x16x4: dependent accumulator chain, and its result read by a VALU op
+#define MFMA64(acc, a, b) asm volatile("v_mfma_f64_16x16x4_f64 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b))
+#define MFMA64USE(acc, a, b)                                             \
+    do {                                                                 \
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0); \
+        a = a + acc[0];                                                  \
+    } while (0)
+#define DPP64(a) asm volatile("v_mov_b64_dpp %0, %0 row_newbcast:3 row_mask:0xf bank_mask:0xf" : "+v"(a))
+#define PL32(a, b) asm volatile("v_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b))
+// LDS round trip: write then read back the same address (dependent through the value)
+#define LDSRT(p, a) asm volatile("ds_write_b64 %1, %0\n\ts_waitcnt lgkmcnt(0)\n\tds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "+v"(a) : "v"(p) : "memory")
+// readlane of a double's low half + scalar compare + branch (a ballot-like wave-uniform decision)
+#define RDL(a, i) asm volatile("v_readfirstlane_b32 %0, %1\n\ts_add_u32 %0, %0, 1\n\tv_mov_b32 %1, %0" : "=s"(i) : "v"(a))
 
 #define TIME(slot, ...)                      \
     {                                         \
@@ -43,8 +56,20 @@ extern "C" __global__ __launch_bounds__(64) void lat(double* out, unsigned long 
     TIME(7, DPP(i0); DPP(i1); DPP(i2); DPP(i3));          // 4 independent dpp movs
     TIME(8, PL16(i0, i1));                                  // dependent permlane16_swap
     TIME(9, RSQ(e0); RSQ(e1); RSQ(e2); RSQ(e3));          // 4 independent rsq
+    typedef double d4v __attribute__((ext_vector_type(4)));
+    d4v acc = {a, a, a, a};
+    TIME(10, MFMA64(acc, b, c));                            // dependent f64 MFMA (accumulator)
+    double u = a;
+    TIME(11, MFMA64USE(acc, u, c));                         // MFMA -> VALU use -> next MFMA operand
+    TIME(12, DPP64(d0));                                    // dependent v_mov_b64_dpp row_newbcast
+    TIME(13, PL32(i0, i1));                                 // dependent permlane32_swap
+    __shared__ double sh[64];
+    const unsigned lp = (unsigned)(l * 8) + (unsigned)(size_t)sh;
+    TIME(14, LDSRT(lp, d1));                                // LDS write -> read round trip
+    int sreg = 0;
+    TIME(15, RDL(i2, sreg));                                // readfirstlane -> SALU -> VALU
     out[l] = a + d0 + d1 + d2 + d3 + e0 + e1 + e2 + e3 + e4 + e5 + e6 + e7 + f0 + f1 + f2 + f3 + f4 + f5 +
-             f6 + f7 + i0 + i1 + i2 + i3;
+             f6 + f7 + i0 + i1 + i2 + i3 + acc[0] + acc[3] + u + sreg;
 }
 
 extern "C" int lat_run(double* out, unsigned long long* cyc, void* stream) {
