@@ -223,6 +223,7 @@ def main():
     cond_parts(ref, out)
     xclamp(ref, out)
     gates(ref, out)
+    xclamp_ipm(ref, out)
     soft_res(ref, out)
     iface(ref, out)
     iface_soft(ref, out)
@@ -325,6 +326,31 @@ def xclamp(ref, out):
         ux, pi, Pb, _ = ref.ric_sv(qp.copy(), compute_pi=1, compute_Pb=1)
         out.append(save_case(f"sv_xclamp_{name}_N10_nx8_nu3", "sv_xclamp", qp, dict(compute_pi=1, compute_Pb=1, **kw),
                              dict(ux=ux, pi=pi, Pb=Pb)))
+
+
+def xclamp_ipm(ref, out):
+    """The clamp problems inside the IPM (tests/test_gpu_parity.py XCLAMP, N=20 with boxes): the c99 answer and the
+    reference builds' spread (c99, c99 + FMA, X64_AVX, X64_AVX2), stored as a gated golden for every variant whose
+    builds spread by more than TOL_IPM / 4 (the GATES rule of gates(): gate = max(1e-10, 4 x spread)).  ADVICE r4: the
+    gate of the one non-converging variant was a hand-measured constant in the test."""
+    from helpers import XCLAMP
+
+    others = x64_apis()
+    for d, off, r in XCLAMP:
+        one = xclamp_qp(N=20, nx=8, nu=3, d=d, off=off, r=r, boxes=True)
+        rs = {"c99": ref.ipm(one.copy(), k_max=50)}
+        rs.update({n: api.ipm(one.copy(), k_max=50) for n, api in others.items()})
+        sp, ds = build_spread(one, rs)
+        print(f"  xclamp d={d:g} off={off:g} r={r:g}: kk {rs['c99']['kk']} ret {rs['c99']['ret']}, build spread "
+              f"{sp:.2e} (stat {ds:.2e})")
+        if not 4 * sp > 1e-10:
+            continue
+        c = rs["c99"]
+        args = dict(k_max=50, mu0=2.0, mu_tol=1e-12, alpha_min=1e-8, xclamp_d=d, xclamp_off=off, xclamp_r=r, spread=sp,
+                    gate=max(1e-10, 4 * sp), stat_gate=max(1e-9, 4 * ds))
+        out.append(save_case(f"ipm_xclamp_d{d:g}_off{off:g}_r{r:g}_N20_nx8_nu3", "ipm", one, args,
+                             dict(ux=c["ux"], pi=c["pi"], lam=c["lam"], t=c["t"], stat=c["stat"], kk=c["kk"],
+                                  ret=c["ret"])))
 
 
 def x64_apis():
@@ -802,6 +828,10 @@ if __name__ == "__main__":
         o = []
         xclamp(ref_api(), o)
         print(f"wrote {len(o)} xclamp cases")
+    elif len(sys.argv) > 1 and sys.argv[1] == "xclamp_ipm":
+        o = []
+        xclamp_ipm(ref_api(), o)
+        print(f"wrote {len(o)} xclamp IPM gate cases")
     elif len(sys.argv) > 1 and sys.argv[1] == "cond_parts":
         o = []
         cond_parts(ref_api(), o)

@@ -359,6 +359,13 @@ def dense_kkt(qp):
     return ux, pi
 
 
+# The clamp variants (d, off, r) of xclamp_qp that tests/test_gpu_parity.py runs through every kernel family: exact
+# clamps, a clamp with a gradient term, a zero pivot, a near-clamp pivot, and two that fail the certificate without a
+# clamp (d = 2e-15 is left out: there the reference's own builds spread by 1e-11).
+XCLAMP = [(1e-16, 1e-9, 0.0), (1e-16, 1e-9, 0.5), (0.0, 0.0, 0.3), (5e-16, 1e-8, 0.2), (1e-8, 1e-9, 0.1),
+          (1e-4, 1e-3, 0.2)]
+
+
 def xclamp_qp(N=10, nx=8, nu=3, d=1e-16, off=1e-9, r=0.0, boxes=False):
     """State 0 of every stage k >= 1 has Hessian diagonal d <= 1e-15, cross terms `off` with the other states,
     gradient r and no effect on the next state (its A' row is zero), so the first x pivot of the reference's

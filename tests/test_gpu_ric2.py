@@ -122,7 +122,7 @@ def test_two_wave_clamp_variants():
     block and hands the x factor over; the row wave adds its row half and p_eff."""
     from hpmpc_amd.batch import BatchSolver
 
-    from test_gpu_parity import XCLAMP as variants
+    from helpers import XCLAMP as variants
 
     qps = [xclamp_qp(N=12, nx=8, nu=3, d=d, off=o, r=r) for d, o, r in variants]
     qp = stack(qps)
