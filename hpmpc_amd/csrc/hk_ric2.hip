@@ -1,29 +1,30 @@
 // hk_ric2.hip -- d_back_ric_rec_sv_tv_res over a batch with TWO waves per problem (gfx950).
 //
 // At the benchmark batches (1024 problems) the one-wave kernel (hpmpc_kernels.hip hk_ric_sv) leaves one wave per
-// SIMD, and that wave is latency-bound: it parks on s_waitcnt for ~47 % of its cycles and issues one instruction per
-// ~17 cycles (profiles/r04b_pmc_mix.json), because every stage interleaves the recursion's dependent chain with
-// the work around it.  Here each problem gets a 128-thread workgroup and the work is split by dependency, as in the
-// multi-wave lone-QP kernel (hk_mw.h) but with two roles and a small LDS footprint (four workgroups per CU):
+// SIMD, and that wave is bound by its own issue: a backward stage of the compiled (4, 12) class executes ~440
+// instructions (tools/loop_icount.py), the SIMD's VALU is ~25 % busy and the wave parks on s_waitcnt for ~47 % of its
+// cycles (profiles/r04b_pmc_mix.json).  Here each problem gets a 128-thread workgroup and the work is split by
+// dependency, as in the multi-wave lone-QP kernel (hk_mw.h) but with two roles and a small LDS footprint (four
+// workgroups per CU):
 //
-//   backward sweep (lqcp_solvers/d_back_ric_rec.c:186-335)
+//   backward sweep (lqcp_solvers/d_back_ric_rec.c:186-335), step j = stage k = N - j
 //     wave 0 (tile): M += BAbt_k P_{k+1} BAbt_k' (MFMA), the clamp certificate (cert_ok) and the tile half of the
 //                    u-block Cholesky -> P_k -- the only chain that carries the recursion forward;
-//     wave 1 (row):  fetches stage k two stages ahead of wave 0 and hands it the ready tile (RSQ + box, bwd_pre) with
-//                    the BAbt operand; then, one stage behind wave 0, the augmented row (P b, ml += BAbt (P b + p),
-//                    the row half of the Cholesky, the gain block) and the stage record -- a second recursion
-//                    (p_{k+1} -> p_k) that needs wave 0's factor but never feeds it (hk_mw.h, same routines).
-//   forward sweep (:339-397)
+//     wave 1 (row):  one step behind wave 0, the augmented row (P b, ml += BAbt (P b + p), the row half of the Cholesky,
+//                    the gain block) and the stage record -- a second recursion (p_{k+1} -> p_k) that needs wave 0's
+//                    factor but never feeds it (hk_mw.h, same routines) -- then, two steps ahead of wave 0, the fetch
+//                    and the ready tile of stage j + 2 (RSQ + box terms, bwd_pre) with the BAbt operand.
+//   forward sweep (:339-397), in blocks of R2_H stages
 //     wave 0: u_k = KG [rhs_u; x_k] and x_{k+1} = b_k + BAbt_k' ux_k (fwd_chain, the chain only);
-//     wave 1: stores ux_k and forms pi_{k-1} = P_k x_k + p_k from stage k's record (fwd_pi).
-// Every value is produced by the same routine on the same operands as in hk_ric_sv (hk_riccati.h), so results agree
-// with it up to the compiler's FMA contraction (tests/test_gpu_ric2.py holds both to the goldens and the oracle).
+//     wave 1, one block behind: stores ux_k and forms pi_{k-1} = P_k x_k + p_k from stage k's record (fwd_pi).
+// Every value is produced by the same routine on the same operands as in hk_ric_sv (hk_riccati.h), so the results
+// agree with it up to the compiler's FMA contraction (tests/test_gpu_ric2.py holds both to the goldens and the oracle).
 //
-// Hand-over: rings in LDS with ticketed flags (one lane stores the flag after the slot data; the LDS performs one
-// wave's ds_ operations in issue order -- the hk_mw.h argument, including its HK_MW_FENCE option).  Slot reuse needs
-// no "free" flags: the order of the other ring's flags implies it (comments at each ring).  A wait that does not end
-// (a bug, never a data condition) sets r2.err after ~2^22 polls, every later wait falls through, and the problem's
-// ux / pi are overwritten with NaN so that the failure is loud.
+// Synchronisation: the waves exchange through LDS rings and meet at one s_barrier per backward step and one per
+// forward block.  A waiting wave sleeps at the barrier instead of polling a flag (a polling wave takes issue slots from
+// the wave it waits for when they share a SIMD).  The barrier is preceded by s_waitcnt lgkmcnt(0) only: the ring writes
+// are complete, wave 1's prefetched loads stay in flight across it.  Every slot's reuse is ordered by a barrier (the
+// comments at each ring say which).
 #include "hk_mw.h"
 #include "hk_launch_guard.h"
 #include "hpmpc_kargs.h"
@@ -32,68 +33,64 @@ using namespace hk;
 
 namespace {
 
-constexpr int R2_D = 3;      // wave 1 -> wave 0 stage slots (wave 1 runs two stages ahead)
-constexpr int R2_ROWS = 10;  // M (4) | bop (4) | dq | ml
-constexpr int R2_DP = 2;     // wave 0 -> wave 1 factor slots
-constexpr int R2_PROWS = 10; // record tile (4) | inverse diagonal | a clamped stage's x factor (4) and inverse diagonal
-constexpr int R2_FD = 8;     // forward slots: [ucol | xcol]
-constexpr int R2_ERR_POLLS = 1 << 22;
+constexpr int R2_D = 3;       // backward stage slots (wave 1 writes step j + 2 while wave 0 reads step j + 1)
+constexpr int R2_ROWS = 10;   // M (4) | bop (4) | dq | ml
+constexpr int R2_DP = 2;      // backward factor slots (wave 0 writes step j, wave 1 reads step j - 1)
+constexpr int R2_PROWS = 10;  // record tile (4) | inverse diagonal | a clamped stage's x factor (4) and inverse diagonal
+constexpr int R2_H = 6;       // forward block (stages per barrier)
 
 struct R2Shared {
     union {
         double mring[R2_D][R2_ROWS][64];
-        double fring[R2_FD][2][64];  // the forward sweep re-uses the backward's stage ring
+        double fring[2 * R2_H][2][64];  // forward: [ucol | xcol] of two blocks, over the backward's stage ring
     };
     double pring[R2_DP][R2_PROWS][64];
     Scratch sm[2];
     double mgc[R2_D];  // the stage's certificate bound g (wave-uniform)
-    int mfull[R2_D], pfull[R2_DP], xfac[R2_DP], ffull[R2_FD];
-    int fdone;  // forward stages wave 1 has read
-    int rdone;  // backward steps whose row half wave 1 has finished (read at the last step only)
-    int err;
+    int xfac[R2_DP];
 };
-static_assert(sizeof(double) * R2_FD * 2 * 64 <= sizeof(double) * R2_D * R2_ROWS * 64, "forward ring overlay");
+static_assert(2 * R2_H * 2 <= R2_D * R2_ROWS, "forward ring overlay");
 
 // one object per workgroup, referred to by name (every access stays a ds_ op; hk_mw.h)
 __shared__ R2Shared r2;
 
-// Diagnostic build (-DHK_STAMPS, tools/ric_waves_probe.py --stamps): s_memtime segment totals of problem 0 into
-// KArgs.dbg -- [0..3] wave 0's backward step by segment (hand-over in, tile update + certificate, Cholesky, hand-over
-// out), [4] / [5] each wave's backward sweep, [6] / [7] each wave's forward sweep, [8] wave 1's waits for the factor,
-// [9] wave 0's forward waits for free slots, [10] wave 1's forward waits.  Stamps wait for the wave's LDS operations.
+// The two waves' meeting point: this wave's LDS writes are complete, then the workgroup barrier (no vmcnt wait).
+__device__ __forceinline__ void r2_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Diagnostic build (-DHK_STAMPS, tools/ric_waves_probe.py --stamps): s_memtime totals of problem 0 into KArgs.dbg --
+// [0] / [1] wave 0's backward work / barrier wait, [2] / [3] wave 1's, [4] / [5] wave 0's forward work / wait, [6] / [7]
+// wave 1's; wave 0's backward step by segment: [8] shape dispatch, [9] tile update + certificate, [10] Cholesky tile
+// half, [11] the whole step before the barrier.  Stamps wait for the wave's LDS operations.
 #ifdef HK_STAMPS
 __device__ unsigned long long* r2_dbg;
-#define R2_CLK(v) const unsigned long long v = mw_clock()
+#define R2_T0(v) unsigned long long v = mw_clock()
 #define R2_ADD(i, d)                                                         \
     do {                                                                     \
         if (r2_dbg && blockIdx.x == 0 && lane_id() == 0) r2_dbg[i] += (d); \
     } while (0)
-#else
-#define R2_CLK(v) \
-    do {          \
+// a barrier whose wait is charged to stamp slot i, the work since the previous barrier to slot i - 1
+#define R2_STEP_BAR(tprev, i)                      \
+    do {                                           \
+        const unsigned long long t_a = mw_clock(); \
+        r2_bar();                                  \
+        const unsigned long long t_b = mw_clock(); \
+        R2_ADD((i) - 1, t_a - tprev);              \
+        R2_ADD(i, t_b - t_a);                      \
+        tprev = t_b;                               \
     } while (0)
-#define R2_ADD(i, d) \
+#else
+#define R2_T0(v) \
+    do {         \
+    } while (0)
+#define R2_STEP_BAR(tprev, i) r2_bar()
+#endif
+#ifdef HK_STAMPS
+#define R2_SEG(i, d) R2_ADD(i, d)
+#else
+#define R2_SEG(i, d) \
     do {             \
     } while (0)
 #endif
-
-__device__ __forceinline__ int r2_flag(const int* f) { return __atomic_load_n(f, __ATOMIC_RELAXED); }
-
-__device__ __forceinline__ void r2_wait(const int* f, int v) {
-    int n = 0;
-    while (r2_flag(f) < v) {
-        if (++n > 64) __builtin_amdgcn_s_sleep(1);
-        if (n > R2_ERR_POLLS) __atomic_store_n(&r2.err, 1, __ATOMIC_RELAXED);
-        if (r2_flag(&r2.err)) break;
-    }
-    mw_acquire_fence();
-}
-
-__device__ __forceinline__ void r2_post(int* f, int v) {
-    mw_release_fence();
-    if (lane_id() == 0) __atomic_store_n(f, v, __ATOMIC_RELAXED);
-    asm volatile("" ::: "memory");
-}
 
 // The stage-table copies of lds_tables (hpmpc_kernels.hip) for a 128-thread workgroup: StageInfo[N+1] and the
 // tile -> box-slot table (the sv's box terms); the rings are the static r2 object.
@@ -113,14 +110,6 @@ __device__ __forceinline__ R2Tabs r2_tables(const KArgs& a) {
     const int* gt = reinterpret_cast<const int*>(a.tileslot);
     int* lt = reinterpret_cast<int*>(ts);
     for (int i = t; i < n1 * 4; i += 128) lt[i] = gt[i];
-    if (t < R2_D) r2.mfull[t] = 0;
-    if (t < R2_DP) r2.pfull[t] = 0;
-    if (t < R2_FD) r2.ffull[t] = 0;
-    if (t == 0) {
-        r2.fdone = 0;
-        r2.rdone = 0;
-        r2.err = 0;
-    }
     __syncthreads();
     return R2Tabs{st, ts};
 }
@@ -150,82 +139,74 @@ __device__ __forceinline__ void row_fetch(const RicIO& io, const SH& sh, int k, 
 }
 
 // ------------------------------------------------------------------------------------------------
-// Backward sweep.  Step j is stage k = N - j.
+// Backward sweep.  Step j is stage k = N - j; steps 0 .. N + 1 (wave 1's row half of stage 0 is step N + 1), each
+// ending at one barrier of both waves; a prologue barrier hands over the first two tiles.
+//   stage slot s % 3: written by wave 1 (prep) at step s - 2 (s = 0, 1: the prologue), read by wave 0 at step s - 1
+//     (its next tile, into registers at the end of the step) and by wave 1's row half at step s + 1 (ml), before
+//     wave 1 overwrites it with stage s + 3 in the same step;
+//   factor slot s % 2: written by wave 0 at step s, read by wave 1 at step s + 1; rewritten at step s + 2.
 // ------------------------------------------------------------------------------------------------
 template <int BM, class FX>
 __device__ __forceinline__ void ric_backward2(const RicIO& io, int w, int update_b, const double* bsrc, int update_q,
                                               const double* qsrc, const BoxCtx& bc, int compute_Pb, double* Pb) {
     const int N = io.N, l = lane_id();
     if (w == 0) {
-        // The tile recursion.  Stage slot j + 1 is read at the start of step j (one step ahead), so its LDS latency is
-        // off the chain.  Factor slot j % R2_DP is free when written at step j: its previous occupant (step j - 2) was
-        // read by wave 1's row half of step j - 2, which precedes (program order) wave 1's post of stage slot j + 1
-        // (its step j - 1), and this wave waited for that post (take) at the start of step j.  The last step has no
-        // take: it waits for the row half of step N - 2 explicitly.
         d4 P = {0.0, 0.0, 0.0, 0.0};  // record tile of stage k+1 (its x block is P_{k+1})
-        d4 Mn, bopn;
-        double dqn, gcn;
-        auto take = [&](int j) __attribute__((always_inline)) {
-            const int s = j % R2_D;
-            r2_wait(&r2.mfull[s], j + 1);
+        d4 M, bop;
+        double dq, gc;
+        auto take = [&](int s) __attribute__((always_inline)) {
+            const int q = s % R2_D;
 #pragma unroll
             for (int r = 0; r < 4; r++) {
-                Mn[r] = r2.mring[s][r][l];
-                bopn[r] = r2.mring[s][4 + r][l];
+                M[r] = r2.mring[q][r][l];
+                bop[r] = r2.mring[q][4 + r][l];
             }
-            dqn = r2.mring[s][8][l];
-            gcn = r2.mgc[s];
+            dq = r2.mring[q][8][l];
+            gc = r2.mgc[q];
         };
-        R2_CLK(tb0);
+        R2_T0(tp);
+        r2_bar();  // prologue: stage slots 0 and 1
         take(0);
-        for (int j = 0; j <= N; j++) {
-            const int k = N - j;
-            d4 M = Mn;
-            const d4 bop = bopn;
-            const double dq = dqn, gc = gcn;
-            R2_CLK(ta);
-            if (j < N) take(j + 1);
-            else if (N >= 2) r2_wait(&r2.rdone, N - 1);
-            R2_CLK(tt);
-            R2_ADD(0, tt - ta);
-            double invd;
-            bool xfac = false;
-            XFac xf;
-            with_shape<FX>(StageRef{io.st, k}, [&](const auto& sh) {
-                using SHT = std::remove_reference_t<decltype(sh)>;
-                bwd_tile_update(sh, SHT::fixed || k < N, bop, P, M);
-                double mld = 0.0;
-                const bool full = !SHT::fixed && k == 0;
-                xfac = !full && !cert_ok(M, dq, gc);
-                R2_CLK(tc);
-                R2_ADD(1, tc - tt);
-                stage_chol<false, false>(M, mld, invd, sh.nu, sh.nx, sh.xo, full, !SHT::fixed, nullptr, k, xfac, &xf);
-                R2_CLK(td);
-                R2_ADD(2, td - tc);
-            });
-            R2_CLK(te);
-            P = M;
-            const int s = j % R2_DP;
+        for (int j = 0; j <= N + 1; j++) {
+            if (j <= N) {
+                const int k = N - j;
+                double invd;
+                bool xfac = false;
+                XFac xf;
+                R2_T0(ts0);
+                with_shape<FX>(StageRef{io.st, k}, [&](const auto& sh) {
+                    using SHT = std::remove_reference_t<decltype(sh)>;
+                    R2_T0(ts1);
+                    bwd_tile_update(sh, SHT::fixed || k < N, bop, P, M);
+                    double mld = 0.0;
+                    const bool full = !SHT::fixed && k == 0;
+                    xfac = !full && !cert_ok(M, dq, gc);
+                    R2_T0(ts2);
+                    stage_chol<false, false>(M, mld, invd, sh.nu, sh.nx, sh.xo, full, !SHT::fixed, nullptr, k, xfac,
+                                             &xf);
+                    R2_T0(ts3);
+                    R2_SEG(8, ts1 - ts0);
+                    R2_SEG(9, ts2 - ts1);
+                    R2_SEG(10, ts3 - ts2);
+                });
+                P = M;
+                const int s = j % R2_DP;
 #pragma unroll
-            for (int r = 0; r < 4; r++) r2.pring[s][r][l] = P[r];
-            r2.pring[s][4][l] = invd;
-            if (xfac) {  // wave-uniform
+                for (int r = 0; r < 4; r++) r2.pring[s][r][l] = P[r];
+                r2.pring[s][4][l] = invd;
+                if (xfac) {  // wave-uniform
 #pragma unroll
-                for (int r = 0; r < 4; r++) r2.pring[s][5 + r][l] = xf.L[r];
-                r2.pring[s][9][l] = xf.invd;
+                    for (int r = 0; r < 4; r++) r2.pring[s][5 + r][l] = xf.L[r];
+                    r2.pring[s][9][l] = xf.invd;
+                }
+                if (l == 0) r2.xfac[s] = xfac ? 1 : 0;
+                if (j < N) take(j + 1);  // written by wave 1 at step j - 1 (or the prologue)
+                R2_T0(ts4);
+                R2_SEG(11, ts4 - ts0);
             }
-            if (l == 0) r2.xfac[s] = xfac ? 1 : 0;
-            r2_post(&r2.pfull[s], j + 1);
-            R2_CLK(tf);
-            R2_ADD(3, tf - te);
+            R2_STEP_BAR(tp, 1);
         }
-        R2_CLK(tb1);
-        R2_ADD(4, tb1 - tb0);
     } else {
-        // Wave 1: at step j it prepares stage j + 2 for wave 0 (fragments fetched two steps ahead), then runs the row
-        // half and the record of stage j.  Stage slot (j + 2) % R2_D last held step j - 1: wave 1 itself read its
-        // row data at step j - 1, and wave 0 read the rest one step before posting factor slot j - 1, which wave 1's
-        // step j - 1 waited for.
         Scratch* sm = &r2.sm[1];
         auto fetch = [&](int j, BwdFrag& f) __attribute__((always_inline)) {
             const int k = N - j;
@@ -240,32 +221,26 @@ __device__ __forceinline__ void ric_backward2(const RicIO& io, int w, int update
             with_shape<FX>(StageRef{io.st, k}, [&](const auto& sh) {
                 bwd_pre<true, BM, CERT_RT>(io, sh, k, f, bc, M, ml, dq, gc);
             });
-            const int s = j % R2_D;
+            const int q = j % R2_D;
 #pragma unroll
             for (int r = 0; r < 4; r++) {
-                r2.mring[s][r][l] = M[r];
-                r2.mring[s][4 + r][l] = f.bop[r];
+                r2.mring[q][r][l] = M[r];
+                r2.mring[q][4 + r][l] = f.bop[r];
             }
-            r2.mring[s][8][l] = dq;
-            r2.mring[s][9][l] = ml;
-            if (l == 0) r2.mgc[s] = gc;
-            r2_post(&r2.mfull[s], j + 1);
+            r2.mring[q][8][l] = dq;
+            r2.mring[q][9][l] = ml;
+            if (l == 0) r2.mgc[q] = gc;
         };
         d4 P1 = {0.0, 0.0, 0.0, 0.0};  // record tile of stage k+1
         double ml_prev = 0.0;           // its row [l_u; p_{k+1}]
         auto row = [&](int j, const RowFrag& rf) __attribute__((always_inline)) {
             const int k = N - j;
-            const int s = j % R2_D;
-            double ml = r2.mring[s][9][l];
+            double ml = r2.mring[j % R2_D][9][l];
             with_shape<FX>(StageRef{io.st, k}, [&](const auto& sh) {
                 using SHT = std::remove_reference_t<decltype(sh)>;
                 bwd_row_update(io, sm, sh, k, SHT::fixed || k < N, rf.bop, rf.brow, P1, ml_prev, compute_Pb, Pb, ml);
             });
             const int sp = j % R2_DP;
-            R2_CLK(tw0);
-            r2_wait(&r2.pfull[sp], j + 1);
-            R2_CLK(tw1);
-            R2_ADD(8, tw1 - tw0);
             d4 S;
 #pragma unroll
             for (int r = 0; r < 4; r++) S[r] = r2.pring[sp][r][l];
@@ -294,69 +269,61 @@ __device__ __forceinline__ void ric_backward2(const RicIO& io, int w, int update
             });
             P1 = S;
             ml_prev = ml;
-            r2_post(&r2.rdone, j + 1);
         };
         auto rfetch = [&](int j, RowFrag& f) __attribute__((always_inline)) {
             const int k = N - j;
             with_shape<FX>(StageRef{io.st, k}, [&](const auto& sh) { row_fetch(io, sh, k, update_b, bsrc, f); });
         };
-        R2_CLK(tb0);
+        R2_T0(tp);
         BwdFrag fa, fb;
         RowFrag ra, rb;
         fetch(0, fa);
         if (1 <= N) fetch(1, fb);
-        rfetch(0, ra);
         prep(0, fa);
         if (2 <= N) fetch(2, fa);
         if (1 <= N) prep(1, fb);
         if (3 <= N) fetch(3, fb);
-        // step j: prep(j + 2) from the fragment fetched at step j - 2, then fetch(j + 4) into it; the row fragment of
-        // step j + 1 is issued before the row half of step j
+        rfetch(0, ra);
+        r2_bar();  // prologue
+        // step j: the row half of step j - 1 (row fragment fetched at step j - 1), the row fragment of step j, then
+        // prep(j + 2) from the fragment fetched at step j - 2 and fetch(j + 4) into it; a pair of steps swaps the roles
         for (int j = 0;;) {
+            if (j >= 1) row(j - 1, rb);
+            if (j + 1 <= N) rfetch(j + 1, rb);
             if (j + 2 <= N) prep(j + 2, fa);
             if (j + 4 <= N) fetch(j + 4, fa);
-            if (j + 1 <= N) rfetch(j + 1, rb);
-            row(j, ra);
-            if (++j > N) break;
+            R2_STEP_BAR(tp, 3);
+            if (++j > N + 1) break;
+            row(j - 1, ra);
+            if (j + 1 <= N) rfetch(j + 1, ra);
             if (j + 2 <= N) prep(j + 2, fb);
             if (j + 4 <= N) fetch(j + 4, fb);
-            if (j + 1 <= N) rfetch(j + 1, ra);
-            row(j, rb);
-            if (++j > N) break;
+            R2_STEP_BAR(tp, 3);
+            if (++j > N + 1) break;
         }
-        R2_CLK(tb1);
-        R2_ADD(5, tb1 - tb0);
     }
 }
 
 // ------------------------------------------------------------------------------------------------
-// Forward sweep: wave 0 -> wave 1 slot k % R2_FD = [ux_k (col) | x_k (col, state tiles only)].  Wave 1 posts fdone
-// every R2_FD / 2 stages; wave 0 checks it once per R2_FD / 2 stages: slots k .. k + R2_FD/2 - 1 are free once
-// stage k + R2_FD/2 - 1 - R2_FD has been read, i.e. fdone >= k + R2_FD/2 - R2_FD.
+// Forward sweep in blocks of R2_H items (item k < N: stage k; item N: x_N): at block b wave 0 computes items
+// [b H, b H + H) into forward slots k % 2H = [ux_k (col) | x_k (col, state tiles only)] while wave 1 stores / forms pi
+// for block b - 1; one barrier per block.  A slot written at block b is read at block b + 1 and rewritten at b + 2.
 // ------------------------------------------------------------------------------------------------
 template <class FX>
 __device__ __forceinline__ void ric_forward2(const RicIO& io, int w, int update_b, const double* bsrc, double* ux,
                                              int compute_pi, double* pi) {
     const int N = io.N, l = lane_id(), g = l >> 4, c = l & 15;
-    constexpr int H = R2_FD / 2;
+    const int nblk = (N + R2_H) / R2_H;  // blocks covering items 0 .. N
     if (w == 0) {
         Scratch* sm = &r2.sm[0];
         double xcol = 0.0;
         FwdFrag f0, f1, f2;
         fwd_fetch_chain_k<0, FX>(io, 0, bsrc, update_b, ux, compute_pi, f0);
         fwd_fetch_chain_k<0, FX>(io, 1 <= N ? 1 : N, bsrc, update_b, ux, compute_pi, f1);
-        R2_CLK(tf0);
         auto put = [&](int k, double u, double x) __attribute__((always_inline)) {
-            if (k >= R2_FD && k % H == 0) {
-                R2_CLK(tw0);
-                r2_wait(&r2.fdone, k + H - R2_FD);
-                R2_CLK(tw1);
-                R2_ADD(9, tw1 - tw0);
-            }
-            const int s = k % R2_FD;
+            const int s = k % (2 * R2_H);
             r2.fring[s][0][l] = u;
             r2.fring[s][1][l] = x;
-            r2_post(&r2.ffull[s], k + 1);
         };
         auto stage = [&](int k, const FwdFrag& fa, FwdFrag& fc) __attribute__((always_inline)) {
             fwd_fetch_chain_k<0, FX>(io, k + 2 <= N ? k + 2 : N, bsrc, update_b, ux, compute_pi, fc);
@@ -365,18 +332,24 @@ __device__ __forceinline__ void ric_forward2(const RicIO& io, int w, int update_
             with_shape<FX>(StageRef{io.st, k}, [&](const auto& sh) { fwd_chain<0>(sm, sh, k, fa, xcol, ucol); });
             put(k, ucol, xk);
         };
-        for (int k = 0;;) {
-            if (k >= N) break;
-            stage(k, f0, f2);
-            if (++k >= N) break;
-            stage(k, f1, f0);
-            if (++k >= N) break;
-            stage(k, f2, f1);
-            ++k;
+        R2_T0(tp);
+        int k = 0, r = 0;  // next item; a stage's fragment is f[r] (three rotating roles)
+        for (int b = 0; b <= nblk; b++) {
+            const int kend = (b + 1) * R2_H < N + 1 ? (b + 1) * R2_H : N + 1;
+            for (; k < kend; k++) {
+                if (k == N) {
+                    put(N, xcol, xcol);
+                } else if (r == 0) {
+                    stage(k, f0, f2);
+                } else if (r == 1) {
+                    stage(k, f1, f0);
+                } else {
+                    stage(k, f2, f1);
+                }
+                r = r == 2 ? 0 : r + 1;
+            }
+            R2_STEP_BAR(tp, 5);
         }
-        put(N, xcol, xcol);
-        R2_CLK(tf1);
-        R2_ADD(6, tf1 - tf0);
     } else {
         Scratch* sm = &r2.sm[1];
         // stage k's record: P_k (pi) and the row [l_u; p_k], in the format of stage k's shape class
@@ -399,15 +372,9 @@ __device__ __forceinline__ void ric_forward2(const RicIO& io, int w, int update_
                 }
             });
         };
-        R2_CLK(tf0);
         auto work = [&](int k, const PiFrag& f) __attribute__((always_inline)) {
-            const int s = k % R2_FD;
-            R2_CLK(tw0);
-            r2_wait(&r2.ffull[s], k + 1);
-            R2_CLK(tw1);
-            R2_ADD(10, tw1 - tw0);
+            const int s = k % (2 * R2_H);
             const double ucol = r2.fring[s][0][l], xk = r2.fring[s][1][l];
-            if (k % H == H - 1 || k == N) r2_post(&r2.fdone, k + 1);
             const DynSh sk(StageRef{io.st, k});
             if (compute_pi && k > 0) {
                 double xrow[4];
@@ -417,18 +384,25 @@ __device__ __forceinline__ void ric_forward2(const RicIO& io, int w, int update_
             const int v = tile_var(c, sk.nu, sk.nx, sk.xo);
             gst(ux, k * V16 + v, k < N ? ucol : xk, g == 0 && v >= 0);
         };
+        R2_T0(tp);
         PiFrag fa, fb;
         fetch(0, fa);
-        for (int k = 0;;) {
-            if (k + 1 <= N) fetch(k + 1, fb);
-            work(k, fa);
-            if (++k > N) break;
-            if (k + 1 <= N) fetch(k + 1, fa);
-            work(k, fb);
-            if (++k > N) break;
+        int k = 0;
+        bool alt = false;
+        for (int b = 0; b <= nblk; b++) {
+            const int kend = b * R2_H < N + 1 ? b * R2_H : N + 1;  // items of blocks 0 .. b - 1
+            for (; k < kend; k++) {
+                if (!alt) {
+                    if (k + 1 <= N) fetch(k + 1, fb);
+                    work(k, fa);
+                } else {
+                    if (k + 1 <= N) fetch(k + 1, fa);
+                    work(k, fb);
+                }
+                alt = !alt;
+            }
+            R2_STEP_BAR(tp, 7);
         }
-        R2_CLK(tf1);
-        R2_ADD(7, tf1 - tf0);
     }
 }
 
@@ -467,16 +441,8 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void h
         ric_backward2<BX_GIVEN, FX>(io, w, a.update_b, b, a.update_q, q, bc, a.compute_Pb, Pb);
     else
         ric_backward2<BX_NONE, FX>(io, w, a.update_b, b, a.update_q, q, bc, a.compute_Pb, Pb);
-    __syncthreads();  // the records stored by wave 1 are read by both waves below; the ring is re-used
+    __syncthreads();  // the records stored by wave 1 are read by both waves below; the stage ring is re-used
     ric_forward2<FX>(io, w, a.update_b, b, a.ux + o16, a.compute_pi, a.pi + o16);
-    __syncthreads();
-    if (r2_flag(&r2.err)) {  // an expired hand-over wait (a bug): make the problem's outputs NaN
-        const double nan = __builtin_nan("");
-        for (int i = threadIdx.x; i < (a.N + 1) * V16; i += 128) {
-            a.ux[o16 + i] = nan;
-            a.pi[o16 + i] = nan;
-        }
-    }
 }
 
 template <class FX>

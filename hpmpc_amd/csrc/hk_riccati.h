@@ -304,42 +304,41 @@ __device__ __forceinline__ bool diag_lane() {
     return (l & 3) == (l >> 4);
 }
 
-// Wave minimum of a double to a conservative f32 bound (<= the exact minimum): one f32 DPP min per row step and two
-// row-group swaps instead of the f64 butterfly; the certificate needs a bound, not the exact value.
+// Wave minimum of a double to a conservative f32 bound (<= the exact minimum): one DPP-sourced f32 min per row step
+// (v_min_f32 with its first operand read through row_ror: no separate move, no NaN canonicalisation) and two row-group
+// swaps instead of the f64 butterfly; the certificate needs a bound, not the exact value.
 __device__ __forceinline__ double wave_min_lb(double x) {
     float f = (float)x;  // round to nearest, then step down one ulp-ish so that f <= x
     f = f - fabsf(f) * 0x1p-22f - 0x1p-126f;
-    f = fminf(f, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, f), 0x128, 0xf, 0xf, true)));
-    f = fminf(f, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, f), 0x124, 0xf, 0xf, true)));
-    f = fminf(f, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, f), 0x122, 0xf, 0xf, true)));
-    f = fminf(f, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, f), 0x121, 0xf, 0xf, true)));
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_min_f32_dpp %0, %0, %0 row_ror:8 row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_min_f32_dpp %0, %0, %0 row_ror:4 row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_min_f32_dpp %0, %0, %0 row_ror:2 row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_min_f32_dpp %0, %0, %0 row_ror:1 row_mask:0xf bank_mask:0xf"
+        : "+v"(f));
     int v = __builtin_bit_cast(int, f);
     const auto a = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-    f = fminf(__builtin_bit_cast(float, (int)a[0]), __builtin_bit_cast(float, (int)a[1]));
+    f = __builtin_fminf(__builtin_bit_cast(float, (int)a[0]), __builtin_bit_cast(float, (int)a[1]));
     v = __builtin_bit_cast(int, f);
     const auto b = __builtin_amdgcn_permlane16_swap(v, v, false, false);
-    return (double)fminf(__builtin_bit_cast(float, (int)b[0]), __builtin_bit_cast(float, (int)b[1]));
+    return (double)__builtin_fminf(__builtin_bit_cast(float, (int)b[0]), __builtin_bit_cast(float, (int)b[1]));
 }
 
-// Gershgorin's g of a stage from its data tile Mi (symmetric, zero outside the active rows / columns): row sums of |Mi|
-// by MFMA against a ones operand (the A fragment of K-chunk kc is register kc itself: lane (g,c) holds Mi[4kc+g][c] =
-// Mi[c][4kc+g]), the diagonal margin on the lane that holds it, then a wave minimum (as a conservative f32 bound).
-// cert_g (after stage_chol below) falls back to a shifted Cholesky where this bound is not positive.
+// Gershgorin's g of a stage from its data tile Mi (symmetric -- load_rsq_tile mirrors the lower triangle -- and zero
+// outside the active rows / columns): the absolute row sums are column sums, so a lane adds its four registers and
+// the four row groups are summed across (xrow_sum): a handful of VALU ops instead of four f64 MFMAs against a ones
+// operand (64 cycles of the matrix pipe each on gfx950).  Then the diagonal margin on the lane that holds the diagonal
+// entry and a wave minimum (as a conservative f32 bound).  cert_g (after stage_chol below) falls back to a shifted
+// Cholesky where this bound is not positive.
 template <class SH>
 __device__ __forceinline__ double cert_g_gersh(const d4& Mi, const SH& sh) {
     const int c = lane_id() & 15;
-    const d4 z = {0.0, 0.0, 0.0, 0.0};
-    d4 r0 = z, r1 = z;
-#pragma unroll
-    for (int kc = 0; kc < 4; kc++) {
-        const bool any = 4 * kc < sh.nu || (4 * kc + 3 >= sh.xo && 4 * kc < sh.xo + sh.nx);
-        if (!any) continue;  // uniform: chunk without an active variable (its rows are zero)
-        if (kc & 1)
-            r1 = mfma(fabs(Mi[kc]), 1.0, r1);
-        else
-            r0 = mfma(fabs(Mi[kc]), 1.0, r0);
-    }
-    const double d = diag_sel(Mi), rs = diag_sel(r0 + r1);
+    const double rs = xrow_sum((fabs(Mi[0]) + fabs(Mi[1])) + (fabs(Mi[2]) + fabs(Mi[3])));
+    const double d = diag_sel(Mi);
     const double m = (diag_lane() && tile_active(c, sh.nu, sh.nx, sh.xo)) ? d + fabs(d) - rs : 1e300;
     return wave_min_lb(m);
 }
@@ -546,6 +545,9 @@ __device__ __forceinline__ double cert_g_shift(const d4& Mi, const SH& sh) {
 template <class SH>
 __device__ __forceinline__ double cert_g(const d4& Mi, const SH& sh) {
     const double g = cert_g_gersh(Mi, sh);
+#ifdef HK_COUNT_NOSHIFT  // static instruction counts of the Gershgorin path alone (tools/loop_icount.py)
+    return g;
+#endif
     if (g > 0.0) return g;
     return cert_g_shift(Mi, sh);
 }

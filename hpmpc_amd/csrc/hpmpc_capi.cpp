@@ -59,12 +59,13 @@ enum { K_SV = 0, K_TRF = 1, K_TRS = 2, K_RES = 3, K_IPM = 4, K_KKT = 5, K_KKT_P1
 constexpr int FSTRIDE = 352, V16 = 16, V32 = 32, BS = 4, NCL = 2;
 
 // d_back_ric_rec_sv_tv_res runs the two-wave kernel (hk_ric2.hip: the tile recursion on one wave, fetch / row half /
-// stores on the other) unless HPMPC_MI355X_RIC_WAVES=1 asks for the one-wave kernel, or the two-wave launch guard
-// refuses the launch (HK_LAUNCH_REFUSED = -2, hk_launch_guard.h); every other entry point is hk_launch's.
+// stores on the other) when HPMPC_MI355X_RIC_WAVES=2 asks for it and its launch guard accepts the launch
+// (HK_LAUNCH_REFUSED = -2, hk_launch_guard.h); the one-wave kernel is the default: it measured faster at every batch
+// (DESIGN.md §4, round 5).  Every other entry point is hk_launch's.
 int launch(int which, const KArgs* a, int count, hipStream_t s) {
     if (which == K_SV) {
         const char* e = getenv("HPMPC_MI355X_RIC_WAVES");
-        if (!(e && e[0] == '1')) {
+        if (e && e[0] == '2') {
             const int r = hk_launch_ric2(which, a, count, s);
             if (r != -2) return r;
         }

@@ -9,8 +9,9 @@ oracle at TOL_RIC (1e-12 relative to max(1, |ref|)), on:
   * generic shapes (DynSh stages, full factor on stage 0 with nx[0] > 0), short horizons N = 1, 2, 3;
   * the reference's inner x-pivot clamp (xclamp_qp variants, the stages the clamp certificate rejects);
   * the aliased (time-invariant) layout.
-The drop-in d_back_ric_rec_sv_tv_res runs the two-wave kernel by default, so every sv golden of test_gpu_parity.py
-(update_b / update_q with box terms, general constraints, the clamp goldens) exercises it too."""
+The one-wave kernel is the default (the two-wave one measured slower); test_sv_goldens_two_wave runs the
+sv goldens (update_b / update_q with box terms, the clamp goldens) through the drop-in entry point on the two-wave
+kernel."""
 import os
 
 import numpy as np
@@ -145,3 +146,18 @@ def test_two_wave_aliased_layout():
     for x, y in zip(r_a, r_b):
         assert torch.equal(x, y)
     check_oracle(qp, *r_b, (0, 63))
+
+
+def test_sv_goldens_two_wave(product):
+    """The drop-in d_back_ric_rec_sv_tv_res on the two-wave kernel (HPMPC_MI355X_RIC_WAVES=2), every sv golden."""
+    from hpmpc_amd.golden import load_all
+    from helpers import check_case, run_case
+
+    cases = [c for c in load_all() if c.kind in ("sv", "sv_xclamp")]
+    assert len(cases) >= 8
+    os.environ["HPMPC_MI355X_RIC_WAVES"] = "2"
+    try:
+        for case in cases:
+            check_case(case, run_case(product, case))
+    finally:
+        os.environ.pop("HPMPC_MI355X_RIC_WAVES", None)

@@ -56,11 +56,25 @@ if STAMPS:
                 print(f"N={N} nx={nx} nu={nu} batch={B} 1-wave: backward {t[60]} ({t[60] / (N + 1):.0f}/stage) "
                       f"forward {t[61]} ({t[61] / N:.0f}/stage) cycles", flush=True)
             else:
-                seg = t[:4] / (N + 1)
-                print(f"N={N} nx={nx} nu={nu} batch={B} 2-wave: backward w0 {t[4]} w1 {t[5]}, forward w0 {t[6]} "
-                      f"w1 {t[7]}; w0 step: in {seg[0]:.0f} tile+cert {seg[1]:.0f} chol {seg[2]:.0f} "
-                      f"out {seg[3]:.0f}; waits: w1 factor {t[8]} w0 fwd {t[9]} w1 fwd {t[10]}", flush=True)
+                print(f"N={N} nx={nx} nu={nu} batch={B} 2-wave (cycles; work / barrier wait): backward w0 {t[0]} / "
+                      f"{t[1]} ({t[0] / (N + 1):.0f} / {t[1] / (N + 1):.0f} per step), w1 {t[2]} / {t[3]}; forward w0 "
+                      f"{t[4]} / {t[5]}, w1 {t[6]} / {t[7]}; w0 step: dispatch {t[8] / (N + 1):.0f} tile+cert "
+                      f"{t[9] / (N + 1):.0f} chol {t[10] / (N + 1):.0f} whole {t[11] / (N + 1):.0f}", flush=True)
     os.environ.pop("HPMPC_MI355X_RIC_WAVES", None)
+    sys.exit(0)
+
+SPLIT = "--split" in sys.argv  # one-wave entry points: sv, sv without pi, trf (backward without the row), trs
+if SPLIT:
+    import torch as _t
+    os.environ["HPMPC_MI355X_RIC_WAVES"] = "1"
+    for (N, nx, nu, B) in CONFIGS[:3]:
+        s = BatchSolver(make_shard(N, nx, nu, 0, 1, B, boxes=False), k_max=1)
+        bb = _t.zeros((B, N + 1, 16), dtype=_t.float64, device="cuda")
+        res = {n: float(np.median([timeit(f) for _ in range(3)])) for n, f in (
+            ("sv", lambda: s.ric_sv(compute_pi=1)), ("sv_nopi", lambda: s.ric_sv(compute_pi=0)),
+            ("trf", lambda: s.ric_trf()), ("trs", lambda: s.ric_trs(bb, bb, compute_Pb=0)))}
+        print(f"N={N} nx={nx} nu={nu} batch={B} one-wave us: " + " ".join(f"{k} {v * 1e3:.1f}" for k, v in res.items()),
+              flush=True)
     sys.exit(0)
 
 for (N, nx, nu, B) in CONFIGS:
