@@ -177,7 +177,6 @@ template <bool AUG, int BM, class FX>
 __device__ __forceinline__ int ric_backward_mw(const RicIO& io, int tb, int w, int update_b, const double* bsrc,
                                                int update_q, const double* qsrc, const BoxCtx& bc, int compute_Pb,
                                                double* Pb) {
-    static_assert(cert_loaded(BM), "the tile wave tests the certificate in threshold form (the IPM's box modes)");
     const int N = io.N, l = lane_id(), c = l & 15;
     Scratch* sm = &hk_mw.sm[w];
     if (w >= 2) {
@@ -293,9 +292,10 @@ __device__ __forceinline__ int ric_backward_mw(const RicIO& io, int tb, int w, i
                 MW_SEG(1);
                 double mld = 0.0;
                 const bool full = !SHT::fixed && k == 0;
-                // gc: the threshold T (IPM modes).  Taken before the u blocks: deferring the ballot past them
-                // (CertDefer) measured 329 vs 319 us per lone-QP IP iteration (profiles/r04/ab_latency_OR.txt)
-                xfac = !full && !cert_ok_thr(M, dq, gc, cert_diag_w());
+                // gc: the threshold tau on tr(P_{k+1}) (cert_tau), tested on the record the stage starts from (P), off
+                // the MFMA products' chain (round 4 tested M after the tile update, on the chain: ~450 ticks a step)
+                xfac = !full && !cert_ok_tr(P, sh.xo1, gc);
+                (void)dq;
                 stage_chol<false, false>(M, mld, invd, sh.nu, sh.nx, sh.xo, full, !SHT::fixed, nullptr, k, xfac, &xf);
                 MW_SEG(2);
             });

@@ -382,6 +382,40 @@ __device__ __forceinline__ bool cert_ok_thr(const d4& M, double dq, double T, co
     return __builtin_amdgcn_ballot_w64(!(d - dq < T)) == 0;
 }
 
+// The test off the recursion's chain (round 5).  e_max = max_i (M_ii - box_i) is bounded without M: with b_i the BAbt_k
+// row of variable i, M_ii - box_i = RSQ_ii + b_i' P_{k+1} b_i <= max_i RSQ_ii + tr(P_{k+1}) max_i |b_i|^2 (P_{k+1} is
+// positive semidefinite: b' P b <= lambda_max(P) |b|^2 <= tr(P) |b|^2; the reference's W W' has the same diagonal,
+// |W_i|^2 = b_i' Lxx Lxx' b_i), so e_max < T holds whenever tr(P_{k+1}) < tau_k = (T - max_i RSQ_ii) / max_i |b_i|^2.
+// tau_k depends on stage k's data alone (formed beside g, cert_tau); the test needs only the trace of the record the
+// stage starts from (cert_ok_tr), so it no longer waits for the stage's MFMA products.  On the benchmark data
+// tr(P) ~ 1e2 against tau ~ 1e10.  Stages with general constraints (DCt diag(Q) DCt' also adds to M_ii) and stages with
+// a negative given box term get tau = -inf (no certificate).  Rounding: T is rounded down by 2^-40 (cert_thr), tau by
+// 2^-30 and the trace is scaled up by 2^-30 before the compare.
+template <class SH>
+__device__ __forceinline__ double cert_tau(double T, const d4& Mi, const d4& bop, double dq, const SH& sh, bool live) {
+    const int c = lane_id() & 15;
+    const bool act = tile_active(c, sh.nu, sh.nx, sh.xo);
+    // max_i RSQ_ii over the active variables, max_i |b_i|^2 (lane c: the squared BAbt row of variable var(c))
+    const double rmax = -wave_min((diag_lane() && act) ? -diag_sel(Mi) : -0.0);
+    double b2 = 0.0;
+    if (live) b2 = xrow_sum(fma(bop[0], bop[0], bop[1] * bop[1]) + fma(bop[2], bop[2], bop[3] * bop[3]));
+    const double bmax = -wave_min(-b2);
+    const double num = T - rmax;
+    double tau = bmax > 0.0 ? num * rcp_nr(bmax) * (1.0 - 0x1p-30) : __builtin_inf();
+    bool none = !(num > 0.0) || __builtin_amdgcn_ballot_w64(dq < 0.0) != 0;
+    if constexpr (!SH::fixed) none = none || sh.ng > 0;
+    return none ? -__builtin_inf() : tau;
+}
+// the certificate of a P-form stage: tr(P_{k+1}) < tau_k, P_{k+1} the x block (tile indices >= xo1) of the record S the
+// stage starts from; wave-uniform
+__device__ __forceinline__ bool cert_ok_tr(const d4& S, int xo1, double tau) {
+    const int c = lane_id() & 15;
+    const d4 w = cert_diag_w();
+    const double d = (c >= xo1) ? w[0] * S[0] + w[1] * S[1] + w[2] * S[2] + w[3] * S[3] : 0.0;
+    const double tr = wave_sum(d);  // identical in every lane
+    return __builtin_amdgcn_readfirstlane((int)(tr * (1.0 + 0x1p-30) < tau)) != 0;
+}
+
 // l[4R + g] (row layout of a col-layout vector over tile block R): the pivot entries of block R
 template <int R>
 __device__ __forceinline__ double lrow_blk(double v) {
@@ -1115,22 +1149,32 @@ __device__ __forceinline__ void load_rsq_tile(const double* R, const SH& sh, d4&
     }
 }
 
-// The certificate's data part g_k of every stage into cert[0..N], as its own pass (stages in groups of eight, the
-// group's tile loads issued before its math): the single-Newton start, whose first factorisation is a phase-2 one.
+// The certificate's threshold tau_k (cert_tau) of every stage into cert[0..N], as its own pass (stages in groups of
+// eight, the group's tile and BAbt-operand loads issued before its math): the single-Newton start, whose first
+// factorisation is a phase-2 one.
 __device__ void cert_pass(const RicIO& io, double* cert) {
+    const int l = lane_id(), g = l >> 4, c = l & 15;
     for (int k0 = 0; k0 <= io.N; k0 += 8) {
-        d4 Mi[8];
+        d4 Mi[8], bop[8];
 #pragma unroll
         for (int j = 0; j < 8; j++) {
             const int k = k0 + j <= io.N ? k0 + j : io.N;
             const DynSh sh(StageRef{io.st, k});
             load_rsq_tile(stage_R(io, sh), sh, Mi[j]);
+            const int vc = tile_var(c, sh.nu, sh.nx, sh.xo);
+            const double* Bk = stage_B(io, sh);
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int s = 4 * r + g - sh.xo1;
+                bop[j][r] = ldsel(Bk, lib4_idx(sh.sdB, vc, s), k < io.N && s >= 0 && s < sh.nx1 && vc >= 0);
+            }
         }
 #pragma unroll
         for (int j = 0; j < 8; j++) {
             const int k = k0 + j <= io.N ? k0 + j : io.N;
             const DynSh sh(StageRef{io.st, k});
-            gst(cert, k0 + j, cert_thr(cert_g(Mi[j], sh)), lane_id() == 0 && k0 + j <= io.N);
+            const double tau = cert_tau(cert_thr(cert_g(Mi[j], sh)), Mi[j], bop[j], 0.0, sh, k < io.N);
+            gst(cert, k0 + j, tau, lane_id() == 0 && k0 + j <= io.N);
         }
     }
 }
@@ -1316,21 +1360,23 @@ __device__ __forceinline__ void bwd_pre(const RicIO& io, const SH& sh, int k, co
 #ifdef HK_COUNT_NOCERT
     gc = 0.0;
 #else
+    // gc: the stage's certificate threshold tau_k on tr(P_{k+1}) (cert_tau), from its data alone
+    const bool live = SH::fixed || k < io.N;
     if constexpr (cert_loaded(BM)) {
-        // the solve's first factorisation forms g from the tile (stage 0 too: a later one may be a P-form stage of
-        // another plan shape) and keeps it for the others; masked store otherwise (fixed vector-memory count)
-        // gc carries the threshold T (cert_thr) in these modes
+        // the solve's first factorisation forms tau from the tile (stage 0 too: a later one may be a P-form stage of
+        // another plan shape) and keeps it for the others; masked store otherwise (fixed vector-memory count).  The box
+        // terms (lam / t >= 0) are the iterate's, not the data's: no dq in these modes
         if constexpr (CN == CERT_LOAD) {
             gc = cur.gc;
         } else if constexpr (CN == CERT_FORM) {
-            gc = cert_thr(cert_g(cur.Mi, sh));
+            gc = cert_tau(cert_thr(cert_g(cur.Mi, sh)), cur.Mi, cur.bop, 0.0, sh, live);
             gst(bc.cert_out, k, gc, lane_id() == 0);
         } else {
-            gc = bc.cert_new ? cert_thr(cert_g(cur.Mi, sh)) : cur.gc;
+            gc = bc.cert_new ? cert_tau(cert_thr(cert_g(cur.Mi, sh)), cur.Mi, cur.bop, 0.0, sh, live) : cur.gc;
             gst(bc.cert_out, k, gc, bc.cert_new && lane_id() == 0);
         }
     } else {
-        gc = (SH::fixed || k > 0) ? cert_g(cur.Mi, sh) : 0.0;
+        gc = (SH::fixed || k > 0) ? cert_tau(cert_thr(cert_g(cur.Mi, sh)), cur.Mi, cur.bop, dq, sh, live) : 0.0;
     }
 #endif
     M = cur.Mi;
@@ -1418,15 +1464,15 @@ __device__ __forceinline__ void bwd_core(const RicIO& io, Scratch* sm, const SH&
     (void)dq;
     (void)gc;
 #else
-    // taken here, before the factorisation: deferring the ballot past the u blocks keeps the comparison live across the
-    // chain -- more spills in the pass kernels (static count), slower in the multi-wave tile wave (measured, hk_mw.h)
-    const bool xcert = !full && (THR ? !cert_ok_thr(M, dq, gc, cert_diag_w()) : !cert_ok(M, dq, gc));
+    // on the record the stage starts from (P_{k+1} = S), off the MFMA products' chain (cert_ok_tr)
+    const bool xcert = !full && !cert_ok_tr(S, sh.xo1, gc);
+    (void)dq;
 #endif
 #ifdef HK_STAMPS  // diagnostic build: how often the certificate fails, at this allowance and (with g) at 10x / 100x
     // smaller ones -- the threshold form only knows its own allowance, so those two count its failures
     if (!full) {
-        const bool xfac = xcert;
-        const bool f12 = THR ? xfac : !cert_ok(M, dq, gc, 1e-12), f13 = THR ? xfac : !cert_ok(M, dq, gc, 1e-13);
+        // (the threshold form knows its own allowance only: the 1e-12 / 1e-13 slots count its failures too)
+        const bool xfac = xcert, f12 = xcert, f13 = xcert;
         if (lane_id() == 0) {
             atomicAdd(&g_xfac_stat[0], 1ull);
             if (xfac) atomicAdd(&g_xfac_stat[1], 1ull);
