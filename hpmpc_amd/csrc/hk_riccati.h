@@ -328,6 +328,32 @@ __device__ __forceinline__ double wave_min_lb(double x) {
     return (double)__builtin_fminf(__builtin_bit_cast(float, (int)b[0]), __builtin_bit_cast(float, (int)b[1]));
 }
 
+// Conservative f32 wave reductions for the certificate (upper bounds): the maximum as -wave_min_lb(-x), and the sum of
+// values rounded up to f32 and added with DPP-sourced f32 adds (six adds of at most 16 + 4 terms: relative error below
+// 2^-20, covered by the final 2^-18 scale).
+__device__ __forceinline__ double wave_max_ub(double x) { return -wave_min_lb(-x); }
+__device__ __forceinline__ double wave_sum_ub(double x) {
+    float f = (float)x;
+    f = f + fabsf(f) * 0x1p-22f + 0x1p-126f;
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_add_f32_dpp %0, %0, %0 row_ror:8 row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_add_f32_dpp %0, %0, %0 row_ror:4 row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_add_f32_dpp %0, %0, %0 row_ror:2 row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_add_f32_dpp %0, %0, %0 row_ror:1 row_mask:0xf bank_mask:0xf"
+        : "+v"(f));
+    int v = __builtin_bit_cast(int, f);
+    const auto a = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    f = __builtin_bit_cast(float, (int)a[0]) + __builtin_bit_cast(float, (int)a[1]);
+    v = __builtin_bit_cast(int, f);
+    const auto b = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    f = __builtin_bit_cast(float, (int)b[0]) + __builtin_bit_cast(float, (int)b[1]);
+    return (double)f * (1.0 + 0x1p-18);
+}
+
 // Gershgorin's g of a stage from its data tile Mi (symmetric -- load_rsq_tile mirrors the lower triangle -- and zero
 // outside the active rows / columns): the absolute row sums are column sums, so a lane adds its four registers and
 // the four row groups are summed across (xrow_sum): a handful of VALU ops instead of four f64 MFMAs against a ones
@@ -390,16 +416,16 @@ __device__ __forceinline__ bool cert_ok_thr(const d4& M, double dq, double T, co
 // stage starts from (cert_ok_tr), so it no longer waits for the stage's MFMA products.  On the benchmark data
 // tr(P) ~ 1e2 against tau ~ 1e10.  Stages with general constraints (DCt diag(Q) DCt' also adds to M_ii) and stages with
 // a negative given box term get tau = -inf (no certificate).  Rounding: T is rounded down by 2^-40 (cert_thr), tau by
-// 2^-30 and the trace is scaled up by 2^-30 before the compare.
+// 2^-30; the maxima and the trace are conservative f32 reductions (wave_max_ub, wave_sum_ub: upper bounds).
 template <class SH>
 __device__ __forceinline__ double cert_tau(double T, const d4& Mi, const d4& bop, double dq, const SH& sh, bool live) {
     const int c = lane_id() & 15;
     const bool act = tile_active(c, sh.nu, sh.nx, sh.xo);
     // max_i RSQ_ii over the active variables, max_i |b_i|^2 (lane c: the squared BAbt row of variable var(c))
-    const double rmax = -wave_min((diag_lane() && act) ? -diag_sel(Mi) : -0.0);
+    const double rmax = wave_max_ub((diag_lane() && act) ? diag_sel(Mi) : 0.0);
     double b2 = 0.0;
     if (live) b2 = xrow_sum(fma(bop[0], bop[0], bop[1] * bop[1]) + fma(bop[2], bop[2], bop[3] * bop[3]));
-    const double bmax = -wave_min(-b2);
+    const double bmax = wave_max_ub(b2);
     const double num = T - rmax;
     double tau = bmax > 0.0 ? num * rcp_nr(bmax) * (1.0 - 0x1p-30) : __builtin_inf();
     bool none = !(num > 0.0) || __builtin_amdgcn_ballot_w64(dq < 0.0) != 0;
@@ -412,8 +438,43 @@ __device__ __forceinline__ bool cert_ok_tr(const d4& S, int xo1, double tau) {
     const int c = lane_id() & 15;
     const d4 w = cert_diag_w();
     const double d = (c >= xo1) ? w[0] * S[0] + w[1] * S[1] + w[2] * S[2] + w[3] * S[3] : 0.0;
-    const double tr = wave_sum(d);  // identical in every lane
-    return __builtin_amdgcn_readfirstlane((int)(tr * (1.0 + 0x1p-30) < tau)) != 0;
+    const double tr = wave_sum_ub(d);  // an upper bound, identical in every lane
+    return __builtin_amdgcn_readfirstlane((int)(tr < tau)) != 0;
+}
+
+// HK_CERT_TRACE (default 0): the per-stage test on the stage matrix M after its MFMA products (cert_ok_thr against T_k,
+// a negative given box term folded into T_k = -inf).  1 builds the test off the chain, on the trace of the record the
+// stage starts from (cert_ok_tr against tau_k): a same-box A/B (profiles/r05/ab_cert/, 3 pairs) measured it slower in
+// every kernel -- headline 1.436 vs 1.460 M IP-iter/s (factorisation 3.15 vs 3.01 ms per step), Riccati sv 3.26 vs
+// 3.37 M fact/s, configs[2] 6.75 vs 7.51 M, the lone QP 343 vs 310 us per IP iteration: its reductions cost more issue
+// than the ballot they replace takes off the chain, the waves being issue-bound.
+#ifndef HK_CERT_TRACE
+#define HK_CERT_TRACE 0
+#endif
+// The stage's data part of the certificate: tau_k (HK_CERT_TRACE) or T_k.  use_dq: the box terms are given data
+// (BX_GIVEN), not the IPM's iterate.
+template <class SH>
+__device__ __forceinline__ double cert_form(const d4& Mi, const d4& bop, double dq, const SH& sh, bool live) {
+    const double T = cert_thr(cert_g(Mi, sh));
+#if HK_CERT_TRACE
+    return cert_tau(T, Mi, bop, dq, sh, live);
+#else
+    (void)bop;
+    (void)live;
+    return __builtin_amdgcn_ballot_w64(dq < 0.0) != 0 ? -__builtin_inf() : T;
+#endif
+}
+// The per-stage test: S the record the stage starts from (P_{k+1}), M the stage matrix after its products.
+__device__ __forceinline__ bool cert_test(const d4& S, const d4& M, int xo1, double dq, double gc) {
+#if HK_CERT_TRACE
+    (void)M;
+    (void)dq;
+    return cert_ok_tr(S, xo1, gc);
+#else
+    (void)S;
+    (void)xo1;
+    return cert_ok_thr(M, dq, gc, cert_diag_w());
+#endif
 }
 
 // l[4R + g] (row layout of a col-layout vector over tile block R): the pivot entries of block R
@@ -1173,7 +1234,7 @@ __device__ void cert_pass(const RicIO& io, double* cert) {
         for (int j = 0; j < 8; j++) {
             const int k = k0 + j <= io.N ? k0 + j : io.N;
             const DynSh sh(StageRef{io.st, k});
-            const double tau = cert_tau(cert_thr(cert_g(Mi[j], sh)), Mi[j], bop[j], 0.0, sh, k < io.N);
+            const double tau = cert_form(Mi[j], bop[j], 0.0, sh, k < io.N);
             gst(cert, k0 + j, tau, lane_id() == 0 && k0 + j <= io.N);
         }
     }
@@ -1369,14 +1430,14 @@ __device__ __forceinline__ void bwd_pre(const RicIO& io, const SH& sh, int k, co
         if constexpr (CN == CERT_LOAD) {
             gc = cur.gc;
         } else if constexpr (CN == CERT_FORM) {
-            gc = cert_tau(cert_thr(cert_g(cur.Mi, sh)), cur.Mi, cur.bop, 0.0, sh, live);
+            gc = cert_form(cur.Mi, cur.bop, 0.0, sh, live);
             gst(bc.cert_out, k, gc, lane_id() == 0);
         } else {
-            gc = bc.cert_new ? cert_tau(cert_thr(cert_g(cur.Mi, sh)), cur.Mi, cur.bop, 0.0, sh, live) : cur.gc;
+            gc = bc.cert_new ? cert_form(cur.Mi, cur.bop, 0.0, sh, live) : cur.gc;
             gst(bc.cert_out, k, gc, bc.cert_new && lane_id() == 0);
         }
     } else {
-        gc = (SH::fixed || k > 0) ? cert_tau(cert_thr(cert_g(cur.Mi, sh)), cur.Mi, cur.bop, dq, sh, live) : 0.0;
+        gc = (SH::fixed || k > 0) ? cert_form(cur.Mi, cur.bop, dq, sh, live) : 0.0;
     }
 #endif
     M = cur.Mi;
@@ -1465,8 +1526,7 @@ __device__ __forceinline__ void bwd_core(const RicIO& io, Scratch* sm, const SH&
     (void)gc;
 #else
     // on the record the stage starts from (P_{k+1} = S), off the MFMA products' chain (cert_ok_tr)
-    const bool xcert = !full && !cert_ok_tr(S, sh.xo1, gc);
-    (void)dq;
+    const bool xcert = !full && !cert_test(S, M, sh.xo1, dq, gc);
 #endif
 #ifdef HK_STAMPS  // diagnostic build: how often the certificate fails, at this allowance and (with g) at 10x / 100x
     // smaller ones -- the threshold form only knows its own allowance, so those two count its failures
