@@ -17,7 +17,7 @@
 // Diagnostic build only: per-phase s_memtime cycle totals of hk_pcond workgroup (0, 0) (tools/pcond_phases.py)
 __device__ unsigned long long* g_pdbg;
 __device__ unsigned long long g_pst_t0;
-extern "C" __attribute__((visibility("default"))) int hk_pcond_debug(void* dev_ptr) {
+extern "C" __attribute__((visibility("default"))) int hpmpc_mi355x_pcond_debug(void* dev_ptr) {
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_pdbg), &dev_ptr, sizeof(void*));
 }
 #define PST(i)                                                                                  \
@@ -44,9 +44,132 @@ __global__ __launch_bounds__(WT) void hk_wide_sv(WideArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// The condensing's state-block Cholesky with its gradient row (d_cond_RSQrq's dpotrf_l on [pL_xx; pL_r],
+// d_part_cond.c:436-470) on one wave, for nx <= 28, as 16x16 MFMA tiles of the 32x32 padded block (the gradient row
+// sits at padded row 31, padding is zero):
+//   T00 rows / cols 0..15 and T11 rows / cols 16..31, symmetric storage (register r at lane (g,c) = A[4r+g][c]);
+//   U the off-diagonal rows 16..31 transposed (register r at lane (g,c) = A[16+c][4r+g]).
+// Pivot block B (4 pivots): its 4x4 diagonal block is broadcast (DPP row_newbcast) and factorised redundantly in
+// every lane, each lane solves its own row of the block column (T00 and U rows, a row-group gather each), and the
+// rank-4 trailing update is one v_mfma_f64_16x16x4 per tile.  Pivot clamp d > 1e-15 else 0 (kernel_dpotrf_c99_lib4.c
+// :555-640) with 1/sqrt(d) from v_rsq_f64 + one refinement (hk::chol_inv); padded pivots clamp to 0.  Replaces the
+// per-pivot readlane broadcasts (two v_readlane per entry of the pivot column).
+// ------------------------------------------------------------------------------------------------
+// The same factorisation for nx > 28 (row i on lane i, nx + 1 <= 64 rows): 16-column panels in registers, the pivot
+// column broadcast by readlane, each panel followed by its update of the later columns.  In place on X.
+__device__ __forceinline__ void xchol_rows(double* X, int ldX, int nxs) {
+    const int i = threadIdx.x & 63;
+    for (int p0 = 0; p0 < nxs; p0 += 16) {
+        const int pw = nxs - p0 < 16 ? nxs - p0 : 16;
+        double cl[16];
+#pragma unroll
+        for (int jj = 0; jj < 16; jj++) cl[jj] = (jj < pw && i >= p0 + jj && i <= nxs) ? X[i + (p0 + jj) * ldX] : 0.0;
+#pragma unroll
+        for (int jj = 0; jj < 16; jj++) {
+            if (jj < pw) {
+                const double d = rdlane(cl[jj], p0 + jj);
+                double sq, inv;
+                hk::chol_pivot(d, sq, inv);
+                cl[jj] = i == p0 + jj ? sq : (i > p0 + jj ? cl[jj] * inv : 0.0);
+#pragma unroll
+                for (int cc = jj + 1; cc < 16; cc++) cl[cc] -= cl[jj] * rdlane(cl[jj], p0 + cc);
+            }
+        }
+#pragma unroll
+        for (int jj = 0; jj < 16; jj++)
+            if (jj < pw && i >= p0 + jj && i <= nxs) X[i + (p0 + jj) * ldX] = cl[jj];
+        for (int c = p0 + 16; c < nxs; c++) {  // the panel's update of column c (rows >= c)
+            double acc = 0.0;
+#pragma unroll
+            for (int jj = 0; jj < 16; jj++) acc += cl[jj] * rdlane(cl[jj], c);
+            if (i >= c && i <= nxs) X[i + c * ldX] -= acc;
+        }
+        wave_sync();
+    }
+}
+
+template <int B, bool OFF>
+__device__ __forceinline__ void xchol_block(hk::d4& D, hk::d4& U, hk::d4& T11) {
+    using hk::row_bcast;
+    const int c = threadIdx.x & 15;
+    double x[4];
+    hk::rowgroup_gather(D[B], x);
+    const double a00 = row_bcast<4 * B + 0>(x[0]);
+    const double a10 = row_bcast<4 * B + 1>(x[0]), a11 = row_bcast<4 * B + 1>(x[1]);
+    const double a20 = row_bcast<4 * B + 2>(x[0]), a21 = row_bcast<4 * B + 2>(x[1]);
+    const double a22 = row_bcast<4 * B + 2>(x[2]);
+    const double a30 = row_bcast<4 * B + 3>(x[0]), a31 = row_bcast<4 * B + 3>(x[1]);
+    const double a32 = row_bcast<4 * B + 3>(x[2]), a33 = row_bcast<4 * B + 3>(x[3]);
+    const double i0 = hk::chol_inv(a00);
+    const double l10 = a10 * i0, l20 = a20 * i0, l30 = a30 * i0;
+    const double y0 = x[0] * i0;
+    const double i1 = hk::chol_inv(fma(-l10, l10, a11));
+    const double l21 = fma(-l20, l10, a21) * i1, l31 = fma(-l30, l10, a31) * i1;
+    const double y1 = fma(-y0, l10, x[1]) * i1;
+    const double i2 = hk::chol_inv(fma(-l21, l21, fma(-l20, l20, a22)));
+    const double l32 = fma(-l31, l21, fma(-l30, l20, a32)) * i2;
+    const double y2 = fma(-y1, l21, fma(-y0, l20, x[2])) * i2;
+    const double i3 = hk::chol_inv(fma(-l32, l32, fma(-l31, l31, fma(-l30, l30, a33))));
+    const double y3 = fma(-y2, l32, fma(-y1, l31, fma(-y0, l30, x[3]))) * i3;
+    // lane (g,c) of register B: L[c][4B+g] (upper storage; the diagonal is d_g * i_g = sqrt(d_g))
+    const double yg = hk::sel_g(y0, y1, y2, y3);
+    D[B] = yg;
+    const double a = c > 4 * B + 3 ? yg : 0.0;
+    if (B < 3) D = hk::mfma(-a, a, D);
+    if (OFF) {
+        double z[4];
+        hk::rowgroup_gather(U[B], z);
+        const double w0 = z[0] * i0;
+        const double w1 = fma(-w0, l10, z[1]) * i1;
+        const double w2 = fma(-w1, l21, fma(-w0, l20, z[2])) * i2;
+        const double w3 = fma(-w2, l32, fma(-w1, l31, fma(-w0, l30, z[3]))) * i3;
+        const double wg = hk::sel_g(w0, w1, w2, w3);  // L[16+c][4B+g]
+        U[B] = wg;
+        U = hk::mfma(-a, wg, U);      // A[16+j][i] -= sum_k L[i][4B+k] L[16+j][4B+k], i below the block
+        T11 = hk::mfma(-wg, wg, T11);  // A[16+i][16+j] -= sum_k L[16+i][4B+k] L[16+j][4B+k]
+    }
+}
+
+// X: (nx+1) x nx lower, dense (ld ldX), row nx = the gradient row; read from src (ld lds, offset so) and the factor
+// written to X.  Wave-level (one wave calls it).
+__device__ __forceinline__ void xchol_tiles(const double* S, int ldS, double* X, int ldX, int nx) {
+    const int l = threadIdx.x & 63, g = l >> 4, c = l & 15;
+    auto src = [&](int t) { return t < nx ? t : (t == 31 ? nx : -1); };
+    auto at = [&](int t1, int t2) -> double {  // A[t1][t2] of the padded symmetric block
+        const int i1 = src(t1), i2 = src(t2);
+        const int r = i1 > i2 ? i1 : i2, q = i1 > i2 ? i2 : i1;
+        return (q >= 0 && q < nx) ? S[r + q * ldS] : 0.0;
+    };
+    hk::d4 T00, U, T11;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        T00[r] = at(4 * r + g, c);
+        U[r] = at(16 + c, 4 * r + g);
+        T11[r] = at(16 + 4 * r + g, 16 + c);
+    }
+    if (nx > 0) xchol_block<0, true>(T00, U, T11);
+    if (nx > 4) xchol_block<1, true>(T00, U, T11);
+    if (nx > 8) xchol_block<2, true>(T00, U, T11);
+    if (nx > 12) xchol_block<3, true>(T00, U, T11);
+    if (nx > 16) xchol_block<0, false>(T11, U, T11);
+    if (nx > 20) xchol_block<1, false>(T11, U, T11);
+    if (nx > 24) xchol_block<2, false>(T11, U, T11);
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int col = 4 * r + g, c1 = 16 + col, row1 = src(16 + c);
+        if (c >= col && c < nx && col < nx) X[c + col * ldX] = T00[r];
+        if (row1 >= 0 && col < nx) X[row1 + col * ldX] = U[r];
+        if (c >= col && row1 >= 0 && c1 < nx) X[row1 + c1 * ldX] = T11[r];
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Partial condensing of one block (d_cond_BAbt :214-303, d_cond_RSQrq :307-574, d_cond_DCtd :579-688).
 // Condensed stage variables: [u_{T-1}; ...; u_0; x_0].  Gamma_j (rows [u_j..u_0, x_0, 1] x nx_{j+1},
-// dense column-major) lives in the problem's scratch; the stage tiles (pL, Lx, BAbt, W) in LDS.
+// dense column-major) is formed once and read again by the RSQrq and DCtd phases through the problem's HBM scratch,
+// with only Gamma_{j-1} in LDS; the stage tiles (pL, Lx, BAbt, W) are in LDS too.  Keeping a whole block's Gammas in
+// LDS instead (130 KiB at configs[4]) measured 2.7x slower: the workgroup's own time fell 17 %, but one workgroup
+// per CU instead of four leaves nothing to hide its dependency chains behind.
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(WT, 4) void hk_pcond(PcArgs a) {  // 4 waves per SIMD: four workgroups per CU (the LDS fits four)
     extern __shared__ double sm[];
@@ -96,7 +219,8 @@ __global__ __launch_bounds__(WT, 4) void hk_pcond(PcArgs a) {  // 4 waves per SI
         const int r0 = s.nu + s.nx + 1;
         load_dense<8>(GA, r0, BAbt + s.oB, s.sdB, r0, s.nx1);
         bar();
-        for (int e = tid; e < r0 * s.nx1; e += WT) G[e] = GA[e];
+        if (T > 1 || (ph & PC_PART))
+            for (int e = tid; e < r0 * s.nx1; e += WT) G[e] = GA[e];
     }
     // BAbt_{j+1} is loaded into registers while Gamma_j is formed (Staged), and stored into LDS at the top of the
     // next step: one memory round trip per block instead of one per stage
@@ -107,6 +231,8 @@ __global__ __launch_bounds__(WT, 4) void hk_pcond(PcArgs a) {  // 4 waves per SI
         const int nuj = s.nu, nxj = s.nx, nx1 = s.nx1, nzj = nuj + nxj + 1;
         const int rp = rows(j - 1), rj = rp + nuj, n = rj * nx1;
         double* Gj = G + goff(j);
+        // the later phases read Gamma_0 .. Gamma_{T-2}; Gamma_{T-1} only goes to B2 (d_cond_BAbt alone returns all)
+        const bool keep = j < T - 1 || (ph & PC_PART);
         PST(1);
         if (staged)
             put_dense(nb, Bt, ldB);
@@ -131,12 +257,12 @@ __global__ __launch_bounds__(WT, 4) void hk_pcond(PcArgs a) {  // 4 waves per SI
             [&](int i, int c, double v) {
                 if (i == rp - 1) v += Bt[nuj + nxj + c * ldB];
                 GA[nuj + i + c * rj] = v;
-                Gj[nuj + i + c * rj] = v;
+                if (keep) Gj[nuj + i + c * rj] = v;
             });
         for (int e = tid; e < nuj * nx1; e += WT) {
             const int i = e % nuj, c = e / nuj;
             GA[i + c * rj] = Bt[i + c * ldB];
-            Gj[i + c * rj] = Bt[i + c * ldB];
+            if (keep) Gj[i + c * rj] = Bt[i + c * ldB];
         }
         (void)n;
         bar();
@@ -158,8 +284,13 @@ __global__ __launch_bounds__(WT, 4) void hk_pcond(PcArgs a) {  // 4 waves per SI
     const int cnux2 = (nv + 1) / 2 * 2;
     if (ph & PC_RSQ) {
     if (!(ph & PC_PART)) {
+        // zeros only where the recursion below writes nothing: the strict upper triangle and the padding (every
+        // entry i >= j, i <= nv, j < nv is stored exactly once by the D / M / final blocks)
         const int n = ((nv + 1 + 3) / 4 * 4) * cnux2;
-        for (int e = tid; e < n; e += WT) R2[e] = 0.0;
+        for (int e = tid; e < n; e += WT) {
+            const int q = e % (4 * cnux2), i = e / (4 * cnux2) * 4 + (q & 3), j = q >> 2;
+            if (i < j || i > nv || j >= nv) R2[e] = 0.0;
+        }
     }
     // offsets of u_s in the condensed variables: off(s) = sum_{r > s} nu_r
     auto uoff = [&](int s) {
@@ -190,78 +321,40 @@ __global__ __launch_bounds__(WT, 4) void hk_pcond(PcArgs a) {  // 4 waves per SI
             // D: the u_s x u_s block
             for (int j = tid >> 6; j < nus; j += WT / 64)
                 for (int i = j + (tid & 63); i < nus; i += 64) *P4w(R2, cnux2, os + i, os + j) = Pl[i + j * ldP];
-            // BAbt_{s-1} / RSQrq_{s-1} (needed after the Cholesky) are loaded into registers now, so their memory
-            // round trip overlaps Gamma_{s-1}'s and the work below; they go to LDS once Bt / pL are free
             const WideStage sp = st[sI - 1];
             const int nuxp = sp.nu + sp.nx, nzp = nuxp + 1;
-            const bool stg = nzp * nxs <= 4 * WT && nzp * nuxp <= 4 * WT;  // uniform
-            Staged<4> pb, pr;
-            if (stg) {
-                pre_dense(pb, BAbt + sp.oB, sp.sdB, nzp, nxs);
-                pre_dense(pr, RSQ + sp.oR, sp.sdR, nzp, nuxp);
-            }
-            // Gamma_{s-1} into GA; the state block of pL (with its gradient row) into X
             const int r0 = rows(sI - 1);
             load_flat<8>(GA, G + goff(sI - 1), r0 * nxs);
-            for (int j = tid >> 6; j < nxs; j += WT / 64)
-                for (int i = j + (tid & 63); i <= nxs; i += 64) X[i + j * ldX] = Pl[nus + i + (nus + j) * ldP];
+            const bool xt = nxs <= 28;  // uniform: the tile Cholesky reads pL directly
+            if (!xt)
+                for (int j = tid >> 6; j < nxs; j += WT / 64)
+                    for (int i = j + (tid & 63); i <= nxs; i += 64) X[i + j * ldX] = Pl[nus + i + (nus + j) * ldP];
             bar();
             PST(5);
-            // M: Gamma_{s-1} times the x_s x u_s block of pL; m: + the r row on the gradient row
-            for (int e = tid; e < ((a.skip & 8) ? 0 : r0 * nus); e += WT) {
-                const int i = e % r0, c = e / r0;
-                double acc = 0.0;
-                for (int l = 0; l < nxs; l++) acc += GA[i + l * r0] * Pl[nus + l + c * ldP];
-                if (i == r0 - 1) acc += Pl[nux + c * ldP];
-                *P4w(R2, cnux2, os + nus + i, os + c) = acc;
-            }
-            PST(6);
-            // Lx = chol_aug(X) inside wave 0 (row i on lane i, nxs + 1 <= 64 rows): 16-column panels factored in
-            // registers (pivot values broadcast by readlane), each followed by its update of the later columns
-            if (tid < 64 && !(a.skip & 4)) {
-                const int i = tid;
-                for (int p0 = 0; p0 < nxs; p0 += 16) {
-                    const int pw = nxs - p0 < 16 ? nxs - p0 : 16;
-                    double cl[16];
-#pragma unroll
-                    for (int jj = 0; jj < 16; jj++)
-                        cl[jj] = (jj < pw && i >= p0 + jj && i <= nxs) ? X[i + (p0 + jj) * ldX] : 0.0;
-#pragma unroll
-                    for (int jj = 0; jj < 16; jj++) {
-                        if (jj < pw) {
-                            const double d = rdlane(cl[jj], p0 + jj);
-                            // the pivot clamp d > 1e-15 else 0 (kernel_dpotrf_c99_lib4.c:555-640) with s = sqrt(d), 1/s from
-                            // v_rsq_f64 plus one third-order refinement (hk::chol_pivot, <= 1.2 half-ulp) instead of an IEEE
-                            // sqrt and divide on the pivot chain
-                            double sq, inv;
-                            hk::chol_pivot(d, sq, inv);
-                            cl[jj] = i == p0 + jj ? sq : (i > p0 + jj ? cl[jj] * inv : 0.0);
-#pragma unroll
-                            for (int cc = jj + 1; cc < 16; cc++) cl[cc] -= cl[jj] * rdlane(cl[jj], p0 + cc);
-                        }
-                    }
-#pragma unroll
-                    for (int jj = 0; jj < 16; jj++)
-                        if (jj < pw && i >= p0 + jj && i <= nxs) X[i + (p0 + jj) * ldX] = cl[jj];
-                    for (int c = p0 + 16; c < nxs; c++) {  // the panel's update of column c (rows >= c)
-                        double acc = 0.0;
-#pragma unroll
-                        for (int jj = 0; jj < 16; jj++) acc += cl[jj] * rdlane(cl[jj], c);
-                        if (i >= c && i <= nxs) X[i + c * ldX] -= acc;
-                    }
-                    wave_sync();
+            if (tid < 64) {
+                // Lx = chol_aug(pL_xx; pL_r) on wave 0 while the other three form M
+                if (!(a.skip & 4)) {
+                    if (xt)
+                        xchol_tiles(Pl + nus + nus * ldP, ldP, X, ldX, nxs);
+                    else
+                        xchol_rows(X, ldX, nxs);
+                }
+                PST(6);
+            } else {
+                // M: Gamma_{s-1} times the x_s x u_s block of pL; m: + the r row on the gradient row
+                for (int e = tid - 64; e < ((a.skip & 8) ? 0 : r0 * nus); e += WT - 64) {
+                    const int i = e % r0, c = e / r0;
+                    double acc = 0.0;
+                    for (int l = 0; l < nxs; l++) acc += GA[i + l * r0] * Pl[nus + l + c * ldP];
+                    if (i == r0 - 1) acc += Pl[nux + c * ldP];
+                    *P4w(R2, cnux2, os + nus + i, os + c) = acc;
                 }
             }
-            bar();
+            bar();  // pL and GA are read until here
             PST(7);
-            // W = BAbt_{s-1} Lx (in place in Bt, row i by one thread), last row += l; pL = RSQ_{s-1} + W W'
-            if (stg) {
-                put_dense(pb, Bt, ldB);
-                put_dense(pr, Pl, ldP);
-            } else {
-                load_dense<8>(Bt, ldB, BAbt + sp.oB, sp.sdB, nzp, nxs);
-                load_dense<8>(Pl, ldP, RSQ + sp.oR, sp.sdR, nzp, nuxp);
-            }
+            // W = BAbt_{s-1} Lx (in place in Bt), last row += l; pL = RSQ_{s-1} + W W'
+            load_dense<8>(Bt, ldB, BAbt + sp.oB, sp.sdB, nzp, nxs);
+            load_dense<8>(Pl, ldP, RSQ + sp.oR, sp.sdR, nzp, nuxp);
             bar();
             PST(8);
             if (!(a.skip & 16)) {
@@ -301,10 +394,8 @@ __global__ __launch_bounds__(WT, 4) void hk_pcond(PcArgs a) {  // 4 waves per SI
         int *cU = I, *cX = I + T, *iob = I + 2 * T, *iog = I + 3 * T, *ntmp = I + 4 * T, *igb = I + 5 * T;
         int* gd = I + 6 * T;  // general constraint ig: (stage << 16) | state index g
         bar();                // the RSQ phase's last LDS reads are done
-        if (!(ph & PC_PART)) {
-            for (int e = tid; e < pnv * cnbg; e += WT) G2[e] = 0.0;
+        if (!(ph & PC_PART))
             for (int e = tid; e < 2 * pnbb + 2 * pnbg; e += WT) d2[e] = 0.0;
-        }
         for (int sI = wv; sI < T; sI += WT / 64) {  // input / state box counts of each stage
             const WideStage s = st[sI];
             int nU = 0, nX = 0;
@@ -371,6 +462,16 @@ __global__ __launch_bounds__(WT, 4) void hk_pcond(PcArgs a) {  // 4 waves per SI
             }
         }
         bar();
+        if (!(ph & PC_PART))  // DCt2 zeros only outside the rows the copy below writes
+            for (int e = tid; e < pnv * cnbg; e += WT) {
+                const int q = e % (4 * cnbg), i = e / (4 * cnbg) * 4 + (q & 3), ig = q >> 2;
+                bool z = ig >= nbg;
+                if (!z) {
+                    const int sI = gd[ig] >> 16, nt = ntmp[sI];
+                    z = i < nt || i >= nt + igb[sI];
+                }
+                if (z) G2[e] = 0.0;
+            }
         for (int ig = wv; ig < nbg; ig += WT / 64) {  // DCt2 column ig: rows nu_tmp + i <- Gamma_{s-1}(i, g)
             const int sI = gd[ig] >> 16, g = gd[ig] & 0xffff, rowsI = igb[sI], r0 = rowsI + 1, nt = ntmp[sI];
             const double* Gp = G + goff(sI - 1);

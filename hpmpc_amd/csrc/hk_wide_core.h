@@ -92,6 +92,54 @@ __device__ __forceinline__ void put_dense(const Staged<CH>& S, double* D, int ld
         if (e < n) D[i + c * ld] = S.r[u];
     }
 }
+// A flat block of at most CH * WT doubles staged in registers (pre_flat issues the loads, put_flat stores to LDS)
+template <int CH>
+struct Flat {
+    double r[CH];
+};
+template <int CH>
+__device__ __forceinline__ void pre_flat(Flat<CH>& S, const double* src, int n) {
+#pragma unroll
+    for (int u = 0; u < CH; u++) S.r[u] = gld(src, u * WT + threadIdx.x, u * WT + (int)threadIdx.x < n);
+}
+template <int CH>
+__device__ __forceinline__ void put_flat(const Flat<CH>& S, double* D, int n) {
+#pragma unroll
+    for (int u = 0; u < CH; u++)
+        if (u * WT + (int)threadIdx.x < n) D[u * WT + threadIdx.x] = S.r[u];
+}
+// The same staging done by a group of NT threads (t = index in the group): at most CH * NT elements
+template <int NT, int CH>
+__device__ __forceinline__ void pre_dense_g(Staged<CH>& S, const double* src, int sd, int nr, int nc, int t) {
+    const int n = nr * nc;
+    S.nr = nr;
+    S.nc = nc;
+#pragma unroll
+    for (int u = 0; u < CH; u++) {
+        const int e = u * NT + t, i = e % nr, c = e / nr;
+        S.r[u] = gld(src, p4i(i, c, sd), e < n);
+    }
+}
+template <int NT, int CH>
+__device__ __forceinline__ void put_dense_g(const Staged<CH>& S, double* D, int ld, int t) {
+    const int nr = S.nr, n = S.nr * S.nc;
+#pragma unroll
+    for (int u = 0; u < CH; u++) {
+        const int e = u * NT + t, i = e % nr, c = e / nr;
+        if (e < n) D[i + c * ld] = S.r[u];
+    }
+}
+template <int NT, int CH>
+__device__ __forceinline__ void pre_flat_g(Flat<CH>& S, const double* src, int n, int t) {
+#pragma unroll
+    for (int u = 0; u < CH; u++) S.r[u] = gld(src, u * NT + t, u * NT + t < n);
+}
+template <int NT, int CH>
+__device__ __forceinline__ void put_flat_g(const Flat<CH>& S, double* D, int n, int t) {
+#pragma unroll
+    for (int u = 0; u < CH; u++)
+        if (u * NT + t < n) D[u * NT + t] = S.r[u];
+}
 // lib4 lower trapezoid rows [j, nz) of cols [0, nc) -> packed lower columns (nz <= 128: two rows per lane)
 template <int CU>
 __device__ void load_lower(double* M, const double* src, int sd, int nz, int nc) {

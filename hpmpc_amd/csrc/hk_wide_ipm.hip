@@ -521,7 +521,7 @@ __device__ __forceinline__ void ric_trs(const WideIpmArgs& A, const IP& P, const
 }  // namespace
 
 #ifdef HK_STAMPS
-extern "C" __attribute__((visibility("default"))) int hk_wide_ipm_debug(void* dev_ptr) {
+extern "C" __attribute__((visibility("default"))) int hpmpc_mi355x_wide_ipm_debug(void* dev_ptr) {
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_wdbg), &dev_ptr, sizeof(void*));
 }
 #define WPH(i)                                                                              \

@@ -17,16 +17,16 @@ qp = make_shard(200, 24, 6, 0, 1, B, boxes=False)  # bench.py's configs[4] leg
 s = hp.PcondSolver(qp, 20)
 dbg = torch.zeros(16, dtype=torch.int64, device="cuda")
 L = hp.lib()
-L.hk_pcond_debug.argtypes = [C.c_void_p]
+L.hpmpc_mi355x_pcond_debug.argtypes = [C.c_void_p]
 s.condense()
 torch.cuda.synchronize()
-assert L.hk_pcond_debug(dbg.data_ptr()) == 0
+assert L.hpmpc_mi355x_pcond_debug(dbg.data_ptr()) == 0
 s.condense()
 torch.cuda.synchronize()
 t = dbg.cpu().numpy().astype(np.int64)
 names = {1: "BAbt phase: Gamma_0 / loop top", 2: "BAbt_j staging", 3: "Gamma_j gemm + Gamma store", 4: "B2 store, barrier",
-         5: "RSQ: D store, Gamma_{s-1} load, X", 6: "M = Gamma M_s (scalar)", 7: "chol_aug (wave 0)",
-         8: "BAbt / RSQ staging", 9: "W and pL gemms", 10: "DCtd, tail"}
+         5: "RSQ: D store, Gamma_{s-1} load", 6: "chol_aug (wave 0) | M (waves 1-3)", 7: "wait for M",
+         8: "BAbt / RSQ into LDS", 9: "W and pL gemms", 10: "DCtd, tail"}
 tot = t[1:11].sum()
 print(f"batch {B}: hk_pcond block (0, 0): {tot} cycles")
 for i in range(1, 11):

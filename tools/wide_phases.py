@@ -18,10 +18,10 @@ s = hp.PcondSolver(qp, 20)
 s.condense()
 dbg = torch.zeros(32, dtype=torch.int64, device="cuda")
 L = hp.lib()
-L.hk_wide_ipm_debug.argtypes = [C.c_void_p]
+L.hpmpc_mi355x_wide_ipm_debug.argtypes = [C.c_void_p]
 s.ipm()
 torch.cuda.synchronize()
-assert L.hk_wide_ipm_debug(dbg.data_ptr()) == 0
+assert L.hpmpc_mi355x_wide_ipm_debug(dbg.data_ptr()) == 0
 s.ipm()
 torch.cuda.synchronize()
 t = dbg.cpu().numpy().astype(np.int64)
