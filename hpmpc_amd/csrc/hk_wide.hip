@@ -57,7 +57,7 @@ __global__ __launch_bounds__(WT) void hk_wide_sv(WideArgs a) {
 // ------------------------------------------------------------------------------------------------
 // The same factorisation for nx > 28 (row i on lane i, nx + 1 <= 64 rows): 16-column panels in registers, the pivot
 // column broadcast by readlane, each panel followed by its update of the later columns.  In place on X.
-__device__ __forceinline__ void xchol_rows(double* X, int ldX, int nxs) {
+__device__ __attribute__((noinline)) void xchol_rows(double* X, int ldX, int nxs) {
     const int i = threadIdx.x & 63;
     for (int p0 = 0; p0 < nxs; p0 += 16) {
         const int pw = nxs - p0 < 16 ? nxs - p0 : 16;
@@ -88,57 +88,16 @@ __device__ __forceinline__ void xchol_rows(double* X, int ldX, int nxs) {
     }
 }
 
-template <int B, bool OFF>
-__device__ __forceinline__ void xchol_block(hk::d4& D, hk::d4& U, hk::d4& T11) {
-    using hk::row_bcast;
-    const int c = threadIdx.x & 15;
-    double x[4];
-    hk::rowgroup_gather(D[B], x);
-    const double a00 = row_bcast<4 * B + 0>(x[0]);
-    const double a10 = row_bcast<4 * B + 1>(x[0]), a11 = row_bcast<4 * B + 1>(x[1]);
-    const double a20 = row_bcast<4 * B + 2>(x[0]), a21 = row_bcast<4 * B + 2>(x[1]);
-    const double a22 = row_bcast<4 * B + 2>(x[2]);
-    const double a30 = row_bcast<4 * B + 3>(x[0]), a31 = row_bcast<4 * B + 3>(x[1]);
-    const double a32 = row_bcast<4 * B + 3>(x[2]), a33 = row_bcast<4 * B + 3>(x[3]);
-    const double i0 = hk::chol_inv(a00);
-    const double l10 = a10 * i0, l20 = a20 * i0, l30 = a30 * i0;
-    const double y0 = x[0] * i0;
-    const double i1 = hk::chol_inv(fma(-l10, l10, a11));
-    const double l21 = fma(-l20, l10, a21) * i1, l31 = fma(-l30, l10, a31) * i1;
-    const double y1 = fma(-y0, l10, x[1]) * i1;
-    const double i2 = hk::chol_inv(fma(-l21, l21, fma(-l20, l20, a22)));
-    const double l32 = fma(-l31, l21, fma(-l30, l20, a32)) * i2;
-    const double y2 = fma(-y1, l21, fma(-y0, l20, x[2])) * i2;
-    const double i3 = hk::chol_inv(fma(-l32, l32, fma(-l31, l31, fma(-l30, l30, a33))));
-    const double y3 = fma(-y2, l32, fma(-y1, l31, fma(-y0, l30, x[3]))) * i3;
-    // lane (g,c) of register B: L[c][4B+g] (upper storage; the diagonal is d_g * i_g = sqrt(d_g))
-    const double yg = hk::sel_g(y0, y1, y2, y3);
-    D[B] = yg;
-    const double a = c > 4 * B + 3 ? yg : 0.0;
-    if (B < 3) D = hk::mfma(-a, a, D);
-    if (OFF) {
-        double z[4];
-        hk::rowgroup_gather(U[B], z);
-        const double w0 = z[0] * i0;
-        const double w1 = fma(-w0, l10, z[1]) * i1;
-        const double w2 = fma(-w1, l21, fma(-w0, l20, z[2])) * i2;
-        const double w3 = fma(-w2, l32, fma(-w1, l31, fma(-w0, l30, z[3]))) * i3;
-        const double wg = hk::sel_g(w0, w1, w2, w3);  // L[16+c][4B+g]
-        U[B] = wg;
-        U = hk::mfma(-a, wg, U);      // A[16+j][i] -= sum_k L[i][4B+k] L[16+j][4B+k], i below the block
-        T11 = hk::mfma(-wg, wg, T11);  // A[16+i][16+j] -= sum_k L[16+i][4B+k] L[16+j][4B+k]
-    }
-}
-
-// X: (nx+1) x nx lower, dense (ld ldX), row nx = the gradient row; read from src (ld lds, offset so) and the factor
-// written to X.  Wave-level (one wave calls it).
-__device__ __forceinline__ void xchol_tiles(const double* S, int ldS, double* X, int ldX, int nx) {
+// The block is read through S(i, j) (i >= j: row i, column j; row nx = the gradient row) and the factor written to X
+// ((nx+1) x nx lower, dense, ld ldX).  Wave-level (one wave calls it).
+template <class FS>
+__device__ __forceinline__ void xchol_tiles(FS S, double* X, int ldX, int nx) {
     const int l = threadIdx.x & 63, g = l >> 4, c = l & 15;
     auto src = [&](int t) { return t < nx ? t : (t == 31 ? nx : -1); };
     auto at = [&](int t1, int t2) -> double {  // A[t1][t2] of the padded symmetric block
         const int i1 = src(t1), i2 = src(t2);
         const int r = i1 > i2 ? i1 : i2, q = i1 > i2 ? i2 : i1;
-        return (q >= 0 && q < nx) ? S[r + q * ldS] : 0.0;
+        return (q >= 0 && q < nx) ? S(r, q) : 0.0;
     };
     hk::d4 T00, U, T11;
 #pragma unroll
@@ -147,13 +106,14 @@ __device__ __forceinline__ void xchol_tiles(const double* S, int ldS, double* X,
         U[r] = at(16 + c, 4 * r + g);
         T11[r] = at(16 + 4 * r + g, 16 + c);
     }
-    if (nx > 0) xchol_block<0, true>(T00, U, T11);
-    if (nx > 4) xchol_block<1, true>(T00, U, T11);
-    if (nx > 8) xchol_block<2, true>(T00, U, T11);
-    if (nx > 12) xchol_block<3, true>(T00, U, T11);
-    if (nx > 16) xchol_block<0, false>(T11, U, T11);
-    if (nx > 20) xchol_block<1, false>(T11, U, T11);
-    if (nx > 24) xchol_block<2, false>(T11, U, T11);
+    double inv = 0.0;  // not needed: the condensing keeps L only
+    if (nx > 0) tile_chol_block<0, 1, true>(T00, &U, 1, &T11, inv);
+    if (nx > 4) tile_chol_block<1, 1, true>(T00, &U, 1, &T11, inv);
+    if (nx > 8) tile_chol_block<2, 1, true>(T00, &U, 1, &T11, inv);
+    if (nx > 12) tile_chol_block<3, 1, true>(T00, &U, 1, &T11, inv);
+    if (nx > 16) tile_chol_block<0, 1, false>(T11, &U, 0, &T11, inv);
+    if (nx > 20) tile_chol_block<1, 1, false>(T11, &U, 0, &T11, inv);
+    if (nx > 24) tile_chol_block<2, 1, false>(T11, &U, 0, &T11, inv);
 #pragma unroll
     for (int r = 0; r < 4; r++) {
         const int col = 4 * r + g, c1 = 16 + col, row1 = src(16 + c);
@@ -188,10 +148,10 @@ __global__ __launch_bounds__(WT, 4) void hk_pcond(PcArgs a) {  // 4 waves per SI
     double* R2 = a.RSQ2 + (long)p * a.sR2 + blk.oR2;
     double* G2 = a.DCt2 + (long)p * a.sG2 + blk.oG2;
     double* d2 = a.d2 + (long)p * a.sD2 + blk.oD2;
-    double* Pl = sm + a.offP;  // pL (dense, ld ldP)
+    double* Pl = sm + a.offP;  // pL (RSQrq_s + W W', a lib4 block in the layout of its stage)
     double* X = sm + a.offX;   // Lx / chol scratch (ld ldX)
     double* Bt = sm + a.offB;  // stage BAbt tile, then W in place (ld ldB)
-    const int ldP = a.ldP, ldX = a.ldX, ldB = a.ldB;
+    const int ldX = a.ldX, ldB = a.ldB;
 
     // Gamma row counts / offsets (rows r_j = sum_{i<=j} nu_i + nx0 + 1)
     auto rows = [&](int j) {
@@ -226,11 +186,12 @@ __global__ __launch_bounds__(WT, 4) void hk_pcond(PcArgs a) {  // 4 waves per SI
     // next step: one memory round trip per block instead of one per stage
     Staged<4> nb;
     bool staged = false;
+    int rp = st[0].nu + nx0 + 1, go = rp * st[0].nx1;  // rows(j - 1) and goff(j), carried along the loop
     for (int j = 1; j < ((a.skip & 1) ? 1 : T); j++) {
         const WideStage s = st[j];
         const int nuj = s.nu, nxj = s.nx, nx1 = s.nx1, nzj = nuj + nxj + 1;
-        const int rp = rows(j - 1), rj = rp + nuj, n = rj * nx1;
-        double* Gj = G + goff(j);
+        const int rj = rp + nuj, n = rj * nx1;
+        double* Gj = G + go;
         // the later phases read Gamma_0 .. Gamma_{T-2}; Gamma_{T-1} only goes to B2 (d_cond_BAbt alone returns all)
         const bool keep = j < T - 1 || (ph & PC_PART);
         PST(1);
@@ -259,20 +220,24 @@ __global__ __launch_bounds__(WT, 4) void hk_pcond(PcArgs a) {  // 4 waves per SI
                 GA[nuj + i + c * rj] = v;
                 if (keep) Gj[nuj + i + c * rj] = v;
             });
+        const float rnu = 1.0f / nuj;
         for (int e = tid; e < nuj * nx1; e += WT) {
-            const int i = e % nuj, c = e / nuj;
+            const int c = fdiv(e, rnu), i = e - c * nuj;
             GA[i + c * rj] = Bt[i + c * ldB];
             if (keep) Gj[i + c * rj] = Bt[i + c * ldB];
         }
         (void)n;
         bar();
         PST(3);
+        rp = rj;
+        go += rj * nx1;
     }
     {
-        const int rT = rows(T - 1), nxT = st[T - 1].nx1;
+        const int rT = rp, nxT = st[T - 1].nx1;  // rows(T - 1)
         const int sd = (nxT + 1) / 2 * 2;
+        const float rrT = 1.0f / rT;
         for (int e = tid; e < rT * nxT; e += WT) {
-            const int i = e % rT, c = e / rT;
+            const int c = fdiv(e, rrT), i = e - c * rT;
             *P4w(B2, sd, i, c) = GA[i + c * rT];
         }
     }
@@ -286,18 +251,13 @@ __global__ __launch_bounds__(WT, 4) void hk_pcond(PcArgs a) {  // 4 waves per SI
     if (!(ph & PC_PART)) {
         // zeros only where the recursion below writes nothing: the strict upper triangle and the padding (every
         // entry i >= j, i <= nv, j < nv is stored exactly once by the D / M / final blocks)
-        const int n = ((nv + 1 + 3) / 4 * 4) * cnux2;
-        for (int e = tid; e < n; e += WT) {
-            const int q = e % (4 * cnux2), i = e / (4 * cnux2) * 4 + (q & 3), j = q >> 2;
-            if (i < j || i > nv || j >= nv) R2[e] = 0.0;
-        }
+        const int npan = (nv + 1 + 3) / 4, pan = 4 * cnux2;  // lib4 panels of 4 rows x cnux2 columns
+        for (int pb = 0; pb < npan; pb++)
+            for (int q = tid; q < pan; q += WT) {
+                const int i = 4 * pb + (q & 3), j = q >> 2;
+                if (i < j || i > nv || j >= nv) R2[pb * pan + q] = 0.0;
+            }
     }
-    // offsets of u_s in the condensed variables: off(s) = sum_{r > s} nu_r
-    auto uoff = [&](int s) {
-        int o = 0;
-        for (int r = s + 1; r < T; r++) o += st[r].nu;
-        return o;
-    };
     bar();
     if (T == 1) {
         const WideStage s = st[0];
@@ -305,76 +265,106 @@ __global__ __launch_bounds__(WT, 4) void hk_pcond(PcArgs a) {  // 4 waves per SI
         for (int j = tid >> 6; j < nux; j += WT / 64)
             for (int i = j + (tid & 63); i <= nux; i += 64) *P4w(R2, cnux2, i, j) = P4(RSQ + s.oR, s.sdR, i, j);
     } else {
+        // pL (RSQrq_s + W W'), BAbt_{s-1} (then W) and Gamma_{s-1} sit in LDS in the layouts they have in memory:
+        // pL and BAbt as lib4 panels (panel stride sd of their stage), Gamma flat.  Each arrives by an asynchronous
+        // LDS DMA (dma_copy) issued as soon as its buffer is free: Gamma_{s-2} and RSQrq_{s-1} when the Cholesky and
+        // M are done, BAbt_{s-2} when the step's gemms are done, so the round trips overlap the work in between.
+        auto PL = [&](int sd, int i, int j) -> double& { return Pl[p4i(i, j, sd)]; };
+        auto BT = [&](int sd, int i, int j) -> double& { return Bt[p4i(i, j, sd)]; };
+        auto lib4n = [&](const WideStage& q, int sd) { return (q.nu + q.nx + 1 + 3) / 4 * 4 * sd; };
+        // Outstanding DMA at the top of step s: RSQrq_s -> pL and Gamma_{s-1} -> GA (issued after step s+1's Cholesky,
+        // needed now), then BAbt_{s-1} -> Bt (issued at the end of step s+1, needed only after this step's Cholesky):
+        // the top waits for all but the BAbt copy (nbk = its instruction count in this wave).
+        int nbk;
+        // carried along the loop: os = sum_{r > sI} nu_r (the offset of u_sI in the condensed variables),
+        // r1 = rows(sI - 1), g1 = goff(sI - 1)
+        int os = 0, r1 = rows(T - 2), g1 = goff(T - 2);
         {
-            const WideStage s = st[T - 1];
-            load_dense<8>(Pl, ldP, RSQ + s.oR, s.sdR, s.nu + s.nx + 1, s.nu + s.nx);
+            const WideStage s = st[T - 1], sp = st[T - 2];
+            dma_copy<WT, 16>(Pl, RSQ + s.oR, lib4n(s, s.sdR), tid);
+            dma_copy_any<WT>(GA, G + g1, r1 * s.nx, tid);
+            nbk = dma_copy<WT, 16>(Bt, BAbt + sp.oB, lib4n(sp, sp.sdB), tid);
         }
-        bar();
         for (int sI = (a.skip & 2) ? 0 : T - 1;; sI--) {
             const WideStage s = st[sI];
-            const int nus = s.nu, nxs = s.nx, nux = nus + nxs, os = uoff(sI);
+            const int nus = s.nu, nxs = s.nx, nux = nus + nxs, sdP = s.sdR;
+            dma_wait_keep(nbk);  // pL_s and Gamma_{s-1} have landed (this wave's part)
+            bar();
             if (sI == 0) {
                 for (int j = tid >> 6; j < nux; j += WT / 64)
-                    for (int i = j + (tid & 63); i <= nux; i += 64) *P4w(R2, cnux2, os + i, os + j) = Pl[i + j * ldP];
+                    for (int i = j + (tid & 63); i <= nux; i += 64) *P4w(R2, cnux2, os + i, os + j) = PL(sdP, i, j);
                 break;
             }
             // D: the u_s x u_s block
             for (int j = tid >> 6; j < nus; j += WT / 64)
-                for (int i = j + (tid & 63); i < nus; i += 64) *P4w(R2, cnux2, os + i, os + j) = Pl[i + j * ldP];
+                for (int i = j + (tid & 63); i < nus; i += 64) *P4w(R2, cnux2, os + i, os + j) = PL(sdP, i, j);
             const WideStage sp = st[sI - 1];
             const int nuxp = sp.nu + sp.nx, nzp = nuxp + 1;
-            const int r0 = rows(sI - 1);
-            load_flat<8>(GA, G + goff(sI - 1), r0 * nxs);
+            const int r0 = r1;
             const bool xt = nxs <= 28;  // uniform: the tile Cholesky reads pL directly
-            if (!xt)
+            if (!xt) {
                 for (int j = tid >> 6; j < nxs; j += WT / 64)
-                    for (int i = j + (tid & 63); i <= nxs; i += 64) X[i + j * ldX] = Pl[nus + i + (nus + j) * ldP];
-            bar();
+                    for (int i = j + (tid & 63); i <= nxs; i += 64) X[i + j * ldX] = PL(sdP, nus + i, nus + j);
+                bar();
+            }
             PST(5);
-            if (tid < 64) {
+            if (__builtin_amdgcn_readfirstlane(tid) < 64) {  // wave-uniform branch
                 // Lx = chol_aug(pL_xx; pL_r) on wave 0 while the other three form M
                 if (!(a.skip & 4)) {
                     if (xt)
-                        xchol_tiles(Pl + nus + nus * ldP, ldP, X, ldX, nxs);
+                        xchol_tiles([&](int i, int j) { return PL(sdP, nus + i, nus + j); }, X, ldX, nxs);
                     else
                         xchol_rows(X, ldX, nxs);
                 }
                 PST(6);
             } else {
-                // M: Gamma_{s-1} times the x_s x u_s block of pL; m: + the r row on the gradient row
+                // M: Gamma_{s-1} times the x_s x u_s block of pL; m: + the r row on the gradient row (measured
+                // against 16-row MFMA tiles: the same time, since it runs beside wave 0's Cholesky, and fewer registers)
+                const float rr0 = 1.0f / r0;
                 for (int e = tid - 64; e < ((a.skip & 8) ? 0 : r0 * nus); e += WT - 64) {
-                    const int i = e % r0, c = e / r0;
+                    const int c = fdiv(e, rr0), i = e - c * r0;
                     double acc = 0.0;
-                    for (int l = 0; l < nxs; l++) acc += GA[i + l * r0] * Pl[nus + l + c * ldP];
-                    if (i == r0 - 1) acc += Pl[nux + c * ldP];
+                    for (int l = 0; l < nxs; l++) acc += GA[i + l * r0] * PL(sdP, nus + l, c);
+                    if (i == r0 - 1) acc += PL(sdP, nux, c);
                     *P4w(R2, cnux2, os + nus + i, os + c) = acc;
                 }
             }
-            bar();  // pL and GA are read until here
+            dma_wait();  // BAbt_{s-1} has landed
+            bar();       // pL and GA are read until here
             PST(7);
-            // W = BAbt_{s-1} Lx (in place in Bt), last row += l; pL = RSQ_{s-1} + W W'
-            load_dense<8>(Bt, ldB, BAbt + sp.oB, sp.sdB, nzp, nxs);
-            load_dense<8>(Pl, ldP, RSQ + sp.oR, sp.sdR, nzp, nuxp);
-            bar();
-            PST(8);
-            if (!(a.skip & 16)) {
-                // W = BAbt_{s-1} Lx (+ l on the last row) in place over Bt, then pL += W W' (lower), both on MFMA
+            // RSQrq_{s-1} into pL and Gamma_{s-2} into GA while W = BAbt_{s-1} Lx (+ l on the last row) forms in place
+            // over BAbt_{s-1}; then pL += W W' (lower); both products on MFMA
+            dma_copy<WT, 16>(Pl, RSQ + sp.oR, lib4n(sp, sp.sdR), tid);
+            const int r2 = r1 - sp.nu, g2 = sI >= 2 ? g1 - r2 * st[sI - 2].nx1 : 0;  // rows / goff(sI - 2)
+            const int ngm = sI >= 2 ? dma_copy_any<WT>(GA, G + g2, r2 * sp.nx, tid) : 0;
+            const int sdB = sp.sdB, sdQ = sp.sdR;
+            if (!(a.skip & 16))
                 mfma_gemm(
-                    nzp, nxs, nxs, [&](int i, int l) { return Bt[i + l * ldB]; },
+                    nzp, nxs, nxs, [&](int i, int l) { return BT(sdB, i, l); },
                     [&](int l, int c) { return l >= c ? X[l + c * ldX] : 0.0; },
                     [&](int i, int c, double v) {
                         if (i == nuxp) v += X[nxs + c * ldX];
-                        Bt[i + c * ldB] = v;
+                        BT(sdB, i, c) = v;
                     });
-                bar();
-                mfma_gemm(
-                    nzp, nuxp, nxs, [&](int i, int l) { return Bt[i + l * ldB]; },
-                    [&](int l, int j) { return Bt[j + l * ldB]; },
-                    [&](int i, int j, double v) {
-                        if (i >= j) Pl[i + j * ldP] += v;
-                    });
-            }
+            dma_wait_keep(ngm);  // RSQrq_{s-1} has landed; Gamma_{s-2} may still be in flight
             bar();
+            PST(8);
+            if (!(a.skip & 16))
+                mfma_gemm(
+                    nzp, nuxp, nxs, [&](int i, int l) { return BT(sdB, i, l); },
+                    [&](int l, int j) { return BT(sdB, j, l); },
+                    [&](int i, int j, double v) {
+                        if (i >= j) PL(sdQ, i, j) += v;
+                    });
+            bar();  // W is read
+            nbk = 0;
+            if (sI >= 2) {
+                const WideStage sq = st[sI - 2];
+                nbk = dma_copy<WT, 16>(Bt, BAbt + sq.oB, lib4n(sq, sq.sdB), tid);
+            }
+            os += nus;
+            r1 = r2;
+            g1 = g2;
             PST(9);
         }
     }
@@ -462,9 +452,10 @@ __global__ __launch_bounds__(WT, 4) void hk_pcond(PcArgs a) {  // 4 waves per SI
             }
         }
         bar();
+        const float rpan = 1.0f / (4 * cnbg);
         if (!(ph & PC_PART))  // DCt2 zeros only outside the rows the copy below writes
             for (int e = tid; e < pnv * cnbg; e += WT) {
-                const int q = e % (4 * cnbg), i = e / (4 * cnbg) * 4 + (q & 3), ig = q >> 2;
+                const int pq = fdiv(e, rpan), q = e - pq * (4 * cnbg), i = pq * 4 + (q & 3), ig = q >> 2;
                 bool z = ig >= nbg;
                 if (!z) {
                     const int sI = gd[ig] >> 16, nt = ntmp[sI];

@@ -19,14 +19,15 @@ constexpr int WS_TILES = 8;  // W = BAbt Lxx output tiles per wave (nz <= 128, n
 constexpr int DT_TILES = 6;  // DCt diag DCt' lower tiles per wave on the LDS-staged path (nz <= 96; larger stages read HBM directly)
 constexpr int BS = 4;
 
-__device__ __forceinline__ int p4i(int i, int j, int sd) { return (i / BS) * BS * sd + i % BS + BS * j; }
+// lib4 index of (i, j), i >= 0 (shifts: the signed / and % by 4 cost a sign fix-up each)
+__device__ __forceinline__ int p4i(int i, int j, int sd) { return (i >> 2) * (BS * sd) + (i & 3) + BS * j; }
 
-__device__ __forceinline__ double P4(const double* A, int sd, int i, int j) {
-    return A[(i / BS) * BS * sd + i % BS + BS * j];
-}
-__device__ __forceinline__ double* P4w(double* A, int sd, int i, int j) {
-    return A + (i / BS) * BS * sd + i % BS + BS * j;
-}
+__device__ __forceinline__ double P4(const double* A, int sd, int i, int j) { return A[p4i(i, j, sd)]; }
+__device__ __forceinline__ double* P4w(double* A, int sd, int i, int j) { return A + p4i(i, j, sd); }
+
+// e / n for 0 <= e < 2^20 from rn = 1.0f / n (a float multiply instead of the ~35-instruction integer division):
+// (e + 0.5) / n lies at least 0.5 / n from an integer, far more than the float rounding of the product.
+__device__ __forceinline__ int fdiv(int e, float rn) { return (int)(((float)e + 0.5f) * rn); }
 // packed lower columns of an nz-row matrix: column j holds rows j..nz-1
 __device__ __forceinline__ int poff(int j, int nz) { return j * nz - (j * (j - 1)) / 2; }
 
@@ -51,18 +52,19 @@ __device__ void load_flat(double* D, const double* src, int n) {
 template <int CH>
 __device__ void load_dense(double* D, int ld, const double* src, int sd, int nr, int nc) {
     const int tid = threadIdx.x, n = nr * nc;
+    const float rn = 1.0f / nr;
     for (int base = 0; base < n; base += WT * CH) {
         double r[CH];
+        int dof[CH];
 #pragma unroll
         for (int u = 0; u < CH; u++) {
-            const int e = base + u * WT + tid, i = e % nr, c = e / nr;
+            const int e = base + u * WT + tid, c = fdiv(e, rn), i = e - c * nr;
             r[u] = gld(src, p4i(i, c, sd), e < n);
+            dof[u] = i + c * ld;
         }
 #pragma unroll
-        for (int u = 0; u < CH; u++) {
-            const int e = base + u * WT + tid, i = e % nr, c = e / nr;
-            if (e < n) D[i + c * ld] = r[u];
-        }
+        for (int u = 0; u < CH; u++)
+            if (base + u * WT + tid < n) D[dof[u]] = r[u];
     }
 }
 // The same copy split in two: pre_dense issues the loads of a block of at most CH * WT elements into registers,
@@ -77,18 +79,20 @@ __device__ __forceinline__ void pre_dense(Staged<CH>& S, const double* src, int 
     const int tid = threadIdx.x, n = nr * nc;
     S.nr = nr;
     S.nc = nc;
+    const float rn = 1.0f / nr;
 #pragma unroll
     for (int u = 0; u < CH; u++) {
-        const int e = u * WT + tid, i = e % nr, c = e / nr;
+        const int e = u * WT + tid, c = fdiv(e, rn), i = e - c * nr;
         S.r[u] = gld(src, p4i(i, c, sd), e < n);
     }
 }
 template <int CH>
 __device__ __forceinline__ void put_dense(const Staged<CH>& S, double* D, int ld) {
     const int tid = threadIdx.x, nr = S.nr, n = S.nr * S.nc;
+    const float rn = 1.0f / nr;
 #pragma unroll
     for (int u = 0; u < CH; u++) {
-        const int e = u * WT + tid, i = e % nr, c = e / nr;
+        const int e = u * WT + tid, c = fdiv(e, rn), i = e - c * nr;
         if (e < n) D[i + c * ld] = S.r[u];
     }
 }
@@ -114,18 +118,20 @@ __device__ __forceinline__ void pre_dense_g(Staged<CH>& S, const double* src, in
     const int n = nr * nc;
     S.nr = nr;
     S.nc = nc;
+    const float rn = 1.0f / nr;
 #pragma unroll
     for (int u = 0; u < CH; u++) {
-        const int e = u * NT + t, i = e % nr, c = e / nr;
+        const int e = u * NT + t, c = fdiv(e, rn), i = e - c * nr;
         S.r[u] = gld(src, p4i(i, c, sd), e < n);
     }
 }
 template <int NT, int CH>
 __device__ __forceinline__ void put_dense_g(const Staged<CH>& S, double* D, int ld, int t) {
     const int nr = S.nr, n = S.nr * S.nc;
+    const float rn = 1.0f / nr;
 #pragma unroll
     for (int u = 0; u < CH; u++) {
-        const int e = u * NT + t, i = e % nr, c = e / nr;
+        const int e = u * NT + t, c = fdiv(e, rn), i = e - c * nr;
         if (e < n) D[i + c * ld] = S.r[u];
     }
 }
@@ -140,6 +146,50 @@ __device__ __forceinline__ void put_flat_g(const Flat<CH>& S, double* D, int n, 
     for (int u = 0; u < CH; u++)
         if (u * NT + t < n) D[u * NT + t] = S.r[u];
 }
+// Asynchronous global -> LDS copy of n doubles (v_global_load_lds): a lane's B bytes land at its wave's LDS base +
+// lane * B without passing through registers, so the copy costs no VGPRs and its round trip overlaps whatever the
+// wave does next.  The NT threads of a group (t = index in the group) split the copy; a wave's part is in LDS after
+// its dma_wait(), and other waves see it after a barrier that follows.  B = 16 needs src and dst 16-byte aligned and
+// n even; B = 4 only 4-byte alignment.
+typedef __attribute__((address_space(3))) void* lds_void_ptr;
+template <int NT, int B>
+__device__ __forceinline__ int dma_copy(double* dst, const double* src, int n, int t) {
+    constexpr int PER = B / 4;  // dwords per lane
+    const int nd = 2 * n, lane = t & 63;
+    int cnt = 0;  // DMA instructions this wave issued (for dma_wait_keep)
+    for (int base = 64 * PER * (t >> 6); base < nd; base += 64 * PER * (NT / 64), cnt++) {  // dwords, wave-uniform
+        if (base + PER * lane < nd) {
+            const void* g = reinterpret_cast<const unsigned*>(src) + base + PER * lane;
+            lds_void_ptr l = (lds_void_ptr)(reinterpret_cast<unsigned*>(dst) + base);
+            if constexpr (B == 16)
+                __builtin_amdgcn_global_load_lds(g, l, 16, 0, 0);
+            else
+                __builtin_amdgcn_global_load_lds(g, l, 4, 0, 0);
+        }
+    }
+    return cnt;
+}
+// 16-byte DMA when both ends are 16-byte aligned and n is even, else 4-byte (uniform choice)
+template <int NT>
+__device__ __forceinline__ int dma_copy_any(double* dst, const double* src, int n, int t) {
+    if ((((unsigned long long)src | (unsigned long long)dst) & 15) == 0 && (n & 1) == 0)
+        return dma_copy<NT, 16>(dst, src, n, t);
+    return dma_copy<NT, 4>(dst, src, n, t);
+}
+__device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// Wait until at most `keep` of this wave's vector-memory operations are outstanding (they complete in issue order):
+// the copies issued before the last `keep` have landed.  keep is wave-uniform; beyond 15 it waits for all.
+__device__ __forceinline__ void dma_wait_keep(int keep) {
+    switch (__builtin_amdgcn_readfirstlane(keep)) {
+#define HK_VMW(n) \
+    case n: asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory"); break;
+        HK_VMW(1) HK_VMW(2) HK_VMW(3) HK_VMW(4) HK_VMW(5) HK_VMW(6) HK_VMW(7) HK_VMW(8)
+        HK_VMW(9) HK_VMW(10) HK_VMW(11) HK_VMW(12) HK_VMW(13) HK_VMW(14) HK_VMW(15)
+#undef HK_VMW
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+}
+
 // lib4 lower trapezoid rows [j, nz) of cols [0, nc) -> packed lower columns (nz <= 128: two rows per lane)
 template <int CU>
 __device__ void load_lower(double* M, const double* src, int sd, int nz, int nc) {
@@ -208,6 +258,63 @@ __device__ __forceinline__ void wave_solve_ln(double* v, const double* M, const 
     }
     if (l < n) v[l] = v0;
     if (l + 64 < n) v[l + 64] = v1;
+}
+
+// One 4-pivot block B of a Cholesky held as 16x16 MFMA tiles (the C/D layout: register r at lane (g,c) holds tile
+// row 4r+g, column c).  D is the diagonal tile in symmetric storage (register r = rows / columns 4r..4r+3, so the
+// tile's row c is its column c); U[0..nU) are the tiles below it, transposed (register r at lane (g,c) = A[16(I+1)+c]
+// [4r+g]: tile row c of U[I] is matrix row 16(I+1)+c).  The block's 4x4 diagonal is broadcast (DPP row_newbcast) and
+// factorised redundantly in every lane (pivot clamp d > 1e-15 else 0, kernel_dpotrf_c99_lib4.c:555-640, 1/sqrt(d)
+// from v_rsq_f64 + one refinement, hk::chol_inv), each lane solves its own row of the block column in D and in
+// every U[I] (one row-group gather each, the reference's in-block operation order), and the rank-4 update of the
+// block's later columns is one v_mfma_f64_16x16x4 per tile.  On return register B of D and of each U[I] holds the
+// factor's block column (lane (g,c): L[row c][4B+g]; D's diagonal is d_g i_g = sqrt(d_g)) and invd the inverse
+// diagonal at lanes c = 4B..4B+3.  T11 (optional, D-shaped): the trailing tile of the rows below, updated by
+// -U[0] U[0]' (the two-tile Cholesky of the condensing).  A pivot index with a zero diagonal entry (padding, or a
+// row that is not a column) clamps to a zero column.
+template <int B, int NB, bool T11UPD>
+__device__ __forceinline__ void tile_chol_block(hk::d4& D, hk::d4* U, int nU, hk::d4* T11, double& invd) {
+    using hk::row_bcast;
+    const int c = threadIdx.x & 15;
+    double x[4];
+    hk::rowgroup_gather(D[B], x);
+    const double a00 = row_bcast<4 * B + 0>(x[0]);
+    const double a10 = row_bcast<4 * B + 1>(x[0]), a11 = row_bcast<4 * B + 1>(x[1]);
+    const double a20 = row_bcast<4 * B + 2>(x[0]), a21 = row_bcast<4 * B + 2>(x[1]);
+    const double a22 = row_bcast<4 * B + 2>(x[2]);
+    const double a30 = row_bcast<4 * B + 3>(x[0]), a31 = row_bcast<4 * B + 3>(x[1]);
+    const double a32 = row_bcast<4 * B + 3>(x[2]), a33 = row_bcast<4 * B + 3>(x[3]);
+    const double i0 = hk::chol_inv(a00);
+    const double l10 = a10 * i0, l20 = a20 * i0, l30 = a30 * i0;
+    const double y0 = x[0] * i0;
+    const double i1 = hk::chol_inv(fma(-l10, l10, a11));
+    const double l21 = fma(-l20, l10, a21) * i1, l31 = fma(-l30, l10, a31) * i1;
+    const double y1 = fma(-y0, l10, x[1]) * i1;
+    const double i2 = hk::chol_inv(fma(-l21, l21, fma(-l20, l20, a22)));
+    const double l32 = fma(-l31, l21, fma(-l30, l20, a32)) * i2;
+    const double y2 = fma(-y1, l21, fma(-y0, l20, x[2])) * i2;
+    const double i3 = hk::chol_inv(fma(-l32, l32, fma(-l31, l31, fma(-l30, l30, a33))));
+    const double y3 = fma(-y2, l32, fma(-y1, l31, fma(-y0, l30, x[3]))) * i3;
+    const double yg = hk::sel_g(y0, y1, y2, y3);
+    D[B] = yg;
+    if ((c >> 2) == B) invd = hk::sel_q(i0, i1, i2, i3);
+    const double a = c > 4 * B + 3 ? yg : 0.0;
+    if (B < 3) D = hk::mfma(-a, a, D);
+#pragma unroll
+    for (int I = 0; I < NB; I++) {
+        if (I < nU) {  // uniform
+            double z[4];
+            hk::rowgroup_gather(U[I][B], z);
+            const double w0 = z[0] * i0;
+            const double w1 = fma(-w0, l10, z[1]) * i1;
+            const double w2 = fma(-w1, l21, fma(-w0, l20, z[2])) * i2;
+            const double w3 = fma(-w2, l32, fma(-w1, l31, fma(-w0, l30, z[3]))) * i3;
+            const double wg = hk::sel_g(w0, w1, w2, w3);
+            U[I][B] = wg;
+            if (B < 3) U[I] = hk::mfma(-a, wg, U[I]);  // A[row j][i] -= sum_k L[i][4B+k] L[row j][4B+k], i below
+            if (T11UPD && I == 0) *T11 = hk::mfma(-wg, wg, *T11);
+        }
+    }
 }
 
 // C (m x n) = A (m x K) B (K x n) on v_mfma_f64_16x16x4: wave w takes output tiles w, w+4, ..; a(i, k) / b(k, j)
@@ -452,6 +559,7 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
             const double* qg = q.qx + s.oD + s.pnb;
             const int ng = s.ng, sdG = s.sdG, nI = (nz + 15) >> 4, nK = (ng + 3) >> 2, nT = nI * (nI + 1) / 2;
             const int ldS = 16 * nI;
+            const float rS = 1.0f / ldS;
             if (nT <= 4 * DT_TILES && 16 * ldS + 32 <= a.offV - a.offW) {  // uniform
                 // K blocks of 16 constraints staged in LDS (W and X are free between the syrk and the Cholesky):
                 // the block's DCt columns (zero beyond nux / ng), diag(Qx_g) and the qx_g entries, one memory round
@@ -468,7 +576,7 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
                     double r[8];
 #pragma unroll
                     for (int u = 0; u < 8; u++) {
-                        const int e = u * WT + tid, i = e % ldS, kk = e / ldS;
+                        const int e = u * WT + tid, kk = fdiv(e, rS), i = e - kk * ldS;
                         r[u] = gld(D, p4i(i, kb + kk, sdG), e < 16 * ldS && i < nux && kb + kk < ng);
                     }
                     const double dq = gld(Qg, kb + (tid & 15), tid < 16 && kb + tid < ng);
@@ -554,58 +662,54 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
         }
         bar();
         WSUB(7);
-        // Cholesky with the augmented row, blocked by 16-column panels: wave 0 factors the panel (row i on
-        // lanes i - j0 and i - j0 + 64, shuffles for the pivot row, no workgroup barrier), then all waves
-        // apply the panel's rank-16 update to the trailing lower tiles on MFMA
+        // Cholesky with the augmented row, blocked by 16-column panels: the four waves factor the panel as MFMA tiles
+        // (each its own rows, no workgroup barrier inside), then apply its rank-16 update to the trailing lower
+        // tiles on MFMA
         double* Lk = F + s.oL;
         double* dL = Lk + poff(nux, nz);
         for (int p0 = 0; p0 < ((a.skip & 2) ? 0 : nux); p0 += 16) {
             const int pe = p0 + 16 < nux ? p0 + 16 : nux;
-            if (wv == 0) {
-                // the panel (rows p0.., its <= 16 columns) in registers: lane L holds rows p0+L and p0+L+64
-                const int pw = pe - p0, r0 = p0 + lane, r1 = r0 + 64;
-                double c0[16], c1[16];
+            {
+                // the panel as MFMA tiles (tile_chol_block): D = rows / columns p0..p0+15, factorised redundantly
+                // by every wave; the tiles below it (rows p0+16(I+1).., nz <= 128: I < 7) are solved by wave I % 4
+                // (U[t] = tile wv + 4t); entries outside the panel's columns read as 0
+                const int pw = pe - p0, nUt = (nz - p0 - 1) >> 4, g = lane >> 4;
+                const int w = __builtin_amdgcn_readfirstlane(wv);
+                const int nU = (w < nUt) + (w + 4 < nUt);
+                auto ld = [&](int r, int j) -> double {  // A[r][j], r >= j
+                    return (j < pe && r < nz) ? M[poff(j, nz) + r - j] : 0.0;
+                };
+                hk::d4 D, U[2];
 #pragma unroll
-                for (int jj = 0; jj < 16; jj++) {
-                    const int j = p0 + jj, cj = poff(j < nux ? j : 0, nz);
-                    c0[jj] = (jj < pw && r0 >= j && r0 < nz) ? M[cj + r0 - j] : 0.0;
-                    c1[jj] = (jj < pw && r1 < nz) ? M[cj + r1 - j] : 0.0;
+                for (int r = 0; r < 4; r++) {
+                    const int i = p0 + 4 * r + g, j = p0 + c16;
+                    D[r] = i >= j ? ld(i, j) : ld(j, i);
+#pragma unroll
+                    for (int t = 0; t < 2; t++)
+                        U[t][r] = t < nU ? ld(p0 + 16 * (w + 4 * t + 1) + c16, p0 + 4 * r + g) : 0.0;
                 }
+                double invd = 0.0;
+                if (pw > 0) tile_chol_block<0, 2, false>(D, U, nU, nullptr, invd);
+                if (pw > 4) tile_chol_block<1, 2, false>(D, U, nU, nullptr, invd);
+                if (pw > 8) tile_chol_block<2, 2, false>(D, U, nU, nullptr, invd);
+                if (pw > 12) tile_chol_block<3, 2, false>(D, U, nU, nullptr, invd);
+                auto put = [&](int row, int j, double v) {
+                    if (row < nz) {
+                        M[poff(j, nz) + row - j] = v;
+                        if (j >= nu) X[(row - nu) + (j - nu) * ldX] = v;
+                    }
+                };
 #pragma unroll
-                for (int jj = 0; jj < 16; jj++) {
-                    if (jj < pw) {
-                        const double d = rdlane(c0[jj], jj);
-                        // the pivot clamp d > 1e-15 else 0 (kernel_dpotrf_c99_lib4.c:555-640) with s = sqrt(d), 1/s from
-                        // v_rsq_f64 plus one third-order refinement (hk::chol_pivot, <= 1.2 half-ulp) instead of an IEEE
-                        // sqrt and divide on the pivot chain
-                        double sq, inv;
-                        hk::chol_pivot(d, sq, inv);
-                        c0[jj] = lane == jj ? sq : (lane > jj ? c0[jj] * inv : 0.0);
-                        c1[jj] = c1[jj] * inv;
-                        if (lane == 0) M[poff(nux, nz) + p0 + jj] = inv;
+                for (int r = 0; r < 4; r++) {
+                    const int j = p0 + 4 * r + g;
+                    if (j < pe) {
+                        if (w == 0 && c16 >= 4 * r + g) put(p0 + c16, j, D[r]);
 #pragma unroll
-                        for (int cc = jj + 1; cc < 16; cc++) {
-                            const double lc = rdlane(c0[jj], cc);
-                            c0[cc] -= c0[jj] * lc;
-                            c1[cc] -= c1[jj] * lc;
-                        }
+                        for (int t = 0; t < 2; t++)
+                            if (t < nU) put(p0 + 16 * (w + 4 * t + 1) + c16, j, U[t][r]);
                     }
                 }
-#pragma unroll
-                for (int jj = 0; jj < 16; jj++) {
-                    const int j = p0 + jj;
-                    if (jj < pw) {
-                        const int cj = poff(j, nz);
-                        if (r0 >= j && r0 < nz) {
-                            M[cj + r0 - j] = c0[jj];
-                            if (j >= nu) X[(r0 - nu) + (j - nu) * ldX] = c0[jj];
-                        }
-                        if (r1 < nz) {
-                            M[cj + r1 - j] = c1[jj];
-                            if (j >= nu) X[(r1 - nu) + (j - nu) * ldX] = c1[jj];
-                        }
-                    }
-                }
+                if (w == 0 && g == 0 && p0 + c16 < pe) M[poff(nux, nz) + p0 + c16] = invd;
             }
             bar();
             WSUB(8);
@@ -640,8 +744,9 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
         for (int e = tid; e < poff(nux, nz) + nux; e += WT) Lk[e] = M[e];
         (void)dL;
         // strictly upper part of the copied Lxx stays zero (the next stage's MFMA trmm reads whole tiles)
+        const float rnx = 1.0f / s.nx;
         for (int e = tid; e < s.nx * s.nx; e += WT) {
-            const int i = e % s.nx, cc = e / s.nx;
+            const int cc = fdiv(e, rnx), i = e - cc * s.nx;
             if (i < cc) X[i + cc * ldX] = 0.0;
         }
         bar();

@@ -397,13 +397,17 @@ bool pc_plan(PcPlan& P, int N, const int* nx, const int* nu_in, const int* nb, c
             Nt += P.blk[ii].T;
         }
     }
+    // LDS carve (doubles, every tile 32-byte aligned for the 16-byte LDS DMA): pL as a lib4 RSQrq block
+    // (rup(nz, 4) x sdR), Lx dense, the BAbt tile dense (d_cond_BAbt) or as a lib4 block (d_cond_RSQrq), Gamma_{j-1}
+    int nuxM = 1;
+    for (int k = 0; k < N; k++) nuxM = std::max(nuxM, nu[k] + nx[k]);
     P.ldP = P.ldW = P.ldB = nzM;
     P.ldX = nxM + 1;
     P.offP = 0;
-    P.offX = P.ldP * nzM;
-    P.offB = P.offX + P.ldX * nxM;
+    P.offX = rup(std::max(P.ldP * nzM, rup(nzM, BS) * rup(nuxM, NCL)), 4);
+    P.offB = P.offX + rup(P.ldX * nxM, 4);
     P.offW = P.offB;  // W is formed in place in the BAbt tile
-    P.offGA = P.offB + P.ldB * nxM;
+    P.offGA = P.offB + rup(std::max(P.ldB * nxM, rup(nzM, BS) * rup(nxM, NCL)), 4);
     P.offGB = 0;
     P.pc_lds = P.offGA + (int)gmax;
     if (gmax > 12 * 256 || nxM > 63) {  // hk_pcond: PC_GCH Gamma outputs per lane; the state Cholesky in one wave
@@ -988,6 +992,10 @@ extern "C" int hpmpc_mi355x_pcond_batch(const hpmpc_mi355x_pcond_plan* q, int np
                                         double* BAbt2, double* RSQrq2, double* DCt2, double* d2, void* stream) {
     if (!q) return HPMPC_MI355X_EUNSUPPORTED;
     hk_set_error(0, nullptr);
+    if (((uintptr_t)BAbt | (uintptr_t)RSQrq) & 15) {  // hk_pcond copies their lib4 blocks by 16-byte LDS DMA
+        hk_set_error(HPMPC_MI355X_EUNSUPPORTED, "pcond_batch: BAbt / RSQrq must be 16-byte aligned");
+        return HPMPC_MI355X_EUNSUPPORTED;
+    }
     PcArgs a;
     fill_pc_args(q->P, a);
     a.nprob = nprob;
