@@ -16,23 +16,29 @@
 #ifdef HK_STAMPS
 // Diagnostic build only: per-phase s_memtime cycle totals of hk_pcond workgroup (0, 0) (tools/pcond_phases.py)
 __device__ unsigned long long* g_pdbg;
-__device__ unsigned long long g_pst_t0;
 extern "C" __attribute__((visibility("default"))) int hpmpc_mi355x_pcond_debug(void* dev_ptr) {
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_pdbg), &dev_ptr, sizeof(void*));
 }
-#define PST(i)                                                                                  \
-    do {                                                                                        \
-        unsigned long long t_;                                                                  \
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");               \
-        if (g_pdbg && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {                 \
-            if ((i) > 0) g_pdbg[i] += t_ - g_pst_t0;                                            \
-            g_pst_t0 = t_;                                                                      \
-        }                                                                                       \
+// per-phase totals kept in (wave-uniform) registers and written once at the end, so a stamp costs no memory access
+#define PST_DECL unsigned long long pst_acc[16] = {}, pst_t0 = 0
+#define PST(i)                                                                    \
+    do {                                                                          \
+        unsigned long long t_;                                                    \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+        if ((i) > 0) pst_acc[i] += t_ - pst_t0;                                   \
+        pst_t0 = t_;                                                              \
+    } while (0)
+#define PST_FLUSH()                                                               \
+    do {                                                                          \
+        if (g_pdbg && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)     \
+            for (int q_ = 0; q_ < 16; q_++) g_pdbg[q_] += pst_acc[q_];            \
     } while (0)
 #else
+#define PST_DECL (void)0
 #define PST(i) \
     do {       \
     } while (0)
+#define PST_FLUSH() (void)0
 #endif
 
 
@@ -40,6 +46,7 @@ extern "C" __attribute__((visibility("default"))) int hpmpc_mi355x_pcond_debug(v
 __global__ __launch_bounds__(WT) void hk_wide_sv(WideArgs a) {
     const int p = blockIdx.x + a.p0;
     if (p >= a.nprob) return;
+    wide_stage_table(a);
     wide_sv_body(a, wide_prob(a, p));
 }
 
@@ -97,7 +104,9 @@ __device__ __forceinline__ void xchol_tiles(FS S, double* X, int ldX, int nx) {
     auto at = [&](int t1, int t2) -> double {  // A[t1][t2] of the padded symmetric block
         const int i1 = src(t1), i2 = src(t2);
         const int r = i1 > i2 ? i1 : i2, q = i1 > i2 ? i2 : i1;
-        return (q >= 0 && q < nx) ? S(r, q) : 0.0;
+        const bool ok = q >= 0 && q < nx;
+        const double v = S(ok ? r : 0, ok ? q : 0);  // unconditional load (no exec-masked branch), then a select
+        return ok ? v : 0.0;
     };
     hk::d4 T00, U, T11;
 #pragma unroll
@@ -131,14 +140,19 @@ __device__ __forceinline__ void xchol_tiles(FS S, double* X, int ldX, int nx) {
 // LDS instead (130 KiB at configs[4]) measured 2.7x slower: the workgroup's own time fell 17 %, but one workgroup
 // per CU instead of four leaves nothing to hide its dependency chains behind.
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(WT, 4) void hk_pcond(PcArgs a) {  // 4 waves per SIMD: four workgroups per CU (the LDS fits four)
+// GM: output tiles per wave of its gemms (host-chosen from the block shapes: 4, or 8 at two workgroups per CU)
+template <int GM>
+__global__ __launch_bounds__(WT, GM <= 4 ? 4 : 2) void hk_pcond(PcArgs a) {  // 4 waves per SIMD at GM 4: four workgroups per CU (the LDS fits four)
     extern __shared__ double sm[];
     const int ii = blockIdx.x, p = blockIdx.y + a.p0;
     if (p >= a.nprob || ii >= a.N2) return;
     const int tid = threadIdx.x;
     const PcBlock blk = a.blk[ii];
     const int T = blk.T, nx0 = blk.nx0, nv = blk.nut + nx0;
-    const WideStage* st = a.st + blk.s0;
+    WideStage* stl = reinterpret_cast<WideStage*>(sm + a.offST);  // the block's stage records, in LDS
+    stage_table_to_lds(stl, a.st + blk.s0, T);
+    bar();
+    const StTab st{stl};
     const double* BAbt = a.BAbt + (long)p * a.sB;
     const double* RSQ = a.RSQ + (long)p * a.sR;
     const double* dv = a.d + (long)p * a.sD;
@@ -172,13 +186,14 @@ __global__ __launch_bounds__(WT, 4) void hk_pcond(PcArgs a) {  // 4 waves per SI
     // held in registers, then overwrites GA and streams to HBM ----
     double* GA = sm + a.offGA;
     const int ph = a.ph;
+    PST_DECL;
     PST(0);
     if (ph & PC_BABT) {
     {
         const WideStage s = st[0];
         const int r0 = s.nu + s.nx + 1;
         load_dense<8>(GA, r0, BAbt + s.oB, s.sdB, r0, s.nx1);
-        bar();
+        lds_bar();
         if (T > 1 || (ph & PC_PART))
             for (int e = tid; e < r0 * s.nx1; e += WT) G[e] = GA[e];
     }
@@ -199,7 +214,7 @@ __global__ __launch_bounds__(WT, 4) void hk_pcond(PcArgs a) {  // 4 waves per SI
             put_dense(nb, Bt, ldB);
         else
             load_dense<8>(Bt, ldB, BAbt + s.oB, s.sdB, nzj, nx1);
-        bar();
+        lds_bar();
         PST(2);
         staged = false;
         if (j + 1 < ((a.skip & 1) ? 1 : T)) {
@@ -210,9 +225,10 @@ __global__ __launch_bounds__(WT, 4) void hk_pcond(PcArgs a) {  // 4 waves per SI
                 staged = true;
             }
         }
+        PST(11);
         // rows nuj.. : Gamma_{j-1} A_j (+ b_j on the last row) on MFMA; rows ..nuj: B_j.  The results overwrite
         // GA (leading dimension rp -> rj) after mfma_gemm's barrier, when every operand read is done.
-        mfma_gemm(
+        mfma_gemm<GM>(
             rp, nx1, nxj, [&](int i, int l) { return GA[i + l * rp]; },
             [&](int l, int c) { return Bt[nuj + l + c * ldB]; },
             [&](int i, int c, double v) {
@@ -221,13 +237,14 @@ __global__ __launch_bounds__(WT, 4) void hk_pcond(PcArgs a) {  // 4 waves per SI
                 if (keep) Gj[nuj + i + c * rj] = v;
             });
         const float rnu = 1.0f / nuj;
+        PST(12);
         for (int e = tid; e < nuj * nx1; e += WT) {
             const int c = fdiv(e, rnu), i = e - c * nuj;
             GA[i + c * rj] = Bt[i + c * ldB];
             if (keep) Gj[i + c * rj] = Bt[i + c * ldB];
         }
         (void)n;
-        bar();
+        lds_bar();
         PST(3);
         rp = rj;
         go += rj * nx1;
@@ -289,7 +306,7 @@ __global__ __launch_bounds__(WT, 4) void hk_pcond(PcArgs a) {  // 4 waves per SI
             const WideStage s = st[sI];
             const int nus = s.nu, nxs = s.nx, nux = nus + nxs, sdP = s.sdR;
             dma_wait_keep(nbk);  // pL_s and Gamma_{s-1} have landed (this wave's part)
-            bar();
+            lds_bar();
             if (sI == 0) {
                 for (int j = tid >> 6; j < nux; j += WT / 64)
                     for (int i = j + (tid & 63); i <= nux; i += 64) *P4w(R2, cnux2, os + i, os + j) = PL(sdP, i, j);
@@ -305,7 +322,7 @@ __global__ __launch_bounds__(WT, 4) void hk_pcond(PcArgs a) {  // 4 waves per SI
             if (!xt) {
                 for (int j = tid >> 6; j < nxs; j += WT / 64)
                     for (int i = j + (tid & 63); i <= nxs; i += 64) X[i + j * ldX] = PL(sdP, nus + i, nus + j);
-                bar();
+                lds_bar();
             }
             PST(5);
             if (__builtin_amdgcn_readfirstlane(tid) < 64) {  // wave-uniform branch
@@ -330,7 +347,7 @@ __global__ __launch_bounds__(WT, 4) void hk_pcond(PcArgs a) {  // 4 waves per SI
                 }
             }
             dma_wait();  // BAbt_{s-1} has landed
-            bar();       // pL and GA are read until here
+            lds_bar();       // pL and GA are read until here
             PST(7);
             // RSQrq_{s-1} into pL and Gamma_{s-2} into GA while W = BAbt_{s-1} Lx (+ l on the last row) forms in place
             // over BAbt_{s-1}; then pL += W W' (lower); both products on MFMA
@@ -338,25 +355,30 @@ __global__ __launch_bounds__(WT, 4) void hk_pcond(PcArgs a) {  // 4 waves per SI
             const int r2 = r1 - sp.nu, g2 = sI >= 2 ? g1 - r2 * st[sI - 2].nx1 : 0;  // rows / goff(sI - 2)
             const int ngm = sI >= 2 ? dma_copy_any<WT>(GA, G + g2, r2 * sp.nx, tid) : 0;
             const int sdB = sp.sdB, sdQ = sp.sdR;
+            PST(13);
             if (!(a.skip & 16))
-                mfma_gemm(
+                mfma_gemm<GM>(
                     nzp, nxs, nxs, [&](int i, int l) { return BT(sdB, i, l); },
-                    [&](int l, int c) { return l >= c ? X[l + c * ldX] : 0.0; },
+                    [&](int l, int c) {
+                        const double v = X[l + c * ldX];
+                        return l >= c ? v : 0.0;
+                    },
                     [&](int i, int c, double v) {
                         if (i == nuxp) v += X[nxs + c * ldX];
                         BT(sdB, i, c) = v;
                     });
+            PST(14);
             dma_wait_keep(ngm);  // RSQrq_{s-1} has landed; Gamma_{s-2} may still be in flight
-            bar();
+            lds_bar();
             PST(8);
             if (!(a.skip & 16))
-                mfma_gemm(
+                mfma_gemm<GM>(
                     nzp, nuxp, nxs, [&](int i, int l) { return BT(sdB, i, l); },
                     [&](int l, int j) { return BT(sdB, j, l); },
                     [&](int i, int j, double v) {
                         if (i >= j) PL(sdQ, i, j) += v;
                     });
-            bar();  // W is read
+            lds_bar();  // W is read
             nbk = 0;
             if (sI >= 2) {
                 const WideStage sq = st[sI - 2];
@@ -479,6 +501,7 @@ __global__ __launch_bounds__(WT, 4) void hk_pcond(PcArgs a) {  // 4 waves per SI
         double* dN = a.d2 + (long)p * a.sD2 + a.oD2N;  // and its bounds (the IPM on the condensed problem reads them)
         for (int e = tid; e < a.nDN; e += WT) dN[e] = dv[sN.oD + e];
     }
+    PST_FLUSH();
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -654,6 +677,7 @@ __global__ __launch_bounds__(WT) void hk_pexpand(PxArgs a) {
 __global__ __launch_bounds__(WT) void hk_wide_trs(WideArgs a) {
     const int p = blockIdx.x + a.p0;
     if (p >= a.nprob) return;
+    wide_stage_table(a);
     wide_trs_body(a, wide_prob(a, p));
 }
 
@@ -671,7 +695,10 @@ extern "C" int hk_wide_launch(int which, const void* args, int count, int lds_do
         }
         case 1: {
             const PcArgs& a = *static_cast<const PcArgs*>(args);
-            hipLaunchKernelGGL(hk_pcond, dim3(a.N2, count), dim3(WT), lds, stream, a);
+            if (a.gm <= 4)
+                hipLaunchKernelGGL(hk_pcond<4>, dim3(a.N2, count), dim3(WT), lds, stream, a);
+            else
+                hipLaunchKernelGGL(hk_pcond<8>, dim3(a.N2, count), dim3(WT), lds, stream, a);
             break;
         }
         case 2: {

@@ -18,6 +18,8 @@ struct WideStage {
     int oG, sdG;           // DCt_k (lib4, nux x ng, panel stride round_up(ng, 2)) in the problem's DCt array
 };
 
+static_assert(sizeof(WideStage) % sizeof(double) == 0, "LDS stage tables are carved in doubles");
+
 struct WideArgs {
     int N, nprob, p0;
     const WideStage* st;
@@ -30,7 +32,8 @@ struct WideArgs {
     double *ux, *pi, *Pb;  // solution vectors per problem (stage offsets oU / oP)
     long long sU, sP;
     int compute_pi, compute_Pb;
-    int offW, offX, offV;  // dynamic LDS carve (doubles): M packed | W | X | v
+    int offW, offX, offV;  // dynamic LDS carve (doubles): M packed | W | X | v | stage table (offST)
+    int offST;
     int ldW, ldX;
     int skip;  // profiling only (HK_WIDE_SKIP): bit 0 forward, bit 1 Cholesky, bit 2 trmm/syrk -- results invalid
     int trf;   // d_back_ric_rec_trf_tv_res: no augmented row (stored as zeros), no forward
@@ -76,12 +79,14 @@ struct PcArgs {
     int sdRN, nzN;           // its lib4 panel stride and rows
     int offP, offX, offW, offB, ldP, ldX, ldW, ldB;  // dynamic LDS carve
     int offGA, offGB;                                // Gamma_{j-1} / Gamma_j tiles (and stage scratch)
+    int offST;                                       // the block's stage records (WideStage, T of them)
     int skip;  // profiling only (HK_PCOND_SKIP): bit 0 Gamma, 1 RSQ phase, 2 its Cholesky, 3 M product, 4 W/syrk
     int oD2N, nDN;  // terminal stage: its bounds d_N (original offset st[N].oD, nDN doubles) -> d2 at oD2N
     // phases (d_part_cond: PC_ALL).  Without PC_BABT the Gammas are inputs, already in the scratch G; PC_PART runs
     // one building block alone (d_cond_BAbt / _RSQrq / _DCtd): outputs are not cleared first (the caller's
     // contents stay where the reference writes nothing) and the terminal stage is not copied
     int ph;
+    int gm;  // output tiles per wave of the kernel's gemms (4 or 8: the hk_pcond instance)
 };
 enum { PC_BABT = 1, PC_RSQ = 2, PC_DCTD = 4, PC_ALL = 7, PC_PART = 8 };
 

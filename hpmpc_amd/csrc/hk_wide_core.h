@@ -32,6 +32,10 @@ __device__ __forceinline__ int fdiv(int e, float rn) { return (int)(((float)e + 
 __device__ __forceinline__ int poff(int j, int nz) { return j * nz - (j * (j - 1)) / 2; }
 
 __device__ __forceinline__ void bar() { __syncthreads(); }
+// A workgroup barrier for LDS data only: this wave's LDS operations are complete, then s_barrier.  Unlike
+// __syncthreads it does not wait for outstanding global loads and stores (a prefetch or an LDS DMA in flight, the
+// stores of a finished tile), so it may only order LDS traffic; global data passed between threads needs bar().
+__device__ __forceinline__ void lds_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // Global -> LDS staging with CH loads in flight per lane: every load of a batch is issued before the first
 // LDS store (raw buffer loads, masked lanes read out of range), so a stage tile costs one or two memory
@@ -146,6 +150,39 @@ __device__ __forceinline__ void put_flat_g(const Flat<CH>& S, double* D, int n, 
     for (int u = 0; u < CH; u++)
         if (u * NT + t < n) D[u * NT + t] = S.r[u];
 }
+// A stage record from an LDS table with every field made wave-uniform (readfirstlane).  Stage tables in global memory
+// cannot be read with scalar loads (the kernels store to global memory, so the compiler cannot prove the table
+// unchanged): each read would be a vector load followed by a wait for ALL outstanding vector-memory operations,
+// prefetches and LDS DMA included.  Kernels copy their stage table into LDS once (stage_table_to_lds) and read it
+// through StTab.
+__device__ __forceinline__ WideStage rfl_stage(const WideStage& v) {
+    constexpr int NI = sizeof(WideStage) / sizeof(int);
+    const int* a = reinterpret_cast<const int*>(&v);
+    WideStage u;
+    int* b = reinterpret_cast<int*>(&u);
+#pragma unroll
+    for (int i = 0; i < NI; i++) b[i] = __builtin_amdgcn_readfirstlane(a[i]);
+    return u;
+}
+struct StTab {
+    const WideStage* p;
+    __device__ __forceinline__ WideStage operator[](int i) const { return rfl_stage(p[i]); }
+};
+// n stage records from global memory into an LDS table (all threads of the workgroup; a barrier must follow)
+__device__ __forceinline__ void stage_table_to_lds(WideStage* dst, const WideStage* src, int n) {
+    constexpr int NI = sizeof(WideStage) / sizeof(int);
+    const int* a = reinterpret_cast<const int*>(src);
+    int* b = reinterpret_cast<int*>(dst);
+    for (int e = threadIdx.x; e < n * NI; e += WT) b[e] = a[e];
+}
+
+// The wide kernels' stage table into LDS at offST (every thread; ends with a barrier)
+__device__ __forceinline__ void wide_stage_table(const WideArgs& a) {
+    extern __shared__ double sm[];
+    stage_table_to_lds(reinterpret_cast<WideStage*>(sm + a.offST), a.st, a.N + 1);
+    __syncthreads();
+}
+
 // Asynchronous global -> LDS copy of n doubles (v_global_load_lds): a lane's B bytes land at its wave's LDS base +
 // lane * B without passing through registers, so the copy costs no VGPRs and its round trip overlaps whatever the
 // wave does next.  The NT threads of a group (t = index in the group) split the copy; a wave's part is in LDS after
@@ -317,39 +354,52 @@ __device__ __forceinline__ void tile_chol_block(hk::d4& D, hk::d4* U, int nU, hk
     }
 }
 
-// C (m x n) = A (m x K) B (K x n) on v_mfma_f64_16x16x4: wave w takes output tiles w, w+4, ..; a(i, k) / b(k, j)
-// read the operands (0 outside), out(i, j, v) stores a result after a workgroup barrier, so C may overwrite
-// an operand.  All threads of the workgroup must call it.  At most 4 * GM_TILES output tiles.
-constexpr int GM_TILES = 8;
-template <class FA, class FB, class FO>
+// C (m x n) = A (m x K) B (K x n) on v_mfma_f64_16x16x4: wave w takes output tiles w, w+4, .. (at most GM per
+// wave, host-checked); a(i, k) / b(k, j) read the operands (LDS; 0 outside), out(i, j, v) stores a result after a
+// workgroup barrier, so C may overwrite an operand.  All threads of the workgroup must call it.  The K chunks are the
+// outer loop and the wave's tiles the inner one, so each chunk issues every tile's operand loads before their MFMAs:
+// one LDS round trip per chunk for all tiles, and independent MFMAs back to back instead of one dependent chain per
+// tile after another.
+template <int GM, class FA, class FB, class FO>
 __device__ __forceinline__ void mfma_gemm(int m, int n, int K, FA a, FB b, FO out) {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, c16 = lane & 15, g4 = lane >> 4;
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), c16 = lane & 15,
+              g4 = lane >> 4;
     const int nI = (m + 15) >> 4, nT = nI * ((n + 15) >> 4), nK = (K + 3) >> 2;
-    hk::d4 acc[GM_TILES];
+    int ra[GM], cb[GM];
+    hk::d4 acc[GM];
 #pragma unroll
-    for (int u = 0; u < GM_TILES; u++) {
+    for (int u = 0; u < GM; u++) {
+        const int t = wv + 4 * u, ti = t / nI;
+        ra[u] = 16 * (t - ti * nI) + c16;
+        cb[u] = 16 * ti + c16;
         acc[u] = hk::d4{0.0, 0.0, 0.0, 0.0};
-        const int t = wv + 4 * u;
-        if (t < nT) {
-            const int ra = 16 * (t % nI) + c16, cb = 16 * (t / nI) + c16;
-            for (int kc = 0; kc < nK; kc++) {
-                const int kk = 4 * kc + g4;
-                const double av = (ra < m && kk < K) ? a(ra, kk) : 0.0;
-                const double bv = (cb < n && kk < K) ? b(kk, cb) : 0.0;
-                acc[u] = hk::mfma(av, bv, acc[u]);
+    }
+    for (int kc = 0; kc < nK; kc++) {
+        const int kk = 4 * kc + g4;
+        double av[GM], bv[GM];
+        const int kq = kk < K ? kk : K - 1;
+#pragma unroll
+        for (int u = 0; u < GM; u++) {
+            if (wv + 4 * u < nT) {  // uniform
+                // unconditional loads at clamped (valid) indices, then a select: a conditional load is compiled to
+                // an exec-masked branch with its own lgkmcnt wait per operand
+                const double x = a(ra[u] < m ? ra[u] : m - 1, kq), y = b(kq, cb[u] < n ? cb[u] : n - 1);
+                av[u] = (ra[u] < m && kk < K) ? x : 0.0;
+                bv[u] = (cb[u] < n && kk < K) ? y : 0.0;
             }
         }
-    }
-    __syncthreads();
 #pragma unroll
-    for (int u = 0; u < GM_TILES; u++) {
-        const int t = wv + 4 * u;
-        if (t < nT) {
-            const int col = 16 * (t / nI) + c16;
+        for (int u = 0; u < GM; u++)
+            if (wv + 4 * u < nT) acc[u] = hk::mfma(av[u], bv[u], acc[u]);
+    }
+    lds_bar();  // every operand read is done (the operands live in LDS)
+#pragma unroll
+    for (int u = 0; u < GM; u++) {
+        if (wv + 4 * u < nT) {
 #pragma unroll
             for (int r = 0; r < 4; r++) {
-                const int row = 16 * (t % nI) + g4 + 4 * r;
-                if (row < m && col < n) out(row, col, acc[u][r]);
+                const int row = ra[u] - c16 + g4 + 4 * r;
+                if (row < m && cb[u] < n) out(row, cb[u], acc[u][r]);
             }
         }
     }
@@ -431,6 +481,7 @@ __device__ __forceinline__ WideProb wide_prob(const WideArgs& a, int p) {
 #endif
 __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) {
     extern __shared__ double sm[];
+    const StTab st{reinterpret_cast<const WideStage*>(sm + a.offST)};  // filled by the kernel (wide_stage_table)
     const int tid = threadIdx.x;
     double* M = sm;
     double* W = sm + a.offW;
@@ -446,7 +497,7 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
     double* Pb = q.Pb;
 
     for (int k = a.N; k >= 0; k--) {
-        const WideStage s = a.st[k];
+        const WideStage s = st[k];
         const int nu = s.nu, nux = s.nu + s.nx, nz = nux + 1, nx1 = s.nx1;
         WSUB(0);
         load_lower<4>(M, RSQ + s.oR, s.sdR, nz, nux);
@@ -756,12 +807,12 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
     // forward substitution: L_k (packed + 1/diag) and BAbt_k are staged into LDS (M, W) per stage
     double* tmp = X;  // Lxx is no longer needed: nx1 doubles of scratch for pi
     {
-        const WideStage s0 = a.st[0];
+        const WideStage s0 = st[0];
         const int nz0 = s0.nu + s0.nx + 1;
         load_flat<16>(M, F + s0.oL, poff(nz0 - 1, nz0) + nz0 - 1);
     }
     for (int k = 0; k < ((a.skip & 1) || a.trf ? 0 : a.N); k++) {
-        const WideStage s = a.st[k];
+        const WideStage s = st[k];
         const int nux = s.nu + s.nx, nz = nux + 1, nx1 = s.nx1, nu1 = s.nu1;
         const int ns = k == 0 ? nux : s.nu;
         const double* dL = M + poff(nux, nz);
@@ -786,7 +837,7 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
             for (int i = 0; i < nux; i++) xn += W[i + tid * ldW] * v[i];
         }
         bar();
-        const WideStage s1 = a.st[k + 1];
+        const WideStage s1 = st[k + 1];
         const int nux1 = nu1 + nx1, nz1 = nux1 + 1;
         if (tid < nx1) {
             v[nu1 + tid] = xn;
@@ -822,6 +873,7 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
 // ------------------------------------------------------------------------------------------------
 __device__ HK_WIDE_BODY void wide_trs_body(const WideArgs& a, const WideProb& q) {
     extern __shared__ double sm[];
+    const StTab st{reinterpret_cast<const WideStage*>(sm + a.offST)};  // filled by the kernel (wide_stage_table)
     const int tid = threadIdx.x;
     double* M = sm;
     double* W = sm + a.offW;
@@ -842,7 +894,7 @@ __device__ HK_WIDE_BODY void wide_trs_body(const WideArgs& a, const WideProb& q)
         return q.hq ? q.hq[sk.oU + i] : P4(q.RSQ + sk.oR, sk.sdR, sk.nu + sk.nx, i);
     };
     for (int k = a.N; k >= 0; k--) {
-        const WideStage s = a.st[k];
+        const WideStage s = st[k];
         const int nux = s.nu + s.nx, nz = nux + 1, nx1 = s.nx1;
         const int ns = k == 0 ? nux : s.nu;
         load_flat<16>(M, F + s.oL, poff(nux, nz) + nux);
@@ -877,7 +929,7 @@ __device__ HK_WIDE_BODY void wide_trs_body(const WideArgs& a, const WideProb& q)
         }
         for (int i = tid; i < nux; i += WT) ux[s.oU + i] = v[i];
         if (k > 0) {  // w for stage k-1: Pb_{k-1} = Lxx_k (Lxx_k' b_{k-1}), plus v_{k,x}
-            const WideStage sp = a.st[k - 1];
+            const WideStage sp = st[k - 1];
             const int nu = s.nu, nx = s.nx;
             double t = 0.0;
             if (tid < nx) {
@@ -898,14 +950,14 @@ __device__ HK_WIDE_BODY void wide_trs_body(const WideArgs& a, const WideProb& q)
     }
     // forward
     {
-        const WideStage s0 = a.st[0];
+        const WideStage s0 = st[0];
         const int nz0 = s0.nu + s0.nx + 1;
         load_flat<16>(M, F + s0.oL, poff(nz0 - 1, nz0) + nz0 - 1);
         load_flat<4>(v, ux + s0.oU, nz0 - 1);
         bar();
     }
     for (int k = 0; k < a.N; k++) {
-        const WideStage s = a.st[k], s1 = a.st[k + 1];
+        const WideStage s = st[k], s1 = st[k + 1];
         const int nux = s.nu + s.nx, nz = nux + 1, nx1 = s.nx1, nu1 = s.nu1;
         const int ns = k == 0 ? nux : s.nu;
         const double* dL = M + poff(nux, nz);
@@ -954,7 +1006,7 @@ __device__ HK_WIDE_BODY void wide_trs_body(const WideArgs& a, const WideProb& q)
             bar();
         }
     }
-    if (tid < a.st[a.N].nx) ux[a.st[a.N].oU + tid] = v[tid];
+    if (tid < st[a.N].nx) ux[st[a.N].oU + tid] = v[tid];
 }
 
 }  // namespace

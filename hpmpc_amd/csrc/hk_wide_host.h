@@ -38,7 +38,7 @@ struct WLayout {
     int N = 0;
     std::vector<WideStage> st;
     long long nB = 0, nR = 0, nL = 0, nU = 0, nP = 0, nD = 0, nI = 0, nG = 0;
-    int lds = 0, offW = 0, offX = 0, offV = 0, ldW = 0, ldX = 0;
+    int lds = 0, offW = 0, offX = 0, offV = 0, ldW = 0, ldX = 0, offST = 0;
     bool any_ng = false;
     bool fits = true;  // hk_wide_sv limits: nu+nx+1 <= 128 (two rows per lane), nx <= 64 (MFMA tiles per wave)
 };
@@ -90,7 +90,8 @@ WLayout make_layout(int N, const int* nx, const int* nu, const int* nb, const in
     L.offW = Mmax + nzM;  // the forward stages L_k with its 1/diag tail into M
     L.offX = L.offW + L.ldW * nxM;
     L.offV = L.offX + L.ldX * nxM;
-    L.lds = L.offV + nzM;
+    L.offST = rup(L.offV + nzM, 2);  // the stage table (WideStage records) in LDS
+    L.lds = L.offST + (N + 1) * (int)(sizeof(WideStage) / sizeof(double));
     if (L.nD == 0) L.nD = 1;
     if (L.nI == 0) L.nI = 1;
     if (L.nB == 0) L.nB = 1;

@@ -83,6 +83,12 @@ __device__ __forceinline__ IP ip_ptrs(const WideIpmArgs& A, int p) {
     return P;
 }
 
+// the stage table in LDS (wide_stage_table; per-lane reads here: the stage index may differ between lanes)
+__device__ __forceinline__ const WideStage* wst(const WideIpmArgs& A) {
+    extern __shared__ double sm[];
+    return reinterpret_cast<const WideStage*>(sm + A.w.offST);
+}
+
 // workgroup reductions (every thread gets the result); red = 8 doubles of LDS
 __device__ __forceinline__ double wg_sum(double v, double* red) {
     v = hk::wave_sum(v);
@@ -108,7 +114,7 @@ __device__ __forceinline__ void alpha_rule(double& al, double v, double dv) {
 // x at a constraint: the boxed variable, or DCt_k' x_k for a general constraint (dgemv_t_lib)
 __device__ __forceinline__ double cval(const WideIpmArgs& A, const IP& P, const double* x, const WideCSlot& c) {
     if (c.var >= 0) return x[c.var];
-    const WideStage s = A.w.st[-1 - c.var];
+    const WideStage s = wst(A)[-1 - c.var];
     // the slots of one wave may sit on different stages: the problem's (wave-uniform) bases, per-lane offsets
     return bdot(
         s.nu + s.nx, [&](int i, bool ok) { return hk::gld(P.DCt, s.oG + p4i(i, c.g, s.sdG), ok); },
@@ -371,13 +377,13 @@ __device__ __forceinline__ double residuals(const WideIpmArgs& A, const IP& P, b
     // from the problem's (wave-uniform) bases.  Every row sums in the reference's order, as before.
     int k = 0, rbase = 0;
     for (int rr = tid;; rr += WT) {
-        while (k <= N && rr >= rbase + A.w.st[k].nu + A.w.st[k].nx + A.w.st[k].nx1) {
-            rbase += A.w.st[k].nu + A.w.st[k].nx + A.w.st[k].nx1;
+        while (k <= N && rr >= rbase + wst(A)[k].nu + wst(A)[k].nx + wst(A)[k].nx1) {
+            rbase += wst(A)[k].nu + wst(A)[k].nx + wst(A)[k].nx1;
             k++;
         }
         if (k > N) break;
         const int r = rr - rbase;
-        const WideStage s = A.w.st[k];
+        const WideStage s = wst(A)[k];
         const int nux = s.nu + s.nx;
         const double* R = P.RSQ + s.oR;
         const double* B = P.BAbt + s.oB;
@@ -400,7 +406,7 @@ __device__ __forceinline__ double residuals(const WideIpmArgs& A, const IP& P, b
                 double v;
                 if (!plain) {
                     v = q;
-                    if (k > 0 && i >= s.nu) v -= P.pi[A.w.st[k - 1].oP + i - s.nu];
+                    if (k > 0 && i >= s.nu) v -= P.pi[wst(A)[k - 1].oP + i - s.nu];
                     if (lo >= 0) v += -P.lam[lo] + P.lam[lo + pnb];
                     v += sy;
                     if (k < N) v += bp;
@@ -410,7 +416,7 @@ __device__ __forceinline__ double residuals(const WideIpmArgs& A, const IP& P, b
                             [&](int g, bool ok) { return gld(P.lam, olg + png + g, ok) - gld(P.lam, olg + g, ok); });
                 } else {
                     v = -q;
-                    if (k > 0 && i >= s.nu) v = -q + P.pi[A.w.st[k - 1].oP + i - s.nu];
+                    if (k > 0 && i >= s.nu) v = -q + P.pi[wst(A)[k - 1].oP + i - s.nu];
                     if (lo >= 0) v += P.lam[lo] - P.lam[lo + pnb];
                     v -= sy;
                     if (s.ng > 0) {
@@ -427,7 +433,7 @@ __device__ __forceinline__ double residuals(const WideIpmArgs& A, const IP& P, b
                 P.rq[s.oU + i] = v;
             } else {
                 const int j = r - nux;
-                const WideStage s1 = A.w.st[k + 1];
+                const WideStage s1 = wst(A)[k + 1];
                 const double b = P.vb ? P.vb[s.oP + j] : P4(B, s.sdB, nux, j);
                 const double x1 = P.ux[s1.oU + s1.nu + j];
                 const double c = bdot(
@@ -549,6 +555,7 @@ __global__ __launch_bounds__(WT) void hk_wide_ipm(WideIpmArgs A) {
     extern __shared__ double sm[];
     const int p = blockIdx.x + A.w.p0;
     if (p >= A.w.nprob) return;
+    wide_stage_table(A.w);
     const int tid = threadIdx.x;
     double* red = sm + A.offR;
     const IP P = ip_ptrs(A, p);

@@ -118,6 +118,7 @@ extern "C" void hk_wide_sv_entry(int N, int* nx, int* nu, int* nb, int** idxb, i
     a.offW = L.offW;
     a.offX = L.offX;
     a.offV = L.offV;
+    a.offST = L.offST;
     a.ldW = L.ldW;
     a.ldX = L.ldX;
     if (!g_w.up(c.o) || !launch(0, &a, 1, L.lds, g_w.stream, "hk_wide_sv") || !g_w.down(c.o)) return;
@@ -142,6 +143,7 @@ void wide_args(const WLayout& L, WideArgs& a) {
     a.offW = L.offW;
     a.offX = L.offX;
     a.offV = L.offV;
+    a.offST = L.offST;
     a.ldW = L.ldW;
     a.ldX = L.ldX;
 }
@@ -277,6 +279,8 @@ struct PcPlan {
     long long ref_d = 0;    // the reference's memory carve: doubles before the idxb2 ints
     int pc_lds = 0, ldP = 0, ldX = 0, ldW = 0, ldB = 0, offP = 0, offX = 0, offW = 0, offB = 0, offGA = 0, offGB = 0;
     int px_lds = 0, ldT = 0, xoB = 0, xoR = 0, xoV = 0, xoW = 0, xoQ = 0;
+    int pc_gm = 4;  // hk_pcond's gemm tiles per wave (4 or 8)
+    int offST = 0;  // hk_pcond's LDS stage table
 };
 
 void problem_size(int N, const int* nx, const int* nu, const int* nb, const int* const* hidxb, const int* ng, int N2,
@@ -386,17 +390,30 @@ bool pc_plan(PcPlan& P, int N, const int* nx, const int* nu_in, const int* nb, c
     for (int l = 0; l < nb[N]; l++) P.idxb2[P.cond.st[N2].oI + l] = idxb[N][l];
     // Gamma tiles: the largest (rows x nx_{j+1}) of any block, also used as the RSQrq_{s-1} tile
     long long gmax = (long long)nzM * nzM;
+    int tmax = 0;  // output tiles of hk_pcond's largest gemm: Gamma_{j-1} A_j, and W / W W' of d_cond_RSQrq
+    auto tiles = [](int m, int n) { return ((m + 15) / 16) * ((n + 15) / 16); };
     {
         int Nt = 0;
         for (int ii = 0; ii < N2; ii++) {
             int rows = nx[Nt] + 1;
             for (int j = 0; j < P.blk[ii].T; j++) {
-                rows += nu[Nt + j];
-                gmax = std::max(gmax, (long long)rows * nx[Nt + j + 1]);
+                const int s = Nt + j;
+                if (j > 0) tmax = std::max(tmax, tiles(rows, nx[s + 1]));  // rows = rows(j - 1)
+                rows += nu[s];
+                gmax = std::max(gmax, (long long)rows * nx[s + 1]);
+                if (j > 0) {  // d_cond_RSQrq at stage s: W (nz_{s-1} x nx_s), W W' (nz_{s-1} x nux_{s-1})
+                    const int nzp = nu[s - 1] + nx[s - 1] + 1;
+                    tmax = std::max(tmax, std::max(tiles(nzp, nx[s]), tiles(nzp, nzp - 1)));
+                }
             }
             Nt += P.blk[ii].T;
         }
     }
+    if (tmax > 32) {
+        hk_set_error(HPMPC_MI355X_EUNSUPPORTED, "condensing block beyond hk_pcond's gemm tiles (32 16x16 tiles)");
+        return false;
+    }
+    P.pc_gm = tmax <= 16 ? 4 : 8;
     // LDS carve (doubles, every tile 32-byte aligned for the 16-byte LDS DMA): pL as a lib4 RSQrq block
     // (rup(nz, 4) x sdR), Lx dense, the BAbt tile dense (d_cond_BAbt) or as a lib4 block (d_cond_RSQrq), Gamma_{j-1}
     int nuxM = 1;
@@ -409,7 +426,10 @@ bool pc_plan(PcPlan& P, int N, const int* nx, const int* nu_in, const int* nb, c
     P.offW = P.offB;  // W is formed in place in the BAbt tile
     P.offGA = P.offB + rup(std::max(P.ldB * nxM, rup(nzM, BS) * rup(nxM, NCL)), 4);
     P.offGB = 0;
-    P.pc_lds = P.offGA + (int)gmax;
+    int Tmax = 1;
+    for (int ii = 0; ii < N2; ii++) Tmax = std::max(Tmax, P.blk[ii].T);
+    P.offST = P.offGA + rup((int)gmax, 4);
+    P.pc_lds = P.offST + Tmax * (int)(sizeof(WideStage) / sizeof(double));
     if (gmax > 12 * 256 || nxM > 63) {  // hk_pcond: PC_GCH Gamma outputs per lane; the state Cholesky in one wave
         hk_set_error(HPMPC_MI355X_EUNSUPPORTED, "condensing block beyond the kernel's tile limits "
                                                 "(Gamma rows x nx <= 3072, nx <= 63)");
@@ -424,7 +444,7 @@ bool pc_plan(PcPlan& P, int N, const int* nx, const int* nu_in, const int* nb, c
     P.xoQ = P.xoW + nzM;
     P.px_lds = P.xoQ + std::max(nzM, nxM);
     for (int ii = 0; ii < N2; ii++)  // hk_pcond's d_cond_DCtd bookkeeping: 6 ints per stage + 1 per general row
-        if (6 * P.blk[ii].T + P.ng2[ii] > 2 * P.pc_lds) {
+        if (6 * P.blk[ii].T + P.ng2[ii] > 2 * P.offST) {  // below the LDS stage table
             hk_set_error(HPMPC_MI355X_EUNSUPPORTED, "condensing block with more state boxes than the LDS tiles hold");
             return false;
         }
@@ -463,6 +483,8 @@ void fill_pc_args(const PcPlan& P, PcArgs& a) {
     a.offGA = P.offGA;
     a.offGB = P.offGB;
     a.ph = PC_ALL;
+    a.gm = P.pc_gm;
+    a.offST = P.offST;
 }
 
 void fill_px_args(const PcPlan& P, PxArgs& a) {
@@ -1047,6 +1069,7 @@ extern "C" int hpmpc_mi355x_pcond_ric_sv_batch(const hpmpc_mi355x_pcond_plan* q,
     a.offW = C.offW;
     a.offX = C.offX;
     a.offV = C.offV;
+    a.offST = C.offST;
     a.ldW = C.ldW;
     a.ldX = C.ldX;
     if (const char* e = getenv("HK_WIDE_SKIP")) a.skip = atoi(e);  // profiling only

@@ -198,6 +198,7 @@ void fill_args(const WIpm& W, const Stage& S, char* D, int N, WideIpmArgs& a) {
     a.w.offW = L.offW;
     a.w.offX = L.offX;
     a.w.offV = L.offV;
+    a.w.offST = L.offST;
     a.w.ldW = L.ldW;
     a.w.ldX = L.ldX;
     a.mu_scal = W.nbt ? 1.0 / (2.0 * (double)W.nbt) : 0.0;
@@ -509,6 +510,7 @@ extern "C" int hpmpc_mi355x_wide_ipm_batch(const hpmpc_mi355x_wide_plan* q, int 
     a.w.offW = L.offW;
     a.w.offX = L.offX;
     a.w.offV = L.offV;
+    a.w.offST = L.offST;
     a.w.ldW = L.ldW;
     a.w.ldX = L.ldX;
     a.w.sU = L.nU;

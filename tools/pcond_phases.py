@@ -24,10 +24,11 @@ assert L.hpmpc_mi355x_pcond_debug(dbg.data_ptr()) == 0
 s.condense()
 torch.cuda.synchronize()
 t = dbg.cpu().numpy().astype(np.int64)
-names = {1: "BAbt phase: Gamma_0 / loop top", 2: "BAbt_j staging", 3: "Gamma_j gemm + Gamma store", 4: "B2 store, barrier",
+names = {1: "BAbt phase: Gamma_0 / loop top", 2: "BAbt_j staging", 11: "BAbt_{j+1} prefetch issue",
+         12: "Gamma_j gemm + Gamma store", 3: "B rows, barrier", 4: "B2 store, barrier",
          5: "RSQ: D store, Gamma_{s-1} load", 6: "chol_aug (wave 0) | M (waves 1-3)", 7: "wait for M",
-         8: "BAbt / RSQ into LDS", 9: "W and pL gemms", 10: "DCtd, tail"}
-tot = t[1:11].sum()
+         13: "RSQ / Gamma DMA issue", 14: "W gemm", 8: "wait RSQ, barrier", 9: "W and pL gemms", 10: "DCtd, tail"}
+tot = t[1:15].sum()
 print(f"batch {B}: hk_pcond block (0, 0): {tot} cycles")
-for i in range(1, 11):
+for i in (1, 2, 11, 12, 3, 4, 5, 6, 7, 13, 14, 8, 9, 10):
     print(f"  {names[i]:34s} {t[i]:10d}  {100.0 * t[i] / max(tot, 1):5.1f} %")
