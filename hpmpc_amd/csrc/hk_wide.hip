@@ -228,14 +228,19 @@ __global__ __launch_bounds__(WT, GM <= 4 ? 4 : 2) void hk_pcond(PcArgs a) {  // 
         PST(11);
         // rows nuj.. : Gamma_{j-1} A_j (+ b_j on the last row) on MFMA; rows ..nuj: B_j.  The results overwrite
         // GA (leading dimension rp -> rj) after mfma_gemm's barrier, when every operand read is done.
-        mfma_gemm<GM>(
-            rp, nx1, nxj, [&](int i, int l) { return GA[i + l * rp]; },
-            [&](int l, int c) { return Bt[nuj + l + c * ldB]; },
-            [&](int i, int c, double v) {
+        {
+            auto fa = [&](int i, int l) { return GA[i + l * rp]; };
+            auto fb = [&](int l, int c) { return Bt[nuj + l + c * ldB]; };
+            auto fo = [&](int i, int c, double v) {
                 if (i == rp - 1) v += Bt[nuj + nxj + c * ldB];
                 GA[nuj + i + c * rj] = v;
                 if (keep) Gj[nuj + i + c * rj] = v;
-            });
+            };
+            if (nxj <= 32)  // uniform: all K chunks unrolled
+                mfma_gemm<GM, 8>(rp, nx1, nxj, fa, fb, fo);
+            else
+                mfma_gemm<GM, 0>(rp, nx1, nxj, fa, fb, fo);
+        }
         const float rnu = 1.0f / nuj;
         PST(12);
         for (int e = tid; e < nuj * nx1; e += WT) {
@@ -356,28 +361,38 @@ __global__ __launch_bounds__(WT, GM <= 4 ? 4 : 2) void hk_pcond(PcArgs a) {  // 
             const int ngm = sI >= 2 ? dma_copy_any<WT>(GA, G + g2, r2 * sp.nx, tid) : 0;
             const int sdB = sp.sdB, sdQ = sp.sdR;
             PST(13);
-            if (!(a.skip & 16))
-                mfma_gemm<GM>(
-                    nzp, nxs, nxs, [&](int i, int l) { return BT(sdB, i, l); },
-                    [&](int l, int c) {
-                        const double v = X[l + c * ldX];
-                        return l >= c ? v : 0.0;
-                    },
-                    [&](int i, int c, double v) {
-                        if (i == nuxp) v += X[nxs + c * ldX];
-                        BT(sdB, i, c) = v;
-                    });
+            // the stage gemms fit one 16x16 tile per wave and eight K chunks at nz, nx <= 32 (configs[4]: 31 x 24)
+            const bool small = nzp <= 32 && nuxp <= 32 && nxs <= 32;  // uniform
+            auto wa = [&](int i, int l) { return BT(sdB, i, l); };
+            auto wb = [&](int l, int c) {
+                const double v = X[l + c * ldX];
+                return l >= c ? v : 0.0;
+            };
+            auto wo = [&](int i, int c, double v) {
+                if (i == nuxp) v += X[nxs + c * ldX];
+                BT(sdB, i, c) = v;
+            };
+            if (!(a.skip & 16)) {
+                if (small)
+                    mfma_gemm<1, 8>(nzp, nxs, nxs, wa, wb, wo);
+                else
+                    mfma_gemm<GM, 0>(nzp, nxs, nxs, wa, wb, wo);
+            }
             PST(14);
             dma_wait_keep(ngm);  // RSQrq_{s-1} has landed; Gamma_{s-2} may still be in flight
             lds_bar();
             PST(8);
-            if (!(a.skip & 16))
-                mfma_gemm<GM>(
-                    nzp, nuxp, nxs, [&](int i, int l) { return BT(sdB, i, l); },
-                    [&](int l, int j) { return BT(sdB, j, l); },
-                    [&](int i, int j, double v) {
-                        if (i >= j) PL(sdQ, i, j) += v;
-                    });
+            auto pa = [&](int i, int l) { return BT(sdB, i, l); };
+            auto pb = [&](int l, int j) { return BT(sdB, j, l); };
+            auto po = [&](int i, int j, double v) {
+                if (i >= j) PL(sdQ, i, j) += v;
+            };
+            if (!(a.skip & 16)) {
+                if (small)
+                    mfma_gemm<1, 8>(nzp, nuxp, nxs, pa, pb, po);
+                else
+                    mfma_gemm<GM, 0>(nzp, nuxp, nxs, pa, pb, po);
+            }
             lds_bar();  // W is read
             nbk = 0;
             if (sI >= 2) {

@@ -360,7 +360,7 @@ __device__ __forceinline__ void tile_chol_block(hk::d4& D, hk::d4* U, int nU, hk
 // outer loop and the wave's tiles the inner one, so each chunk issues every tile's operand loads before their MFMAs:
 // one LDS round trip per chunk for all tiles, and independent MFMAs back to back instead of one dependent chain per
 // tile after another.
-template <int GM, class FA, class FB, class FO>
+template <int GM, int KM, class FA, class FB, class FO>
 __device__ __forceinline__ void mfma_gemm(int m, int n, int K, FA a, FB b, FO out) {
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), c16 = lane & 15,
               g4 = lane >> 4;
@@ -374,23 +374,30 @@ __device__ __forceinline__ void mfma_gemm(int m, int n, int K, FA a, FB b, FO ou
         cb[u] = 16 * ti + c16;
         acc[u] = hk::d4{0.0, 0.0, 0.0, 0.0};
     }
-    for (int kc = 0; kc < nK; kc++) {
-        const int kk = 4 * kc + g4;
-        double av[GM], bv[GM];
-        const int kq = kk < K ? kk : K - 1;
+    // K chunks in groups of KG: every load of a group is issued before its MFMAs.  Loads are unconditional, at
+    // clamped (valid) indices, followed by a select -- a conditional load is compiled to an exec-masked branch with
+    // its own lgkmcnt wait per operand.  KM (the caller's bound on the chunk count, or 0) only sets the group size.
+    constexpr int KG = KM == 0 ? 1 : (GM >= 8 ? 1 : (8 / GM < KM ? 8 / GM : KM));
+    for (int kc0 = 0; kc0 < nK; kc0 += KG) {
+        double av[KG][GM], bv[KG][GM];
 #pragma unroll
-        for (int u = 0; u < GM; u++) {
-            if (wv + 4 * u < nT) {  // uniform
-                // unconditional loads at clamped (valid) indices, then a select: a conditional load is compiled to
-                // an exec-masked branch with its own lgkmcnt wait per operand
-                const double x = a(ra[u] < m ? ra[u] : m - 1, kq), y = b(kq, cb[u] < n ? cb[u] : n - 1);
-                av[u] = (ra[u] < m && kk < K) ? x : 0.0;
-                bv[u] = (cb[u] < n && kk < K) ? y : 0.0;
+        for (int j = 0; j < KG; j++) {
+            const int kk = 4 * (kc0 + j) + g4, kq = kk < K ? kk : K - 1;
+#pragma unroll
+            for (int u = 0; u < GM; u++) {
+                if (wv + 4 * u < nT) {  // uniform
+                    const double x = a(ra[u] < m ? ra[u] : m - 1, kq), y = b(kq, cb[u] < n ? cb[u] : n - 1);
+                    av[j][u] = (ra[u] < m && kk < K) ? x : 0.0;
+                    bv[j][u] = (cb[u] < n && kk < K) ? y : 0.0;
+                }
             }
         }
 #pragma unroll
-        for (int u = 0; u < GM; u++)
-            if (wv + 4 * u < nT) acc[u] = hk::mfma(av[u], bv[u], acc[u]);
+        for (int j = 0; j < KG; j++)
+            if (kc0 + j < nK)  // uniform
+#pragma unroll
+                for (int u = 0; u < GM; u++)
+                    if (wv + 4 * u < nT) acc[u] = hk::mfma(av[j][u], bv[j][u], acc[u]);
     }
     lds_bar();  // every operand read is done (the operands live in LDS)
 #pragma unroll
