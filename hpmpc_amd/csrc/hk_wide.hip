@@ -98,7 +98,7 @@ __device__ __attribute__((noinline)) void xchol_rows(double* X, int ldX, int nxs
 // The block is read through S(i, j) (i >= j: row i, column j; row nx = the gradient row) and the factor written to X
 // ((nx+1) x nx lower, dense, ld ldX).  Wave-level (one wave calls it).
 template <class FS>
-__device__ __forceinline__ void xchol_tiles(FS S, double* X, int ldX, int nx) {
+__device__ __forceinline__ void xchol_tiles(FS S, double* X, int ldX, int nx) {  // the P form's fallback
     const int l = threadIdx.x & 63, g = l >> 4, c = l & 15;
     auto src = [&](int t) { return t < nx ? t : (t == 31 ? nx : -1); };
     auto at = [&](int t1, int t2) -> double {  // A[t1][t2] of the padded symmetric block
@@ -165,6 +165,8 @@ __global__ __launch_bounds__(WT, GM <= 4 ? 4 : 2) void hk_pcond(PcArgs a) {  // 
     double* Pl = sm + a.offP;  // pL (RSQrq_s + W W', a lib4 block in the layout of its stage)
     double* X = sm + a.offX;   // Lx / chol scratch (ld ldX)
     double* Bt = sm + a.offB;  // stage BAbt tile, then W in place (ld ldB)
+    double* Ucol = sm + a.offU;  // P form: the u columns of pL_s (x rows and gradient row), ld ldU
+    const int ldU = a.ldX;
     const int ldX = a.ldX, ldB = a.ldB;
 
     // Gamma row counts / offsets (rows r_j = sum_{i<=j} nu_i + nx0 + 1)
@@ -294,10 +296,49 @@ __global__ __launch_bounds__(WT, GM <= 4 ? 4 : 2) void hk_pcond(PcArgs a) {  // 
         auto PL = [&](int sd, int i, int j) -> double& { return Pl[p4i(i, j, sd)]; };
         auto BT = [&](int sd, int i, int j) -> double& { return Bt[p4i(i, j, sd)]; };
         auto lib4n = [&](const WideStage& q, int sd) { return (q.nu + q.nx + 1 + 3) / 4 * 4 * sd; };
+        // The clamp certificate of the state-block Cholesky (the reference clamps a pivot
+        // d <= 1e-15 to 0, kernel_dpotrf_c99_lib4.c:555-640): X = pL_s[x,x] = RSQrq_s[x,x] + (W W')[x,x] >= RSQrq_s[x,x],
+        // so every exact pivot of X is at least g_s = the Gershgorin bound of RSQrq_s[x,x] (from the data), and the
+        // reference's computed pivots (exact pivots of X + dX, |dX_ij| <= c n eps max_i X_ii) stay above the clamp when
+        // g_s - 1e-11 max_i X_ii > 1e-15.  Then L L' = X (to rounding) and d_cond_RSQrq's W W' = [BAbt | e] X^ [BAbt | e]'
+        // with X^ the state block and its gradient row (P form): no Cholesky on the stage chain.  Otherwise the stage
+        // takes the reference's route (Cholesky, W = BAbt L + l, W W').
+        // g_s for every stage of the block, before the loop: one thread per (stage, row) forms the row's Gershgorin
+        // value of RSQrq_s[x,x] from memory (eight loads in flight), GA holds them until the per-stage minimum
+        // (GA is free between the d_cond_BAbt phase and the first Gamma copy below).
+        double* gtab = sm + a.offGT;  // g_1 .. g_{T-1}
+        const int nxw = a.ldX - 1;    // rows per stage in the scratch (the largest nx)
+        if (a.pform) {
+            for (int e = tid; e < (T - 1) * nxw; e += WT) {
+                const int sg = 1 + e / nxw, i = e - (sg - 1) * nxw;
+                const WideStage q = st[sg];
+                double r = 1e300;
+                if (i < q.nx) {
+                    const double* R = RSQ + q.oR;
+                    const double off = bdot(
+                        q.nx,
+                        [&](int j, bool ok) {
+                            const int a1 = i > j ? i : j, a2 = i > j ? j : i;
+                            return j == i ? 0.0 : fabs(gld(R, p4i(q.nu + a1, q.nu + a2, q.sdR), ok));
+                        },
+                        [&](int, bool) { return 1.0; });
+                    r = gld(R, p4i(q.nu + i, q.nu + i, q.sdR)) - off;
+                }
+                GA[e] = r;
+            }
+            bar();
+            for (int sg = 1 + tid; sg < T; sg += WT) {
+                double g = 1e300;
+                for (int i = 0; i < nxw; i++) g = fmin(g, GA[(sg - 1) * nxw + i]);
+                gtab[sg] = g;
+            }
+            bar();
+        }
         // Outstanding DMA at the top of step s: RSQrq_s -> pL and Gamma_{s-1} -> GA (issued after step s+1's Cholesky,
         // needed now), then BAbt_{s-1} -> Bt (issued at the end of step s+1, needed only after this step's Cholesky):
         // the top waits for all but the BAbt copy (nbk = its instruction count in this wave).
-        int nbk;
+        int nbk;            // this wave's DMA instructions of the BAbt copy the next top may leave in flight
+        bool bpend = true;  // workgroup-uniform: that copy may be in flight at the next top
         // carried along the loop: os = sum_{r > sI} nu_r (the offset of u_sI in the condensed variables),
         // r1 = rows(sI - 1), g1 = goff(sI - 1)
         int os = 0, r1 = rows(T - 2), g1 = goff(T - 2);
@@ -323,13 +364,83 @@ __global__ __launch_bounds__(WT, GM <= 4 ? 4 : 2) void hk_pcond(PcArgs a) {  // 
             const WideStage sp = st[sI - 1];
             const int nuxp = sp.nu + sp.nx, nzp = nuxp + 1;
             const int r0 = r1;
+            const int r2 = r1 - sp.nu, g2 = sI >= 2 ? g1 - r2 * st[sI - 2].nx1 : 0;  // rows / goff(sI - 2)
+            const int sdB = sp.sdB, sdQ = sp.sdR;
+            // the stage gemms fit one 16x16 tile per wave and eight K chunks at nz, nx <= 32 (configs[4]: 31 x 24)
+            const bool small = nzp <= 32 && nuxp <= 32 && nxs <= 32;  // uniform
+            double emax = 0.0;  // max_i X_ii
+            {
+                const int i = tid & 63;
+                emax = -hk::wave_min(i < nxs ? -PL(sdP, nus + i, nus + i) : 0.0);
+            }
+            const bool pf = a.pform && small && gtab[sI] - 1e-11 * emax > 1e-15;  // uniform
+            auto M_product = [&](auto&& pxu, int t0, int nt) {  // M = Gamma_{s-1} pL_s[x,u] (+ the r row)
+                const float rr0 = 1.0f / r0;
+                for (int e = tid - t0; e < ((a.skip & 8) ? 0 : r0 * nus); e += nt) {
+                    const int c = fdiv(e, rr0), i = e - c * r0;
+                    double acc = 0.0;
+                    for (int l = 0; l < nxs; l++) acc += GA[i + l * r0] * pxu(l, c);
+                    if (i == r0 - 1) acc += pxu(nxs, c);
+                    *P4w(R2, cnux2, os + nus + i, os + c) = acc;
+                }
+            };
+            PST(5);
+            int ngm = 0;
+            if (pf) {
+                // ---- P form: T = X^ [BAbt | e]' ((nx+1) x nz_{s-1}, in the X tile, ld ldX), pL_{s-1} = RSQrq_{s-1} +
+                // [BAbt | e] T (lower).  RSQrq_{s-1} arrives by LDS DMA while M is formed.
+                if (bpend) {  // BAbt_{s-1} may still be in flight (the top left it): T needs it now
+                    dma_wait();
+                    lds_bar();
+                }
+                // the u columns of pL_s (x rows and the gradient row) for M, so pL's buffer is free after T
+                for (int e = tid; e < (nxs + 1) * nus; e += WT) {
+                    const int c = e / (nxs + 1), i = e - c * (nxs + 1);
+                    Ucol[i + c * ldU] = PL(sdP, nus + i, c);
+                }
+                auto xh = [&](int i, int l) {  // X^[i][l], symmetric; the corner X^[nx][nx] is never used
+                    const int a1 = i > l ? i : l, a2 = i > l ? l : i;
+                    return PL(sdP, nus + a1, nus + a2);
+                };
+                mfma_gemm<1, 8>(
+                    nxs + 1, nzp, nxs, xh, [&](int l, int c) { return BT(sdB, c, l); },
+                    [&](int i, int c, double v) {
+                        if (c == nuxp && i < nxs) v += xh(nxs, i);  // the e column: X^[i][nx]
+                        X[i + c * ldX] = v;
+                    });
+                lds_bar();  // T's epilogue read pL_s too (the gradient row)
+                PST(6);
+                // every read of pL_s is done: RSQrq_{s-1} into its buffer
+                dma_copy<WT, 16>(Pl, RSQ + sp.oR, lib4n(sp, sdQ), tid);
+                M_product([&](int l, int c) { return Ucol[l + c * ldU]; }, 0, WT);
+                dma_wait();
+                lds_bar();  // M is done (GA free), RSQrq_{s-1} and T are in LDS
+                PST(7);
+                ngm = sI >= 2 ? dma_copy_any<WT>(GA, G + g2, r2 * sp.nx, tid) : 0;
+                PST(13);
+                mfma_gemm<1, 8>(
+                    nzp, nuxp, nxs, [&](int i, int l) { return BT(sdB, i, l); },
+                    [&](int l, int j) { return X[l + j * ldX]; },
+                    [&](int i, int j, double v) {
+                        if (i == nuxp) v += X[nxs + j * ldX];  // the e row of [BAbt | e]
+                        if (i >= j) PL(sdQ, i, j) += v;
+                    });
+                lds_bar();  // BAbt_{s-1} and T are read
+                PST(14);
+                if (sI >= 2) {
+                    const WideStage sq = st[sI - 2];
+                    dma_copy<WT, 16>(Bt, BAbt + sq.oB, lib4n(sq, sq.sdB), tid);
+                }
+                nbk = 0;  // the next step's top waits for BAbt_{s-2} too (a P-form step needs it at once)
+                bpend = false;
+                PST(8);
+            } else {
             const bool xt = nxs <= 28;  // uniform: the tile Cholesky reads pL directly
             if (!xt) {
                 for (int j = tid >> 6; j < nxs; j += WT / 64)
                     for (int i = j + (tid & 63); i <= nxs; i += 64) X[i + j * ldX] = PL(sdP, nus + i, nus + j);
                 lds_bar();
             }
-            PST(5);
             if (__builtin_amdgcn_readfirstlane(tid) < 64) {  // wave-uniform branch
                 // Lx = chol_aug(pL_xx; pL_r) on wave 0 while the other three form M
                 if (!(a.skip & 4)) {
@@ -338,31 +449,15 @@ __global__ __launch_bounds__(WT, GM <= 4 ? 4 : 2) void hk_pcond(PcArgs a) {  // 
                     else
                         xchol_rows(X, ldX, nxs);
                 }
-                PST(6);
             } else {
-                // M: Gamma_{s-1} times the x_s x u_s block of pL; m: + the r row on the gradient row (measured
-                // against 16-row MFMA tiles: the same time, since it runs beside wave 0's Cholesky, and fewer registers)
-                const float rr0 = 1.0f / r0;
-                for (int e = tid - 64; e < ((a.skip & 8) ? 0 : r0 * nus); e += WT - 64) {
-                    const int c = fdiv(e, rr0), i = e - c * r0;
-                    double acc = 0.0;
-                    for (int l = 0; l < nxs; l++) acc += GA[i + l * r0] * PL(sdP, nus + l, c);
-                    if (i == r0 - 1) acc += PL(sdP, nux, c);
-                    *P4w(R2, cnux2, os + nus + i, os + c) = acc;
-                }
+                M_product([&](int l, int c) { return PL(sdP, nus + l, c); }, 64, WT - 64);
             }
             dma_wait();  // BAbt_{s-1} has landed
             lds_bar();       // pL and GA are read until here
-            PST(7);
             // RSQrq_{s-1} into pL and Gamma_{s-2} into GA while W = BAbt_{s-1} Lx (+ l on the last row) forms in place
             // over BAbt_{s-1}; then pL += W W' (lower); both products on MFMA
             dma_copy<WT, 16>(Pl, RSQ + sp.oR, lib4n(sp, sp.sdR), tid);
-            const int r2 = r1 - sp.nu, g2 = sI >= 2 ? g1 - r2 * st[sI - 2].nx1 : 0;  // rows / goff(sI - 2)
-            const int ngm = sI >= 2 ? dma_copy_any<WT>(GA, G + g2, r2 * sp.nx, tid) : 0;
-            const int sdB = sp.sdB, sdQ = sp.sdR;
-            PST(13);
-            // the stage gemms fit one 16x16 tile per wave and eight K chunks at nz, nx <= 32 (configs[4]: 31 x 24)
-            const bool small = nzp <= 32 && nuxp <= 32 && nxs <= 32;  // uniform
+            ngm = sI >= 2 ? dma_copy_any<WT>(GA, G + g2, r2 * sp.nx, tid) : 0;
             auto wa = [&](int i, int l) { return BT(sdB, i, l); };
             auto wb = [&](int l, int c) {
                 const double v = X[l + c * ldX];
@@ -378,10 +473,8 @@ __global__ __launch_bounds__(WT, GM <= 4 ? 4 : 2) void hk_pcond(PcArgs a) {  // 
                 else
                     mfma_gemm<GM, 0>(nzp, nxs, nxs, wa, wb, wo);
             }
-            PST(14);
             dma_wait_keep(ngm);  // RSQrq_{s-1} has landed; Gamma_{s-2} may still be in flight
             lds_bar();
-            PST(8);
             auto pa = [&](int i, int l) { return BT(sdB, i, l); };
             auto pb = [&](int l, int j) { return BT(sdB, j, l); };
             auto po = [&](int i, int j, double v) {
@@ -399,6 +492,9 @@ __global__ __launch_bounds__(WT, GM <= 4 ? 4 : 2) void hk_pcond(PcArgs a) {  // 
                 const WideStage sq = st[sI - 2];
                 nbk = dma_copy<WT, 16>(Bt, BAbt + sq.oB, lib4n(sq, sq.sdB), tid);
             }
+            bpend = true;
+            }
+            (void)ngm;
             os += nus;
             r1 = r2;
             g1 = g2;

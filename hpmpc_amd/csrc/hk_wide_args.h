@@ -80,6 +80,9 @@ struct PcArgs {
     int offP, offX, offW, offB, ldP, ldX, ldW, ldB;  // dynamic LDS carve
     int offGA, offGB;                                // Gamma_{j-1} / Gamma_j tiles (and stage scratch)
     int offST;                                       // the block's stage records (WideStage, T of them)
+    int offU;                                        // P form: the u columns of pL_s ((nx+1) x nu, ld ldX)
+    int pform;                                       // 0: every stage takes the Cholesky route (A/B, tests)
+    int offGT;                                       // P form: the certificate bounds g_s of the block's stages
     int skip;  // profiling only (HK_PCOND_SKIP): bit 0 Gamma, 1 RSQ phase, 2 its Cholesky, 3 M product, 4 W/syrk
     int oD2N, nDN;  // terminal stage: its bounds d_N (original offset st[N].oD, nDN doubles) -> d2 at oD2N
     // phases (d_part_cond: PC_ALL).  Without PC_BABT the Gammas are inputs, already in the scratch G; PC_PART runs

@@ -538,19 +538,28 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
             // W = BAbt_k Lxx_{k+1} (dtrmm_nt_u) on MFMA: 16x16 output tiles, K over the nx1 columns of BAbt; the
             // tiles are kept in registers and written back over BAbt after a barrier
             {
-                const int nI = (nz + 15) >> 4, nJ = (nx1 + 15) >> 4, nK = (nx1 + 3) >> 2;
+                const int nI = (nz + 15) >> 4, nJ = (nx1 + 15) >> 4, nK = (nx1 + 3) >> 2, nT = nI * nJ;
+                const int w = __builtin_amdgcn_readfirstlane(wv);
                 hk::d4 acc[WS_TILES];
+                int ra[WS_TILES], cb[WS_TILES];
 #pragma unroll
                 for (int u = 0; u < WS_TILES; u++) {
                     acc[u] = hk::d4{0.0, 0.0, 0.0, 0.0};
-                    const int t = wv + 4 * u;
-                    if (t < nI * nJ) {
-                        const int I = t % nI, J = t / nI, ra = 16 * I + c16, cb = 16 * J + c16;
-                        for (int kc = 0; kc < nK; kc++) {
-                            const int kk = 4 * kc + g4;
-                            const double av = (ra < nz && kk < nx1) ? W[ra + kk * ldW] : 0.0;
-                            const double bv = (cb < nx1 && kk < nx1) ? X[kk + cb * ldX] : 0.0;
-                            acc[u] = hk::mfma(av, bv, acc[u]);
+                    const int t = w + 4 * u, J = t / nI;
+                    ra[u] = 16 * (t - J * nI) + c16;
+                    cb[u] = 16 * J + c16;
+                }
+                // K chunks outer, the wave's tiles inner (independent MFMAs back to back); operand loads at clamped
+                // indices and a select (a conditional LDS load becomes an exec-masked branch with its own wait)
+                for (int kc = 0; kc < nK; kc++) {
+                    const int kk = 4 * kc + g4, kq = kk < nx1 ? kk : nx1 - 1;
+#pragma unroll
+                    for (int u = 0; u < WS_TILES; u++) {
+                        if (w + 4 * u < nT) {  // uniform
+                            const double x = W[(ra[u] < nz ? ra[u] : nz - 1) + kq * ldW];
+                            const double y = X[kq + (cb[u] < nx1 ? cb[u] : nx1 - 1) * ldX];
+                            acc[u] = hk::mfma((ra[u] < nz && kk < nx1) ? x : 0.0, (cb[u] < nx1 && kk < nx1) ? y : 0.0,
+                                              acc[u]);
                         }
                     }
                 }
@@ -587,11 +596,13 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
                     while ((I + 1) * (I + 2) / 2 <= t) I++;
                     const int J = t - I * (I + 1) / 2;
                     const int ra = 16 * I + c16, rb = 16 * J + c16;
+                    const int rac = ra < nz ? ra : nz - 1, rbc = rb < nux ? rb : nux - 1;
                     hk::d4 acc = {0.0, 0.0, 0.0, 0.0};
                     for (int kc = 0; kc < nK; kc++) {
-                        const int kk = 4 * kc + g4;
-                        const double av = (ra < nz && kk < nx1) ? W[ra + kk * ldW] : 0.0;
-                        const double bv = (rb < nux && kk < nx1) ? W[rb + kk * ldW] : 0.0;
+                        const int kk = 4 * kc + g4, kq = kk < nx1 ? kk : nx1 - 1;
+                        const double x = W[rac + kq * ldW], y = W[rbc + kq * ldW];  // unconditional, then a select
+                        const double av = (ra < nz && kk < nx1) ? x : 0.0;
+                        const double bv = (rb < nux && kk < nx1) ? y : 0.0;
                         acc = hk::mfma(av, bv, acc);
                     }
                     const int col = 16 * J + c16;
@@ -780,11 +791,14 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
                     const int J = t - I * (I + 1) / 2;
                     const int ra = 16 * (T0 + I) + c16, rb = 16 * (T0 + J) + c16;
                     hk::d4 acc = {0.0, 0.0, 0.0, 0.0};
+                    const int rac = ra < nz ? ra : nz - 1, rbc = rb < nux ? rb : nux - 1;
                     for (int kc = 0; kc < nK; kc++) {
                         const int kk = p0 + 4 * kc + g4;
                         const bool kok = kk < pe;
-                        const double av = (ra < nz && kok) ? M[poff(kk, nz) + ra - kk] : 0.0;
-                        const double bv = (rb < nux && kok) ? M[poff(kk, nz) + rb - kk] : 0.0;
+                        const int kq = kok ? kk : pe - 1, ck = poff(kq, nz) - kq;
+                        const double x = M[ck + rac], y = M[ck + rbc];  // unconditional (rows >= pe > kq), then a select
+                        const double av = (ra < nz && kok) ? x : 0.0;
+                        const double bv = (rb < nux && kok) ? y : 0.0;
                         acc = hk::mfma(av, bv, acc);
                     }
                     const int col = 16 * (T0 + J) + c16;

@@ -281,6 +281,9 @@ struct PcPlan {
     int px_lds = 0, ldT = 0, xoB = 0, xoR = 0, xoV = 0, xoW = 0, xoQ = 0;
     int pc_gm = 4;  // hk_pcond's gemm tiles per wave (4 or 8)
     int offST = 0;  // hk_pcond's LDS stage table
+    int offU = 0;   // hk_pcond's P-form u columns
+    int offGT = 0;  // hk_pcond's P-form certificate bounds
+    bool pform_ok = true;
 };
 
 void problem_size(int N, const int* nx, const int* nu, const int* nb, const int* const* hidxb, const int* ng, int N2,
@@ -422,14 +425,20 @@ bool pc_plan(PcPlan& P, int N, const int* nx, const int* nu_in, const int* nb, c
     P.ldX = nxM + 1;
     P.offP = 0;
     P.offX = rup(std::max(P.ldP * nzM, rup(nzM, BS) * rup(nuxM, NCL)), 4);
-    P.offB = P.offX + rup(P.ldX * nxM, 4);
+    P.offB = P.offX + rup(P.ldX * nzM, 4);  // Lx, or the P form's T = X^ [BAbt | e]' ((nx+1) x nz)
     P.offW = P.offB;  // W is formed in place in the BAbt tile
     P.offGA = P.offB + rup(std::max(P.ldB * nxM, rup(nzM, BS) * rup(nxM, NCL)), 4);
     P.offGB = 0;
     int Tmax = 1;
     for (int ii = 0; ii < N2; ii++) Tmax = std::max(Tmax, P.blk[ii].T);
     P.offST = P.offGA + rup((int)gmax, 4);
-    P.pc_lds = P.offST + Tmax * (int)(sizeof(WideStage) / sizeof(double));
+    int nuM = 1;
+    for (int k = 0; k < N; k++) nuM = std::max(nuM, nu[k]);
+    P.offU = P.offST + rup(Tmax * (int)(sizeof(WideStage) / sizeof(double)), 2);
+    P.offGT = P.offU + P.ldX * nuM;
+    P.pc_lds = P.offGT + Tmax;
+    // the P form's per-row scratch (one row value per stage and state) lives in the Gamma tile before d_cond_RSQrq
+    P.pform_ok = (long long)(Tmax - 1) * nxM <= gmax;
     if (gmax > 12 * 256 || nxM > 63) {  // hk_pcond: PC_GCH Gamma outputs per lane; the state Cholesky in one wave
         hk_set_error(HPMPC_MI355X_EUNSUPPORTED, "condensing block beyond the kernel's tile limits "
                                                 "(Gamma rows x nx <= 3072, nx <= 63)");
@@ -485,6 +494,11 @@ void fill_pc_args(const PcPlan& P, PcArgs& a) {
     a.ph = PC_ALL;
     a.gm = P.pc_gm;
     a.offST = P.offST;
+    a.offU = P.offU;
+    // HPMPC_MI355X_PCOND_PFORM=0: every stage takes the Cholesky route (read per call: tests compare the two routes)
+    const char* pf = getenv("HPMPC_MI355X_PCOND_PFORM");
+    a.pform = P.pform_ok && (pf ? atoi(pf) : 1);
+    a.offGT = P.offGT;
 }
 
 void fill_px_args(const PcPlan& P, PxArgs& a) {

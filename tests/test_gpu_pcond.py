@@ -304,3 +304,36 @@ def _pcond_ipm_vs_oracle(oracle, bq, N2, problems, solver=None):
             ref = max(float(np.max(np.abs(x), initial=0)) for x in ro[key])
             assert got <= max(10 * ref, 1e-9), (p, key, got, ref)
     return s
+
+
+@pytest.mark.parametrize("coupled", [False, True], ids=["mass_spring", "coupled"])
+def test_pcond_pform_matches_cholesky_route(coupled):
+    """hk_pcond's P form (W W' = [BAbt | e] X^ [BAbt | e]' on stages whose clamp certificate holds) against the
+    reference's route on every stage (HPMPC_MI355X_PCOND_PFORM=0: state-block Cholesky, W = BAbt L + l, W W'):
+    the condensed data agree to rounding (1e-12 relative), on the benchmark's data (every certificate holds) and on
+    coupled, non-diagonally-dominant stage Hessians (the Gershgorin certificate fails and the stages fall back)."""
+    import os
+
+    import torch
+
+    from hpmpc_amd.pcond import PcondSolver
+    from hpmpc_amd.shard import coupled_shard, make_shard
+
+    gen = coupled_shard if coupled else make_shard
+    qp = gen(60, 24, 6, 0, 1, 16, boxes=True)
+    out = []
+    for pf in (None, "0"):
+        if pf is None:
+            os.environ.pop("HPMPC_MI355X_PCOND_PFORM", None)
+        else:
+            os.environ["HPMPC_MI355X_PCOND_PFORM"] = pf
+        try:
+            s = PcondSolver(qp, 6)
+            s.condense()
+            torch.cuda.synchronize()
+            out.append([t.clone() for t in (s.BAbt2, s.RSQrq2, s.DCt2, s.d2)])
+        finally:
+            os.environ.pop("HPMPC_MI355X_PCOND_PFORM", None)
+    for a, b in zip(*out):
+        scale = float(b.abs().max()) or 1.0
+        assert float((a - b).abs().max()) <= 1e-12 * scale
