@@ -402,13 +402,22 @@ __global__ __launch_bounds__(WT, GM <= 4 ? 4 : 2) void hk_pcond(PcArgs a) {  // 
                     const int a1 = i > l ? i : l, a2 = i > l ? l : i;
                     return PL(sdP, nus + a1, nus + a2);
                 };
+                // the e column's term X^[i][nx] of this wave's output tile (one tile per wave), read before the gemm's
+                // barrier so that pL's buffer is free when the gemm returns
+                double xr[4];
+                {
+                    const int nI2 = (nxs + 1 + 15) >> 4, t = __builtin_amdgcn_readfirstlane(tid >> 6), ti = t / nI2;
+                    const int col = 16 * ti + (tid & 15), rb = 16 * (t - ti * nI2) + ((tid & 63) >> 4);
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const int i = rb + 4 * r;
+                        const double v = xh(nxs, i < nxs ? i : nxs - 1);
+                        xr[r] = (col == nuxp && i < nxs) ? v : 0.0;
+                    }
+                }
                 mfma_gemm<1, 8>(
                     nxs + 1, nzp, nxs, xh, [&](int l, int c) { return BT(sdB, c, l); },
-                    [&](int i, int c, double v) {
-                        if (c == nuxp && i < nxs) v += xh(nxs, i);  // the e column: X^[i][nx]
-                        X[i + c * ldX] = v;
-                    });
-                lds_bar();  // T's epilogue read pL_s too (the gradient row)
+                    [&](int i, int c, double v) { X[i + c * ldX] = v + xr[(i & 15) >> 2]; });
                 PST(6);
                 // every read of pL_s is done: RSQrq_{s-1} into its buffer
                 dma_copy<WT, 16>(Pl, RSQ + sp.oR, lib4n(sp, sdQ), tid);
@@ -427,11 +436,11 @@ __global__ __launch_bounds__(WT, GM <= 4 ? 4 : 2) void hk_pcond(PcArgs a) {  // 
                     });
                 lds_bar();  // BAbt_{s-1} and T are read
                 PST(14);
-                if (sI >= 2) {
+                if (sI >= 2) {  // (register staging of this copy across the step measured the same: 1.567 ms)
                     const WideStage sq = st[sI - 2];
                     dma_copy<WT, 16>(Bt, BAbt + sq.oB, lib4n(sq, sq.sdB), tid);
                 }
-                nbk = 0;  // the next step's top waits for BAbt_{s-2} too (a P-form step needs it at once)
+                nbk = 0;  // the next step's top waits for anything still in flight (a P-form step needs BAbt at once)
                 bpend = false;
                 PST(8);
             } else {
