@@ -154,4 +154,5 @@ struct WideIpmArgs {
     int* ret;
     double* mu;    // per problem: final mu (residual routines: in / out)
     int offR;      // LDS reduction scratch (8 doubles) after the Riccati carve
+    int offKC;     // LDS: the general-constraint chunk limits ((N+1) x 8 ints) and their valid flag
 };

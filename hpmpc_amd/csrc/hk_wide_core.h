@@ -17,6 +17,8 @@ using hk::gld;
 constexpr int WT = 256;  // threads per workgroup
 constexpr int WS_TILES = 8;  // W = BAbt Lxx output tiles per wave (nz <= 128, nx <= 64: <= 32 tiles, host-checked)
 constexpr int DT_TILES = 6;  // DCt diag DCt' lower tiles per wave on the LDS-staged path (nz <= 96; larger stages read HBM directly)
+constexpr int DS_LD = 17;   // row stride (doubles) of the staged DCt block: 16 columns + 1 pad against LDS bank conflicts
+
 constexpr int BS = 4;
 
 // lib4 index of (i, j), i >= 0 (shifts: the signed / and % by 4 cost a sign fix-up each)
@@ -440,6 +442,9 @@ struct WideProb {
     const double *hb, *hq;                  // trs: b / q vectors (null: the augmented rows)
     int compute_pi, compute_Pb;
     bool dev_box;                           // sv: apply the box terms Qx / qx at idxb on the device
+    int* kct;                               // LDS (nullable): per stage and 16-row tile of M, 1 + the last DCt column
+                                            // with a nonzero entry in the tile's rows
+    bool kc_use;                            // kct is complete (a factorisation has scanned every chunk): use it
 };
 
 __device__ __forceinline__ WideProb wide_prob(const WideArgs& a, int p) {
@@ -460,6 +465,8 @@ __device__ __forceinline__ WideProb wide_prob(const WideArgs& a, int p) {
     q.compute_pi = a.compute_pi;
     q.compute_Pb = a.compute_Pb;
     q.dev_box = a.dev_box != 0;
+    q.kct = nullptr;
+    q.kc_use = false;
     return q;
 }
 
@@ -629,69 +636,90 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
             const int ng = s.ng, sdG = s.sdG, nI = (nz + 15) >> 4, nK = (ng + 3) >> 2, nT = nI * (nI + 1) / 2;
             const int ldS = 16 * nI;
             const float rS = 1.0f / ldS;
-            if (nT <= 4 * DT_TILES && 16 * ldS + 32 <= a.offV - a.offW) {  // uniform
+            if (nT <= 4 * DT_TILES && DS_LD * ldS + 32 <= a.offV - a.offW) {  // uniform
                 // K blocks of 16 constraints staged in LDS (W and X are free between the syrk and the Cholesky):
                 // the block's DCt columns (zero beyond nux / ng), diag(Qx_g) and the qx_g entries, one memory round
                 // trip per block for the whole workgroup.  Each wave keeps its output tiles in registers across
                 // the blocks; the MFMA chain of a tile runs over the same K chunks in the same order as the direct
                 // loop below, so M gets the same sums.
-                double* Ds = W;
-                double* dqs = W + 16 * ldS;
+                double* Ds = W;  // Ds[kk + DS_LD i]: a chunk's four columns are compile-time offsets from a row
+                double* dqs = W + DS_LD * ldS;
                 double* qrs = dqs + 16;
+                // In an IPM the DCt blocks are the same in every factorisation and often block-staircase (the
+                // condensed problem's state boxes of inner stage s have no entries above its nu_tmp): the first
+                // factorisation records per 16-row tile of M the last column with a nonzero entry in the tile's rows
+                // (kct), the later ones skip the 16-column K blocks beyond it for tiles whose B operand lies in those
+                // rows -- products of exact zeros, so M is unchanged.
+                int* kck = q.kct ? q.kct + k * 8 : nullptr;
+                const bool kcu = kck && q.kc_use, kcr = kck && !q.kc_use;  // uniform
                 hk::d4 acc[DT_TILES];
+                int kcl[DT_TILES], tI[DT_TILES], tJ[DT_TILES];  // wave-uniform: the tile's K limit and block row / col
 #pragma unroll
-                for (int u = 0; u < DT_TILES; u++) acc[u] = hk::d4{0.0, 0.0, 0.0, 0.0};
-                for (int kb = 0; kb < ng; kb += 16) {
-                    double r[8];
+                for (int u = 0; u < DT_TILES; u++) {
+                    acc[u] = hk::d4{0.0, 0.0, 0.0, 0.0};
+                    int I = 0;
+                    const int t = wv + 4 * u;
+                    while ((I + 1) * (I + 2) / 2 <= t) I++;
+                    tI[u] = I;
+                    tJ[u] = t - I * (I + 1) / 2;
+                    kcl[u] = t >= nT ? 0 : kcu ? __builtin_amdgcn_readfirstlane(kck[tJ[u]]) : ng;
+                }
+                // the next block's loads are issued before this block's MFMAs, so their latency hides behind them
+                double r[8], dq, qq;
+                auto stage_load = [&](int kb) {
 #pragma unroll
                     for (int u = 0; u < 8; u++) {
                         const int e = u * WT + tid, kk = fdiv(e, rS), i = e - kk * ldS;
                         r[u] = gld(D, p4i(i, kb + kk, sdG), e < 16 * ldS && i < nux && kb + kk < ng);
                     }
-                    const double dq = gld(Qg, kb + (tid & 15), tid < 16 && kb + tid < ng);
-                    const double qq = gld(qg, kb + (tid & 15), tid < 16 && kb + tid < ng);
+                    dq = gld(Qg, kb + (tid & 15), tid < 16 && kb + tid < ng);
+                    qq = gld(qg, kb + (tid & 15), tid < 16 && kb + tid < ng);
+                };
+                for (int kb = 0; kb < ng; kb += 16) {
+                    stage_load(kb);
                     bar();  // the previous block's operands are read
 #pragma unroll
                     for (int u = 0; u < 8; u++) {
-                        const int e = u * WT + tid;
-                        if (e < 16 * ldS) Ds[e] = r[u];  // Ds[i + kk ldS]
+                        const int e = u * WT + tid, kk = fdiv(e, rS), i = e - kk * ldS;
+                        if (e < 16 * ldS) Ds[kk + DS_LD * i] = r[u];
+                        if (kcr && e < 16 * ldS && r[u] != 0.0) atomicMax(&kck[i >> 4], kb + kk + 1);
                     }
                     if (tid < 16) {
                         dqs[tid] = dq;
                         qrs[tid] = qq;
                     }
-                    bar();
+                    lds_bar();
+                    // a tile runs the block if its B rows have a nonzero column in it (the block's chunks beyond the
+                    // limit are products of zeros); the four chunks' operands are read before the four MFMAs
 #pragma unroll
                     for (int u = 0; u < DT_TILES; u++) {
-                        const int t = wv + 4 * u;
-                        if (t < nT) {
-                            int I = 0;
-                            while ((I + 1) * (I + 2) / 2 <= t) I++;
-                            const int J = t - I * (I + 1) / 2;
-                            const int ra = 16 * I + c16, rb = 16 * J + c16;
+                        if (kb < kcl[u]) {
+                            int ti = __builtin_amdgcn_readfirstlane(tI[u]), tj = __builtin_amdgcn_readfirstlane(tJ[u]);
+                            asm volatile("" : "+s"(ti), "+s"(tj));  // tile addresses per block, not hoisted (VGPRs)
+                            const int ra = 16 * ti + c16;
+                            const double* pa = Ds + g4 + DS_LD * ra;
+                            const double* pb = Ds + g4 + DS_LD * (16 * tj + c16);
+                            double av[4], bv[4];
+                            // row nux of Ds is zero: its A operand is qx_g (0 in a pure factorisation), the others'
+                            // is diag(Qx_g) DCt, with no select for the compiler to turn into a branch over the reads
+                            const double sq = (ra == nux && !a.trf) ? 1.0 : 0.0;
 #pragma unroll
                             for (int kc = 0; kc < 4; kc++) {
-                                if (kb + 4 * kc >= ng) break;  // the direct loop's chunk count, nK
-                                const int kk = 4 * kc + g4;
-                                double av = Ds[ra + kk * ldS] * dqs[kk];
-                                if (ra == nux) av = a.trf ? 0.0 : qrs[kk];
-                                const double bv = Ds[rb + kk * ldS];
-                                acc[u] = hk::mfma(av, bv, acc[u]);
+                                av[kc] = fma(qrs[4 * kc + g4], sq, pa[4 * kc] * dqs[4 * kc + g4]);
+                                bv[kc] = pb[4 * kc];
                             }
+#pragma unroll
+                            for (int kc = 0; kc < 4; kc++) acc[u] = hk::mfma(av[kc], bv[kc], acc[u]);
                         }
                     }
                 }
 #pragma unroll
                 for (int u = 0; u < DT_TILES; u++) {
-                    const int t = wv + 4 * u;
-                    if (t < nT) {
-                        int I = 0;
-                        while ((I + 1) * (I + 2) / 2 <= t) I++;
-                        const int J = t - I * (I + 1) / 2;
-                        const int col = 16 * J + c16;
+                    if (wv + 4 * u < nT) {
+                        const int col = 16 * tJ[u] + c16;
 #pragma unroll
                         for (int rr = 0; rr < 4; rr++) {
-                            const int row = 16 * I + g4 + 4 * rr;
+                            const int row = 16 * tI[u] + g4 + 4 * rr;
                             if (row < nz && col < nux && row >= col) M[poff(col, nz) + row - col] += acc[u][rr];
                         }
                     }

@@ -497,9 +497,14 @@ __device__ __forceinline__ void ric_sv(const WideIpmArgs& A, const IP& P, const 
     q.compute_pi = A.compute_mult;
     q.compute_Pb = 1;
     q.dev_box = box;
+    extern __shared__ double sm[];
+    int* kct = reinterpret_cast<int*>(sm + A.offKC);
+    q.kct = kct;
+    q.kc_use = __builtin_amdgcn_readfirstlane(kct[(A.w.N + 1) * 8]) != 0;
     bar();
     wide_sv_body(A.w, q);
     bar();
+    if (threadIdx.x == 0 && box) kct[(A.w.N + 1) * 8] = 1;  // every chunk has been scanned once (read after a barrier)
 }
 
 __device__ __forceinline__ void ric_trs(const WideIpmArgs& A, const IP& P, const double* hb, const double* hq, int compute_Pb,
@@ -547,7 +552,7 @@ extern "C" __attribute__((visibility("default"))) int hpmpc_mi355x_wide_ipm_debu
     } while (0)
 #endif
 
-__global__ __launch_bounds__(WT) void hk_wide_ipm(WideIpmArgs A) {
+__global__ __launch_bounds__(WT, 2) void hk_wide_ipm(WideIpmArgs A) {
 #ifdef HK_STAMPS
     unsigned long long t0_ = 0;
     int ph_ = -1;
@@ -555,6 +560,10 @@ __global__ __launch_bounds__(WT) void hk_wide_ipm(WideIpmArgs A) {
     extern __shared__ double sm[];
     const int p = blockIdx.x + A.w.p0;
     if (p >= A.w.nprob) return;
+    {
+        int* kct = reinterpret_cast<int*>(sm + A.offKC);  // the DCt chunk limits, empty
+        for (int e = threadIdx.x; e < (A.w.N + 1) * 8 + 1; e += WT) kct[e] = 0;
+    }
     wide_stage_table(A.w);
     const int tid = threadIdx.x;
     double* red = sm + A.offR;

@@ -12,6 +12,11 @@
 #include "hk_wide_host.h"
 
 extern "C" int hk_wide_ipm_launch(const WideIpmArgs* a, int count, int lds_doubles, hipStream_t stream);
+namespace {
+// the wide IPM's LDS: the Riccati carve, 8 doubles of reduction scratch, the DCt chunk-limit table ((N+1) x 8 ints
+// and a flag, hk_wide_core.h)
+inline int ipm_lds(const WLayout& L) { return L.lds + 8 + ((L.N + 1) * 8 + 2) / 2; }
+}  // namespace
 
 namespace {
 
@@ -103,7 +108,7 @@ bool ipm_check(const WIpm& W, int N, const int* nx, const int* nu, const int* nb
             }
         }
     }
-    if (!W.L.fits || W.L.lds + 8 > LDS_MAX_DOUBLES) {
+    if (!W.L.fits || ipm_lds(W.L) > LDS_MAX_DOUBLES) {
         hk_set_error(HPMPC_MI355X_EUNSUPPORTED, "wide stage beyond the kernel's tile limits (64 KiB LDS, nu+nx < 128, "
                                                 "nx <= 64)");
         return false;
@@ -229,11 +234,12 @@ void fill_args(const WIpm& W, const Stage& S, char* D, int N, WideIpmArgs& a) {
     a.ret = a.kk + 1;
     a.mu = reinterpret_cast<double*>(D + S.oCtl + 8);
     a.offR = L.lds;
+    a.offKC = L.lds + 8;
 }
 
 bool run(const WIpm& W, const Stage& S, const WideIpmArgs& a) {
     if (!g_w.up(S.total)) return false;
-    const int e = hk_wide_ipm_launch(&a, 1, W.L.lds + 8, g_w.stream);
+    const int e = hk_wide_ipm_launch(&a, 1, ipm_lds(W.L), g_w.stream);
     if (e) {
         char msg[96];
         snprintf(msg, sizeof msg, "hk_wide_ipm launch %s (%d)", e == -2 ? "refused: scratch / LDS beyond the limits" : "failed", e);
@@ -553,8 +559,9 @@ extern "C" int hpmpc_mi355x_wide_ipm_batch(const hpmpc_mi355x_wide_plan* q, int 
     a.ret = ret;
     a.mu = nullptr;
     a.offR = L.lds;
+    a.offKC = L.lds + 8;
     if (count == 0) return 0;
-    const int e = hk_wide_ipm_launch(&a, count, L.lds + 8, (hipStream_t)stream);
+    const int e = hk_wide_ipm_launch(&a, count, ipm_lds(L), (hipStream_t)stream);
     if (e) {
         char msg[96];
         snprintf(msg, sizeof msg, "hk_wide_ipm launch %s (%d)", e == -2 ? "refused: scratch / LDS beyond the limits" : "failed", e);
