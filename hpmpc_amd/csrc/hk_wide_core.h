@@ -269,17 +269,33 @@ __device__ __forceinline__ void wave_sync() {
 // dL: v[0..n) sits in registers, two entries per lane (v[l], v[l + 64], n <= 128), each pivot is broadcast by
 // readlane.  Every entry sees the same operations in the same order as the column loops over LDS they replace
 // (one LDS round trip and wave barrier per pivot), so the results are the same.
+// The pivots go in groups of four whose factor entries and inverse diagonals are read before the group's chain of
+// broadcasts (clamped in-range reads, then a select), so the LDS latency is paid once per group.
 // L' y = v on the first ns unknowns, descending (dtrsv_t over the u block): v[j] -= L[i][j] y_i for j < i.
 __device__ __forceinline__ void wave_solve_lt(double* v, const double* M, const double* dL, int nz, int ns) {
     const int l = threadIdx.x & 63;
     double v0 = l < ns ? v[l] : 0.0, v1 = l + 64 < ns ? v[l + 64] : 0.0;
-    for (int i = ns - 1; i >= 0; i--) {
-        const double y = rdlane(i < 64 ? v0 : v1, i & 63) * dL[i];
-        if (l < i) v0 -= M[poff(l, nz) + i - l] * y;
-        if (l + 64 < i) v1 -= M[poff(l + 64, nz) + i - l - 64] * y;
+    const int c0 = l < ns ? poff(l, nz) - l : 0, c1 = l + 64 < ns ? poff(l + 64, nz) - l - 64 : 0;
+    auto step = [&](int i, double m0, double m1, double d) {
+        const double y = rdlane(i < 64 ? v0 : v1, i & 63) * d;
+        if (l < i) v0 -= m0 * y;
+        if (l + 64 < i) v1 -= m1 * y;
         if (l == i) v0 = y;
         if (l + 64 == i) v1 = y;
+    };
+    int i = ns - 1;
+    for (; i >= 3; i -= 4) {
+        double m0[4], m1[4], d[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            m0[q] = M[c0 + (l < i - q ? i - q : l)];
+            m1[q] = M[c1 + (l + 64 < i - q ? i - q : l + 64)];
+            d[q] = dL[i - q];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) step(i - q, m0[q], m1[q], d[q]);
     }
+    for (; i >= 0; i--) step(i, M[c0 + (l < i ? i : l)], M[c1 + (l + 64 < i ? i : l + 64)], dL[i]);
     if (l < ns) v[l] = v0;
     if (l + 64 < ns) v[l + 64] = v1;
 }
@@ -287,14 +303,28 @@ __device__ __forceinline__ void wave_solve_lt(double* v, const double* M, const 
 __device__ __forceinline__ void wave_solve_ln(double* v, const double* M, const double* dL, int nz, int ns, int n) {
     const int l = threadIdx.x & 63;
     double v0 = l < n ? v[l] : 0.0, v1 = l + 64 < n ? v[l + 64] : 0.0;
-    for (int j = 0; j < ns; j++) {
-        const double y = rdlane(j < 64 ? v0 : v1, j & 63) * dL[j];
-        const int cj = poff(j, nz) - j;
-        if (l > j && l < n) v0 -= M[cj + l] * y;
-        if (l + 64 > j && l + 64 < n) v1 -= M[cj + l + 64] * y;
+    const int r0 = l < n ? l : 0, r1 = l + 64 < n ? l + 64 : 0;  // in-range rows for the unconditional reads
+    auto step = [&](int j, double m0, double m1, double d) {
+        const double y = rdlane(j < 64 ? v0 : v1, j & 63) * d;
+        if (l > j && l < n) v0 -= m0 * y;
+        if (l + 64 > j && l + 64 < n) v1 -= m1 * y;
         if (l == j) v0 = y;
         if (l + 64 == j) v1 = y;
+    };
+    auto rd = [&](int j, int r) { return M[poff(j, nz) - j + (r > j ? r : j)]; };
+    int j = 0;
+    for (; j + 3 < ns; j += 4) {
+        double m0[4], m1[4], d[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            m0[q] = rd(j + q, r0);
+            m1[q] = rd(j + q, r1);
+            d[q] = dL[j + q];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) step(j + q, m0[q], m1[q], d[q]);
     }
+    for (; j < ns; j++) step(j, rd(j, r0), rd(j, r1), dL[j]);
     if (l < n) v[l] = v0;
     if (l + 64 < n) v[l + 64] = v1;
 }
@@ -871,6 +901,7 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
         for (int j = tid; j < ns; j += WT) {
             const int cj = poff(j, nz) - j;
             double r = -M[cj + nux];
+            #pragma unroll 8
             for (int m = ns; m < nux; m++) r -= M[cj + m] * v[m];
             v[j] = r;
         }
@@ -883,6 +914,7 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
         double xn = 0.0;
         if (tid < nx1) {
             xn = q.vb ? q.vb[s.oP + tid] : W[nux + tid * ldW];  // b_k: the update_b vector when given
+            #pragma unroll 8
             for (int i = 0; i < nux; i++) xn += W[i + tid * ldW] * v[i];
         }
         bar();
@@ -898,12 +930,14 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
             if (tid < nx1) {
                 const int cj = poff(nu1 + tid, nz1) - (nu1 + tid);
                 double tj = M[cj + nux1];
+                #pragma unroll 8
                 for (int i = tid; i < nx1; i++) tj += M[cj + nu1 + i] * v[nu1 + i];
                 tmp[tid] = tj;
             }
             bar();
             if (tid < nx1) {
                 double acc = 0.0;
+                #pragma unroll 8
                 for (int j = 0; j <= tid; j++) acc += M[poff(nu1 + j, nz1) + tid - j] * tmp[j];
                 pi[s.oP + tid] = acc;
             }
@@ -967,6 +1001,7 @@ __device__ HK_WIDE_BODY void wide_trs_body(const WideArgs& a, const WideProb& q)
         if (k < a.N) {
             double c = 0.0;
             if (tid < nux)
+                #pragma unroll 8
                 for (int j = 0; j < nx1; j++) c += W[tid + j * ldW] * X[j];
             bar();
             if (tid < nux) v[tid] += c;
@@ -983,6 +1018,7 @@ __device__ HK_WIDE_BODY void wide_trs_body(const WideArgs& a, const WideProb& q)
             double t = 0.0;
             if (tid < nx) {
                 const int cj = poff(nu + tid, nz) - (nu + tid);
+                #pragma unroll 8
                 for (int i = tid; i < nx; i++) t += M[cj + nu + i] * bk(sp, i);
             }
             bar();
@@ -990,6 +1026,7 @@ __device__ HK_WIDE_BODY void wide_trs_body(const WideArgs& a, const WideProb& q)
             bar();
             if (tid < nx) {
                 double acc = 0.0;
+                #pragma unroll 8
                 for (int j = 0; j <= tid; j++) acc += M[poff(nu + j, nz) + tid - j] * W[j];
                 if (q.compute_Pb) Pb[sp.oP + tid] = acc;
                 X[tid] = (q.compute_Pb ? acc : Pb[sp.oP + tid]) + v[nu + tid];
@@ -1019,6 +1056,7 @@ __device__ HK_WIDE_BODY void wide_trs_body(const WideArgs& a, const WideProb& q)
         if (tid < ns) {  // - L[ns:nux, 0:ns]' x_k
             const int cj = poff(tid, nz) - tid;
             r = v[tid];
+            #pragma unroll 8
             for (int m = ns; m < nux; m++) r -= M[cj + m] * v[m];
         }
         bar();
@@ -1030,6 +1068,7 @@ __device__ HK_WIDE_BODY void wide_trs_body(const WideArgs& a, const WideProb& q)
         double xn = 0.0;
         if (tid < nx1) {
             xn = bk(s, tid);
+            #pragma unroll 8
             for (int i = 0; i < nux; i++) xn += W[i + tid * ldW] * v[i];
         }
         bar();
@@ -1043,12 +1082,14 @@ __device__ HK_WIDE_BODY void wide_trs_body(const WideArgs& a, const WideProb& q)
             if (tid < nx1) {
                 const int cj = poff(nu1 + tid, nz1) - (nu1 + tid);
                 double tj = 0.0;
+                #pragma unroll 8
                 for (int i = tid; i < nx1; i++) tj += M[cj + nu1 + i] * v[nu1 + i];
                 X[tid] = tj;
             }
             bar();
             if (tid < nx1) {
                 double acc = 0.0;
+                #pragma unroll 8
                 for (int j = 0; j <= tid; j++) acc += M[poff(nu1 + j, nz1) + tid - j] * X[j];
                 pi[s.oP + tid] = acc + pk;
             }
