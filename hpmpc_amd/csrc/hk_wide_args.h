@@ -19,6 +19,8 @@ struct WideStage {
 };
 
 static_assert(sizeof(WideStage) % sizeof(double) == 0, "LDS stage tables are carved in doubles");
+// per stage: the last nonzero DCt column + 1 of each 16-row tile of M (8 tiles), then a 'recorded' flag
+constexpr int KC_STRIDE = 9;
 
 struct WideArgs {
     int N, nprob, p0;
@@ -154,5 +156,5 @@ struct WideIpmArgs {
     int* ret;
     double* mu;    // per problem: final mu (residual routines: in / out)
     int offR;      // LDS reduction scratch (8 doubles) after the Riccati carve
-    int offKC;     // LDS: the general-constraint chunk limits ((N+1) x 8 ints) and their valid flag
+    int offKC;     // LDS: the general-constraint chunk limits ((N+1) x KC_STRIDE ints) and their valid flag
 };

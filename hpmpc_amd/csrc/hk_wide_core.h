@@ -229,27 +229,20 @@ __device__ __forceinline__ void dma_wait_keep(int keep) {
     }
 }
 
-// lib4 lower trapezoid rows [j, nz) of cols [0, nc) -> packed lower columns (nz <= 128: two rows per lane)
-template <int CU>
-__device__ void load_lower(double* M, const double* src, int sd, int nz, int nc) {
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-    for (int j0 = w; j0 < nc; j0 += 4 * CU) {
-        double r[CU][2];
-#pragma unroll
-        for (int u = 0; u < CU; u++)
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const int j = j0 + 4 * u, i = j + l + 64 * h;
-                r[u][h] = gld(src, p4i(i, j, sd), j < nc && i < nz);
+// lib4 lower trapezoid rows [j, nz) of cols [0, nc) -> packed lower columns by DMA, no VGPRs for the data: one
+// wave instruction moves 32 doubles of a packed column, two lanes per double (4 bytes each) gathered from the lib4
+// panels, so the whole trapezoid is one memory round trip.  In LDS after dma_wait() and a barrier.
+__device__ __forceinline__ void dma_lower(double* M, const double* src, int sd, int nz, int nc) {
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;
+    for (int j = w; j < nc; j += WT / 64)
+        for (int r0 = j; r0 < nz; r0 += 32) {
+            const int i = r0 + (l >> 1);
+            if (i < nz) {
+                const void* g = reinterpret_cast<const unsigned*>(src + p4i(i, j, sd)) + (l & 1);
+                lds_void_ptr d = (lds_void_ptr)(M + poff(j, nz) + r0 - j);
+                __builtin_amdgcn_global_load_lds(g, d, 4, 0, 0);
             }
-#pragma unroll
-        for (int u = 0; u < CU; u++)
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const int j = j0 + 4 * u, i = j + l + 64 * h;
-                if (j < nc && i < nz) M[poff(j, nz) + i - j] = r[u][h];
-            }
-    }
+        }
 }
 // broadcast lane l's double (l wave-uniform) through SGPRs
 __device__ __forceinline__ double rdlane(double v, int l) {
@@ -445,20 +438,20 @@ __device__ __forceinline__ void mfma_gemm(int m, int n, int K, FA a, FB b, FO ou
 }
 
 // sum_{j < n} a(j) b(j), accumulated in the order j = 0, 1, .. exactly as the plain loop (so bitwise the same
-// result), with the operands of 8 terms loaded before their multiply-adds: a global-memory dot product then costs
-// one memory latency per 8 terms instead of one per term.  a(j, ok) / b(j, ok) load term j (0 when !ok).
-template <class FA, class FB>
+// result), with the operands of NB terms loaded before their multiply-adds: a global-memory dot product then costs
+// one memory latency per NB terms instead of one per term.  a(j, ok) / b(j, ok) load term j (0 when !ok).
+template <int NB = 8, class FA, class FB>
 __device__ __forceinline__ double bdot(int n, FA a, FB b, double acc = 0.0) {
-    for (int j0 = 0; j0 < n; j0 += 8) {
-        double x[8], y[8];
+    for (int j0 = 0; j0 < n; j0 += NB) {
+        double x[NB], y[NB];
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
+        for (int u = 0; u < NB; u++) {
             const bool ok = j0 + u < n;
             x[u] = a(j0 + u, ok);
             y[u] = b(j0 + u, ok);
         }
 #pragma unroll
-        for (int u = 0; u < 8; u++)
+        for (int u = 0; u < NB; u++)
             if (j0 + u < n) acc += x[u] * y[u];
     }
     return acc;
@@ -472,8 +465,9 @@ struct WideProb {
     const double *hb, *hq;                  // trs: b / q vectors (null: the augmented rows)
     int compute_pi, compute_Pb;
     bool dev_box;                           // sv: apply the box terms Qx / qx at idxb on the device
-    int* kct;                               // LDS (nullable): per stage and 16-row tile of M, 1 + the last DCt column
-                                            // with a nonzero entry in the tile's rows
+    int* kct;                               // LDS (nullable): per stage (KC_STRIDE) and 16-row tile of M, 1 + the last
+                                            // DCt column with a nonzero entry in the tile's rows; then the stage's
+                                            // 'recorded' flag
     bool kc_use;                            // kct is complete (a factorisation has scanned every chunk): use it
 };
 
@@ -523,6 +517,11 @@ __device__ __forceinline__ WideProb wide_prob(const WideArgs& a, int p) {
     do {        \
     } while (0)
 #endif
+#ifndef TSUB
+#define TSUB(i) \
+    do {        \
+    } while (0)
+#endif
 __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) {
     extern __shared__ double sm[];
     const StTab st{reinterpret_cast<const WideStage*>(sm + a.offST)};  // filled by the kernel (wide_stage_table)
@@ -544,7 +543,8 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
         const WideStage s = st[k];
         const int nu = s.nu, nux = s.nu + s.nx, nz = nux + 1, nx1 = s.nx1;
         WSUB(0);
-        load_lower<4>(M, RSQ + s.oR, s.sdR, nz, nux);
+        dma_lower(M, RSQ + s.oR, s.sdR, nz, nux);
+        dma_wait();
         if (q.vq || q.dev_box) {  // device-side q_k row and box terms (d_back_ric_rec.c:197-209, :249-291): the
             bar();           // staged RSQrq is the caller's original, so diag[idxb] = bd + Qx is a += Qx
             if (q.vq && !a.trf)
@@ -680,7 +680,7 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
                 // factorisation records per 16-row tile of M the last column with a nonzero entry in the tile's rows
                 // (kct), the later ones skip the 16-column K blocks beyond it for tiles whose B operand lies in those
                 // rows -- products of exact zeros, so M is unchanged.
-                int* kck = q.kct ? q.kct + k * 8 : nullptr;
+                int* kck = q.kct ? q.kct + k * KC_STRIDE : nullptr;
                 const bool kcu = kck && q.kc_use, kcr = kck && !q.kc_use;  // uniform
                 hk::d4 acc[DT_TILES];
                 int kcl[DT_TILES], tI[DT_TILES], tJ[DT_TILES];  // wave-uniform: the tile's K limit and block row / col
@@ -743,6 +743,7 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
                         }
                     }
                 }
+                if (kcr && tid == 0) kck[KC_STRIDE - 1] = 1;  // this stage's limits are recorded
 #pragma unroll
                 for (int u = 0; u < DT_TILES; u++) {
                     if (wv + 4 * u < nT) {
@@ -850,15 +851,20 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
                     const int ra = 16 * (T0 + I) + c16, rb = 16 * (T0 + J) + c16;
                     hk::d4 acc = {0.0, 0.0, 0.0, 0.0};
                     const int rac = ra < nz ? ra : nz - 1, rbc = rb < nux ? rb : nux - 1;
-                    for (int kc = 0; kc < nK; kc++) {
+                    // the panel's (at most four) K chunks: every operand read before the first MFMA
+                    double av[4], bv[4];
+#pragma unroll
+                    for (int kc = 0; kc < 4; kc++) {
                         const int kk = p0 + 4 * kc + g4;
                         const bool kok = kk < pe;
                         const int kq = kok ? kk : pe - 1, ck = poff(kq, nz) - kq;
                         const double x = M[ck + rac], y = M[ck + rbc];  // unconditional (rows >= pe > kq), then a select
-                        const double av = (ra < nz && kok) ? x : 0.0;
-                        const double bv = (rb < nux && kok) ? y : 0.0;
-                        acc = hk::mfma(av, bv, acc);
+                        av[kc] = (ra < nz && kok) ? x : 0.0;
+                        bv[kc] = (rb < nux && kok) ? y : 0.0;
                     }
+#pragma unroll
+                    for (int kc = 0; kc < 4; kc++)
+                        if (kc < nK) acc = hk::mfma(av[kc], bv[kc], acc);
                     const int col = 16 * (T0 + J) + c16;
 #pragma unroll
                     for (int r = 0; r < 4; r++) {
@@ -980,24 +986,39 @@ __device__ HK_WIDE_BODY void wide_trs_body(const WideArgs& a, const WideProb& q)
         const WideStage s = st[k];
         const int nux = s.nu + s.nx, nz = nux + 1, nx1 = s.nx1;
         const int ns = k == 0 ? nux : s.nu;
+        TSUB(0);
         load_flat<16>(M, F + s.oL, poff(nux, nz) + nux);
         if (k < a.N) load_dense<8>(W, ldW, BAbt + s.oB, s.sdB, nux, nx1);
         for (int i = tid; i < nux; i += WT) v[i] = qk(s, i);
+        if (k > 0)  // b_{k-1} for Pb_{k-1} into W's unused row nux, read with the other loads of the stage
+            for (int i = tid; i < s.nx; i += WT) W[nux + i * ldW] = bk(st[k - 1], i);
         bar();
-        if (tid == 0)
-            for (int l = 0; l < s.nb; l++) v[a.idxb[s.oI + l]] += qx[s.oD + l];
+        TSUB(1);
+        for (int l = tid; l < s.nb; l += WT) v[a.idxb[s.oI + l]] += qx[s.oD + l];  // distinct indices (as the sv)
         bar();
         if (q.DCt && s.ng > 0) {  // + DCt qx_g (dgemv_n_lib, d_back_ric_rec.c:620-633)
-            if (tid < nux) {
-                const double* D = q.DCt + s.oG;
-                const double* qg = qx + s.oD + s.pnb;
-                const double c = bdot(
-                    s.ng, [&](int g, bool ok) { return gld(D, p4i(tid, g, s.sdG), ok); },
-                    [&](int g, bool ok) { return gld(qg, g, ok); });
-                v[tid] += c;
-            }
+            // nch lanes of one wave per row, each summing a contiguous column chunk (12 loads in flight per batch),
+            // the chunk sums gathered by the row's first lane; columns past the last nonzero of the row's 16-row
+            // tile (kct, recorded by the factorisation) are products of zeros and skipped
+            const double* D = q.DCt + s.oG;
+            const double* qg = qx + s.oD + s.pnb;
+            const int nch = nux <= 64 ? 4 : nux <= 84 ? 3 : nux <= 128 ? 2 : 1, R = 64 / nch;
+            const int w = tid >> 6, l = tid & 63, il = l / nch, ch = l - il * nch, i = w * R + il;
+            const int* kck = q.kct ? q.kct + k * KC_STRIDE : nullptr;
+            const bool kcu = kck && q.kc_use && __builtin_amdgcn_readfirstlane(kck[KC_STRIDE - 1]) != 0;
+            const bool row = il < R && i < nux;
+            const int lim = (kcu && row) ? kck[i >> 4] : s.ng;
+            const int cs = (s.ng + nch - 1) / nch, g0 = ch * cs, g1 = min(g0 + cs, lim);
+            const double part = row ? bdot<12>(
+                                          g1 - g0, [&](int g, bool ok) { return gld(D, p4i(i, g0 + g, s.sdG), ok); },
+                                          [&](int g, bool ok) { return gld(qg, g0 + g, ok); })
+                                    : 0.0;
+            double c = 0.0;
+            for (int h = 0; h < nch; h++) c += __shfl(part, il * nch + h);  // chunk order
+            if (row && ch == 0) v[i] += c;
             bar();
         }
+        TSUB(2);
         if (k < a.N) {
             double c = 0.0;
             if (tid < nux)
@@ -1011,6 +1032,7 @@ __device__ HK_WIDE_BODY void wide_trs_body(const WideArgs& a, const WideProb& q)
             if (tid < 64) wave_solve_ln(v, M, dL, nz, ns, nux);
             bar();
         }
+        TSUB(3);
         for (int i = tid; i < nux; i += WT) ux[s.oU + i] = v[i];
         if (k > 0) {  // w for stage k-1: Pb_{k-1} = Lxx_k (Lxx_k' b_{k-1}), plus v_{k,x}
             const WideStage sp = st[k - 1];
@@ -1019,7 +1041,7 @@ __device__ HK_WIDE_BODY void wide_trs_body(const WideArgs& a, const WideProb& q)
             if (tid < nx) {
                 const int cj = poff(nu + tid, nz) - (nu + tid);
                 #pragma unroll 8
-                for (int i = tid; i < nx; i++) t += M[cj + nu + i] * bk(sp, i);
+                for (int i = tid; i < nx; i++) t += M[cj + nu + i] * W[nux + i * ldW];
             }
             bar();
             if (tid < nx) W[tid] = t;  // W is free: scratch
@@ -1033,6 +1055,7 @@ __device__ HK_WIDE_BODY void wide_trs_body(const WideArgs& a, const WideProb& q)
             }
         }
         bar();
+        TSUB(4);
     }
     // forward
     {
@@ -1047,6 +1070,7 @@ __device__ HK_WIDE_BODY void wide_trs_body(const WideArgs& a, const WideProb& q)
         const int nux = s.nu + s.nx, nz = nux + 1, nx1 = s.nx1, nu1 = s.nu1;
         const int ns = k == 0 ? nux : s.nu;
         const double* dL = M + poff(nux, nz);
+        TSUB(0);
         load_dense<8>(W, ldW, BAbt + s.oB, s.sdB, nux, nx1);
         double pk = 0.0;
         if (tid < nx1) pk = ux[s1.oU + nu1 + tid];  // v_{k+1,x} of the backward, before x_{k+1} replaces it
@@ -1062,8 +1086,10 @@ __device__ HK_WIDE_BODY void wide_trs_body(const WideArgs& a, const WideProb& q)
         bar();
         if (tid < ns) v[tid] = r;
         bar();
+        TSUB(5);
         if (tid < 64) wave_solve_lt(v, M, dL, nz, ns);
         bar();
+        TSUB(6);
         for (int j = tid; j < nux; j += WT) ux[s.oU + j] = v[j];
         double xn = 0.0;
         if (tid < nx1) {
@@ -1078,6 +1104,7 @@ __device__ HK_WIDE_BODY void wide_trs_body(const WideArgs& a, const WideProb& q)
         for (int j = tid; j < nu1; j += WT) v[j] = ux[s1.oU + j];
         if (tid < nx1) v[nu1 + tid] = xn;
         bar();
+        TSUB(7);
         if (q.compute_pi) {
             if (tid < nx1) {
                 const int cj = poff(nu1 + tid, nz1) - (nu1 + tid);
@@ -1095,6 +1122,7 @@ __device__ HK_WIDE_BODY void wide_trs_body(const WideArgs& a, const WideProb& q)
             }
             bar();
         }
+        TSUB(8);
     }
     if (tid < st[a.N].nx) ux[st[a.N].oU + tid] = v[tid];
 }

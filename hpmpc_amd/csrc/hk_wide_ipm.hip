@@ -33,6 +33,15 @@ __device__ unsigned long long g_wsub_t0;
             g_wsub_t0 = t_;                                                                 \
         }                                                                                   \
     } while (0)
+#define TSUB(i)                                                                             \
+    do {                                                                                    \
+        unsigned long long t_;                                                              \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");           \
+        if (g_wdbg && blockIdx.x == 0 && threadIdx.x == 0) {                                \
+            if ((i) > 0) g_wdbg[22 + (i)] += t_ - g_wsub_t0;                                \
+            g_wsub_t0 = t_;                                                                 \
+        }                                                                                   \
+    } while (0)
 #endif
 #include "hk_wide_core.h"
 
@@ -375,6 +384,11 @@ __device__ __forceinline__ double residuals(const WideIpmArgs& A, const IP& P, b
     // the rows of every stage (nux r_q rows, then nx1 r_b rows) form one flat range that all threads share, so a
     // stage's ~100 rows do not leave most of the workgroup idle; each row's dot products load 8 terms at a time
     // from the problem's (wave-uniform) bases.  Every row sums in the reference's order, as before.
+    // a general-constraint row term stops at the row's 16-row tile's last nonzero DCt column once the factorisation
+    // has recorded it (kct): the skipped terms are products of exact zeros
+    extern __shared__ double sm[];
+    const int* kct = reinterpret_cast<const int*>(sm + A.offKC);
+    const bool kcu = __builtin_amdgcn_readfirstlane(kct[(N + 1) * KC_STRIDE]) != 0;
     int k = 0, rbase = 0;
     for (int rr = tid;; rr += WT) {
         while (k <= N && rr >= rbase + wst(A)[k].nu + wst(A)[k].nx + wst(A)[k].nx1) {
@@ -393,7 +407,8 @@ __device__ __forceinline__ double residuals(const WideIpmArgs& A, const IP& P, b
             if (r < nux) {
                 const int i = r;
                 const double q = P.vq ? P.vq[s.oU + i] : P4(R, s.sdR, nux, i);
-                const double sy = bdot(
+                const int glim = (kcu && kct[k * KC_STRIDE + KC_STRIDE - 1]) ? kct[k * KC_STRIDE + (i >> 4)] : s.ng;
+                const double sy = bdot<16>(
                     nux,
                     [&](int j, bool ok) {
                         return gld(P.RSQ, s.oR + (i >= j ? p4i(i, j, s.sdR) : p4i(j, i, s.sdR)), ok);
@@ -411,8 +426,8 @@ __device__ __forceinline__ double residuals(const WideIpmArgs& A, const IP& P, b
                     v += sy;
                     if (k < N) v += bp;
                     if (s.ng > 0)
-                        v += bdot(
-                            s.ng, [&](int g, bool ok) { return gld(P.DCt, s.oG + p4i(i, g, s.sdG), ok); },
+                        v += bdot<16>(
+                            glim, [&](int g, bool ok) { return gld(P.DCt, s.oG + p4i(i, g, s.sdG), ok); },
                             [&](int g, bool ok) { return gld(P.lam, olg + png + g, ok) - gld(P.lam, olg + g, ok); });
                 } else {
                     v = -q;
@@ -421,9 +436,9 @@ __device__ __forceinline__ double residuals(const WideIpmArgs& A, const IP& P, b
                     v -= sy;
                     if (s.ng > 0) {
                         auto dg = [&](int g, bool ok) { return gld(P.DCt, s.oG + p4i(i, g, s.sdG), ok); };
-                        const double ca = bdot(s.ng, dg, [&](int g, bool ok) { return gld(P.lam, olg + g, ok); });
+                        const double ca = bdot<16>(glim, dg, [&](int g, bool ok) { return gld(P.lam, olg + g, ok); });
                         const double cb =
-                            bdot(s.ng, dg, [&](int g, bool ok) { return gld(P.lam, olg + png + g, ok); });
+                            bdot<16>(glim, dg, [&](int g, bool ok) { return gld(P.lam, olg + png + g, ok); });
                         v += ca;
                         v -= cb;
                     }
@@ -436,7 +451,7 @@ __device__ __forceinline__ double residuals(const WideIpmArgs& A, const IP& P, b
                 const WideStage s1 = wst(A)[k + 1];
                 const double b = P.vb ? P.vb[s.oP + j] : P4(B, s.sdB, nux, j);
                 const double x1 = P.ux[s1.oU + s1.nu + j];
-                const double c = bdot(
+                const double c = bdot<16>(
                     nux, [&](int i, bool ok) { return gld(P.BAbt, s.oB + p4i(i, j, s.sdB), ok); },
                     [&](int i, bool ok) { return gld(P.ux, s.oU + i, ok); });
                 P.rb[s.oP + j] = plain ? -((x1 - b) - c) : (b - x1) + c;
@@ -500,11 +515,11 @@ __device__ __forceinline__ void ric_sv(const WideIpmArgs& A, const IP& P, const 
     extern __shared__ double sm[];
     int* kct = reinterpret_cast<int*>(sm + A.offKC);
     q.kct = kct;
-    q.kc_use = __builtin_amdgcn_readfirstlane(kct[(A.w.N + 1) * 8]) != 0;
+    q.kc_use = __builtin_amdgcn_readfirstlane(kct[(A.w.N + 1) * KC_STRIDE]) != 0;
     bar();
     wide_sv_body(A.w, q);
     bar();
-    if (threadIdx.x == 0 && box) kct[(A.w.N + 1) * 8] = 1;  // every chunk has been scanned once (read after a barrier)
+    if (threadIdx.x == 0 && box) kct[(A.w.N + 1) * KC_STRIDE] = 1;  // every chunk has been scanned once (read after a barrier)
 }
 
 __device__ __forceinline__ void ric_trs(const WideIpmArgs& A, const IP& P, const double* hb, const double* hq, int compute_Pb,
@@ -524,6 +539,10 @@ __device__ __forceinline__ void ric_trs(const WideIpmArgs& A, const IP& P, const
     q.compute_pi = A.compute_mult;
     q.compute_Pb = compute_Pb;
     q.dev_box = false;
+    extern __shared__ double sm[];
+    int* kct = reinterpret_cast<int*>(sm + A.offKC);  // the general-constraint column limits of the factorisation
+    q.kct = kct;
+    q.kc_use = __builtin_amdgcn_readfirstlane(kct[(A.w.N + 1) * KC_STRIDE]) != 0;
     bar();
     wide_trs_body(A.w, q);
     bar();
@@ -562,7 +581,7 @@ __global__ __launch_bounds__(WT, 2) void hk_wide_ipm(WideIpmArgs A) {
     if (p >= A.w.nprob) return;
     {
         int* kct = reinterpret_cast<int*>(sm + A.offKC);  // the DCt chunk limits, empty
-        for (int e = threadIdx.x; e < (A.w.N + 1) * 8 + 1; e += WT) kct[e] = 0;
+        for (int e = threadIdx.x; e < (A.w.N + 1) * KC_STRIDE + 1; e += WT) kct[e] = 0;
     }
     wide_stage_table(A.w);
     const int tid = threadIdx.x;

@@ -15,7 +15,7 @@ extern "C" int hk_wide_ipm_launch(const WideIpmArgs* a, int count, int lds_doubl
 namespace {
 // the wide IPM's LDS: the Riccati carve, 8 doubles of reduction scratch, the DCt chunk-limit table ((N+1) x 8 ints
 // and a flag, hk_wide_core.h)
-inline int ipm_lds(const WLayout& L) { return L.lds + 8 + ((L.N + 1) * 8 + 2) / 2; }
+inline int ipm_lds(const WLayout& L) { return L.lds + 8 + ((L.N + 1) * KC_STRIDE + 2) / 2; }
 }  // namespace
 
 namespace {

@@ -38,3 +38,10 @@ st = t[12:23]
 print(f"  inside every ric_sv of the solve (phase 1 included), {st.sum()} cycles:")
 for i, n in enumerate(sub):
     print(f"    {n:26s} {st[i]:12d}  {100.0 * st[i] / max(st.sum(), 1):5.1f} %")
+tsub = ["backward: L, BAbt, q loads", "backward: box + DCt qx_g", "backward: + BAbt w, n-form solve",
+        "backward: Pb, w", "forward: BAbt load, L' x product", "forward: t-form solve (wave 0)",
+        "forward: x_{k+1}, next L load", "forward: pi"]
+tt = t[23:31]
+print(f"  inside every ric_trs of the solve, {tt.sum()} cycles:")
+for i, n in enumerate(tsub):
+    print(f"    {n:34s} {tt[i]:12d}  {100.0 * tt[i] / max(tt.sum(), 1):5.1f} %")
