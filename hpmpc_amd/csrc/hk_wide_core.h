@@ -217,13 +217,15 @@ __device__ __forceinline__ int dma_copy_any(double* dst, const double* src, int 
 }
 __device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 // Wait until at most `keep` of this wave's vector-memory operations are outstanding (they complete in issue order):
-// the copies issued before the last `keep` have landed.  keep is wave-uniform; beyond 15 it waits for all.
+// the copies issued before the last `keep` have landed.  keep is wave-uniform; beyond 31 it waits for all.
 __device__ __forceinline__ void dma_wait_keep(int keep) {
     switch (__builtin_amdgcn_readfirstlane(keep)) {
 #define HK_VMW(n) \
     case n: asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory"); break;
         HK_VMW(1) HK_VMW(2) HK_VMW(3) HK_VMW(4) HK_VMW(5) HK_VMW(6) HK_VMW(7) HK_VMW(8)
-        HK_VMW(9) HK_VMW(10) HK_VMW(11) HK_VMW(12) HK_VMW(13) HK_VMW(14) HK_VMW(15)
+        HK_VMW(9) HK_VMW(10) HK_VMW(11) HK_VMW(12) HK_VMW(13) HK_VMW(14) HK_VMW(15) HK_VMW(16)
+        HK_VMW(17) HK_VMW(18) HK_VMW(19) HK_VMW(20) HK_VMW(21) HK_VMW(22) HK_VMW(23) HK_VMW(24)
+        HK_VMW(25) HK_VMW(26) HK_VMW(27) HK_VMW(28) HK_VMW(29) HK_VMW(30) HK_VMW(31)
 #undef HK_VMW
         default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -243,6 +245,22 @@ __device__ __forceinline__ void dma_lower(double* M, const double* src, int sd, 
                 __builtin_amdgcn_global_load_lds(g, d, 4, 0, 0);
             }
         }
+}
+// lib4 rows [0, nr) x cols [0, nc) -> dense column-major (ld) by DMA, no VGPRs for the data: one wave instruction per
+// 32 rows of a column (two lanes per double, 4 bytes each); returns the instructions this wave issued (dma_wait_keep)
+__device__ __forceinline__ int dma_dense(double* D, int ld, const double* src, int sd, int nr, int nc) {
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;
+    int cnt = 0;
+    for (int j = w; j < nc; j += WT / 64)
+        for (int r0 = 0; r0 < nr; r0 += 32, cnt++) {
+            const int i = r0 + (l >> 1);
+            if (i < nr) {
+                const void* g = reinterpret_cast<const unsigned*>(src + p4i(i, j, sd)) + (l & 1);
+                lds_void_ptr d = (lds_void_ptr)(D + r0 + j * ld);
+                __builtin_amdgcn_global_load_lds(g, d, 4, 0, 0);
+            }
+        }
+    return cnt;
 }
 // broadcast lane l's double (l wave-uniform) through SGPRs
 __device__ __forceinline__ double rdlane(double v, int l) {
@@ -889,20 +907,24 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
         WSUB(10);
     }
 
-    // forward substitution: L_k (packed + 1/diag) and BAbt_k are staged into LDS (M, W) per stage
+    // forward substitution: L_k (packed + 1/diag) and BAbt_k are staged into LDS (M, W) per stage by DMA, each issued
+    // as soon as its buffer is free -- L_{k+1} while x_{k+1} is formed, BAbt_{k+1} during pi_k and stage k+1's solve --
+    // with LDS-only barriers in between so that the copies stay in flight
     double* tmp = X;  // Lxx is no longer needed: nx1 doubles of scratch for pi
-    {
+    const int nfw = (a.skip & 1) || a.trf ? 0 : a.N;
+    if (nfw > 0) {
         const WideStage s0 = st[0];
         const int nz0 = s0.nu + s0.nx + 1;
-        load_flat<16>(M, F + s0.oL, poff(nz0 - 1, nz0) + nz0 - 1);
+        dma_copy_any<WT>(M, F + s0.oL, poff(nz0 - 1, nz0) + nz0 - 1, tid);
+        dma_dense(W, ldW, BAbt + s0.oB, s0.sdB, nz0, s0.nx1);
+        dma_wait();
+        bar();
     }
-    for (int k = 0; k < ((a.skip & 1) || a.trf ? 0 : a.N); k++) {
+    for (int k = 0; k < nfw; k++) {
         const WideStage s = st[k];
         const int nux = s.nu + s.nx, nz = nux + 1, nx1 = s.nx1, nu1 = s.nu1;
         const int ns = k == 0 ? nux : s.nu;
         const double* dL = M + poff(nux, nz);
-        load_dense<8>(W, ldW, BAbt + s.oB, s.sdB, nz, nx1);
-        bar();
         // v[0:ns] = -l[0:ns] - L[ns:nux, 0:ns]' v[ns:nux]   (v[ns:nux] = x_k from the previous stage)
         for (int j = tid; j < ns; j += WT) {
             const int cj = poff(j, nz) - j;
@@ -911,10 +933,14 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
             for (int m = ns; m < nux; m++) r -= M[cj + m] * v[m];
             v[j] = r;
         }
-        bar();
+        lds_bar();
         // back substitution with L[0:ns, 0:ns]' (inv_diag multiply), column-oriented inside wave 0
         if (tid < 64) wave_solve_lt(v, M, dL, nz, ns);
+        dma_wait();  // BAbt_k (issued during the previous stage) has landed, every wave's part after the barrier
         bar();
+        const WideStage s1 = st[k + 1];
+        const int nux1 = nu1 + nx1, nz1 = nux1 + 1;
+        dma_copy_any<WT>(M, F + s1.oL, poff(nux1, nz1) + nux1, tid);  // L_k is done with
         for (int j = tid; j < nux; j += WT) ux[s.oU + j] = v[j];
         // x_{k+1} = b_k + BAbt_k' ux_k
         double xn = 0.0;
@@ -923,15 +949,14 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
             #pragma unroll 8
             for (int i = 0; i < nux; i++) xn += W[i + tid * ldW] * v[i];
         }
-        bar();
-        const WideStage s1 = st[k + 1];
-        const int nux1 = nu1 + nx1, nz1 = nux1 + 1;
+        lds_bar();  // W is read
         if (tid < nx1) {
             v[nu1 + tid] = xn;
             ux[s1.oU + nu1 + tid] = xn;
         }
-        load_flat<16>(M, F + s1.oL, poff(nux1, nz1) + nux1);
-        bar();
+        const int nB = k + 1 < nfw ? dma_dense(W, ldW, BAbt + s1.oB, s1.sdB, nz1, st[k + 1].nx1) : 0;
+        dma_wait_keep(nB);  // L_{k+1} has landed (this wave's part); BAbt_{k+1} stays in flight
+        lds_bar();
         if (q.compute_pi) {  // pi_k = Lxx (Lxx' x + l), Lxx of stage k+1 (rows / cols nu1..)
             if (tid < nx1) {
                 const int cj = poff(nu1 + tid, nz1) - (nu1 + tid);
@@ -940,16 +965,17 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
                 for (int i = tid; i < nx1; i++) tj += M[cj + nu1 + i] * v[nu1 + i];
                 tmp[tid] = tj;
             }
-            bar();
+            lds_bar();
             if (tid < nx1) {
                 double acc = 0.0;
                 #pragma unroll 8
                 for (int j = 0; j <= tid; j++) acc += M[poff(nu1 + j, nz1) + tid - j] * tmp[j];
                 pi[s.oP + tid] = acc;
             }
-            bar();
+            lds_bar();
         }
     }
+    dma_wait();
     WSUB(11);
 }
 
