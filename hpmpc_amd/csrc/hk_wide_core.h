@@ -1083,12 +1083,15 @@ __device__ HK_WIDE_BODY void wide_trs_body(const WideArgs& a, const WideProb& q)
         bar();
         TSUB(4);
     }
-    // forward
-    {
+    // forward: as the sv forward, L_{k+1} and BAbt_{k+1} by DMA as soon as their buffers are free, the stage's vector
+    // reads issued at its top, LDS-only barriers while the copies are in flight
+    if (a.N > 0) {
         const WideStage s0 = st[0];
         const int nz0 = s0.nu + s0.nx + 1;
-        load_flat<16>(M, F + s0.oL, poff(nz0 - 1, nz0) + nz0 - 1);
+        dma_copy_any<WT>(M, F + s0.oL, poff(nz0 - 1, nz0) + nz0 - 1, tid);
+        dma_dense(W, ldW, BAbt + s0.oB, s0.sdB, nz0 - 1, s0.nx1);
         load_flat<4>(v, ux + s0.oU, nz0 - 1);
+        dma_wait();
         bar();
     }
     for (int k = 0; k < a.N; k++) {
@@ -1097,11 +1100,14 @@ __device__ HK_WIDE_BODY void wide_trs_body(const WideArgs& a, const WideProb& q)
         const int ns = k == 0 ? nux : s.nu;
         const double* dL = M + poff(nux, nz);
         TSUB(0);
-        load_dense<8>(W, ldW, BAbt + s.oB, s.sdB, nux, nx1);
-        double pk = 0.0;
-        if (tid < nx1) pk = ux[s1.oU + nu1 + tid];  // v_{k+1,x} of the backward, before x_{k+1} replaces it
+        double pk = 0.0, bq = 0.0;
+        if (tid < nx1) {
+            pk = ux[s1.oU + nu1 + tid];  // v_{k+1,x} of the backward, before x_{k+1} replaces it
+            bq = bk(s, tid);
+        }
+        const double un = tid < nu1 ? ux[s1.oU + tid] : 0.0;  // the backward's processed u part of stage k+1
         for (int j = tid; j < ns; j += WT) v[j] = -v[j];
-        bar();
+        lds_bar();
         double r = 0.0;
         if (tid < ns) {  // - L[ns:nux, 0:ns]' x_k
             const int cj = poff(tid, nz) - tid;
@@ -1109,27 +1115,30 @@ __device__ HK_WIDE_BODY void wide_trs_body(const WideArgs& a, const WideProb& q)
             #pragma unroll 8
             for (int m = ns; m < nux; m++) r -= M[cj + m] * v[m];
         }
-        bar();
+        lds_bar();
         if (tid < ns) v[tid] = r;
-        bar();
+        lds_bar();
         TSUB(5);
         if (tid < 64) wave_solve_lt(v, M, dL, nz, ns);
+        dma_wait();  // BAbt_k (issued during the previous stage) has landed, every wave's part after the barrier
         bar();
         TSUB(6);
+        const int nux1 = nu1 + nx1, nz1 = nux1 + 1;
+        dma_copy_any<WT>(M, F + s1.oL, poff(nux1, nz1) + nux1, tid);  // L_k is done with
         for (int j = tid; j < nux; j += WT) ux[s.oU + j] = v[j];
         double xn = 0.0;
         if (tid < nx1) {
-            xn = bk(s, tid);
+            xn = bq;
             #pragma unroll 8
             for (int i = 0; i < nux; i++) xn += W[i + tid * ldW] * v[i];
         }
-        bar();
-        const int nux1 = nu1 + nx1, nz1 = nux1 + 1;
-        load_flat<16>(M, F + s1.oL, poff(nux1, nz1) + nux1);
+        lds_bar();  // W and v are read
         // v <- stage k+1: the backward's processed u part, and the actual state x_{k+1}
-        for (int j = tid; j < nu1; j += WT) v[j] = ux[s1.oU + j];
+        if (tid < nu1) v[tid] = un;
         if (tid < nx1) v[nu1 + tid] = xn;
-        bar();
+        const int nB = k + 1 < a.N ? dma_dense(W, ldW, BAbt + s1.oB, s1.sdB, nux1, st[k + 1].nx1) : 0;
+        dma_wait_keep(nB);  // L_{k+1} has landed (this wave's part); BAbt_{k+1} stays in flight
+        lds_bar();
         TSUB(7);
         if (q.compute_pi) {
             if (tid < nx1) {
@@ -1139,17 +1148,18 @@ __device__ HK_WIDE_BODY void wide_trs_body(const WideArgs& a, const WideProb& q)
                 for (int i = tid; i < nx1; i++) tj += M[cj + nu1 + i] * v[nu1 + i];
                 X[tid] = tj;
             }
-            bar();
+            lds_bar();
             if (tid < nx1) {
                 double acc = 0.0;
                 #pragma unroll 8
                 for (int j = 0; j <= tid; j++) acc += M[poff(nu1 + j, nz1) + tid - j] * X[j];
                 pi[s.oP + tid] = acc + pk;
             }
-            bar();
+            lds_bar();
         }
         TSUB(8);
     }
+    dma_wait();
     if (tid < st[a.N].nx) ux[st[a.N].oU + tid] = v[tid];
 }
 
