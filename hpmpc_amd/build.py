@@ -14,9 +14,9 @@ CSRC = os.path.join(ROOT, "hpmpc_amd", "csrc")
 LIBDIR = os.path.join(ROOT, "hpmpc_amd", "lib")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("HPMPC_ARCH", "gfx950")
-SOURCES = ["hpmpc_kernels.hip", "hk_ric2.hip", "hk_wide.hip", "hk_wide_ipm.hip", "hk_soft.hip", "hpmpc_capi.cpp", "hpmpc_capi_wide.cpp",
+SOURCES = ["hpmpc_kernels.hip", "hk_wide.hip", "hk_wide_ipm.hip", "hk_soft.hip", "hpmpc_capi.cpp", "hpmpc_capi_wide.cpp",
            "hpmpc_capi_wide_ipm.cpp", "hpmpc_capi_iface.cpp", "hpmpc_capi_mpc.cpp"]
-HEADERS = ["hpmpc_api.h", "hk_prims.h", "hk_riccati.h", "hk_ipm.h", "hk_mw.h", "hpmpc_kargs.h", "hk_wide_args.h", "hk_wide_core.h", "hk_wide_host.h", "hk_soft_args.h", "hk_launch_guard.h"]
+HEADERS = ["hpmpc_api.h", "hk_ipm_body.h", "hk_prims.h", "hk_riccati.h", "hk_ipm.h", "hk_mw.h", "hpmpc_kargs.h", "hk_wide_args.h", "hk_wide_core.h", "hk_wide_host.h", "hk_soft_args.h", "hk_launch_guard.h"]
 # MFMA accumulators stay in ordinary VGPRs: the stage tile is read and written by VALU code between
 # MFMAs, and the AGPR form costs 8 v_accvgpr moves each way per MFMA group.
 KFLAGS = ["-mllvm", "-amdgpu-mfma-vgpr-form"] + os.environ.get("HK_EXTRA_FLAGS", "").split()
@@ -56,7 +56,7 @@ def _deps(src, hdrs_all):
     return sorted(seen | {h for h in hdrs_all if os.path.basename(h) == "hpmpc_mi355x.h"})
 
 
-def build_hip(force: bool = False, verbose: bool = False, variant: str | None = None, extra=()) -> str:
+def build_hip(force: bool = False, verbose: bool = False, variant: str | None = None, extra=(), sources=()) -> str:
     """Each source compiles to its own object under build/ (rebuilt when it or a header is newer), then one
     link; a one-file change recompiles one translation unit.  variant: an A/B build with `extra` compiler flags,
     objects under build/obj_<variant>, library hpmpc_amd/lib/ab/lib<variant>.so (tools/gpu_ab.sh)."""
@@ -72,7 +72,7 @@ def build_hip(force: bool = False, verbose: bool = False, variant: str | None = 
     common = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall",
               "-Wno-unused-function"] + KFLAGS + list(extra)
     objs, procs = [], []
-    for src in SOURCES:
+    for src in SOURCES + list(sources):
         obj = os.path.join(objdir, src + ".o")
         objs.append(obj)
         if force or not _newer(obj, [os.path.join(CSRC, src)] + _deps(src, hdrs_all)):
@@ -104,6 +104,12 @@ def build_stamps(verbose: bool = False, force: bool = False) -> str:
     return dst
 
 
+def build_ric2(verbose: bool = False, force: bool = False) -> str:
+    """The two-wave Riccati sv (hk_ric2.hip, a measured negative result) is not in the product
+    library: this variant links it (-DHK_RIC2, HPMPC_MI355X_RIC_WAVES=2 selects it), for tests/test_gpu_ric2.py."""
+    return build_hip(force=force, verbose=verbose, variant="ric2", extra=["-DHK_RIC2"], sources=["hk_ric2.hip"])
+
+
 def build_calib(verbose: bool = False) -> str:
     """HBM counter calibration kernel (tools/hbm_calib.hip; profiling tool, not part of the product)."""
     os.makedirs(LIBDIR, exist_ok=True)
@@ -131,6 +137,7 @@ def build_oracle(force: bool = False) -> None:
 def build_all(force: bool = False, verbose: bool = False) -> None:
     build_hip(force=force, verbose=verbose)
     build_stamps(verbose=verbose, force=force)
+    build_ric2(verbose=verbose, force=force)
     build_calib(verbose=verbose)
     build_oracle(force=force)
 

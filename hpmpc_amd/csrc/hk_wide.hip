@@ -373,7 +373,9 @@ __global__ __launch_bounds__(WT, GM <= 4 ? 4 : 2) void hk_pcond(PcArgs a) {  // 
                 const int i = tid & 63;
                 emax = -hk::wave_min(i < nxs ? -PL(sdP, nus + i, nus + i) : 0.0);
             }
-            const bool pf = a.pform && small && gtab[sI] - 1e-11 * emax > 1e-15;  // uniform
+            // the P form's T = X^ [BAbt | e]' is (nx+1) x nz_{s-1}: one tile per wave covers it only with nx + 1 <= 32
+            // (nx = 32 would need a third tile row: those stages take the Cholesky route)
+            const bool pf = a.pform && small && nxs + 1 <= 32 && gtab[sI] - 1e-11 * emax > 1e-15;  // uniform
             auto M_product = [&](auto&& pxu, int t0, int nt) {  // M = Gamma_{s-1} pL_s[x,u] (+ the r row)
                 const float rr0 = 1.0f / r0;
                 for (int e = tid - t0; e < ((a.skip & 8) ? 0 : r0 * nus); e += nt) {

@@ -26,7 +26,9 @@
 #include "hk_wide_args.h"
 
 extern "C" int hk_launch(int which, const KArgs* a, int count, hipStream_t stream);
-extern "C" int hk_launch_ric2(int which, const KArgs* a, int count, hipStream_t stream);  // hk_ric2.hip
+#ifdef HK_RIC2  // the two-wave sv (hk_ric2.hip), a measured negative result: only in the ric2 build variant
+extern "C" int hk_launch_ric2(int which, const KArgs* a, int count, hipStream_t stream);
+#endif
 extern "C" int hk_fixcls(int nu, int nx);
 // wide-stage path (hpmpc_capi_wide.cpp, hpmpc_capi_wide_ipm.cpp)
 extern "C" long long hk_wide_ipm_bytes(int N, const int* nx, const int* nu, const int* nb, const int* ng);
@@ -59,10 +61,12 @@ enum { K_SV = 0, K_TRF = 1, K_TRS = 2, K_RES = 3, K_IPM = 4, K_KKT = 5, K_KKT_P1
 constexpr int FSTRIDE = 352, V16 = 16, V32 = 32, BS = 4, NCL = 2;
 
 // d_back_ric_rec_sv_tv_res runs the two-wave kernel (hk_ric2.hip: the tile recursion on one wave, fetch / row half /
-// stores on the other) when HPMPC_MI355X_RIC_WAVES=2 asks for it and its launch guard accepts the launch
-// (HK_LAUNCH_REFUSED = -2, hk_launch_guard.h); the one-wave kernel is the default: it measured faster at every batch
-// (DESIGN.md §4, round 5).  Every other entry point is hk_launch's.
+// stores on the other) when the library is the ric2 build variant (hpmpc_amd.build.build_ric2, -DHK_RIC2),
+// HPMPC_MI355X_RIC_WAVES=2 asks for it and its launch guard accepts the launch (HK_LAUNCH_REFUSED = -2,
+// hk_launch_guard.h).  The product library has the one-wave kernel only: it measured faster at every batch (DESIGN.md
+// §4, round 5).  Every other entry point is hk_launch's.
 int launch(int which, const KArgs* a, int count, hipStream_t s) {
+#ifdef HK_RIC2
     if (which == K_SV) {
         const char* e = getenv("HPMPC_MI355X_RIC_WAVES");
         if (e && e[0] == '2') {
@@ -70,6 +74,7 @@ int launch(int which, const KArgs* a, int count, hipStream_t s) {
             if (r != -2) return r;
         }
     }
+#endif
     return hk_launch(which, a, count, s);
 }
 
@@ -506,7 +511,8 @@ struct PollState {
     }
 };
 
-constexpr int kPollEvents = 2 * (8 * 4 + 1) + 2;  // enough for queue_run<R> with R <= 8
+constexpr int kPollEvents = 2 * (8 * 4 + 1) + 3;  // enough for queue_run<R> with R <= 8 (+1: after a drain)
+constexpr int HK_LAUNCH_REFUSED_H = -2;  // hk_launch_guard.h HK_LAUNCH_REFUSED
 
 PollState* poll_state(hipStream_t st) {
     thread_local std::vector<std::unique_ptr<PollState>> pool;
@@ -523,8 +529,8 @@ PollState* poll_state(hipStream_t st) {
         if (!hip_ok(hipEventCreate(&x), "event create")) return nullptr;
         p->e.push_back(x);
     }
-    if (!hip_ok(hipHostMalloc((void**)&p->hint, 2 * sizeof(int), hipHostMallocDefault), "host alloc")) return nullptr;
-    p->hint[0] = p->hint[1] = 0;
+    if (!hip_ok(hipHostMalloc((void**)&p->hint, 8 * sizeof(int), hipHostMallocDefault), "host alloc")) return nullptr;
+    for (int i = 0; i < 8; i++) p->hint[i] = 0;
     pool.push_back(std::move(p));
     return pool.back().get();
 }
@@ -534,7 +540,7 @@ PollState* poll_state(hipStream_t st) {
 // problem data and solver parameters; R ticks per chunk.
 template <int R>
 int queue_run(KArgs a, int nq, int n_slots, int* qctl, int k_max, double* pass_ms, int* n_ticks, hipStream_t st) {
-    static_assert(2 * (R * 4 + 1) + 2 <= kPollEvents, "poll pool sized for R <= 8");
+    static_assert(2 * (R * 4 + 1) + 3 <= kPollEvents, "poll pool sized for R <= 8");
     if (n_ticks) *n_ticks = 0;
     if (pass_ms)
         for (int i = 0; i < 5; i++) pass_ms[i] = 0.0;
@@ -583,7 +589,11 @@ int queue_run(KArgs a, int nq, int n_slots, int* qctl, int k_max, double* pass_m
     // least every k_max ticks, so this bound is never reached by a correct run
     const long cap = (long)k_max * ((nq + n_slots - 1) / n_slots + 1) + R;
     long ticks = 0;
-    bool pending = false;
+    bool pending = false, drained = false;
+    // the drain threshold (slots still iterating once the queue is empty): HPMPC_MI355X_QUEUE_DRAIN, default 256
+    // (one survivor per CU); 0 keeps the ticks to the end (results then bitwise the batched solve's)
+    int drain_max = 256;
+    if (const char* e = getenv("HPMPC_MI355X_QUEUE_DRAIN")) drain_max = atoi(e);
     for (int c = 0;; c++) {
         const int par = c & 1;
         hipEvent_t* e = &ev[par * nev];
@@ -596,13 +606,34 @@ int queue_run(KArgs a, int nq, int n_slots, int* qctl, int k_max, double* pass_m
             }
         }
         ticks += R;
-        if (!hip_ok(hipMemcpyAsync(&hdone[par], qctl + 1, sizeof(int), hipMemcpyDeviceToHost, st), "copy") ||
+        // per chunk parity: [4 par] finished, [4 par + 1] handed out, [4 par + 2 .. 3] the two active-list lengths
+        int* hc = &hdone[4 * par];
+        if (!hip_ok(hipMemcpyAsync(hc, qctl, 2 * sizeof(int), hipMemcpyDeviceToHost, st), "copy") ||
+            !hip_ok(hipMemcpyAsync(hc + 2, qctl + 2 + n_slots, 2 * sizeof(int), hipMemcpyDeviceToHost, st), "copy") ||
             !hip_ok(hipEventRecord(done_ev[par], st), "event record"))
             return g_err;
         if (pending) {  // look at the previous chunk while this one runs
             if (!hip_ok(hipEventSynchronize(done_ev[par ^ 1]), "event sync")) return g_err;
             if (pass_ms && !harvest(par ^ 1)) return g_err;
-            if (hdone[par ^ 1] >= nq) break;
+            const int* hp = &hdone[4 * (par ^ 1)];  // [0] handed out, [1] finished, [2 .. 3] list lengths
+            if (hp[1] >= nq) break;
+            // Drain: every entry handed out and at most drain_max slots still iterating (as of the previous chunk):
+            // the survivors finish in one multi-wave launch (hk_ipm_qdrain_mw) after the chunk just enqueued, on
+            // the active list its last update filled
+            const int nact = hp[2 + (int)((ticks - R) & 1)];
+            if (drain_max > 0 && hp[0] >= nq && nact <= drain_max) {
+                a.qpar = (int)(ticks & 1);
+                const int r = hk_launch(17, &a, n_slots, st);
+                if (r == 0) {
+                    drained = true;
+                    break;
+                }
+                if (r != HK_LAUNCH_REFUSED_H) {
+                    set_err(HPMPC_MI355X_EHIP, "hk_ipm_qdrain_mw launch failed");
+                    return g_err;
+                }
+                drain_max = 0;  // refused: keep ticking
+            }
         }
         pending = true;
         if (ticks >= cap) {
@@ -611,10 +642,19 @@ int queue_run(KArgs a, int nq, int n_slots, int* qctl, int k_max, double* pass_m
         }
     }
     // the chunk enqueued last finds every slot idle; profiled runs wait for it so that pass_ms covers
-    // every launch (n_ticks of each pass kernel), otherwise it completes on the stream
+    // every launch (n_ticks of each pass kernel), otherwise it completes on the stream.  A drain launch goes to
+    // pass_ms[0] with the init.
     if (pass_ms) {
         const int par = (int)((ticks / R - 1) & 1);
+        if (drained && !hip_ok(hipEventRecord(ev[2 * nev + 2], st), "event record")) return g_err;
         if (!hip_ok(hipEventSynchronize(done_ev[par]), "event sync") || !harvest(par)) return g_err;
+        if (drained) {
+            float ms = 0.f;
+            if (!hip_ok(hipEventSynchronize(ev[2 * nev + 2]), "event sync") ||
+                !hip_ok(hipEventElapsedTime(&ms, done_ev[par], ev[2 * nev + 2]), "event time"))
+                return g_err;
+            pass_ms[0] += ms;
+        }
     }
     if (n_ticks) *n_ticks = (int)ticks;
     return g_err = 0;

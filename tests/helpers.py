@@ -515,11 +515,13 @@ def check_case(case, got):
         assert e <= t, f"{case.name}: {key} err {e:.3e} > {t:.0e}"
 
 
-def random_qp(N, nx, nu, nb=None, seed=0, box=1.0, ng=None):
+def random_qp(N, nx, nu, nb=None, seed=0, box=1.0, ng=None, coupling=1.0):
     """Random well-posed OCP QP with per-stage sizes (lists of length N+1; nu[N] is forced to 0),
     random box subsets idxb (any variable order), SPD stage Hessians.  Exercises size patterns the
     mass-spring workload does not (odd sizes, nu > nx, varying stage sizes, x-only boxes).
-    ng: general constraints per stage, lg <= D ux <= ug with a random dense D (0 strictly feasible)."""
+    ng: general constraints per stage, lg <= D ux <= ug with a random dense D (0 strictly feasible).
+    coupling: scale of the off-identity part of the stage Hessians (small values: diagonally dominant data, on which
+    the clamp certificates hold)."""
     from hpmpc_amd.ocp import OCPQP, pack_lib4, rup
 
     rng = np.random.default_rng(seed)
@@ -540,7 +542,7 @@ def random_qp(N, nx, nu, nb=None, seed=0, box=1.0, ng=None):
             M[nux] = 0.3 * rng.standard_normal(nx1)
             BAbt.append(pack_lib4(M))
         G = rng.standard_normal((nux, nux))
-        H = G @ G.T / max(nux, 1) + np.eye(nux)
+        H = coupling * (G @ G.T) / max(nux, 1) + np.eye(nux)
         M = np.zeros((nux + 1, nux))
         M[:nux] = H
         M[nux] = 0.5 * rng.standard_normal(nux)
@@ -626,3 +628,14 @@ def parse_ric_driver(text):
             except ValueError:
                 cur = None
     return blocks
+
+
+def stack_qps(qps):
+    """A batch of single problems that share stage sizes and idxb."""
+    from hpmpc_amd.ocp import OCPQP
+
+    q0 = qps[0]
+    return OCPQP(q0.N, q0.nx.copy(), q0.nu.copy(), q0.nb.copy(), q0.ng.copy(), [i.copy() for i in q0.idxb],
+                 [np.stack([q.BAbt[k] for q in qps]) for k in range(q0.N)],
+                 [np.stack([q.RSQrq[k] for q in qps]) for k in range(q0.N + 1)],
+                 [np.stack([q.d[k] for q in qps]) for k in range(q0.N + 1)], [], len(qps))

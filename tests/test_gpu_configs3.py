@@ -20,6 +20,13 @@ N, NX, NU, WORLD, PER = 100, 12, 4, 8, 512
 SLOTS = max(2 * PER, 2048)
 
 
+@pytest.fixture(autouse=True)
+def _queue_ticks_to_the_end(monkeypatch):
+    """The rank block is compared bitwise with the world-1 batched solve: no multi-wave drain (test_gpu_parity.py
+    test_queue_drain_matches_oracle covers it)."""
+    monkeypatch.setenv("HPMPC_MI355X_QUEUE_DRAIN", "0")
+
+
 def _solve_queue(qp, nq):
     import torch
 

@@ -27,6 +27,14 @@ CASES = load_all()
 GATES = {int(c.args["problem"]): c for c in CASES if "gate" in c.args and "problem" in c.args}
 
 
+@pytest.fixture(autouse=True)
+def _queue_ticks_to_the_end(monkeypatch):
+    """Queue results in this module are compared bitwise with the batched solve, so the queue ticks to the end: the
+    multi-wave drain (hk_ipm_qdrain_mw, HPMPC_MI355X_QUEUE_DRAIN) agrees with it to rounding only, and
+    test_queue_drain_matches_oracle turns it back on."""
+    monkeypatch.setenv("HPMPC_MI355X_QUEUE_DRAIN", "0")
+
+
 @pytest.mark.parametrize("case", CASES, ids=[c.name for c in CASES])
 def test_golden_through_c_abi(product, case):
     check_case(case, run_case(product, case))
@@ -515,6 +523,63 @@ def test_queue_full_size_matches_batch():
     _queue_equals_batch(s, Q, 2048)
     # two batches back to back would take 2 x 50 iterations; the queue needs far fewer
     assert ticks < 100
+
+
+def test_queue_drain_matches_oracle(oracle, monkeypatch):
+    """The queue's drain: once every entry is handed out and at most HPMPC_MI355X_QUEUE_DRAIN slots still iterate,
+    the survivors finish on the multi-wave kernel (one four-wave workgroup each).  The benchmark workload, two batches
+    through 2048 slots: every entry's ret equals the batched solve's, entries that never reached the drain are bitwise
+    the batched solve, and every entry that finished in the drain (results to rounding: the multi-wave bodies contract
+    a few products differently, hk_mw.h) meets the CPU oracle at the IPM gate -- the headline's ill-conditioned
+    problems at their reference-spread gates (GATES), the others at max(TOL_IPM, 4 x the oracle's -mfma build spread)
+    (the GATES rule), a divergent infeasible draw by ret and kk +-2."""
+    import torch
+
+    from hpmpc_amd.batch import BatchSolver
+    from hpmpc_amd.cabi import HpmpcAPI, load
+    from hpmpc_amd.shard import make_shard
+
+    oracle_fma = HpmpcAPI(load(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle",
+                                            "liboracle_fma.so")), "orc_")
+    monkeypatch.setenv("HPMPC_MI355X_QUEUE_DRAIN", "256")
+    qp = make_shard(100, 12, 4, 0, 1, 1024)
+    s = BatchSolver(qp, k_max=50)
+    s.ipm()
+    Q = s.queue(2048, 2048)
+    pass_ms, ticks = Q.run(profiled=True)
+    torch.cuda.synchronize()
+    assert int(Q.qctl[1]) == 2048 and bool((Q.qctl[2:2 + 2048] == -1).all())
+    idx = torch.arange(2048, device=s.ux.device) % 1024
+    assert torch.equal(Q.ret, s.ret[idx])
+    same = torch.ones(2048, dtype=torch.bool, device=s.ux.device)
+    for n in ("ux", "pi", "lam", "t", "kk"):
+        a, b = getattr(Q, n), getattr(s, n)[idx]
+        same &= (a == b).reshape(2048, -1).all(dim=1)
+    drained = [int(q) for q in torch.nonzero(~same).flatten()]
+    assert 0 < len(drained) < 400, len(drained)  # the drain ran, on the survivors only
+    g = {n: getattr(Q, n).cpu().numpy() for n in ("ux", "pi", "lam", "t", "kk", "ret")}
+    for q in drained:
+        p = q % 1024
+        one = qp.problem(p)
+        got = dict(kk=int(g["kk"][q]), ret=int(g["ret"][q]), ux=[g["ux"][q, k] for k in range(101)],
+                   pi=[g["pi"][q, k] for k in range(100)], lam=[g["lam"][q, k] for k in range(101)],
+                   t=[g["t"][q, k] for k in range(101)])
+        if p in GATES:
+            c = GATES[p]
+            got["stat"] = Q.stat[q].cpu().numpy()[: c.out["stat"].size]
+            check_case(c, got)
+            continue
+        # the GATES rule: max(TOL_IPM, 4 x the oracle's own build spread on this problem) -- the drained problems are
+        # the batch's slowest (alpha_min and k_max exits), whose last Newton systems lift last bits the most
+        r = oracle.ipm(one.copy(), k_max=50)
+        lam_max = max(float(np.max(np.abs(x))) for x in r["lam"])
+        if r["ret"] == 1 and lam_max > 1e12:
+            # a divergence that runs into k_max before its step length falls below alpha_min (lam ~1e20): as for
+            # the ret-2 divergences (helpers.compare_ipm) only the exit is comparable -- same kk (k_max) and ret
+            assert (got["kk"], got["ret"]) == (r["kk"], r["ret"]), (p, got["kk"], got["ret"], r["kk"], r["ret"])
+            continue
+        spread = compare_ipm(one, oracle_fma.ipm(one.copy(), k_max=50), r, tol=float("inf"), allow_divergent=True)
+        compare_ipm(one, got, r, tol=max(TOL_IPM, 4 * spread), allow_divergent=True)
 
 
 def test_gate_problems_every_path():

@@ -337,3 +337,37 @@ def test_pcond_pform_matches_cholesky_route(coupled):
     for a, b in zip(*out):
         scale = float(b.abs().max()) or 1.0
         assert float((a - b).abs().max()) <= 1e-12 * scale
+
+
+def test_pcond_pform_wide_state_stage():
+    """A time-varying block whose stage s has nx_s = 32 after a stage with nu + nx = 30: the P form's
+    T = X^ [BAbt | e]' would need a third 16-row tile (nx + 1 = 33 rows), more than its one-tile-per-wave gemm covers,
+    so such a stage takes the Cholesky route; the condensed data match the Cholesky route everywhere to rounding."""
+    import os
+
+    import torch
+
+    from hpmpc_amd.pcond import PcondSolver
+    from helpers import random_qp, stack_qps as stack
+
+    N = 8
+    nx = [0, 24, 24, 32, 32, 24, 24, 24, 24]
+    nu = [6] * (N + 1)
+    qps = [random_qp(N, nx, nu, nb=[0] * (N + 1), seed=300 + i, coupling=0.05) for i in range(4)]
+    qp = stack(qps)
+    out = []
+    for pf in (None, "0"):
+        if pf is None:
+            os.environ.pop("HPMPC_MI355X_PCOND_PFORM", None)
+        else:
+            os.environ["HPMPC_MI355X_PCOND_PFORM"] = pf
+        try:
+            s = PcondSolver(qp, 2)
+            s.condense()
+            torch.cuda.synchronize()
+            out.append([t.clone() for t in (s.BAbt2, s.RSQrq2, s.d2)])
+        finally:
+            os.environ.pop("HPMPC_MI355X_PCOND_PFORM", None)
+    for a, b in zip(*out):
+        scale = float(b.abs().max()) or 1.0
+        assert float((a - b).abs().max()) <= 1e-12 * scale

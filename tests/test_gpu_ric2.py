@@ -9,35 +9,42 @@ oracle at TOL_RIC (1e-12 relative to max(1, |ref|)), on:
   * generic shapes (DynSh stages, full factor on stage 0 with nx[0] > 0), short horizons N = 1, 2, 3;
   * the reference's inner x-pivot clamp (xclamp_qp variants, the stages the clamp certificate rejects);
   * the aliased (time-invariant) layout.
-The one-wave kernel is the default (the two-wave one measured slower); test_sv_goldens_two_wave runs the
-sv goldens (update_b / update_q with box terms, the clamp goldens) through the drop-in entry point on the two-wave
-kernel."""
+The one-wave kernel is the product's (the two-wave one measured slower), and the two-wave kernel lives
+only in the ric2 build variant (hpmpc_amd.build.build_ric2, hpmpc_amd/lib/ab/libric2.so): test_two_wave_suite runs this
+module in a child process on that library (HPMPC_MI355X_LIB); the tests below run only there.  test_sv_goldens_two_wave
+runs the sv goldens (update_b / update_q with box terms, the clamp goldens) through the drop-in entry point on the
+two-wave kernel."""
 import os
+import subprocess
+import sys
 
 import numpy as np
 import pytest
 
-from helpers import TOL_RIC, random_qp, xclamp_qp
+from helpers import TOL_RIC, random_qp, stack_qps as stack, xclamp_qp
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+VARIANT = os.path.join(ROOT, "hpmpc_amd", "lib", "ab", "libric2.so")
+ON_VARIANT = os.path.abspath(os.environ.get("HPMPC_MI355X_LIB", "") or ".") == VARIANT
+variant_only = pytest.mark.skipif(not ON_VARIANT, reason="runs on the ric2 build variant (test_two_wave_suite)")
+
+
+@pytest.mark.skipif(ON_VARIANT, reason="the child process itself")
+def test_two_wave_suite():
+    """This module's tests on the ric2 variant library, in a child process (the product library has no two-wave sv)."""
+    assert os.path.exists(VARIANT), "build the variant: hpmpc_amd.build.build_ric2()"
+    env = dict(os.environ, HPMPC_MI355X_LIB=VARIANT)
+    r = subprocess.run([sys.executable, "-m", "pytest", os.path.abspath(__file__), "-m", "gpu", "-x", "-q",
+                        "-p", "no:cacheprovider"], env=env, cwd=ROOT, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
+    assert "11 passed" in r.stdout, r.stdout[-2000:]
 
 
 def _oracle():
     from hpmpc_amd.cabi import HpmpcAPI, load
 
     return HpmpcAPI(load(os.path.join(ROOT, "oracle", "liboracle.so")), "orc_")
-
-
-def stack(qps):
-    """A batch of single problems that share stage sizes and idxb."""
-    from hpmpc_amd.ocp import OCPQP
-
-    q0 = qps[0]
-    return OCPQP(q0.N, q0.nx.copy(), q0.nu.copy(), q0.nb.copy(), q0.ng.copy(), [i.copy() for i in q0.idxb],
-                 [np.stack([q.BAbt[k] for q in qps]) for k in range(q0.N)],
-                 [np.stack([q.RSQrq[k] for q in qps]) for k in range(q0.N + 1)],
-                 [np.stack([q.d[k] for q in qps]) for k in range(q0.N + 1)], [], len(qps))
 
 
 def run_sv(s, waves, **kw):
@@ -77,6 +84,7 @@ def check_oracle(qp, ux, pi, Pb, sample, tol=TOL_RIC):
     return worst
 
 
+@variant_only
 @pytest.mark.parametrize("N,nx,nu,batch", [(100, 12, 4, 1024), (50, 8, 3, 1024)])
 def test_two_wave_benchmark_shapes(N, nx, nu, batch):
     import torch
@@ -102,6 +110,7 @@ def test_two_wave_benchmark_shapes(N, nx, nu, batch):
     check_oracle(qp, ux2, pi2, Pb2, (0, 1, batch // 2 - 1, batch - 1))
 
 
+@variant_only
 @pytest.mark.parametrize("N,nx,nu", [(1, 6, 2), (2, 5, 3), (3, 12, 4), (20, 10, 3), (17, 7, 5), (30, 12, 3)])
 def test_two_wave_generic_shapes(N, nx, nu):
     from hpmpc_amd.batch import BatchSolver
@@ -118,6 +127,7 @@ def test_two_wave_generic_shapes(N, nx, nu):
     check_oracle(qp, ux2, pi2, Pb2, range(8))
 
 
+@variant_only
 def test_two_wave_clamp_variants():
     """Stages the clamp certificate rejects (the reference clamps an inner x pivot): the tile wave factorises the x
     block and hands the x factor over; the row wave adds its row half and p_eff."""
@@ -132,6 +142,7 @@ def test_two_wave_clamp_variants():
     check_oracle(qp, ux2, pi2, Pb2, range(len(variants)))
 
 
+@variant_only
 def test_two_wave_aliased_layout():
     import torch
 
@@ -148,6 +159,7 @@ def test_two_wave_aliased_layout():
     check_oracle(qp, *r_b, (0, 63))
 
 
+@variant_only
 def test_sv_goldens_two_wave(product):
     """The drop-in d_back_ric_rec_sv_tv_res on the two-wave kernel (HPMPC_MI355X_RIC_WAVES=2), every sv golden."""
     from hpmpc_amd.golden import load_all
