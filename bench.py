@@ -6,10 +6,11 @@ MPC QPs per GPU, N=100, nx=12, nu=4 (nb = 4 / 10 / 6 on stage 0 / inner / N), fp
 stage data (no aliased buffers), solved by the residual-based Mehrotra IPM
 (d_ip2_res_mpc_hard_tv: mu0=2, mu_tol=1e-12, alpha_min=1e-8, k_max=50).
 
-A "step" is one batch of 1024 problems (default K = 40 steps).  The K timed steps are solved through one problem queue
-(hpmpc_mi355x_ipm_queue): 2 x 1024 resident solver slots, each taking the next problem as soon as its
-own has converged (iterations are ticks of the pass kernels hk_ipm_fact, hk_ipm_pred, hk_ipm_corr,
-hk_ipm_update over all slots).  value = IP iterations per second over all ranks (sum of per-problem
+A "step" is one batch of 1024 problems (default K = 20 steps, the driver's count; the same line reports K = 40 in
+"k40").  The K timed steps are solved through one problem queue (hpmpc_mi355x_ipm_queue): 8 x 1024 resident solver
+slots, each taking the next problem as soon as its own has converged (iterations are ticks of the pass kernels
+hk_ipm_fact, hk_ipm_pred, hk_ipm_corr, hk_ipm_update over all slots; once the queue is empty and few slots still
+iterate, they finish on the multi-wave kernel hk_ipm_qdrain_mw).  value = IP iterations per second over all ranks (sum of per-problem
 iteration counts / max-over-ranks time).  The roofline object is for the dominant kernel (the pass
 with the largest device time per step, priced with that pass's own algorithmic bytes; `per_pass` lists
 all four), timed with hipEvents at every kernel boundary inside the timed region.  An isolated single-batch solve is reported beside it.
@@ -42,18 +43,18 @@ PEAK_FP64_TFS = 78.6   # MI355X fp64 (vector = MFMA dense)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # 40 batches: the queue's drain (the last problems, ~9 % of which run to k_max or alpha_min, finishing at one
-    # wave per SIMD) is a fixed cost per run; 40 batches amortise it towards the steady state of a continuously fed
-    # queue without hiding it (DESIGN.md §6 reports the K dependence)
-    ap.add_argument("--steps", type=int, default=40)
+    # 20 batches, the driver's count; the line also reports 40 batches ("k40": the queue's drain -- the last
+    # problems, ~9 % of which run to k_max or alpha_min -- is a fixed cost per run)
+    ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=1024, help="problems per GPU")
     ap.add_argument("--N", type=int, default=100)
     ap.add_argument("--nx", type=int, default=12)
     ap.add_argument("--nu", type=int, default=4)
     ap.add_argument("--k-max", type=int, default=50)
-    ap.add_argument("--slots", type=int, default=0, help="resident solver slots (default max(2 x batch, 2048): "
-                    "two problems per SIMD)")
+    ap.add_argument("--slots", type=int, default=0, help="resident solver slots (default max(8 x batch, 8192): "
+                    "two problems per SIMD resident, the rest dispatched as they finish; tools/slots_probe.py)")
+    ap.add_argument("--no-k40", action="store_true", help="skip the 40-batch queue run reported beside the headline")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-threads", type=int, default=16, help="host threads for the CPU baseline "
                     "(the GPU box's CPU share is 16 per GPU)")
@@ -737,7 +738,10 @@ def main():
     # K x (max iterations).  Profiled run: one hipEvent per kernel boundary on the solve's stream.
     # two resident problems per SIMD of the chip (256 CUs x 4 SIMDs): a per-GPU batch below 1024 (the strong-
     # scaling split of configs[3], 4096 over 8 GPUs = 512 per GPU) still fills every SIMD twice from the queue
-    slots = args.slots if args.slots > 0 else max(2 * B, 2048)
+    # more slots than the chip holds resident (2 per SIMD = 2048): each pass launch then dispatches the waiting slots
+    # as earlier ones finish, so a launch no longer waits for its slowest resident slot (tools/slots_probe.py: 2048 /
+    # 4096 / 6144 / 8192 slots 1.53 / 1.56 / 1.59 / 1.61 M IP-iter/s at K = 20 with the drain)
+    slots = args.slots if args.slots > 0 else max(8 * B, 8192)
     if args.warmup > 0:
         wq = solver.queue(args.warmup * B, slots)
         wq.run()
@@ -753,6 +757,7 @@ def main():
     kk = Q.kk.cpu().numpy()
     ret = Q.ret.cpu().numpy()
     iters_rank = float(kk.sum())
+    drain_iters, drain_probs = Q.drained()
     iters_total = sum_over_ranks(iters_rank)
     value = iters_total / dt
     names = ["hk_ipm_init", "hk_ipm_fact", "hk_ipm_pred", "hk_ipm_corr", "hk_ipm_update"]
@@ -761,7 +766,8 @@ def main():
     # (algorithmic_bytes_per_pass), over its average launch duration (both from this timed run)
     dom = 1 + int(np.argmax(pass_ms[1:]))
     bytes_pass = algorithmic_bytes_per_pass(qp)
-    probs_per_launch = iters_rank / ticks
+    # the problem-iterations the tick launches ran (the drain's own are not in the pass kernels)
+    probs_per_launch = (iters_rank - drain_iters) / ticks
     per_pass = {}
     for i in range(1, len(names)):
         lm = pass_ms[i] / ticks
@@ -779,6 +785,19 @@ def main():
     par_ipm = parity_ipm(ref, qp, dict(ux=Q.ux, pi=Q.pi, lam=Q.lam, t=Q.t, kk=Q.kk, ret=Q.ret, k_max=args.k_max),
                          [(q, q % B) for q in spread(8, nq)])
     del Q
+
+    # the same queue with 40 batches (the drain's fixed cost amortised over twice the work), beside the driver's K
+    k40 = None
+    if not args.no_k40 and args.steps != 40:
+        Q = solver.queue(40 * B, slots)
+        barrier()
+        q0 = time.perf_counter()
+        Q.run()
+        barrier()
+        qdt = max_over_ranks(time.perf_counter() - q0)
+        k40 = {"steps": 40, "value": sum_over_ranks(float(Q.kk.sum().item())) / qdt, "unit": "IP-iter/s",
+               "ms_per_step": qdt / 40 * 1e3}
+        del Q
 
     # the same K batches through a queue with one resident slot per problem of the batch (B slots: the
     # metric's literal batch resident at once), beside the headline's 2 x B slots
@@ -911,6 +930,8 @@ def main():
                          "frac": achieved / PEAK_HBM_GBS, "traffic": traffic, "kernel": names[dom],
                          "launch_ms": launch_ms, "launches": int(ticks),
                          "problem_iters_per_launch": probs_per_launch,
+                         "drain": {"kernel": "hk_ipm_qdrain_mw", "problems": drain_probs, "iterations": drain_iters,
+                                   "ms_with_init": float(pass_ms[0])},
                          "algorithmic_bytes_per_problem_iter": bytes_dom,
                          "per_pass": per_pass,
                          "pass_ms_per_step": {n: float(v / args.steps) for n, v in zip(names, pass_ms)},
@@ -921,6 +942,7 @@ def main():
                          "ipm_whole_solve": {"achieved_GBps": iters_rank * bytes_iter / (ipm_ms * 1e-3) / 1e9,
                                              "algorithmic_bytes_per_ip_iter": bytes_iter,
                                              "fp64_tflops": iters_rank * fl_iter / (ipm_ms * 1e-3) / 1e12}},
+            "k40": k40,
             "queue_batch_slots": qb,
             "aliased": ali,
             "coupled": cpl,

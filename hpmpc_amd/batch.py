@@ -417,7 +417,12 @@ class IpmQueue:
         self.ret = torch.zeros(nq, dtype=torch.int32, device=dev)
         self.stat = torch.zeros((nq, 5 * solver.k_max), dtype=f64, device=dev)
         self.ws = torch.zeros((n_slots, solver.wsd), dtype=f64, device=dev)
-        self.qctl = torch.zeros(4 + 3 * n_slots, dtype=torch.int32, device=dev)  # include/hpmpc_mi355x.h
+        self.qctl = torch.zeros(6 + 3 * n_slots, dtype=torch.int32, device=dev)  # include/hpmpc_mi355x.h
+
+    def drained(self):
+        """(iterations, problems) the multi-wave drain finished in the last run (read after a synchronise)."""
+        ns = self.n_slots
+        return int(self.qctl[4 + 3 * ns].item()), int(self.qctl[5 + 3 * ns].item())
 
     def run(self, *, mu0=2.0, mu_tol=1e-12, alpha_min=1e-8, warm_start=0, compute_mult=1, profiled=False):
         """Solve every entry.  Returns (pass_ms[5] or None, ticks).  Polls the device once per chunk;

@@ -574,7 +574,8 @@ int queue_run(KArgs a, int nq, int n_slots, int* qctl, int k_max, double* pass_m
         return true;
     };
     if (!hip_ok(hipMemsetAsync(qctl, 0, 2 * sizeof(int), st), "memset") ||
-        !hip_ok(hipMemsetAsync(qctl + 2 + n_slots, 0, 2 * sizeof(int), st), "memset"))
+        !hip_ok(hipMemsetAsync(qctl + 2 + n_slots, 0, 2 * sizeof(int), st), "memset") ||
+        !hip_ok(hipMemsetAsync(qctl + 4 + 3 * n_slots, 0, 2 * sizeof(int), st), "memset"))
         return g_err;
     if (pass_ms && !hip_ok(hipEventRecord(ev[0], st), "event record")) return g_err;
     if (!launch(10)) return g_err;
@@ -590,9 +591,11 @@ int queue_run(KArgs a, int nq, int n_slots, int* qctl, int k_max, double* pass_m
     const long cap = (long)k_max * ((nq + n_slots - 1) / n_slots + 1) + R;
     long ticks = 0;
     bool pending = false, drained = false;
-    // the drain threshold (slots still iterating once the queue is empty): HPMPC_MI355X_QUEUE_DRAIN, default 256
-    // (one survivor per CU); 0 keeps the ticks to the end (results then bitwise the batched solve's)
-    int drain_max = 256;
+    // the drain threshold (slots still iterating once the queue is empty): HPMPC_MI355X_QUEUE_DRAIN, default 768
+    // (tools/slots_probe.py: 512 / 768 / 1024 / 1536 within 1 % at 6144-8192 slots; the host looks one chunk
+    // behind, so fewer survivors are left when the drain starts); 0 keeps the ticks to the end (results then
+    // bitwise the batched solve's)
+    int drain_max = 768;
     if (const char* e = getenv("HPMPC_MI355X_QUEUE_DRAIN")) drain_max = atoi(e);
     for (int c = 0;; c++) {
         const int par = c & 1;
@@ -850,7 +853,7 @@ Arena arena(const hpmpc_mi355x_plan* P, int k_max) {
     A.vPb = take(n1 * V16);
     A.stat = take(5 * (size_t)(k_max > 0 ? k_max : 1) + 8);
     A.ints = take(8);
-    A.qctl = take(8);  // queue control of the one-entry queue the IPM entry points run (16 ints >= 4 + 3 slots)
+    A.qctl = take(8);  // queue control of the one-entry queue the IPM entry points run (16 ints >= 6 + 3 slots)
     A.total = o;
     return A;
 }

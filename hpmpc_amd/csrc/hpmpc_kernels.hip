@@ -460,11 +460,16 @@ __global__ __launch_bounds__(256) void hk_ipm_qdrain_mw(KArgs a) {
     if ((int)blockIdx.x >= n) return;
     const int s = __builtin_amdgcn_readfirstlane(qlist(a, a.qpar)[blockIdx.x]);
     const int q = __builtin_amdgcn_readfirstlane(a.qctl[2 + s]);
-    if (q < 0 || carve(a.ws + (long)s * a.sW, a.N).state[S_ACTIVE] == 0.0) return;
+    const double* st = carve(a.ws + (long)s * a.sW, a.N).state;
+    if (q < 0 || st[S_ACTIVE] == 0.0) return;
+    const int kk0 = (int)st[S_KK];
+    __syncthreads();  // every wave has read the state before the solve rewrites it
     mw_solve<FX>(a, T, Who{s, q, q % a.nprob});
     __syncthreads();
     if (threadIdx.x == 0) {
         a.qctl[2 + s] = -1;
+        atomicAdd(&a.qctl[4 + 3 * a.nslots], a.kk[q] - kk0);  // the drain's iterations and problems
+        atomicAdd(&a.qctl[5 + 3 * a.nslots], 1);
         atomicAdd(&a.qctl[1], 1);
     }
 }

@@ -329,16 +329,21 @@ int hpmpc_mi355x_ipm_batch_profiled(const hpmpc_mi355x_plan *plan, const hpmpc_m
 /* Problem queue (continuous batching): solve nq problems with n_slots resident solver slots.  Queue
  * entry q solves data problem q % nprob (BAbt/RSQrq/d as in hpmpc_mi355x_ipm_batch, nprob problems);
  * ux/pi/lam/t/kk/ret/stat are per queue entry (nq of each, same strides); ws holds n_slots
- * workspaces; qctl is device scratch of 4 + 3 * n_slots ints (counters, the entry each slot holds, and two
+ * workspaces; qctl is device scratch of 6 + 3 * n_slots ints (counters, the entry each slot holds, two
  * lists of the slots that iterate: workgroup i of an iteration runs the i-th listed slot, so a draining queue
- * keeps one slot per SIMD).  A slot whose problem has finished takes
+ * keeps one slot per SIMD; and at [4 + 3 n_slots] / [5 + 3 n_slots] the iterations / problems the drain
+ * finished).  A slot whose problem has finished takes
  * the next entry at the following iteration, so the GPU is not left idle behind the slowest problem
- * of a batch.  Results are those of hpmpc_mi355x_ipm_batch on each entry (the per-slot workspace is
- * reused, so a queue solve leaves no factor behind for d_kkt_solve_new_rhs_res_mpc_hard_tv; for the same
- * reason its update pass writes neither the iterate backups nor r_m, which only that re-solve reads).
+ * of a batch.  Drain: once every entry is handed out and at most HPMPC_MI355X_QUEUE_DRAIN (environment,
+ * default 768) slots still iterate, the survivors finish one per four-wave workgroup (the multi-wave body of
+ * hpmpc_mi355x_ipm_solo) in one launch.  Results are those of hpmpc_mi355x_ipm_batch on each entry: bitwise
+ * for the entries finished by the iteration passes (all of them with HPMPC_MI355X_QUEUE_DRAIN=0), to rounding
+ * for those finished in the drain (the multi-wave bodies contract a few products differently).  The per-slot
+ * workspace is reused, so a queue solve leaves no factor behind for d_kkt_solve_new_rhs_res_mpc_hard_tv; for
+ * the same reason its update pass writes neither the iterate backups nor r_m, which only that re-solve reads.
  * Synchronises with the device once per chunk of iterations (it polls the finished counter); on
  * return the last chunk may still be running on `stream`.  pass_ms (nullable): device time of
- * [init, fact, pred, corr, update] summed over the run; n_ticks (nullable): iterations enqueued. */
+ * [init + drain, fact, pred, corr, update] summed over the run; n_ticks (nullable): iterations enqueued. */
 int hpmpc_mi355x_ipm_queue(const hpmpc_mi355x_plan *plan, const hpmpc_mi355x_layout *lay, int nprob, int nq,
                            int n_slots, const double *BAbt, const double *RSQrq, const double *d, double *ux,
                            double *pi, double *lam, double *t, double *ws, int *qctl, int k_max, double mu0,
