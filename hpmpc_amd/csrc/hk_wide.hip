@@ -188,16 +188,63 @@ __global__ __launch_bounds__(WT, GM <= 4 ? 4 : 2) void hk_pcond(PcArgs a) {  // 
     // held in registers, then overwrites GA and streams to HBM ----
     double* GA = sm + a.offGA;
     const int ph = a.ph;
+    // Deferred cross terms (full condensing only): d_cond_RSQrq runs first and leaves, per stage s, the operand of its
+    // cross term M_s = Gamma_{s-1} pL_s[x, u] (the (nx_s + 1) x nu_s u columns of pL_s: x rows and gradient row) in the
+    // scratch; d_cond_BAbt runs second and forms M_s, and the general constraints of stage s (d_cond_DCtd), while
+    // Gamma_{s-1} is in LDS.  No Gamma goes through HBM (the scratch carries ~(nx + 1) nu doubles per stage instead of
+    // a Gamma of (sum nu + nx + 1) x nx), and every value is formed by the same operations on the same operands.
+    const bool dm = ph == PC_ALL && a.dm;
+    int* I = reinterpret_cast<int*>(sm);  // d_cond_DCtd's bookkeeping (the LDS tiles are free when it runs)
+    int *cU = I, *cX = I + T, *iob = I + 2 * T, *iog = I + 3 * T, *ntmp = I + 4 * T, *igb = I + 5 * T;
+    int* gd = I + 6 * T;  // general constraint ig: (stage << 16) | state index g
+    int* gj = gd + blk.ng2;  // ... and its box index in the stage (dm)
+    auto soff = [&](int sI) {  // dm: stage sI's cross-term operand in the scratch, (nx + 1) x nu, ld nx + 1
+        int o = 0;
+        for (int r = 1; r < sI; r++) o += (st[r].nx + 1) * st[r].nu;
+        return o;
+    };
+    // dm: stage s's cross term from Gamma_{s-1} (in GA, leading dimension r0 = rows(s-1)) and the general constraints
+    // of its state boxes (DCt2 columns and the bounds' constant terms), as d_cond_RSQrq's M_product and d_cond_DCtd
+    // form them from the scratch Gammas
+    auto dm_stage = [&](int sI, int r0) __attribute__((always_inline)) {
+        const WideStage q = st[sI];
+        const int nus = q.nu, nxs = q.nx, ldS = nxs + 1;
+        const double* Ss = G + soff(sI);
+        for (int e = tid; e < ldS * nus; e += WT) Ucol[e] = Ss[e];
+        lds_bar();
+        const int os = ntmp[sI] - nus;
+        const float rr0 = 1.0f / r0;
+        for (int e = tid; e < ((a.skip & 8) ? 0 : r0 * nus); e += WT) {
+            const int c = fdiv(e, rr0), i = e - c * r0;
+            double acc = 0.0;
+            for (int l = 0; l < nxs; l++) acc += GA[i + l * r0] * Ucol[l + c * ldS];
+            if (i == r0 - 1) acc += Ucol[nxs + c * ldS];
+            *P4w(R2, (nv + 1) / 2 * 2, os + nus + i, os + c) = acc;
+        }
+        const int nbb = blk.nb2, nbg = blk.ng2, pnbb = (nbb + 3) / 4 * 4, pnbg = (nbg + 3) / 4 * 4;
+        const int cnbg = (nbg + 1) / 2 * 2, rowsI = igb[sI], nt = ntmp[sI];
+        const int wv = tid >> 6, ln = tid & 63;
+        for (int ig = iog[sI] + wv; ig < iog[sI] + cX[sI]; ig += WT / 64) {
+            const int g = gd[ig] & 0xffff, jj = gj[ig];
+            for (int i = ln; i < rowsI; i += 64) *P4w(G2, cnbg, nt + i, ig) = GA[i + g * r0];
+            if (ln == 0) {
+                const double c0 = GA[rowsI + g * r0];
+                d2[2 * pnbb + ig] = dv[q.oD + jj] - c0;
+                d2[2 * pnbb + pnbg + ig] = dv[q.oD + q.pnb + jj] - c0;
+            }
+        }
+    };
     PST_DECL;
     PST(0);
-    if (ph & PC_BABT) {
+    auto babt_phase = [&]() __attribute__((always_inline)) {
     {
         const WideStage s = st[0];
         const int r0 = s.nu + s.nx + 1;
         load_dense<8>(GA, r0, BAbt + s.oB, s.sdB, r0, s.nx1);
         lds_bar();
-        if (T > 1 || (ph & PC_PART))
+        if (!dm && (T > 1 || (ph & PC_PART)))
             for (int e = tid; e < r0 * s.nx1; e += WT) G[e] = GA[e];
+        if (dm && T > 1) dm_stage(1, r0);
     }
     // BAbt_{j+1} is loaded into registers while Gamma_j is formed (Staged), and stored into LDS at the top of the
     // next step: one memory round trip per block instead of one per stage
@@ -210,7 +257,7 @@ __global__ __launch_bounds__(WT, GM <= 4 ? 4 : 2) void hk_pcond(PcArgs a) {  // 
         const int rj = rp + nuj, n = rj * nx1;
         double* Gj = G + go;
         // the later phases read Gamma_0 .. Gamma_{T-2}; Gamma_{T-1} only goes to B2 (d_cond_BAbt alone returns all)
-        const bool keep = j < T - 1 || (ph & PC_PART);
+        const bool keep = !dm && (j < T - 1 || (ph & PC_PART));
         PST(1);
         if (staged)
             put_dense(nb, Bt, ldB);
@@ -253,6 +300,7 @@ __global__ __launch_bounds__(WT, GM <= 4 ? 4 : 2) void hk_pcond(PcArgs a) {  // 
         (void)n;
         lds_bar();
         PST(3);
+        if (dm && j + 1 < T) dm_stage(j + 1, rj);
         rp = rj;
         go += rj * nx1;
     }
@@ -265,7 +313,8 @@ __global__ __launch_bounds__(WT, GM <= 4 ? 4 : 2) void hk_pcond(PcArgs a) {  // 
             *P4w(B2, sd, i, c) = GA[i + c * rT];
         }
     }
-    }  // PC_BABT
+    };  // babt_phase
+    if ((ph & PC_BABT) && !dm) babt_phase();
     bar();  // Gamma scratch complete (written by this block's threads) before the later phases read it
     PST(4);
 
@@ -345,7 +394,7 @@ __global__ __launch_bounds__(WT, GM <= 4 ? 4 : 2) void hk_pcond(PcArgs a) {  // 
         {
             const WideStage s = st[T - 1], sp = st[T - 2];
             dma_copy<WT, 16>(Pl, RSQ + s.oR, lib4n(s, s.sdR), tid);
-            dma_copy_any<WT>(GA, G + g1, r1 * s.nx, tid);
+            if (!dm) dma_copy_any<WT>(GA, G + g1, r1 * s.nx, tid);
             nbk = dma_copy<WT, 16>(Bt, BAbt + sp.oB, lib4n(sp, sp.sdB), tid);
         }
         for (int sI = (a.skip & 2) ? 0 : T - 1;; sI--) {
@@ -386,6 +435,13 @@ __global__ __launch_bounds__(WT, GM <= 4 ? 4 : 2) void hk_pcond(PcArgs a) {  // 
                     *P4w(R2, cnux2, os + nus + i, os + c) = acc;
                 }
             };
+            auto M_store = [&](auto&& pxu, int t0, int nt) {  // dm: the cross term's operand to the scratch
+                double* Ss = G + soff(sI);
+                for (int e = tid - t0; e < (nxs + 1) * nus; e += nt) {
+                    const int c = e / (nxs + 1), l = e - c * (nxs + 1);
+                    Ss[e] = pxu(l, c);
+                }
+            };
             PST(5);
             int ngm = 0;
             if (pf) {
@@ -423,11 +479,14 @@ __global__ __launch_bounds__(WT, GM <= 4 ? 4 : 2) void hk_pcond(PcArgs a) {  // 
                 PST(6);
                 // every read of pL_s is done: RSQrq_{s-1} into its buffer
                 dma_copy<WT, 16>(Pl, RSQ + sp.oR, lib4n(sp, sdQ), tid);
-                M_product([&](int l, int c) { return Ucol[l + c * ldU]; }, 0, WT);
+                if (dm)
+                    M_store([&](int l, int c) { return Ucol[l + c * ldU]; }, 0, WT);
+                else
+                    M_product([&](int l, int c) { return Ucol[l + c * ldU]; }, 0, WT);
                 dma_wait();
                 lds_bar();  // M is done (GA free), RSQrq_{s-1} and T are in LDS
                 PST(7);
-                ngm = sI >= 2 ? dma_copy_any<WT>(GA, G + g2, r2 * sp.nx, tid) : 0;
+                ngm = (sI >= 2 && !dm) ? dma_copy_any<WT>(GA, G + g2, r2 * sp.nx, tid) : 0;
                 PST(13);
                 mfma_gemm<1, 8>(
                     nzp, nuxp, nxs, [&](int i, int l) { return BT(sdB, i, l); },
@@ -461,14 +520,17 @@ __global__ __launch_bounds__(WT, GM <= 4 ? 4 : 2) void hk_pcond(PcArgs a) {  // 
                         xchol_rows(X, ldX, nxs);
                 }
             } else {
-                M_product([&](int l, int c) { return PL(sdP, nus + l, c); }, 64, WT - 64);
+                if (dm)
+                    M_store([&](int l, int c) { return PL(sdP, nus + l, c); }, 64, WT - 64);
+                else
+                    M_product([&](int l, int c) { return PL(sdP, nus + l, c); }, 64, WT - 64);
             }
             dma_wait();  // BAbt_{s-1} has landed
             lds_bar();       // pL and GA are read until here
             // RSQrq_{s-1} into pL and Gamma_{s-2} into GA while W = BAbt_{s-1} Lx (+ l on the last row) forms in place
             // over BAbt_{s-1}; then pL += W W' (lower); both products on MFMA
             dma_copy<WT, 16>(Pl, RSQ + sp.oR, lib4n(sp, sp.sdR), tid);
-            ngm = sI >= 2 ? dma_copy_any<WT>(GA, G + g2, r2 * sp.nx, tid) : 0;
+            ngm = (sI >= 2 && !dm) ? dma_copy_any<WT>(GA, G + g2, r2 * sp.nx, tid) : 0;
             auto wa = [&](int i, int l) { return BT(sdB, i, l); };
             auto wb = [&](int l, int c) {
                 const double v = X[l + c * ldX];
@@ -524,9 +586,6 @@ __global__ __launch_bounds__(WT, GM <= 4 ? 4 : 2) void hk_pcond(PcArgs a) {  // 
         const int cnbg = (nbg + 1) / 2 * 2, pnv = (nv + 3) / 4 * 4;
         const int wv = tid >> 6, ln = tid & 63;
         const unsigned long long below = (1ull << ln) - 1ull;
-        int* I = reinterpret_cast<int*>(sm);
-        int *cU = I, *cX = I + T, *iob = I + 2 * T, *iog = I + 3 * T, *ntmp = I + 4 * T, *igb = I + 5 * T;
-        int* gd = I + 6 * T;  // general constraint ig: (stage << 16) | state index g
         bar();                // the RSQ phase's last LDS reads are done
         if (!(ph & PC_PART))
             for (int e = tid; e < 2 * pnbb + 2 * pnbg; e += WT) d2[e] = 0.0;
@@ -570,7 +629,7 @@ __global__ __launch_bounds__(WT, GM <= 4 ? 4 : 2) void hk_pcond(PcArgs a) {  // 
         for (int sI = wv; sI < T; sI += WT / 64) {
             const WideStage s = st[sI];
             const int r0 = sI > 0 ? igb[sI] + 1 : 0, gb = igb[sI];
-            const double* Gp = sI > 0 ? G + goff(sI - 1) : nullptr;
+            const double* Gp = (sI > 0 && !dm) ? G + goff(sI - 1) : nullptr;
             int rU = iob[sI], rX = iog[sI];
             for (int j0 = 0; j0 < s.nb; j0 += 64) {
                 const int jj = j0 + ln;
@@ -586,10 +645,13 @@ __global__ __launch_bounds__(WT, GM <= 4 ? 4 : 2) void hk_pcond(PcArgs a) {  // 
                 }
                 if (isg) {
                     const int ig = rX + __popcll(mg & below), g = vv - s.nu;
-                    const double c0 = Gp[gb + g * r0];
-                    d2[2 * pnbb + ig] = dv[s.oD + jj] - c0;
-                    d2[2 * pnbb + pnbg + ig] = dv[s.oD + s.pnb + jj] - c0;
+                    if (!dm) {  // dm: the bounds' constant terms come with Gamma_{s-1} (dm_stage)
+                        const double c0 = Gp[gb + g * r0];
+                        d2[2 * pnbb + ig] = dv[s.oD + jj] - c0;
+                        d2[2 * pnbb + pnbg + ig] = dv[s.oD + s.pnb + jj] - c0;
+                    }
                     gd[ig] = (sI << 16) | g;
+                    gj[ig] = jj;
                 }
                 rU += __popcll(mb);
                 rX += __popcll(mg);
@@ -607,11 +669,15 @@ __global__ __launch_bounds__(WT, GM <= 4 ? 4 : 2) void hk_pcond(PcArgs a) {  // 
                 }
                 if (z) G2[e] = 0.0;
             }
-        for (int ig = wv; ig < nbg; ig += WT / 64) {  // DCt2 column ig: rows nu_tmp + i <- Gamma_{s-1}(i, g)
+        for (int ig = wv; ig < (dm ? 0 : nbg); ig += WT / 64) {  // DCt2 column ig: rows nu_tmp + i <- Gamma_{s-1}(i, g)
             const int sI = gd[ig] >> 16, g = gd[ig] & 0xffff, rowsI = igb[sI], r0 = rowsI + 1, nt = ntmp[sI];
             const double* Gp = G + goff(sI - 1);
             for (int i = ln; i < rowsI; i += 64) *P4w(G2, cnbg, nt + i, ig) = Gp[i + g * r0];
         }
+    }
+    if (dm) {  // d_cond_BAbt last: Gamma_j in LDS forms the cross terms and general constraints of stage j + 1
+        bar();  // the bookkeeping and the cross-term operands in the scratch are complete
+        babt_phase();
     }
     PST(10);
     // the terminal condensed stage is the original's (d_part_cond.c:1052-1056): block N2-1 copies it

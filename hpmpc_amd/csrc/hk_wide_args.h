@@ -92,6 +92,7 @@ struct PcArgs {
     // contents stay where the reference writes nothing) and the terminal stage is not copied
     int ph;
     int gm;  // output tiles per wave of the kernel's gemms (4 or 8: the hk_pcond instance)
+    int dm;  // full condensing (PC_ALL): d_cond_RSQrq first, the cross terms deferred to d_cond_BAbt (hk_pcond)
 };
 enum { PC_BABT = 1, PC_RSQ = 2, PC_DCTD = 4, PC_ALL = 7, PC_PART = 8 };
 

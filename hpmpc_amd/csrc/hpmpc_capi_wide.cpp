@@ -284,6 +284,7 @@ struct PcPlan {
     int offU = 0;   // hk_pcond's P-form u columns
     int offGT = 0;  // hk_pcond's P-form certificate bounds
     bool pform_ok = true;
+    bool pc_dm_ok = true;  // hk_pcond's deferred cross terms fit the Gamma scratch
 };
 
 void problem_size(int N, const int* nx, const int* nu, const int* nb, const int* const* hidxb, const int* ng, int N2,
@@ -348,14 +349,17 @@ bool pc_plan(PcPlan& P, int N, const int* nx, const int* nu_in, const int* nb, c
         b.nut = 0;
         b.oG = (int)P.nG;
         int rows = b.nx0 + 1;
+        long long sneed = 0;  // hk_pcond's deferred cross terms: (nx_s + 1) x nu_s per stage s >= 1 of the block
         for (int j = 0; j < b.T; j++) {
             const int s = N_tmp + j;
             b.nut += nu[s];
             rows += nu[s];
             P.nG += (long long)rows * nx[s + 1];
+            if (j > 0) sneed += (long long)(nx[s] + 1) * nu[s];
             nzM = std::max(nzM, nu[s] + nx[s] + 1);
             nxM = std::max(nxM, nx[s + 1]);
         }
+        if (sneed > P.nG - b.oG) P.pc_dm_ok = false;  // the block's Gamma scratch holds them (it always does at nu <= nx)
         b.oB2 = P.cond.st[ii].oB;
         b.oR2 = P.cond.st[ii].oR;
         b.oD2 = P.cond.st[ii].oD;
@@ -499,6 +503,10 @@ void fill_pc_args(const PcPlan& P, PcArgs& a) {
     const char* pf = getenv("HPMPC_MI355X_PCOND_PFORM");
     a.pform = P.pform_ok && (pf ? atoi(pf) : 1);
     a.offGT = P.offGT;
+    // d_cond_RSQrq before d_cond_BAbt with the cross terms deferred (no Gamma through HBM) unless
+    // HPMPC_MI355X_PCOND_DM=0 (read per call: tests compare the two orders bitwise)
+    const char* dmv = getenv("HPMPC_MI355X_PCOND_DM");
+    a.dm = P.pc_dm_ok && (dmv ? atoi(dmv) : 1);
 }
 
 void fill_px_args(const PcPlan& P, PxArgs& a) {

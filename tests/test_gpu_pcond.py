@@ -371,3 +371,41 @@ def test_pcond_pform_wide_state_stage():
     for a, b in zip(*out):
         scale = float(b.abs().max()) or 1.0
         assert float((a - b).abs().max()) <= 1e-12 * scale
+
+
+@pytest.mark.parametrize("shape", ["bench", "coupled", "tv"])
+def test_pcond_deferred_cross_terms_bitwise(shape):
+    """hk_pcond's full condensing runs d_cond_RSQrq first and forms each stage's cross term M_s = Gamma_{s-1} pL_s[x, u]
+    and its general constraints later, while d_cond_BAbt has Gamma_{s-1} in LDS (no Gamma through the HBM scratch).  Same
+    operations on the same operands as the reference's order (HPMPC_MI355X_PCOND_DM=0): the condensed problem is bitwise
+    the same, on the benchmark data, on coupled stage Hessians (Cholesky route) and with time-varying stage sizes."""
+    import os
+
+    import torch
+
+    from hpmpc_amd.pcond import PcondSolver
+    from hpmpc_amd.shard import coupled_shard, make_shard
+    from helpers import stack_qps
+
+    if shape == "bench":
+        qp, N2 = make_shard(60, 24, 6, 0, 1, 16, boxes=True), 6
+    elif shape == "coupled":
+        qp, N2 = coupled_shard(60, 24, 6, 0, 1, 16, boxes=True), 6
+    else:
+        N = 13
+        nx = [0, 5, 9, 24, 7, 12, 12, 3, 16, 10, 8, 8, 20, 6]
+        nu = [3, 2, 6, 1, 4, 4, 5, 2, 3, 6, 2, 3, 1, 0]
+        nb = [2, 4, 8, 3, 5, 9, 7, 2, 6, 8, 4, 5, 9, 3]
+        qp, N2 = stack_qps([random_qp(N, nx, nu, nb=nb, seed=700 + i, coupling=0.1) for i in range(6)]), 4
+    out = []
+    for dm in ("1", "0"):
+        os.environ["HPMPC_MI355X_PCOND_DM"] = dm
+        try:
+            s = PcondSolver(qp, N2)
+            s.condense()
+            torch.cuda.synchronize()
+            out.append([t.clone() for t in (s.BAbt2, s.RSQrq2, s.DCt2, s.d2)])
+        finally:
+            os.environ.pop("HPMPC_MI355X_PCOND_DM", None)
+    for name, a, b in zip(("BAbt2", "RSQrq2", "DCt2", "d2"), *out):
+        assert torch.equal(a, b), name
