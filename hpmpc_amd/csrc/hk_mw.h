@@ -292,9 +292,8 @@ __device__ __forceinline__ int ric_backward_mw(const RicIO& io, int tb, int w, i
                 MW_SEG(1);
                 double mld = 0.0;
                 const bool full = !SHT::fixed && k == 0;
-                // gc: the threshold tau on tr(P_{k+1}) (cert_tau), tested on the record the stage starts from (P), off
-                // the MFMA products' chain (round 4 tested M after the tile update, on the chain: ~450 ticks a step)
-                xfac = !full && !cert_test(P, M, sh.xo1, dq, gc);
+                // gc: the threshold T_k, tested on M after the tile update (cert_ok_thr)
+                xfac = !full && !cert_test(M, dq, gc);
                 stage_chol<false, false>(M, mld, invd, sh.nu, sh.nx, sh.xo, full, !SHT::fixed, nullptr, k, xfac, &xf);
                 MW_SEG(2);
             });

@@ -34,18 +34,7 @@ __device__ int g_dbg_stage;
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-// HK_OPAQUE_LANE: the lane index is re-derived behind an empty asm at every call, so lane-dependent
-// masks and constants are recomputed where they are used instead of being hoisted out of the stage
-// loops into registers (fewer VGPRs, more instructions).
-#ifdef HK_OPAQUE_LANE
-__device__ __forceinline__ int lane_id() {
-    int l = threadIdx.x & 63;
-    asm volatile("" : "+v"(l));
-    return l;
-}
-#else
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
-#endif
 
 __device__ __forceinline__ double mk(int hi, int lo) { return __hiloint2double(hi, lo); }
 

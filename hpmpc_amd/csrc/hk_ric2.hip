@@ -180,7 +180,7 @@ __device__ __forceinline__ void ric_backward2(const RicIO& io, int w, int update
                     bwd_tile_update(sh, SHT::fixed || k < N, bop, P, M);
                     double mld = 0.0;
                     const bool full = !SHT::fixed && k == 0;
-                    xfac = !full && !cert_test(P, M, sh.xo1, dq, gc);  // gc: cert_form's tau_k or T_k
+                    xfac = !full && !cert_test(M, dq, gc);  // gc: cert_form's T_k
                     R2_T0(ts2);
                     stage_chol<false, false>(M, mld, invd, sh.nu, sh.nx, sh.xo, full, !SHT::fixed, nullptr, k, xfac,
                                              &xf);

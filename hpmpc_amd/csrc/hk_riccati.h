@@ -56,24 +56,6 @@ __device__ __forceinline__ int lib4_idx(int sd, int i, int j) { return (i >> 2) 
 // counted s_waitcnt vmcnt(N) instead of draining the whole prefetch queue.
 __device__ __forceinline__ double ldsel(const double* p, int idx, bool ok) { return gld(p, idx, ok); }
 
-// HK_WIDE_BOP (an A/B build): two tile registers of a lib4 operand whose lane (g, c) element is
-// (row c, column j_r) -- the BAbt operand of the compiled (4, 12) class, where tile index = variable -- fetched with
-// one 16-B load per lane instead of two 8-B ones: rows c and c+1 of a column are 16 contiguous bytes (c even), so the
-// even lane of each pair loads column ja's pair, the odd lane column jb's, and they swap the half the other needs
-// (DPP quad_perm [1,0,3,2]).  oka / okb: this lane's elements exist (column in range; rows always are).
-__device__ __forceinline__ void ld_pair16(const double* B, int sd, int c, int ja, int jb, bool oka, bool okb,
-                                          double& va, double& vb) {
-    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
-    const bool odd = (c & 1) != 0;
-    const int j = odd ? jb : ja;
-    const int off = (odd ? okb : oka) ? lib4_idx(sd, c & ~1, j) * 8 : (int)0xFFFFFFF0;
-    const u4 q = __builtin_amdgcn_raw_buffer_load_b128(rsrc(B), off, 0, 0);
-    const double d0 = mk((int)q[1], (int)q[0]), d1 = mk((int)q[3], (int)q[2]);
-    const double recv = dpp_mov<0xB1>(odd ? d0 : d1);  // quad_perm [1,0,3,2]: the pair partner's half
-    va = oka ? (odd ? recv : d0) : 0.0;
-    vb = okb ? (odd ? d1 : recv) : 0.0;
-}
-
 // LDS scratch for col->row layout conversion: 16 doubles per wave.
 struct Scratch {
     double v[32];
@@ -328,32 +310,6 @@ __device__ __forceinline__ double wave_min_lb(double x) {
     return (double)__builtin_fminf(__builtin_bit_cast(float, (int)b[0]), __builtin_bit_cast(float, (int)b[1]));
 }
 
-// Conservative f32 wave reductions for the certificate (upper bounds): the maximum as -wave_min_lb(-x), and the sum of
-// values rounded up to f32 and added with DPP-sourced f32 adds (six adds of at most 16 + 4 terms: relative error below
-// 2^-20, covered by the final 2^-18 scale).
-__device__ __forceinline__ double wave_max_ub(double x) { return -wave_min_lb(-x); }
-__device__ __forceinline__ double wave_sum_ub(double x) {
-    float f = (float)x;
-    f = f + fabsf(f) * 0x1p-22f + 0x1p-126f;
-    asm volatile(
-        "s_nop 1\n\t"
-        "v_add_f32_dpp %0, %0, %0 row_ror:8 row_mask:0xf bank_mask:0xf\n\t"
-        "s_nop 1\n\t"
-        "v_add_f32_dpp %0, %0, %0 row_ror:4 row_mask:0xf bank_mask:0xf\n\t"
-        "s_nop 1\n\t"
-        "v_add_f32_dpp %0, %0, %0 row_ror:2 row_mask:0xf bank_mask:0xf\n\t"
-        "s_nop 1\n\t"
-        "v_add_f32_dpp %0, %0, %0 row_ror:1 row_mask:0xf bank_mask:0xf"
-        : "+v"(f));
-    int v = __builtin_bit_cast(int, f);
-    const auto a = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-    f = __builtin_bit_cast(float, (int)a[0]) + __builtin_bit_cast(float, (int)a[1]);
-    v = __builtin_bit_cast(int, f);
-    const auto b = __builtin_amdgcn_permlane16_swap(v, v, false, false);
-    f = __builtin_bit_cast(float, (int)b[0]) + __builtin_bit_cast(float, (int)b[1]);
-    return (double)f * (1.0 + 0x1p-18);
-}
-
 // Gershgorin's g of a stage from its data tile Mi (symmetric -- load_rsq_tile mirrors the lower triangle -- and zero
 // outside the active rows / columns): the absolute row sums are column sums, so a lane adds its four registers and
 // the four row groups are summed across (xrow_sum): a handful of VALU ops instead of four f64 MFMAs against a ones
@@ -408,73 +364,17 @@ __device__ __forceinline__ bool cert_ok_thr(const d4& M, double dq, double T, co
     return __builtin_amdgcn_ballot_w64(!(d - dq < T)) == 0;
 }
 
-// The test off the recursion's chain (round 5).  e_max = max_i (M_ii - box_i) is bounded without M: with b_i the BAbt_k
-// row of variable i, M_ii - box_i = RSQ_ii + b_i' P_{k+1} b_i <= max_i RSQ_ii + tr(P_{k+1}) max_i |b_i|^2 (P_{k+1} is
-// positive semidefinite: b' P b <= lambda_max(P) |b|^2 <= tr(P) |b|^2; the reference's W W' has the same diagonal,
-// |W_i|^2 = b_i' Lxx Lxx' b_i), so e_max < T holds whenever tr(P_{k+1}) < tau_k = (T - max_i RSQ_ii) / max_i |b_i|^2.
-// tau_k depends on stage k's data alone (formed beside g, cert_tau); the test needs only the trace of the record the
-// stage starts from (cert_ok_tr), so it no longer waits for the stage's MFMA products.  On the benchmark data
-// tr(P) ~ 1e2 against tau ~ 1e10.  Stages with general constraints (DCt diag(Q) DCt' also adds to M_ii) and stages with
-// a negative given box term get tau = -inf (no certificate).  Rounding: T is rounded down by 2^-40 (cert_thr), tau by
-// 2^-30; the maxima and the trace are conservative f32 reductions (wave_max_ub, wave_sum_ub: upper bounds).
+// The stage's data part of the certificate, the threshold T_k (a negative given box term folded into T_k = -inf).
+// (A test off the chain, on the trace of the record the stage starts from against a data threshold tau_k, measured
+// slower in every kernel in round 5: profiles/r05/ab_cert/)
 template <class SH>
-__device__ __forceinline__ double cert_tau(double T, const d4& Mi, const d4& bop, double dq, const SH& sh, bool live) {
-    const int c = lane_id() & 15;
-    const bool act = tile_active(c, sh.nu, sh.nx, sh.xo);
-    // max_i RSQ_ii over the active variables, max_i |b_i|^2 (lane c: the squared BAbt row of variable var(c))
-    const double rmax = wave_max_ub((diag_lane() && act) ? diag_sel(Mi) : 0.0);
-    double b2 = 0.0;
-    if (live) b2 = xrow_sum(fma(bop[0], bop[0], bop[1] * bop[1]) + fma(bop[2], bop[2], bop[3] * bop[3]));
-    const double bmax = wave_max_ub(b2);
-    const double num = T - rmax;
-    double tau = bmax > 0.0 ? num * rcp_nr(bmax) * (1.0 - 0x1p-30) : __builtin_inf();
-    bool none = !(num > 0.0) || __builtin_amdgcn_ballot_w64(dq < 0.0) != 0;
-    if constexpr (!SH::fixed) none = none || sh.ng > 0;
-    return none ? -__builtin_inf() : tau;
-}
-// the certificate of a P-form stage: tr(P_{k+1}) < tau_k, P_{k+1} the x block (tile indices >= xo1) of the record S the
-// stage starts from; wave-uniform
-__device__ __forceinline__ bool cert_ok_tr(const d4& S, int xo1, double tau) {
-    const int c = lane_id() & 15;
-    const d4 w = cert_diag_w();
-    const double d = (c >= xo1) ? w[0] * S[0] + w[1] * S[1] + w[2] * S[2] + w[3] * S[3] : 0.0;
-    const double tr = wave_sum_ub(d);  // an upper bound, identical in every lane
-    return __builtin_amdgcn_readfirstlane((int)(tr < tau)) != 0;
-}
-
-// HK_CERT_TRACE (default 0): the per-stage test on the stage matrix M after its MFMA products (cert_ok_thr against T_k,
-// a negative given box term folded into T_k = -inf).  1 builds the test off the chain, on the trace of the record the
-// stage starts from (cert_ok_tr against tau_k): a same-box A/B (profiles/r05/ab_cert/, 3 pairs) measured it slower in
-// every kernel -- headline 1.436 vs 1.460 M IP-iter/s (factorisation 3.15 vs 3.01 ms per step), Riccati sv 3.26 vs
-// 3.37 M fact/s, configs[2] 6.75 vs 7.51 M, the lone QP 343 vs 310 us per IP iteration: its reductions cost more issue
-// than the ballot they replace takes off the chain, the waves being issue-bound.
-#ifndef HK_CERT_TRACE
-#define HK_CERT_TRACE 0
-#endif
-// The stage's data part of the certificate: tau_k (HK_CERT_TRACE) or T_k.  use_dq: the box terms are given data
-// (BX_GIVEN), not the IPM's iterate.
-template <class SH>
-__device__ __forceinline__ double cert_form(const d4& Mi, const d4& bop, double dq, const SH& sh, bool live) {
+__device__ __forceinline__ double cert_form(const d4& Mi, double dq, const SH& sh) {
     const double T = cert_thr(cert_g(Mi, sh));
-#if HK_CERT_TRACE
-    return cert_tau(T, Mi, bop, dq, sh, live);
-#else
-    (void)bop;
-    (void)live;
     return __builtin_amdgcn_ballot_w64(dq < 0.0) != 0 ? -__builtin_inf() : T;
-#endif
 }
-// The per-stage test: S the record the stage starts from (P_{k+1}), M the stage matrix after its products.
-__device__ __forceinline__ bool cert_test(const d4& S, const d4& M, int xo1, double dq, double gc) {
-#if HK_CERT_TRACE
-    (void)M;
-    (void)dq;
-    return cert_ok_tr(S, xo1, gc);
-#else
-    (void)S;
-    (void)xo1;
+// The per-stage test on the stage matrix M after its products.
+__device__ __forceinline__ bool cert_test(const d4& M, double dq, double gc) {
     return cert_ok_thr(M, dq, gc, cert_diag_w());
-#endif
 }
 
 // l[4R + g] (row layout of a col-layout vector over tile block R): the pivot entries of block R
@@ -734,14 +634,6 @@ struct FixSh {
           oR(srd(s, &StageInfo::oR)), fl(srd(s, &StageInfo::r0)) {}
 };
 
-// HK_WIDE_BOP applies to the compiled (4, 12) class only (tile index = variable index, ld_pair16)
-template <class SH>
-constexpr bool wide_bop_shape() {
-    if constexpr (SH::fixed)
-        return SH::nu == 4 && SH::nx == 12;
-    else
-        return false;
-}
 
 // The stage's data blocks: per problem, or shared by the batch (StageInfo r0 bits 1 / 2; wave-uniform selects).
 __device__ __forceinline__ int stage_flags(const StageInfo& s) { return s.r0; }
@@ -933,43 +825,15 @@ __device__ __forceinline__ void ld_lu(const double* p, const BoxLane& b, double&
     vup = mk((int)ch[1], (int)cl[1]);
 }
 
-// The same paired load with the exchange deferred to the use (lu_split): a prefetched fragment would
-// otherwise wait for its own load right after issuing it.
-__device__ __forceinline__ double ld_lu_raw(const double* p, const BoxLane& b) {
-    const bool odd = (lane_id() & 16) != 0;
-    const int m = -(int)odd;
-    return gld(p, (b.up & m) | (b.lo & ~m), b.ok);
-}
-__device__ __forceinline__ void lu_split(double x, double& vlo, double& vup) {
-    const int xl = __double2loint(x), xh = __double2hiint(x);
-    const auto cl = __builtin_amdgcn_permlane16_swap(xl, xl, false, false);
-    const auto ch = __builtin_amdgcn_permlane16_swap(xh, xh, false, false);
-    vlo = mk((int)ch[0], (int)cl[0]);
-    vup = mk((int)ch[1], (int)cl[1]);
-}
-
-// Box pairs in the solves' prefetched fragments: HK_SOLVE_PAIRS = 1 loads a pair with one ld_lu_raw into the
-// even slot and splits it at the use; 0 (default) keeps two loads into slots (e0, e1).  A same-box A/B
-// (tools/gpu_ab.sh, profiles/ab_solve_pairs/) measured the paired form 0.5-1 % slower in pred and corr: the
-// saved load does not pay for the exchange on their chains.  The factorisation keeps ld_lu (fact 2.87 -> 2.75).
-#ifndef HK_SOLVE_PAIRS
-#define HK_SOLVE_PAIRS 0
-#endif
+// The solves' prefetched fragments load a box pair's lower and upper value separately: a paired load (ld_lu) needs its
+// exchange at the use, and a same-box A/B measured that 0.5-1 % slower in pred and corr (profiles/ab_solve_pairs/).
 __device__ __forceinline__ void fetch_pair(const double* p, const BoxLane& b, double& e0, double& e1) {
-    if (HK_SOLVE_PAIRS) {
-        e0 = ld_lu_raw(p, b);
-    } else {
-        e0 = gld(p, b.lo, b.ok);
-        e1 = gld(p, b.up, b.ok);
-    }
+    e0 = gld(p, b.lo, b.ok);
+    e1 = gld(p, b.up, b.ok);
 }
 __device__ __forceinline__ void use_pair(double e0, double e1, double& vlo, double& vup) {
-    if (HK_SOLVE_PAIRS) {
-        lu_split(e0, vlo, vup);
-    } else {
-        vlo = e0;
-        vup = e1;
-    }
+    vlo = e0;
+    vup = e1;
 }
 
 // A box pair's lower and upper value with ONE store: row group 0 writes the lower slot, row group 1 the
@@ -1210,7 +1074,7 @@ __device__ __forceinline__ void load_rsq_tile(const double* R, const SH& sh, d4&
     }
 }
 
-// The certificate's threshold tau_k (cert_tau) of every stage into cert[0..N], as its own pass (stages in groups of
+// The certificate's threshold T_k of every stage into cert[0..N], as its own pass (stages in groups of
 // eight, the group's tile and BAbt-operand loads issued before its math): the single-Newton start, whose first
 // factorisation is a phase-2 one.
 __device__ void cert_pass(const RicIO& io, double* cert) {
@@ -1234,7 +1098,7 @@ __device__ void cert_pass(const RicIO& io, double* cert) {
         for (int j = 0; j < 8; j++) {
             const int k = k0 + j <= io.N ? k0 + j : io.N;
             const DynSh sh(StageRef{io.st, k});
-            const double tau = cert_form(Mi[j], bop[j], 0.0, sh, k < io.N);
+            const double tau = cert_form(Mi[j], 0.0, sh);
             gst(cert, k0 + j, tau, lane_id() == 0 && k0 + j <= io.N);
         }
     }
@@ -1284,17 +1148,6 @@ __device__ __forceinline__ void bwd_fetch(const RicIO& io, const SH& sh, int k, 
     for (int r = 0; r < 4; r++) {
         const int s = 4 * r + g - sh.xo1;
         const bool ok = live && s >= 0 && s < sh.nx1;
-#ifdef HK_WIDE_BOP
-        if constexpr (wide_bop_shape<SH>()) {  // registers 1 and 2 in one 16-B load, 0 is masked
-            if (r == 1) {
-                double b1, b2;
-                ld_pair16(Bk, sh.sdB, c, s, s + 4, ok, live && s + 4 < sh.nx1, b1, b2);
-                f.bop[1] = b1;
-                f.bop[2] = b2;
-            }
-            if (r == 0 || r == 3) f.bop[r] = ldsel(Bk, lib4_idx(sh.sdB, vc, s), ok && vc >= 0);
-        } else
-#endif
         f.bop[r] = ldsel(Bk, lib4_idx(sh.sdB, vc, s), ok && vc >= 0);
         if (BM != BX_P2R) f.brow[r] = AUG ? ldsel(bp, update_b ? s : lib4_idx(sh.sdB, nux, s), ok) : 0.0;
     }
@@ -1421,23 +1274,22 @@ __device__ __forceinline__ void bwd_pre(const RicIO& io, const SH& sh, int k, co
 #ifdef HK_COUNT_NOCERT
     gc = 0.0;
 #else
-    // gc: the stage's certificate threshold tau_k on tr(P_{k+1}) (cert_tau), from its data alone
-    const bool live = SH::fixed || k < io.N;
+    // gc: the stage's certificate threshold T_k (cert_thr), from its data alone
     if constexpr (cert_loaded(BM)) {
-        // the solve's first factorisation forms tau from the tile (stage 0 too: a later one may be a P-form stage of
+        // the solve's first factorisation forms T_k from the tile (stage 0 too: a later one may be a P-form stage of
         // another plan shape) and keeps it for the others; masked store otherwise (fixed vector-memory count).  The box
         // terms (lam / t >= 0) are the iterate's, not the data's: no dq in these modes
         if constexpr (CN == CERT_LOAD) {
             gc = cur.gc;
         } else if constexpr (CN == CERT_FORM) {
-            gc = cert_form(cur.Mi, cur.bop, 0.0, sh, live);
+            gc = cert_form(cur.Mi, 0.0, sh);
             gst(bc.cert_out, k, gc, lane_id() == 0);
         } else {
-            gc = bc.cert_new ? cert_form(cur.Mi, cur.bop, 0.0, sh, live) : cur.gc;
+            gc = bc.cert_new ? cert_form(cur.Mi, 0.0, sh) : cur.gc;
             gst(bc.cert_out, k, gc, bc.cert_new && lane_id() == 0);
         }
     } else {
-        gc = (SH::fixed || k > 0) ? cert_form(cur.Mi, cur.bop, dq, sh, live) : 0.0;
+        gc = (SH::fixed || k > 0) ? cert_form(cur.Mi, dq, sh) : 0.0;
     }
 #endif
     M = cur.Mi;
@@ -1525,8 +1377,8 @@ __device__ __forceinline__ void bwd_core(const RicIO& io, Scratch* sm, const SH&
     (void)dq;
     (void)gc;
 #else
-    // on the record the stage starts from (P_{k+1} = S), off the MFMA products' chain (cert_ok_tr)
-    const bool xcert = !full && !cert_test(S, M, sh.xo1, dq, gc);
+    // on the stage matrix after its products (cert_ok_thr)
+    const bool xcert = !full && !cert_test(M, dq, gc);
 #endif
 #ifdef HK_STAMPS  // diagnostic build: how often the certificate fails, at this allowance and (with g) at 10x / 100x
     // smaller ones -- the threshold form only knows its own allowance, so those two count its failures
@@ -1573,13 +1425,11 @@ __device__ __forceinline__ void bwd_step(const RicIO& io, Scratch* sm, const SH&
 //   BM                                    : box Hessian / gradient terms (BoxMode)
 //   Pb (state order)                      : P_{k+1} b_k (compute_Pb, AUG only)
 // Vector arguments use a per-stage stride of V16.
-// PD: prefetch depth in stages.  2 (stage k-2's fragment in flight while stage k runs) for the Riccati entry points,
-// which run one wave per SIMD at the benchmark batches and wait on memory for over half of their cycles; the IPM
-// passes (two waves per SIMD, ~200 VGPRs) keep 1 -- a third fragment would push them past 256 VGPRs.
-template <bool AUG, int BM, class FX, int CN = CERT_LOAD, int PD = 1>
+// Prefetch depth one stage (two measured no faster in the Riccati entry points: N=100 3.48 vs 3.50 M fact/s, configs[2]
+// 7.14 vs 7.25 M, profiles/r04/ab_ric_LO.txt; the IPM passes have no registers for a third fragment).
+template <bool AUG, int BM, class FX, int CN = CERT_LOAD>
 __device__ void ric_backward(const RicIO& io, Scratch* sm, int update_b, const double* bsrc, int update_q,
                              const double* qsrc, const BoxCtx& bc, int compute_Pb, double* Pb) {
-    static_assert(PD == 1 || (PD == 2 && BM != BX_P2R), "depth 2 is for the Riccati entry points");
     d4 S = {0.0, 0.0, 0.0, 0.0};
     double ml_prev = 0.0, invd_prev = 0.0, kg_prev = 0.0;
 #ifdef HK_STAMPS
@@ -1623,52 +1473,12 @@ __device__ void ric_backward(const RicIO& io, Scratch* sm, int update_b, const d
         HK_STAMP(4, k);
         si = sn;
     };
-    if constexpr (PD == 1) {
-        BwdFrag alt;
-        for (int k = io.N;;) {
-            stage(k, cur, alt);
-            if (--k < 0) break;
-            stage(k, alt, cur);
-            if (--k < 0) break;
-        }
-    } else {
-        // depth 2: fragments rotate over three registers sets; stage k runs on fa with stage k-1's fragment (fb)
-        // already in flight and fetches stage k-2 into fc (clamped at 0: the last passes re-read stage 0)
-        auto stage2 = [&](int k, const BwdFrag& fa, BwdFrag& fc) __attribute__((always_inline)) {
-            HK_STAMP(0, k);
-            const int kn = k > 1 ? k - 2 : 0;
-            with_shape<FX>(StageRef{io.st, kn},
-                           [&](const auto& sh) { bwd_fetch<AUG, BM>(io, sh, kn, update_b, bsrc, update_q, qsrc, bc, fc); });
-            double* Fk1 = io.F + (long)(k + 1) * FSTRIDE;
-            if constexpr (FX::enabled) {
-                if (rec_fixed)
-                    store_factor_fixed<FX::nx>(Fk1, S, AUG ? ml_prev : 0.0, invd_prev, kg_prev, k < io.N);
-                else
-                    store_factor(Fk1, S, AUG ? ml_prev : 0.0, invd_prev, kg_prev, k < io.N);
-            } else {
-                store_factor(Fk1, S, AUG ? ml_prev : 0.0, invd_prev, kg_prev, k < io.N);
-            }
-            asm volatile("" ::: "memory");
-            with_shape<FX>(StageRef{io.st, k}, [&](const auto& sh) {
-                bwd_step<AUG, BM, CN>(io, sm, sh, k, fa, bc, compute_Pb, Pb, S, ml_prev, invd_prev, kg_prev);
-                rec_fixed = std::remove_reference_t<decltype(sh)>::fixed;
-            });
-            HK_STAMP(4, k);
-        };
-        BwdFrag f1, f2;
-        {
-            const int k1 = io.N > 0 ? io.N - 1 : 0;
-            with_shape<FX>(StageRef{io.st, k1},
-                           [&](const auto& sh) { bwd_fetch<AUG, BM>(io, sh, k1, update_b, bsrc, update_q, qsrc, bc, f1); });
-        }
-        for (int k = io.N;;) {
-            stage2(k, cur, f2);
-            if (--k < 0) break;
-            stage2(k, f1, cur);
-            if (--k < 0) break;
-            stage2(k, f2, f1);
-            if (--k < 0) break;
-        }
+    BwdFrag alt;
+    for (int k = io.N;;) {
+        stage(k, cur, alt);
+        if (--k < 0) break;
+        stage(k, alt, cur);
+        if (--k < 0) break;
     }
     store_factor(io.F, S, AUG ? ml_prev : 0.0, invd_prev, kg_prev);
 #ifdef HK_STAMPS
@@ -2119,17 +1929,6 @@ __device__ __forceinline__ void trs_fetch(const RicIO& io, const SH& sh, int k, 
     for (int r = 0; r < 4; r++) {
         const int sr = g + 4 * r - sh.xo1;
         const bool ok = live && sr >= 0 && sr < sh.nx1;
-#ifdef HK_WIDE_BOP
-        if constexpr (wide_bop_shape<SH>()) {  // registers 1 and 2 in one 16-B load, 0 is masked
-            if (r == 1) {
-                double b1, b2;
-                ld_pair16(Bk, sh.sdB, c, sr, sr + 4, ok, live && sr + 4 < sh.nx1, b1, b2);
-                f.bop[1] = b1;
-                f.bop[2] = b2;
-            }
-            if (r == 0 || r == 3) f.bop[r] = ldsel(Bk, lib4_idx(sh.sdB, vc, sr), ok && vc >= 0);
-        } else
-#endif
         f.bop[r] = ldsel(Bk, lib4_idx(sh.sdB, vc, sr), ok && vc >= 0);
         f.brow[r] = RPB ? ldsel(bp, hb ? sr : lib4_idx(sh.sdB, nux, sr), ok && compute_Pb) : 0.0;
     }

@@ -12,11 +12,6 @@
 // ------------------------------------------------------------------------------------------------
 // d_back_ric_rec_sv_tv_res / _trf_ / _trs_ over a batch (one problem per workgroup)
 // ------------------------------------------------------------------------------------------------
-// Prefetch depth of the Riccati entry points' backward sweep (ric_backward PD).  2 measured no faster than 1 on the
-// 1024-problem sv batches (N=100: 3.48 vs 3.50 M fact/s; configs[2]: 7.14 vs 7.25 M, profiles/r04/ab_ric_LO.txt)
-#ifndef HK_RIC_PD
-#define HK_RIC_PD 1
-#endif
 template <class FX>
 __global__ __launch_bounds__(64) void hk_ric_sv(KArgs a) {
     const LdsTabs T = lds_tables(a);
@@ -36,9 +31,9 @@ __global__ __launch_bounds__(64) void hk_ric_sv(KArgs a) {
     const unsigned long long t0 = mw_clock();
 #endif
     if (a.use_box)
-        ric_backward<true, BX_GIVEN, FX, CERT_LOAD, HK_RIC_PD>(io, &sm, a.update_b, b, a.update_q, q, bc, a.compute_Pb, Pb);
+        ric_backward<true, BX_GIVEN, FX, CERT_LOAD>(io, &sm, a.update_b, b, a.update_q, q, bc, a.compute_Pb, Pb);
     else
-        ric_backward<true, BX_NONE, FX, CERT_LOAD, HK_RIC_PD>(io, &sm, a.update_b, b, a.update_q, q, bc, a.compute_Pb, Pb);
+        ric_backward<true, BX_NONE, FX, CERT_LOAD>(io, &sm, a.update_b, b, a.update_q, q, bc, a.compute_Pb, Pb);
     wsync();
 #ifdef HK_STAMPS
     const unsigned long long t1 = mw_clock();
@@ -65,9 +60,9 @@ __global__ __launch_bounds__(64) void hk_ric_trf(KArgs a) {
     BoxCtx bc{};
     bc.Qx = a.vQx ? a.vQx + o16 : nullptr;
     if (a.use_box)
-        ric_backward<false, BX_GIVEN, FX, CERT_LOAD, HK_RIC_PD>(io, &sm, 0, nullptr, 0, nullptr, bc, 0, nullptr);
+        ric_backward<false, BX_GIVEN, FX, CERT_LOAD>(io, &sm, 0, nullptr, 0, nullptr, bc, 0, nullptr);
     else
-        ric_backward<false, BX_NONE, FX, CERT_LOAD, HK_RIC_PD>(io, &sm, 0, nullptr, 0, nullptr, bc, 0, nullptr);
+        ric_backward<false, BX_NONE, FX, CERT_LOAD>(io, &sm, 0, nullptr, 0, nullptr, bc, 0, nullptr);
 }
 
 template <class FX>
@@ -175,10 +170,7 @@ __global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_corr(KArgs a) {
     corr_body<FX>(a, T, v);
 }
 
-// Stages per chunk of the update pass (quads loaded before any is used; HK_UPD_CH=6 for an A/B)
-#ifndef HK_UPD_CH
-#define HK_UPD_CH 4
-#endif
+// The update pass loads 4 quads (16 stages) before using any (6 measured slower: profiles/r04/ab_headline_OP.txt)
 template <class FX>
 __global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_update(KArgs a) {
     Who who;
@@ -186,7 +178,7 @@ __global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_update(KArgs a) {
     const LdsTabs T = lds_tables(a);
     IpmView v = ipm_view(a, T, who);
     if (v.w.state[S_ACTIVE] == 0.0) return;
-    bool again = update_body<FX, HK_UPD_CH>(a, v);
+    bool again = update_body<FX, 4>(a, v);
     if (!again && a.nq) {
         if (v.l == 0) atomicAdd(&a.qctl[1], 1);
         again = ipm_refill<FX, 4, false>(a, T, who.s);  // queue mode: the slot takes the next entry
