@@ -437,28 +437,59 @@ def bench_pcond_ipm(args, torch, red, rank, world, barrier):
            "sum_kk_per_step": float(kk.sum()),
            "ret_counts": {str(int(v)): int((ret == v).sum()) for v in np.unique(ret)}}
     if rank == 0 and world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_pcond_ipm_baseline(qp, N2, k_max, args.cpu_seconds * 0.25)
+        out["cpu_baseline"] = cpu_pcond_ipm_baseline(qp, N2, k_max, args.cpu_seconds * 0.5, args.cpu_threads)
     return out
 
 
-def cpu_pcond_ipm_baseline(qp, N2, k_max, seconds):
-    """The oracle's d_part_cond -> d_ip2_res_mpc_hard_tv -> d_part_expand_solution, one host thread, over the
-    first problems of the batch until `seconds` have elapsed (the reference's own c99 condensing cannot serve:
-    it is numerically wrong for nu > 4)."""
+def cpu_pcond_ipm_baseline(qp, N2, k_max, seconds, threads):
+    """IP iterations/s of the configs[4] IPM pipeline on the host cores: d_part_cond -> d_ip2_res_mpc_hard_tv on the
+    condensed problem -> d_part_expand_solution from the reference's c99 build (oracle/_ref, kind 'reference': its
+    condensing is numerically wrong for nu > 4, DESIGN.md §3b, so its IPM solves a slightly different condensed problem
+    -- the same work per iteration), or the oracle (kind 'port') without it; `threads` host threads over a bounded
+    sample of the batch, and one thread."""
+    import threading
+
     from hpmpc_amd.cabi import HpmpcAPI, load
 
-    api = HpmpcAPI(load(os.path.join(ROOT, "oracle", "liboracle.so")), "orc_")
-    n, it, t0 = 0, 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds and n < qp.batch:
-        one = qp.problem(n)
-        c, _ = api.part_cond(one.copy(), N2)
-        r = api.ipm(c, k_max=k_max)
-        api.part_expand(one, c, r["ux"], r["pi"], r["lam"], r["t"])
-        it += r["kk"]
-        n += 1
-    dt = time.perf_counter() - t0
-    return {"value": it / dt, "unit": "IP-iter/s", "cores": 1, "kind": "port",
-            "sample": f"first {n} problems of the batch, oracle (clean-room C) pipeline, {dt:.1f} s"}
+    ref = os.path.join(ROOT, "oracle", "_ref", "libhpmpc_ref.so")
+    orc = os.path.join(ROOT, "oracle", "liboracle.so")
+    if os.path.exists(ref):
+        api, kind = HpmpcAPI(load(ref)), "reference"
+    elif os.path.exists(orc):
+        api, kind = HpmpcAPI(load(orc), "orc_"), "port"
+    else:
+        return None
+    calls = [api.prepare_pcond_ipm(qp.problem(p), N2, k_max=k_max) for p in range(min(qp.batch, 2 * threads))]
+
+    def run(nthr, secs):
+        done, iters = [0] * nthr, [0] * nthr
+        stop = time.perf_counter() + secs
+
+        def worker(i):
+            j = 0
+            while time.perf_counter() < stop:
+                call, kk = calls[(i + nthr * j) % len(calls)]
+                call()
+                iters[i] += kk.value
+                done[i] += 1
+                j += 1
+
+        th = [threading.Thread(target=worker, args=(i,)) for i in range(nthr)]
+        t0 = time.perf_counter()
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        dt = time.perf_counter() - t0
+        return sum(iters) / dt, sum(done), sum(iters)
+
+    v1, n1, i1 = run(1, seconds * 0.3)
+    vn, nn, itn = run(threads, seconds * 0.7)
+    return {"value": vn, "unit": "IP-iter/s", "cores": threads, "kind": kind, "host": host_cpu(),
+            "sample": f"{len(calls)} problems of the configs[4] batch with boxes, d_part_cond + condensed "
+                      f"d_ip2_res_mpc_hard_tv (k_max={k_max}) + d_part_expand_solution, pre-marshalled ctypes calls, "
+                      f"{threads} host threads ({nn} pipelines, {itn} IP iterations) and 1 thread ({n1}, {i1})",
+            "single_core": {"value": v1, "solves": n1, "iters": i1}}
 
 
 def bench_single_qp(args, torch, stream):

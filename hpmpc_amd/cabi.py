@@ -503,6 +503,60 @@ class HpmpcAPI:
 
         return call
 
+    def prepare_pcond_ipm(self, qp: OCPQP, N2: int, *, k_max=50, mu0=2.0, mu_tol=1e-12, alpha_min=1e-8):
+        """Pre-marshalled configs[4] IPM pipeline for CPU timing: returns (call, kk) where call() runs d_part_cond ->
+        d_ip2_res_mpc_hard_tv on the condensed problem (cold start) -> d_part_expand_solution on private buffers and
+        kk.value holds the condensed IPM's iteration count (ctypes argument tuples built once, the GIL released inside
+        each foreign call).  The terminal condensed pointers are re-pointed at the caller's stage N after every
+        d_part_cond (the reference build clobbers them, see part_cond)."""
+        N = qp.N
+        qp = qp.copy()
+        idxb = [np.ascontiguousarray(i, dtype=np.int32) for i in qp.idxb]
+        nx2, nu2, nb2, ng2 = self.part_cond_sizes(qp, N2)
+        cn = [iv(a) for a in (nx2, nu2, nb2, ng2)]
+        head = (C.c_int(N), iv(qp.nx), iv(qp.nu), iv(qp.nb), ipp(idxb), iv(qp.ng), C.c_int(N2), *cn)
+        msz = self.fn("d_part_cond_memory_space_size_bytes")(*head)
+        wsz = self.fn("d_part_cond_work_space_size_bytes")(*head)
+        memory = np.zeros(2 * (msz // 8) + 512)
+        work = np.zeros(2 * (wsz // 8) + 512)
+        hidxb2 = (IP * (N2 + 1))()
+        pB, pR, pG, pd = ((DP * (N2 + 1))() for _ in range(4))
+        dct = qp.DCt if qp.DCt else [np.zeros(8) for _ in range(N + 1)]
+        pBAbt, pRSQ, pDCt, pdd, pidx = dpp(qp.BAbt), dpp(qp.RSQrq), dpp(dct), dpp(qp.d), ipp(idxb)
+        cond_args = (C.c_int(N), iv(qp.nx), iv(qp.nu), iv(qp.nb), pidx, iv(qp.ng), pBAbt, pRSQ, pDCt, pdd,
+                     C.c_int(N2), cn[0], cn[1], cn[2], hidxb2, cn[3], pB, pR, pG, pd, _dptr(memory), _dptr(work))
+        wipm = np.zeros(self.fn("d_ip2_res_mpc_hard_tv_work_space_size_bytes")(C.c_int(N2), *cn) // 8 + 64)
+        ux2 = [np.zeros(rup(int(nu2[k] + nx2[k]) + 1, 4) + 4) for k in range(N2 + 1)]
+        pi2 = [np.zeros(rup(int(nx2[k + 1]), 4) + 4) for k in range(N2)] + [np.zeros(8)]
+        lam2 = [np.zeros(2 * rup(int(nb2[k]), 4) + 2 * rup(int(ng2[k]), 4) + 4) for k in range(N2 + 1)]
+        t2 = [x.copy() for x in lam2]
+        stat = np.zeros(5 * k_max + 5)
+        kk = C.c_int(0)
+        ipm_args = (C.byref(kk), C.c_int(k_max), C.c_double(mu0), C.c_double(mu_tol), C.c_double(alpha_min),
+                    C.c_int(0), _dptr(stat), C.c_int(N2), cn[0], cn[1], cn[2], hidxb2, cn[3], pB, pR, pG, pd,
+                    dpp(ux2), C.c_int(1), dpp(pi2), dpp(lam2), dpp(t2), _dptr(wipm))
+        b, q = bq_from_qp(qp)
+        ux, pi, lam, t = qp.alloc_solution()
+        wx = np.zeros(self.fn("d_part_expand_work_space_size_bytes")(C.c_int(N), iv(qp.nx), iv(qp.nu), iv(qp.nb),
+                                                                    iv(qp.ng)) // 8 + 64)
+        ex_args = (C.c_int(N), iv(qp.nx), iv(qp.nu), iv(qp.nb), pidx, iv(qp.ng), pBAbt, dpp(b), pRSQ, dpp(q), pDCt,
+                   dpp(ux), dpp(pi), dpp(lam), dpp(t), C.c_int(N2), cn[0], cn[1], cn[2], hidxb2, cn[3], dpp(ux2),
+                   dpp(pi2), dpp(lam2), dpp(t2), _dptr(wx))
+        f_cond, f_ipm, f_ex = self.fn("d_part_cond"), self.fn("d_ip2_res_mpc_hard_tv"), \
+            self.fn("d_part_expand_solution")
+        keep = (qp, idxb, memory, work, wipm, ux2, pi2, lam2, t2, stat, b, q, ux, pi, lam, t, wx, dct)
+        last = (pRSQ[N], pDCt[N], pdd[N], pidx[N])
+
+        def call():
+            _ = keep
+            f_cond(*cond_args)
+            pR[N2], pG[N2], pd[N2], hidxb2[N2] = last
+            r = f_ipm(*ipm_args)
+            f_ex(*ex_args)
+            return r
+
+        return call, kk
+
     # --------------------------------------------------------------------------------------------- c_interface.h
     def _iface_args(self, P, order):
         """Dense interface-form problem (oracle/iface_oracle.py) -> the wrappers' double** arguments; column-major
