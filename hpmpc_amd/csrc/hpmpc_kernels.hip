@@ -376,7 +376,7 @@ __device__ __forceinline__ void mw_solve(const KArgs& a, const LdsTabs& T, const
 #define HK_MW_PHASE(i)                            \
     do {                                          \
         const unsigned long long t_ = mw_clock(); \
-        if (i >= 0) tph[i] += t_ - tm;            \
+        if (i >= 0) tph[(i) & 3] += t_ - tm;      \
         tm = t_;                                  \
     } while (0)
 #else

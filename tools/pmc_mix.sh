@@ -14,5 +14,5 @@ run e TA_TA_BUSY_sum TA_BUFFER_WAVEFRONTS_sum GRBM_GUI_ACTIVE
 python3 tools/pmc_mix_summarize.py gpurun_out/mix gpurun_out/pmc_mix.json || exit 1
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof/fetch -o run --output-format csv -- python3 tools/pmc_run.py > gpurun_out/pmc_fetch.log 2>&1 || { echo fetch failed; tail -5 gpurun_out/pmc_fetch.log; exit 1; }
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof/write -o run --output-format csv -- python3 tools/pmc_run.py > gpurun_out/pmc_write.log 2>&1 || { echo write failed; tail -5 gpurun_out/pmc_write.log; exit 1; }
-KK=$(grep kk_sum gpurun_out/pmc_write.log | awk '{print $2}')
+KK=$(grep kk_pass gpurun_out/pmc_write.log | awk '{print $2}')
 python3 tools/pmc_summarize.py gpurun_out/prof/fetch gpurun_out/prof/write gpurun_out/pmc_hk_ipm.json $KK

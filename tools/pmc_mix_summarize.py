@@ -19,10 +19,15 @@ def main(root, out):
     for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                m = re.search(r"(hk_[a-z0-9_]+)", row.get("Kernel_Name", ""))
+                kn = row.get("Kernel_Name", "")
+                m = re.search(r"(hk_[a-z0-9_]+)", kn)
                 if not m:
                     continue
-                vals[m.group(1)][row["Counter_Name"]].append(float(row["Counter_Value"]))
+                name = m.group(1)
+                sh = re.search(r"FixSh<(\d+), *(\d+)>", kn)
+                if name == "hk_ric_sv" and sh and sh.groups() != ("4", "12"):
+                    name += f"_nu{sh.group(1)}_nx{sh.group(2)}"  # configs[2]'s instance
+                vals[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
     res = {"method": "rocprofv3 --pmc, one pass per counter group (tools/pmc_mix.sh) over tools/pmc_run.py; "
                      "values are per-launch means", "kernels": {}}
     for k, cs in sorted(vals.items()):
