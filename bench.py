@@ -872,9 +872,32 @@ def main():
         torch.cuda.synchronize()
         iso_ms = float(solver.ipm_profiled().sum())
         iso_iters = float(solver.kk.sum().item())
+        # the same batch through the other two entry points: a queue of one batch in as many slots (ticks, then
+        # the multi-wave drain of the survivors) and the solo kernel over the batch (one 4-wave workgroup per
+        # problem from the first iteration)
+        def dev_ms(fn):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            fn()
+            e0.record(stream)
+            fn()
+            e1.record(stream)
+            torch.cuda.synchronize()
+            return e0.elapsed_time(e1)
+
+        q1 = solver.queue(B, B)
+        q_ms = dev_ms(q1.run)
+        q_iters = float(q1.kk.sum().item())
+        so_ms = dev_ms(solver.ipm_solo)
+        so_iters = float(solver.kk.sum().item())
+        del q1
         iso = {"ms": iso_ms, "value": iso_iters / (iso_ms * 1e-3), "unit": "IP-iter/s",
                "note": "one batch solved alone (hpmpc_mi355x_ipm_batch): every pass runs k_max times, so the "
-                       "slowest problem sets the time"}
+                       "slowest problem sets the time",
+               "queue_one_batch": {"ms": q_ms, "value": q_iters / (q_ms * 1e-3),
+                                   "path": "hpmpc_mi355x_ipm_queue, nq = n_slots = batch (ticks, then the drain)"},
+               "solo_batch": {"ms": so_ms, "value": so_iters / (so_ms * 1e-3),
+                              "path": "hpmpc_mi355x_ipm_solo over the batch (hk_ipm_solo_mw, one 4-wave "
+                                      "workgroup per problem)"}}
 
     ali = None if args.no_aliased else bench_aliased(args, torch, red, rank, world, barrier, slots)
     cpl = None if args.no_coupled else bench_coupled(args, torch, red, rank, world, barrier, slots, value)

@@ -399,10 +399,15 @@ def flops_ip_iter(N, nx, nu):
     return flops_sv(N, nx, nu) + trs + res
 
 
+QUEUE_LANES_MAX = 4  # include/hpmpc_mi355x.h HPMPC_MI355X_QUEUE_LANES_MAX
+
+
 class IpmQueue:
     """Problem queue over a BatchSolver's data (hpmpc_mi355x_ipm_queue): ``nq`` entries solved by
     ``n_slots`` resident slots; a slot whose problem has finished takes the next entry at the next
-    iteration.  Iterates and outputs are per entry, workspaces per slot."""
+    iteration.  Iterates and outputs are per entry, workspaces per slot.  From 2048 slots up the queue runs as
+    lanes on their own streams (one per 1024 slots, at most 4; HPMPC_MI355X_QUEUE_LANES) that hand out entries
+    from one shared counter, joined back into the caller's stream at the end."""
 
     def __init__(self, solver: BatchSolver, nq: int, n_slots: int):
         torch = solver.torch
@@ -417,12 +422,34 @@ class IpmQueue:
         self.ret = torch.zeros(nq, dtype=torch.int32, device=dev)
         self.stat = torch.zeros((nq, 5 * solver.k_max), dtype=f64, device=dev)
         self.ws = torch.zeros((n_slots, solver.wsd), dtype=f64, device=dev)
-        self.qctl = torch.zeros(6 + 3 * n_slots, dtype=torch.int32, device=dev)  # include/hpmpc_mi355x.h
+        # HPMPC_MI355X_QUEUE_CTL_INTS (include/hpmpc_mi355x.h): up to QUEUE_LANES_MAX lane blocks + drain counters
+        self.qctl = torch.zeros(6 * QUEUE_LANES_MAX + 2 + 3 * n_slots, dtype=torch.int32, device=dev)
+
+    def lanes(self):
+        """The lane split of hpmpc_mi355x_ipm_queue (the C driver's rule): [(control-block offset in qctl, slots)]
+        per lane; HPMPC_MI355X_QUEUE_LANES lanes (default 4), at most one per 1024 slots.  The lanes hand out entries
+        from one shared counter."""
+        L = int(os.environ.get("HPMPC_MI355X_QUEUE_LANES", "4"))
+        L = max(1, min(L, self.n_slots // 1024, QUEUE_LANES_MAX, self.nq, self.n_slots))
+        out, s0 = [], 0
+        for i in range(L):
+            ns = self.n_slots // L + (i < self.n_slots % L)
+            out.append((6 * i + 3 * s0, ns))
+            s0 += ns
+        return out
+
+    def finished(self):
+        """Entries finished in the last run, over every lane (read after a synchronise)."""
+        return sum(int(self.qctl[o + 1].item()) for o, _ in self.lanes())
+
+    def idle(self):
+        """Whether every slot of every lane was left without an entry (read after a synchronise)."""
+        return all(bool((self.qctl[o + 2:o + 2 + ns] == -1).all()) for o, ns in self.lanes())
 
     def drained(self):
         """(iterations, problems) the multi-wave drain finished in the last run (read after a synchronise)."""
-        ns = self.n_slots
-        return int(self.qctl[4 + 3 * ns].item()), int(self.qctl[5 + 3 * ns].item())
+        o = 6 * QUEUE_LANES_MAX + 3 * self.n_slots
+        return int(self.qctl[o].item()), int(self.qctl[o + 1].item())
 
     def run(self, *, mu0=2.0, mu_tol=1e-12, alpha_min=1e-8, warm_start=0, compute_mult=1, profiled=False):
         """Solve every entry.  Returns (pass_ms[5] or None, ticks).  Polls the device once per chunk;

@@ -441,7 +441,7 @@ __device__ bool ipm_refill(const KArgs& a, const LdsTabs& T, int s) {
     const bool l0 = lane_id() == 0;
     for (;;) {
         int q = 0;
-        if (l0) q = atomicAdd(&a.qctl[0], 1);
+        if (l0) q = atomicAdd(a.qnext, 1);
         q = __builtin_amdgcn_readfirstlane(q);
         if (q >= a.nq) {
             if (l0) a.qctl[2 + s] = -1;

@@ -511,7 +511,7 @@ struct PollState {
     }
 };
 
-constexpr int kPollEvents = 2 * (8 * 4 + 1) + 3;  // enough for queue_run<R> with R <= 8 (+1: after a drain)
+constexpr int kPollEvents = 2 * (8 * 4 + 1) + 4;  // queue lanes with R <= 8: chunk events, 2 copies, drain, fork/join
 constexpr int HK_LAUNCH_REFUSED_H = -2;  // hk_launch_guard.h HK_LAUNCH_REFUSED
 
 PollState* poll_state(hipStream_t st) {
@@ -535,36 +535,62 @@ PollState* poll_state(hipStream_t st) {
     return pool.back().get();
 }
 
-// The queue driver shared by hpmpc_mi355x_ipm_queue and the single-problem entry points (which run their one
-// problem as a queue of one entry in one slot, so no pass is enqueued after it has converged).  `a` carries the
-// problem data and solver parameters; R ticks per chunk.
+// Streams of the queue's extra lanes (lane i >= 1), pooled per host thread and (device, caller stream): created
+// once, non-blocking, alive as long as the thread.
+struct LaneStreams {
+    int dev = -1;
+    hipStream_t caller = nullptr;
+    std::vector<hipStream_t> s;
+    ~LaneStreams() {
+        for (hipStream_t x : s) (void)hipStreamDestroy(x);
+    }
+};
+
+hipStream_t lane_stream(hipStream_t caller, int i) {
+    thread_local std::vector<std::unique_ptr<LaneStreams>> pool;
+    int dev = 0;
+    if (!hip_ok(hipGetDevice(&dev), "get device")) return nullptr;
+    LaneStreams* ls = nullptr;
+    for (auto& p : pool)
+        if (p->dev == dev && p->caller == caller) ls = p.get();
+    if (!ls) {
+        pool.push_back(std::make_unique<LaneStreams>());
+        ls = pool.back().get();
+        ls->dev = dev;
+        ls->caller = caller;
+    }
+    while ((int)ls->s.size() < i) {
+        hipStream_t x;
+        if (!hip_ok(hipStreamCreateWithFlags(&x, hipStreamNonBlocking), "stream create")) return nullptr;
+        ls->s.push_back(x);
+    }
+    return ls->s[i - 1];
+}
+
+// One lane of the queue: an independent queue over its own slots, entries, control block and stream.  R ticks
+// per chunk; the host enqueues chunk c and then looks at chunk c - 1 (waiting for it), so the stream never runs dry.
 template <int R>
-int queue_run(KArgs a, int nq, int n_slots, int* qctl, int k_max, double* pass_ms, int* n_ticks, hipStream_t st) {
-    static_assert(2 * (R * 4 + 1) + 3 <= kPollEvents, "poll pool sized for R <= 8");
-    if (n_ticks) *n_ticks = 0;
-    if (pass_ms)
-        for (int i = 0; i < 5; i++) pass_ms[i] = 0.0;
-    if (nq == 0) return g_err = 0;
-    a.nq = nq;
-    a.qctl = qctl;
-    a.nslots = n_slots;
-    a.qpar = 0;  // hk_ipm_init fills active list 0; iteration t runs list t & 1
-    // 2 chunk parities x (R*4 + 1) kernel boundaries + 2 "finished count copied" events, and the pinned host copy
-    // of the finished counter, from the (device, stream) pool above
-    const int nev = R * 4 + 1;
-    PollState* ps = poll_state(st);
-    if (!ps) return g_err;
-    hipEvent_t* ev = ps->e.data();
-    int* hdone = ps->hint;
-    hipEvent_t* done_ev = &ev[2 * nev];
-    auto launch = [&](int which) {
-        if (hk_launch(which, &a, n_slots, st)) {
+struct QueueLane {
+    static constexpr int nev = R * 4 + 1;
+    KArgs a;
+    int nq = 0, ns = 0, drain_max = 0;  // nq: the whole queue's entries (the lanes share the entry counter)
+    hipStream_t st = nullptr;
+    // 2 chunk parities x nev kernel boundaries, then the two "counters copied" events and the drain's end event
+    // (the (device, stream) poll pool); hdone: the pinned host copy of the counters
+    hipEvent_t* ev = nullptr;
+    int* hdone = nullptr;
+    double* pass_ms = nullptr;  // [init + drain, fact, pred, corr, update] of this lane, or null
+    long ticks = 0, cap = 0;
+    bool pending = false, drained = false, done = false;
+
+    bool launch(int which) {
+        if (hk_launch(which, &a, ns, st)) {
             set_err(HPMPC_MI355X_EHIP, "hk_ipm_queue launch failed");
             return false;
         }
         return true;
-    };
-    auto harvest = [&](int par) {  // chunk parity par has completed: accumulate its kernel times
+    }
+    bool harvest(int par) {  // chunk parity par has completed: accumulate its kernel times
         hipEvent_t* e = &ev[par * nev];
         for (int i = 0; i < R * 4; i++) {
             float ms = 0.f;
@@ -572,68 +598,74 @@ int queue_run(KArgs a, int nq, int n_slots, int* qctl, int k_max, double* pass_m
             pass_ms[1 + i % 4] += ms;
         }
         return true;
-    };
-    if (!hip_ok(hipMemsetAsync(qctl, 0, 2 * sizeof(int), st), "memset") ||
-        !hip_ok(hipMemsetAsync(qctl + 2 + n_slots, 0, 2 * sizeof(int), st), "memset") ||
-        !hip_ok(hipMemsetAsync(qctl + 4 + 3 * n_slots, 0, 2 * sizeof(int), st), "memset"))
-        return g_err;
-    if (pass_ms && !hip_ok(hipEventRecord(ev[0], st), "event record")) return g_err;
-    if (!launch(10)) return g_err;
-    if (pass_ms) {
-        if (!hip_ok(hipEventRecord(ev[1], st), "event record") || !hip_ok(hipStreamSynchronize(st), "sync"))
-            return g_err;
-        float ms = 0.f;
-        if (!hip_ok(hipEventElapsedTime(&ms, ev[0], ev[1]), "event time")) return g_err;
-        pass_ms[0] = ms;
     }
-    // every entry retires within k_max ticks of being handed out, and a slot is handed a new entry at
-    // least every k_max ticks, so this bound is never reached by a correct run
-    const long cap = (long)k_max * ((nq + n_slots - 1) / n_slots + 1) + R;
-    long ticks = 0;
-    bool pending = false, drained = false;
-    // the drain threshold (slots still iterating once the queue is empty): HPMPC_MI355X_QUEUE_DRAIN, default 768
-    // (tools/slots_probe.py: 512 / 768 / 1024 / 1536 within 1 % at 6144-8192 slots; the host looks one chunk
-    // behind, so fewer survivors are left when the drain starts); 0 keeps the ticks to the end (results then
-    // bitwise the batched solve's)
-    int drain_max = 768;
-    if (const char* e = getenv("HPMPC_MI355X_QUEUE_DRAIN")) drain_max = atoi(e);
-    for (int c = 0;; c++) {
+    // the lane's counters and the init launch (every slot takes its first entry; the iterating ones form list 0)
+    bool begin(int k_max) {
+        if (!hip_ok(hipMemsetAsync(a.qctl + 1, 0, sizeof(int), st), "memset") ||
+            !hip_ok(hipMemsetAsync(a.qctl + 2 + ns, 0, 2 * sizeof(int), st), "memset"))
+            return false;
+        if (pass_ms && !hip_ok(hipEventRecord(ev[0], st), "event record")) return false;
+        if (!launch(10)) return false;
+        if (pass_ms) {
+            if (!hip_ok(hipEventRecord(ev[1], st), "event record") || !hip_ok(hipStreamSynchronize(st), "sync"))
+                return false;
+            float ms = 0.f;
+            if (!hip_ok(hipEventElapsedTime(&ms, ev[0], ev[1]), "event time")) return false;
+            pass_ms[0] = ms;
+        }
+        // every entry retires within k_max ticks of being handed out, and a slot is handed a new entry at
+        // least every k_max ticks, so this bound is never reached by a correct run
+        cap = (long)k_max * ((nq + ns - 1) / ns + 1) + R;
+        return true;
+    }
+    // chunk c: R ticks of the four passes, then the copy of the counters
+    bool enqueue(int c) {
         const int par = c & 1;
         hipEvent_t* e = &ev[par * nev];
-        if (pass_ms && !hip_ok(hipEventRecord(e[0], st), "event record")) return g_err;
+        if (pass_ms && !hip_ok(hipEventRecord(e[0], st), "event record")) return false;
         for (int i = 0; i < R; i++) {
             a.qpar = (int)((ticks + i) & 1);  // active-slot list of this iteration (kernel args are copied at launch)
             for (int k = 0; k < 4; k++) {
-                if (!launch(11 + k)) return g_err;
-                if (pass_ms && !hip_ok(hipEventRecord(e[4 * i + k + 1], st), "event record")) return g_err;
+                if (!launch(11 + k)) return false;
+                if (pass_ms && !hip_ok(hipEventRecord(e[4 * i + k + 1], st), "event record")) return false;
             }
         }
         ticks += R;
-        // per chunk parity: [4 par] finished, [4 par + 1] handed out, [4 par + 2 .. 3] the two active-list lengths
+        // per chunk parity: [4 par] handed out (all lanes), [4 par + 1] finished (this lane), [4 par + 2 .. 3] the
+        // two active-list lengths
         int* hc = &hdone[4 * par];
-        if (!hip_ok(hipMemcpyAsync(hc, qctl, 2 * sizeof(int), hipMemcpyDeviceToHost, st), "copy") ||
-            !hip_ok(hipMemcpyAsync(hc + 2, qctl + 2 + n_slots, 2 * sizeof(int), hipMemcpyDeviceToHost, st), "copy") ||
-            !hip_ok(hipEventRecord(done_ev[par], st), "event record"))
-            return g_err;
-        if (pending) {  // look at the previous chunk while this one runs
-            if (!hip_ok(hipEventSynchronize(done_ev[par ^ 1]), "event sync")) return g_err;
-            if (pass_ms && !harvest(par ^ 1)) return g_err;
-            const int* hp = &hdone[4 * (par ^ 1)];  // [0] handed out, [1] finished, [2 .. 3] list lengths
-            if (hp[1] >= nq) break;
-            // Drain: every entry handed out and at most drain_max slots still iterating (as of the previous chunk):
-            // the survivors finish in one multi-wave launch (hk_ipm_qdrain_mw) after the chunk just enqueued, on
-            // the active list its last update filled
+        return hip_ok(hipMemcpyAsync(hc, a.qnext, sizeof(int), hipMemcpyDeviceToHost, st), "copy") &&
+               hip_ok(hipMemcpyAsync(hc + 1, a.qctl + 1, sizeof(int), hipMemcpyDeviceToHost, st), "copy") &&
+               hip_ok(hipMemcpyAsync(hc + 2, a.qctl + 2 + ns, 2 * sizeof(int), hipMemcpyDeviceToHost, st), "copy") &&
+               hip_ok(hipEventRecord(ev[2 * nev + par], st), "event record");
+    }
+    // after chunk c is enqueued: look at chunk c - 1; every entry handed out and none left iterating in this lane,
+    // or the drain launched -> done
+    bool poll(int c) {
+        const int par = c & 1;
+        if (pending) {
+            if (!hip_ok(hipEventSynchronize(ev[2 * nev + (par ^ 1)]), "event sync")) return false;
+            if (pass_ms && !harvest(par ^ 1)) return false;
+            const int* hp = &hdone[4 * (par ^ 1)];
+            // slots still iterating after chunk c - 1 (the active list its last update filled)
             const int nact = hp[2 + (int)((ticks - R) & 1)];
+            if (hp[0] >= nq && nact == 0) {
+                done = true;
+                return true;
+            }
+            // Drain: every entry handed out and at most drain_max slots still iterating (as of the previous
+            // chunk): the survivors finish in one multi-wave launch (hk_ipm_qdrain_mw) after the chunk just
+            // enqueued, on the active list its last update filled
             if (drain_max > 0 && hp[0] >= nq && nact <= drain_max) {
                 a.qpar = (int)(ticks & 1);
-                const int r = hk_launch(17, &a, n_slots, st);
+                const int r = hk_launch(17, &a, ns, st);
                 if (r == 0) {
-                    drained = true;
-                    break;
+                    drained = done = true;
+                    return true;
                 }
                 if (r != HK_LAUNCH_REFUSED_H) {
                     set_err(HPMPC_MI355X_EHIP, "hk_ipm_qdrain_mw launch failed");
-                    return g_err;
+                    return false;
                 }
                 drain_max = 0;  // refused: keep ticking
             }
@@ -641,23 +673,118 @@ int queue_run(KArgs a, int nq, int n_slots, int* qctl, int k_max, double* pass_m
         pending = true;
         if (ticks >= cap) {
             set_err(HPMPC_MI355X_EHIP, "hk_ipm_queue did not drain");
-            return HPMPC_MI355X_EHIP;
+            return false;
         }
+        return true;
     }
-    // the chunk enqueued last finds every slot idle; profiled runs wait for it so that pass_ms covers
-    // every launch (n_ticks of each pass kernel), otherwise it completes on the stream.  A drain launch goes to
-    // pass_ms[0] with the init.
-    if (pass_ms) {
+    // the chunk enqueued last finds every slot idle; profiled runs wait for it so that pass_ms covers every
+    // launch (ticks of each pass kernel), otherwise it completes on the stream.  A drain goes to pass_ms[0].
+    bool end() {
+        if (!pass_ms) return true;
         const int par = (int)((ticks / R - 1) & 1);
-        if (drained && !hip_ok(hipEventRecord(ev[2 * nev + 2], st), "event record")) return g_err;
-        if (!hip_ok(hipEventSynchronize(done_ev[par]), "event sync") || !harvest(par)) return g_err;
+        hipEvent_t* done_ev = &ev[2 * nev];
+        if (drained && !hip_ok(hipEventRecord(ev[2 * nev + 2], st), "event record")) return false;
+        if (!hip_ok(hipEventSynchronize(done_ev[par]), "event sync") || !harvest(par)) return false;
         if (drained) {
             float ms = 0.f;
             if (!hip_ok(hipEventSynchronize(ev[2 * nev + 2]), "event sync") ||
                 !hip_ok(hipEventElapsedTime(&ms, done_ev[par], ev[2 * nev + 2]), "event time"))
-                return g_err;
+                return false;
             pass_ms[0] += ms;
         }
+        return true;
+    }
+};
+
+// The problem-queue driver (hpmpc_mi355x_ipm_queue).  `a` carries the problem data and solver parameters.  The
+// slots are split into `lanes` contiguous lanes, each a queue with its own control block in qctl and its own stream
+// (lane 0 on the caller's; the others forked from it and joined back into it at the end), all handing out entries
+// from one shared counter: one lane's pass kernels fill the tail of another's, where a single queue's launch waits
+// for its last waves, and no lane runs out of entries before the others.  Each entry's solve is the same whatever
+// its lane and slot.
+template <int R>
+int queue_run(KArgs a, int nq, int n_slots, int* qctl, int* dctr, int lanes, int k_max, double* pass_ms,
+              int* n_ticks, hipStream_t st) {
+    static_assert(2 * (R * 4 + 1) + 3 < kPollEvents, "poll pool sized for R <= 8, plus the fork / join event");
+    if (n_ticks) *n_ticks = 0;
+    if (pass_ms)
+        for (int i = 0; i < 5; i++) pass_ms[i] = 0.0;
+    if (nq == 0) return g_err = 0;
+    lanes = std::max(1, std::min({lanes, HPMPC_MI355X_QUEUE_LANES_MAX, nq, n_slots}));
+    // the drain threshold (slots still iterating once the queue is empty; split over the lanes in proportion to
+    // their slots): HPMPC_MI355X_QUEUE_DRAIN, default 768 (tools/slots_probe.py: 512 / 768 / 1024 / 1536 within
+    // 1 % at 6144-8192 slots); 0 keeps the ticks to the end (results then bitwise the batched solve's)
+    int drain_max = 768;
+    if (const char* e = getenv("HPMPC_MI355X_QUEUE_DRAIN")) drain_max = atoi(e);
+    QueueLane<R> L[HPMPC_MI355X_QUEUE_LANES_MAX];
+    double lane_ms[HPMPC_MI355X_QUEUE_LANES_MAX][5] = {};
+    a.dctr = dctr;
+    a.qnext = qctl;  // lane 0's [0]: the entry counter every lane hands out from
+    if (!hip_ok(hipMemsetAsync(dctr, 0, 2 * sizeof(int), st), "memset") ||
+        !hip_ok(hipMemsetAsync(qctl, 0, sizeof(int), st), "memset"))
+        return g_err;
+    PollState* ps0 = poll_state(st);
+    if (!ps0) return g_err;
+    hipEvent_t fork = ps0->e[kPollEvents - 1];
+    if (lanes > 1 && !hip_ok(hipEventRecord(fork, st), "event record")) return g_err;
+    int s0 = 0;
+    for (int i = 0; i < lanes; i++) {
+        QueueLane<R>& l = L[i];
+        l.ns = n_slots / lanes + (i < n_slots % lanes);
+        l.nq = nq;
+        l.st = i == 0 ? st : lane_stream(st, i);  // (the caller's may be the null stream)
+        if (i > 0 && !l.st) return g_err;
+        PollState* ps = poll_state(l.st);
+        if (!ps) return g_err;
+        l.ev = ps->e.data();
+        l.hdone = ps->hint;
+        if (i > 0 && !hip_ok(hipStreamWaitEvent(l.st, fork, 0), "stream wait")) return g_err;
+        l.a = a;
+        l.a.nq = nq;
+        l.a.nslots = l.ns;
+        l.a.qctl = qctl + 6 * i + 3 * s0;
+        l.a.qpar = 0;
+        l.a.ws = a.ws + (long)s0 * a.sW;
+        l.drain_max = drain_max > 0 ? std::max(1, (int)((long)drain_max * l.ns / n_slots)) : 0;
+        l.pass_ms = pass_ms ? lane_ms[i] : nullptr;
+        s0 += l.ns;
+    }
+    // Each lane runs the protocol "enqueue chunk c, then look at chunk c - 1" on its own: a lane whose chunk c - 1
+    // has completed is looked at and given chunk c + 1 at once, whatever the other lanes are doing (polled without
+    // blocking; with one lane this is the same sequence as waiting for the event).
+    int c[HPMPC_MI355X_QUEUE_LANES_MAX] = {};
+    for (int i = 0; i < lanes; i++) {
+        QueueLane<R>& l = L[i];
+        if (!l.begin(k_max) || !l.enqueue(0) || !l.poll(0) || !l.enqueue(1)) return g_err;
+        c[i] = 1;
+    }
+    for (int left = lanes; left > 0;) {
+        for (int i = 0; i < lanes; i++) {
+            QueueLane<R>& l = L[i];
+            if (l.done) continue;
+            const hipError_t q = hipEventQuery(l.ev[2 * QueueLane<R>::nev + ((c[i] - 1) & 1)]);
+            if (q == hipErrorNotReady) continue;
+            if (!hip_ok(q, "event query") || !l.poll(c[i])) return g_err;
+            if (l.done) {
+                left--;
+                continue;
+            }
+            if (!l.enqueue(++c[i])) return g_err;
+        }
+    }
+    long ticks = 0;
+    for (int i = 0; i < lanes; i++) {
+        QueueLane<R>& l = L[i];
+        if (!l.end()) return g_err;
+        if (i > 0) {  // join: the caller's stream waits for the lane's last chunk (and drain)
+            hipEvent_t join = l.ev[kPollEvents - 1];
+            if (!hip_ok(hipEventRecord(join, l.st), "event record") ||
+                !hip_ok(hipStreamWaitEvent(st, join, 0), "stream wait"))
+                return g_err;
+        }
+        ticks += l.ticks;
+        if (pass_ms)
+            for (int k = 0; k < 5; k++) pass_ms[k] += lane_ms[i][k];
     }
     if (n_ticks) *n_ticks = (int)ticks;
     return g_err = 0;
@@ -692,7 +819,12 @@ extern "C" int hpmpc_mi355x_ipm_queue(const hpmpc_mi355x_plan* plan, const hpmpc
     a.ret = ret;
     a.stat = stat;
     a.no_bkp = 1;  // slots are reused and no KKT re-solve follows a queue solve (header): backups are dead stores
-    return queue_run<8>(a, nq, n_slots, qctl, k_max, pass_ms, n_ticks, (hipStream_t)stream);
+    // lanes: HPMPC_MI355X_QUEUE_LANES (default 4), at most one per 1024 slots (a smaller queue keeps one lane)
+    int lanes = 4;
+    if (const char* e = getenv("HPMPC_MI355X_QUEUE_LANES")) lanes = atoi(e);
+    lanes = std::min(lanes, n_slots / 1024);
+    int* dctr = qctl + 6 * HPMPC_MI355X_QUEUE_LANES_MAX + 3 * n_slots;
+    return queue_run<8>(a, nq, n_slots, qctl, dctr, lanes, k_max, pass_ms, n_ticks, (hipStream_t)stream);
 }
 
 extern "C" int hpmpc_mi355x_ric_sv_batch(const hpmpc_mi355x_plan* plan, const hpmpc_mi355x_layout* lay, int nprob,

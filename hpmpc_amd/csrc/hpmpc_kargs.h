@@ -45,4 +45,6 @@ struct KArgs {
     int no_bkp;  // public queue API: the update pass writes no iterate backups (only the KKT re-solve reads them)
     int qpar;    // queue tick parity: workgroup i of an iteration kernel runs slot list[qpar][i]; the update
                  // pass lists the slots that iterate again in list qpar ^ 1 (hk_ipm_init fills list qpar)
+    int* dctr;   // queue: [0] iterations and [1] problems the multi-wave drain finished (summed over lanes)
+    int* qnext;  // queue: the next entry to hand out, shared by the lanes
 };

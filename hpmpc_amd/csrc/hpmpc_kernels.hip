@@ -460,8 +460,8 @@ __global__ __launch_bounds__(256) void hk_ipm_qdrain_mw(KArgs a) {
     __syncthreads();
     if (threadIdx.x == 0) {
         a.qctl[2 + s] = -1;
-        atomicAdd(&a.qctl[4 + 3 * a.nslots], a.kk[q] - kk0);  // the drain's iterations and problems
-        atomicAdd(&a.qctl[5 + 3 * a.nslots], 1);
+        atomicAdd(&a.dctr[0], a.kk[q] - kk0);  // the drain's iterations and problems
+        atomicAdd(&a.dctr[1], 1);
         atomicAdd(&a.qctl[1], 1);
     }
 }

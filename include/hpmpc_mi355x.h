@@ -37,6 +37,10 @@ extern "C" {
 #define HPMPC_MI355X_EUNSUPPORTED (-10)
 #define HPMPC_MI355X_EHIP (-11)
 #define HPMPC_MI355X_EMW (-20)
+/* Problem queue control block (hpmpc_mi355x_ipm_queue's qctl): ints for n_slots slots, up to
+ * HPMPC_MI355X_QUEUE_LANES_MAX lanes. */
+#define HPMPC_MI355X_QUEUE_LANES_MAX 4
+#define HPMPC_MI355X_QUEUE_CTL_INTS(n_slots) (6 * HPMPC_MI355X_QUEUE_LANES_MAX + 2 + 3 * (n_slots))
 
 /* ================================ Part 1: reference entry points ================================ */
 
@@ -329,21 +333,27 @@ int hpmpc_mi355x_ipm_batch_profiled(const hpmpc_mi355x_plan *plan, const hpmpc_m
 /* Problem queue (continuous batching): solve nq problems with n_slots resident solver slots.  Queue
  * entry q solves data problem q % nprob (BAbt/RSQrq/d as in hpmpc_mi355x_ipm_batch, nprob problems);
  * ux/pi/lam/t/kk/ret/stat are per queue entry (nq of each, same strides); ws holds n_slots
- * workspaces; qctl is device scratch of 6 + 3 * n_slots ints (counters, the entry each slot holds, two
- * lists of the slots that iterate: workgroup i of an iteration runs the i-th listed slot, so a draining queue
- * keeps one slot per SIMD; and at [4 + 3 n_slots] / [5 + 3 n_slots] the iterations / problems the drain
- * finished).  A slot whose problem has finished takes
- * the next entry at the following iteration, so the GPU is not left idle behind the slowest problem
- * of a batch.  Drain: once every entry is handed out and at most HPMPC_MI355X_QUEUE_DRAIN (environment,
- * default 768) slots still iterate, the survivors finish one per four-wave workgroup (the multi-wave body of
- * hpmpc_mi355x_ipm_solo) in one launch.  Results are those of hpmpc_mi355x_ipm_batch on each entry: bitwise
+ * workspaces; qctl is device scratch of HPMPC_MI355X_QUEUE_CTL_INTS(n_slots) ints.  A slot whose problem has
+ * finished takes the next entry at the following iteration, so the GPU is not left idle behind the slowest
+ * problem of a batch.  Lanes: the slots are split into L contiguous lanes (HPMPC_MI355X_QUEUE_LANES, environment,
+ * default 4, at most one per 1024 slots and HPMPC_MI355X_QUEUE_LANES_MAX), each a queue on its own stream (lane 0
+ * on `stream`, the others forked from it and joined back into it) handing out entries from one shared counter
+ * (qctl[0]), so that one lane's pass kernels fill the tail of another's.  Lane i's control block starts at
+ * qctl[6 i + 3 s_i] (s_i: its first slot): [0] (lane 0: the shared counter of entries handed out), [1] entries
+ * the lane finished, [2 + s] the entry its slot s holds (-1 none), then the lengths and entries of two lists of
+ * the slots that iterate (workgroup i of an iteration runs the i-th listed slot, so a draining queue keeps one
+ * slot per SIMD).  qctl[6 HPMPC_MI355X_QUEUE_LANES_MAX + 3 n_slots] and the
+ * next int hold the iterations / problems the drain finished.  Drain: once a lane has handed out every entry and
+ * at most its share (by slots) of HPMPC_MI355X_QUEUE_DRAIN (environment, default 768) slots still iterate, its
+ * survivors finish one per four-wave workgroup (the multi-wave body of hpmpc_mi355x_ipm_solo) in one launch.  Results are those of hpmpc_mi355x_ipm_batch on each entry: bitwise
  * for the entries finished by the iteration passes (all of them with HPMPC_MI355X_QUEUE_DRAIN=0), to rounding
  * for those finished in the drain (the multi-wave bodies contract a few products differently).  The per-slot
  * workspace is reused, so a queue solve leaves no factor behind for d_kkt_solve_new_rhs_res_mpc_hard_tv; for
  * the same reason its update pass writes neither the iterate backups nor r_m, which only that re-solve reads.
  * Synchronises with the device once per chunk of iterations (it polls the finished counter); on
  * return the last chunk may still be running on `stream`.  pass_ms (nullable): device time of
- * [init + drain, fact, pred, corr, update] summed over the run; n_ticks (nullable): iterations enqueued. */
+ * [init + drain, fact, pred, corr, update] summed over the run and the lanes (the lanes' kernels overlap);
+ * n_ticks (nullable): iterations enqueued, summed over the lanes (launches of each pass kernel). */
 int hpmpc_mi355x_ipm_queue(const hpmpc_mi355x_plan *plan, const hpmpc_mi355x_layout *lay, int nprob, int nq,
                            int n_slots, const double *BAbt, const double *RSQrq, const double *d, double *ux,
                            double *pi, double *lam, double *t, double *ws, int *qctl, int k_max, double mu0,

@@ -385,12 +385,37 @@ def test_queue_matches_batch(small_batch, n_slots, nq):
     pass_ms, ticks = Q.run(profiled=True)
     torch.cuda.synchronize()
     _queue_equals_batch(s, Q, nq)
-    assert int(Q.qctl[1]) == nq and bool((Q.qctl[2:2 + n_slots] == -1).all())
+    assert Q.finished() == nq and Q.idle()
     kk = s.kk.cpu().numpy()
     assert ticks >= int(kk.max()) and pass_ms[1] > 0.0
     Q.run()  # a second run over the same buffers gives the same answers
     torch.cuda.synchronize()
     _queue_equals_batch(s, Q, nq)
+
+
+@pytest.mark.parametrize("lanes", [3, 4])
+def test_queue_lanes_match_batch(monkeypatch, lanes):
+    """A queue split into lanes (each a queue over its own slots on its own stream, forked from and joined back into
+    the caller's, all handing out entries from one counter): every entry is bitwise the batched solve of its problem,
+    with an uneven split of the slots, and the caller's stream sees every lane's results."""
+    import torch
+
+    from hpmpc_amd.batch import BatchSolver
+    from hpmpc_amd.shard import make_shard
+
+    monkeypatch.setenv("HPMPC_MI355X_QUEUE_LANES", str(lanes))
+    s = BatchSolver(make_shard(100, 12, 4, 0, 1, 1024), k_max=50)
+    s.ipm()
+    Q = s.queue(5001, 4096)
+    assert len(Q.lanes()) == lanes
+    pass_ms, ticks = Q.run(profiled=True)
+    torch.cuda.synchronize()
+    _queue_equals_batch(s, Q, 5001)
+    assert Q.finished() == 5001 and Q.idle() and Q.drained() == (0, 0)
+    assert ticks >= lanes * int(s.kk.max().item()) and pass_ms[1] > 0.0
+    Q.ux.zero_()
+    Q.run()  # unprofiled: the results land on the caller's stream (the lanes are joined back into it)
+    _queue_equals_batch(s, Q, 5001)
 
 
 def test_queue_back_to_back_on_two_streams(small_batch):
@@ -548,7 +573,7 @@ def test_queue_drain_matches_oracle(oracle, monkeypatch):
     Q = s.queue(2048, 2048)
     pass_ms, ticks = Q.run(profiled=True)
     torch.cuda.synchronize()
-    assert int(Q.qctl[1]) == 2048 and bool((Q.qctl[2:2 + 2048] == -1).all())
+    assert len(Q.lanes()) == 2 and Q.finished() == 2048 and Q.idle()
     idx = torch.arange(2048, device=s.ux.device) % 1024
     assert torch.equal(Q.ret, s.ret[idx])
     same = torch.ones(2048, dtype=torch.bool, device=s.ux.device)

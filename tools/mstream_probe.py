@@ -43,13 +43,19 @@ def run(s, K, L, slots):
 
 
 def main():
+    """Three rounds of: the library's own lanes (one queue of 8192 slots, HPMPC_MI355X_QUEUE_LANES=4), four host
+    threads each driving a one-lane queue of 2048 slots, and one one-lane queue of 8192 slots."""
     K = int(sys.argv[1]) if len(sys.argv) > 1 else 20
     s = BatchSolver(make_shard(100, 12, 4, 0, 1, 1024), k_max=50)
     run(s, 4, 1, 8192)
-    for L, slots in ((1, 8192), (2, 4096), (2, 8192), (4, 2048), (4, 4096), (1, 8192)):
-        run(s, 4, L, slots)
-        best = max(run(s, K, L, slots) for _ in range(2))
-        print(f"K={K} queues={L} slots/queue={slots}: {best[0]:.0f} IP-iter/s ({best[1] * 1e3:.1f} ms)", flush=True)
+    for rnd in range(3):
+        for name, lanes_env, L, slots in (("C lanes", "4", 1, 8192), ("py threads", "1", 4, 2048),
+                                          ("one lane", "1", 1, 8192)):
+            os.environ["HPMPC_MI355X_QUEUE_LANES"] = lanes_env
+            run(s, 4, L, slots)
+            best = max(run(s, K, L, slots) for _ in range(2))
+            print(f"round {rnd} K={K} {name}: queues={L} slots/queue={slots} lanes env={lanes_env}: "
+                  f"{best[0]:.0f} IP-iter/s ({best[1] * 1e3:.1f} ms)", flush=True)
 
 
 if __name__ == "__main__":
