@@ -8,12 +8,14 @@ stage data (no aliased buffers), solved by the residual-based Mehrotra IPM
 
 A "step" is one batch of 1024 problems (default K = 20 steps, the driver's count; the same line reports K = 40 in
 "k40").  The K timed steps are solved through one problem queue (hpmpc_mi355x_ipm_queue): 8 x 1024 resident solver
-slots, each taking the next problem as soon as its own has converged (iterations are ticks of the pass kernels
-hk_ipm_fact, hk_ipm_pred, hk_ipm_corr, hk_ipm_update over all slots; once the queue is empty and few slots still
-iterate, they finish on the multi-wave kernel hk_ipm_qdrain_mw).  value = IP iterations per second over all ranks (sum of per-problem
-iteration counts / max-over-ranks time).  The roofline object is for the dominant kernel (the pass
-with the largest device time per step, priced with that pass's own algorithmic bytes; `per_pass` lists
-all four), timed with hipEvents at every kernel boundary inside the timed region.  An isolated single-batch solve is reported beside it.
+slots in four lanes of 2048 on four streams, each slot taking the next problem (one shared counter) as soon as its
+own has converged (iterations are ticks of the pass kernels hk_ipm_fact, hk_ipm_pred, hk_ipm_corr, hk_ipm_update over
+a lane's slots; once the queue is empty and few slots still iterate, they finish on the multi-wave kernel
+hk_ipm_qdrain_mw).  value = IP iterations per second over all ranks (sum of per-problem iteration counts /
+max-over-ranks time).  The lanes run the four passes concurrently, so the roofline's unit of work is one step (all
+four passes' algorithmic bytes over the step's IP iterations, over the step's wall time); the dominant pass's
+per-launch figures (hipEvents at every kernel boundary inside the timed region) and `per_pass` are kept beside it.
+An isolated single-batch solve is reported beside it.
 The Riccati factorisation rate (d_back_ric_rec_sv_tv_res, nb = 0, compute_pi = 1) of the same
 batch is reported in the same JSON line, and so is configs[4] ("pcond": 512 x N=200 nx=24 nu=6 condensed into
 20 blocks, the condensed Riccati and the expansion, with its own roofline and CPU baseline).
@@ -771,7 +773,10 @@ def main():
     # scaling split of configs[3], 4096 over 8 GPUs = 512 per GPU) still fills every SIMD twice from the queue
     # more slots than the chip holds resident (2 per SIMD = 2048): each pass launch then dispatches the waiting slots
     # as earlier ones finish, so a launch no longer waits for its slowest resident slot (tools/slots_probe.py: 2048 /
-    # 4096 / 6144 / 8192 slots 1.53 / 1.56 / 1.59 / 1.61 M IP-iter/s at K = 20 with the drain)
+    # 4096 / 6144 / 8192 slots 1.53 / 1.56 / 1.59 / 1.61 M IP-iter/s at K = 20 with the drain).  The queue runs its
+    # slots as four lanes of 2048 on four streams (one shared entry counter), whose pass kernels overlap one another's
+    # launch tails (tools/mstream_probe.py: 1.60 -> 1.70 M at K = 20; the lanes' kernel times overlap, so the per-pass
+    # launch_ms below are per lane launch, summed over the lanes' concurrent streams by rocprofv3 alike)
     slots = args.slots if args.slots > 0 else max(8 * B, 8192)
     if args.warmup > 0:
         wq = solver.queue(args.warmup * B, slots)
@@ -808,7 +813,9 @@ def main():
     bytes_dom = bytes_pass[names[dom]]
     achieved = per_pass[names[dom]]["achieved_GBps"]
     bytes_iter = algorithmic_bytes_per_ip_iter(qp)
-    ipm_ms = float(pass_ms.sum())
+    dt_rank = t1 - t0
+    step_achieved = iters_rank * bytes_iter / dt_rank / 1e9
+    n_lanes = len(Q.lanes())
     fl_iter = flops_ip_iter(N, nx, nu)
     # parity sample of the timed run (after it): 8 queue entries spread over the K batches against the reference
     ref = ref_api() if rank == 0 else None
@@ -922,7 +929,7 @@ def main():
     sv_bytes = algorithmic_bytes_per_sv(qp_ric)
     sv_achieved = B * sv_bytes / (sv_ms * 1e-3) / 1e9
 
-    traffic = None
+    traffic = traffic_dom_launch = None
     pmc = os.path.join(ROOT, "profiles", "pmc_hk_ipm.json")
     if os.path.exists(pmc):
         try:
@@ -939,7 +946,12 @@ def main():
                         pp["traffic_bytes_per_problem_iter"] = per_it
                         pp["traffic_over_algorithmic"] = per_it / pp["algorithmic_bytes_per_problem_iter"]
                 t_dom = per_pass[names[dom]].get("traffic_bytes_per_problem_iter")
-                traffic = None if t_dom is None else t_dom * probs_per_launch
+                traffic_dom_launch = None if t_dom is None else t_dom * probs_per_launch
+                # per step: the four passes' measured bytes per problem-iteration x this run's iterations per step
+                # (the drained iterations priced at the pass kernels' rate)
+                t_it = [pp.get("traffic_bytes_per_problem_iter") for pp in per_pass.values()]
+                if all(x is not None for x in t_it):
+                    traffic = sum(t_it) * iters_rank / args.steps
         except Exception:
             traffic = None
 
@@ -980,22 +992,38 @@ def main():
                                    f"{B} slots",
                        "sum_kk_per_step": iters_total / args.steps, "ret_counts": {
                            str(int(r)): int((ret == r).sum()) for r in np.unique(ret)}},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": achieved / PEAK_HBM_GBS, "traffic": traffic, "kernel": names[dom],
-                         "launch_ms": launch_ms, "launches": int(ticks),
-                         "problem_iters_per_launch": probs_per_launch,
+            # The queue's four lanes run the four pass kernels concurrently on four streams, so a pass launch's
+            # duration overlaps the other lanes' launches and per-launch rates understate the device: the roofline's
+            # unit of work is one step (a batch of B problems solved through the queue, init and drain included),
+            # its algorithmic bytes the sum over the step's IP iterations of the four passes' algorithmic bytes,
+            # over the step's wall time (conservative: host gaps, init and drain included).  The dominant pass's
+            # per-lane-launch figures (which rocprofv3's kernel stats reproduce) are kept beside it.
+            "roofline": {"bound": "hbm", "achieved": step_achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": step_achieved / PEAK_HBM_GBS, "traffic": traffic,
+                         "kernel": "hk_ipm_fact + hk_ipm_pred + hk_ipm_corr + hk_ipm_update (one IP iteration, "
+                                   f"{n_lanes} concurrent lanes)",
+                         "unit_of_work": "one step: a batch of B problems through the queue (per rank)",
+                         "algorithmic_bytes_per_step": bytes_iter * iters_rank / args.steps,
+                         "traffic_over_algorithmic": (None if traffic is None else
+                                                      traffic / (bytes_iter * iters_rank / args.steps)),
+                         "lanes": n_lanes,
+                         "dominant_pass": {"kernel": names[dom], "launch_ms": launch_ms, "launches": int(ticks),
+                                           "problem_iters_per_launch": probs_per_launch,
+                                           "achieved_GBps_per_launch": achieved,
+                                           "frac_per_launch": achieved / PEAK_HBM_GBS,
+                                           "traffic_per_launch": traffic_dom_launch},
                          "drain": {"kernel": "hk_ipm_qdrain_mw", "problems": drain_probs, "iterations": drain_iters,
                                    "ms_with_init": float(pass_ms[0])},
                          "algorithmic_bytes_per_problem_iter": bytes_dom,
                          "per_pass": per_pass,
                          "pass_ms_per_step": {n: float(v / args.steps) for n, v in zip(names, pass_ms)},
-                         # fixed fields: the two tied passes and the whole iteration, whichever pass 'kernel' names
+                         # fixed fields: the two tied passes (per lane launch) and the whole iteration
                          "frac_fact": per_pass["hk_ipm_fact"]["achieved_GBps"] / PEAK_HBM_GBS,
                          "frac_corr": per_pass["hk_ipm_corr"]["achieved_GBps"] / PEAK_HBM_GBS,
-                         "frac_whole_iteration": iters_rank * bytes_iter / (ipm_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
-                         "ipm_whole_solve": {"achieved_GBps": iters_rank * bytes_iter / (ipm_ms * 1e-3) / 1e9,
+                         "frac_whole_iteration": step_achieved / PEAK_HBM_GBS,
+                         "ipm_whole_solve": {"achieved_GBps": step_achieved,
                                              "algorithmic_bytes_per_ip_iter": bytes_iter,
-                                             "fp64_tflops": iters_rank * fl_iter / (ipm_ms * 1e-3) / 1e12}},
+                                             "fp64_tflops": iters_rank * fl_iter / dt_rank / 1e12}},
             "k40": k40,
             "queue_batch_slots": qb,
             "aliased": ali,
