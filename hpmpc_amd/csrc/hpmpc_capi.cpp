@@ -130,7 +130,8 @@ struct hpmpc_mi355x_plan {
         std::vector<StageInfoH> st;
         void* d = nullptr;
     };
-    std::vector<LayoutTable> ltabs;
+    std::vector<LayoutTable> ltabs;  // at most kMaxLayouts, guarded by ltabs_mu (calls on one plan from several threads)
+    std::mutex ltabs_mu;
     int fixcls = 0;                             // compiled inner-stage class (kernel instance)
     int nbt = 0;                                // sum of nb + ng
     int ngt = 0;                                // sum of ng
@@ -196,8 +197,17 @@ const void* plan_stage_table(hpmpc_mi355x_plan* P, const long long* offB, const 
     }
     const size_t bytes = sizeof(StageInfoH) * (N + 1);
     if (!memcmp(st.data(), P->st.data(), bytes)) return P->d_st;
+    std::lock_guard<std::mutex> lock(P->ltabs_mu);
     for (const auto& t : P->ltabs)
         if (!memcmp(st.data(), t.st.data(), bytes)) return t.d;
+    // each distinct layout keeps a device table (and its first use a synchronous upload) until the plan is destroyed:
+    // a caller whose offsets change from call to call would grow it without bound, so the cache is capped
+    constexpr size_t kMaxLayouts = 64;
+    if (P->ltabs.size() >= kMaxLayouts) {
+        set_err(HPMPC_MI355X_EUNSUPPORTED, "more than 64 distinct stage layouts on one plan (create a plan per layout "
+                                           "family, or keep the offsets fixed)");
+        return nullptr;
+    }
     void* d = nullptr;
     if (!hip_ok(hipMalloc(&d, bytes), "layout stage table")) return nullptr;
     if (!hip_ok(hipMemcpy(d, st.data(), bytes, hipMemcpyHostToDevice), "layout stage table")) {

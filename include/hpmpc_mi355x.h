@@ -277,7 +277,8 @@ void hpmpc_mi355x_plan_destroy(hpmpc_mi355x_plan *plan);
  * every problem (likewise RSQrq).  Shared blocks give the time-invariant / aliased mode of the reference drivers
  * (test_problems/test_d_ip_hard.c:652-662: every inner stage points at one block) across a whole batch: e.g. only
  * stage 0 per problem (its b row carries A x0 + b) and one shared inner block for every other stage.  The offsets
- * must fit in 32 bits. */
+ * must fit in 32 bits.  A plan keeps one device table per distinct layout it has seen (its first use uploads it,
+ * synchronously), up to 64: a call with a 65th distinct layout fails with HPMPC_MI355X_EUNSUPPORTED. */
 typedef struct {
     long long BAbt_stride;   /* doubles between problems (0: shared by all problems) */
     long long RSQrq_stride;
