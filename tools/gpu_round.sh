@@ -18,6 +18,6 @@ step bench timeout -k 10 600 python3 bench.py
 grep '^{' gpurun_out/bench.log | tail -1 > gpurun_out/${R}_bench.json
 # kernel stats of the timed region only: no warmup queue, no isolated batch, so every hk_ipm_* launch
 # in the trace is one of the timed queue's (its average matches the bench line's launch_ms)
-step stats timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/stats -o run --output-format csv -- python3 bench.py --no-cpu --warmup 0 --no-isolated --no-queue-batch-slots --no-aliased --no-k40
+step stats timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/stats -o run --output-format csv -- python3 bench.py --no-cpu --warmup 0 --no-isolated --no-queue-batch-slots --no-aliased --no-coupled --no-k40
 find gpurun_out/prof/stats -name "*kernel_stats.csv" -exec cp {} gpurun_out/${R}_kernel_stats.csv \;
 head -12 gpurun_out/${R}_kernel_stats.csv | cut -c1-160
