@@ -627,7 +627,7 @@ def bench_aliased(args, torch, red, rank, world, barrier, slots):
     and the problems differ only in x0, so the batched layout holds one copy of every stage block except stage 0's
     (hpmpc_mi355x_layout BAbt_shared / RSQrq_shared) and the stage data stay in L2 / the Infinity Cache.  Timed
     through the same problem queue; beside it the same data in the ordinary per-problem layout."""
-    from hpmpc_amd.batch import BatchSolver
+    from hpmpc_amd.batch import BatchSolver, IpmQueue
     from hpmpc_amd.shard import make_shard
 
     B, N, nx, nu = args.batch, args.N, args.nx, args.nu
@@ -646,7 +646,7 @@ def bench_aliased(args, torch, red, rank, world, barrier, slots):
         r = {"value": it / dt, "ms_per_step": dt / args.steps * 1e3,
              "stage_data_bytes": int((s.BAbt.numel() + s.RSQrq.numel()) * 8),
              "pass_ms_per_step": {n: float(v) / args.steps for n, v in
-                                  zip(["hk_ipm_init", "hk_ipm_fact", "hk_ipm_pred", "hk_ipm_corr", "hk_ipm_update"], pm)}}
+                                  zip(IpmQueue.PASS_KERNELS, pm) if n}}
         if aliased:
             out.update(r)
             ref = ref_api() if rank == 0 else None
@@ -664,7 +664,7 @@ def bench_coupled(args, torch, red, rank, world, barrier, slots, headline_value)
     inner stage).  The clamp certificate then rests on the shifted-Cholesky bound (hk_riccati.h cert_g_shift); before
     it, every stage of every factorisation took the clamped x-block fallback.  Same queue, slots and steps as the
     headline; the ratio to the headline's rate is reported beside it."""
-    from hpmpc_amd.batch import BatchSolver
+    from hpmpc_amd.batch import BatchSolver, IpmQueue
     from hpmpc_amd.shard import coupled_shard
 
     B, N, nx, nu = args.batch, args.N, args.nx, args.nu
@@ -684,7 +684,7 @@ def bench_coupled(args, torch, red, rank, world, barrier, slots, headline_value)
            "steps": K, "ms_per_step": dt / K * 1e3, "vs_headline": (it / dt) / headline_value,
            "ret_counts": {str(int(r)): int((ret == r).sum()) for r in np.unique(ret)},
            "pass_ms_per_step": {n: float(v) / K for n, v in
-                                zip(["hk_ipm_init", "hk_ipm_fact", "hk_ipm_pred", "hk_ipm_corr", "hk_ipm_update"], pm)}}
+                                zip(IpmQueue.PASS_KERNELS, pm) if n}}
     ref = ref_api() if rank == 0 else None
     out["parity"] = parity_ipm(ref, qc, dict(ux=Q.ux, pi=Q.pi, lam=Q.lam, t=Q.t, kk=Q.kk, ret=Q.ret, k_max=args.k_max),
                                [(q, q % B) for q in spread(8, K * B)])
@@ -768,7 +768,7 @@ def main():
         dist.init_process_group("nccl")
     print(f"bench.py: rank {rank} of world {world} on cuda:{local}", file=sys.stderr, flush=True)
 
-    from hpmpc_amd.batch import (BatchSolver, algorithmic_bytes_per_ip_iter, algorithmic_bytes_per_pass,
+    from hpmpc_amd.batch import (BatchSolver, IpmQueue, algorithmic_bytes_per_ip_iter, algorithmic_bytes_per_pass,
                                  algorithmic_bytes_per_sv, flops_ip_iter, flops_sv)
     from hpmpc_amd.shard import Reducer, make_shard
 
@@ -825,16 +825,19 @@ def main():
     drain_iters, drain_probs = Q.drained()
     iters_total = sum_over_ranks(iters_rank)
     value = iters_total / dt
-    names = ["hk_ipm_init", "hk_ipm_fact", "hk_ipm_pred", "hk_ipm_corr", "hk_ipm_update"]
-    # roofline of the dominant pass kernel (largest device time per step): each pass runs one launch per
-    # tick; per launch, the problem-iterations it processes (sum kk / ticks) x that pass's algorithmic bytes
-    # (algorithmic_bytes_per_pass), over its average launch duration (both from this timed run)
-    dom = 1 + int(np.argmax(pass_ms[1:]))
+    # a tick is three launches (IpmQueue.PASS_KERNELS: fact, predictor + corrector, update); names[i] times pass_ms[i]
+    names = list(IpmQueue.PASS_KERNELS)
+    # the dominant launch (largest device time per step): each kernel runs one launch per tick; per launch, the
+    # problem-iterations it processes (sum kk / ticks) x that kernel's algorithmic bytes (algorithmic_bytes_per_pass),
+    # over its average launch duration (both from this timed run)
+    dom = max((i for i in range(1, len(names)) if names[i]), key=lambda i: pass_ms[i])
     bytes_pass = algorithmic_bytes_per_pass(qp)
     # the problem-iterations the tick launches ran (the drain's own are not in the pass kernels)
     probs_per_launch = (iters_rank - drain_iters) / ticks
     per_pass = {}
     for i in range(1, len(names)):
+        if not names[i]:
+            continue
         lm = pass_ms[i] / ticks
         per_pass[names[i]] = {"launch_ms": float(lm), "algorithmic_bytes_per_problem_iter": bytes_pass[names[i]],
                               "achieved_GBps": probs_per_launch * bytes_pass[names[i]] / (lm * 1e-3) / 1e9}
@@ -898,7 +901,7 @@ def main():
         dyn = {"workload": f"ipm_N{N}_nx10_nu3_batch{B}_generic_kernels", "value": itd / ddt, "unit": "IP-iter/s",
                "steps": Kd, "fact_us_per_problem_iter": pd[1] * 1e3 / itd,
                "headline_fact_us_per_problem_iter": pass_ms[1] * 1e3 / iters_rank,
-               "pass_ms_per_step": {n: float(v) / Kd for n, v in zip(names, pd)}}
+               "pass_ms_per_step": {n: float(v) / Kd for n, v in zip(names, pd) if n}}
         del Qd, sd
 
     # one isolated batch (no queue): the latency of a batch solve, reported beside the queue rate
@@ -1042,10 +1045,10 @@ def main():
                                    "ms_with_init": float(pass_ms[0])},
                          "algorithmic_bytes_per_problem_iter": bytes_dom,
                          "per_pass": per_pass,
-                         "pass_ms_per_step": {n: float(v / args.steps) for n, v in zip(names, pass_ms)},
-                         # fixed fields: the two tied passes (per lane launch) and the whole iteration
+                         "pass_ms_per_step": {n: float(v / args.steps) for n, v in zip(names, pass_ms) if n},
+                         # fixed fields: the two largest launches (per lane launch) and the whole iteration
                          "frac_fact": per_pass["hk_ipm_fact"]["achieved_GBps"] / PEAK_HBM_GBS,
-                         "frac_corr": per_pass["hk_ipm_corr"]["achieved_GBps"] / PEAK_HBM_GBS,
+                         "frac_predcorr": per_pass["hk_ipm_predcorr"]["achieved_GBps"] / PEAK_HBM_GBS,
                          "frac_whole_iteration": step_achieved / PEAK_HBM_GBS,
                          "ipm_whole_solve": {"achieved_GBps": step_achieved,
                                              "algorithmic_bytes_per_ip_iter": bytes_iter,

@@ -357,9 +357,10 @@ def algorithmic_bytes_per_pass(qp: OCPQP) -> dict:
       written; boxes t, dt, dlam, lam, r_d read, r_m, dt, dlam written (16);
     - hk_ipm_update (queue API: no backups, no r_m store -- nothing in a queue solve reads them): ux, dux
       read, ux written (3 nux), the same for pi (3 nx'); boxes lam, t, dlam, dt, d read, lam, t, r_d
-      written (16)."""
+      written (16);
+    - hk_ipm_predcorr (the queue's launch of both): hk_ipm_pred + hk_ipm_corr."""
     out = {"hk_ipm_fact": algorithmic_bytes_per_fact(qp), "hk_ipm_pred": 0.0, "hk_ipm_corr": 0.0,
-           "hk_ipm_update": 0.0}
+           "hk_ipm_update": 0.0, "hk_ipm_predcorr": 0.0}
     N = qp.N
     for k in range(N + 1):
         nux = qp.nux(k)
@@ -371,6 +372,7 @@ def algorithmic_bytes_per_pass(qp: OCPQP) -> dict:
         out["hk_ipm_pred"] += 8.0 * (L + babt + 10 * nb)
         out["hk_ipm_corr"] += 8.0 * (L + babt + nux + nx1 + nux + nx1 + 16 * nb)
         out["hk_ipm_update"] += 8.0 * (3 * nux + 3 * nx1 + 16 * nb)
+    out["hk_ipm_predcorr"] = out["hk_ipm_pred"] + out["hk_ipm_corr"]  # the queue's fused launch: both passes' data
     return out
 
 
@@ -451,9 +453,13 @@ class IpmQueue:
         o = 6 * QUEUE_LANES_MAX + 3 * self.n_slots
         return int(self.qctl[o].item()), int(self.qctl[o + 1].item())
 
+    # what pass_ms[i] of run(profiled=True) times (include/hpmpc_mi355x.h): a tick is hk_ipm_fact, hk_ipm_predcorr
+    # (predictor and corrector back to back) and hk_ipm_update; [3] stays 0
+    PASS_KERNELS = ("hk_ipm_init + hk_ipm_qdrain_mw", "hk_ipm_fact", "hk_ipm_predcorr", None, "hk_ipm_update")
+
     def run(self, *, mu0=2.0, mu_tol=1e-12, alpha_min=1e-8, warm_start=0, compute_mult=1, profiled=False):
-        """Solve every entry.  Returns (pass_ms[5] or None, ticks).  Polls the device once per chunk;
-        the caller synchronises before reading results."""
+        """Solve every entry.  Returns (pass_ms[5] or None, ticks): see PASS_KERNELS.  Polls the device once per
+        chunk; the caller synchronises before reading results."""
         s = self.s
         out = np.zeros(5)
         ticks = C.c_int(0)

@@ -579,9 +579,15 @@ hipStream_t lane_stream(hipStream_t caller, int i) {
 
 // One lane of the queue: an independent queue over its own slots, entries, control block and stream.  R ticks
 // per chunk; the host enqueues chunk c and then looks at chunk c - 1 (waiting for it), so the stream never runs dry.
+// A tick of the queue: three launches, hk_ipm_fact, hk_ipm_predcorr (predictor + corrector of a problem back to back)
+// and hk_ipm_update; their device time goes to pass_ms[1], [2] and [4] ([3] stays 0: the corrector runs inside [2]).
+constexpr int TL = 3;
+constexpr int kTick[TL] = {11, 18, 14};
+constexpr int kTickPass[TL] = {1, 2, 4};
+
 template <int R>
 struct QueueLane {
-    static constexpr int nev = R * 4 + 1;
+    static constexpr int nev = R * TL + 1;
     KArgs a;
     int nq = 0, ns = 0, drain_max = 0;  // nq: the whole queue's entries (the lanes share the entry counter)
     hipStream_t st = nullptr;
@@ -602,10 +608,10 @@ struct QueueLane {
     }
     bool harvest(int par) {  // chunk parity par has completed: accumulate its kernel times
         hipEvent_t* e = &ev[par * nev];
-        for (int i = 0; i < R * 4; i++) {
+        for (int i = 0; i < R * TL; i++) {
             float ms = 0.f;
             if (!hip_ok(hipEventElapsedTime(&ms, e[i], e[i + 1]), "event time")) return false;
-            pass_ms[1 + i % 4] += ms;
+            pass_ms[kTickPass[i % TL]] += ms;
         }
         return true;
     }
@@ -635,9 +641,9 @@ struct QueueLane {
         if (pass_ms && !hip_ok(hipEventRecord(e[0], st), "event record")) return false;
         for (int i = 0; i < R; i++) {
             a.qpar = (int)((ticks + i) & 1);  // active-slot list of this iteration (kernel args are copied at launch)
-            for (int k = 0; k < 4; k++) {
-                if (!launch(11 + k)) return false;
-                if (pass_ms && !hip_ok(hipEventRecord(e[4 * i + k + 1], st), "event record")) return false;
+            for (int k = 0; k < TL; k++) {
+                if (!launch(kTick[k])) return false;
+                if (pass_ms && !hip_ok(hipEventRecord(e[TL * i + k + 1], st), "event record")) return false;
             }
         }
         ticks += R;
@@ -715,7 +721,7 @@ struct QueueLane {
 template <int R>
 int queue_run(KArgs a, int nq, int n_slots, int* qctl, int* dctr, int lanes, int k_max, double* pass_ms,
               int* n_ticks, hipStream_t st) {
-    static_assert(2 * (R * 4 + 1) + 3 < kPollEvents, "poll pool sized for R <= 8, plus the fork / join event");
+    static_assert(2 * (R * TL + 1) + 3 < kPollEvents, "poll pool sized for R <= 8, plus the fork / join event");
     if (n_ticks) *n_ticks = 0;
     if (pass_ms)
         for (int i = 0; i < 5; i++) pass_ms[i] = 0.0;

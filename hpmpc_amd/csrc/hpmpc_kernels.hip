@@ -170,6 +170,28 @@ __global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_corr(KArgs a) {
     corr_body<FX>(a, T, v);
 }
 
+// The queue's second launch of a tick: the predictor and the corrector of one problem back to back (one launch
+// boundary, one launch tail and one set of workgroup prologues fewer per tick than two pass kernels; the corrector's
+// trs backward starts on the stages the predictor's forward ended on).  Each body gets a fresh view (the slot, entry
+// and problem made opaque in between), so each keeps the register allocation it has in its own pass kernel.
+template <class FX>
+__global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_predcorr(KArgs a) {
+    Who who;
+    if (!who_am_i(a, who) || !slot_active(a, who)) return;  // idle slots leave before staging the tables
+    const LdsTabs T = lds_tables(a);
+    {
+        IpmView v = ipm_view(a, T, who);
+        if (v.w.state[S_ACTIVE] == 0.0) return;
+        pred_body<FX>(a, T, v);
+    }
+    wsync();
+    int s = who.s, q = who.q, d = who.d;
+    asm volatile("" : "+v"(s), "+v"(q), "+v"(d));
+    const Who w2{__builtin_amdgcn_readfirstlane(s), __builtin_amdgcn_readfirstlane(q), __builtin_amdgcn_readfirstlane(d)};
+    IpmView v = ipm_view(a, T, w2);
+    corr_body<FX>(a, T, v);
+}
+
 // The update pass loads 4 quads (16 stages) before using any (6 measured slower: profiles/r04/ab_headline_OP.txt)
 template <class FX>
 __global__ __launch_bounds__(64) HK_TWO_WAVES void hk_ipm_update(KArgs a) {
@@ -657,6 +679,8 @@ static int launch_t(int which, const KArgs* a, int count, hipStream_t stream) {
         case 12: hipLaunchKernelGGL(hk_ipm_pred<FX>, grid, block, lds, stream, *a); break;
         case 13: hipLaunchKernelGGL(hk_ipm_corr<FX>, grid, block, lds, stream, *a); break;
         case 14: hipLaunchKernelGGL(hk_ipm_update<FX>, grid, block, lds, stream, *a); break;
+        // the queue's tick: fact (11), predictor + corrector (18), update (14)
+        case 18: hipLaunchKernelGGL(hk_ipm_predcorr<FX>, grid, block, lds, stream, *a); break;
         // the whole IPM per problem in one launch (hk_ipm_solo)
         case 15:
         case 16: {

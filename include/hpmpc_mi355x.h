@@ -352,9 +352,10 @@ int hpmpc_mi355x_ipm_batch_profiled(const hpmpc_mi355x_plan *plan, const hpmpc_m
  * workspace is reused, so a queue solve leaves no factor behind for d_kkt_solve_new_rhs_res_mpc_hard_tv; for
  * the same reason its update pass writes neither the iterate backups nor r_m, which only that re-solve reads.
  * Synchronises with the device once per chunk of iterations (it polls the finished counter); on
- * return the last chunk may still be running on `stream`.  pass_ms (nullable): device time of
- * [init + drain, fact, pred, corr, update] summed over the run and the lanes (the lanes' kernels overlap);
- * n_ticks (nullable): iterations enqueued, summed over the lanes (launches of each pass kernel). */
+ * return the last chunk may still be running on `stream`.  An iteration (tick) is three launches: the
+ * factorisation, the predictor and corrector of each problem back to back, and the update.  pass_ms (nullable):
+ * device time of [init + drain, fact, pred + corr, 0, update] summed over the run and the lanes (the lanes'
+ * kernels overlap); n_ticks (nullable): iterations enqueued, summed over the lanes (launches of each kernel). */
 int hpmpc_mi355x_ipm_queue(const hpmpc_mi355x_plan *plan, const hpmpc_mi355x_layout *lay, int nprob, int nq,
                            int n_slots, const double *BAbt, const double *RSQrq, const double *d, double *ux,
                            double *pi, double *lam, double *t, double *ws, int *qctl, int k_max, double mu0,

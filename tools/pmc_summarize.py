@@ -40,7 +40,7 @@ def main(fetch_dir, write_dir, out, kk_sum):
            "calib": {"fetch_factor": cf, "write_factor": cw,
                      "raw_fetch": F["calib_copy"]["FETCH_SIZE"], "raw_write": W["calib_copy"]["WRITE_SIZE"]},
            "kernels": {}}
-    for k in ("hk_ipm_fact", "hk_ipm_pred", "hk_ipm_corr", "hk_ipm_update", "hk_ipm_qdrain_mw", "hk_ric_sv",
+    for k in ("hk_ipm_fact", "hk_ipm_pred", "hk_ipm_corr", "hk_ipm_predcorr", "hk_ipm_update", "hk_ipm_qdrain_mw", "hk_ric_sv",
               "hk_ric_sv_nu3_nx8", "hk_pcond", "hk_wide_sv", "hk_pexpand"):
         if k not in F or k not in W:
             continue
