@@ -346,6 +346,25 @@ def bench_pcond(args, torch, red, rank, world, barrier):
     barrier()
     dt = red.max(time.perf_counter() - t0)
     ms = np.array([[e[j].elapsed_time(e[j + 1]) for j in range(3)] for e in ev]).mean(axis=0)
+    # the same K pipelines with args.sv_streams batches in flight (own solver buffers per stream): the condensing of
+    # one batch overlaps the condensed Riccati of the other, whose one workgroup per problem leaves CUs idle
+    # (tools/pcond_streams_probe.py: +10 %); the per-kernel roofline below is the one-stream run's
+    sols = [s] + [PcondSolver(qp, N2) for _ in range(max(args.sv_streams, 1) - 1)]
+    streams = [stream] + [torch.cuda.Stream() for _ in range(len(sols) - 1)]
+    for x in sols[1:]:
+        x.solve()
+    for st in streams[1:]:
+        st.wait_stream(stream)
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(K):
+        j = i % len(sols)
+        with torch.cuda.stream(streams[j]):
+            sols[j].solve()
+    for st in streams[1:]:
+        stream.wait_stream(st)
+    barrier()
+    dt_f = red.max(time.perf_counter() - t0)
     names = ["hk_pcond", "hk_wide_sv", "hk_pexpand"]
     by = pcond_algorithmic_bytes(qp, N2)
     fl = pcond_flops(qp, N2)
@@ -354,8 +373,10 @@ def bench_pcond(args, torch, red, rank, world, barrier):
     kern = {n: {"ms": float(m), "algorithmic_bytes_per_problem": b, "flops_per_problem": f,
                 "achieved_GBps": B * b / (m * 1e-3) / 1e9, "fp64_tflops": B * f / (m * 1e-3) / 1e12}
             for n, m, b, f in zip(names, ms, by, fl)}
-    out = {"workload": f"pcond_N{N}_nx{nx}_nu{nu}_N2_{N2}_batch{B}", "value": B * world * K / dt,
-           "unit": "solves/s", "ms_per_step": dt / K * 1e3, "batch_per_gpu": B,
+    out = {"workload": f"pcond_N{N}_nx{nx}_nu{nu}_N2_{N2}_batch{B}", "value": B * world * K / dt_f,
+           "unit": "solves/s", "ms_per_step": dt_f / K * 1e3, "batch_per_gpu": B, "batches_in_flight": len(sols),
+           "one_batch_in_flight": {"value": B * world * K / dt, "ms_per_step": dt / K * 1e3,
+                                   "note": "the run the per-kernel roofline and 'kernels' are measured on"},
            "condensed": {"N2": N2, "nu2": 60, "nx2": 24},
            "riccati_fact_per_s": B * world / (ms[1] * 1e-3),
            "roofline": {"bound": "hbm", "kernel": names[dom], "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
@@ -371,12 +392,13 @@ def bench_pcond(args, torch, red, rank, world, barrier):
         torch.cuda.synchronize()
         e = 0.0
         for p in spread(8, B):
-            U, Pi = s.solution(p)
             u2, p2, _, _ = ref.ric_sv(qp.problem(p), compute_pi=1, compute_Pb=0)
-            for k in range(N + 1):
-                e = max(e, rel_err(U[k], u2[k][:qp.nux(k)]))
-                if k < N:
-                    e = max(e, rel_err(Pi[k], p2[k][:int(qp.nx[k + 1])]))
+            for x in sols:  # every stream's buffers
+                U, Pi = x.solution(p)
+                for k in range(N + 1):
+                    e = max(e, rel_err(U[k], u2[k][:qp.nux(k)]))
+                    if k < N:
+                        e = max(e, rel_err(Pi[k], p2[k][:int(qp.nx[k + 1])]))
         out["parity"] = {"reference": "oracle/_ref c99 d_back_ric_rec_sv_tv_res on the uncondensed problem",
                          "problems": spread(8, B), "max_rel_err": e}
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -424,13 +446,35 @@ def bench_pcond_ipm(args, torch, red, rank, world, barrier):
     ret = s.ret2.cpu().numpy()
     iters = red.sum(float(kk.sum()) * K)
     ms = np.array([[e[j].elapsed_time(e[j + 1]) for j in range(3)] for e in ev]).mean(axis=0)
+    # the same K pipelines with args.sv_streams batches in flight (own solver buffers per stream): one workgroup per
+    # problem and 512 problems leave room on the chip for a second batch (tools/pcond_streams_probe.py: +10 %); the
+    # roofline below is the one-stream run's
+    sols = [s] + [PcondSolver(qp, N2) for _ in range(max(args.sv_streams, 1) - 1)]
+    streams = [stream] + [torch.cuda.Stream() for _ in range(len(sols) - 1)]
+    for x in sols[1:]:
+        x.solve_ipm(k_max=k_max)
+    for st in streams[1:]:
+        st.wait_stream(stream)
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(K * len(sols)):
+        j = i % len(sols)
+        with torch.cuda.stream(streams[j]):
+            sols[j].solve_ipm(k_max=k_max)
+    for st in streams[1:]:
+        stream.wait_stream(st)
+    barrier()
+    dt_f = red.max(time.perf_counter() - t0)
+    iters_f = red.sum(sum(float(x.kk2.sum().item()) for x in sols) * K)
     # roofline of the wide-stage IPM (one launch solves the batch): algorithmic bytes of one condensed IP
     # iteration (pcond.wide_ipm_algorithmic_bytes) x the launch's iterations / its duration
     c = s.cond_sizes()
     bpi = wide_ipm_algorithmic_bytes(c["nx"], c["nu"], c["nb"], c["ng"])
     ach = float(kk.sum()) * bpi / (ms[1] * 1e-3) / 1e9
-    out = {"workload": f"pcond_ipm_N{N}_nx{nx}_nu{nu}_N2_{N2}_boxes_batch{B}", "value": iters / dt,
-           "unit": "IP-iter/s", "x0_scale": x0_scale,
+    out = {"workload": f"pcond_ipm_N{N}_nx{nx}_nu{nu}_N2_{N2}_boxes_batch{B}", "value": iters_f / dt_f,
+           "unit": "IP-iter/s", "x0_scale": x0_scale, "batches_in_flight": len(sols),
+           "one_batch_in_flight": {"value": iters / dt, "solves_per_s": B * world * K / dt,
+                                   "note": "the run the roofline, 'ms' and 'solves_per_s' are measured on"},
            "roofline": {"bound": "hbm", "kernel": "hk_wide_ipm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                         "frac": ach / PEAK_HBM_GBS, "bytes_per_ip_iter": bpi, "launch_ms": float(ms[1]),
                         "ip_iters_per_launch": float(kk.sum())},
