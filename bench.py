@@ -612,26 +612,33 @@ def bench_single_qp(args, torch, stream):
 def sv_timed(torch, solvers, steps, barrier, red):
     """K = steps batched sv launches (one batch each) issued round-robin on len(solvers) streams, each solver with its
     own output buffers: len(solvers) batches in flight.  One wave per problem, so one batch of 1024 fills one wave per
-    SIMD and a second batch in flight is a second wave on every SIMD.  Returns (max-over-ranks wall seconds, mean
-    launch ms from a hipEvent pair per launch on its own stream)."""
+    SIMD and a second batch in flight is a second wave on every SIMD.  The launches are pre-marshalled foreign calls
+    (BatchSolver.ric_sv_bound), so that the host keeps ahead of kernels of ~0.1 ms.  Returns (max-over-ranks wall
+    seconds, mean launch ms: a hipEvent pair per launch on its own stream, one stream only -- with several the events
+    would overlap and cost host time between the launches)."""
     S = len(solvers)
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(S - 1)]
+    calls = [x.ric_sv_bound(st) for x, st in zip(solvers, streams)]
     for st in streams[1:]:
         st.wait_stream(streams[0])
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     barrier()
     t0 = time.perf_counter()
-    for i in range(steps):
-        j = i % S
-        with torch.cuda.stream(streams[j]):
-            ev[i][0].record(streams[j])
-            solvers[j].ric_sv()
-            ev[i][1].record(streams[j])
+    if S == 1:
+        for i in range(steps):
+            ev[i][0].record(streams[0])
+            if calls[0]():
+                raise RuntimeError("hpmpc_mi355x_ric_sv_batch failed")
+            ev[i][1].record(streams[0])
+    else:
+        for i in range(steps):
+            if calls[i % S]():
+                raise RuntimeError("hpmpc_mi355x_ric_sv_batch failed")
     for st in streams[1:]:
         streams[0].wait_stream(st)
     barrier()
     dt = red.max(time.perf_counter() - t0)
-    return dt, float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    return dt, (float(np.mean([a.elapsed_time(b) for a, b in ev])) if S == 1 else None)
 
 
 def bench_riccati_small(args, torch, red, rank, world, barrier, stream):
@@ -648,6 +655,7 @@ def bench_riccati_small(args, torch, red, rank, world, barrier, stream):
             s.ric_sv()
     dt1, ms1 = sv_timed(torch, sols[:1], args.steps, barrier, red)
     dt, ms = sv_timed(torch, sols, args.steps, barrier, red)
+    ms = ms1 if ms is None else ms
     by = algorithmic_bytes_per_sv(qp)
     ach = B * args.steps * by / dt / 1e9  # device level: every launch's bytes over the wall time of the K launches
     ref = ref_api() if rank == 0 else None
@@ -660,7 +668,7 @@ def bench_riccati_small(args, torch, red, rank, world, barrier, stream):
             "roofline": {"bound": "hbm", "kernel": "hk_ric_sv", "achieved": ach, "peak": PEAK_HBM_GBS,
                          "unit": "GB/s", "frac": ach / PEAK_HBM_GBS, "algorithmic_bytes_per_sv": by,
                          "unit_of_work": f"K = {args.steps} launches of one batch, {len(sols)} in flight, over their "
-                                         f"wall time (the launches overlap; launch_ms is per launch)"},
+                                         f"wall time (the launches overlap; launch_ms is the one-stream run's)"},
             "one_batch_in_flight": {"value": B * world * args.steps / dt1, "launch_ms": ms1,
                                     "frac": B * by / (ms1 * 1e-3) / 1e9 / PEAK_HBM_GBS}}
 
@@ -994,6 +1002,7 @@ def main():
             r_.ric_sv()
     rdt1, sv_ms1 = sv_timed(torch, rics[:1], args.steps, barrier, red)
     rdt, sv_ms = sv_timed(torch, rics, args.steps, barrier, red)
+    sv_ms = sv_ms1 if sv_ms is None else sv_ms
     fact_total = B * world * args.steps
     par_sv = None
     if ref is not None:
@@ -1111,8 +1120,8 @@ def main():
                                      "frac": sv_achieved / PEAK_HBM_GBS,
                                      "algorithmic_bytes_per_sv": sv_bytes,
                                      "unit_of_work": f"K = {args.steps} launches of one batch, {len(rics)} in flight, "
-                                                     "over their wall time (the launches overlap; launch_ms is per "
-                                                     "launch)",
+                                                     "over their wall time (the launches overlap; launch_ms is the "
+                                                     "one-stream run's per-launch time)",
                                      "fp64_tflops": B * args.steps * flops_sv(N, nx, nu) / rdt / 1e12},
                         "one_batch_in_flight": {"value": fact_total / rdt1, "launch_ms": sv_ms1,
                                                 "frac": B * sv_bytes / (sv_ms1 * 1e-3) / 1e9 / PEAK_HBM_GBS}},

@@ -291,6 +291,17 @@ class BatchSolver:
         if rc != 0:
             raise RuntimeError(f"hpmpc_mi355x_ric_sv_batch failed ({rc})")
 
+    def ric_sv_bound(self, stream=None, *, compute_pi=1, compute_Pb=0):
+        """ric_sv over the whole batch as a zero-argument callable with every argument marshalled once (a stream
+        handle, or the current stream at bind time): a launch loop then costs one foreign call per launch.  The
+        callable returns the library's code (0 on success)."""
+        fn = lib().hpmpc_mi355x_ric_sv_batch
+        st = C.c_void_p(self.torch.cuda.current_stream(self.dev).cuda_stream if stream is None else stream.cuda_stream)
+        args = (self.plan, C.byref(self.layout), self.nprob, 0, self.nprob, C.c_void_p(self.BAbt.data_ptr()),
+                C.c_void_p(self.RSQrq.data_ptr()), C.c_void_p(self.ux.data_ptr()), C.c_void_p(self.pi.data_ptr()),
+                C.c_void_p(self.ws.data_ptr()), compute_pi, compute_Pb, C.c_void_p(self.Pb.data_ptr()), st)
+        return lambda: fn(*args)
+
     def ric_trf(self, *, p0=0, count=None):
         """Batched d_back_ric_rec_trf_tv_res (nb = ng = 0): factor into ws."""
         count = self.nprob - p0 if count is None else count
