@@ -350,11 +350,12 @@ def bench_pcond(args, torch, red, rank, world, barrier):
     # one batch overlaps the condensed Riccati of the other, whose one workgroup per problem leaves CUs idle
     # (tools/pcond_streams_probe.py: +10 %); the per-kernel roofline below is the one-stream run's
     sols = [s] + [PcondSolver(qp, N2) for _ in range(max(args.sv_streams, 1) - 1)]
-    streams = [stream] + [torch.cuda.Stream() for _ in range(len(sols) - 1)]
-    for x in sols[1:]:
-        x.solve()
-    for st in streams[1:]:
+    streams = [stream] + side_streams(torch, len(sols) - 1)
+    for x, st in zip(sols[1:], streams[1:]):  # untimed: each stream's first use pays its queue's set-up
         st.wait_stream(stream)
+        with torch.cuda.stream(st):
+            x.solve()
+    torch.cuda.synchronize()
     barrier()
     t0 = time.perf_counter()
     for i in range(K):
@@ -450,11 +451,12 @@ def bench_pcond_ipm(args, torch, red, rank, world, barrier):
     # problem and 512 problems leave room on the chip for a second batch (tools/pcond_streams_probe.py: +10 %); the
     # roofline below is the one-stream run's
     sols = [s] + [PcondSolver(qp, N2) for _ in range(max(args.sv_streams, 1) - 1)]
-    streams = [stream] + [torch.cuda.Stream() for _ in range(len(sols) - 1)]
-    for x in sols[1:]:
-        x.solve_ipm(k_max=k_max)
-    for st in streams[1:]:
+    streams = [stream] + side_streams(torch, len(sols) - 1)
+    for x, st in zip(sols[1:], streams[1:]):  # untimed: each stream's first use pays its queue's set-up
         st.wait_stream(stream)
+        with torch.cuda.stream(st):
+            x.solve_ipm(k_max=k_max)
+    torch.cuda.synchronize()
     barrier()
     t0 = time.perf_counter()
     for i in range(K * len(sols)):
@@ -609,6 +611,18 @@ def bench_single_qp(args, torch, stream):
             "dropin_ms_per_solve": host_ms, "dropin_kk": int(kkc.value), "parity": par}
 
 
+_SIDE = []
+
+
+def side_streams(torch, n):
+    """The streams the legs with several batches in flight use beside the current one, created once and shared by
+    every such leg: the process has four hardware queues (GPU_MAX_HW_QUEUES), the queue's lanes hold three of them,
+    and a stream created later can land on the current stream's queue and serialise behind it."""
+    while len(_SIDE) < n:
+        _SIDE.append(torch.cuda.Stream())
+    return _SIDE[:n]
+
+
 def sv_timed(torch, solvers, steps, barrier, red):
     """K = steps batched sv launches (one batch each) issued round-robin on len(solvers) streams, each solver with its
     own output buffers: len(solvers) batches in flight.  One wave per problem, so one batch of 1024 fills one wave per
@@ -617,10 +631,12 @@ def sv_timed(torch, solvers, steps, barrier, red):
     seconds, mean launch ms: a hipEvent pair per launch on its own stream, one stream only -- with several the events
     would overlap and cost host time between the launches)."""
     S = len(solvers)
-    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(S - 1)]
+    streams = [torch.cuda.current_stream()] + side_streams(torch, S - 1)
     calls = [x.ric_sv_bound(st) for x, st in zip(solvers, streams)]
-    for st in streams[1:]:
-        st.wait_stream(streams[0])
+    for c in calls:  # one untimed launch per stream: a stream's first launch pays its queue's set-up
+        if c():
+            raise RuntimeError("hpmpc_mi355x_ric_sv_batch failed")
+    torch.cuda.synchronize()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     barrier()
     t0 = time.perf_counter()
