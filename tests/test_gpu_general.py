@@ -57,8 +57,11 @@ def test_ipm_general_vs_oracle(product, oracle, case):
     for key, size in (("ux", qp.nux), ("lam", qp.nconstr), ("t", qp.nconstr)):
         spread = max(_rel(kf[key][k][:size(k)], kb[key][k][:size(k)]) for k in range(N + 1))
         gate = max(TOL_IPM, 4 * spread)
-        for k in range(N + 1):
-            assert _rel(ka[key][k][:size(k)], kb[key][k][:size(k)]) <= gate, (key, k, gate)
+        err = max(_rel(ka[key][k][:size(k)], kb[key][k][:size(k)]) for k in range(N + 1))
+        assert err <= gate, (key, err, gate)
+        # regression pin: the largest error measured since the P-form records is 1.05e-10 (N6, lam), at
+        # 0.81 of its gate; an error above 1.5e-10 is a regression even where a wider oracle spread would admit it
+        assert err <= max(TOL_IPM, 1.5e-10), (key, err, "above the pinned P-form error")
 
 
 @pytest.mark.parametrize("case", CASES[:3], ids=[f"N{c[0]}_{i}" for i, c in enumerate(CASES[:3])])
