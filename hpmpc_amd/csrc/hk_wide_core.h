@@ -749,11 +749,15 @@ __device__ HK_WIDE_BODY void wide_sv_body(const WideArgs& a, const WideProb& q) 
                             const double* pb = Ds + g4 + DS_LD * (16 * tj + c16);
                             double av[4], bv[4];
                             // row nux of Ds is zero: its A operand is qx_g (0 in a pure factorisation), the others'
-                            // is diag(Qx_g) DCt, with no select for the compiler to turn into a branch over the reads
-                            const double sq = (ra == nux && !a.trf) ? 1.0 : 0.0;
+                            // is diag(Qx_g) DCt.  qx_g is read on every row and selected as a value (v_cndmask, no
+                            // branch over the reads); a select rather than a product with 0 keeps a non-finite qx_g
+                            // out of the other rows, as in the reference.  Finite values: the same two
+                            // roundings as the former fma(qx_g, 0 or 1, product), so the same sums.
+                            const bool sq = ra == nux && !a.trf;
 #pragma unroll
                             for (int kc = 0; kc < 4; kc++) {
-                                av[kc] = fma(qrs[4 * kc + g4], sq, pa[4 * kc] * dqs[4 * kc + g4]);
+                                const double qv = qrs[4 * kc + g4];
+                                av[kc] = __dadd_rn(sq ? qv : 0.0, __dmul_rn(pa[4 * kc], dqs[4 * kc + g4]));
                                 bv[kc] = pb[4 * kc];
                             }
 #pragma unroll
